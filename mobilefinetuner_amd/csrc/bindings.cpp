@@ -1,0 +1,366 @@
+// Torch bindings of the gfx950 kernels (module mobilefinetuner_amd._C).
+// Every op validates dtype/device/layout, allocates outputs/workspaces through PyTorch's
+// stream-ordered caching allocator (so the ops are hipGraph-capturable) and launches on the
+// current HIP stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "kernels.h"
+
+namespace py = pybind11;
+using torch::Tensor;
+using mft::bf16_t;
+
+namespace {
+
+inline hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == torch::kBFloat16, #t " must be bf16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == torch::kFloat32, #t " must be fp32")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+
+inline bf16_t* bp(const Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+inline float* fp(const Tensor& t) { return t.data_ptr<float>(); }
+template <typename T>
+inline T* optp(const c10::optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// ------------------------------------------------------------------ norms
+std::vector<Tensor> layernorm_fwd(Tensor x, c10::optional<Tensor> delta, Tensor w, Tensor b, double eps) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(w); CHECK_F32(b);
+  const int N = x.size(-1);
+  TORCH_CHECK(N % 8 == 0 && N <= 4096, "layernorm: width must be a multiple of 8 and <= 4096");
+  const int M = x.numel() / N;
+  c10::hip::HIPGuard g(x.device());
+  auto y = torch::empty_like(x);
+  auto mean = torch::empty({M}, x.options().dtype(torch::kFloat32));
+  auto rstd = torch::empty({M}, x.options().dtype(torch::kFloat32));
+  Tensor s;
+  if (delta.has_value()) {
+    CHECK_CONTIG((*delta));
+    s = torch::empty_like(x);
+  }
+  mft::layernorm_fwd(bp(x), delta ? bp(*delta) : nullptr, s.defined() ? bp(s) : nullptr, fp(w), fp(b), bp(y), fp(mean),
+                     fp(rstd), M, N, (float)eps, stream());
+  return {y, s.defined() ? s : Tensor(), mean, rstd};
+}
+
+Tensor layernorm_bwd(Tensor x, Tensor dy, Tensor w, Tensor mean, Tensor rstd, c10::optional<Tensor> dresid,
+                     c10::optional<Tensor> dw, c10::optional<Tensor> db) {
+  CHECK_CONTIG(x); CHECK_CONTIG(dy);
+  const int N = x.size(-1), M = x.numel() / N;
+  c10::hip::HIPGuard g(x.device());
+  auto dx = torch::empty_like(x);
+  Tensor work;
+  float* dwp = optp<float>(dw);
+  if (dwp) work = torch::empty({2L * mft::norm_bwd_partial_blocks(M) * N}, x.options().dtype(torch::kFloat32));
+  mft::layernorm_bwd(bp(x), bp(dy), fp(w), fp(mean), fp(rstd), dresid ? bp(*dresid) : nullptr, bp(dx), dwp,
+                     optp<float>(db), dwp ? fp(work) : nullptr, M, N, 1, stream());
+  return dx;
+}
+
+std::vector<Tensor> rmsnorm_fwd(Tensor x, c10::optional<Tensor> delta, Tensor w, double eps, double offset) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(w);
+  const int N = x.size(-1);
+  TORCH_CHECK(N % 8 == 0 && N <= 4096, "rmsnorm: width must be a multiple of 8 and <= 4096");
+  const int M = x.numel() / N;
+  c10::hip::HIPGuard g(x.device());
+  auto y = torch::empty_like(x);
+  auto rstd = torch::empty({M}, x.options().dtype(torch::kFloat32));
+  Tensor s;
+  if (delta.has_value()) s = torch::empty_like(x);
+  mft::rmsnorm_fwd(bp(x), delta ? bp(*delta) : nullptr, s.defined() ? bp(s) : nullptr, fp(w), bp(y), fp(rstd), M, N,
+                   (float)eps, (float)offset, stream());
+  return {y, s.defined() ? s : Tensor(), rstd};
+}
+
+Tensor rmsnorm_bwd(Tensor x, Tensor dy, Tensor w, Tensor rstd, c10::optional<Tensor> dresid, double offset,
+                   c10::optional<Tensor> dw) {
+  CHECK_CONTIG(x); CHECK_CONTIG(dy);
+  const int N = x.size(-1), M = x.numel() / N;
+  c10::hip::HIPGuard g(x.device());
+  auto dx = torch::empty_like(x);
+  Tensor work;
+  float* dwp = optp<float>(dw);
+  if (dwp) work = torch::empty({2L * mft::norm_bwd_partial_blocks(M) * N}, x.options().dtype(torch::kFloat32));
+  mft::rmsnorm_bwd(bp(x), bp(dy), fp(w), fp(rstd), dresid ? bp(*dresid) : nullptr, bp(dx), dwp,
+                   dwp ? fp(work) : nullptr, M, N, (float)offset, 1, stream());
+  return dx;
+}
+
+// ------------------------------------------------------------------ attention
+void fill_st(long* st, const Tensor& t) {  // [B, S, H, D] strides
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, "attention tensors must be [B,S,H,D] with contiguous D");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0,
+              "attention strides must be multiples of 8 elements (16-B vector access)");
+  st[0] = t.stride(0); st[1] = t.stride(1); st[2] = t.stride(2);
+}
+
+std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, double scale, bool causal, int64_t window,
+                             c10::optional<Tensor> kv_lens) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v);
+  const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
+  const int Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(H % Hkv == 0, "H must be a multiple of Hkv");
+  TORCH_CHECK(D == 64 || D == 128 || D == 256, "head dim must be 64, 128 or 256");
+  c10::hip::HIPGuard g(q.device());
+  auto o = torch::empty({B, Sq, H, D}, q.options());
+  auto lse = torch::empty({B, H, Sq}, q.options().dtype(torch::kFloat32));
+  mft::AttnArgs a{};
+  a.q = bp(q); a.k = bp(k); a.v = bp(v); a.o = bp(o); a.lse = fp(lse);
+  fill_st(a.q_st, q); fill_st(a.k_st, k); fill_st(a.v_st, v); fill_st(a.o_st, o);
+  a.B = B; a.H = H; a.Hkv = Hkv; a.Sq = Sq; a.Sk = Sk; a.D = D;
+  a.scale = (float)scale; a.causal = causal; a.window = (int)window;
+  a.kv_lens = kv_lens ? kv_lens->data_ptr<int>() : nullptr;
+  mft::attn_fwd(a, stream());
+  return {o, lse};
+}
+
+void attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor dq, Tensor dk, Tensor dv,
+              double scale, bool causal, int64_t window, c10::optional<Tensor> kv_lens) {
+  const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
+  const int Sk = k.size(1), Hkv = k.size(2);
+  c10::hip::HIPGuard g(q.device());
+  auto delta = torch::empty({B, H, Sq}, q.options().dtype(torch::kFloat32));
+  auto dq_acc = torch::empty({B, Sq, H, D}, q.options().dtype(torch::kFloat32));
+  Tensor dk_tmp, dv_tmp;
+  mft::AttnBwdArgs a{};
+  if (H != Hkv) {
+    dk_tmp = torch::empty({B, Sk, H, D}, q.options());
+    dv_tmp = torch::empty({B, Sk, H, D}, q.options());
+    a.dk_tmp = bp(dk_tmp); a.dv_tmp = bp(dv_tmp);
+    fill_st(a.tmp_st, dk_tmp);
+  }
+  a.q = bp(q); a.k = bp(k); a.v = bp(v); a.o = bp(o); a.dout = bp(dout); a.lse = fp(lse);
+  a.delta = fp(delta); a.dq_acc = fp(dq_acc); a.dq = bp(dq); a.dk = bp(dk); a.dv = bp(dv);
+  fill_st(a.q_st, q); fill_st(a.k_st, k); fill_st(a.v_st, v); fill_st(a.o_st, o); fill_st(a.do_st, dout);
+  fill_st(a.dq_st, dq); fill_st(a.dk_st, dk); fill_st(a.dv_st, dv);
+  a.B = B; a.H = H; a.Hkv = Hkv; a.Sq = Sq; a.Sk = Sk; a.D = D;
+  a.scale = (float)scale; a.causal = causal; a.window = (int)window;
+  a.kv_lens = kv_lens ? kv_lens->data_ptr<int>() : nullptr;
+  mft::attn_bwd(a, stream());
+}
+
+// ------------------------------------------------------------------ activations
+Tensor gelu_fwd(Tensor x) {
+  CHECK_BF16(x); CHECK_CONTIG(x);
+  auto y = torch::empty_like(x);
+  mft::gelu_fwd(bp(x), bp(y), x.numel(), stream());
+  return y;
+}
+Tensor gelu_bwd(Tensor x, Tensor dy) {
+  CHECK_CONTIG(x); CHECK_CONTIG(dy);
+  auto dx = torch::empty_like(x);
+  mft::gelu_bwd(bp(x), bp(dy), bp(dx), x.numel(), stream());
+  return dx;
+}
+Tensor gated_fwd(Tensor gu, int64_t act) {
+  CHECK_BF16(gu); CHECK_CONTIG(gu);
+  const int I = gu.size(-1) / 2;
+  TORCH_CHECK(I % 8 == 0, "gated: intermediate size must be a multiple of 8");
+  auto sizes = gu.sizes().vec();
+  sizes.back() = I;
+  auto y = torch::empty(sizes, gu.options());
+  mft::gated_fwd(bp(gu), bp(y), gu.numel() / (2 * I), I, (int)act, stream());
+  return y;
+}
+Tensor gated_bwd(Tensor gu, Tensor dy, int64_t act) {
+  CHECK_CONTIG(gu); CHECK_CONTIG(dy);
+  const int I = gu.size(-1) / 2;
+  auto dgu = torch::empty_like(gu);
+  mft::gated_bwd(bp(gu), bp(dy), bp(dgu), gu.numel() / (2 * I), I, (int)act, stream());
+  return dgu;
+}
+
+// ------------------------------------------------------------------ embedding
+Tensor embed_fwd(Tensor ids, Tensor wte, c10::optional<Tensor> wpe, int64_t S, int64_t pos0, double scale) {
+  CHECK_CUDA(ids); TORCH_CHECK(ids.scalar_type() == torch::kInt64, "ids must be int64"); CHECK_CONTIG(ids);
+  CHECK_BF16(wte); CHECK_CONTIG(wte);
+  const long M = ids.numel();
+  const int C = wte.size(1);
+  TORCH_CHECK(C % 8 == 0, "embedding width must be a multiple of 8");
+  auto out = torch::empty({M, C}, wte.options());
+  mft::embed_fwd(ids.data_ptr<int64_t>(), bp(wte), wpe ? bp(*wpe) : nullptr, bp(out), M, C, (int)S, (int)pos0,
+                 (float)scale, stream());
+  return out;
+}
+void embed_bwd(Tensor ids, Tensor dout, c10::optional<Tensor> dwte, c10::optional<Tensor> dwpe, int64_t S, int64_t pos0,
+               double scale) {
+  CHECK_CONTIG(dout);
+  const long M = ids.numel();
+  const int C = dout.size(-1);
+  mft::embed_bwd(ids.data_ptr<int64_t>(), bp(dout), optp<float>(dwte), optp<float>(dwpe), M, C, (int)S, (int)pos0,
+                 (float)scale, stream());
+}
+
+// ------------------------------------------------------------------ cross entropy
+void xent_fwd_bwd(Tensor logits, Tensor labels, Tensor loss, int64_t V, c10::optional<Tensor> scale, double extra,
+                  bool write_grad) {
+  CHECK_BF16(logits); TORCH_CHECK(logits.stride(1) == 1, "logits rows must be contiguous");
+  TORCH_CHECK(logits.stride(0) % 8 == 0, "logits row stride must be a multiple of 8");
+  TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.is_contiguous(), "labels must be contiguous int64");
+  CHECK_F32(loss);
+  mft::xent_fwd_bwd(bp(logits), labels.data_ptr<int64_t>(), fp(loss), logits.size(0), (int)V, logits.stride(0),
+                    optp<float>(scale), (float)extra, write_grad, stream());
+}
+Tensor logsoftmax_gather(Tensor logits, Tensor idx, int64_t V) {
+  CHECK_BF16(logits); TORCH_CHECK(logits.stride(1) == 1, "logits rows must be contiguous");
+  auto out = torch::empty({logits.size(0), idx.numel()}, logits.options().dtype(torch::kFloat32));
+  mft::logsoftmax_gather(bp(logits), idx.data_ptr<int64_t>(), fp(out), logits.size(0), (int)V, logits.stride(0),
+                         idx.numel(), stream());
+  return out;
+}
+
+// ------------------------------------------------------------------ optimizer
+void sumsq(Tensor x, Tensor out, bool accumulate) {
+  CHECK_F32(x); CHECK_CONTIG(x);
+  auto part = torch::empty({mft::sumsq_blocks(x.numel())}, x.options());
+  mft::sumsq(fp(x), x.numel(), fp(part), fp(out), accumulate, stream());
+}
+void nonfinite_check(Tensor x, Tensor flag) {
+  CHECK_F32(x); CHECK_CONTIG(x);
+  mft::nonfinite_check(fp(x), x.numel(), flag.data_ptr<int>(), stream());
+}
+void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor step, c10::optional<Tensor> sumsq_t,
+                double beta1, double beta2, double eps, double wd, double max_norm, bool l2_coupled,
+                c10::optional<Tensor> shadow, c10::optional<Tensor> nonfinite) {
+  CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v);
+  CHECK_CONTIG(p); CHECK_CONTIG(g); CHECK_CONTIG(m); CHECK_CONTIG(v);
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adamw: size mismatch");
+  mft::AdamWArgs a{};
+  a.p = fp(p); a.g = fp(g); a.m = fp(m); a.v = fp(v); a.n = p.numel();
+  a.lr_ptr = fp(lr); a.step_ptr = fp(step); a.sumsq = optp<float>(sumsq_t);
+  a.beta1 = beta1; a.beta2 = beta2; a.eps = eps; a.weight_decay = wd; a.max_norm = max_norm; a.l2_coupled = l2_coupled;
+  a.shadow = optp<bf16_t>(shadow);
+  if (a.shadow) TORCH_CHECK(shadow->numel() == p.numel() && shadow->is_contiguous(), "shadow must match params");
+  a.nonfinite = optp<int>(nonfinite);
+  mft::adamw_step(a, stream());
+}
+
+// ------------------------------------------------------------------ LoRA
+void lora_rowdot(Tensor X, Tensor W, int64_t wsk, int64_t wsr, Tensor U, double s) {
+  CHECK_BF16(X); CHECK_BF16(W); CHECK_BF16(U);
+  TORCH_CHECK(X.stride(-1) == 1 && U.stride(-1) == 1, "rows must be contiguous");
+  const int K = X.size(-1), R = U.size(-1);
+  const long M = X.numel() / K;
+  TORCH_CHECK(K % 8 == 0, "lora: in-features must be a multiple of 8");
+  mft::lora_rowdot(bp(X), X.stride(-2), bp(W), wsk, wsr, bp(U), U.stride(-2), M, K, R, (float)s, stream());
+}
+void lora_update(Tensor base, c10::optional<Tensor> bias, Tensor U, Tensor W, int64_t wsr, int64_t wsn, Tensor Y,
+                 double s) {
+  CHECK_BF16(base); CHECK_BF16(Y);
+  const int N = Y.size(-1), R = U.size(-1);
+  const long M = Y.numel() / N;
+  TORCH_CHECK(N % 8 == 0, "lora: out-features must be a multiple of 8");
+  mft::lora_update(bp(base), base.stride(-2), optp<float>(bias), bp(U), U.stride(-2), bp(W), wsr, wsn, bp(Y),
+                   Y.stride(-2), M, N, R, (float)s, stream());
+}
+void lora_wgrad(Tensor X, Tensor Y, Tensor out, int64_t osk, int64_t osr, double scale) {
+  CHECK_BF16(X); CHECK_BF16(Y); CHECK_F32(out);
+  const int K = X.size(-1), R = Y.size(-1);
+  const long M = X.numel() / K;
+  mft::lora_wgrad(bp(X), X.stride(-2), bp(Y), Y.stride(-2), fp(out), osk, osr, M, K, R, (float)scale, stream());
+}
+void lora_merge(Tensor W, int64_t wsk, int64_t wsn, Tensor A, Tensor B, double s) {
+  CHECK_F32(A); CHECK_F32(B); CHECK_CONTIG(A); CHECK_CONTIG(B);
+  const int K = A.size(0), R = A.size(1), N = B.size(1);
+  const bool isbf = W.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(isbf || W.scalar_type() == torch::kFloat32, "merge target must be bf16 or fp32");
+  mft::lora_merge(W.data_ptr(), isbf, wsk, wsn, fp(A), fp(B), K, N, R, (float)s, stream());
+}
+
+// ------------------------------------------------------------------ RoPE
+void rope_apply(Tensor x, Tensor cos_t, Tensor sin_t, int64_t pos0, bool interleaved, bool inverse) {
+  long st[3];
+  fill_st(st, x);
+  mft::rope_apply(bp(x), st, x.size(0), x.size(1), x.size(2), x.size(3), fp(cos_t), fp(sin_t), (int)pos0, interleaved,
+                  inverse, stream());
+}
+std::vector<Tensor> qknorm_rope_fwd(Tensor x, Tensor w, Tensor cos_t, Tensor sin_t, int64_t pos0, double eps,
+                                    double offset, bool interleaved) {
+  long st[3];
+  fill_st(st, x);
+  const int B = x.size(0), S = x.size(1), H = x.size(2), D = x.size(3);
+  auto y = torch::empty({B, S, H, D}, x.options());
+  auto rstd = torch::empty({(long)B * S * H}, x.options().dtype(torch::kFloat32));
+  mft::qknorm_rope_fwd(bp(x), st, bp(y), fp(rstd), fp(w), B, S, H, D, fp(cos_t), fp(sin_t), (int)pos0, (float)eps,
+                       (float)offset, interleaved, stream());
+  return {y, rstd};
+}
+void qknorm_rope_bwd(Tensor x, Tensor dy, Tensor rstd, Tensor w, Tensor dx, c10::optional<Tensor> dw, Tensor cos_t,
+                     Tensor sin_t, int64_t pos0, double offset, bool interleaved) {
+  long st[3], dst[3];
+  fill_st(st, x);
+  fill_st(dst, dx);
+  CHECK_CONTIG(dy);
+  const int B = x.size(0), S = x.size(1), H = x.size(2), D = x.size(3);
+  Tensor work;
+  float* dwp = optp<float>(dw);
+  if (dwp) work = torch::empty({(long)mft::qknorm_rope_bwd_blocks((long)B * S * H) * D}, x.options().dtype(torch::kFloat32));
+  mft::qknorm_rope_bwd(bp(x), st, bp(dy), fp(rstd), fp(w), bp(dx), dst, dwp, dwp ? fp(work) : nullptr, B, S, H, D,
+                       fp(cos_t), fp(sin_t), (int)pos0, (float)offset, interleaved, 1, stream());
+}
+
+// ------------------------------------------------------------------ misc
+void cast_f32_bf16(Tensor x, Tensor y) {
+  CHECK_F32(x); CHECK_BF16(y); CHECK_CONTIG(x); CHECK_CONTIG(y);
+  TORCH_CHECK(x.numel() == y.numel(), "cast: size mismatch");
+  mft::cast_f32_bf16(fp(x), bp(y), x.numel(), stream());
+}
+void cast_bf16_f32(Tensor x, Tensor y) {
+  CHECK_BF16(x); CHECK_F32(y); CHECK_CONTIG(x); CHECK_CONTIG(y);
+  TORCH_CHECK(x.numel() == y.numel(), "cast: size mismatch");
+  mft::cast_bf16_f32(bp(x), fp(y), x.numel(), stream());
+}
+Tensor scale_bf16(Tensor x, c10::optional<Tensor> sdev, double s) {
+  CHECK_BF16(x); CHECK_CONTIG(x);
+  auto y = torch::empty_like(x);
+  mft::scale_bf16(bp(x), bp(y), x.numel(), optp<float>(sdev), (float)s, stream());
+  return y;
+}
+Tensor add_bf16(Tensor a, Tensor b) {
+  CHECK_BF16(a); CHECK_CONTIG(a); CHECK_CONTIG(b);
+  auto y = torch::empty_like(a);
+  mft::add_bf16(bp(a), bp(b), bp(y), a.numel(), stream());
+  return y;
+}
+
+}  // namespace
+
+void register_runtime(py::module_& m);  // csrc/runtime_bindings.cpp
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "mobilefinetuner_amd native kernels (gfx950 HIP) and C++ runtime";
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("gated_fwd", &gated_fwd);
+  m.def("gated_bwd", &gated_bwd);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
+  m.def("xent_fwd_bwd", &xent_fwd_bwd);
+  m.def("logsoftmax_gather", &logsoftmax_gather);
+  m.def("sumsq", &sumsq);
+  m.def("nonfinite_check", &nonfinite_check);
+  m.def("adamw_step", &adamw_step);
+  m.def("lora_rowdot", &lora_rowdot);
+  m.def("lora_update", &lora_update);
+  m.def("lora_wgrad", &lora_wgrad);
+  m.def("lora_merge", &lora_merge);
+  m.def("rope_apply", &rope_apply);
+  m.def("qknorm_rope_fwd", &qknorm_rope_fwd);
+  m.def("qknorm_rope_bwd", &qknorm_rope_bwd);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("cast_bf16_f32", &cast_bf16_f32);
+  m.def("scale_bf16", &scale_bf16);
+  m.def("add_bf16", &add_bf16);
+  register_runtime(m);
+}

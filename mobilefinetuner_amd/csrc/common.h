@@ -1,0 +1,117 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of mobilefinetuner_amd.
+//
+// Conventions used by every kernel in csrc/kernels:
+//  * bf16 tensors are passed as raw uint16_t storage; math is done in fp32.
+//  * wave64 everywhere (block sizes are multiples of 64, reductions use 64-lane shuffles).
+//  * global loads/stores of bf16 are vectorised to 16 B per lane (8 x bf16) whenever the
+//    row length allows it (Guideline 13 of the CDNA HIP guide).
+//  * every launcher takes an explicit hipStream_t and never allocates or synchronises, so the
+//    whole training step can be captured into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace mft {
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef uint16_t u16x8_t __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);  // RNE; lowers to v_cvt_pk_bf16_f32 on gfx950
+  return __bfloat16_as_ushort(h);
+}
+
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024 (any multiple of 64). `smem` needs >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* smem) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) smem[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += smem[i];
+  return r;
+}
+
+__device__ __forceinline__ float block_max(float v, float* smem) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) smem[wid] = v;
+  __syncthreads();
+  float r = -INFINITY;
+  for (int i = 0; i < nw; ++i) r = fmaxf(r, smem[i]);
+  return r;
+}
+
+__device__ __forceinline__ void load8(const bf16_t* p, float* f) {
+  u16x8_t v = *reinterpret_cast<const u16x8_t*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = bf2f(v[j]);
+}
+
+__device__ __forceinline__ void store8(bf16_t* p, const float* f) {
+  u16x8_t v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = f2bf(f[j]);
+  *reinterpret_cast<u16x8_t*>(p) = v;
+}
+
+// XCD-aware bijective remap of a 1-D block id (CDNA HIP guide §5 "XCD swizzle must be bijective"):
+// consecutive logical tiles land on the same XCD (same L2) instead of being dealt round-robin.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace mft
+
+#define MFT_HIP_CHECK(expr)                                                            \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess) {                                                            \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
+      abort();                                                                         \
+    }                                                                                  \
+  } while (0)

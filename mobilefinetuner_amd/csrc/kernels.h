@@ -1,0 +1,133 @@
+// Host-side launcher API of the gfx950 kernels (raw device pointers + explicit stream).
+// The torch bindings (csrc/bindings.cpp) are the only caller; nothing here allocates or
+// synchronises, so every launcher is hipGraph-capturable.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mft {
+typedef uint16_t bf16_t;
+
+// ---------------------------------------------------------------- norms (norm.hip)
+int norm_bwd_partial_blocks(int M);
+void layernorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, const float* b,
+                   bf16_t* y, float* mean, float* rstd, int M, int N, float eps, hipStream_t st);
+void rmsnorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, bf16_t* y, float* rstd,
+                 int M, int N, float eps, float w_offset, hipStream_t st);
+void layernorm_bwd(const bf16_t* x, const bf16_t* dy, const float* w, const float* mean, const float* rstd,
+                   const bf16_t* dresid, bf16_t* dx, float* dw, float* db, float* work, int M, int N, int accumulate,
+                   hipStream_t st);
+void rmsnorm_bwd(const bf16_t* x, const bf16_t* dy, const float* w, const float* rstd, const bf16_t* dresid, bf16_t* dx,
+                 float* dw, float* work, int M, int N, float w_offset, int accumulate, hipStream_t st);
+
+// ---------------------------------------------------------------- attention (attention.hip)
+struct AttnArgs {
+  const bf16_t *q, *k, *v;
+  bf16_t* o;
+  float* lse;
+  long q_st[3], k_st[3], v_st[3], o_st[3];  // batch, seq, head strides (elements)
+  int B, H, Hkv, Sq, Sk, D;
+  float scale;
+  int causal, window;
+  const int* kv_lens;
+};
+struct AttnBwdArgs {
+  const bf16_t *q, *k, *v, *o, *dout;
+  const float* lse;
+  float* delta;   // [B,H,Sq] workspace
+  float* dq_acc;  // [B,Sq,H,D] fp32 workspace
+  bf16_t *dq, *dk, *dv;
+  bf16_t *dk_tmp, *dv_tmp;  // [B,Sk,H,D] workspaces (GQA only)
+  long q_st[3], k_st[3], v_st[3], o_st[3], do_st[3], dq_st[3], dk_st[3], dv_st[3], tmp_st[3];
+  int B, H, Hkv, Sq, Sk, D;
+  float scale;
+  int causal, window;
+  const int* kv_lens;
+};
+void attn_fwd(const AttnArgs& a, hipStream_t s);
+void attn_bwd(const AttnBwdArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- activations (act.hip)
+void gelu_fwd(const bf16_t* x, bf16_t* y, long n, hipStream_t st);
+void gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, long n, hipStream_t st);
+// gu: [M, 2I] (gate | up); y: [M, I]; act 0 = gelu_tanh (GeGLU), 1 = silu (SwiGLU)
+void gated_fwd(const bf16_t* gu, bf16_t* y, long M, int I, int act, hipStream_t st);
+void gated_bwd(const bf16_t* gu, const bf16_t* dy, bf16_t* dgu, long M, int I, int act, hipStream_t st);
+
+// ---------------------------------------------------------------- embedding (embed.hip)
+// out[m] = wte[ids[m]] * scale (+ wpe[pos0 + m % S])
+void embed_fwd(const int64_t* ids, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, long M, int C, int S, int pos0,
+               float scale, hipStream_t st);
+// dwte[ids[m]] += dout[m]*scale (fp32 atomics); dwpe[p] += sum over batch
+void embed_bwd(const int64_t* ids, const bf16_t* dout, float* dwte, float* dwpe, long M, int C, int S, int pos0,
+               float scale, hipStream_t st);
+
+// ---------------------------------------------------------------- cross entropy (xent.hip)
+// logits [M, ld] bf16 (first V columns valid); labels [M] (-100 = ignore).  Writes per-row loss
+// (0 for ignored rows) and overwrites logits[:, :V] with dlogits = (softmax - onehot) * (*scale)
+// (columns >= V set to 0).  scale may be null (=> 1.0); extra multiplies it.
+void xent_fwd_bwd(bf16_t* logits, const int64_t* labels, float* loss, long M, int V, long ld, const float* scale,
+                  float extra, int write_grad, hipStream_t st);
+// log-softmax gather: out[m, c] = logits[m, idx[c]] - lse(logits[m])  (MMLU scoring)
+void logsoftmax_gather(const bf16_t* logits, const int64_t* idx, float* out, long M, int V, long ld, int nidx,
+                       hipStream_t st);
+
+// ---------------------------------------------------------------- optimizer (optim.hip)
+// sum of squares of n fp32 values -> partial[nblk]; then out[0] = sum(partial)
+int sumsq_blocks(long n);
+void sumsq(const float* x, long n, float* partial, float* out, int accumulate, hipStream_t st);
+// Fused AdamW over flat fp32 buffers.  clip: grads scaled by min(1, max_norm/(sqrt(*sumsq)+1e-6))
+// if sumsq != null.  lr read from device (*lr_ptr) so a captured graph can replay with new LRs.
+// If shadow != null also writes the bf16 copy of the updated params (shadow[i] at shadow_idx map).
+struct AdamWArgs {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  long n;
+  const float* lr_ptr;
+  float beta1, beta2, eps, weight_decay;
+  const float* step_ptr;  // device step count (float, already incremented)
+  const float* sumsq;     // device grad-norm^2 (or null)
+  float max_norm;
+  int l2_coupled;         // reference-compat: g += wd*p instead of decoupled decay
+  bf16_t* shadow;         // optional bf16 copy
+  const int* nonfinite;   // optional device flag: skip the step when set
+};
+void adamw_step(const AdamWArgs& a, hipStream_t st);
+// flag[0] = any(!isfinite(x))  (accumulates with OR)
+void nonfinite_check(const float* x, long n, int* flag, hipStream_t st);
+
+// ---------------------------------------------------------------- LoRA (lora.hip)
+// U[m, r] = s * sum_k X[m, k] * W[k*wsk + r*wsr]            (x A, s * dy B^T)
+void lora_rowdot(const bf16_t* X, long ldx, const bf16_t* W, long wsk, long wsr, bf16_t* U, long ldu, long M, int K,
+                 int R, float s, hipStream_t st);
+// Y[m, n] = base[m, n] (+ bias[n]) + s * sum_r U[m, r] * W[r*wsr + n*wsn]   (Y may alias base)
+void lora_update(const bf16_t* base, long ldb, const float* bias, const bf16_t* U, long ldu, const bf16_t* W, long wsr,
+                 long wsn, bf16_t* Y, long ldy, long M, int N, int R, float s, hipStream_t st);
+// out[k*osk + r*osr] += scale * sum_m X[m, k] * Y[m, r]     (fp32 atomics into the grad buffer)
+void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out, long osk, long osr, long M, int K, int R,
+                float scale, hipStream_t st);
+// W[k*wsk + n*wsn] += s * sum_r A[k, r] * B[r, n]   (A [K,R], B [R,N] fp32)
+void lora_merge(void* W, int w_is_bf16, long wsk, long wsn, const float* A, const float* B, int K, int N, int R, float s,
+                hipStream_t st);
+
+// ---------------------------------------------------------------- RoPE (rope.hip)
+// x strided [B,S,H,D] (st = batch, seq, head strides), in place.  cos/sin tables [S_max, D/2].
+void rope_apply(bf16_t* x, const long* st, int B, int S, int H, int D, const float* cos_t, const float* sin_t, int pos0,
+                int interleaved, int inverse, hipStream_t stream);
+// y[row, :] = rope(rmsnorm(x[row]) * (w + off)), y contiguous [B*S*H, D]; rstd [B*S*H]
+void qknorm_rope_fwd(const bf16_t* x, const long* st, bf16_t* y, float* rstd, const float* w, int B, int S, int H, int D,
+                     const float* cos_t, const float* sin_t, int pos0, float eps, float off, int interleaved,
+                     hipStream_t stream);
+int qknorm_rope_bwd_blocks(long rows);
+void qknorm_rope_bwd(const bf16_t* x, const long* st, const bf16_t* dy, const float* rstd, const float* w, bf16_t* dx,
+                     const long* dst, float* dw, float* work, int B, int S, int H, int D, const float* cos_t,
+                     const float* sin_t, int pos0, float off, int interleaved, int accumulate, hipStream_t stream);
+
+// ---------------------------------------------------------------- misc (misc.hip)
+void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t st);
+void cast_bf16_f32(const bf16_t* x, float* y, long n, hipStream_t st);
+void scale_bf16(const bf16_t* x, bf16_t* y, long n, const float* scale_dev, float scale, hipStream_t st);
+void add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, hipStream_t st);
+}  // namespace mft

@@ -1,0 +1,69 @@
+// Token (+ position) embedding gather and its scatter-add backward.
+// Replaces GPT2Model::embedding_lookup + the in-place wpe add (graph/gpt2_model.cpp:346-381,
+// :500-528; no autograd there — SURVEY §8 Q5) and Gemma's embed*sqrt(H) (graph/gemma_model.cpp:222-259).
+// Forward: one wave per token row, 16-B vector copies.  Backward: fp32 atomics for the token table
+// (rows are ~random, one 256-B contiguous atomic wave-instruction per chunk group) and a
+// deterministic per-position column reduction over the batch for wpe.
+#include "common.h"
+#include "kernels.h"
+
+namespace mft {
+
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ wte,
+                                                        const bf16_t* __restrict__ wpe, bf16_t* __restrict__ out, long M,
+                                                        int C, int S, int pos0, float scale) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const long id = ids[row];
+  const int pos = pos0 + (int)(row % S);
+  for (int c = lane * 8; c < C; c += 64 * 8) {
+    float a[8];
+    load8(wte + id * C + c, a);
+    if (scale != 1.f) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = bf2f(f2bf(a[j] * scale));
+    }
+    if (wpe) {
+      float p[8];
+      load8(wpe + (long)pos * C + c, p);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += p[j];
+    }
+    store8(out + row * C + c, a);
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ dout,
+                                                            float* __restrict__ dwte, long M, int C, float scale) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const long id = ids[row];
+  for (int c = lane; c < C; c += 64) atomicAdd(dwte + id * C + c, bf2f(dout[row * C + c]) * scale);
+}
+
+// dwpe[pos0 + s, c] += sum_b dout[b*S + s, c]
+__global__ void embed_bwd_wpe_kernel(const bf16_t* __restrict__ dout, float* __restrict__ dwpe, long M, int C, int S,
+                                     int pos0) {
+  const int s = blockIdx.x;
+  const long nb = M / S;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float acc = 0.f;
+    for (long b = 0; b < nb; ++b) acc += bf2f(dout[(b * S + s) * C + c]);
+    dwpe[(long)(pos0 + s) * C + c] += acc;
+  }
+}
+
+void embed_fwd(const int64_t* ids, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, long M, int C, int S, int pos0,
+               float scale, hipStream_t st) {
+  embed_fwd_kernel<<<cdiv(M, 4), 256, 0, st>>>(ids, wte, wpe, out, M, C, S, pos0, scale);
+}
+
+void embed_bwd(const int64_t* ids, const bf16_t* dout, float* dwte, float* dwpe, long M, int C, int S, int pos0,
+               float scale, hipStream_t st) {
+  if (dwte) embed_bwd_wte_kernel<<<cdiv(M, 4), 256, 0, st>>>(ids, dout, dwte, M, C, scale);
+  if (dwpe) embed_bwd_wpe_kernel<<<S, 256, 0, st>>>(dout, dwpe, M, C, S, pos0);
+}
+
+}  // namespace mft

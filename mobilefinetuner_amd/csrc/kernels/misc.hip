@@ -1,0 +1,82 @@
+// Small vectorised elementwise kernels: fp32<->bf16 casts (offload quantisation, master->shadow
+// copies; replaces ops::cast core/ops.cpp:2705-2745 and the sharder's software fp16 conversion
+// opt_ops/sharding/parameter_sharder.cpp:21-76), device-scalar scaling (loss / accumulation
+// scaling without host sync), and residual adds.
+#include "common.h"
+#include "kernels.h"
+
+namespace mft {
+
+static inline int grid_for(long n8) {
+  long g = (n8 + 255) / 256;
+  return (int)(g < 8192 ? (g > 0 ? g : 1) : 8192);
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  const long n8 = n / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const float4* x4 = reinterpret_cast<const float4*>(x + i * 8);
+    float4 a = x4[0], b = x4[1];
+    float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    store8(y + i * 8, f);
+  }
+  if (blockIdx.x == 0)
+    for (long i = n8 * 8 + threadIdx.x; i < n; i += blockDim.x) y[i] = f2bf(x[i]);
+}
+
+__global__ void cast_bf16_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, long n) {
+  const long n8 = n / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    load8(x + i * 8, f);
+    float4* y4 = reinterpret_cast<float4*>(y + i * 8);
+    y4[0] = make_float4(f[0], f[1], f[2], f[3]);
+    y4[1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+  if (blockIdx.x == 0)
+    for (long i = n8 * 8 + threadIdx.x; i < n; i += blockDim.x) y[i] = bf2f(x[i]);
+}
+
+__global__ void scale_bf16_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long n,
+                                  const float* __restrict__ sdev, float s) {
+  const float sc = (sdev ? *sdev : 1.f) * s;
+  const long n8 = n / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    load8(x + i * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= sc;
+    store8(y + i * 8, f);
+  }
+  if (blockIdx.x == 0)
+    for (long i = n8 * 8 + threadIdx.x; i < n; i += blockDim.x) y[i] = f2bf(bf2f(x[i]) * sc);
+}
+
+__global__ void add_bf16_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, bf16_t* __restrict__ y, long n) {
+  const long n8 = n / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8], g[8];
+    load8(a + i * 8, f);
+    load8(b + i * 8, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] += g[j];
+    store8(y + i * 8, f);
+  }
+  if (blockIdx.x == 0)
+    for (long i = n8 * 8 + threadIdx.x; i < n; i += blockDim.x) y[i] = f2bf(bf2f(a[i]) + bf2f(b[i]));
+}
+
+void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t st) {
+  cast_f32_bf16_kernel<<<grid_for(n / 8), 256, 0, st>>>(x, y, n);
+}
+void cast_bf16_f32(const bf16_t* x, float* y, long n, hipStream_t st) {
+  cast_bf16_f32_kernel<<<grid_for(n / 8), 256, 0, st>>>(x, y, n);
+}
+void scale_bf16(const bf16_t* x, bf16_t* y, long n, const float* scale_dev, float scale, hipStream_t st) {
+  scale_bf16_kernel<<<grid_for(n / 8), 256, 0, st>>>(x, y, n, scale_dev, scale);
+}
+void add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, hipStream_t st) {
+  add_bf16_kernel<<<grid_for(n / 8), 256, 0, st>>>(a, b, y, n);
+}
+
+}  // namespace mft

@@ -1,0 +1,264 @@
+// LayerNorm / RMSNorm forward + backward for gfx950.
+//
+// Replaces the reference's scalar CPU loops ops::layer_norm / ops::rms_norm
+// (operators/finetune_ops/core/ops.cpp:1404-1458, :1489-1574) and their backward classes
+// (core/backward_functions.cpp:425-561).
+//
+// Design: one wave64 per row, 4 rows per 256-thread block; each lane owns CH chunks of 8
+// contiguous bf16 (16-B vector loads), the row stays in registers between the statistics pass
+// and the normalise pass, so the row is read from HBM exactly once.  Optional fused residual
+// add (s = x + d; y = norm(s)) removes a separate elementwise pass per transformer sub-block.
+// Statistics (mean/rstd) are saved in fp32 for the backward.  The affine weight is fp32.
+#include "common.h"
+#include "kernels.h"
+
+namespace mft {
+
+template <int CH, bool RMS, bool RESID>
+__global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ d,
+                                                       bf16_t* __restrict__ s_out, const float* __restrict__ w,
+                                                       const float* __restrict__ b, bf16_t* __restrict__ y,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                       int M, int N, float eps, float w_offset) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nch = N >> 3;
+  const bf16_t* xr = x + (long)row * N;
+  float v[CH][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      load8(xr + ch * 8, v[c]);
+      if (RESID) {
+        float dv[8];
+        load8(d + (long)row * N + ch * 8, dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += dv[j];
+        store8(s_out + (long)row * N + ch * 8, v[c]);
+        // round like the stored residual so forward/backward see the same value
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = bf2f(f2bf(v[c][j]));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += v[c][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+  }
+  float mean = 0.f;
+  if (!RMS) mean = wave_sum(sum) / N;
+  float sq = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = v[c][j] - mean;
+        sq += t * t;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / N + eps);
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      float o[8];
+      const float4* w4 = reinterpret_cast<const float4*>(w + ch * 8);
+      float4 wa = w4[0], wb = w4[1];
+      float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+      if (RMS) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = v[c][j] * rstd * (wv[j] + w_offset);
+      } else {
+        const float4* b4 = reinterpret_cast<const float4*>(b + ch * 8);
+        float4 ba = b4[0], bb = b4[1];
+        float bv[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * wv[j] + bv[j];
+      }
+      store8(y + (long)row * N + ch * 8, o);
+    }
+  }
+  if (lane == 0) {
+    if (!RMS) mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// Backward: dx = rstd * (w*dy - mean(w*dy) - xhat*mean(w*dy*xhat))  (LayerNorm)
+//           dx = rstd * (w'*dy - xhat*mean(w'*dy*xhat))              (RMSNorm, w' = w + offset)
+// plus optional dresid added in (residual branch of a fused add+norm).  dw/db partials are
+// accumulated per block over its rows (grid-stride) into part[blockIdx][N] (fp32); a second tiny
+// kernel sums the partials, so no float atomics are needed and the result is deterministic.
+template <int CH, bool RMS, bool WGRAD>
+__global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                       const float* __restrict__ w, const float* __restrict__ mean_in,
+                                                       const float* __restrict__ rstd_in, const bf16_t* __restrict__ dresid,
+                                                       bf16_t* __restrict__ dx, float* __restrict__ dw_part,
+                                                       float* __restrict__ db_part, int M, int N, float w_offset) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nch = N >> 3;
+  float dwa[CH][8], dba[CH][8];
+  if (WGRAD) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dwa[c][j] = dba[c][j] = 0.f;
+  }
+  for (int row = blockIdx.x * 4 + wid; row < M; row += gridDim.x * 4) {
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float xh[CH][8], g[CH][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        float xv[8], dv[8];
+        load8(x + (long)row * N + ch * 8, xv);
+        load8(dy + (long)row * N + ch * 8, dv);
+        const float4* w4 = reinterpret_cast<const float4*>(w + ch * 8);
+        float4 wa = w4[0], wb = w4[1];
+        float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[c][j] = (xv[j] - mean) * rstd;
+          g[c][j] = dv[j] * (wv[j] + w_offset);
+          s1 += g[c][j];
+          s2 += g[c][j] * xh[c][j];
+          if (WGRAD) {
+            dwa[c][j] += dv[j] * xh[c][j];
+            dba[c][j] += dv[j];
+          }
+        }
+      }
+    }
+    s1 = RMS ? 0.f : wave_sum(s1) / N;
+    s2 = wave_sum(s2) / N;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[c][j] - s1 - xh[c][j] * s2);
+        if (dresid) {
+          float r[8];
+          load8(dresid + (long)row * N + ch * 8, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        }
+        store8(dx + (long)row * N + ch * 8, o);
+      }
+    }
+  }
+  if (WGRAD) {
+    // reduce the 4 waves of the block through LDS, then one row of partials per block
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [4][N] x2
+    for (int c = 0; c < CH; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch)
+        for (int j = 0; j < 8; ++j) {
+          red[wid * N + ch * 8 + j] = dwa[c][j];
+          red[4 * N + wid * N + ch * 8 + j] = dba[c][j];
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+      float a = red[i] + red[N + i] + red[2 * N + i] + red[3 * N + i];
+      float bb = red[4 * N + i] + red[5 * N + i] + red[6 * N + i] + red[7 * N + i];
+      dw_part[(long)blockIdx.x * N + i] = a;
+      if (!RMS) db_part[(long)blockIdx.x * N + i] = bb;
+    }
+  }
+}
+
+// out[i] (+)= sum_b part[b][i]
+__global__ void reduce_rows_kernel(const float* __restrict__ part, float* __restrict__ out, int nb, int N,
+                                   int accumulate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(long)b * N + i];
+  out[i] = accumulate ? out[i] + s : s;
+}
+
+template <bool RMS>
+static void norm_fwd_dispatch(const bf16_t* x, const bf16_t* d, bf16_t* s_out, const float* w, const float* b,
+                              bf16_t* y, float* mean, float* rstd, int M, int N, float eps, float w_offset,
+                              hipStream_t st) {
+  const int nch = N / 8, ch = (nch + 63) / 64;
+  dim3 grid(cdiv(M, 4)), block(256);
+#define MFT_NF(CHV)                                                                                        \
+  if (d)                                                                                                   \
+    norm_fwd_kernel<CHV, RMS, true><<<grid, block, 0, st>>>(x, d, s_out, w, b, y, mean, rstd, M, N, eps, w_offset); \
+  else                                                                                                     \
+    norm_fwd_kernel<CHV, RMS, false><<<grid, block, 0, st>>>(x, d, s_out, w, b, y, mean, rstd, M, N, eps, w_offset);
+  if (ch <= 1) { MFT_NF(1) }
+  else if (ch <= 2) { MFT_NF(2) }
+  else if (ch <= 4) { MFT_NF(4) }
+  else { MFT_NF(8) }
+#undef MFT_NF
+}
+
+template <bool RMS>
+static void norm_bwd_dispatch(const bf16_t* x, const bf16_t* dy, const float* w, const float* mean, const float* rstd,
+                              const bf16_t* dresid, bf16_t* dx, float* dw, float* db, float* work, int M, int N,
+                              float w_offset, int accumulate, hipStream_t st) {
+  const int nch = N / 8, ch = (nch + 63) / 64;
+  const bool wgrad = dw != nullptr;
+  // with weight grads: a bounded grid so the partial buffer stays small (work: 2*nb*N floats)
+  const int nb = wgrad ? norm_bwd_partial_blocks(M) : cdiv(M, 4);
+  float* dw_part = work;
+  float* db_part = work ? work + (long)nb * N : nullptr;
+  const size_t shm = wgrad ? sizeof(float) * 8 * N : 0;
+  dim3 grid(nb), block(256);
+#define MFT_NB(CHV)                                                                                           \
+  if (wgrad)                                                                                                  \
+    norm_bwd_kernel<CHV, RMS, true><<<grid, block, shm, st>>>(x, dy, w, mean, rstd, dresid, dx, dw_part, db_part, M, N, w_offset); \
+  else                                                                                                        \
+    norm_bwd_kernel<CHV, RMS, false><<<grid, block, 0, st>>>(x, dy, w, mean, rstd, dresid, dx, dw_part, db_part, M, N, w_offset);
+  if (ch <= 1) { MFT_NB(1) }
+  else if (ch <= 2) { MFT_NB(2) }
+  else if (ch <= 4) { MFT_NB(4) }
+  else { MFT_NB(8) }
+#undef MFT_NB
+  if (wgrad) {
+    reduce_rows_kernel<<<cdiv(N, 256), 256, 0, st>>>(dw_part, dw, nb, N, accumulate);
+    if (!RMS && db) reduce_rows_kernel<<<cdiv(N, 256), 256, 0, st>>>(db_part, db, nb, N, accumulate);
+  }
+}
+
+int norm_bwd_partial_blocks(int M) {
+  int nb = (M + 3) / 4;
+  return nb < 512 ? nb : 512;
+}
+
+void layernorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, const float* b,
+                   bf16_t* y, float* mean, float* rstd, int M, int N, float eps, hipStream_t st) {
+  norm_fwd_dispatch<false>(x, resid_delta, resid_out, w, b, y, mean, rstd, M, N, eps, 0.f, st);
+}
+
+void rmsnorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, bf16_t* y,
+                 float* rstd, int M, int N, float eps, float w_offset, hipStream_t st) {
+  norm_fwd_dispatch<true>(x, resid_delta, resid_out, w, nullptr, y, nullptr, rstd, M, N, eps, w_offset, st);
+}
+
+void layernorm_bwd(const bf16_t* x, const bf16_t* dy, const float* w, const float* mean, const float* rstd,
+                   const bf16_t* dresid, bf16_t* dx, float* dw, float* db, float* work, int M, int N, int accumulate,
+                   hipStream_t st) {
+  norm_bwd_dispatch<false>(x, dy, w, mean, rstd, dresid, dx, dw, db, work, M, N, 0.f, accumulate, st);
+}
+
+void rmsnorm_bwd(const bf16_t* x, const bf16_t* dy, const float* w, const float* rstd, const bf16_t* dresid,
+                 bf16_t* dx, float* dw, float* work, int M, int N, float w_offset, int accumulate, hipStream_t st) {
+  norm_bwd_dispatch<true>(x, dy, w, nullptr, rstd, dresid, dx, dw, nullptr, work, M, N, w_offset, accumulate, st);
+}
+
+}  // namespace mft

@@ -1,0 +1,123 @@
+// Fused optimizer kernels: global grad-norm (two-stage, deterministic), non-finite check, and a
+// single-launch AdamW over the flat fp32 parameter/grad/moment buffers.
+// Replaces Adam::step (optim/adam.cpp:25-90, per-element loops per tensor with coupled L2 decay,
+// SURVEY §8 Q8) and the three copies of clip_grad_norm (gpt2_lora_finetune/main.cpp:491-516,
+// optim/gemma_trainer.cpp:84-102, optim/trainer.cpp:66-92).
+// Everything that depends on step-time values (lr, step count, grad-norm, skip flag) is read from
+// device memory, so a captured hipGraph of the whole train step replays without host sync.
+#include "common.h"
+#include "kernels.h"
+
+namespace mft {
+
+int sumsq_blocks(long n) {
+  long b = (n / 4 + 255) / 256;
+  if (b < 1) b = 1;
+  return (int)(b < 1024 ? b : 1024);
+}
+
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ x, long n, float* __restrict__ part) {
+  __shared__ float red[16];
+  float s = 0.f;
+  const long n4 = n / 4;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = x4[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  if (blockIdx.x == 0)
+    for (long i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += x[i] * x[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ void sumsq_final_kernel(const float* __restrict__ part, int nb, float* __restrict__ out, int accumulate) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[0] = accumulate ? out[0] + s : s;
+}
+
+void sumsq(const float* x, long n, float* partial, float* out, int accumulate, hipStream_t st) {
+  const int nb = sumsq_blocks(n);
+  sumsq_partial_kernel<<<nb, 256, 0, st>>>(x, n, partial);
+  sumsq_final_kernel<<<1, 256, 0, st>>>(partial, nb, out, accumulate);
+}
+
+__global__ void nonfinite_kernel(const float* __restrict__ x, long n, int* __restrict__ flag) {
+  int bad = 0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    bad |= !isfinite(x[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+void nonfinite_check(const float* x, long n, int* flag, hipStream_t st) {
+  long g = (n + 255) / 256;
+  nonfinite_kernel<<<(int)(g < 1024 ? (g > 0 ? g : 1) : 1024), 256, 0, st>>>(x, n, flag);
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
+  if (a.nonfinite && *a.nonfinite) return;  // skip-step on NaN/Inf grads (fault tolerance)
+  const float lr = *a.lr_ptr;
+  const float t = *a.step_ptr;
+  const float bc1 = 1.f - powf(a.beta1, t);
+  const float bc2 = 1.f - powf(a.beta2, t);
+  float clip = 1.f;
+  if (a.sumsq) {
+    const float norm = sqrtf(*a.sumsq);
+    if (norm > a.max_norm) clip = a.max_norm / (norm + 1e-6f);
+  }
+  const float step_size = lr / bc1;
+  const float rbc2 = 1.f / sqrtf(bc2);
+  const float decay = a.l2_coupled ? 1.f : 1.f - lr * a.weight_decay;
+  const long n4 = a.n / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 p = reinterpret_cast<float4*>(a.p)[i];
+    float4 g = reinterpret_cast<const float4*>(a.g)[i];
+    float4 m = reinterpret_cast<float4*>(a.m)[i];
+    float4 v = reinterpret_cast<float4*>(a.v)[i];
+    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w}, mm[4] = {m.x, m.y, m.z, m.w},
+          vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gj = gg[j] * clip;
+      if (a.l2_coupled) gj += a.weight_decay * pp[j];
+      mm[j] = a.beta1 * mm[j] + (1.f - a.beta1) * gj;
+      vv[j] = a.beta2 * vv[j] + (1.f - a.beta2) * gj * gj;
+      const float denom = sqrtf(vv[j]) * rbc2 + a.eps;
+      pp[j] = pp[j] * decay - step_size * mm[j] / denom;
+    }
+    reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    reinterpret_cast<float4*>(a.m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+    reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    if (a.shadow) {
+      uint2 sh;
+      sh.x = pack_bf2(pp[0], pp[1]);
+      sh.y = pack_bf2(pp[2], pp[3]);
+      reinterpret_cast<uint2*>(a.shadow)[i] = sh;
+    }
+  }
+  if (blockIdx.x == 0) {
+    for (long i = n4 * 4 + threadIdx.x; i < a.n; i += blockDim.x) {
+      float gj = a.g[i] * clip;
+      float pj = a.p[i];
+      if (a.l2_coupled) gj += a.weight_decay * pj;
+      const float mj = a.beta1 * a.m[i] + (1.f - a.beta1) * gj;
+      const float vj = a.beta2 * a.v[i] + (1.f - a.beta2) * gj * gj;
+      pj = pj * decay - step_size * mj / (sqrtf(vj) * rbc2 + a.eps);
+      a.p[i] = pj;
+      a.m[i] = mj;
+      a.v[i] = vj;
+      if (a.shadow) a.shadow[i] = f2bf(pj);
+    }
+  }
+}
+
+void adamw_step(const AdamWArgs& a, hipStream_t st) {
+  long g = (a.n / 4 + 255) / 256;
+  if (g < 1) g = 1;
+  adamw_kernel<<<(int)(g < 2048 ? g : 2048), 256, 0, st>>>(a);
+}
+
+}  // namespace mft

@@ -1,0 +1,103 @@
+"""Building-block modules whose forward calls the fused ops of ``ops/functional.py``.
+
+Weight layouts: linear weights are ``[out, in]`` (nn.Linear convention; GPT-2's HF Conv1D
+``[in, out]`` weights are transposed once at load time, models/gpt2.py).  Linear/embedding weights
+are stored in the compute dtype (bf16 on GPU) when frozen; trainable ones become fp32 masters with
+a bf16 ``shadow`` once handed to ``utils.params.FlatParams``.  Norm weights are fp32.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from ..ops import functional as Fx
+
+
+@dataclass
+class LoRASlice:
+    """One LoRA adapter on columns [col0, col0 + ncols) of a (possibly fused) linear output.
+    A: [in, r], B: [r, ncols] (the reference checkpoint layout, graph/lora_saver.cpp:123-126)."""
+    col0: int
+    ncols: int
+    A: nn.Parameter
+    B: nn.Parameter
+    name: str = ""
+
+
+class Linear(nn.Module):
+    def __init__(self, in_features, out_features, bias=True, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features, dtype=dtype, device=device),
+                                   requires_grad=False)
+        self.bias = nn.Parameter(torch.zeros(out_features, dtype=dtype, device=device),
+                                 requires_grad=False) if bias else None
+        self.lora_slices: list[LoRASlice] = []
+        self.lora_scale = 0.0
+        self.lora_enabled = True
+        self._lora_params = nn.ParameterList()
+
+    def add_lora(self, col0, ncols, rank, scale, init_A, name=""):
+        dev = self.weight.device
+        A = nn.Parameter(init_A.to(device=dev, dtype=torch.float32))
+        B = nn.Parameter(torch.zeros(rank, ncols, dtype=torch.float32, device=dev))
+        self._lora_params.append(A)
+        self._lora_params.append(B)
+        self.lora_slices.append(LoRASlice(col0, ncols, A, B, name))
+        self.lora_scale = float(scale)
+        return A, B
+
+    def clear_lora(self):
+        self.lora_slices = []
+        self._lora_params = nn.ParameterList()
+
+    def forward(self, x):
+        if self.lora_slices and self.lora_enabled:
+            return Fx.lora_linear(x, self.weight, self.bias,
+                                  [(s.col0, s.ncols, s.A, s.B) for s in self.lora_slices], self.lora_scale)
+        return Fx.linear(x, self.weight, self.bias)
+
+    @torch.no_grad()
+    def merge_lora(self, sign: float = 1.0):
+        """W[col0:col0+n, :] += sign * s * (A B)^T  (merge; sign=-1 unmerges) — K10."""
+        for sl in self.lora_slices:
+            A, B = sl.A.detach().float(), sl.B.detach().float()
+            delta = (A @ B).t() * (sign * self.lora_scale)  # [n, in]
+            w = self.weight.data
+            w[sl.col0:sl.col0 + sl.ncols] = (w[sl.col0:sl.col0 + sl.ncols].float() + delta).to(w.dtype)
+            if getattr(self.weight, "shadow", None) is not None:
+                self.weight.shadow.copy_(self.weight.data.to(self.weight.shadow.dtype))
+
+    def extra_repr(self):
+        return f"in={self.in_features}, out={self.out_features}, lora_slices={len(self.lora_slices)}"
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, n, eps=1e-5, device=None):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(n, device=device), requires_grad=False)
+        self.bias = nn.Parameter(torch.zeros(n, device=device), requires_grad=False)
+        self.eps = eps
+
+    def forward(self, x):
+        return Fx.layer_norm(x, self.weight, self.bias, self.eps)
+
+    def add_forward(self, x, delta):
+        return Fx.add_layer_norm(x, delta, self.weight, self.bias, self.eps)
+
+
+class RMSNorm(nn.Module):
+    """Gemma-style RMSNorm: y = x * rstd * (offset + w), offset 1 (reference core/ops.cpp:1515)."""
+
+    def __init__(self, n, eps=1e-6, offset=1.0, device=None):
+        super().__init__()
+        self.weight = nn.Parameter(torch.zeros(n, device=device), requires_grad=False)
+        self.eps, self.offset = eps, offset
+
+    def forward(self, x):
+        return Fx.rms_norm(x, self.weight, self.eps, self.offset)
+
+    def add_forward(self, x, delta):
+        return Fx.add_rms_norm(x, delta, self.weight, self.eps, self.offset)

@@ -1,0 +1,568 @@
+"""Autograd-aware fused ops.
+
+GPU tensors -> the gfx950 HIP kernels of ``_C`` (no silent fallback: a missing extension raises).
+CPU tensors -> the fp32 PyTorch reference (``ops/reference.py``).
+
+Gradient convention (replaces the reference's overwrite-on-backward): every trainable
+parameter's ``.grad`` is a persistent view into a flat fp32 grad buffer (see
+``utils/params.py``).  The GPU backward kernels ACCUMULATE straight into ``p.grad`` and return
+``None`` for that input; if a parameter has no grad buffer yet a fresh gradient is returned and
+autograd's AccumulateGrad adds it.  Each accumulation calls ``grad_ready(p)`` so data-parallel
+engines can launch bucket all-reduces while backward is still running.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch.autograd import Function
+
+from .._ext import native
+from . import reference as ref
+
+# ---------------------------------------------------------------- parameter helpers
+
+_ready_hooks: list = []
+
+
+def register_grad_ready_hook(fn):
+    _ready_hooks.append(fn)
+    return fn
+
+
+def remove_grad_ready_hook(fn):
+    if fn in _ready_hooks:
+        _ready_hooks.remove(fn)
+
+
+def grad_ready(p):
+    for h in _ready_hooks:
+        h(p)
+
+
+def cw(p):
+    """Compute view of a parameter: its bf16 shadow if it has one, else the tensor itself."""
+    if p is None:
+        return None
+    return getattr(p, "shadow", None) if getattr(p, "shadow", None) is not None else p
+
+
+def _needs(p):
+    return p is not None and p.requires_grad
+
+
+def _sink(p, g):
+    """Accumulate fp32 gradient g into p.grad; returns what backward must return for p."""
+    if not _needs(p):
+        return None
+    if p.grad is not None:
+        p.grad.add_(g.view_as(p.grad).to(p.grad.dtype))
+        grad_ready(p)
+        return None
+    return g.to(p.dtype).view_as(p)
+
+
+def _grad_buf(p):
+    """fp32 buffer the kernels accumulate into directly (p.grad), or None."""
+    if _needs(p) and p.grad is not None and p.grad.dtype == torch.float32 and p.grad.is_contiguous():
+        return p.grad
+    return None
+
+
+# ---------------------------------------------------------------- normalisation
+class _Norm(Function):
+    @staticmethod
+    def forward(ctx, x, delta, w, b, eps, rms, offset):
+        C = native()
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        d2 = delta.reshape(-1, shape[-1]).contiguous() if delta is not None else None
+        wc = cw(w).float() if cw(w).dtype != torch.float32 else cw(w)
+        if rms:
+            y, s, rstd = C.rmsnorm_fwd(x2, d2, wc, eps, offset)
+            mean = None
+        else:
+            bc = cw(b).float() if cw(b).dtype != torch.float32 else cw(b)
+            y, s, mean, rstd = C.layernorm_fwd(x2, d2, wc, bc, eps)
+        xs = s if d2 is not None else x2
+        ctx.save_for_backward(xs, wc, mean if mean is not None else rstd, rstd)
+        ctx.params = (w, b)
+        ctx.rms, ctx.offset, ctx.has_delta, ctx.shape = rms, offset, d2 is not None, shape
+        if d2 is not None:
+            return s.view(shape), y.view(shape)
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        C = native()
+        xs, wc, mean, rstd = ctx.saved_tensors
+        w, b = ctx.params
+        N = ctx.shape[-1]
+        if ctx.has_delta:
+            ds, dy = grads
+        else:
+            ds, dy = None, grads[0]
+        dy2 = dy.reshape(-1, N).contiguous() if dy is not None else torch.zeros_like(xs)
+        if ds is not None and dy is None:
+            dy2 = torch.zeros_like(xs)
+        ds2 = ds.reshape(-1, N).contiguous() if ds is not None else None
+        dwb = _grad_buf(w)
+        tmp_w = torch.zeros(N, device=xs.device, dtype=torch.float32) if (_needs(w) and dwb is None) else None
+        dw_t = dwb if dwb is not None else tmp_w
+        if ctx.rms:
+            dx = C.rmsnorm_bwd(xs, dy2, wc, rstd, ds2, ctx.offset, dw_t)
+            gb = None
+        else:
+            dbb = _grad_buf(b)
+            tmp_b = torch.zeros(N, device=xs.device, dtype=torch.float32) if (_needs(b) and dbb is None) else None
+            db_t = dbb if dbb is not None else tmp_b
+            dx = C.layernorm_bwd(xs, dy2, wc, mean, rstd, ds2, dw_t, db_t)
+            gb = tmp_b if tmp_b is not None else None
+            if dbb is not None:
+                grad_ready(b)
+        gw = tmp_w if tmp_w is not None else None
+        if dwb is not None:
+            grad_ready(w)
+        dx = dx.view(ctx.shape)
+        gwr = gw.to(w.dtype).view_as(w) if gw is not None else None
+        gbr = gb.to(b.dtype).view_as(b) if gb is not None else None
+        return dx, (dx if ctx.has_delta else None), gwr, gbr, None, None, None
+
+
+def layer_norm(x, w, b, eps=1e-5):
+    if not x.is_cuda:
+        return ref.layer_norm(x, cw(w), cw(b), eps).to(x.dtype)
+    return _Norm.apply(x, None, w, b, eps, False, 0.0)
+
+
+def add_layer_norm(x, delta, w, b, eps=1e-5):
+    """s = x + delta; y = LayerNorm(s)  -> (s, y) (fused residual + norm)."""
+    if not x.is_cuda:
+        s = x + delta
+        return s, ref.layer_norm(s, cw(w), cw(b), eps).to(x.dtype)
+    return _Norm.apply(x, delta, w, b, eps, False, 0.0)
+
+
+def rms_norm(x, w, eps=1e-6, offset=1.0):
+    if not x.is_cuda:
+        return ref.rms_norm(x, cw(w), eps, offset).to(x.dtype)
+    return _Norm.apply(x, None, w, None, eps, True, offset)
+
+
+def add_rms_norm(x, delta, w, eps=1e-6, offset=1.0):
+    if not x.is_cuda:
+        s = x + delta
+        return s, ref.rms_norm(s, cw(w), eps, offset).to(x.dtype)
+    return _Norm.apply(x, delta, w, None, eps, True, offset)
+
+
+# ---------------------------------------------------------------- activations
+class _Gelu(Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        ctx.save_for_backward(x)
+        return native().gelu_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return native().gelu_bwd(x, dy.contiguous())
+
+
+class _Gated(Function):
+    @staticmethod
+    def forward(ctx, gu, act):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu)
+        ctx.act = act
+        return native().gated_fwd(gu, act)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (gu,) = ctx.saved_tensors
+        return native().gated_bwd(gu, dy.contiguous(), ctx.act), None
+
+
+def gelu(x):
+    if not x.is_cuda:
+        return ref.gelu_tanh(x).to(x.dtype)
+    return _Gelu.apply(x)
+
+
+def gated_act(gu, act="gelu"):
+    """gelu_tanh(gate) * up (GeGLU, Gemma) or silu(gate) * up (SwiGLU); gu = [gate | up]."""
+    a = 0 if act in ("gelu", "gelu_tanh", "gelu_pytorch_tanh") else 1
+    if not gu.is_cuda:
+        return ref.gated(gu, a).to(gu.dtype)
+    return _Gated.apply(gu, a)
+
+
+# ---------------------------------------------------------------- embedding
+class _Embedding(Function):
+    @staticmethod
+    def forward(ctx, ids, wte, wpe, S, scale):
+        ids = ids.reshape(-1).contiguous()
+        out = native().embed_fwd(ids, cw(wte), cw(wpe) if wpe is not None else None, S, 0, scale)
+        ctx.save_for_backward(ids)
+        ctx.params = (wte, wpe)
+        ctx.S, ctx.scale = S, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (ids,) = ctx.saved_tensors
+        wte, wpe = ctx.params
+        dout = dout.contiguous()
+        gte = gpe = None
+        if _needs(wte) or _needs(wpe):
+            bte = _grad_buf(wte)
+            bpe = _grad_buf(wpe)
+            tte = torch.zeros(wte.shape, device=dout.device) if (_needs(wte) and bte is None) else None
+            tpe = torch.zeros(wpe.shape, device=dout.device) if (_needs(wpe) and bpe is None) else None
+            native().embed_bwd(ids, dout, bte if bte is not None else tte, bpe if bpe is not None else tpe, ctx.S, 0,
+                               ctx.scale)
+            if bte is not None:
+                grad_ready(wte)
+            if bpe is not None:
+                grad_ready(wpe)
+            gte = tte.to(wte.dtype) if tte is not None else None
+            gpe = tpe.to(wpe.dtype) if tpe is not None else None
+        return None, gte, gpe, None, None
+
+
+def embedding(ids, wte, wpe=None, scale=1.0):
+    """ids [B,S] -> [B*S, C]: wte[ids]*scale (+ wpe[pos])."""
+    B, S = ids.shape
+    if not ids.is_cuda:
+        e = cw(wte)[ids.reshape(-1)].float()
+        if scale != 1.0:
+            e = e * scale
+        if wpe is not None:
+            e = e + cw(wpe)[:S].float().repeat(B, 1)
+        return e.to(cw(wte).dtype)
+    return _Embedding.apply(ids, wte, wpe, S, float(scale))
+
+
+# ---------------------------------------------------------------- attention
+class _FlashAttn(Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale, causal, window, kv_lens):
+        o, lse = native().attn_fwd(q, k, v, scale, causal, window, kv_lens)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.cfg = (scale, causal, window, kv_lens)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        scale, causal, window, kv_lens = ctx.cfg
+        dq = torch.empty(q.shape, device=q.device, dtype=q.dtype)
+        dk = torch.empty(k.shape, device=k.device, dtype=k.dtype)
+        dv = torch.empty(v.shape, device=v.device, dtype=v.dtype)
+        native().attn_bwd(q, k, v, o, do.contiguous(), lse, dq, dk, dv, scale, causal, window, kv_lens)
+        return dq, dk, dv, None, None, None, None
+
+
+class _FlashAttnPacked(Function):
+    """qkv [B,S,3,H,D] packed GEMM output consumed in place; backward writes one packed dqkv."""
+
+    @staticmethod
+    def forward(ctx, qkv, scale, causal, window, kv_lens):
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        o, lse = native().attn_fwd(q, k, v, scale, causal, window, kv_lens)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.cfg = (scale, causal, window, kv_lens)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        scale, causal, window, kv_lens = ctx.cfg
+        dqkv = torch.empty_like(qkv)
+        native().attn_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, do.contiguous(), lse, dqkv[:, :, 0],
+                          dqkv[:, :, 1], dqkv[:, :, 2], scale, causal, window, kv_lens)
+        return dqkv, None, None, None, None
+
+
+def flash_attention(q, k, v, scale=None, causal=True, window=0, kv_lens=None):
+    """q [B,Sq,H,D], k/v [B,Sk,Hkv,D] (strided views OK) -> o [B,Sq,H,D]."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if not q.is_cuda:
+        return ref.attention(q, k, v, scale, causal, window, kv_lens)[0].to(q.dtype).contiguous()
+    return _FlashAttn.apply(q, k, v, float(scale), bool(causal), int(window or 0), kv_lens)
+
+
+def flash_attention_qkvpacked(qkv, scale=None, causal=True, window=0, kv_lens=None):
+    if scale is None:
+        scale = 1.0 / math.sqrt(qkv.shape[-1])
+    if not qkv.is_cuda:
+        return ref.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], scale, causal, window, kv_lens)[0].to(qkv.dtype).contiguous()
+    return _FlashAttnPacked.apply(qkv, float(scale), bool(causal), int(window or 0), kv_lens)
+
+
+# ---------------------------------------------------------------- fused per-head RMSNorm + RoPE
+class _QKNormRoPE(Function):
+    @staticmethod
+    def forward(ctx, x, w, cos, sin, eps, offset, interleaved):
+        wc = cw(w)
+        y, rstd = native().qknorm_rope_fwd(x, wc, cos, sin, 0, eps, offset, interleaved)
+        ctx.save_for_backward(x, rstd, wc, cos, sin)
+        ctx.w = w
+        ctx.cfg = (offset, interleaved)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, rstd, wc, cos, sin = ctx.saved_tensors
+        w = ctx.w
+        offset, interleaved = ctx.cfg
+        dx = torch.empty(x.shape, device=x.device, dtype=x.dtype)
+        buf = _grad_buf(w)
+        tmp = torch.zeros(w.shape, device=x.device) if (_needs(w) and buf is None) else None
+        native().qknorm_rope_bwd(x, dy.contiguous(), rstd, wc, dx, buf if buf is not None else tmp, cos, sin, 0,
+                                 offset, interleaved)
+        if buf is not None:
+            grad_ready(w)
+        return dx, (tmp.to(w.dtype) if tmp is not None else None), None, None, None, None, None
+
+
+def qk_norm_rope(x, w, cos, sin, eps=1e-6, offset=1.0, interleaved=False):
+    """x [B,S,H,D] strided view -> rope(rmsnorm(x) * (w + offset)) contiguous [B,S,H,D]."""
+    if not x.is_cuda:
+        y = ref.rms_norm(x, cw(w), eps, offset).to(x.dtype)
+        return ref.rope(y, cos, sin, 0, interleaved).to(x.dtype)
+    return _QKNormRoPE.apply(x, w, cos, sin, float(eps), float(offset), bool(interleaved))
+
+
+# ---------------------------------------------------------------- linear layers
+def _mm_wgrad_into(buf, dy2, x2):
+    """buf (fp32 [N,K]) += dy2^T @ x2 with fp32 accumulation (hipBLASLt)."""
+    buf.add_(torch.mm(dy2.t(), x2, out_dtype=torch.float32))
+
+
+class _Linear(Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        wc, bc = cw(w), cw(b)
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        y = torch.addmm(bc, x2, wc.t()) if bc is not None else torch.mm(x2, wc.t())
+        ctx.save_for_backward(x2 if _needs(w) else None)
+        ctx.params = (w, b)
+        ctx.wc = wc
+        ctx.shape = shape
+        return y.view(*shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x2,) = ctx.saved_tensors
+        w, b = ctx.params
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2, ctx.wc).view(ctx.shape)
+        gw = gb = None
+        if _needs(w):
+            buf = _grad_buf(w)
+            if buf is not None:
+                _mm_wgrad_into(buf, dy2, x2)
+                grad_ready(w)
+            else:
+                gw = torch.mm(dy2.t(), x2, out_dtype=torch.float32).to(w.dtype)
+        if _needs(b):
+            s = dy2.float().sum(0)
+            gb = _sink(b, s)
+        return dx, gw, gb
+
+
+def linear(x, w, b=None):
+    """y = x W^T + b with W [out, in] (nn.Linear layout)."""
+    if not x.is_cuda:
+        y = x.float() @ cw(w).float().t()
+        if b is not None:
+            y = y + cw(b).float()
+        return y.to(x.dtype)
+    return _Linear.apply(x, w, b)
+
+
+class _LoRALinear(Function):
+    """y = x W^T + b + sum_i s * (x A_i) B_i placed in column slices [c0_i, c0_i + n_i) of y.
+
+    W (and b) frozen; A_i [in, r], B_i [r, n_i] fp32 masters with bf16 shadows (``p.shadow``).
+    One hipBLASLt base GEMM for the whole (possibly fused, e.g. q|k|v) weight, then the rank-r
+    work per slice in lora.hip (reference: LoRALinear slices {A,B,scale,col0,cols},
+    nn/lora_linear.h:17-97)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, s, slices, *ab):
+        C = native()
+        wc, bc = cw(w), cw(b)
+        shape = x.shape
+        K, N = shape[-1], wc.shape[0]
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        y = torch.addmm(bc, x2, wc.t()) if bc is not None else torch.mm(x2, wc.t())
+        us = []
+        for i, (c0, n) in enumerate(slices):
+            Ac, Bc = cw(ab[2 * i]), cw(ab[2 * i + 1])
+            R = Ac.shape[1]
+            u = torch.empty(x2.shape[0], R, device=x.device, dtype=x.dtype)
+            C.lora_rowdot(x2, Ac, R, 1, u, 1.0)                      # u = x A
+            ys = y[:, c0:c0 + n]
+            C.lora_update(ys, None, u, Bc, n, 1, ys, float(s))       # y[:, slice] += s u B
+            us.append(u)
+        ctx.save_for_backward(x2, *us)
+        ctx.params = ab
+        ctx.slices, ctx.wc = slices, wc
+        ctx.s, ctx.shape, ctx.N = float(s), shape, N
+        return y.view(*shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        x2, *us = ctx.saved_tensors
+        ab = ctx.params
+        s, N = ctx.s, ctx.N
+        K = x2.shape[1]
+        dy2 = dy.reshape(-1, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = torch.mm(dy2, ctx.wc) if ctx.needs_input_grad[0] else None
+        grads = []
+        for i, (c0, n) in enumerate(ctx.slices):
+            A, B = ab[2 * i], ab[2 * i + 1]
+            Ac, Bc = cw(A), cw(B)
+            R = Ac.shape[1]
+            dys = dy2[:, c0:c0 + n]
+            v = torch.empty(dy2.shape[0], R, device=dy.device, dtype=dy.dtype)
+            C.lora_rowdot(dys, Bc, 1, n, v, s)                       # v = s dy B^T
+            if dx is not None:
+                C.lora_update(dx, None, v, Ac, 1, R, dx, 1.0)        # dx += v A^T
+            gA = gB = None
+            if _needs(A):
+                buf = _grad_buf(A)
+                tgt = buf if buf is not None else torch.zeros(K, R, device=dy.device)
+                C.lora_wgrad(x2, v, tgt, R, 1, 1.0)                  # dA += x^T v
+                if buf is not None:
+                    grad_ready(A)
+                else:
+                    gA = tgt
+            if _needs(B):
+                buf = _grad_buf(B)
+                tgt = buf if buf is not None else torch.zeros(R, n, device=dy.device)
+                C.lora_wgrad(dys, us[i], tgt, 1, n, s)               # dB += s u^T dy
+                if buf is not None:
+                    grad_ready(B)
+                else:
+                    gB = tgt
+            grads += [gA, gB]
+        if dx is not None:
+            dx = dx.view(ctx.shape)
+        return (dx, None, None, None, None, *grads)
+
+
+def lora_linear(x, w, b, slices, scale):
+    """slices: list of (col0, ncols, A, B).  See _LoRALinear."""
+    if not x.is_cuda:
+        xf = x.float()
+        y = xf @ cw(w).float().t()
+        if b is not None:
+            y = y + cw(b).float()
+        parts = []
+        for (c0, n, A, B) in slices:
+            parts.append((c0, n, scale * ((xf @ cw(A).float()) @ cw(B).float())))
+        if parts:
+            y = y.clone()
+            for c0, n, d in parts:
+                y[..., c0:c0 + n] = y[..., c0:c0 + n] + d
+        return y.to(x.dtype)
+    meta = tuple((int(c0), int(n)) for (c0, n, _, _) in slices)
+    ab = []
+    for (_, _, A, B) in slices:
+        ab += [A, B]
+    return _LoRALinear.apply(x, w, b, float(scale), meta, *ab)
+
+
+# ---------------------------------------------------------------- fused LM head + cross entropy
+def default_ce_chunk(vpad: int) -> int:
+    """Rows per chunk so one chunk of bf16 logits (~96 MiB) stays in the 256 MiB Infinity Cache."""
+    rows = (96 << 20) // (2 * vpad)
+    return max(64, min(4096, rows // 64 * 64))
+
+
+class _LMHeadCE(Function):
+    @staticmethod
+    def forward(ctx, h, w, labels, V, chunk, w_grad_scale):
+        C = native()
+        wc = cw(w)
+        M = h.shape[0]
+        h = h.contiguous()
+        labels = labels.reshape(-1).contiguous()
+        valid = (labels >= 0).sum().float()
+        scale = 1.0 / valid.clamp(min=1.0)
+        loss_rows = torch.empty(M, device=h.device, dtype=torch.float32)
+        need_grad = ctx.needs_input_grad[0] or _needs(w)
+        dh = torch.empty_like(h) if need_grad else None
+        wbuf = _grad_buf(w) if need_grad else None
+        wtmp = torch.zeros(w.shape, device=h.device) if (need_grad and _needs(w) and wbuf is None) else None
+        for i in range(0, M, chunk):
+            hc = h[i:i + chunk]
+            logits = torch.mm(hc, wc.t())
+            C.xent_fwd_bwd(logits, labels[i:i + chunk], loss_rows[i:i + chunk], V, scale, 1.0, need_grad)
+            if need_grad:
+                torch.mm(logits, wc, out=dh[i:i + chunk])
+                if wbuf is not None or wtmp is not None:
+                    tgt = wbuf if wbuf is not None else wtmp
+                    tgt.add_(torch.mm(logits.t(), hc, out_dtype=torch.float32), alpha=w_grad_scale)
+        if wbuf is not None:
+            grad_ready(w)
+        loss = loss_rows.sum() * scale
+        ctx.save_for_backward(dh if dh is not None else torch.empty(0))
+        ctx.wtmp = wtmp
+        ctx.w = w
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        (dh,) = ctx.saved_tensors
+        dh = native().scale_bf16(dh, gout.float().reshape(1), 1.0)
+        gw = ctx.wtmp.to(ctx.w.dtype) if ctx.wtmp is not None else None
+        return dh, gw, None, None, None, None
+
+
+def lm_head_cross_entropy(h, w, labels, vocab_size, chunk=None, w_grad_scale=1.0):
+    """Mean token NLL of logits = h W^T (W [Vpad, C], first vocab_size rows real) vs labels
+    (already shifted; -100 = ignore).  Never materialises the full logits: chunks of rows are
+    GEMM'd, turned into dlogits in place and immediately multiplied back (dh, dW).
+    NOTE: the W gradient is produced during forward and scaled by ``w_grad_scale`` (pass the
+    same factor the loss is later multiplied by, e.g. 1/grad_accum); dh honours grad_output."""
+    if not h.is_cuda:
+        logits = h.float() @ cw(w).float().t()
+        logits = logits[:, :vocab_size]
+        return torch.nn.functional.cross_entropy(logits, labels.reshape(-1), ignore_index=-100)
+    if chunk is None:
+        chunk = default_ce_chunk(cw(w).shape[0])
+    return _LMHeadCE.apply(h, w, labels, int(vocab_size), int(chunk), float(w_grad_scale))
+
+
+def lm_head_token_nll(h, w, labels, vocab_size, chunk=None):
+    """Per-row NLL (no grad) for evaluation: returns (sum_nll, n_valid) device scalars."""
+    with torch.no_grad():
+        if not h.is_cuda:
+            logits = (h.float() @ cw(w).float().t())[:, :vocab_size]
+            nll = torch.nn.functional.cross_entropy(logits, labels.reshape(-1), ignore_index=-100, reduction="sum")
+            return nll, (labels >= 0).sum()
+        C = native()
+        wc = cw(w)
+        M = h.shape[0]
+        if chunk is None:
+            chunk = default_ce_chunk(wc.shape[0])
+        labels = labels.reshape(-1).contiguous()
+        loss_rows = torch.empty(M, device=h.device, dtype=torch.float32)
+        for i in range(0, M, chunk):
+            logits = torch.mm(h[i:i + chunk], wc.t())
+            C.xent_fwd_bwd(logits, labels[i:i + chunk], loss_rows[i:i + chunk], vocab_size, None, 1.0, False)
+        return loss_rows.sum(), (labels >= 0).sum()

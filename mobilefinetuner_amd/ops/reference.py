@@ -1,0 +1,103 @@
+"""Plain-PyTorch fp32 reference implementations of every fused op.
+
+These are (1) the numerics oracle the HIP kernels are tested against and (2) the path taken
+for CPU tensors (CPU-only CI, tokenizer/data tooling).  They mirror the semantics of the
+reference engine's ops where SURVEY §8 says we keep them, and HF/PEFT semantics elsewhere.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+
+def layer_norm(x, w, b, eps):
+    return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps)
+
+
+def rms_norm(x, w, eps, offset):
+    xf = x.float()
+    r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return xf * r * (w.float() + offset)
+
+
+def gelu_tanh(x):
+    return F.gelu(x.float(), approximate="tanh")
+
+
+def gated(gu, act):
+    g, u = gu.float().chunk(2, dim=-1)
+    a = F.gelu(g, approximate="tanh") if act == 0 else F.silu(g)
+    return a * u
+
+
+def attention(q, k, v, scale, causal=True, window=0, kv_lens=None):
+    """q [B,Sq,H,D], k/v [B,Sk,Hkv,D] -> o [B,Sq,H,D] (fp32), lse [B,H,Sq]."""
+    B, Sq, H, D = q.shape
+    Sk, Hkv = k.shape[1], k.shape[2]
+    G = H // Hkv
+    qf = q.float().permute(0, 2, 1, 3)
+    kf = k.float().permute(0, 2, 1, 3).repeat_interleave(G, dim=1)
+    vf = v.float().permute(0, 2, 1, 3).repeat_interleave(G, dim=1)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    i = torch.arange(Sq, device=q.device)[:, None] + (Sk - Sq)
+    j = torch.arange(Sk, device=q.device)[None, :]
+    allowed = torch.ones(Sq, Sk, dtype=torch.bool, device=q.device)
+    if causal:
+        allowed &= j <= i
+    if window and window > 0:
+        allowed &= (i - j) < window
+    allowed = allowed[None, None].expand(B, H, Sq, Sk).clone()
+    if kv_lens is not None:
+        allowed &= (j[None, None] < kv_lens.view(B, 1, 1, 1).to(q.device))
+    s = s.masked_fill(~allowed, float("-inf"))
+    lse = torch.logsumexp(s, dim=-1)
+    p = torch.softmax(s, dim=-1)
+    p = torch.nan_to_num(p, nan=0.0)
+    o = torch.matmul(p, vf).permute(0, 2, 1, 3)
+    return o, lse
+
+
+def rope_tables(seq_len, dim, theta, device=None, scaling_factor=1.0):
+    """cos/sin tables [seq_len, dim/2] fp32 (HF default rope; linear scaling divides positions)."""
+    inv = 1.0 / (theta ** (torch.arange(0, dim, 2, dtype=torch.float64) / dim))
+    pos = torch.arange(seq_len, dtype=torch.float64) / scaling_factor
+    f = torch.outer(pos, inv)
+    return f.cos().float().to(device), f.sin().float().to(device)
+
+
+def rope(x, cos, sin, pos0=0, interleaved=False):
+    """x [B,S,H,D]; rotate-half (HF) or interleaved pairs (reference compat)."""
+    S, D = x.shape[1], x.shape[-1]
+    c = cos[pos0:pos0 + S].view(1, S, 1, D // 2)
+    s = sin[pos0:pos0 + S].view(1, S, 1, D // 2)
+    xf = x.float()
+    if interleaved:
+        a, b = xf[..., 0::2], xf[..., 1::2]
+        out = torch.empty_like(xf)
+        out[..., 0::2] = a * c - b * s
+        out[..., 1::2] = b * c + a * s
+        return out
+    a, b = xf[..., : D // 2], xf[..., D // 2:]
+    return torch.cat([a * c - b * s, b * c + a * s], dim=-1)
+
+
+def cross_entropy_rows(logits, labels, V):
+    lf = logits[:, :V].float()
+    lse = torch.logsumexp(lf, dim=-1)
+    valid = (labels >= 0) & (labels < V)
+    lab = labels.clamp(0, V - 1)
+    tgt = lf.gather(1, lab[:, None]).squeeze(1)
+    return torch.where(valid, lse - tgt, torch.zeros_like(lse))
+
+
+def lm_cross_entropy(logits, labels, ignore_index=-100, reduction="mean"):
+    """HF-style shifted LM loss (core/lm_loss.cpp:106-210): logits[:, :-1] vs labels[:, 1:]."""
+    lg = logits[:, :-1].reshape(-1, logits.shape[-1]).float()
+    lb = labels[:, 1:].reshape(-1)
+    return F.cross_entropy(lg, lb, ignore_index=ignore_index, reduction=reduction)
+
+
+def perplexity(loss):
+    return math.exp(loss)

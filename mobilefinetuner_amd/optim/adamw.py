@@ -1,0 +1,133 @@
+"""Fused AdamW over the flat parameter buffer + global grad-norm clipping.
+
+Reference: Adam (operators/finetune_ops/optim/adam.h:23-104, adam.cpp:25-140) — bias-corrected Adam
+with *coupled* L2 weight decay (adam.cpp:65-67), AMSGrad option, save_state/load_state (stub) — and
+the clip_grad_norm copies (gpt2_lora_finetune/main.cpp:491-516: global L2 norm, scale
+max/(norm+1e-6) when norm > max).
+
+Here: decoupled AdamW by default (the PyTorch/PEFT alignment scripts' semantics,
+pytorch_alignment/gpt2_lora_finetune.py:239), ``l2_coupled=True`` reproduces the reference.  One
+kernel launch updates every trainable parameter, applies the clip factor computed on device, skips
+the step when any grad is non-finite, and writes the bf16 shadow weights.  lr / step / grad-norm
+live in device memory so the whole optimizer step can be replayed from a hipGraph.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .._ext import native
+from ..utils.params import FlatParams
+
+
+class FusedAdamW:
+    def __init__(self, flat: FlatParams, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 max_grad_norm: float | None = 1.0, l2_coupled: bool = False, skip_nonfinite: bool = True,
+                 param_range: tuple[int, int] | None = None):
+        self.flat = flat
+        self.beta1, self.beta2 = betas
+        self.eps, self.weight_decay = eps, weight_decay
+        self.max_grad_norm = max_grad_norm if (max_grad_norm or 0) > 0 else None
+        self.l2_coupled = l2_coupled
+        self.skip_nonfinite = skip_nonfinite
+        dev = flat.master.device
+        # optional sub-range (ZeRO-1/2: this rank owns [lo, hi) of the flat buffer)
+        self.lo, self.hi = param_range if param_range is not None else (0, flat.numel)
+        n = self.hi - self.lo
+        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.lr_dev = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
+        self.step_dev = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.sumsq_dev = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.nonfinite_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.lr = float(lr)
+        self.step_count = 0
+        self._lr_host = torch.zeros(1, dtype=torch.float32).pin_memory() if dev.type == "cuda" else None
+
+    # ---- host-side control (outside any captured graph)
+    def set_lr(self, lr: float):
+        self.lr = float(lr)
+        if self._lr_host is not None:
+            self._lr_host[0] = self.lr
+            self.lr_dev.copy_(self._lr_host, non_blocking=True)
+        else:
+            self.lr_dev.fill_(self.lr)
+
+    def grad_norm(self) -> float:
+        """Global grad L2 norm of the last step (host sync)."""
+        return math.sqrt(max(float(self.sumsq_dev.item()), 0.0))
+
+    def skipped_last(self) -> bool:
+        return bool(self.nonfinite_dev.item())
+
+    # ---- device work (graph-capturable)
+    def compute_grad_sumsq(self, extra_sumsq=None):
+        g = self.flat.grad[self.lo:self.hi]
+        if g.is_cuda:
+            native().sumsq(g, self.sumsq_dev, False)
+        else:
+            self.sumsq_dev.copy_(g.double().pow(2).sum().float().reshape(1))
+        if extra_sumsq is not None:  # sharded (ZeRO) norm: caller all-reduces
+            extra_sumsq(self.sumsq_dev)
+
+    def step(self, sumsq_ready: bool = False):
+        self.step_count += 1
+        self.step_dev.add_(1.0)
+        p = self.flat.master[self.lo:self.hi]
+        g = self.flat.grad[self.lo:self.hi]
+        if (self.max_grad_norm is not None) and not sumsq_ready:
+            self.compute_grad_sumsq()
+        if p.is_cuda:
+            C = native()
+            if self.skip_nonfinite:
+                self.nonfinite_dev.zero_()
+                C.nonfinite_check(g, self.nonfinite_dev)
+            sh = self.flat.shadow[self.lo:self.hi] if self.flat.shadow is not None else None
+            C.adamw_step(p, g, self.m, self.v, self.lr_dev, self.step_dev,
+                         self.sumsq_dev if self.max_grad_norm is not None else None,
+                         self.beta1, self.beta2, self.eps, self.weight_decay,
+                         float(self.max_grad_norm or 0.0), self.l2_coupled, sh,
+                         self.nonfinite_dev if self.skip_nonfinite else None)
+        else:
+            self._step_reference(p, g)
+
+    @torch.no_grad()
+    def _step_reference(self, p, g):
+        if self.skip_nonfinite and not torch.isfinite(g).all():
+            self.nonfinite_dev.fill_(1)
+            return
+        self.nonfinite_dev.fill_(0)
+        clip = 1.0
+        if self.max_grad_norm is not None:
+            norm = float(self.sumsq_dev.sqrt())
+            if norm > self.max_grad_norm:
+                clip = self.max_grad_norm / (norm + 1e-6)
+        t = float(self.step_dev)
+        lr = float(self.lr_dev)
+        gg = g * clip
+        if self.l2_coupled:
+            gg = gg + self.weight_decay * p
+        self.m.mul_(self.beta1).add_(gg, alpha=1 - self.beta1)
+        self.v.mul_(self.beta2).addcmul_(gg, gg, value=1 - self.beta2)
+        bc1 = 1 - self.beta1 ** t
+        bc2 = 1 - self.beta2 ** t
+        denom = self.v.sqrt() / math.sqrt(bc2) + self.eps
+        if not self.l2_coupled:
+            p.mul_(1 - lr * self.weight_decay)
+        p.addcdiv_(self.m, denom, value=-lr / bc1)
+        if self.flat.shadow is not None:
+            self.flat.shadow[self.lo:self.hi].copy_(p.to(self.flat.shadow.dtype))
+
+    # ---- state (full training-state checkpoint)
+    def state_dict(self):
+        return {"m": self.m.detach().cpu(), "v": self.v.detach().cpu(), "step": self.step_count,
+                "lr": self.lr, "betas": (self.beta1, self.beta2), "eps": self.eps,
+                "weight_decay": self.weight_decay, "range": (self.lo, self.hi)}
+
+    def load_state_dict(self, sd):
+        self.m.copy_(sd["m"].to(self.m.device))
+        self.v.copy_(sd["v"].to(self.v.device))
+        self.step_count = int(sd["step"])
+        self.step_dev.fill_(float(self.step_count))
+        self.set_lr(sd.get("lr", self.lr))

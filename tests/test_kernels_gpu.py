@@ -1,0 +1,327 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op (GPU only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, f"{msg} max abs err {err:.3e} > {tol:.3e}"
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+def test_native_loaded():
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    assert "_C" in C.__file__ or C.__name__.endswith("_C")
+
+
+@pytest.mark.parametrize("N", [768, 640, 1600, 256])
+@pytest.mark.parametrize("resid", [False, True])
+def test_layernorm(N, resid):
+    from mobilefinetuner_amd.ops import functional as Fx
+    M = 333
+    x = torch.randn(M, N, device=DEV).bfloat16().requires_grad_()
+    d = torch.randn(M, N, device=DEV).bfloat16().requires_grad_() if resid else None
+    w = torch.nn.Parameter(torch.randn(N, device=DEV))
+    b = torch.nn.Parameter(torch.randn(N, device=DEV))
+    if resid:
+        s, y = Fx.add_layer_norm(x, d, w, b)
+    else:
+        y = Fx.layer_norm(x, w, b)
+    gy = torch.randn_like(y)
+    gs = torch.randn_like(y) if resid else None
+    loss = (y.float() * gy.float()).sum() + ((s.float() * gs.float()).sum() if resid else 0)
+    loss.backward()
+    xr = x.detach().float().requires_grad_()
+    dr = d.detach().float().requires_grad_() if resid else None
+    wr = w.detach().clone().requires_grad_()
+    br = b.detach().clone().requires_grad_()
+    sr = (xr + dr).bfloat16().float() if resid else xr
+    yr = torch.nn.functional.layer_norm(sr, (N,), wr, br, 1e-5)
+    lr_ = (yr * gy.float()).sum() + ((sr * gs.float()).sum() if resid else 0)
+    lr_.backward()
+    _close(y, yr, 0.05, msg="ln y")
+    _close(x.grad, xr.grad, 0.08, 0.01, msg="ln dx")
+    _close(w.grad, wr.grad, 0.5, 0.01, msg="ln dw")
+    _close(b.grad, br.grad, 0.5, 0.01, msg="ln db")
+    if resid:
+        _close(d.grad, dr.grad, 0.08, 0.01, msg="ln ddelta")
+
+
+@pytest.mark.parametrize("N", [640, 1152, 256])
+def test_rmsnorm(N):
+    from mobilefinetuner_amd.ops import functional as Fx
+    M = 257
+    x = torch.randn(M, N, device=DEV).bfloat16().requires_grad_()
+    w = torch.nn.Parameter(torch.randn(N, device=DEV) * 0.1)
+    y = Fx.rms_norm(x, w, 1e-6, 1.0)
+    gy = torch.randn_like(y)
+    (y.float() * gy.float()).sum().backward()
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().clone().requires_grad_()
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + wr)
+    (yr * gy.float()).sum().backward()
+    _close(y, yr, 0.05, msg="rms y")
+    _close(x.grad, xr.grad, 0.08, 0.01, msg="rms dx")
+    _close(w.grad, wr.grad, 0.5, 0.01, msg="rms dw")
+
+
+def test_gelu_and_gated():
+    from mobilefinetuner_amd.ops import functional as Fx
+    x = torch.randn(129, 3072, device=DEV).bfloat16().requires_grad_()
+    y = Fx.gelu(x)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    xr = x.detach().float().requires_grad_()
+    yr = torch.nn.functional.gelu(xr, approximate="tanh")
+    (yr * g.float()).sum().backward()
+    _close(y, yr, 0.03, msg="gelu")
+    _close(x.grad, xr.grad, 0.05, msg="gelu dx")
+    for act in ("gelu", "silu"):
+        gu = torch.randn(77, 2 * 256, device=DEV).bfloat16().requires_grad_()
+        y = Fx.gated_act(gu, act)
+        g = torch.randn_like(y)
+        (y.float() * g.float()).sum().backward()
+        r = gu.detach().float().requires_grad_()
+        a, u = r.chunk(2, -1)
+        yr = (torch.nn.functional.gelu(a, approximate="tanh") if act == "gelu" else torch.nn.functional.silu(a)) * u
+        (yr * g.float()).sum().backward()
+        _close(y, yr, 0.05, msg=f"gated {act}")
+        _close(gu.grad, r.grad, 0.1, 0.01, msg=f"gated {act} grad")
+
+
+def _attn_ref(q, k, v, scale, causal, window, kv_lens=None):
+    from mobilefinetuner_amd.ops import reference as ref
+    return ref.attention(q, k, v, scale, causal, window, kv_lens)
+
+
+@pytest.mark.parametrize("B,S,H,Hkv,D,causal,window", [
+    (2, 128, 4, 4, 64, True, 0),
+    (3, 100, 2, 2, 64, True, 0),
+    (2, 256, 4, 1, 256, True, 0),
+    (1, 320, 4, 1, 256, True, 64),
+    (2, 64, 4, 2, 128, False, 0),
+    (1, 1024, 2, 2, 64, True, 0),
+])
+def test_flash_attention(B, S, H, Hkv, D, causal, window):
+    from mobilefinetuner_amd.ops import functional as Fx
+    q = torch.randn(B, S, H, D, device=DEV).bfloat16().requires_grad_()
+    k = torch.randn(B, S, Hkv, D, device=DEV).bfloat16().requires_grad_()
+    v = torch.randn(B, S, Hkv, D, device=DEV).bfloat16().requires_grad_()
+    scale = 1.0 / math.sqrt(D)
+    o = Fx.flash_attention(q, k, v, scale, causal, window)
+    go = torch.randn_like(o)
+    (o.float() * go.float()).sum().backward()
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf, _ = _attn_ref(qr, kr, vr, scale, causal, window)
+    (orf * go.float()).sum().backward()
+    _close(o, orf, 0.03, msg="attn o")
+    _close(q.grad, qr.grad, 0.06, 0.02, msg="attn dq")
+    _close(k.grad, kr.grad, 0.06, 0.02, msg="attn dk")
+    _close(v.grad, vr.grad, 0.06, 0.02, msg="attn dv")
+
+
+def test_flash_attention_lse_and_spike():
+    """Force the online-softmax rescale branch (guide §5.4 rule 26): spike one key."""
+    from mobilefinetuner_amd._ext import native
+    B, S, H, D = 1, 256, 2, 64
+    q = torch.randn(B, S, H, D, device=DEV)
+    k = torch.randn(B, S, H, D, device=DEV)
+    v = torch.randn(B, S, H, D, device=DEV)
+    k[0, 200] *= 30.0
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    o, lse = native().attn_fwd(q, k, v, 0.125, True, 0, None)
+    orf, lser = _attn_ref(q.float(), k.float(), v.float(), 0.125, True, 0)
+    _close(o, orf, 0.03, msg="spike o")
+    _close(lse, lser, 0.05, msg="spike lse")
+
+
+def test_flash_attention_packed_and_kvlens():
+    from mobilefinetuner_amd.ops import functional as Fx
+    B, S, H, D = 2, 128, 3, 64
+    qkv = torch.randn(B, S, 3, H, D, device=DEV).bfloat16().requires_grad_()
+    kv = torch.tensor([128, 77], dtype=torch.int32, device=DEV)
+    o = Fx.flash_attention_qkvpacked(qkv, 0.125, True, 0, kv)
+    go = torch.randn_like(o)
+    (o.float() * go.float()).sum().backward()
+    r = qkv.detach().float().requires_grad_()
+    orf, _ = _attn_ref(r[:, :, 0], r[:, :, 1], r[:, :, 2], 0.125, True, 0, kv)
+    (orf * go.float()).sum().backward()
+    # rows >= kv_len of batch 1 still attend to keys < 77 (causal + padding)
+    _close(o, orf, 0.03, msg="packed o")
+    _close(qkv.grad, r.grad, 0.06, 0.02, msg="packed dqkv")
+
+
+@pytest.mark.parametrize("V,C", [(50257, 768), (1000, 128)])
+def test_lm_head_ce(V, C):
+    from mobilefinetuner_amd.ops import functional as Fx
+    M = 300
+    Vp = (V + 127) // 128 * 128
+    h = (torch.randn(M, C, device=DEV) * 0.5).bfloat16().requires_grad_()
+    w = torch.zeros(Vp, C, device=DEV)
+    w[:V] = torch.randn(V, C, device=DEV) * 0.05
+    w = torch.nn.Parameter(w.bfloat16())
+    lab = torch.randint(0, V, (M,), device=DEV)
+    lab[::7] = -100
+    loss = Fx.lm_head_cross_entropy(h, w, lab, V, chunk=128)
+    (loss * 0.5).backward()
+    hr = h.detach().float().requires_grad_()
+    wr = w.detach().float()[:V].requires_grad_()
+    lr_ = torch.nn.functional.cross_entropy(hr @ wr.t(), lab, ignore_index=-100)
+    (lr_ * 0.5).backward()
+    assert abs(loss.item() - lr_.item()) < 2e-2 * max(1.0, lr_.item())
+    _close(h.grad, hr.grad, 2e-3, 0.03, msg="ce dh")
+
+
+def test_lora_linear():
+    from mobilefinetuner_amd.ops import functional as Fx
+    M, K, N, R = 250, 768, 2304, 8
+    x = (torch.randn(M, K, device=DEV) * 0.5).bfloat16().requires_grad_()
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    slices = []
+    refs = []
+    for (c0, n) in [(0, 768), (768, 768), (1536, 768)]:
+        A = torch.nn.Parameter(torch.randn(K, R, device=DEV) * 0.05)
+        B = torch.nn.Parameter(torch.randn(R, n, device=DEV) * 0.05)
+        A.shadow = A.detach().bfloat16()
+        B.shadow = B.detach().bfloat16()
+        slices.append((c0, n, A, B))
+    y = Fx.lora_linear(x, W, b, slices, 2.0)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    xr = x.detach().float().requires_grad_()
+    yr = xr @ W.float().t() + b.float()
+    parts = []
+    for (c0, n, A, B) in slices:
+        Ar = A.shadow.float().requires_grad_()
+        Br = B.shadow.float().requires_grad_()
+        refs.append((Ar, Br))
+        parts.append(2.0 * (xr @ Ar) @ Br)
+    yr = yr + torch.cat(parts, dim=1)
+    (yr * g.float()).sum().backward()
+    _close(y, yr, 0.05, 0.01, msg="lora y")
+    _close(x.grad, xr.grad, 0.1, 0.01, msg="lora dx")
+    for (c0, n, A, B), (Ar, Br) in zip(slices, refs):
+        _close(A.grad, Ar.grad, 0.05, 0.02, msg="lora dA")
+        _close(B.grad, Br.grad, 0.05, 0.02, msg="lora dB")
+
+
+def test_embedding():
+    from mobilefinetuner_amd.ops import functional as Fx
+    V, C, B, S = 1000, 128, 3, 17
+    wte = torch.nn.Parameter(torch.randn(V, C, device=DEV).bfloat16().float())
+    wte.shadow = wte.detach().bfloat16()
+    wpe = torch.nn.Parameter(torch.randn(64, C, device=DEV).bfloat16().float())
+    wpe.shadow = wpe.detach().bfloat16()
+    wte.grad = torch.zeros_like(wte)
+    wpe.grad = torch.zeros_like(wpe)
+    ids = torch.randint(0, V, (B, S), device=DEV)
+    out = Fx.embedding(ids, wte, wpe)
+    ref = (wte.detach()[ids.reshape(-1)] + wpe.detach()[:S].repeat(B, 1))
+    _close(out, ref, 0.05, msg="emb")
+    g = torch.randn_like(out)
+    (out.float() * g.float()).sum().backward()
+    dwte = torch.zeros(V, C, device=DEV).index_add_(0, ids.reshape(-1), g.float())
+    dwpe = g.float().view(B, S, C).sum(0)
+    _close(wte.grad, dwte, 0.05, msg="emb dwte")
+    _close(wpe.grad[:S], dwpe, 0.05, msg="emb dwpe")
+
+
+def test_qknorm_rope():
+    from mobilefinetuner_amd.ops import functional as Fx
+    from mobilefinetuner_amd.ops import reference as ref
+    B, S, H, D = 2, 64, 4, 256
+    big = torch.randn(B, S, H + 2, D, device=DEV).bfloat16().requires_grad_()
+    x = big[:, :, 1:1 + H]
+    w = torch.nn.Parameter(torch.randn(D, device=DEV) * 0.1)
+    cos, sin = ref.rope_tables(S, D, 10000.0, DEV)
+    y = Fx.qk_norm_rope(x, w, cos, sin, 1e-6, 1.0)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    r = big.detach().float().requires_grad_()
+    wr = w.detach().clone().requires_grad_()
+    xr = r[:, :, 1:1 + H]
+    yn = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + wr)
+    yr = ref.rope(yn, cos, sin)
+    (yr * g.float()).sum().backward()
+    _close(y, yr, 0.06, msg="qkrope y")
+    _close(big.grad, r.grad, 0.1, 0.01, msg="qkrope dx")
+    _close(w.grad, wr.grad, 0.5, 0.01, msg="qkrope dw")
+
+
+def test_adamw_matches_reference():
+    from mobilefinetuner_amd.optim.adamw import FusedAdamW
+    from mobilefinetuner_amd.utils.params import FlatParams
+    ps = [("a", torch.nn.Parameter(torch.randn(1000))), ("b", torch.nn.Parameter(torch.randn(37, 5)))]
+    ps_cpu = [("a", torch.nn.Parameter(ps[0][1].detach().clone())), ("b", torch.nn.Parameter(ps[1][1].detach().clone()))]
+    fg = FlatParams(ps, DEV)
+    fc = FlatParams(ps_cpu, "cpu")
+    og = FusedAdamW(fg, lr=1e-2, weight_decay=0.1, max_grad_norm=0.5)
+    oc = FusedAdamW(fc, lr=1e-2, weight_decay=0.1, max_grad_norm=0.5)
+    for it in range(5):
+        grads = [torch.randn(1000), torch.randn(37, 5)]
+        for (_, p), gr in zip(fg.named(), grads):
+            p.grad.copy_(gr.to(DEV))
+        for (_, p), gr in zip(fc.named(), grads):
+            p.grad.copy_(gr)
+        og.step()
+        oc.step()
+    _close(fg.master.cpu(), fc.master, 1e-5, 1e-5, msg="adamw master")
+    _close(fg.shadow.cpu().float(), fc.master, 2e-2, msg="adamw shadow")
+    assert abs(og.grad_norm() - oc.grad_norm()) < 1e-3 * oc.grad_norm()
+
+
+def test_adamw_skips_nonfinite():
+    from mobilefinetuner_amd.optim.adamw import FusedAdamW
+    from mobilefinetuner_amd.utils.params import FlatParams
+    fg = FlatParams([("a", torch.nn.Parameter(torch.randn(100)))], DEV)
+    before = fg.master.clone()
+    o = FusedAdamW(fg, lr=1e-1)
+    fg.grad[3] = float("nan")
+    o.step()
+    assert torch.equal(fg.master, before) and o.skipped_last()
+
+
+def test_casts_and_scale():
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    x = torch.randn(1001, device=DEV)
+    y = torch.empty(1001, device=DEV, dtype=torch.bfloat16)
+    C.cast_f32_bf16(x, y)
+    assert torch.equal(y, x.bfloat16())
+    z = torch.empty(1001, device=DEV)
+    C.cast_bf16_f32(y, z)
+    assert torch.equal(z, y.float())
+    s = C.scale_bf16(y, torch.tensor([2.0], device=DEV), 0.5)
+    _close(s, y.float(), 1e-2)
+
+
+def test_gpt2_train_step_decreases_loss():
+    from mobilefinetuner_amd.models.gpt2 import GPT2Config, GPT2Model
+    from mobilefinetuner_amd.optim.adamw import FusedAdamW
+    from mobilefinetuner_amd.peft.lora import LoraSpec, inject_gpt2, lora_parameters
+    from mobilefinetuner_amd.train.engine import TrainStep
+    from mobilefinetuner_amd.utils.params import FlatParams
+    cfg = GPT2Config.preset("gpt2-tiny")
+    m = GPT2Model(cfg, device=DEV)
+    inject_gpt2(m, LoraSpec(rank=8, alpha=16, targets=["AttnQKV", "AttnProj", "MlpFcIn", "MlpFcOut"]))
+    flat = FlatParams(lora_parameters(m), DEV)
+    opt = FusedAdamW(flat, lr=3e-3)
+    st = TrainStep(m, flat, opt, use_graph=True)
+    ids = torch.randint(0, cfg.vocab_size, (4, 65), device=DEV)
+    batch = [(ids[:, :-1].contiguous(), ids[:, 1:].contiguous())]
+    losses = [float(st(batch).item()) for _ in range(30)]
+    assert losses[-1] < losses[0] - 0.1, losses
