@@ -4,7 +4,7 @@
 // current HIP stream.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 
 #include "kernels.h"
 
@@ -34,7 +34,7 @@ std::vector<Tensor> layernorm_fwd(Tensor x, c10::optional<Tensor> delta, Tensor 
   const int N = x.size(-1);
   TORCH_CHECK(N % 8 == 0 && N <= 4096, "layernorm: width must be a multiple of 8 and <= 4096");
   const int M = x.numel() / N;
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   auto y = torch::empty_like(x);
   auto mean = torch::empty({M}, x.options().dtype(torch::kFloat32));
   auto rstd = torch::empty({M}, x.options().dtype(torch::kFloat32));
@@ -52,7 +52,7 @@ Tensor layernorm_bwd(Tensor x, Tensor dy, Tensor w, Tensor mean, Tensor rstd, c1
                      c10::optional<Tensor> dw, c10::optional<Tensor> db) {
   CHECK_CONTIG(x); CHECK_CONTIG(dy);
   const int N = x.size(-1), M = x.numel() / N;
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   auto dx = torch::empty_like(x);
   Tensor work;
   float* dwp = optp<float>(dw);
@@ -67,7 +67,7 @@ std::vector<Tensor> rmsnorm_fwd(Tensor x, c10::optional<Tensor> delta, Tensor w,
   const int N = x.size(-1);
   TORCH_CHECK(N % 8 == 0 && N <= 4096, "rmsnorm: width must be a multiple of 8 and <= 4096");
   const int M = x.numel() / N;
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   auto y = torch::empty_like(x);
   auto rstd = torch::empty({M}, x.options().dtype(torch::kFloat32));
   Tensor s;
@@ -81,7 +81,7 @@ Tensor rmsnorm_bwd(Tensor x, Tensor dy, Tensor w, Tensor rstd, c10::optional<Ten
                    c10::optional<Tensor> dw) {
   CHECK_CONTIG(x); CHECK_CONTIG(dy);
   const int N = x.size(-1), M = x.numel() / N;
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   auto dx = torch::empty_like(x);
   Tensor work;
   float* dwp = optp<float>(dw);
@@ -106,7 +106,7 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, double scale, bool ca
   const int Sk = k.size(1), Hkv = k.size(2);
   TORCH_CHECK(H % Hkv == 0, "H must be a multiple of Hkv");
   TORCH_CHECK(D == 64 || D == 128 || D == 256, "head dim must be 64, 128 or 256");
-  c10::hip::HIPGuard g(q.device());
+  c10::DeviceGuard g(q.device());
   auto o = torch::empty({B, Sq, H, D}, q.options());
   auto lse = torch::empty({B, H, Sq}, q.options().dtype(torch::kFloat32));
   mft::AttnArgs a{};
@@ -123,7 +123,7 @@ void attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, T
               double scale, bool causal, int64_t window, c10::optional<Tensor> kv_lens) {
   const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
   const int Sk = k.size(1), Hkv = k.size(2);
-  c10::hip::HIPGuard g(q.device());
+  c10::DeviceGuard g(q.device());
   auto delta = torch::empty({B, H, Sq}, q.options().dtype(torch::kFloat32));
   auto dq_acc = torch::empty({B, Sq, H, D}, q.options().dtype(torch::kFloat32));
   Tensor dk_tmp, dv_tmp;
@@ -241,32 +241,39 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor step, 
 }
 
 // ------------------------------------------------------------------ LoRA
-void lora_rowdot(Tensor X, Tensor W, int64_t wsk, int64_t wsr, Tensor U, double s) {
-  CHECK_BF16(X); CHECK_BF16(W); CHECK_BF16(U);
-  TORCH_CHECK(X.stride(-1) == 1 && U.stride(-1) == 1, "rows must be contiguous");
-  const int K = X.size(-1), R = U.size(-1);
+// U = s * X Wt^T   (X [.., K] rows contiguous, Wt [R, K] contiguous rows)
+void lora_rowdot(Tensor X, Tensor Wt, Tensor U, double s) {
+  CHECK_BF16(X); CHECK_BF16(Wt); CHECK_BF16(U);
+  TORCH_CHECK(X.stride(-1) == 1 && U.stride(-1) == 1 && Wt.stride(-1) == 1, "rows must be contiguous");
+  const int K = X.size(-1), R = Wt.size(0);
+  TORCH_CHECK(Wt.size(1) == K && U.size(-1) == R, "lora_rowdot: shape mismatch");
+  TORCH_CHECK(K % 32 == 0, "lora: in-features must be a multiple of 32");
+  TORCH_CHECK(X.stride(-2) % 8 == 0 && Wt.stride(0) % 8 == 0, "lora_rowdot: row strides must be multiples of 8");
   const long M = X.numel() / K;
-  TORCH_CHECK(K % 8 == 0, "lora: in-features must be a multiple of 8");
-  mft::lora_rowdot(bp(X), X.stride(-2), bp(W), wsk, wsr, bp(U), U.stride(-2), M, K, R, (float)s, stream());
+  mft::lora_rowdot(bp(X), X.stride(-2), bp(Wt), Wt.stride(0), bp(U), U.stride(-2), M, K, R, (float)s, stream());
 }
-void lora_update(Tensor base, c10::optional<Tensor> bias, Tensor U, Tensor W, int64_t wsr, int64_t wsn, Tensor Y,
-                 double s) {
-  CHECK_BF16(base); CHECK_BF16(Y);
+// Y = base + s * U W   (W [R, N]); Y may alias base
+void lora_update(Tensor base, Tensor U, Tensor W, Tensor Y, double s) {
+  CHECK_BF16(base); CHECK_BF16(Y); CHECK_BF16(U); CHECK_BF16(W);
   const int N = Y.size(-1), R = U.size(-1);
+  TORCH_CHECK(W.size(0) == R && W.size(1) == N && W.stride(1) == 1, "lora_update: W must be [R, N]");
+  TORCH_CHECK(N % 8 == 0 && W.stride(0) % 8 == 0 && base.stride(-2) % 8 == 0 && Y.stride(-2) % 8 == 0,
+              "lora_update: widths/strides must be multiples of 8");
   const long M = Y.numel() / N;
-  TORCH_CHECK(N % 8 == 0, "lora: out-features must be a multiple of 8");
-  mft::lora_update(bp(base), base.stride(-2), optp<float>(bias), bp(U), U.stride(-2), bp(W), wsr, wsn, bp(Y),
-                   Y.stride(-2), M, N, R, (float)s, stream());
+  mft::lora_update(bp(base), base.stride(-2), bp(U), U.stride(-2), bp(W), W.stride(0), bp(Y), Y.stride(-2), M, N, R,
+                   (float)s, stream());
 }
 void lora_wgrad(Tensor X, Tensor Y, Tensor out, int64_t osk, int64_t osr, double scale) {
   CHECK_BF16(X); CHECK_BF16(Y); CHECK_F32(out);
+  TORCH_CHECK(X.stride(-1) == 1 && X.stride(-2) % 8 == 0, "lora_wgrad: X rows must be contiguous, stride % 8 == 0");
   const int K = X.size(-1), R = Y.size(-1);
+  TORCH_CHECK(K % 8 == 0, "lora_wgrad: K must be a multiple of 8");
   const long M = X.numel() / K;
   mft::lora_wgrad(bp(X), X.stride(-2), bp(Y), Y.stride(-2), fp(out), osk, osr, M, K, R, (float)scale, stream());
 }
 void lora_merge(Tensor W, int64_t wsk, int64_t wsn, Tensor A, Tensor B, double s) {
   CHECK_F32(A); CHECK_F32(B); CHECK_CONTIG(A); CHECK_CONTIG(B);
-  const int K = A.size(0), R = A.size(1), N = B.size(1);
+  const int R = A.size(0), K = A.size(1), N = B.size(1);
   const bool isbf = W.scalar_type() == torch::kBFloat16;
   TORCH_CHECK(isbf || W.scalar_type() == torch::kFloat32, "merge target must be bf16 or fp32");
   mft::lora_merge(W.data_ptr(), isbf, wsk, wsn, fp(A), fp(B), K, N, R, (float)s, stream());

@@ -1,110 +1,155 @@
-// LoRA rank-r kernels (r <= 64): the skinny products around the frozen base GEMM.
+// LoRA rank-r kernels: the skinny products around the frozen base GEMM.
 //
 // Replaces LoRALinear::forward/merge/unmerge (nn/lora_linear.cpp:47-178), whose partial-column
 // slices were added without autograd, and the never-constructed
 // LoRALinearBackward (core/backward_functions.cpp:1012-1226).
 //
-// For y = x W (+b) + s (x A) B with W frozen, the base GEMM runs on hipBLASLt and these kernels
-// do the rank-r work:
-//   lora_rowdot : u[m, r] = s * sum_k X[m, k] W[k, r]           (x A  and  s * dy B^T)
-//   lora_update : Y[m, n] = base[m, n] (+ bias[n]) + s * sum_r U[m, r] W[r, n]
-//                 (forward epilogue y = base + b + s u B, and dx += v A^T in backward; in place)
-//   lora_wgrad  : out[k, r] += scale * sum_m X[m, k] Y[m, r]    (dA = x^T v, dB = s u^T dy),
-//                 accumulated straight into the fp32 flat grad buffer with atomics (grad
-//                 accumulation semantics).
-//   lora_merge  : W[k, n] += s * sum_r A[k, r] B[r, n]           (merge / unmerge, K10)
-// All row-streaming kernels use 16-B vector loads; the rank-r factor is tiny and L1/L2 resident.
-#include "common.h"
+// Internal layouts: A is [R, K] (PEFT lora_A.weight), B is [R, N] (reference lora_B layout), so
+// every rank-r operand is read along contiguous rows.  For y = x W^T + s (x A^T) B:
+//   lora_rowdot : U[m, r] = s * sum_k X[m, k] Wt[r, k]           u = x A^T (Wt = A), v = s dy B^T (Wt = B)
+//                 MFMA 16x16x32: one 16-row tile per 4-wave block, K split over the waves and
+//                 reduced through LDS; X streamed once from HBM with 16-B loads.
+//   lora_update : Y[m, n] = base[m, n] + s * sum_r U[m, r] W[r, n]  y += s u B (W = B), dx += v A (W = A)
+//                 VALU; each thread keeps its 8 columns of W in registers for a strip of rows.
+//   lora_wgrad  : out[k*osk + r*osr] += scale * sum_m X[m, k] Y[m, r]
+//                 dA = v^T x, dB = s u^T dy.  MFMA with the X / Y tiles staged row-major in LDS
+//                 and read transposed (ds_read_b64_tr_b16); one fp32 atomic per output element
+//                 per 512-row chunk straight into the flat grad buffer (accumulation semantics).
+//   lora_merge  : W[k, n] += s * sum_r A[r, k] B[r, n]                merge / unmerge (K10)
+#include "mfma.h"
 #include "kernels.h"
 
 namespace mft {
 
-// one wave per row m; lanes stride over 8-wide k chunks; R partial sums per lane, wave-reduced.
-template <int R>
-__global__ __launch_bounds__(256) void lora_rowdot_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
-                                                          long wsk, long wsr, bf16_t* __restrict__ U, long ldu, long M,
-                                                          int K, float s) {
-  const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (m >= M) return;
-  float acc[R];
+// ------------------------------------------------------------------------------------ rowdot
+// block = 4 waves; rows [16*blockIdx.x, +16); wave w handles k in [w*Kq, (w+1)*Kq).
+// Each 16-col output tile covers ranks [16*t, 16*t+16) of R (RT tiles).
+template <int RT>
+__global__ __launch_bounds__(256) void lora_rowdot_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Wt,
+                                                          long ldw, bf16_t* __restrict__ U, long ldu, long M, int K, int R,
+                                                          float s) {
+  __shared__ __attribute__((aligned(16))) float red[4][RT][64][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long m0 = (long)blockIdx.x * 16;
+  const long mr = m0 + (lane & 15);
+  const bool row_ok = mr < M;
+  const int nks = K / 32;
+  const int per = (nks + 3) / 4;
+  const int ks0 = w * per, ks1 = min(nks, ks0 + per);
+  f32x4_t acc[RT];
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.f;
-  for (int k = lane * 8; k < K; k += 512) {
-    float xv[8];
-    load8(X + m * ldx + k, xv);
+  for (int t = 0; t < RT; ++t) acc[t] = zero4();
+  for (int ks = ks0; ks < ks1; ++ks) {
+    const int k = ks * 32 + 8 * (lane >> 4);
+    bf16x8_t a = row_ok ? *reinterpret_cast<const bf16x8_t*>(X + mr * ldx + k) : bf16x8_t{};
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] += xv[j] * bf2f(W[(k + j) * wsk + r * wsr]);
+    for (int t = 0; t < RT; ++t) {
+      const int r = t * 16 + (lane & 15);
+      bf16x8_t b = r < R ? *reinterpret_cast<const bf16x8_t*>(Wt + (long)r * ldw + k) : bf16x8_t{};
+      acc[t] = mfma16(a, b, acc[t]);
+    }
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
-  if (lane < R) {
-    float v = 0.f;
+  for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-      if (lane == r) v = acc[r];
-    U[m * ldu + lane] = f2bf(v * s);
+    for (int i = 0; i < 4; ++i) red[w][t][lane][i] = acc[t][i];
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = red[0][t][lane][i] + red[1][t][lane][i] + red[2][t][lane][i] + red[3][t][lane][i];
+        const long m = m0 + 4 * (lane >> 4) + i;
+        const int r = t * 16 + (lane & 15);
+        if (m < M && r < R) U[m * ldu + r] = f2bf(v * s);
+      }
+    }
   }
 }
 
+// ------------------------------------------------------------------------------------ update
+// grid (ceil(N/8/blockDim), ceil(M/ROWS)); thread owns 8 columns, W[0..R)[n..n+8) in registers.
 template <int R>
-__global__ __launch_bounds__(256) void lora_update_kernel(const bf16_t* base, long ldb, const float* __restrict__ bias,
-                                                          const bf16_t* __restrict__ U, long ldu, const bf16_t* __restrict__ W,
-                                                          long wsr, long wsn, bf16_t* Y, long ldy, long M, int N, float s) {
-  const int c8 = N / 8;
-  const long total = M * c8;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const long m = t / c8;
-    const int n = (int)(t % c8) * 8;
+__global__ __launch_bounds__(256) void lora_update_kernel(const bf16_t* base, long ldb, const bf16_t* __restrict__ U, long ldu,
+                                                          const bf16_t* __restrict__ W, long ldw, bf16_t* Y, long ldy, long M,
+                                                          int N, int rows, float s) {
+  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (n >= N) return;
+  float wr[R][8];
+#pragma unroll
+  for (int r = 0; r < R; ++r) load8(W + (long)r * ldw + n, wr[r]);
+  const long m0 = (long)blockIdx.y * rows;
+  const long m1 = min(M, m0 + rows);
+  for (long m = m0; m < m1; ++m) {
     float y[8], u[R];
     load8(base + m * ldb + n, y);
 #pragma unroll
     for (int r = 0; r < R; ++r) u[r] = bf2f(U[m * ldu + r]) * s;
-    if (bias) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] += bias[n + j];
-    }
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] += u[r] * bf2f(W[r * wsr + (n + j) * wsn]);
+      for (int j = 0; j < 8; ++j) y[j] += u[r] * wr[r][j];
     store8(Y + m * ldy + n, y);
   }
 }
 
-// grid: (K/8/64 column groups, Mchunks); one thread = 8 columns k, R outputs each.
-template <int R>
-__global__ __launch_bounds__(64) void lora_wgrad_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Y,
-                                                        long ldy, float* __restrict__ out, long osk, long osr, long M, int K,
-                                                        long rows_per_chunk, float scale) {
-  const int k = (blockIdx.x * 64 + threadIdx.x) * 8;
-  if (k >= K) return;
-  const long m0 = blockIdx.y * rows_per_chunk;
-  const int r0 = blockIdx.z * R;  // rank columns handled by this block
-  Y += r0;
-  out += r0 * osr;
-  const long m1 = min(M, m0 + rows_per_chunk);
-  float acc[8][R];
+// ------------------------------------------------------------------------------------ wgrad
+// block = 4 waves, columns [64*blockIdx.x, +64) (16 per wave), rows [chunk*blockIdx.y, +chunk),
+// ranks [16*blockIdx.z, +16).  LDS tiles of 64 rows: Xs[64][64], Ys[64][16].
+__global__ __launch_bounds__(256) void lora_wgrad_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Y,
+                                                         long ldy, float* __restrict__ out, long osk, long osr, long M, int K,
+                                                         int R, long chunk, float scale) {
+  constexpr int MT = 64;
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[MT * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t Ys[MT * 16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k0 = blockIdx.x * 64;
+  const int r0 = blockIdx.z * 16;
+  const long mbeg = (long)blockIdx.y * chunk;
+  const long mend = min(M, mbeg + chunk);
+  f32x4_t acc = zero4();
+  for (long mt = mbeg; mt < mend; mt += MT) {
+    __syncthreads();
+    // stage X[mt:mt+64][k0:k0+64]: 64 rows x 8 chunks of 16 B = 512 chunks, 2 per thread
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+    for (int c = threadIdx.x; c < MT * 8; c += 256) {
+      const int rr = c >> 3, cc = (c & 7) * 8;
+      const long m = mt + rr;
+      u16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (m < mend && k0 + cc < K) v = *reinterpret_cast<const u16x8_t*>(X + m * ldx + k0 + cc);
+      *reinterpret_cast<u16x8_t*>(Xs + rr * 64 + cc) = v;
+    }
+    // stage Y[mt:mt+64][r0:r0+16] (zero-pad ranks >= R)
+    if (threadIdx.x < MT * 2) {
+      const int rr = threadIdx.x >> 1, cc = (threadIdx.x & 1) * 8;
+      const long m = mt + rr;
+      u16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (m < mend) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[j][r] = 0.f;
-  for (long m = m0; m < m1; ++m) {
-    float xv[8], yv[R];
-    load8(X + m * ldx + k, xv);
+        for (int j = 0; j < 8; ++j)
+          if (r0 + cc + j < R) v[j] = Y[m * ldy + r0 + cc + j];
+      }
+      *reinterpret_cast<u16x8_t*>(Ys + rr * 16 + cc) = v;
+    }
+    __syncthreads();
 #pragma unroll
-    for (int r = 0; r < R; ++r) yv[r] = bf2f(Y[m * ldy + r]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[j][r] += xv[j] * yv[r];
+    for (int s = 0; s < MT / 32; ++s) {
+      // A[k][m] = X[m][k] (transposed read), B[m][r] = Y[m][r] (transposed read)
+      const bf16x8_t a = frag_tr(Xs, 64, s * 32, 16 * w);
+      const bf16x8_t b = frag_tr(Ys, 16, s * 32, 0);
+      acc = mfma16(a, b, acc);
+    }
   }
+  // C[k][r]: row k = 4*(lane>>4)+i (within the wave's 16 columns), col r = lane&15
+  const int r = r0 + (lane & 15);
+  if (r < R) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int r = 0; r < R; ++r) atomicAdd(out + (k + j) * osk + r * osr, acc[j][r] * scale);
+    for (int i = 0; i < 4; ++i) {
+      const int k = k0 + 16 * w + 4 * (lane >> 4) + i;
+      if (k < K) atomicAdd(out + (long)k * osk + (long)r * osr, acc[i] * scale);
+    }
+  }
 }
 
 template <typename T>
@@ -114,7 +159,7 @@ __global__ void lora_merge_kernel(T* W, long wsk, long wsn, const float* __restr
   if (t >= (long)K * N) return;
   const int k = t / N, n = t % N;
   float acc = 0.f;
-  for (int r = 0; r < R; ++r) acc += A[(long)k * R + r] * B[(long)r * N + n];
+  for (int r = 0; r < R; ++r) acc += A[(long)r * K + k] * B[(long)r * N + n];
   T* p = W + k * wsk + n * wsn;
   if constexpr (sizeof(T) == 2) {
     *p = f2bf(bf2f(*p) + s * acc);
@@ -123,42 +168,50 @@ __global__ void lora_merge_kernel(T* W, long wsk, long wsn, const float* __restr
   }
 }
 
-#define MFT_RANK_DISPATCH(R, ...)                                                  \
-  switch (R) {                                                                     \
-    case 1: { constexpr int RR = 1; __VA_ARGS__; } break;                          \
-    case 2: { constexpr int RR = 2; __VA_ARGS__; } break;                          \
-    case 4: { constexpr int RR = 4; __VA_ARGS__; } break;                          \
-    case 8: { constexpr int RR = 8; __VA_ARGS__; } break;                          \
-    case 16: { constexpr int RR = 16; __VA_ARGS__; } break;                        \
-    case 32: { constexpr int RR = 32; __VA_ARGS__; } break;                        \
-    case 64: { constexpr int RR = 64; __VA_ARGS__; } break;                        \
-    default: fprintf(stderr, "lora: unsupported rank %d (use 1,2,4,8,16,32,64)\n", R); abort(); \
-  }
-
-void lora_rowdot(const bf16_t* X, long ldx, const bf16_t* W, long wsk, long wsr, bf16_t* U, long ldu, long M, int K,
-                 int R, float s, hipStream_t st) {
-  MFT_RANK_DISPATCH(R, lora_rowdot_kernel<RR><<<cdiv(M, 4), 256, 0, st>>>(X, ldx, W, wsk, wsr, U, ldu, M, K, s));
+void lora_rowdot(const bf16_t* X, long ldx, const bf16_t* Wt, long ldw, bf16_t* U, long ldu, long M, int K, int R, float s,
+                 hipStream_t st) {
+  const int grid = cdiv(M, 16);
+  if (R <= 16) lora_rowdot_kernel<1><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s);
+  else if (R <= 32) lora_rowdot_kernel<2><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s);
+  else lora_rowdot_kernel<4><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s);
 }
 
-void lora_update(const bf16_t* base, long ldb, const float* bias, const bf16_t* U, long ldu, const bf16_t* W, long wsr,
-                 long wsn, bf16_t* Y, long ldy, long M, int N, int R, float s, hipStream_t st) {
-  long g = (M * (N / 8) + 255) / 256;
-  const int grid = (int)(g < 8192 ? (g > 0 ? g : 1) : 8192);
-  MFT_RANK_DISPATCH(R, lora_update_kernel<RR><<<grid, 256, 0, st>>>(base, ldb, bias, U, ldu, W, wsr, wsn, Y, ldy, M, N, s));
+void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const bf16_t* W, long ldw, bf16_t* Y, long ldy,
+                 long M, int N, int R, float s, hipStream_t st) {
+  const int nthreads_x = (N / 8 + 63) / 64 * 64;
+  const int bx = nthreads_x < 256 ? nthreads_x : 256;
+  const int gx = cdiv(N / 8, bx);
+  // ~2k blocks in total, at least 16 rows per block to amortise the W register load
+  long rows = (M * gx + 2047) / 2048;
+  if (rows < 16) rows = 16;
+  dim3 grid(gx, (unsigned)cdiv(M, rows));
+  switch (R) {
+#define MFT_UPD(RV) case RV: lora_update_kernel<RV><<<grid, bx, 0, st>>>(base, ldb, U, ldu, W, ldw, Y, ldy, M, N, (int)rows, s); break;
+    MFT_UPD(1) MFT_UPD(2) MFT_UPD(4) MFT_UPD(8) MFT_UPD(16)
+#undef MFT_UPD
+    default: {
+      // larger ranks: apply in slices of 16 (in place after the first)
+      for (int r0 = 0; r0 < R; r0 += 16) {
+        const int rr = R - r0 < 16 ? R - r0 : 16;
+        if (rr != 16) { fprintf(stderr, "lora_update: rank %d must be a multiple of 16 above 16\n", R); abort(); }
+        lora_update_kernel<16><<<grid, bx, 0, st>>>(r0 == 0 ? base : Y, r0 == 0 ? ldb : ldy, U + r0, ldu,
+                                                     W + (long)r0 * ldw, ldw, Y, ldy, M, N, (int)rows, s);
+      }
+    }
+  }
 }
 
 void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out, long osk, long osr, long M, int K, int R,
                 float scale, hipStream_t st) {
-  const int gx = cdiv(K / 8, 64);
-  // enough M-chunks for ~1k blocks, but at least 64 rows per chunk to amortise the atomics
-  long chunks = 1024 / gx;
+  const int gx = cdiv(K, 64);
+  const int gz = cdiv(R, 16);
+  long chunks = 1024 / (gx * gz);
   if (chunks < 1) chunks = 1;
-  long rows = (M + chunks - 1) / chunks;
-  if (rows < 64) rows = 64;
-  chunks = (M + rows - 1) / rows;
-  const int rb = R < 8 ? R : 8;  // <= 64 fp32 accumulators per thread
-  dim3 grid(gx, (unsigned)chunks, R / rb);
-  MFT_RANK_DISPATCH(rb, lora_wgrad_kernel<RR><<<grid, 64, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, rows, scale));
+  long chunk = (M + chunks - 1) / chunks;
+  chunk = (chunk + 63) / 64 * 64;
+  if (chunk < 256) chunk = 256;
+  dim3 grid(gx, (unsigned)cdiv(M, chunk), gz);
+  lora_wgrad_kernel<<<grid, 256, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale);
 }
 
 void lora_merge(void* W, int w_is_bf16, long wsk, long wsn, const float* A, const float* B, int K, int N, int R, float s,

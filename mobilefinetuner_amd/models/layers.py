@@ -18,7 +18,8 @@ from ..ops import functional as Fx
 @dataclass
 class LoRASlice:
     """One LoRA adapter on columns [col0, col0 + ncols) of a (possibly fused) linear output.
-    A: [in, r], B: [r, ncols] (the reference checkpoint layout, graph/lora_saver.cpp:123-126)."""
+    A: [r, in] (PEFT lora_A.weight layout), B: [r, ncols] (reference lora_B layout).  The reference
+    checkpoint stores A as [in, r] (graph/lora_saver.cpp:123-126); io/lora_checkpoint.py transposes."""
     col0: int
     ncols: int
     A: nn.Parameter
@@ -61,10 +62,10 @@ class Linear(nn.Module):
 
     @torch.no_grad()
     def merge_lora(self, sign: float = 1.0):
-        """W[col0:col0+n, :] += sign * s * (A B)^T  (merge; sign=-1 unmerges) — K10."""
+        """W[col0:col0+n, :] += sign * s * B^T A  (merge; sign=-1 unmerges) — K10."""
         for sl in self.lora_slices:
-            A, B = sl.A.detach().float(), sl.B.detach().float()
-            delta = (A @ B).t() * (sign * self.lora_scale)  # [n, in]
+            A, B = sl.A.detach().float(), sl.B.detach().float()   # [r, in], [r, n]
+            delta = (B.t() @ A) * (sign * self.lora_scale)          # [n, in]
             w = self.weight.data
             w[sl.col0:sl.col0 + sl.ncols] = (w[sl.col0:sl.col0 + sl.ncols].float() + delta).to(w.dtype)
             if getattr(self.weight, "shadow", None) is not None:

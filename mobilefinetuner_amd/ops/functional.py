@@ -388,12 +388,12 @@ def linear(x, w, b=None):
 
 
 class _LoRALinear(Function):
-    """y = x W^T + b + sum_i s * (x A_i) B_i placed in column slices [c0_i, c0_i + n_i) of y.
+    """y = x W^T + b + sum_i s * (x A_i^T) B_i placed in column slices [c0_i, c0_i + n_i) of y.
 
-    W (and b) frozen; A_i [in, r], B_i [r, n_i] fp32 masters with bf16 shadows (``p.shadow``).
-    One hipBLASLt base GEMM for the whole (possibly fused, e.g. q|k|v) weight, then the rank-r
-    work per slice in lora.hip (reference: LoRALinear slices {A,B,scale,col0,cols},
-    nn/lora_linear.h:17-97)."""
+    W (and b) frozen; A_i [r, in] (PEFT lora_A layout), B_i [r, n_i] fp32 masters with bf16
+    shadows (``p.shadow``).  One hipBLASLt base GEMM for the whole (possibly fused, e.g. q|k|v)
+    weight, then the rank-r work per slice in lora.hip (reference: LoRALinear slices
+    {A,B,scale,col0,cols}, nn/lora_linear.h:17-97)."""
 
     @staticmethod
     def forward(ctx, x, w, b, s, slices, *ab):
@@ -408,11 +408,11 @@ class _LoRALinear(Function):
         us = []
         for i, (c0, n) in enumerate(slices):
             Ac, Bc = cw(ab[2 * i]), cw(ab[2 * i + 1])
-            R = Ac.shape[1]
+            R = Ac.shape[0]
             u = torch.empty(x2.shape[0], R, device=x.device, dtype=x.dtype)
-            C.lora_rowdot(x2, Ac, R, 1, u, 1.0)                      # u = x A
+            C.lora_rowdot(x2, Ac, u, 1.0)                     # u = x A^T
             ys = y[:, c0:c0 + n]
-            C.lora_update(ys, None, u, Bc, n, 1, ys, float(s))       # y[:, slice] += s u B
+            C.lora_update(ys, u, Bc, ys, float(s))            # y[:, slice] += s u B
             us.append(u)
         ctx.save_for_backward(x2, *us)
         ctx.params = ab
@@ -435,17 +435,17 @@ class _LoRALinear(Function):
         for i, (c0, n) in enumerate(ctx.slices):
             A, B = ab[2 * i], ab[2 * i + 1]
             Ac, Bc = cw(A), cw(B)
-            R = Ac.shape[1]
+            R = Ac.shape[0]
             dys = dy2[:, c0:c0 + n]
             v = torch.empty(dy2.shape[0], R, device=dy.device, dtype=dy.dtype)
-            C.lora_rowdot(dys, Bc, 1, n, v, s)                       # v = s dy B^T
+            C.lora_rowdot(dys, Bc, v, s)                      # v = s dy B^T
             if dx is not None:
-                C.lora_update(dx, None, v, Ac, 1, R, dx, 1.0)        # dx += v A^T
+                C.lora_update(dx, v, Ac, dx, 1.0)             # dx += v A
             gA = gB = None
             if _needs(A):
                 buf = _grad_buf(A)
-                tgt = buf if buf is not None else torch.zeros(K, R, device=dy.device)
-                C.lora_wgrad(x2, v, tgt, R, 1, 1.0)                  # dA += x^T v
+                tgt = buf if buf is not None else torch.zeros(R, K, device=dy.device)
+                C.lora_wgrad(x2, v, tgt, 1, K, 1.0)           # dA[r, k] += sum_m v[m, r] x[m, k]
                 if buf is not None:
                     grad_ready(A)
                 else:
@@ -453,7 +453,7 @@ class _LoRALinear(Function):
             if _needs(B):
                 buf = _grad_buf(B)
                 tgt = buf if buf is not None else torch.zeros(R, n, device=dy.device)
-                C.lora_wgrad(dys, us[i], tgt, 1, n, s)               # dB += s u^T dy
+                C.lora_wgrad(dys, us[i], tgt, 1, n, s)        # dB[r, n] += s sum_m u[m, r] dy[m, n]
                 if buf is not None:
                     grad_ready(B)
                 else:
@@ -473,7 +473,7 @@ def lora_linear(x, w, b, slices, scale):
             y = y + cw(b).float()
         parts = []
         for (c0, n, A, B) in slices:
-            parts.append((c0, n, scale * ((xf @ cw(A).float()) @ cw(B).float())))
+            parts.append((c0, n, scale * ((xf @ cw(A).float().t()) @ cw(B).float())))
         if parts:
             y = y.clone()
             for c0, n, d in parts:
@@ -488,9 +488,17 @@ def lora_linear(x, w, b, slices, scale):
 
 # ---------------------------------------------------------------- fused LM head + cross entropy
 def default_ce_chunk(vpad: int) -> int:
-    """Rows per chunk so one chunk of bf16 logits (~96 MiB) stays in the 256 MiB Infinity Cache."""
-    rows = (96 << 20) // (2 * vpad)
-    return max(64, min(4096, rows // 64 * 64))
+    """Rows of bf16 logits materialised at once (the rest of the vocab-chunked CE never exists).
+
+    Measured on MI355X (profiles/): hipBLASLt's LM-head GEMM is far more efficient at M = 8192
+    than at 1024 (the L3-resident 96 MiB chunk lost 20% end-to-end), so we cap by a 2 GiB logits
+    budget instead — 8192 rows for GPT-2 (50304 cols), 4096 for Gemma-3 (262144 cols)."""
+    import os
+    env = os.environ.get("MFT_CE_CHUNK")
+    if env:
+        return int(env)
+    rows = (2 << 30) // (2 * vpad)
+    return max(64, min(8192, rows // 64 * 64))
 
 
 class _LMHeadCE(Function):

@@ -83,14 +83,16 @@ class LoraSpec:
 
 
 def _gpt2_init_A(in_f, out_f, r, seed_base):
+    """Reference init (graph/lora_injector.cpp:70-85): A[in, r] ~ U(+-sqrt(6/(in+r))); returned as [r, in]."""
     g = torch.Generator().manual_seed(seed_base + in_f + out_f)
     bound = math.sqrt(6.0 / (in_f + r))
-    return (torch.rand(in_f, r, generator=g) * 2 - 1) * bound
+    return ((torch.rand(in_f, r, generator=g) * 2 - 1) * bound).t().contiguous()
 
 
 def _peft_init_A(in_f, r, g):
+    """PEFT kaiming_uniform(a=sqrt(5)) on lora_A.weight [r, in] == U(+-1/sqrt(in))."""
     bound = 1.0 / math.sqrt(in_f)
-    return (torch.rand(in_f, r, generator=g) * 2 - 1) * bound
+    return (torch.rand(r, in_f, generator=g) * 2 - 1) * bound
 
 
 def inject_gpt2(model, spec: LoraSpec):

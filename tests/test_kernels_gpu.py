@@ -185,16 +185,17 @@ def test_lm_head_ce(V, C):
     _close(h.grad, hr.grad, 2e-3, 0.03, msg="ce dh")
 
 
-def test_lora_linear():
+@pytest.mark.parametrize("R", [8, 16, 32])
+def test_lora_linear(R):
     from mobilefinetuner_amd.ops import functional as Fx
-    M, K, N, R = 250, 768, 2304, 8
+    M, K, N = 250, 768, 2304
     x = (torch.randn(M, K, device=DEV) * 0.5).bfloat16().requires_grad_()
     W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
     b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
     slices = []
     refs = []
     for (c0, n) in [(0, 768), (768, 768), (1536, 768)]:
-        A = torch.nn.Parameter(torch.randn(K, R, device=DEV) * 0.05)
+        A = torch.nn.Parameter(torch.randn(R, K, device=DEV) * 0.05)
         B = torch.nn.Parameter(torch.randn(R, n, device=DEV) * 0.05)
         A.shadow = A.detach().bfloat16()
         B.shadow = B.detach().bfloat16()
@@ -209,7 +210,7 @@ def test_lora_linear():
         Ar = A.shadow.float().requires_grad_()
         Br = B.shadow.float().requires_grad_()
         refs.append((Ar, Br))
-        parts.append(2.0 * (xr @ Ar) @ Br)
+        parts.append(2.0 * (xr @ Ar.t()) @ Br)
     yr = yr + torch.cat(parts, dim=1)
     (yr * g.float()).sum().backward()
     _close(y, yr, 0.05, 0.01, msg="lora y")
