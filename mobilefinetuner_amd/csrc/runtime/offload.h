@@ -1,0 +1,84 @@
+// Host-DRAM (pinned) / disk offload tier with LRU residency and async copies on a side stream.
+//
+// Replaces ParameterSharder's disk LRU (opt_ops/sharding/parameter_sharder.h:36-93,
+// .cpp:86-276): register -> (optionally quantised) copy off the device, require() -> refill,
+// mark_dirty -> write back on eviction, byte budget with LRU victims, throw if a single entry
+// exceeds the budget.  MI355X design: the backing store is pinned host memory (hipHostMalloc,
+// ~50+ GB/s over PCIe Gen5 per direction vs SSD), copies are hipMemcpyAsync on a dedicated copy
+// stream ordered against the compute stream with hipEvents (so a prefetch of layer i+1 overlaps
+// compute of layer i), and an optional disk tier (the reference's --shard_dir) spills host
+// buffers to files when host memory is also budgeted.  Device buffers stay owned by PyTorch's
+// caching allocator; this engine moves bytes and tracks residency.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <list>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace mft {
+
+class HostTier {
+ public:
+  HostTier(size_t device_budget_bytes, const std::string& disk_dir, size_t host_budget_bytes);
+  ~HostTier();
+  HostTier(const HostTier&) = delete;
+  HostTier& operator=(const HostTier&) = delete;
+
+  void add(const std::string& name, size_t nbytes);
+  bool has(const std::string& name) const { return entries_.count(name) != 0; }
+  // device -> host (async on the copy stream, ordered after `compute` work so far)
+  void offload(const std::string& name, const void* dev, hipStream_t compute);
+  // host -> device (async on the copy stream); `compute` waits for it (hipStreamWaitEvent)
+  void fetch(const std::string& name, void* dev, hipStream_t compute);
+  // block the host until the last copy of `name` completed
+  void synchronize(const std::string& name);
+  void synchronize_all();
+  // residency bookkeeping (LRU over entries currently resident on the device)
+  void mark_resident(const std::string& name, bool resident);
+  void touch(const std::string& name);
+  void mark_dirty(const std::string& name);
+  bool dirty(const std::string& name) const;
+  bool resident(const std::string& name) const;
+  // names to evict (LRU first) so that `need` more bytes fit in the device budget; `keep` excluded
+  std::vector<std::string> victims(size_t need, const std::string& keep) const;
+  size_t resident_bytes() const { return resident_bytes_; }
+  size_t device_budget() const { return budget_; }
+  void set_device_budget(size_t b) { budget_ = b; }
+  size_t bytes(const std::string& name) const;
+  // raw host pointer (pinned) for host-side inspection / quantised views
+  void* host_ptr(const std::string& name);
+  // disk tier
+  void spill(const std::string& name);
+  void unspill(const std::string& name);
+  bool on_disk(const std::string& name) const;
+  size_t host_bytes() const { return host_bytes_; }
+  uint64_t h2d_bytes() const { return h2d_bytes_; }
+  uint64_t d2h_bytes() const { return d2h_bytes_; }
+
+ private:
+  struct Entry {
+    std::string name;
+    size_t bytes = 0;
+    void* host = nullptr;
+    bool resident = false, dirty = false, on_disk = false;
+    uint64_t last_used = 0;
+    hipEvent_t ev = nullptr;
+    bool ev_pending = false;
+  };
+  Entry& get(const std::string& name);
+  const Entry& get(const std::string& name) const;
+  std::unordered_map<std::string, Entry> entries_;
+  size_t budget_, host_budget_;
+  size_t resident_bytes_ = 0, host_bytes_ = 0;
+  uint64_t clock_ = 0, h2d_bytes_ = 0, d2h_bytes_ = 0;
+  std::string disk_dir_;
+  hipStream_t copy_ = nullptr;
+  hipEvent_t order_ev_ = nullptr;
+  mutable std::mutex mu_;
+};
+
+}  // namespace mft
