@@ -24,6 +24,7 @@ import torch.nn as nn
 
 from ..ops import functional as Fx
 from ..ops import reference as ref
+from ..parallel.sharder import gate
 from .layers import Linear, RMSNorm
 
 
@@ -214,17 +215,26 @@ class Gemma3Model(nn.Module):
         dev = input_ids.device
         gcos, gsin = self.rope("global", S, dev)
         lcos, lsin = self.rope("local", S, dev)
+        sh = getattr(self, "sharder", None)
+        if sh is not None:
+            sh.require("embed")
         x = Fx.embedding(input_ids, self.embed, None, self.embed_scale)
         h = self.layers[0].input_layernorm(x)
         n = len(self.layers)
         for i, L in enumerate(self.layers):
             nxt = self.layers[i + 1].input_layernorm if i + 1 < n else self.norm
             cos, sin = (lcos, lsin) if L.sliding else (gcos, gsin)
+            if sh is not None:
+                sh.require(f"block{i}")
             if self.activation_checkpointing and self.training and torch.is_grad_enabled():
                 x, h = torch.utils.checkpoint.checkpoint(self._layer, L, nxt, x, h, B, S, cos, sin, kv_lens,
                                                          use_reentrant=False)
             else:
                 x, h = self._layer(L, nxt, x, h, B, S, cos, sin, kv_lens)
+            if sh is not None:
+                x, h = gate(x, sh, f"block{i}"), gate(h, sh, f"block{i}")
+        if sh is not None:
+            sh.require("embed")
         return h
 
     @staticmethod

@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import functional as Fx
+from ..parallel.sharder import gate
 from .layers import LayerNorm, Linear
 
 
@@ -146,16 +147,25 @@ class GPT2Model(nn.Module):
     def hidden(self, input_ids, kv_lens=None):
         B, S = input_ids.shape
         assert S <= self.cfg.n_positions, f"sequence {S} exceeds n_positions {self.cfg.n_positions}"
+        sh = getattr(self, "sharder", None)
+        if sh is not None:
+            sh.require("embed")
         x = Fx.embedding(input_ids, self.wte, self.wpe)  # [B*S, C]
         h = self.blocks[0].ln_1(x)
         n = len(self.blocks)
         for i, blk in enumerate(self.blocks):
             nxt = self.blocks[i + 1].ln_1 if i + 1 < n else self.ln_f
+            if sh is not None:
+                sh.require(f"block{i}")
             if self.activation_checkpointing and self.training and torch.is_grad_enabled():
                 x, h = torch.utils.checkpoint.checkpoint(self._block, blk, nxt, x, h, B, S, kv_lens,
                                                          use_reentrant=False)
             else:
                 x, h = self._block(blk, nxt, x, h, B, S, kv_lens)
+            if sh is not None:  # backward re-fetches this block's weights before its dgrad
+                x, h = gate(x, sh, f"block{i}"), gate(h, sh, f"block{i}")
+        if sh is not None:
+            sh.require("embed")  # tied LM head
         return h  # = ln_f(x) [B*S, C]
 
     @staticmethod

@@ -80,6 +80,8 @@ class LayerNorm(nn.Module):
         super().__init__()
         self.weight = nn.Parameter(torch.ones(n, device=device), requires_grad=False)
         self.bias = nn.Parameter(torch.zeros(n, device=device), requires_grad=False)
+        self.weight._mft_fp32_compute = True
+        self.bias._mft_fp32_compute = True
         self.eps = eps
 
     def forward(self, x):
@@ -95,6 +97,7 @@ class RMSNorm(nn.Module):
     def __init__(self, n, eps=1e-6, offset=1.0, device=None):
         super().__init__()
         self.weight = nn.Parameter(torch.zeros(n, device=device), requires_grad=False)
+        self.weight._mft_fp32_compute = True
         self.eps, self.offset = eps, offset
 
     def forward(self, x):

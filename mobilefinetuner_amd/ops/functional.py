@@ -47,6 +47,14 @@ def cw(p):
     return getattr(p, "shadow", None) if getattr(p, "shadow", None) is not None else p
 
 
+def rw(p):
+    """Weight view for the CPU reference path: the autograd-tracked parameter itself when trainable
+    (so AccumulateGrad fills p.grad), else its compute view."""
+    if p is None:
+        return None
+    return p if p.requires_grad else cw(p)
+
+
 def _needs(p):
     return p is not None and p.requires_grad
 
@@ -131,7 +139,7 @@ class _Norm(Function):
 
 def layer_norm(x, w, b, eps=1e-5):
     if not x.is_cuda:
-        return ref.layer_norm(x, cw(w), cw(b), eps).to(x.dtype)
+        return ref.layer_norm(x, rw(w), rw(b), eps).to(x.dtype)
     return _Norm.apply(x, None, w, b, eps, False, 0.0)
 
 
@@ -139,20 +147,20 @@ def add_layer_norm(x, delta, w, b, eps=1e-5):
     """s = x + delta; y = LayerNorm(s)  -> (s, y) (fused residual + norm)."""
     if not x.is_cuda:
         s = x + delta
-        return s, ref.layer_norm(s, cw(w), cw(b), eps).to(x.dtype)
+        return s, ref.layer_norm(s, rw(w), rw(b), eps).to(x.dtype)
     return _Norm.apply(x, delta, w, b, eps, False, 0.0)
 
 
 def rms_norm(x, w, eps=1e-6, offset=1.0):
     if not x.is_cuda:
-        return ref.rms_norm(x, cw(w), eps, offset).to(x.dtype)
+        return ref.rms_norm(x, rw(w), eps, offset).to(x.dtype)
     return _Norm.apply(x, None, w, None, eps, True, offset)
 
 
 def add_rms_norm(x, delta, w, eps=1e-6, offset=1.0):
     if not x.is_cuda:
         s = x + delta
-        return s, ref.rms_norm(s, cw(w), eps, offset).to(x.dtype)
+        return s, ref.rms_norm(s, rw(w), eps, offset).to(x.dtype)
     return _Norm.apply(x, delta, w, None, eps, True, offset)
 
 
@@ -235,12 +243,12 @@ def embedding(ids, wte, wpe=None, scale=1.0):
     """ids [B,S] -> [B*S, C]: wte[ids]*scale (+ wpe[pos])."""
     B, S = ids.shape
     if not ids.is_cuda:
-        e = cw(wte)[ids.reshape(-1)].float()
+        e = rw(wte)[ids.reshape(-1)].float()
         if scale != 1.0:
             e = e * scale
         if wpe is not None:
-            e = e + cw(wpe)[:S].float().repeat(B, 1)
-        return e.to(cw(wte).dtype)
+            e = e + rw(wpe)[:S].float().repeat(B, 1)
+        return e.to(rw(wte).dtype)
     return _Embedding.apply(ids, wte, wpe, S, float(scale))
 
 
@@ -331,7 +339,7 @@ class _QKNormRoPE(Function):
 def qk_norm_rope(x, w, cos, sin, eps=1e-6, offset=1.0, interleaved=False):
     """x [B,S,H,D] strided view -> rope(rmsnorm(x) * (w + offset)) contiguous [B,S,H,D]."""
     if not x.is_cuda:
-        y = ref.rms_norm(x, cw(w), eps, offset).to(x.dtype)
+        y = ref.rms_norm(x, rw(w), eps, offset).to(x.dtype)
         return ref.rope(y, cos, sin, 0, interleaved).to(x.dtype)
     return _QKNormRoPE.apply(x, w, cos, sin, float(eps), float(offset), bool(interleaved))
 
@@ -380,9 +388,9 @@ class _Linear(Function):
 def linear(x, w, b=None):
     """y = x W^T + b with W [out, in] (nn.Linear layout)."""
     if not x.is_cuda:
-        y = x.float() @ cw(w).float().t()
+        y = x.float() @ rw(w).float().t()
         if b is not None:
-            y = y + cw(b).float()
+            y = y + rw(b).float()
         return y.to(x.dtype)
     return _Linear.apply(x, w, b)
 
@@ -468,12 +476,12 @@ def lora_linear(x, w, b, slices, scale):
     """slices: list of (col0, ncols, A, B).  See _LoRALinear."""
     if not x.is_cuda:
         xf = x.float()
-        y = xf @ cw(w).float().t()
+        y = xf @ rw(w).float().t()
         if b is not None:
-            y = y + cw(b).float()
+            y = y + rw(b).float()
         parts = []
         for (c0, n, A, B) in slices:
-            parts.append((c0, n, scale * ((xf @ cw(A).float().t()) @ cw(B).float())))
+            parts.append((c0, n, scale * ((xf @ rw(A).float().t()) @ rw(B).float())))
         if parts:
             y = y.clone()
             for c0, n, d in parts:
@@ -548,7 +556,7 @@ def lm_head_cross_entropy(h, w, labels, vocab_size, chunk=None, w_grad_scale=1.0
     NOTE: the W gradient is produced during forward and scaled by ``w_grad_scale`` (pass the
     same factor the loss is later multiplied by, e.g. 1/grad_accum); dh honours grad_output."""
     if not h.is_cuda:
-        logits = h.float() @ cw(w).float().t()
+        logits = h.float() @ rw(w).float().t()
         logits = logits[:, :vocab_size]
         return torch.nn.functional.cross_entropy(logits, labels.reshape(-1), ignore_index=-100)
     if chunk is None:
@@ -560,7 +568,7 @@ def lm_head_token_nll(h, w, labels, vocab_size, chunk=None):
     """Per-row NLL (no grad) for evaluation: returns (sum_nll, n_valid) device scalars."""
     with torch.no_grad():
         if not h.is_cuda:
-            logits = (h.float() @ cw(w).float().t())[:, :vocab_size]
+            logits = (h.float() @ rw(w).float().t())[:, :vocab_size]
             nll = torch.nn.functional.cross_entropy(logits, labels.reshape(-1), ignore_index=-100, reduction="sum")
             return nll, (labels >= 0).sum()
         C = native()

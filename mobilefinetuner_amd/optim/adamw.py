@@ -43,16 +43,11 @@ class FusedAdamW:
         self.nonfinite_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.lr = float(lr)
         self.step_count = 0
-        self._lr_host = torch.zeros(1, dtype=torch.float32).pin_memory() if dev.type == "cuda" else None
 
     # ---- host-side control (outside any captured graph)
     def set_lr(self, lr: float):
         self.lr = float(lr)
-        if self._lr_host is not None:
-            self._lr_host[0] = self.lr
-            self.lr_dev.copy_(self._lr_host, non_blocking=True)
-        else:
-            self.lr_dev.fill_(self.lr)
+        self.lr_dev.fill_(self.lr)  # value travels as a kernel argument: no host-buffer race
 
     def grad_norm(self) -> float:
         """Global grad L2 norm of the last step (host sync)."""

@@ -100,8 +100,10 @@ class TrainStep:
             if sid.data_ptr() != ids.data_ptr():
                 sid.copy_(ids, non_blocking=True)
                 slab.copy_(lab, non_blocking=True)
+        if self.dp is not None:
+            self.dp.begin_step()
         self.graph.replay()
         if not self.graph_comm:
-            self._reduce_flat()
+            self._reduce()
             self._opt()
         return self.loss_dev

@@ -35,14 +35,16 @@ class ParamSlot:
 
 
 class FlatParams:
-    def __init__(self, named_params, device, shadow: bool = True, shadow_dtype=torch.bfloat16):
+    def __init__(self, named_params, device, shadow: bool = True, shadow_dtype=torch.bfloat16,
+                 pad_multiple: int = 1):
         named_params = [(n, p) for n, p in named_params if p.requires_grad]
         self.slots: list[ParamSlot] = []
         off = 0
         for n, p in named_params:
             self.slots.append(ParamSlot(n, p, off, p.numel()))
             off += _round(p.numel())
-        self.numel = max(off, ALIGN)
+        # pad_multiple: ZeRO needs world_size equal, ALIGN-aligned shards
+        self.numel = _round(max(off, ALIGN), ALIGN * max(1, pad_multiple))
         self.device = torch.device(device)
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
@@ -53,7 +55,8 @@ class FlatParams:
             mv.copy_(p.data.to(device=self.device, dtype=torch.float32))
             p.data = mv
             p.grad = self.grad[s.offset:s.offset + s.numel].view(p.shape)
-            if self.shadow is not None:
+            # norm weights compute in fp32 straight from the master (no bf16 rounding)
+            if self.shadow is not None and not getattr(p, "_mft_fp32_compute", False):
                 p.shadow = self.shadow[s.offset:s.offset + s.numel].view(p.shape)
         self.refresh_shadow()
 

