@@ -52,6 +52,10 @@ class ParameterSharder:
             self.tier.offload(f"{name}#{i}", t)  # host copy now (weights are frozen: never dirty)
         self.groups[name] = g
         self.order.append(name)
+        # register_parameter(keep_in_memory=false): drop the device copy until first require()
+        for i in range(len(tensors)):
+            self.tier.synchronize(f"{name}#{i}")
+        self._evict(name)
 
     def _evict(self, name):
         g = self.groups[name]
