@@ -242,7 +242,14 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor step, 
 
 // ------------------------------------------------------------------ LoRA
 // U = s * X Wt^T   (X [.., K] rows contiguous, Wt [R, K] contiguous rows)
-void lora_rowdot(Tensor X, Tensor Wt, Tensor U, double s) {
+mft::LoraDrop mkdrop(double p, int64_t salt, c10::optional<Tensor> ctr) {
+  mft::LoraDrop d{};
+  d.p = (float)p;
+  d.salt = (uint32_t)salt;
+  d.ctr = (ctr.has_value() && ctr->defined()) ? ctr->data_ptr<int64_t>() : nullptr;
+  return d;
+}
+void lora_rowdot(Tensor X, Tensor Wt, Tensor U, double s, double drop_p, int64_t salt, c10::optional<Tensor> ctr) {
   CHECK_BF16(X); CHECK_BF16(Wt); CHECK_BF16(U);
   TORCH_CHECK(X.stride(-1) == 1 && U.stride(-1) == 1 && Wt.stride(-1) == 1, "rows must be contiguous");
   const int K = X.size(-1), R = Wt.size(0);
@@ -250,10 +257,12 @@ void lora_rowdot(Tensor X, Tensor Wt, Tensor U, double s) {
   TORCH_CHECK(K % 32 == 0, "lora: in-features must be a multiple of 32");
   TORCH_CHECK(X.stride(-2) % 8 == 0 && Wt.stride(0) % 8 == 0, "lora_rowdot: row strides must be multiples of 8");
   const long M = X.numel() / K;
-  mft::lora_rowdot(bp(X), X.stride(-2), bp(Wt), Wt.stride(0), bp(U), U.stride(-2), M, K, R, (float)s, stream());
+  mft::lora_rowdot(bp(X), X.stride(-2), bp(Wt), Wt.stride(0), bp(U), U.stride(-2), M, K, R, (float)s,
+                   mkdrop(drop_p, salt, ctr), stream());
 }
 // Y = base + s * U W   (W [R, N]); Y may alias base
-void lora_update(Tensor base, Tensor U, Tensor W, Tensor Y, double s) {
+void lora_update(Tensor base, Tensor U, Tensor W, Tensor Y, double s, double drop_p, int64_t salt,
+                 c10::optional<Tensor> ctr) {
   CHECK_BF16(base); CHECK_BF16(Y); CHECK_BF16(U); CHECK_BF16(W);
   const int N = Y.size(-1), R = U.size(-1);
   TORCH_CHECK(W.size(0) == R && W.size(1) == N && W.stride(1) == 1, "lora_update: W must be [R, N]");
@@ -261,15 +270,17 @@ void lora_update(Tensor base, Tensor U, Tensor W, Tensor Y, double s) {
               "lora_update: widths/strides must be multiples of 8");
   const long M = Y.numel() / N;
   mft::lora_update(bp(base), base.stride(-2), bp(U), U.stride(-2), bp(W), W.stride(0), bp(Y), Y.stride(-2), M, N, R,
-                   (float)s, stream());
+                   (float)s, mkdrop(drop_p, salt, ctr), stream());
 }
-void lora_wgrad(Tensor X, Tensor Y, Tensor out, int64_t osk, int64_t osr, double scale) {
+void lora_wgrad(Tensor X, Tensor Y, Tensor out, int64_t osk, int64_t osr, double scale, double drop_p, int64_t salt,
+                c10::optional<Tensor> ctr) {
   CHECK_BF16(X); CHECK_BF16(Y); CHECK_F32(out);
   TORCH_CHECK(X.stride(-1) == 1 && X.stride(-2) % 8 == 0, "lora_wgrad: X rows must be contiguous, stride % 8 == 0");
   const int K = X.size(-1), R = Y.size(-1);
   TORCH_CHECK(K % 8 == 0, "lora_wgrad: K must be a multiple of 8");
   const long M = X.numel() / K;
-  mft::lora_wgrad(bp(X), X.stride(-2), bp(Y), Y.stride(-2), fp(out), osk, osr, M, K, R, (float)scale, stream());
+  mft::lora_wgrad(bp(X), X.stride(-2), bp(Y), Y.stride(-2), fp(out), osk, osr, M, K, R, (float)scale,
+                  mkdrop(drop_p, salt, ctr), stream());
 }
 void lora_merge(Tensor W, int64_t wsk, int64_t wsn, Tensor A, Tensor B, double s) {
   CHECK_F32(A); CHECK_F32(B); CHECK_CONTIG(A); CHECK_CONTIG(B);

@@ -100,15 +100,21 @@ void nonfinite_check(const float* x, long n, int* flag, hipStream_t st);
 
 // ---------------------------------------------------------------- LoRA (lora.hip)
 // Layouts: A [R, K] (PEFT lora_A.weight), B [R, N].
+// LoRA-input dropout: mask(m, k) = hash(*ctr, salt, m*K + k) >= p, kept values scaled 1/(1-p).
+struct LoraDrop {
+  const int64_t* ctr;  // device step counter (may be null)
+  uint32_t salt;       // per-adapter constant
+  float p;             // 0 disables
+};
 // U[m, r] = s * sum_k X[m, k] * Wt[r, k]          (u = x A^T with Wt = A; v = s dy B^T with Wt = B)
 void lora_rowdot(const bf16_t* X, long ldx, const bf16_t* Wt, long ldw, bf16_t* U, long ldu, long M, int K, int R, float s,
-                 hipStream_t st);
+                 LoraDrop drop, hipStream_t st);
 // Y[m, n] = base[m, n] + s * sum_r U[m, r] * W[r, n]   (Y may alias base; y += s u B, dx += v A)
 void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const bf16_t* W, long ldw, bf16_t* Y, long ldy,
-                 long M, int N, int R, float s, hipStream_t st);
+                 long M, int N, int R, float s, LoraDrop drop, hipStream_t st);
 // out[k*osk + r*osr] += scale * sum_m X[m, k] * Y[m, r]   (fp32 atomics into the grad buffer)
 void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out, long osk, long osr, long M, int K, int R,
-                float scale, hipStream_t st);
+                float scale, LoraDrop drop, hipStream_t st);
 // W[k*wsk + n*wsn] += s * sum_r A[r, k] * B[r, n]   (A [R,K], B [R,N] fp32)
 void lora_merge(void* W, int w_is_bf16, long wsk, long wsn, const float* A, const float* B, int K, int N, int R, float s,
                 hipStream_t st);

@@ -21,15 +21,44 @@
 
 namespace mft {
 
+// ------------------------------------------------------------------------------------ dropout
+// PEFT applies dropout to the LoRA input: u = dropout(x) A^T (the reference stored lora_dropout but
+// never applied it).  The mask is a counter-based hash of (step counter, layer salt,
+// element index): recomputed wherever it is needed (u in forward, dA and the dx term in backward), so
+// no mask tensor is ever written.  The step counter lives on the device (graph-replay safe).
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x7feb352dU;
+  h ^= h >> 15;
+  h *= 0x846ca68bU;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ float drop_mult(const LoraDrop& d, uint32_t seed, long m, int k, int K) {
+  const uint64_t idx = (uint64_t)m * (uint64_t)K + (uint64_t)k;
+  const uint32_t h = mix32((uint32_t)idx ^ mix32((uint32_t)(idx >> 32) ^ seed));
+  return ((h >> 8) * (1.0f / 16777216.0f)) >= d.p ? 1.0f / (1.0f - d.p) : 0.0f;
+}
+__device__ __forceinline__ uint32_t drop_seed(const LoraDrop& d) {
+  return mix32(d.salt * 0x9E3779B9U ^ (uint32_t)(d.ctr ? *d.ctr : 0) * 0x85EBCA6BU);
+}
+__device__ __forceinline__ bf16x8_t apply_drop8(bf16x8_t a, const LoraDrop& d, uint32_t seed, long m, int k, int K) {
+  u16x8_t v = __builtin_bit_cast(u16x8_t, a);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(v[j]) * drop_mult(d, seed, m, k + j, K));
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
 // ------------------------------------------------------------------------------------ rowdot
 // block = 4 waves; rows [16*blockIdx.x, +16); wave w handles k in [w*Kq, (w+1)*Kq).
 // Each 16-col output tile covers ranks [16*t, 16*t+16) of R (RT tiles).
 template <int RT>
 __global__ __launch_bounds__(256) void lora_rowdot_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Wt,
                                                           long ldw, bf16_t* __restrict__ U, long ldu, long M, int K, int R,
-                                                          float s) {
+                                                          float s, LoraDrop drop) {
   __shared__ __attribute__((aligned(16))) float red[4][RT][64][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t dseed = drop.p > 0.f ? drop_seed(drop) : 0u;
   const long m0 = (long)blockIdx.x * 16;
   const long mr = m0 + (lane & 15);
   const bool row_ok = mr < M;
@@ -42,6 +71,7 @@ __global__ __launch_bounds__(256) void lora_rowdot_kernel(const bf16_t* __restri
   for (int ks = ks0; ks < ks1; ++ks) {
     const int k = ks * 32 + 8 * (lane >> 4);
     bf16x8_t a = row_ok ? *reinterpret_cast<const bf16x8_t*>(X + mr * ldx + k) : bf16x8_t{};
+    if (drop.p > 0.f) a = apply_drop8(a, drop, dseed, mr, k, K);
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
       const int r = t * 16 + (lane & 15);
@@ -70,85 +100,99 @@ __global__ __launch_bounds__(256) void lora_rowdot_kernel(const bf16_t* __restri
 
 // ------------------------------------------------------------------------------------ update
 // grid (ceil(N/8/blockDim), ceil(M/ROWS)); thread owns 8 columns, W[0..R)[n..n+8) in registers.
+// With dropout (dx += mask * (v A) in backward) the mask of element (m, n) is re-derived.
 template <int R>
 __global__ __launch_bounds__(256) void lora_update_kernel(const bf16_t* base, long ldb, const bf16_t* __restrict__ U, long ldu,
                                                           const bf16_t* __restrict__ W, long ldw, bf16_t* Y, long ldy, long M,
-                                                          int N, int rows, float s) {
+                                                          int N, int rows, float s, LoraDrop drop) {
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
   if (n >= N) return;
+  const uint32_t dseed = drop.p > 0.f ? drop_seed(drop) : 0u;
   float wr[R][8];
 #pragma unroll
   for (int r = 0; r < R; ++r) load8(W + (long)r * ldw + n, wr[r]);
   const long m0 = (long)blockIdx.y * rows;
   const long m1 = min(M, m0 + rows);
   for (long m = m0; m < m1; ++m) {
-    float y[8], u[R];
+    float y[8], u[R], d[8];
     load8(base + m * ldb + n, y);
 #pragma unroll
     for (int r = 0; r < R; ++r) u[r] = bf2f(U[m * ldu + r]) * s;
 #pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = 0.f;
+#pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] += u[r] * wr[r][j];
+      for (int j = 0; j < 8; ++j) d[j] += u[r] * wr[r][j];
+    if (drop.p > 0.f) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] *= drop_mult(drop, dseed, m, n + j, N);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] += d[j];
     store8(Y + m * ldy + n, y);
   }
 }
 
 // ------------------------------------------------------------------------------------ wgrad
-// block = 4 waves, columns [64*blockIdx.x, +64) (16 per wave), rows [chunk*blockIdx.y, +chunk),
-// ranks [16*blockIdx.z, +16).  LDS tiles of 64 rows: Xs[64][64], Ys[64][16].
+// Streaming VALU form (the reduction runs over M, the long axis; each X row is read once).
+// block = 256 threads = 64 column-chunks of 8 x 4 row groups; each thread accumulates an 8 x RB
+// fp32 outer-product tile over its rows; the 4 row groups are summed in LDS and one fp32 atomic per
+// output element per block goes straight into the grad buffer.  RB <= 8 ranks per z-block.
+template <int RB>
 __global__ __launch_bounds__(256) void lora_wgrad_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Y,
                                                          long ldy, float* __restrict__ out, long osk, long osr, long M, int K,
-                                                         int R, long chunk, float scale) {
-  constexpr int MT = 64;
-  __shared__ __attribute__((aligned(16))) bf16_t Xs[MT * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t Ys[MT * 16];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int k0 = blockIdx.x * 64;
-  const int r0 = blockIdx.z * 16;
+                                                         int R, long chunk, float scale, LoraDrop drop) {
+  __shared__ __attribute__((aligned(16))) float red[3][64][8 * RB + 1];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int k = (blockIdx.x * 64 + c) * 8;
+  const int r0 = blockIdx.z * RB;
   const long mbeg = (long)blockIdx.y * chunk;
   const long mend = min(M, mbeg + chunk);
-  f32x4_t acc = zero4();
-  for (long mt = mbeg; mt < mend; mt += MT) {
-    __syncthreads();
-    // stage X[mt:mt+64][k0:k0+64]: 64 rows x 8 chunks of 16 B = 512 chunks, 2 per thread
+  const bool kok = k < K;
+  const uint32_t dseed = drop.p > 0.f ? drop_seed(drop) : 0u;
+  float acc[8][RB];
 #pragma unroll
-    for (int c = threadIdx.x; c < MT * 8; c += 256) {
-      const int rr = c >> 3, cc = (c & 7) * 8;
-      const long m = mt + rr;
-      u16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (m < mend && k0 + cc < K) v = *reinterpret_cast<const u16x8_t*>(X + m * ldx + k0 + cc);
-      *reinterpret_cast<u16x8_t*>(Xs + rr * 64 + cc) = v;
-    }
-    // stage Y[mt:mt+64][r0:r0+16] (zero-pad ranks >= R)
-    if (threadIdx.x < MT * 2) {
-      const int rr = threadIdx.x >> 1, cc = (threadIdx.x & 1) * 8;
-      const long m = mt + rr;
-      u16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (m < mend) {
+  for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (r0 + cc + j < R) v[j] = Y[m * ldy + r0 + cc + j];
+    for (int r = 0; r < RB; ++r) acc[j][r] = 0.f;
+#pragma unroll 2
+  for (long m = mbeg + g; m < mend; m += 4) {
+    float xv[8], yv[RB];
+    if (kok) {
+      load8(X + m * ldx + k, xv);
+      if (drop.p > 0.f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] *= drop_mult(drop, dseed, m, k + j, K);
       }
-      *reinterpret_cast<u16x8_t*>(Ys + rr * 16 + cc) = v;
-    }
-    __syncthreads();
+    } else {
 #pragma unroll
-    for (int s = 0; s < MT / 32; ++s) {
-      // A[k][m] = X[m][k] (transposed read), B[m][r] = Y[m][r] (transposed read)
-      const bf16x8_t a = frag_tr(Xs, 64, s * 32, 16 * w);
-      const bf16x8_t b = frag_tr(Ys, 16, s * 32, 0);
-      acc = mfma16(a, b, acc);
+      for (int j = 0; j < 8; ++j) xv[j] = 0.f;
     }
+    const bf16_t* yr = Y + m * ldy + r0;  // wave-uniform address: one broadcast request
+#pragma unroll
+    for (int r = 0; r < RB; ++r) yv[r] = (r0 + r < R) ? bf2f(yr[r]) : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < RB; ++r) acc[j][r] += xv[j] * yv[r];
   }
-  // C[k][r]: row k = 4*(lane>>4)+i (within the wave's 16 columns), col r = lane&15
-  const int r = r0 + (lane & 15);
-  if (r < R) {
+  if (g > 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = k0 + 16 * w + 4 * (lane >> 4) + i;
-      if (k < K) atomicAdd(out + (long)k * osk + (long)r * osr, acc[i] * scale);
-    }
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < RB; ++r) red[g - 1][c][j * RB + r] = acc[j][r];
+  }
+  __syncthreads();
+  if (g == 0 && kok) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        if (r0 + r >= R) continue;
+        const float v = acc[j][r] + red[0][c][j * RB + r] + red[1][c][j * RB + r] + red[2][c][j * RB + r];
+        atomicAdd(out + (long)(k + j) * osk + (long)(r0 + r) * osr, v * scale);
+      }
   }
 }
 
@@ -169,15 +213,15 @@ __global__ void lora_merge_kernel(T* W, long wsk, long wsn, const float* __restr
 }
 
 void lora_rowdot(const bf16_t* X, long ldx, const bf16_t* Wt, long ldw, bf16_t* U, long ldu, long M, int K, int R, float s,
-                 hipStream_t st) {
+                 LoraDrop drop, hipStream_t st) {
   const int grid = cdiv(M, 16);
-  if (R <= 16) lora_rowdot_kernel<1><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s);
-  else if (R <= 32) lora_rowdot_kernel<2><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s);
-  else lora_rowdot_kernel<4><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s);
+  if (R <= 16) lora_rowdot_kernel<1><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);
+  else if (R <= 32) lora_rowdot_kernel<2><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);
+  else lora_rowdot_kernel<4><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);
 }
 
 void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const bf16_t* W, long ldw, bf16_t* Y, long ldy,
-                 long M, int N, int R, float s, hipStream_t st) {
+                 long M, int N, int R, float s, LoraDrop drop, hipStream_t st) {
   const int nthreads_x = (N / 8 + 63) / 64 * 64;
   const int bx = nthreads_x < 256 ? nthreads_x : 256;
   const int gx = cdiv(N / 8, bx);
@@ -186,7 +230,7 @@ void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const 
   if (rows < 16) rows = 16;
   dim3 grid(gx, (unsigned)cdiv(M, rows));
   switch (R) {
-#define MFT_UPD(RV) case RV: lora_update_kernel<RV><<<grid, bx, 0, st>>>(base, ldb, U, ldu, W, ldw, Y, ldy, M, N, (int)rows, s); break;
+#define MFT_UPD(RV) case RV: lora_update_kernel<RV><<<grid, bx, 0, st>>>(base, ldb, U, ldu, W, ldw, Y, ldy, M, N, (int)rows, s, drop); break;
     MFT_UPD(1) MFT_UPD(2) MFT_UPD(4) MFT_UPD(8) MFT_UPD(16)
 #undef MFT_UPD
     default: {
@@ -195,23 +239,29 @@ void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const 
         const int rr = R - r0 < 16 ? R - r0 : 16;
         if (rr != 16) { fprintf(stderr, "lora_update: rank %d must be a multiple of 16 above 16\n", R); abort(); }
         lora_update_kernel<16><<<grid, bx, 0, st>>>(r0 == 0 ? base : Y, r0 == 0 ? ldb : ldy, U + r0, ldu,
-                                                     W + (long)r0 * ldw, ldw, Y, ldy, M, N, (int)rows, s);
+                                                     W + (long)r0 * ldw, ldw, Y, ldy, M, N, (int)rows, s, drop);
       }
     }
   }
 }
 
 void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out, long osk, long osr, long M, int K, int R,
-                float scale, hipStream_t st) {
-  const int gx = cdiv(K, 64);
-  const int gz = cdiv(R, 16);
+                float scale, LoraDrop drop, hipStream_t st) {
+  const int rb = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : 8;
+  const int gx = cdiv(K, 512);
+  const int gz = cdiv(R, rb);
+  // ~1k blocks; each block's 4 row groups stream >= 64 rows each
   long chunks = 1024 / (gx * gz);
   if (chunks < 1) chunks = 1;
   long chunk = (M + chunks - 1) / chunks;
-  chunk = (chunk + 63) / 64 * 64;
   if (chunk < 256) chunk = 256;
   dim3 grid(gx, (unsigned)cdiv(M, chunk), gz);
-  lora_wgrad_kernel<<<grid, 256, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale);
+  switch (rb) {
+    case 1: lora_wgrad_kernel<1><<<grid, 256, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop); break;
+    case 2: lora_wgrad_kernel<2><<<grid, 256, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop); break;
+    case 4: lora_wgrad_kernel<4><<<grid, 256, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop); break;
+    default: lora_wgrad_kernel<8><<<grid, 256, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop); break;
+  }
 }
 
 void lora_merge(void* W, int w_is_bf16, long wsk, long wsn, const float* A, const float* B, int K, int N, int R, float s,

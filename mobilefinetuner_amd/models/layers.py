@@ -15,6 +15,12 @@ import torch.nn as nn
 from ..ops import functional as Fx
 
 
+def _salt(name: str) -> int:
+    """Stable per-adapter salt for the dropout hash (zlib.crc32: not randomised per process)."""
+    import zlib
+    return zlib.crc32(name.encode())
+
+
 @dataclass
 class LoRASlice:
     """One LoRA adapter on columns [col0, col0 + ncols) of a (possibly fused) linear output.
@@ -37,6 +43,7 @@ class Linear(nn.Module):
                                  requires_grad=False) if bias else None
         self.lora_slices: list[LoRASlice] = []
         self.lora_scale = 0.0
+        self.lora_dropout = 0.0
         self.lora_enabled = True
         self._lora_params = nn.ParameterList()
 
@@ -56,8 +63,8 @@ class Linear(nn.Module):
 
     def forward(self, x):
         if self.lora_slices and self.lora_enabled:
-            return Fx.lora_linear(x, self.weight, self.bias,
-                                  [(s.col0, s.ncols, s.A, s.B) for s in self.lora_slices], self.lora_scale)
+            sl = [(s.col0, s.ncols, s.A, s.B, self.lora_dropout, _salt(s.name)) for s in self.lora_slices]
+            return Fx.lora_linear(x, self.weight, self.bias, sl, self.lora_scale, self.training)
         return Fx.linear(x, self.weight, self.bias)
 
     @torch.no_grad()

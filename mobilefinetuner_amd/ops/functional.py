@@ -414,13 +414,14 @@ class _LoRALinear(Function):
             x2 = x2.contiguous()
         y = torch.addmm(bc, x2, wc.t()) if bc is not None else torch.mm(x2, wc.t())
         us = []
-        for i, (c0, n) in enumerate(slices):
+        ctr = dropout_counter(x.device)
+        for i, (c0, n, dp, salt) in enumerate(slices):
             Ac, Bc = cw(ab[2 * i]), cw(ab[2 * i + 1])
             R = Ac.shape[0]
             u = torch.empty(x2.shape[0], R, device=x.device, dtype=x.dtype)
-            C.lora_rowdot(x2, Ac, u, 1.0)                     # u = x A^T
+            C.lora_rowdot(x2, Ac, u, 1.0, dp, salt, ctr)      # u = dropout(x) A^T
             ys = y[:, c0:c0 + n]
-            C.lora_update(ys, u, Bc, ys, float(s))            # y[:, slice] += s u B
+            C.lora_update(ys, u, Bc, ys, float(s), 0.0, 0, None)  # y[:, slice] += s u B
             us.append(u)
         ctx.save_for_backward(x2, *us)
         ctx.params = ab
@@ -440,20 +441,21 @@ class _LoRALinear(Function):
             dy2 = dy2.contiguous()
         dx = torch.mm(dy2, ctx.wc) if ctx.needs_input_grad[0] else None
         grads = []
-        for i, (c0, n) in enumerate(ctx.slices):
+        ctr = dropout_counter(dy.device)
+        for i, (c0, n, dp, salt) in enumerate(ctx.slices):
             A, B = ab[2 * i], ab[2 * i + 1]
             Ac, Bc = cw(A), cw(B)
             R = Ac.shape[0]
             dys = dy2[:, c0:c0 + n]
             v = torch.empty(dy2.shape[0], R, device=dy.device, dtype=dy.dtype)
-            C.lora_rowdot(dys, Bc, v, s)                      # v = s dy B^T
+            C.lora_rowdot(dys, Bc, v, s, 0.0, 0, None)        # v = s dy B^T
             if dx is not None:
-                C.lora_update(dx, v, Ac, dx, 1.0)             # dx += v A
+                C.lora_update(dx, v, Ac, dx, 1.0, dp, salt, ctr)  # dx += mask * (v A)
             gA = gB = None
             if _needs(A):
                 buf = _grad_buf(A)
                 tgt = buf if buf is not None else torch.zeros(R, K, device=dy.device)
-                C.lora_wgrad(x2, v, tgt, 1, K, 1.0)           # dA[r, k] += sum_m v[m, r] x[m, k]
+                C.lora_wgrad(x2, v, tgt, 1, K, 1.0, dp, salt, ctr)  # dA[r, k] += sum_m v[m, r] drop(x)[m, k]
                 if buf is not None:
                     grad_ready(A)
                 else:
@@ -461,7 +463,7 @@ class _LoRALinear(Function):
             if _needs(B):
                 buf = _grad_buf(B)
                 tgt = buf if buf is not None else torch.zeros(R, n, device=dy.device)
-                C.lora_wgrad(dys, us[i], tgt, 1, n, s)        # dB[r, n] += s sum_m u[m, r] dy[m, n]
+                C.lora_wgrad(dys, us[i], tgt, 1, n, s, 0.0, 0, None)  # dB[r, n] += s sum_m u[m, r] dy[m, n]
                 if buf is not None:
                     grad_ready(B)
                 else:
@@ -472,26 +474,50 @@ class _LoRALinear(Function):
         return (dx, None, None, None, None, *grads)
 
 
-def lora_linear(x, w, b, slices, scale):
-    """slices: list of (col0, ncols, A, B).  See _LoRALinear."""
+def lora_linear(x, w, b, slices, scale, training: bool = True):
+    """slices: list of (col0, ncols, A, B[, dropout_p, salt]).  See _LoRALinear.  Dropout (PEFT
+    semantics: on the LoRA input only) is active when ``training`` and grad mode are on."""
+    norm = []
+    for sl in slices:
+        c0, n, A, B = sl[:4]
+        p = float(sl[4]) if len(sl) > 4 else 0.0
+        salt = int(sl[5]) if len(sl) > 5 else 0
+        if not (training and torch.is_grad_enabled()):
+            p = 0.0
+        norm.append((c0, n, A, B, p, salt))
     if not x.is_cuda:
         xf = x.float()
         y = xf @ rw(w).float().t()
         if b is not None:
             y = y + rw(b).float()
         parts = []
-        for (c0, n, A, B) in slices:
-            parts.append((c0, n, scale * ((xf @ rw(A).float().t()) @ rw(B).float())))
+        for (c0, n, A, B, p, salt) in norm:
+            xd = torch.nn.functional.dropout(xf, p) if p > 0 else xf
+            parts.append((c0, n, scale * ((xd @ rw(A).float().t()) @ rw(B).float())))
         if parts:
             y = y.clone()
             for c0, n, d in parts:
                 y[..., c0:c0 + n] = y[..., c0:c0 + n] + d
         return y.to(x.dtype)
-    meta = tuple((int(c0), int(n)) for (c0, n, _, _) in slices)
+    meta = tuple((int(c0), int(n), float(p), int(salt) & 0xFFFFFFFF) for (c0, n, _, _, p, salt) in norm)
     ab = []
-    for (_, _, A, B) in slices:
-        ab += [A, B]
+    for sl in norm:
+        ab += [sl[2], sl[3]]
     return _LoRALinear.apply(x, w, b, float(scale), meta, *ab)
+
+
+_DROP_CTR = {}
+
+
+def dropout_counter(device):
+    """Device-resident step counter feeding the counter-based LoRA dropout masks; the training
+    engine bumps it once per step (inside the captured graph)."""
+    key = str(device)
+    t = _DROP_CTR.get(key)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int64, device=device)
+        _DROP_CTR[key] = t
+    return t
 
 
 # ---------------------------------------------------------------- fused LM head + cross entropy

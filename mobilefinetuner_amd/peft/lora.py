@@ -124,6 +124,7 @@ def inject_gpt2(model, spec: LoraSpec):
             else:
                 A0 = _gpt2_init_A(lin.in_features, n, spec.rank, spec.seed)
             A, B = lin.add_lora(c0, n, spec.rank, spec.scale, A0, name)
+            lin.lora_dropout = float(spec.dropout)
             added.append((name, A, B))
     model.lora_spec = spec
     return added
@@ -159,6 +160,7 @@ def inject_gemma(model, spec: LoraSpec):
         for lin, c0, n, name in plan:
             A0 = _peft_init_A(lin.in_features, spec.rank, g)
             A, B = lin.add_lora(c0, n, spec.rank, spec.scale, A0, name)
+            lin.lora_dropout = float(spec.dropout)
             added.append((name, A, B))
     model.lora_spec = spec
     return added

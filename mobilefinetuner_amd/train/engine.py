@@ -40,6 +40,8 @@ class TrainStep:
             self.loss_dev = torch.zeros(1, device=self.flat.grad.device, dtype=torch.float32)
         self.loss_dev.zero_()
         self.flat.grad.zero_()
+        from ..ops.functional import dropout_counter
+        dropout_counter(self.flat.grad.device).add_(1)  # fresh LoRA-dropout masks every step
         for ids, lab in batches:
             loss = self.loss_fn(self.model, ids, lab, scale)
             (loss * scale).backward()

@@ -326,3 +326,42 @@ def test_gpt2_train_step_decreases_loss():
     batch = [(ids[:, :-1].contiguous(), ids[:, 1:].contiguous())]
     losses = [float(st(batch).item()) for _ in range(30)]
     assert losses[-1] < losses[0] - 0.1, losses
+
+
+def test_lora_dropout_consistent_fwd_bwd():
+    """The hash mask must be identical in u = drop(x)A^T (fwd), dA and the dx term (bwd)."""
+    from mobilefinetuner_amd._ext import native
+    from mobilefinetuner_amd.ops import functional as Fx
+    C = native()
+    M, K, N, R, p, salt = 96, 64, 64, 8, 0.3, 1234
+    ctr = Fx.dropout_counter(DEV)
+    # recover the mask with A = I: u = drop(ones) -> mask/(1-p)
+    ones = torch.ones(M, K, device=DEV, dtype=torch.bfloat16)
+    eye = torch.eye(K, device=DEV, dtype=torch.bfloat16)
+    um = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    C.lora_rowdot(ones, eye, um, 1.0, p, salt, ctr)
+    mask = (um.float() * (1 - p)).round()
+    assert set(mask.unique().tolist()) <= {0.0, 1.0}
+    assert abs(1 - mask.mean().item() - p) < 0.05
+    x = (torch.randn(M, K, device=DEV) * 0.5).bfloat16().requires_grad_()
+    W = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    A = torch.nn.Parameter(torch.randn(R, K, device=DEV) * 0.1)
+    B = torch.nn.Parameter(torch.randn(R, N, device=DEV) * 0.1)
+    A.shadow, B.shadow = A.detach().bfloat16(), B.detach().bfloat16()
+    y = Fx.lora_linear(x, W, None, [(0, N, A, B, p, salt)], 2.0, training=True)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    xr = x.detach().float().requires_grad_()
+    Ar = A.shadow.float().requires_grad_()
+    Br = B.shadow.float().requires_grad_()
+    xd = xr * mask / (1 - p)
+    yr = xr @ W.float().t() + 2.0 * (xd @ Ar.t()) @ Br
+    (yr * g.float()).sum().backward()
+    _close(y, yr, 0.03, 0.01, msg="drop y")
+    _close(x.grad, xr.grad, 0.05, 0.01, msg="drop dx")
+    _close(A.grad, Ar.grad, 0.05, 0.02, msg="drop dA")
+    _close(B.grad, Br.grad, 0.05, 0.02, msg="drop dB")
+    ctr.add_(1)
+    um2 = torch.empty_like(um)
+    C.lora_rowdot(ones, eye, um2, 1.0, p, salt, ctr)
+    assert not torch.equal(um, um2), "a new step must draw a new mask"
