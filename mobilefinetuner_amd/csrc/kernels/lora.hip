@@ -16,6 +16,7 @@
 //                 and read transposed (ds_read_b64_tr_b16); one fp32 atomic per output element
 //                 per 512-row chunk straight into the flat grad buffer (accumulation semantics).
 //   lora_merge  : W[k, n] += s * sum_r A[r, k] B[r, n]                merge / unmerge (K10)
+#include <cstdlib>
 #include "mfma.h"
 #include "kernels.h"
 
@@ -135,64 +136,127 @@ __global__ __launch_bounds__(256) void lora_update_kernel(const bf16_t* base, lo
 }
 
 // ------------------------------------------------------------------------------------ wgrad
-// Streaming VALU form (the reduction runs over M, the long axis; each X row is read once).
-// block = 256 threads = 64 column-chunks of 8 x 4 row groups; each thread accumulates an 8 x RB
-// fp32 outer-product tile over its rows; the 4 row groups are summed in LDS and one fp32 atomic per
-// output element per block goes straight into the grad buffer.  RB <= 8 ranks per z-block.
-template <int RB>
-__global__ __launch_bounds__(256) void lora_wgrad_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Y,
-                                                         long ldy, float* __restrict__ out, long osk, long osr, long M, int K,
-                                                         int R, long chunk, float scale, LoraDrop drop) {
-  __shared__ __attribute__((aligned(16))) float red[3][64][8 * RB + 1];
-  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int k = (blockIdx.x * 64 + c) * 8;
+// Streaming VALU form: the reduction runs over M (the long axis) so every X element is read
+// exactly once with fully coalesced 8-B/lane loads.  A 1024-thread block = 16 waves that share one
+// 256-column strip (4 columns per lane) and split the block's row chunk round-robin; each lane keeps
+// a 4 x RB fp32 outer-product tile in registers and issues U independent row loads before using any
+// (the kernel is pure HBM streaming: bytes in flight, not FLOPs, set its speed).  The 16 wave tiles
+// are folded in LDS (16 -> 8 -> final sum) and each output element gets ONE fp32 atomic per block,
+// straight into the grad buffer.  The launcher picks the row chunk so that ~4 waves per SIMD are
+// live while atomics stay a small fraction of the X traffic.
+template <int RB, bool YVEC, bool DROP>
+__global__ __launch_bounds__(1024) void lora_wgrad_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Y,
+                                                          long ldy, float* __restrict__ out, long osk, long osr, long M, int K,
+                                                          int R, long chunk, float scale, LoraDrop drop) {
+  constexpr int U = DROP ? 6 : 12;
+  __shared__ __attribute__((aligned(16))) float red[8][RB][256];
+  __shared__ __attribute__((aligned(16))) bf16_t ysh[2][16 * U][RB];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int k = blockIdx.x * 256 + lane * 4;
   const int r0 = blockIdx.z * RB;
   const long mbeg = (long)blockIdx.y * chunk;
   const long mend = min(M, mbeg + chunk);
   const bool kok = k < K;
-  const uint32_t dseed = drop.p > 0.f ? drop_seed(drop) : 0u;
-  float acc[8][RB];
+  const uint32_t dseed = DROP ? drop_seed(drop) : 0u;
+  float acc[4][RB];
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int r = 0; r < RB; ++r) acc[j][r] = 0.f;
-#pragma unroll 2
-  for (long m = mbeg + g; m < mend; m += 4) {
-    float xv[8], yv[RB];
-    if (kok) {
-      load8(X + m * ldx + k, xv);
-      if (drop.p > 0.f) {
+  // all X loads are unconditional (row / column indices clamped into range; out-of-range rows are
+  // zeroed after the load) so the U row loads issue back to back.  Y rows of the block's current
+  // 16*U-row tile are staged once in LDS (double-buffered: one barrier per tile) and read back as
+  // wave-uniform broadcasts.
+  const int kc = kok ? k : K - 4;
+  int t = 0;
+  for (long mb0 = mbeg; mb0 < mend; mb0 += 16 * U, ++t) {
+    bf16_t* ys = ysh[t & 1][0];
+    // Y tile load first (its wait then covers only itself), X loads next, then the LDS store
+    const long my = mb0 + threadIdx.x;
+    const bool ystage = threadIdx.x < 16 * U;
+    const bf16_t* yp = Y + (ystage && my < mend ? my : mbeg) * ldy + r0;
+    u16x8_t yv8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (ystage) {
+      if constexpr (YVEC && RB == 8) {
+        yv8 = *reinterpret_cast<const u16x8_t*>(yp);
+      } else if constexpr (YVEC && RB == 4) {
+        const u16x4_t v = *reinterpret_cast<const u16x4_t*>(yp);
+        yv8 = u16x8_t{v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+      } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] *= drop_mult(drop, dseed, m, k + j, K);
+        for (int r = 0; r < RB; ++r) yv8[r] = (r0 + r < R) ? yp[r] : (bf16_t)0;
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xv[j] = 0.f;
+      if (my >= mend) yv8 = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
     }
-    const bf16_t* yr = Y + m * ldy + r0;  // wave-uniform address: one broadcast request
+    u16x4_t xr[U];
 #pragma unroll
-    for (int r = 0; r < RB; ++r) yv[r] = (r0 + r < R) ? bf2f(yr[r]) : 0.f;
+    for (int u = 0; u < U; ++u) {
+      const long m = mb0 + w + 16 * u;
+      const long mc = m < mend ? m : mend - 1;
+      xr[u] = *reinterpret_cast<const u16x4_t*>(X + mc * ldx + kc);
+    }
+    if (ystage) {
+      bf16_t* yd = ys + threadIdx.x * RB;
+      if constexpr (RB == 8) {
+        *reinterpret_cast<u16x8_t*>(yd) = yv8;
+      } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+        for (int r = 0; r < RB; ++r) yd[r] = yv8[r];
+      }
+    }
+    __syncthreads();
 #pragma unroll
-      for (int r = 0; r < RB; ++r) acc[j][r] += xv[j] * yv[r];
+    for (int u = 0; u < U; ++u) {
+      const long m = mb0 + w + 16 * u;
+      float xv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xv[j] = bf2f(xr[u][j]);
+      if constexpr (DROP) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xv[j] *= drop_mult(drop, dseed, m, kc + j, K);
+      }
+      const bf16_t* yrow = ys + (w + 16 * u) * RB;
+      float yv[RB];
+      if constexpr (RB == 8) {
+        load8(yrow, yv);
+      } else {
+#pragma unroll
+        for (int r = 0; r < RB; ++r) yv[r] = bf2f(yrow[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j][r] += xv[j] * yv[r];
+    }
   }
-  if (g > 0) {
+  // 16 -> 8 wave tiles.  LDS image per wave: [r][256 columns] so the final pass reads columns
+  // contiguously and every atomic wave-instruction covers 256 contiguous bytes when osk == 1
+  // (MI355X_MICROARCH.md "Global float atomics": scattered 4-B lanes run ~17x slower).
+  if (w >= 8) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int r = 0; r < RB; ++r) red[g - 1][c][j * RB + r] = acc[j][r];
+    for (int r = 0; r < RB; ++r)
+      *reinterpret_cast<f32x4_t*>(&red[w - 8][r][lane * 4]) = f32x4_t{acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
   }
   __syncthreads();
-  if (g == 0 && kok) {
+  if (w < 8) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int r = 0; r < RB; ++r) {
+      f32x4_t* q = reinterpret_cast<f32x4_t*>(&red[w][r][lane * 4]);
+      *q = *q + f32x4_t{acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
+    }
+  }
+  __syncthreads();
+  // final 8-way sum over RB x 256 outputs; lane order follows the unit-stride output axis
+  for (int o = threadIdx.x; o < RB * 256; o += 1024) {
+    int r, c;
+    if (osk == 1) { r = o >> 8; c = o & 255; }
+    else { c = o / RB; r = o % RB; }
+    const int kk = blockIdx.x * 256 + c;
+    if (kk >= K || r0 + r >= R) continue;
+    float v = 0.f;
 #pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        if (r0 + r >= R) continue;
-        const float v = acc[j][r] + red[0][c][j * RB + r] + red[1][c][j * RB + r] + red[2][c][j * RB + r];
-        atomicAdd(out + (long)(k + j) * osk + (long)(r0 + r) * osr, v * scale);
-      }
+    for (int i = 0; i < 8; ++i) v += red[i][r][c];
+    atomicAdd(out + (long)kk * osk + (long)(r0 + r) * osr, v * scale);
   }
 }
 
@@ -247,21 +311,40 @@ void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const 
 
 void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out, long osk, long osr, long M, int K, int R,
                 float scale, LoraDrop drop, hipStream_t st) {
-  const int rb = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : 8;
-  const int gx = cdiv(K, 512);
-  const int gz = cdiv(R, rb);
-  // ~1k blocks; each block's 4 row groups stream >= 64 rows each
-  long chunks = 1024 / (gx * gz);
-  if (chunks < 1) chunks = 1;
-  long chunk = (M + chunks - 1) / chunks;
-  if (chunk < 256) chunk = 256;
-  dim3 grid(gx, (unsigned)cdiv(M, chunk), gz);
-  switch (rb) {
-    case 1: lora_wgrad_kernel<1><<<grid, 256, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop); break;
-    case 2: lora_wgrad_kernel<2><<<grid, 256, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop); break;
-    case 4: lora_wgrad_kernel<4><<<grid, 256, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop); break;
-    default: lora_wgrad_kernel<8><<<grid, 256, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop); break;
+  if ((K % 4) || (ldx % 4) || (reinterpret_cast<uintptr_t>(X) % 8)) {
+    fprintf(stderr, "lora_wgrad: K (%d) and ldx (%ld) must be multiples of 4 and X 8-byte aligned\n", K, ldx);
+    abort();
   }
+  const int rb = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : 8;
+  const int gx = cdiv(K, 256);
+  const int gz = cdiv(R, rb);
+  // ~4 live waves per SIMD (4096 waves = 256 blocks of 16) but at least U=8 rows per wave; the
+  // chunk is a multiple of 16 rows so every wave streams the same number of rows
+  static const long target = getenv("MFT_WGRAD_BLOCKS") ? atol(getenv("MFT_WGRAD_BLOCKS")) : 256;
+  long nrc = cdiv(target, (long)gx * gz);
+  const long max_nrc = cdiv(M, 16 * 8);  // >= 8 rows per wave
+  if (nrc > max_nrc) nrc = max_nrc;
+  if (nrc < 1) nrc = 1;
+  long chunk = cdiv(M, nrc);
+  chunk = cdiv(chunk, 16) * 16;
+  dim3 grid(gx, (unsigned)cdiv(M, chunk), gz);
+  // vector Y loads need every rank block complete and 2*RB-byte aligned rows
+  const bool yvec = (rb == 8 || rb == 4) && R % rb == 0 && ldy % rb == 0 &&
+                    reinterpret_cast<uintptr_t>(Y) % (2 * rb) == 0;
+#define MFT_WG(RBV, YV)                                                                                         \
+  do {                                                                                                          \
+    if (drop.p > 0.f)                                                                                           \
+      lora_wgrad_kernel<RBV, YV, true><<<grid, 1024, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop);  \
+    else                                                                                                        \
+      lora_wgrad_kernel<RBV, YV, false><<<grid, 1024, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop); \
+  } while (0)
+  switch (rb) {
+    case 1: MFT_WG(1, false); break;
+    case 2: MFT_WG(2, false); break;
+    case 4: if (yvec) MFT_WG(4, true); else MFT_WG(4, false); break;
+    default: if (yvec) MFT_WG(8, true); else MFT_WG(8, false); break;
+  }
+#undef MFT_WG
 }
 
 void lora_merge(void* W, int w_is_bf16, long wsk, long wsn, const float* A, const float* B, int K, int N, int R, float s,

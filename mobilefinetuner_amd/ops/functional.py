@@ -512,6 +512,9 @@ _DROP_CTR = {}
 def dropout_counter(device):
     """Device-resident step counter feeding the counter-based LoRA dropout masks; the training
     engine bumps it once per step (inside the captured graph)."""
+    device = torch.device(device)
+    if device.type == "cuda" and device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
     key = str(device)
     t = _DROP_CTR.get(key)
     if t is None:
