@@ -124,8 +124,12 @@ void attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, T
   const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
   const int Sk = k.size(1), Hkv = k.size(2);
   c10::DeviceGuard g(q.device());
-  auto delta = torch::empty({B, H, Sq}, q.options().dtype(torch::kFloat32));
-  auto dq_acc = torch::empty({B, Sq, H, D}, q.options().dtype(torch::kFloat32));
+  const bool short_path = mft::attn_short_path(D, Sq, Sk, (int)window);
+  Tensor delta, dq_acc;
+  if (!short_path) {
+    delta = torch::empty({B, H, Sq}, q.options().dtype(torch::kFloat32));
+    dq_acc = torch::empty({B, Sq, H, D}, q.options().dtype(torch::kFloat32));
+  }
   Tensor dk_tmp, dv_tmp;
   mft::AttnBwdArgs a{};
   if (H != Hkv) {
@@ -135,7 +139,9 @@ void attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, T
     fill_st(a.tmp_st, dk_tmp);
   }
   a.q = bp(q); a.k = bp(k); a.v = bp(v); a.o = bp(o); a.dout = bp(dout); a.lse = fp(lse);
-  a.delta = fp(delta); a.dq_acc = fp(dq_acc); a.dq = bp(dq); a.dk = bp(dk); a.dv = bp(dv);
+  a.delta = short_path ? nullptr : fp(delta);
+  a.dq_acc = short_path ? nullptr : fp(dq_acc);
+  a.dq = bp(dq); a.dk = bp(dk); a.dv = bp(dv);
   fill_st(a.q_st, q); fill_st(a.k_st, k); fill_st(a.v_st, v); fill_st(a.o_st, o); fill_st(a.do_st, dout);
   fill_st(a.dq_st, dq); fill_st(a.dk_st, dk); fill_st(a.dv_st, dv);
   a.B = B; a.H = H; a.Hkv = Hkv; a.Sq = Sq; a.Sk = Sk; a.D = D;

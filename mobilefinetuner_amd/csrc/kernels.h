@@ -46,6 +46,8 @@ struct AttnBwdArgs {
 };
 void attn_fwd(const AttnArgs& a, hipStream_t s);
 void attn_bwd(const AttnBwdArgs& a, hipStream_t s);
+// true when the single-workgroup-per-(batch, head) kernels run (no delta / dq_acc workspaces)
+bool attn_short_path(int D, int Sq, int Sk, int window);
 
 // ---------------------------------------------------------------- activations (act.hip)
 void gelu_fwd(const bf16_t* x, bf16_t* y, long n, hipStream_t st);

@@ -175,25 +175,28 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// delta[b,h,i] = sum_d dO[b,i,h,d] * O[b,i,h,d]   (one thread per row)
+// delta[b,h,i] = sum_d dO[b,i,h,d] * O[b,i,h,d]; D/8 consecutive lanes share one row so every row
+// is read as contiguous 16-B pieces (a thread-per-row form strides the rows across lanes).
 template <int D>
 __global__ void attn_bwd_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
                                       float* __restrict__ delta, AttnStrides os, AttnStrides ds, int B, int H, int Sq) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)B * H * Sq) return;
-  const int i = idx % Sq, h = (idx / Sq) % H, b = idx / ((long)Sq * H);
-  const bf16_t* orow = o + b * os.sb + (long)i * os.ss + h * os.sh;
-  const bf16_t* drow = dout + b * ds.sb + (long)i * ds.ss + h * ds.sh;
+  constexpr int LPR = D / 8;  // lanes per row
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long idx = t / LPR;
+  const int c = (int)(t % LPR) * 8;
+  const bool ok = idx < (long)B * H * Sq;
   float s = 0.f;
-#pragma unroll 4
-  for (int c = 0; c < D; c += 8) {
+  if (ok) {
+    const int i = idx % Sq, h = (idx / Sq) % H, b = idx / ((long)Sq * H);
     float a[8], g[8];
-    load8(orow + c, a);
-    load8(drow + c, g);
+    load8(o + b * os.sb + (long)i * os.ss + h * os.sh + c, a);
+    load8(dout + b * ds.sb + (long)i * ds.ss + h * ds.sh + c, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += a[j] * g[j];
   }
-  delta[idx] = s;
+#pragma unroll
+  for (int off = 1; off < LPR; off <<= 1) s += __shfl_xor(s, off, 64);
+  if (ok && c == 0) delta[idx] = s;
 }
 
 // Backward: one workgroup = 64 keys of one (batch, q-head); 4 waves x 16 keys.  dK/dV for the
@@ -360,10 +363,310 @@ __global__ void gqa_reduce_kernel(const bf16_t* __restrict__ in, bf16_t* __restr
   store8(out + b * s.sb + (long)i * s.ss + hk * s.sh + d, acc);
 }
 
+// ============================================================================================
+// Short-sequence path: Sq == Sk <= 128, D == 64, no sliding window (GPT-2 fine-tuning at seq 128).
+// One workgroup = one (batch, head), 8 waves.  K and V (and for the backward Q, dO) are staged
+// ONCE into LDS, so nothing is re-read across query/key blocks, the whole score row lives in
+// registers (no online rescaling), the backward needs no dQ atomics or fp32 dQ workspace (dS^T is
+// shared through LDS and dQ is formed in a second phase inside the same workgroup), and delta
+// (rowsum dO*O) is computed while staging.  Outputs go through a per-wave LDS tile so every global
+// store is a 16-B row piece.
+// ============================================================================================
+constexpr int kShortS = 128;
+
+__host__ __device__ constexpr int short_ldp() { return kShortS + 8; }
+
+// per-wave [16][D] C-layout tile (acc[n][i] = row 4(l>>4)+i, col n*16+(l&15)) -> 16 global rows
+template <int D>
+__device__ __forceinline__ void store_tile16(bf16_t* scratch, int ld, const f32x4_t* acc, const float* rs,
+                                             bf16_t* dst, AttnStrides st, int b, int h, int row0, int nrows) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int n = 0; n < D / 16; ++n)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) scratch[(4 * (lane >> 4) + i) * ld + n * 16 + (lane & 15)] = f2bf(acc[n][i] * rs[i]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  constexpr int CPR = D / 8;             // 16-B pieces per row
+  for (int c = lane; c < 16 * CPR; c += 64) {
+    const int r = c / CPR, ch = c % CPR;
+    if (r < nrows)
+      *reinterpret_cast<u16x8_t*>(dst + b * st.sb + (long)(row0 + r) * st.ss + h * st.sh + ch * 8) =
+          *reinterpret_cast<const u16x8_t*>(scratch + r * ld + ch * 8);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int D>
+__global__ __launch_bounds__(512) void attn_fwd_short_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                             const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+                                                             float* __restrict__ lse, AttnStrides qs, AttnStrides ks,
+                                                             AttnStrides vs, AttnStrides os, int H, int Hkv, int S,
+                                                             float scale, int causal, const int* __restrict__ kv_lens) {
+  constexpr int SM = kShortS, LDP = short_ldp(), NB = SM / 16, CPR = D / 8;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* Ks = smem;            // [SM][D]
+  bf16_t* Vs = Ks + SM * D;     // [SM][D]
+  bf16_t* Pw = Vs + SM * D + (threadIdx.x >> 6) * 16 * LDP;  // per-wave [16][LDP]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = blockIdx.x, b = blockIdx.y, hk = h / (H / Hkv);
+  const int kv_len = kv_lens ? min(kv_lens[b], S) : S;
+  const float c2 = scale * kLog2e;
+  // issue every global load first (K, V pieces and this wave's Q fragments), then fill LDS
+  constexpr int PER = SM * CPR / 512;
+  u16x8_t kr[PER], vr[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = threadIdx.x + j * 512, r = c / CPR, ch = c % CPR;
+    const bool ok = r < S;
+    kr[j] = ok ? *reinterpret_cast<const u16x8_t*>(k + b * ks.sb + (long)r * ks.ss + hk * ks.sh + ch * 8) : u16x8_t{};
+    vr[j] = ok ? *reinterpret_cast<const u16x8_t*>(v + b * vs.sb + (long)r * vs.ss + hk * vs.sh + ch * 8) : u16x8_t{};
+  }
+  bf16x8_t qf[D / 32];
+  {
+    const int qr = 16 * w + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s)
+      qf[s] = qr < S ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qr * qs.ss + h * qs.sh + s * 32 + 8 * (lane >> 4))
+                     : bf16x8_t{};
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = threadIdx.x + j * 512, r = c / CPR, ch = c % CPR;
+    *reinterpret_cast<u16x8_t*>(Ks + r * D + ch * 8) = kr[j];
+    *reinterpret_cast<u16x8_t*>(Vs + r * D + ch * 8) = vr[j];
+  }
+  __syncthreads();
+  if (16 * w >= S) return;  // no query rows for this wave (after the only barrier)
+  const int nbmax = causal ? w + 1 : NB;  // key blocks of 16 visible to rows 16w..16w+15
+  f32x4_t sacc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    sacc[nb] = zero4();
+    if (nb < nbmax) {
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) sacc[nb] = mfma16(qf[s], frag_row(Ks, D, nb * 16, s * 32), sacc[nb]);
+    }
+  }
+  float mrow[4], lrow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int qi = 16 * w + 4 * (lane >> 4) + i;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int kj = nb * 16 + (lane & 15);
+      const bool ok = nb < nbmax && kj < kv_len && (!causal || kj <= qi);
+      const float sv = ok ? sacc[nb][i] * c2 : -INFINITY;
+      sacc[nb][i] = sv;
+      mx = fmaxf(mx, sv);
+    }
+#pragma unroll
+    for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
+    const float ms = mx == -INFINITY ? 0.f : mx;
+    float rs = 0.f;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const float p = exp2f(sacc[nb][i] - ms);
+      sacc[nb][i] = p;
+      rs += p;
+    }
+#pragma unroll
+    for (int o2 = 1; o2 < 16; o2 <<= 1) rs += __shfl_xor(rs, o2, 64);
+    mrow[i] = mx;
+    lrow[i] = rs;
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Pw[(4 * (lane >> 4) + i) * LDP + nb * 16 + (lane & 15)] = f2bf(sacc[nb][i]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  f32x4_t acc[D / 16];
+#pragma unroll
+  for (int n = 0; n < D / 16; ++n) acc[n] = zero4();
+  const int ksmax = causal ? (16 * w + 15) / 32 + 1 : SM / 32;
+#pragma unroll
+  for (int kk = 0; kk < SM / 32; ++kk) {
+    if (kk < ksmax) {
+      const bf16x8_t pa = frag_row(Pw, LDP, 0, kk * 32);
+#pragma unroll
+      for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr(Vs, D, kk * 32, n * 16), acc[n]);
+    }
+  }
+  float inv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    inv[i] = lrow[i] > 0.f ? 1.f / lrow[i] : 0.f;
+    const int qi = 16 * w + 4 * (lane >> 4) + i;
+    if ((lane & 15) == 0 && qi < S)
+      lse[((long)b * H + h) * S + qi] = lrow[i] > 0.f ? (mrow[i] + log2f(lrow[i])) / kLog2e : 1e30f;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  store_tile16<D>(Pw, LDP, acc, inv, o, os, b, h, 16 * w, min(16, S - 16 * w));
+}
+
+template <int D>
+__global__ __launch_bounds__(512) void attn_bwd_short_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    bf16_t* __restrict__ dq, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, AttnStrides qs, AttnStrides ks,
+    AttnStrides vs, AttnStrides ost, AttnStrides dos, AttnStrides dqs, AttnStrides dks, AttnStrides dvs, int H, int Hkv,
+    int S, float scale, int causal, const int* __restrict__ kv_lens, int dkv_per_qhead) {
+  constexpr int SM = kShortS, LDT = short_ldp(), NB = SM / 16, CPR = D / 8;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* Ks = smem;              // [SM][D]
+  bf16_t* Vs = Ks + SM * D;       // [SM][D]
+  bf16_t* Qs = Vs + SM * D;       // [SM][D]
+  bf16_t* dOs = Qs + SM * D;      // [SM][D]
+  bf16_t* DST = dOs + SM * D;     // [SM keys][LDT]  dS^T * scale
+  bf16_t* PTw = DST + SM * LDT + (threadIdx.x >> 6) * 16 * LDT;  // per-wave [16][LDT]
+  float* lse_s = reinterpret_cast<float*>(DST + SM * LDT + 8 * 16 * LDT);  // [SM]
+  float* del_s = lse_s + SM;                                             // [SM]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = blockIdx.x, b = blockIdx.y, hk = h / (H / Hkv);
+  const int kv_len = kv_lens ? min(kv_lens[b], S) : S;
+  const float c2 = scale * kLog2e;
+
+  // ---- stage K, V, Q, dO; delta = rowsum(dO * O) from the same registers (CPR lanes per row)
+  {
+    constexpr int PER = SM * CPR / 512;
+    u16x8_t kr[PER], vr[PER], qr[PER], dr[PER], orr[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = threadIdx.x + j * 512, r = c / CPR, ch = c % CPR;
+      const bool ok = r < S;
+      kr[j] = ok ? *reinterpret_cast<const u16x8_t*>(k + b * ks.sb + (long)r * ks.ss + hk * ks.sh + ch * 8) : u16x8_t{};
+      vr[j] = ok ? *reinterpret_cast<const u16x8_t*>(v + b * vs.sb + (long)r * vs.ss + hk * vs.sh + ch * 8) : u16x8_t{};
+      qr[j] = ok ? *reinterpret_cast<const u16x8_t*>(q + b * qs.sb + (long)r * qs.ss + h * qs.sh + ch * 8) : u16x8_t{};
+      dr[j] = ok ? *reinterpret_cast<const u16x8_t*>(dout + b * dos.sb + (long)r * dos.ss + h * dos.sh + ch * 8) : u16x8_t{};
+      orr[j] = ok ? *reinterpret_cast<const u16x8_t*>(o + b * ost.sb + (long)r * ost.ss + h * ost.sh + ch * 8) : u16x8_t{};
+    }
+    if (threadIdx.x < SM) lse_s[threadIdx.x] = threadIdx.x < S ? lse[((long)b * H + h) * S + threadIdx.x] * kLog2e : 1e30f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = threadIdx.x + j * 512, r = c / CPR, ch = c % CPR;
+      *reinterpret_cast<u16x8_t*>(Ks + r * D + ch * 8) = kr[j];
+      *reinterpret_cast<u16x8_t*>(Vs + r * D + ch * 8) = vr[j];
+      *reinterpret_cast<u16x8_t*>(Qs + r * D + ch * 8) = qr[j];
+      *reinterpret_cast<u16x8_t*>(dOs + r * D + ch * 8) = dr[j];
+      float dsum = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum += bf2f(dr[j][e]) * bf2f(orr[j][e]);
+#pragma unroll
+      for (int off = 1; off < CPR; off <<= 1) dsum += __shfl_xor(dsum, off, 64);
+      if (ch == 0) del_s[r] = dsum;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 1: wave w owns keys 16w..16w+15: P^T, dS^T rows, dV and dK
+  f32x4_t dKa[D / 16], dVa[D / 16];
+#pragma unroll
+  for (int n = 0; n < D / 16; ++n) { dKa[n] = zero4(); dVa[n] = zero4(); }
+  const int nbmin = causal ? w : 0;  // query blocks of 16 that can see these keys
+  {
+    f32x4_t st[NB], dpt[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      st[nb] = zero4();
+      dpt[nb] = zero4();
+      if (nb >= nbmin) {
+#pragma unroll
+        for (int s = 0; s < D / 32; ++s) {
+          st[nb] = mfma16(frag_row(Ks, D, 16 * w, s * 32), frag_row(Qs, D, nb * 16, s * 32), st[nb]);
+          dpt[nb] = mfma16(frag_row(Vs, D, 16 * w, s * 32), frag_row(dOs, D, nb * 16, s * 32), dpt[nb]);
+        }
+      }
+    }
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int qi = nb * 16 + (lane & 15);
+      const float lq = lse_s[qi], dq_ = del_s[qi];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int kr = 16 * w + 4 * (lane >> 4) + i;
+        const bool ok = nb >= nbmin && qi < S && kr < kv_len && (!causal || kr <= qi);
+        const float p = ok ? exp2f(st[nb][i] * c2 - lq) : 0.f;
+        const float ds = p * (dpt[nb][i] - dq_) * scale;
+        PTw[(4 * (lane >> 4) + i) * LDT + qi] = f2bf(p);
+        DST[kr * LDT + qi] = f2bf(ds);
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    const int ksmin = causal ? (16 * w) / 32 : 0;
+#pragma unroll
+    for (int kk = 0; kk < SM / 32; ++kk) {
+      if (kk >= ksmin) {
+        const bf16x8_t pa = frag_row(PTw, LDT, 0, kk * 32);
+        const bf16x8_t da = frag_row(DST, LDT, 16 * w, kk * 32);
+#pragma unroll
+        for (int n = 0; n < D / 16; ++n) {
+          dVa[n] = mfma16(pa, frag_tr(dOs, D, kk * 32, n * 16), dVa[n]);
+          dKa[n] = mfma16(da, frag_tr(Qs, D, kk * 32, n * 16), dKa[n]);
+        }
+      }
+    }
+  }
+  __syncthreads();  // every wave's dS^T rows are in LDS
+
+  // ---- phase 2: wave w owns queries 16w..16w+15: dQ = dS K
+  f32x4_t dQa[D / 16];
+#pragma unroll
+  for (int n = 0; n < D / 16; ++n) dQa[n] = zero4();
+  {
+    const int ksmax = causal ? (16 * w + 15) / 32 + 1 : SM / 32;
+#pragma unroll
+    for (int kk = 0; kk < SM / 32; ++kk) {
+      if (kk < ksmax) {
+        const bf16x8_t a = frag_tr(DST, LDT, kk * 32, 16 * w);
+#pragma unroll
+        for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(a, frag_tr(Ks, D, kk * 32, n * 16), dQa[n]);
+      }
+    }
+  }
+  if (16 * w >= S) return;
+  const float one[4] = {1.f, 1.f, 1.f, 1.f};
+  const int nrows = min(16, S - 16 * w);
+  const int hout = dkv_per_qhead ? h : hk;
+  store_tile16<D>(PTw, LDT, dQa, one, dq, dqs, b, h, 16 * w, nrows);
+  store_tile16<D>(PTw, LDT, dKa, one, dk, dks, b, hout, 16 * w, nrows);
+  store_tile16<D>(PTw, LDT, dVa, one, dv, dvs, b, hout, 16 * w, nrows);
+}
+
+bool attn_short_path(int D, int Sq, int Sk, int window) {
+  return D == 64 && Sq == Sk && Sq <= kShortS && window <= 0;
+}
+
 static AttnStrides mk(const long* st) { return AttnStrides{st[0], st[1], st[2]}; }
 
 template <int D>
 static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
+  if constexpr (D == 64) {
+    if (attn_short_path(D, a.Sq, a.Sk, a.window)) {
+      const size_t shm = sizeof(bf16_t) * (2 * kShortS * D + 8 * 16 * short_ldp());
+      static bool attr = false;
+      if (!attr) {
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_short_kernel<D>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+      }
+      attn_fwd_short_kernel<D><<<dim3(a.H, a.B), 512, shm, stream>>>(a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st),
+                                                                      mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.scale,
+                                                                      a.causal, a.kv_lens);
+      return;
+    }
+  }
   constexpr int BQ = 64, BK = 64, LDP = BK + 8;
   const size_t shm = sizeof(bf16_t) * (2 * BK * D + 4 * 16 * LDP);
   dim3 grid(cdiv(a.Sq, BQ), a.H, a.B);
@@ -374,11 +677,34 @@ static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
 
 template <int D>
 static void bwd_launch(const AttnBwdArgs& a, hipStream_t stream) {
+  if constexpr (D == 64) {
+    if (attn_short_path(D, a.Sq, a.Sk, a.window)) {
+      const size_t shm = sizeof(bf16_t) * (4 * kShortS * D + 2 * kShortS * short_ldp()) + sizeof(float) * 2 * kShortS;
+      static bool attr = false;
+      if (!attr) {
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_short_kernel<D>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+      }
+      const int per_qhead = a.H != a.Hkv;
+      attn_bwd_short_kernel<D><<<dim3(a.H, a.B), 512, shm, stream>>>(
+          a.q, a.k, a.v, a.o, a.dout, a.lse, a.dq, per_qhead ? a.dk_tmp : a.dk, per_qhead ? a.dv_tmp : a.dv,
+          mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.o_st), mk(a.do_st), mk(a.dq_st),
+          per_qhead ? mk(a.tmp_st) : mk(a.dk_st), per_qhead ? mk(a.tmp_st) : mk(a.dv_st), a.H, a.Hkv, a.Sq, a.scale,
+          a.causal, a.kv_lens, per_qhead);
+      if (per_qhead) {
+        const long nk8 = (long)a.B * a.Sk * a.Hkv * D / 8;
+        gqa_reduce_kernel<<<cdiv(nk8, 256), 256, 0, stream>>>(a.dk_tmp, a.dk, mk(a.dk_st), a.B, a.Sk, a.H, a.Hkv, D);
+        gqa_reduce_kernel<<<cdiv(nk8, 256), 256, 0, stream>>>(a.dv_tmp, a.dv, mk(a.dv_st), a.B, a.Sk, a.H, a.Hkv, D);
+      }
+      return;
+    }
+  }
   constexpr int BQ = 64, BK = 64, LDT = BQ + 8;
   {
     const long rows = (long)a.B * a.H * a.Sq;
-    attn_bwd_delta_kernel<D><<<cdiv(rows, 256), 256, 0, stream>>>(a.o, a.dout, a.delta, mk(a.o_st), mk(a.do_st), a.B,
-                                                                  a.H, a.Sq);
+    attn_bwd_delta_kernel<D><<<cdiv(rows * (D / 8), 256), 256, 0, stream>>>(a.o, a.dout, a.delta, mk(a.o_st),
+                                                                            mk(a.do_st), a.B, a.H, a.Sq);
   }
   MFT_HIP_CHECK(hipMemsetAsync(a.dq_acc, 0, sizeof(float) * (size_t)a.B * a.Sq * a.H * D, stream));
   const size_t shm = sizeof(bf16_t) * (2 * BK * D + 2 * BQ * D + 2 * BK * LDT) + sizeof(float) * 2 * BQ;

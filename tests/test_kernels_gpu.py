@@ -108,8 +108,12 @@ def _attn_ref(q, k, v, scale, causal, window, kv_lens=None):
 
 
 @pytest.mark.parametrize("B,S,H,Hkv,D,causal,window", [
-    (2, 128, 4, 4, 64, True, 0),
-    (3, 100, 2, 2, 64, True, 0),
+    (2, 128, 4, 4, 64, True, 0),     # short path (one workgroup per (batch, head))
+    (3, 100, 2, 2, 64, True, 0),     # short path, partial tile
+    (2, 128, 4, 2, 64, True, 0),     # short path + GQA
+    (2, 128, 2, 2, 64, False, 0),    # short path, non-causal
+    (1, 17, 2, 2, 64, True, 0),      # short path, tiny S
+    (2, 160, 4, 4, 64, True, 0),     # general path at D=64
     (2, 256, 4, 1, 256, True, 0),
     (1, 320, 4, 1, 256, True, 64),
     (2, 64, 4, 2, 128, False, 0),
