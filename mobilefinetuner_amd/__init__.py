@@ -9,4 +9,6 @@ host offload.
 """
 __version__ = "0.1.0"
 
+import torch  # noqa: F401  (the extension links libtorch / libamdhip64: load them first)
+
 from ._ext import native  # noqa: F401

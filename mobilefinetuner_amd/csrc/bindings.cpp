@@ -352,9 +352,55 @@ Tensor add_bf16(Tensor a, Tensor b) {
   return y;
 }
 
+
+// ------------------------------------------------------------------ GEMM (gemm.hip)
+// C = epi(alpha * A op(B)); A [M,K]; B [N,K] (b_nn = false) or [K,N] (b_nn = true).
+// Returns {C, aux}: aux is the pre-activation written by GEMM_EPI_BIAS_GELU.
+std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::optional<Tensor> bias,
+                            c10::optional<Tensor> aux, double alpha, int64_t bm, c10::optional<Tensor> out) {
+  CHECK_CUDA(A); CHECK_BF16(A); CHECK_BF16(B);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "gemm: row-contiguous 2-D operands");
+  const int M = A.size(0), K = A.size(1);
+  const int N = b_nn ? B.size(1) : B.size(0);
+  TORCH_CHECK((b_nn ? B.size(0) : B.size(1)) == K, "gemm: inner dimensions differ");
+  TORCH_CHECK(mft::gemm_supported(M, N, K), "gemm: needs K % 64 == 0 and N % 8 == 0");
+  TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "gemm: leading dimensions must be multiples of 8");
+  c10::DeviceGuard g(A.device());
+  Tensor C;
+  if (out.has_value()) {
+    C = *out;
+    TORCH_CHECK(C.size(0) == M && C.size(1) == N && C.stride(1) == 1, "gemm: out shape");
+    TORCH_CHECK(C.scalar_type() == (epi == mft::GEMM_EPI_F32ACC ? torch::kFloat32 : torch::kBFloat16), "gemm: out dtype");
+  } else {
+    TORCH_CHECK(epi != mft::GEMM_EPI_F32ACC, "gemm: fp32 accumulate needs out=");
+    C = torch::empty({M, N}, A.options());
+  }
+  Tensor X;
+  if (epi == mft::GEMM_EPI_BIAS_GELU) {
+    X = aux.has_value() ? *aux : torch::empty({M, N}, A.options());
+  } else if (epi == mft::GEMM_EPI_DGELU) {
+    TORCH_CHECK(aux.has_value(), "gemm: dGELU needs aux (pre-activation)");
+    X = *aux;
+  }
+  if (X.defined()) TORCH_CHECK(X.size(0) == M && X.size(1) == N && X.stride(1) == 1 && X.stride(0) % 8 == 0, "gemm: aux shape");
+  if (epi == mft::GEMM_EPI_BIAS || epi == mft::GEMM_EPI_BIAS_GELU) {
+    TORCH_CHECK(bias.has_value() && bias->numel() == N && bias->scalar_type() == torch::kBFloat16, "gemm: bf16 bias [N]");
+  }
+  mft::GemmArgs a{};
+  a.A = bp(A); a.lda = A.stride(0);
+  a.B = bp(B); a.ldb = B.stride(0);
+  a.C = C.data_ptr(); a.ldc = C.stride(0);
+  a.bias = bias.has_value() ? bp(*bias) : nullptr;
+  a.aux = X.defined() ? bp(X) : nullptr; a.ldaux = X.defined() ? X.stride(0) : 0;
+  a.M = M; a.N = N; a.K = K; a.alpha = (float)alpha;
+  mft::gemm(a, b_nn, (int)epi, (int)bm, stream());
+  return {C, X};
+}
+
 }  // namespace
 
 void register_runtime(py::module_& m);  // csrc/runtime_bindings.cpp
+void register_gemm_lt(py::module_& m);  // csrc/gemm_lt.cpp
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "mobilefinetuner_amd native kernels (gfx950 HIP) and C++ runtime";
@@ -379,6 +425,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_update", &lora_update);
   m.def("lora_wgrad", &lora_wgrad);
   m.def("lora_merge", &lora_merge);
+  m.def("gemm", &gemm_op);
   m.def("rope_apply", &rope_apply);
   m.def("qknorm_rope_fwd", &qknorm_rope_fwd);
   m.def("qknorm_rope_bwd", &qknorm_rope_bwd);
@@ -387,4 +434,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("scale_bf16", &scale_bf16);
   m.def("add_bf16", &add_bf16);
   register_runtime(m);
+  register_gemm_lt(m);
 }

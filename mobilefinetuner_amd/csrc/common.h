@@ -89,18 +89,24 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// GELU (tanh form, GPT-2 "gelu_new") via 0.5 (1 + tanh(u)) = sigmoid(2u): one v_exp_f32 and one
+// v_rcp_f32 instead of a libm tanhf (which dominated the fused GEMM epilogues).  Saturates
+// correctly: exp -> inf gives sigmoid 0, exp -> 0 gives 1.
+__device__ __forceinline__ float sigmoid_fast(float z) { return __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
+
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  const float u = k0 * (x + k1 * x * x * x);
+  return x * sigmoid_fast(2.f * u);
 }
 
+// d/dx: s + 2 x s (1 - s) k0 (1 + 3 k1 x^2), s = sigmoid(2u)   (0.5 (1 - tanh^2) = 2 s (1 - s))
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  const float x2 = x * x;
+  const float u = k0 * (x + k1 * x2 * x);
+  const float s = sigmoid_fast(2.f * u);
+  return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x2);
 }
 
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

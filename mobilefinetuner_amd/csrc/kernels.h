@@ -49,6 +49,25 @@ void attn_bwd(const AttnBwdArgs& a, hipStream_t s);
 // true when the single-workgroup-per-(batch, head) kernels run (no delta / dq_acc workspaces)
 bool attn_short_path(int D, int Sq, int Sk, int window);
 
+// ---------------------------------------------------------------- GEMM (gemm.hip)
+enum GemmEpi { GEMM_EPI_NONE = 0, GEMM_EPI_BIAS = 1, GEMM_EPI_BIAS_GELU = 2, GEMM_EPI_DGELU = 3, GEMM_EPI_F32ACC = 4 };
+struct GemmArgs {
+  const bf16_t* A;
+  long lda;  // A [M, K] row-major
+  const bf16_t* B;
+  long ldb;  // NT: B [N, K]; NN: B [K, N]
+  void* C;
+  long ldc;  // bf16 [M, N] (fp32 for GEMM_EPI_F32ACC, accumulated)
+  const bf16_t* bias;  // [N]
+  bf16_t* aux;
+  long ldaux;  // BIAS_GELU: pre-activation out; DGELU: pre-activation in
+  int M, N, K;
+  float alpha;
+};
+bool gemm_supported(int M, int N, int K);
+// cfg: tile configuration (gemm.hip launch_e): 0 = 256x256, 1 = 128x256, 2 = 128x128, 3 = 256x128
+void gemm(const GemmArgs& g, bool b_nn, int epi, int cfg, hipStream_t st);
+
 // ---------------------------------------------------------------- activations (act.hip)
 void gelu_fwd(const bf16_t* x, bf16_t* y, long n, hipStream_t st);
 void gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, long n, hipStream_t st);

@@ -96,7 +96,7 @@ class GPT2Block(nn.Module):
         return self.c_proj(o.view(B * S, self.H * self.D))
 
     def mlp(self, h):
-        return self.mlp_proj(Fx.gelu(self.c_fc(h)))
+        return Fx.mlp_gelu(h, self.c_fc, self.mlp_proj)
 
 
 class GPT2Model(nn.Module):

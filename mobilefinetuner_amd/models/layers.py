@@ -77,6 +77,7 @@ class Linear(nn.Module):
             w[sl.col0:sl.col0 + sl.ncols] = (w[sl.col0:sl.col0 + sl.ncols].float() + delta).to(w.dtype)
             if getattr(self.weight, "shadow", None) is not None:
                 self.weight.shadow.copy_(self.weight.data.to(self.weight.shadow.dtype))
+        Fx.drop_weight_t(self.weight)
 
     def extra_repr(self):
         return f"in={self.in_features}, out={self.out_features}, lora_slices={len(self.lora_slices)}"

@@ -395,6 +395,101 @@ def linear(x, w, b=None):
     return _Linear.apply(x, w, b)
 
 
+GEMM_EPI_NONE, GEMM_EPI_BIAS, GEMM_EPI_BIAS_GELU, GEMM_EPI_DGELU, GEMM_EPI_F32ACC = 0, 1, 2, 3, 4
+
+
+def weight_t(p):
+    """Row-major [in, out] copy of a [out, in] weight so data-gradient GEMMs (dx = dy W) run in the
+    K-contiguous "NT" form of gemm.hip.  Frozen weights cache it on the parameter (one extra copy of
+    the frozen weights -- trivial against 288 GB HBM; ``Linear.merge_lora`` and the loaders drop
+    it); trainable (full fine-tuning) or sharded weights get a fresh transpose each call."""
+    wc = cw(p)
+    if _needs(p) or getattr(p, "_mft_sharded", False):
+        return wc.t().contiguous()
+    c = getattr(p, "_mft_wt", None)
+    if c is None or c.data_ptr() == 0 or c.shape != (wc.shape[1], wc.shape[0]):
+        c = wc.t().contiguous()
+        p._mft_wt = c
+    return c
+
+
+def drop_weight_t(p):
+    if hasattr(p, "_mft_wt"):
+        del p._mft_wt
+
+
+class _MLPGelu(Function):
+    """y = GELU(x W1^T + b1) W2^T + b2 with both GELU passes fused into the hand-written MFMA GEMM
+    (csrc/kernels/gemm.hip): the fc GEMM's epilogue adds the bias and writes BOTH the
+    pre-activation (saved for backward) and GELU(pre); the mlp_proj data-grad GEMM's epilogue
+    multiplies by GELU'(pre), so no separate GELU pass touches the [M, 4C] activations in either
+    direction.  Reference MLP: graph/gpt2_model.cpp (c_fc matmul, gelu_new, c_proj matmul as three
+    separate ops)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        C = native()
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        w1c, b1c, w2c, b2c = cw(w1), cw(b1), cw(w2), cw(b2)
+        h, pre = C.gemm(x2, w1c, False, GEMM_EPI_BIAS_GELU, b1c, None, 1.0, 0, None)
+        y = torch.addmm(b2c, h, w2c.t())
+        ctx.save_for_backward(x2 if _needs(w1) else None, pre, h if _needs(w2) else None)
+        ctx.params = (w1, b1, w2, b2)
+        ctx.wc = w1c
+        ctx.shape = shape
+        return y.view(*shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        x2, pre, h = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        w1c = ctx.wc
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dpre = C.gemm(dy2, weight_t(w2), False, GEMM_EPI_DGELU, None, pre, 1.0, 0, None)[0]
+        grads = [None] * 5
+        if ctx.needs_input_grad[0]:
+            grads[0] = torch.mm(dpre, w1c).view(ctx.shape)
+        for i, (p, g_out, g_in) in enumerate(((w2, dy2, h), (w1, dpre, x2))):
+            if not _needs(p):
+                continue
+            buf = _grad_buf(p)
+            if buf is not None:
+                _mm_wgrad_into(buf, g_out, g_in)
+                grad_ready(p)
+            else:
+                grads[3 if i == 0 else 1] = torch.mm(g_out.t(), g_in, out_dtype=torch.float32).to(p.dtype)
+        if _needs(b2):
+            grads[4] = _sink(b2, dy2.float().sum(0))
+        if _needs(b1):
+            grads[2] = _sink(b1, dpre.float().sum(0))
+        return tuple(grads)
+
+
+def fused_mlp_available() -> bool:
+    """Fused-epilogue MLP (MFT_FUSED_MLP=1).  Off by default: measured in the GPT-2 bench step on
+    MI355X the gemm.hip main loop (~0.8-0.9 PF/s at these shapes) still trails hipBLASLt
+    (0.9-1.3 PF/s) by more than the GELU passes it removes (1.198M vs 1.221M tok/s)."""
+    import os
+    return os.environ.get("MFT_FUSED_MLP", "0") == "1"
+
+
+def mlp_gelu(x, fc, proj):
+    """GPT-2 MLP: proj(GELU(fc(x))).  Fused-epilogue path when neither Linear carries an active
+    LoRA adapter (the adapter's rank-r update lands between the GEMM and the GELU)."""
+    plain = not ((fc.lora_slices and fc.lora_enabled) or (proj.lora_slices and proj.lora_enabled))
+    K = x.shape[-1]
+    if (x.is_cuda and plain and fc.bias is not None and proj.bias is not None and fused_mlp_available()
+            and K % 64 == 0 and fc.out_features % 64 == 0):
+        return _MLPGelu.apply(x, fc.weight, fc.bias, proj.weight, proj.bias)
+    return proj(gelu(fc(x)))
+
+
 class _LoRALinear(Function):
     """y = x W^T + b + sum_i s * (x A_i^T) B_i placed in column slices [c0_i, c0_i + n_i) of y.
 

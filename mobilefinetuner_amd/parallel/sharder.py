@@ -142,6 +142,8 @@ def shard_gpt2(model, budget_bytes: int, disk_dir: str = "") -> ParameterSharder
     sh = ParameterSharder(budget_bytes, disk_dir)
     sh.register_group("embed", [model.wte.data, model.wpe.data])
     for i, b in enumerate(model.blocks):
+        for lin in (b.c_attn, b.c_proj, b.c_fc, b.mlp_proj):
+            lin.weight._mft_sharded = True  # no cached transposed copies of offloaded weights
         ts = [b.c_attn.weight.data, b.c_attn.bias.data, b.c_proj.weight.data, b.c_proj.bias.data,
               b.c_fc.weight.data, b.c_fc.bias.data, b.mlp_proj.weight.data, b.mlp_proj.bias.data]
         sh.register_group(f"block{i}", [t for t in ts if not t.requires_grad])
@@ -153,6 +155,8 @@ def shard_gemma(model, budget_bytes: int, disk_dir: str = "") -> ParameterSharde
     sh = ParameterSharder(budget_bytes, disk_dir)
     sh.register_group("embed", [model.embed.data])
     for i, L in enumerate(model.layers):
+        for lin in (L.qkv_proj, L.o_proj, L.gate_up_proj, L.down_proj):
+            lin.weight._mft_sharded = True
         ts = [L.qkv_proj.weight.data, L.o_proj.weight.data, L.gate_up_proj.weight.data, L.down_proj.weight.data]
         sh.register_group(f"block{i}", ts)
     model.sharder = sh

@@ -102,6 +102,69 @@ def test_gelu_and_gated():
         _close(gu.grad, r.grad, 0.1, 0.01, msg=f"gated {act} grad")
 
 
+@pytest.mark.parametrize("M,K,N,nn,bm", [(300, 128, 264, False, 0), (1000, 192, 512, True, 0),
+                                          (777, 256, 136, False, 1), (64, 64, 8, True, 1),
+                                          (517, 320, 392, False, 2), (517, 320, 392, True, 2),
+                                          (300, 128, 264, False, 3), (300, 128, 264, True, 3)])
+def test_gemm_mfma(M, K, N, nn, bm):
+    """gemm.hip (NT and NN operand layouts, M/N tails) and its epilogues vs fp32 torch."""
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(K, N, device=DEV) if nn else torch.randn(N, K, device=DEV)).mul(0.1).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16()
+    ref_ = x.float() @ (w.float() if nn else w.float().t())
+    y = C.gemm(x, w, nn, 0, None, None, 1.0, bm, None)[0]
+    _close(y, ref_, 0.02, 0.01, msg="gemm")
+    y = C.gemm(x, w, nn, 1, b, None, 0.5, bm, None)[0]
+    _close(y, 0.5 * ref_ + b.float(), 0.02, 0.01, msg="gemm bias")
+    h, pre = C.gemm(x, w, nn, 2, b, None, 1.0, bm, None)
+    pr = ref_ + b.float()
+    _close(pre, pr, 0.02, 0.01, msg="gemm pre")
+    _close(h, torch.nn.functional.gelu(pr, approximate="tanh"), 0.02, 0.01, msg="gemm gelu")
+    g = C.gemm(x, w, nn, 3, None, pre, 1.0, bm, None)[0]
+    pf = pre.float()
+    xg = pf.clone().requires_grad_()
+    torch.nn.functional.gelu(xg, approximate="tanh").sum().backward()
+    _close(g, ref_ * xg.grad, 0.03, 0.01, msg="gemm dgelu")
+    acc = torch.ones(M, N, device=DEV)
+    C.gemm(x, w, nn, 4, None, None, 2.0, bm, acc)
+    _close(acc, 1 + 2 * ref_, 0.05, 0.01, msg="gemm f32 acc")
+
+
+@pytest.mark.parametrize("trainable", [False, True])
+def test_fused_mlp_gelu_epilogues(trainable, monkeypatch):
+    """gemm.hip BIAS_GELU / DGELU epilogue MLP vs the fp32 reference (tanh GELU)."""
+    monkeypatch.setenv("MFT_FUSED_MLP", "1")
+    from mobilefinetuner_amd.models.layers import Linear
+    from mobilefinetuner_amd.ops import functional as Fx
+    from mobilefinetuner_amd.ops import reference as ref
+    assert Fx.fused_mlp_available()
+    M, C = 500, 256
+    fc, proj = Linear(C, 4 * C, device=DEV), Linear(4 * C, C, device=DEV)
+    with torch.no_grad():
+        for lin in (fc, proj):
+            lin.weight.copy_(torch.randn_like(lin.weight, dtype=torch.float32) * 0.05)
+            lin.bias.copy_(torch.randn_like(lin.bias, dtype=torch.float32) * 0.5)
+    if trainable:
+        for lin in (fc, proj):
+            lin.weight.requires_grad_(True)
+            lin.bias.requires_grad_(True)
+    x = torch.randn(M, C, device=DEV).bfloat16().requires_grad_()
+    y = Fx.mlp_gelu(x, fc, proj)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    xr = x.detach().float().requires_grad_()
+    ps = [t.detach().float().requires_grad_(trainable) for t in (fc.weight, fc.bias, proj.weight, proj.bias)]
+    yr = ref.gelu_tanh(xr @ ps[0].t() + ps[1]) @ ps[2].t() + ps[3]
+    (yr * g.float()).sum().backward()
+    _close(y, yr, 0.03, 0.02, msg="mlp y")
+    _close(x.grad, xr.grad, 0.03, 0.03, msg="mlp dx")
+    if trainable:
+        for p, r, n in zip((fc.weight, fc.bias, proj.weight, proj.bias), ps, ("w1", "b1", "w2", "b2")):
+            _close(p.grad, r.grad, 0.05, 0.03, msg=f"mlp d{n}")
+
+
 def _attn_ref(q, k, v, scale, causal, window, kv_lens=None):
     from mobilefinetuner_amd.ops import reference as ref
     return ref.attention(q, k, v, scale, causal, window, kv_lens)
