@@ -29,13 +29,22 @@ inline T* optp(const c10::optional<Tensor>& t) {
 }
 
 // ------------------------------------------------------------------ norms
-std::vector<Tensor> layernorm_fwd(Tensor x, c10::optional<Tensor> delta, Tensor w, Tensor b, double eps) {
+// out_cols > N: y is allocated [M, out_cols] and only its first N columns are written (room for
+// appended LoRA columns); the caller owns the rest.
+Tensor alloc_wide(const Tensor& x, int M, int N, int64_t out_cols) {
+  if (out_cols <= N) return torch::empty_like(x);
+  TORCH_CHECK(out_cols % 8 == 0, "out_cols must be a multiple of 8");
+  return torch::empty({M, out_cols}, x.options());
+}
+
+std::vector<Tensor> layernorm_fwd(Tensor x, c10::optional<Tensor> delta, Tensor w, Tensor b, double eps,
+                                  int64_t out_cols) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(w); CHECK_F32(b);
   const int N = x.size(-1);
   TORCH_CHECK(N % 8 == 0 && N <= 4096, "layernorm: width must be a multiple of 8 and <= 4096");
   const int M = x.numel() / N;
   c10::DeviceGuard g(x.device());
-  auto y = torch::empty_like(x);
+  auto y = alloc_wide(x, M, N, out_cols);
   auto mean = torch::empty({M}, x.options().dtype(torch::kFloat32));
   auto rstd = torch::empty({M}, x.options().dtype(torch::kFloat32));
   Tensor s;
@@ -44,50 +53,56 @@ std::vector<Tensor> layernorm_fwd(Tensor x, c10::optional<Tensor> delta, Tensor 
     s = torch::empty_like(x);
   }
   mft::layernorm_fwd(bp(x), delta ? bp(*delta) : nullptr, s.defined() ? bp(s) : nullptr, fp(w), fp(b), bp(y), fp(mean),
-                     fp(rstd), M, N, (float)eps, stream());
+                     fp(rstd), M, N, (float)eps, y.size(-1), stream());
   return {y, s.defined() ? s : Tensor(), mean, rstd};
 }
 
+// dy may be a wide [M, >= N] row-strided gradient (see out_cols); only its first N columns are read
 Tensor layernorm_bwd(Tensor x, Tensor dy, Tensor w, Tensor mean, Tensor rstd, c10::optional<Tensor> dresid,
                      c10::optional<Tensor> dw, c10::optional<Tensor> db) {
-  CHECK_CONTIG(x); CHECK_CONTIG(dy);
+  CHECK_CONTIG(x);
   const int N = x.size(-1), M = x.numel() / N;
+  TORCH_CHECK(dy.stride(-1) == 1 && dy.size(-1) >= N && dy.numel() / dy.size(-1) == M && dy.stride(0) % 8 == 0,
+              "layernorm_bwd: dy must be [M, >= N] with unit column stride");
   c10::DeviceGuard g(x.device());
   auto dx = torch::empty_like(x);
   Tensor work;
   float* dwp = optp<float>(dw);
   if (dwp) work = torch::empty({2L * mft::norm_bwd_partial_blocks(M) * N}, x.options().dtype(torch::kFloat32));
   mft::layernorm_bwd(bp(x), bp(dy), fp(w), fp(mean), fp(rstd), dresid ? bp(*dresid) : nullptr, bp(dx), dwp,
-                     optp<float>(db), dwp ? fp(work) : nullptr, M, N, 1, stream());
+                     optp<float>(db), dwp ? fp(work) : nullptr, M, N, 1, dy.dim() == 2 ? dy.stride(0) : N, stream());
   return dx;
 }
 
-std::vector<Tensor> rmsnorm_fwd(Tensor x, c10::optional<Tensor> delta, Tensor w, double eps, double offset) {
+std::vector<Tensor> rmsnorm_fwd(Tensor x, c10::optional<Tensor> delta, Tensor w, double eps, double offset,
+                                int64_t out_cols) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(w);
   const int N = x.size(-1);
   TORCH_CHECK(N % 8 == 0 && N <= 4096, "rmsnorm: width must be a multiple of 8 and <= 4096");
   const int M = x.numel() / N;
   c10::DeviceGuard g(x.device());
-  auto y = torch::empty_like(x);
+  auto y = alloc_wide(x, M, N, out_cols);
   auto rstd = torch::empty({M}, x.options().dtype(torch::kFloat32));
   Tensor s;
   if (delta.has_value()) s = torch::empty_like(x);
   mft::rmsnorm_fwd(bp(x), delta ? bp(*delta) : nullptr, s.defined() ? bp(s) : nullptr, fp(w), bp(y), fp(rstd), M, N,
-                   (float)eps, (float)offset, stream());
+                   (float)eps, (float)offset, y.size(-1), stream());
   return {y, s.defined() ? s : Tensor(), rstd};
 }
 
 Tensor rmsnorm_bwd(Tensor x, Tensor dy, Tensor w, Tensor rstd, c10::optional<Tensor> dresid, double offset,
                    c10::optional<Tensor> dw) {
-  CHECK_CONTIG(x); CHECK_CONTIG(dy);
+  CHECK_CONTIG(x);
   const int N = x.size(-1), M = x.numel() / N;
+  TORCH_CHECK(dy.stride(-1) == 1 && dy.size(-1) >= N && dy.numel() / dy.size(-1) == M && dy.stride(0) % 8 == 0,
+              "rmsnorm_bwd: dy must be [M, >= N] with unit column stride");
   c10::DeviceGuard g(x.device());
   auto dx = torch::empty_like(x);
   Tensor work;
   float* dwp = optp<float>(dw);
   if (dwp) work = torch::empty({2L * mft::norm_bwd_partial_blocks(M) * N}, x.options().dtype(torch::kFloat32));
   mft::rmsnorm_bwd(bp(x), bp(dy), fp(w), fp(rstd), dresid ? bp(*dresid) : nullptr, bp(dx), dwp,
-                   dwp ? fp(work) : nullptr, M, N, (float)offset, 1, stream());
+                   dwp ? fp(work) : nullptr, M, N, (float)offset, 1, dy.dim() == 2 ? dy.stride(0) : N, stream());
   return dx;
 }
 
@@ -99,15 +114,25 @@ void fill_st(long* st, const Tensor& t) {  // [B, S, H, D] strides
   st[0] = t.stride(0); st[1] = t.stride(1); st[2] = t.stride(2);
 }
 
+// out_cols > H*D: the output is allocated [B, Sq, out_cols] with O in the first H*D columns (room
+// for the appended LoRA columns of the consumer); the kernel writes it through its row strides.
 std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, double scale, bool causal, int64_t window,
-                             c10::optional<Tensor> kv_lens) {
+                             c10::optional<Tensor> kv_lens, int64_t out_cols) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v);
   const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
   const int Sk = k.size(1), Hkv = k.size(2);
   TORCH_CHECK(H % Hkv == 0, "H must be a multiple of Hkv");
   TORCH_CHECK(D == 64 || D == 128 || D == 256, "head dim must be 64, 128 or 256");
   c10::DeviceGuard g(q.device());
-  auto o = torch::empty({B, Sq, H, D}, q.options());
+  Tensor o_full, o;
+  if (out_cols > (int64_t)H * D) {
+    TORCH_CHECK(out_cols % 8 == 0, "attn_fwd: out_cols must be a multiple of 8");
+    o_full = torch::empty({B, Sq, out_cols}, q.options());
+    o = o_full.narrow(2, 0, (int64_t)H * D).view({B, Sq, H, D});
+  } else {
+    o = torch::empty({B, Sq, H, D}, q.options());
+    o_full = o;
+  }
   auto lse = torch::empty({B, H, Sq}, q.options().dtype(torch::kFloat32));
   mft::AttnArgs a{};
   a.q = bp(q); a.k = bp(k); a.v = bp(v); a.o = bp(o); a.lse = fp(lse);
@@ -116,7 +141,9 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, double scale, bool ca
   a.scale = (float)scale; a.causal = causal; a.window = (int)window;
   a.kv_lens = kv_lens ? kv_lens->data_ptr<int>() : nullptr;
   mft::attn_fwd(a, stream());
-  return {o, lse};
+  if (o_full.dim() == 3)  // widened output: the appended columns start out zero (consumer contract)
+    mft::zero_cols(bp(o_full), out_cols, (long)B * Sq, H * D, (int)(out_cols - (int64_t)H * D), stream());
+  return {o_full, lse, o};
 }
 
 void attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor dq, Tensor dk, Tensor dv,
@@ -397,6 +424,17 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
   return {C, X};
 }
 
+
+// Zero columns [c0, ncols) of a row-strided 2-D bf16 tensor (one small kernel, graph-capturable).
+// Deliberately outside autograd: the padding columns of augmented LoRA inputs are read by no
+// autograd-visible op (an in-place torch op there would trip the view/version checks).
+void zero_cols(Tensor t, int64_t c0) {
+  CHECK_CUDA(t); CHECK_BF16(t);
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.stride(0) % 8 == 0 && c0 % 8 == 0 && t.size(1) % 8 == 0,
+              "zero_cols: 2-D row-contiguous bf16 tensor, 8-aligned columns");
+  c10::DeviceGuard g(t.device());
+  mft::zero_cols(bp(t), t.stride(0), t.size(0), (int)c0, (int)(t.size(1) - c0), stream());
+}
 }  // namespace
 
 void register_runtime(py::module_& m);  // csrc/runtime_bindings.cpp
@@ -426,6 +464,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_wgrad", &lora_wgrad);
   m.def("lora_merge", &lora_merge);
   m.def("gemm", &gemm_op);
+  m.def("zero_cols", &zero_cols);
   m.def("rope_apply", &rope_apply);
   m.def("qknorm_rope_fwd", &qknorm_rope_fwd);
   m.def("qknorm_rope_bwd", &qknorm_rope_bwd);

@@ -10,15 +10,17 @@ typedef uint16_t bf16_t;
 
 // ---------------------------------------------------------------- norms (norm.hip)
 int norm_bwd_partial_blocks(int M);
+// ldy / lddy: row stride of the normalised output / of its gradient (0 = N).  A wider output row
+// leaves room for appended columns (the LoRA augmented-K input [x | u], lora.hip).
 void layernorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, const float* b,
-                   bf16_t* y, float* mean, float* rstd, int M, int N, float eps, hipStream_t st);
+                   bf16_t* y, float* mean, float* rstd, int M, int N, float eps, long ldy, hipStream_t st);
 void rmsnorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, bf16_t* y, float* rstd,
-                 int M, int N, float eps, float w_offset, hipStream_t st);
+                 int M, int N, float eps, float w_offset, long ldy, hipStream_t st);
 void layernorm_bwd(const bf16_t* x, const bf16_t* dy, const float* w, const float* mean, const float* rstd,
                    const bf16_t* dresid, bf16_t* dx, float* dw, float* db, float* work, int M, int N, int accumulate,
-                   hipStream_t st);
+                   long lddy, hipStream_t st);
 void rmsnorm_bwd(const bf16_t* x, const bf16_t* dy, const float* w, const float* rstd, const bf16_t* dresid, bf16_t* dx,
-                 float* dw, float* work, int M, int N, float w_offset, int accumulate, hipStream_t st);
+                 float* dw, float* work, int M, int N, float w_offset, int accumulate, long lddy, hipStream_t st);
 
 // ---------------------------------------------------------------- attention (attention.hip)
 struct AttnArgs {
@@ -158,4 +160,6 @@ void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t st);
 void cast_bf16_f32(const bf16_t* x, float* y, long n, hipStream_t st);
 void scale_bf16(const bf16_t* x, bf16_t* y, long n, const float* scale_dev, float scale, hipStream_t st);
 void add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, hipStream_t st);
+// p[row, c0 : c0 + ncols] = 0 for every row (c0, ncols, ld multiples of 8)
+void zero_cols(bf16_t* p, long ld, long M, int c0, int ncols, hipStream_t st);
 }  // namespace mft

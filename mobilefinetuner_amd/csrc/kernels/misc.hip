@@ -72,6 +72,21 @@ void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t st) {
 void cast_bf16_f32(const bf16_t* x, float* y, long n, hipStream_t st) {
   cast_bf16_f32_kernel<<<grid_for(n / 8), 256, 0, st>>>(x, y, n);
 }
+// zero columns [c0, c0 + 8 * nch) of every row (16-B stores; the padding of augmented LoRA inputs)
+__global__ void zero_cols_kernel(bf16_t* __restrict__ p, long ld, long M, int c0, int nch) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= M * nch) return;
+  const long row = t / nch;
+  const int ch = (int)(t % nch);
+  *reinterpret_cast<u16x8_t*>(p + row * ld + c0 + ch * 8) = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+}
+
+void zero_cols(bf16_t* p, long ld, long M, int c0, int ncols, hipStream_t st) {
+  const int nch = ncols / 8;
+  if (M <= 0 || nch <= 0) return;
+  zero_cols_kernel<<<cdiv(M * nch, 256), 256, 0, st>>>(p, ld, M, c0, nch);
+}
+
 void scale_bf16(const bf16_t* x, bf16_t* y, long n, const float* scale_dev, float scale, hipStream_t st) {
   scale_bf16_kernel<<<grid_for(n / 8), 256, 0, st>>>(x, y, n, scale_dev, scale);
 }

@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
                                                        bf16_t* __restrict__ s_out, const float* __restrict__ w,
                                                        const float* __restrict__ b, bf16_t* __restrict__ y,
                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                       int M, int N, float eps, float w_offset) {
+                                                       int M, int N, float eps, float w_offset, long ldy) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -82,9 +82,12 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * wv[j] + bv[j];
       }
-      store8(y + (long)row * N + ch * 8, o);
+      store8(y + (long)row * ldy + ch * 8, o);
     }
   }
+  // a wider output row (appended LoRA columns, see kernels.h) leaves its extra columns zeroed
+  for (long c = N + lane * 8; c < ldy; c += 64 * 8)
+    *reinterpret_cast<u16x8_t*>(y + (long)row * ldy + c) = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
   if (lane == 0) {
     if (!RMS) mean_out[row] = mean;
     rstd_out[row] = rstd;
@@ -101,7 +104,8 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ w, const float* __restrict__ mean_in,
                                                        const float* __restrict__ rstd_in, const bf16_t* __restrict__ dresid,
                                                        bf16_t* __restrict__ dx, float* __restrict__ dw_part,
-                                                       float* __restrict__ db_part, int M, int N, float w_offset) {
+                                                       float* __restrict__ db_part, int M, int N, float w_offset,
+                                                       long lddy) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nch = N >> 3;
   float dwa[CH][8], dba[CH][8];
@@ -122,7 +126,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
       if (ch < nch) {
         float xv[8], dv[8];
         load8(x + (long)row * N + ch * 8, xv);
-        load8(dy + (long)row * N + ch * 8, dv);
+        load8(dy + (long)row * lddy + ch * 8, dv);
         const float4* w4 = reinterpret_cast<const float4*>(w + ch * 8);
         float4 wa = w4[0], wb = w4[1];
         float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
@@ -192,14 +196,14 @@ __global__ void reduce_rows_kernel(const float* __restrict__ part, float* __rest
 template <bool RMS>
 static void norm_fwd_dispatch(const bf16_t* x, const bf16_t* d, bf16_t* s_out, const float* w, const float* b,
                               bf16_t* y, float* mean, float* rstd, int M, int N, float eps, float w_offset,
-                              hipStream_t st) {
+                              long ldy, hipStream_t st) {
   const int nch = N / 8, ch = (nch + 63) / 64;
   dim3 grid(cdiv(M, 4)), block(256);
 #define MFT_NF(CHV)                                                                                        \
   if (d)                                                                                                   \
-    norm_fwd_kernel<CHV, RMS, true><<<grid, block, 0, st>>>(x, d, s_out, w, b, y, mean, rstd, M, N, eps, w_offset); \
+    norm_fwd_kernel<CHV, RMS, true><<<grid, block, 0, st>>>(x, d, s_out, w, b, y, mean, rstd, M, N, eps, w_offset, ldy); \
   else                                                                                                     \
-    norm_fwd_kernel<CHV, RMS, false><<<grid, block, 0, st>>>(x, d, s_out, w, b, y, mean, rstd, M, N, eps, w_offset);
+    norm_fwd_kernel<CHV, RMS, false><<<grid, block, 0, st>>>(x, d, s_out, w, b, y, mean, rstd, M, N, eps, w_offset, ldy);
   if (ch <= 1) { MFT_NF(1) }
   else if (ch <= 2) { MFT_NF(2) }
   else if (ch <= 4) { MFT_NF(4) }
@@ -210,7 +214,7 @@ static void norm_fwd_dispatch(const bf16_t* x, const bf16_t* d, bf16_t* s_out, c
 template <bool RMS>
 static void norm_bwd_dispatch(const bf16_t* x, const bf16_t* dy, const float* w, const float* mean, const float* rstd,
                               const bf16_t* dresid, bf16_t* dx, float* dw, float* db, float* work, int M, int N,
-                              float w_offset, int accumulate, hipStream_t st) {
+                              float w_offset, int accumulate, long lddy, hipStream_t st) {
   const int nch = N / 8, ch = (nch + 63) / 64;
   const bool wgrad = dw != nullptr;
   // with weight grads: a bounded grid so the partial buffer stays small (work: 2*nb*N floats)
@@ -221,9 +225,9 @@ static void norm_bwd_dispatch(const bf16_t* x, const bf16_t* dy, const float* w,
   dim3 grid(nb), block(256);
 #define MFT_NB(CHV)                                                                                           \
   if (wgrad)                                                                                                  \
-    norm_bwd_kernel<CHV, RMS, true><<<grid, block, shm, st>>>(x, dy, w, mean, rstd, dresid, dx, dw_part, db_part, M, N, w_offset); \
+    norm_bwd_kernel<CHV, RMS, true><<<grid, block, shm, st>>>(x, dy, w, mean, rstd, dresid, dx, dw_part, db_part, M, N, w_offset, lddy); \
   else                                                                                                        \
-    norm_bwd_kernel<CHV, RMS, false><<<grid, block, 0, st>>>(x, dy, w, mean, rstd, dresid, dx, dw_part, db_part, M, N, w_offset);
+    norm_bwd_kernel<CHV, RMS, false><<<grid, block, 0, st>>>(x, dy, w, mean, rstd, dresid, dx, dw_part, db_part, M, N, w_offset, lddy);
   if (ch <= 1) { MFT_NB(1) }
   else if (ch <= 2) { MFT_NB(2) }
   else if (ch <= 4) { MFT_NB(4) }
@@ -241,24 +245,28 @@ int norm_bwd_partial_blocks(int M) {
 }
 
 void layernorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, const float* b,
-                   bf16_t* y, float* mean, float* rstd, int M, int N, float eps, hipStream_t st) {
-  norm_fwd_dispatch<false>(x, resid_delta, resid_out, w, b, y, mean, rstd, M, N, eps, 0.f, st);
+                   bf16_t* y, float* mean, float* rstd, int M, int N, float eps, long ldy, hipStream_t st) {
+  norm_fwd_dispatch<false>(x, resid_delta, resid_out, w, b, y, mean, rstd, M, N, eps, 0.f, ldy > 0 ? ldy : N, st);
 }
 
 void rmsnorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, bf16_t* y,
-                 float* rstd, int M, int N, float eps, float w_offset, hipStream_t st) {
-  norm_fwd_dispatch<true>(x, resid_delta, resid_out, w, nullptr, y, nullptr, rstd, M, N, eps, w_offset, st);
+                 float* rstd, int M, int N, float eps, float w_offset, long ldy, hipStream_t st) {
+  norm_fwd_dispatch<true>(x, resid_delta, resid_out, w, nullptr, y, nullptr, rstd, M, N, eps, w_offset,
+                          ldy > 0 ? ldy : N, st);
 }
 
 void layernorm_bwd(const bf16_t* x, const bf16_t* dy, const float* w, const float* mean, const float* rstd,
                    const bf16_t* dresid, bf16_t* dx, float* dw, float* db, float* work, int M, int N, int accumulate,
-                   hipStream_t st) {
-  norm_bwd_dispatch<false>(x, dy, w, mean, rstd, dresid, dx, dw, db, work, M, N, 0.f, accumulate, st);
+                   long lddy, hipStream_t st) {
+  norm_bwd_dispatch<false>(x, dy, w, mean, rstd, dresid, dx, dw, db, work, M, N, 0.f, accumulate,
+                           lddy > 0 ? lddy : N, st);
 }
 
 void rmsnorm_bwd(const bf16_t* x, const bf16_t* dy, const float* w, const float* rstd, const bf16_t* dresid,
-                 bf16_t* dx, float* dw, float* work, int M, int N, float w_offset, int accumulate, hipStream_t st) {
-  norm_bwd_dispatch<true>(x, dy, w, nullptr, rstd, dresid, dx, dw, nullptr, work, M, N, w_offset, accumulate, st);
+                 bf16_t* dx, float* dw, float* work, int M, int N, float w_offset, int accumulate, long lddy,
+                 hipStream_t st) {
+  norm_bwd_dispatch<true>(x, dy, w, nullptr, rstd, dresid, dx, dw, nullptr, work, M, N, w_offset, accumulate,
+                          lddy > 0 ? lddy : N, st);
 }
 
 }  // namespace mft

@@ -142,6 +142,8 @@ class Gemma3Layer(nn.Module):
         self.gate_up_proj = Linear(H, 2 * cfg.intermediate_size, False, dtype, device)
         self.down_proj = Linear(cfg.intermediate_size, H, False, dtype, device)
         self.post_feedforward_layernorm = RMSNorm(H, eps, 1.0, device)
+        self.input_layernorm.set_consumer(self.qkv_proj)
+        self.pre_feedforward_layernorm.set_consumer(self.gate_up_proj)
         self.act = cfg.hidden_activation
         self.interleaved_rope = False
 

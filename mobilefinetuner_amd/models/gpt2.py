@@ -89,11 +89,16 @@ class GPT2Block(nn.Module):
         self.c_fc = Linear(C, 4 * C, True, dtype, device)
         self.mlp_proj = Linear(4 * C, C, True, dtype, device)
         self.H, self.D = cfg.n_head, cfg.head_dim
+        # norms write straight into their consumer's augmented LoRA input when it has one
+        self.ln_1.set_consumer(self.c_attn)
+        self.ln_2.set_consumer(self.c_fc)
 
     def attn(self, h, B, S, kv_lens):
         qkv = self.c_attn(h).view(B, S, 3, self.H, self.D)
-        o = Fx.flash_attention_qkvpacked(qkv, 1.0 / math.sqrt(self.D), True, 0, kv_lens)
-        return self.c_proj(o.view(B * S, self.H * self.D))
+        # c_proj with an active LoRA adapter takes the attention output widened to its augmented-K
+        # input (Linear.aug_cols); the attention kernel writes O straight into that buffer.
+        o = Fx.flash_attention_qkvpacked(qkv, 1.0 / math.sqrt(self.D), True, 0, kv_lens, self.c_proj.aug_cols())
+        return self.c_proj(o.reshape(B * S, o.shape[-1] if o.dim() == 3 else self.H * self.D))
 
     def mlp(self, h):
         return Fx.mlp_gelu(h, self.c_fc, self.mlp_proj)

@@ -60,10 +60,41 @@ class Linear(nn.Module):
     def clear_lora(self):
         self.lora_slices = []
         self._lora_params = nn.ParameterList()
+        self.__dict__.pop("_waug", None)
+
+    def aug_cols(self) -> int:
+        """Input width the producer should allocate for the augmented-K LoRA forward
+        (ops.functional._LoRALinearAug), or 0 when this Linear takes a plain input: no active
+        adapter, a trainable base weight, CPU tensors, in_features not a multiple of 32, or
+        MFT_LORA_AUG=0."""
+        import os
+        if not (self.lora_slices and self.lora_enabled) or self.weight.requires_grad or not self.weight.is_cuda:
+            return 0
+        if getattr(self.weight, "_mft_sharded", False):  # no resident W copy for offloaded weights
+            return 0
+        if self.in_features % 32 or os.environ.get("MFT_LORA_AUG", "1") == "0":
+            return 0
+        return Fx.lora_aug_cols(self.in_features, [sl.A.shape[0] for sl in self.lora_slices])
+
+    def _aug_weight(self, ka: int):
+        """[out, ka] bf16 buffer = [W | (s B^T per slice, written each forward) | 0]; W copied once
+        (dropped by merge_lora / clear_lora so a changed base weight is re-copied)."""
+        wa = self.__dict__.get("_waug")
+        wc = Fx.cw(self.weight)
+        if wa is None or wa.shape[1] != ka or wa.device != wc.device:
+            wa = torch.zeros(self.out_features, ka, dtype=wc.dtype, device=wc.device)
+            wa[:, : self.in_features].copy_(wc)
+            self.__dict__["_waug"] = wa
+        return wa
 
     def forward(self, x):
         if self.lora_slices and self.lora_enabled:
             sl = [(s.col0, s.ncols, s.A, s.B, self.lora_dropout, _salt(s.name)) for s in self.lora_slices]
+            if x.is_cuda and x.shape[-1] != self.in_features:
+                ka = self.aug_cols()
+                assert x.shape[-1] == ka, f"augmented input width {x.shape[-1]} != {ka}"
+                return Fx.lora_linear_aug(x, self.weight, self.bias, sl, self.lora_scale, self._aug_weight(ka),
+                                          self.training)
             return Fx.lora_linear(x, self.weight, self.bias, sl, self.lora_scale, self.training)
         return Fx.linear(x, self.weight, self.bias)
 
@@ -78,6 +109,7 @@ class Linear(nn.Module):
             if getattr(self.weight, "shadow", None) is not None:
                 self.weight.shadow.copy_(self.weight.data.to(self.weight.shadow.dtype))
         Fx.drop_weight_t(self.weight)
+        self.__dict__.pop("_waug", None)
 
     def extra_repr(self):
         return f"in={self.in_features}, out={self.out_features}, lora_slices={len(self.lora_slices)}"
@@ -91,12 +123,22 @@ class LayerNorm(nn.Module):
         self.weight._mft_fp32_compute = True
         self.bias._mft_fp32_compute = True
         self.eps = eps
+        self.__dict__["_consumer"] = None  # Linear fed by this norm (not a submodule)
+
+    def set_consumer(self, lin):
+        """Register the Linear this norm feeds so the output can be widened for its LoRA
+        augmented-K input (Linear.aug_cols)."""
+        self.__dict__["_consumer"] = lin
+
+    def _out_cols(self):
+        c = self.__dict__["_consumer"]
+        return c.aug_cols() if c is not None else 0
 
     def forward(self, x):
-        return Fx.layer_norm(x, self.weight, self.bias, self.eps)
+        return Fx.layer_norm(x, self.weight, self.bias, self.eps, self._out_cols())
 
     def add_forward(self, x, delta):
-        return Fx.add_layer_norm(x, delta, self.weight, self.bias, self.eps)
+        return Fx.add_layer_norm(x, delta, self.weight, self.bias, self.eps, self._out_cols())
 
 
 class RMSNorm(nn.Module):
@@ -107,9 +149,17 @@ class RMSNorm(nn.Module):
         self.weight = nn.Parameter(torch.zeros(n, device=device), requires_grad=False)
         self.weight._mft_fp32_compute = True
         self.eps, self.offset = eps, offset
+        self.__dict__["_consumer"] = None
+
+    def set_consumer(self, lin):
+        self.__dict__["_consumer"] = lin
+
+    def _out_cols(self):
+        c = self.__dict__["_consumer"]
+        return c.aug_cols() if c is not None else 0
 
     def forward(self, x):
-        return Fx.rms_norm(x, self.weight, self.eps, self.offset)
+        return Fx.rms_norm(x, self.weight, self.eps, self.offset, self._out_cols())
 
     def add_forward(self, x, delta):
-        return Fx.add_rms_norm(x, delta, self.weight, self.eps, self.offset)
+        return Fx.add_rms_norm(x, delta, self.weight, self.eps, self.offset, self._out_cols())

@@ -80,25 +80,26 @@ def _grad_buf(p):
 # ---------------------------------------------------------------- normalisation
 class _Norm(Function):
     @staticmethod
-    def forward(ctx, x, delta, w, b, eps, rms, offset):
+    def forward(ctx, x, delta, w, b, eps, rms, offset, out_cols):
         C = native()
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         d2 = delta.reshape(-1, shape[-1]).contiguous() if delta is not None else None
         wc = cw(w).float() if cw(w).dtype != torch.float32 else cw(w)
         if rms:
-            y, s, rstd = C.rmsnorm_fwd(x2, d2, wc, eps, offset)
+            y, s, rstd = C.rmsnorm_fwd(x2, d2, wc, eps, offset, out_cols)
             mean = None
         else:
             bc = cw(b).float() if cw(b).dtype != torch.float32 else cw(b)
-            y, s, mean, rstd = C.layernorm_fwd(x2, d2, wc, bc, eps)
+            y, s, mean, rstd = C.layernorm_fwd(x2, d2, wc, bc, eps, out_cols)
         xs = s if d2 is not None else x2
         ctx.save_for_backward(xs, wc, mean if mean is not None else rstd, rstd)
         ctx.params = (w, b)
         ctx.rms, ctx.offset, ctx.has_delta, ctx.shape = rms, offset, d2 is not None, shape
+        yshape = (*shape[:-1], y.shape[-1])  # wider than x when out_cols > N (appended columns)
         if d2 is not None:
-            return s.view(shape), y.view(shape)
-        return y.view(shape)
+            return s.view(shape), y.view(yshape)
+        return y.view(yshape)
 
     @staticmethod
     def backward(ctx, *grads):
@@ -110,7 +111,12 @@ class _Norm(Function):
             ds, dy = grads
         else:
             ds, dy = None, grads[0]
-        dy2 = dy.reshape(-1, N).contiguous() if dy is not None else torch.zeros_like(xs)
+        if dy is not None:
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            if dy2.stride(-1) != 1 or dy2.stride(0) % 8:
+                dy2 = dy2.contiguous()
+        else:
+            dy2 = torch.zeros_like(xs)
         if ds is not None and dy is None:
             dy2 = torch.zeros_like(xs)
         ds2 = ds.reshape(-1, N).contiguous() if ds is not None else None
@@ -134,34 +140,37 @@ class _Norm(Function):
         dx = dx.view(ctx.shape)
         gwr = gw.to(w.dtype).view_as(w) if gw is not None else None
         gbr = gb.to(b.dtype).view_as(b) if gb is not None else None
-        return dx, (dx if ctx.has_delta else None), gwr, gbr, None, None, None
+        return dx, (dx if ctx.has_delta else None), gwr, gbr, None, None, None, None
 
 
-def layer_norm(x, w, b, eps=1e-5):
+# out_cols > width: the GPU output is allocated [.., out_cols] with the normalised values in the first
+# `width` columns and the rest left for the consumer (a LoRA Linear appends its rank-r projections
+# there, _LoRALinearAug).  CPU paths ignore it.
+def layer_norm(x, w, b, eps=1e-5, out_cols=0):
     if not x.is_cuda:
         return ref.layer_norm(x, rw(w), rw(b), eps).to(x.dtype)
-    return _Norm.apply(x, None, w, b, eps, False, 0.0)
+    return _Norm.apply(x, None, w, b, eps, False, 0.0, int(out_cols))
 
 
-def add_layer_norm(x, delta, w, b, eps=1e-5):
+def add_layer_norm(x, delta, w, b, eps=1e-5, out_cols=0):
     """s = x + delta; y = LayerNorm(s)  -> (s, y) (fused residual + norm)."""
     if not x.is_cuda:
         s = x + delta
         return s, ref.layer_norm(s, rw(w), rw(b), eps).to(x.dtype)
-    return _Norm.apply(x, delta, w, b, eps, False, 0.0)
+    return _Norm.apply(x, delta, w, b, eps, False, 0.0, int(out_cols))
 
 
-def rms_norm(x, w, eps=1e-6, offset=1.0):
+def rms_norm(x, w, eps=1e-6, offset=1.0, out_cols=0):
     if not x.is_cuda:
         return ref.rms_norm(x, rw(w), eps, offset).to(x.dtype)
-    return _Norm.apply(x, None, w, None, eps, True, offset)
+    return _Norm.apply(x, None, w, None, eps, True, offset, int(out_cols))
 
 
-def add_rms_norm(x, delta, w, eps=1e-6, offset=1.0):
+def add_rms_norm(x, delta, w, eps=1e-6, offset=1.0, out_cols=0):
     if not x.is_cuda:
         s = x + delta
         return s, ref.rms_norm(s, rw(w), eps, offset).to(x.dtype)
-    return _Norm.apply(x, delta, w, None, eps, True, offset)
+    return _Norm.apply(x, delta, w, None, eps, True, offset, int(out_cols))
 
 
 # ---------------------------------------------------------------- activations
@@ -256,7 +265,7 @@ def embedding(ids, wte, wpe=None, scale=1.0):
 class _FlashAttn(Function):
     @staticmethod
     def forward(ctx, q, k, v, scale, causal, window, kv_lens):
-        o, lse = native().attn_fwd(q, k, v, scale, causal, window, kv_lens)
+        o, lse, _ = native().attn_fwd(q, k, v, scale, causal, window, kv_lens, 0)
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.cfg = (scale, causal, window, kv_lens)
         return o
@@ -276,21 +285,27 @@ class _FlashAttnPacked(Function):
     """qkv [B,S,3,H,D] packed GEMM output consumed in place; backward writes one packed dqkv."""
 
     @staticmethod
-    def forward(ctx, qkv, scale, causal, window, kv_lens):
+    def forward(ctx, qkv, scale, causal, window, kv_lens, out_cols):
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-        o, lse = native().attn_fwd(q, k, v, scale, causal, window, kv_lens)
+        o_full, lse, o = native().attn_fwd(q, k, v, scale, causal, window, kv_lens, out_cols)
         ctx.save_for_backward(qkv, o, lse)
         ctx.cfg = (scale, causal, window, kv_lens)
-        return o
+        ctx.wide = out_cols > 0 and o_full.dim() == 3
+        return o_full
 
     @staticmethod
     def backward(ctx, do):
         qkv, o, lse = ctx.saved_tensors
         scale, causal, window, kv_lens = ctx.cfg
         dqkv = torch.empty_like(qkv)
-        native().attn_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, do.contiguous(), lse, dqkv[:, :, 0],
+        B, S, _, H, D = qkv.shape
+        if ctx.wide:  # [B, S, out_cols] gradient of the widened output: O's columns come first
+            do = do[..., :H * D].view(B, S, H, D)
+        if do.stride(-1) != 1:
+            do = do.contiguous()
+        native().attn_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, do, lse, dqkv[:, :, 0],
                           dqkv[:, :, 1], dqkv[:, :, 2], scale, causal, window, kv_lens)
-        return dqkv, None, None, None, None
+        return dqkv, None, None, None, None, None
 
 
 def flash_attention(q, k, v, scale=None, causal=True, window=0, kv_lens=None):
@@ -302,12 +317,16 @@ def flash_attention(q, k, v, scale=None, causal=True, window=0, kv_lens=None):
     return _FlashAttn.apply(q, k, v, float(scale), bool(causal), int(window or 0), kv_lens)
 
 
-def flash_attention_qkvpacked(qkv, scale=None, causal=True, window=0, kv_lens=None):
+def flash_attention_qkvpacked(qkv, scale=None, causal=True, window=0, kv_lens=None, out_cols=0):
+    """qkv [B,S,3,H,D] -> o [B,S,H,D]; with out_cols > H*D (GPU) -> [B,S,out_cols] whose first H*D
+    columns hold O (room for the consumer's appended LoRA columns, _LoRALinearAug)."""
     if scale is None:
         scale = 1.0 / math.sqrt(qkv.shape[-1])
     if not qkv.is_cuda:
         return ref.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], scale, causal, window, kv_lens)[0].to(qkv.dtype).contiguous()
-    return _FlashAttnPacked.apply(qkv, float(scale), bool(causal), int(window or 0), kv_lens)
+    H, D = qkv.shape[3], qkv.shape[4]
+    oc = int(out_cols) if out_cols and out_cols > H * D else 0
+    return _FlashAttnPacked.apply(qkv, float(scale), bool(causal), int(window or 0), kv_lens, oc)
 
 
 # ---------------------------------------------------------------- fused per-head RMSNorm + RoPE
@@ -567,6 +586,124 @@ class _LoRALinear(Function):
         if dx is not None:
             dx = dx.view(ctx.shape)
         return (dx, None, None, None, None, *grads)
+
+
+class _LoRALinearAug(Function):
+    """LoRA Linear whose forward is ONE GEMM over an augmented K dimension:
+
+        y = [x | u_1 .. u_n | 0] . [W | s B_1^T .. s B_n^T | 0]^T + b,   u_i = dropout(x) A_i^T
+
+    The producer of x (LayerNorm / attention) wrote it into the first K columns of a wider buffer
+    ``xa`` [M, Ka] and ZEROED columns [K, Ka) (contract: padding meets zero weights, and 0 * NaN from
+    uninitialised memory would not be 0); the rank-r projections u_i are written into the appended
+    columns by lora_rowdot,
+    and ``waug`` [N, Ka] (owned by the Linear) carries W once plus s B_i^T, refreshed every call, in
+    each slice's rows.  This removes the per-slice rank-r update pass over y [M, N] (lora_update)
+    from the forward: the rank-r work rides in the GEMM's K loop (Ka = K + 64 for r <= 64 total).
+    Backward: dx = dy W (W part of waug) + mask * (v A) written straight into the wide grad
+    buffer; dA/dB by lora_wgrad as in _LoRALinear.  Reference: LoRALinear, nn/lora_linear.h:17-97."""
+
+    @staticmethod
+    def forward(ctx, xa, w, b, s, slices, K, waug, *ab):
+        C = native()
+        shape = xa.shape
+        Ka = shape[-1]
+        xa2 = xa.reshape(-1, Ka)
+        x2 = xa2[:, :K]
+        ctr = dropout_counter(xa.device)
+        off = K
+        for i, (c0, n, dp, salt) in enumerate(slices):
+            Ac, Bc = cw(ab[2 * i]), cw(ab[2 * i + 1])
+            R = Ac.shape[0]
+            C.lora_rowdot(x2, Ac, xa2[:, off:off + R], 1.0, dp, salt, ctr)  # u_i -> appended columns
+            torch.mul(Bc.t(), s, out=waug[c0:c0 + n, off:off + R])          # s B_i^T -> W' rows of slice i
+            off += R
+        bc = cw(b)
+        y = torch.addmm(bc, xa2, waug.t()) if bc is not None else torch.mm(xa2, waug.t())
+        ctx.save_for_backward(xa)  # the input itself (a no-grad view of it must not be saved)
+        ctx.params = ab
+        ctx.slices, ctx.waug, ctx.K = slices, waug, K
+        ctx.s, ctx.shape = float(s), shape
+        return y.view(*shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        (xa,) = ctx.saved_tensors
+        ab, s, K = ctx.params, ctx.s, ctx.K
+        xa2 = xa.reshape(-1, xa.shape[-1])
+        M, Ka = xa2.shape
+        x2 = xa2[:, :K]
+        N = ctx.waug.shape[0]
+        dy2 = dy.reshape(-1, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dxa = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2, ctx.waug[:, :K])
+            # columns [K, Ka) of the input gradient are never read (the producers' backward reads
+            # only their own K columns through the row stride), so they are left unwritten
+            dxa = torch.empty(M, Ka, device=dy.device, dtype=dy.dtype)
+        grads = []
+        ctr = dropout_counter(dy.device)
+        off = K
+        first = True
+        for i, (c0, n, dp, salt) in enumerate(ctx.slices):
+            A, B = ab[2 * i], ab[2 * i + 1]
+            Ac, Bc = cw(A), cw(B)
+            R = Ac.shape[0]
+            dys = dy2[:, c0:c0 + n]
+            v = torch.empty(M, R, device=dy.device, dtype=dy.dtype)
+            C.lora_rowdot(dys, Bc, v, s, 0.0, 0, None)  # v = s dy B^T
+            if dxa is not None:
+                # dx (+)= mask * (v A); the first slice also moves dx into the wide gradient buffer
+                C.lora_update(dx if first else dxa[:, :K], v, Ac, dxa[:, :K], 1.0, dp, salt, ctr)
+                first = False
+            gA = gB = None
+            if _needs(A):
+                buf = _grad_buf(A)
+                tgt = buf if buf is not None else torch.zeros(R, K, device=dy.device)
+                C.lora_wgrad(x2, v, tgt, 1, K, 1.0, dp, salt, ctr)
+                if buf is not None:
+                    grad_ready(A)
+                else:
+                    gA = tgt
+            if _needs(B):
+                buf = _grad_buf(B)
+                tgt = buf if buf is not None else torch.zeros(R, n, device=dy.device)
+                C.lora_wgrad(dys, xa2[:, off:off + R], tgt, 1, n, s, 0.0, 0, None)  # dB += s u^T dy
+                if buf is not None:
+                    grad_ready(B)
+                else:
+                    gB = tgt
+            grads += [gA, gB]
+            off += R
+        if dxa is not None and first:  # no slices (cannot happen via Linear, kept for safety)
+            dxa[:, :K].copy_(dx)
+        if dxa is not None:
+            dxa = dxa.view(ctx.shape)
+        return (dxa, None, None, None, None, None, None, *grads)
+
+
+def lora_aug_cols(in_features: int, ranks) -> int:
+    """Width of the augmented LoRA input [x | u_1..u_n | 0]: K + sum(r), rounded up to 64 (hipBLASLt
+    measured slower at K + 8 .. K + 32 than at K + 64 on gfx950, scripts/probe_kpad.py)."""
+    return (in_features + sum(ranks) + 63) // 64 * 64
+
+
+def lora_linear_aug(xa, w, b, slices, scale, waug, training: bool = True):
+    """xa [.., Ka] holds x in its first w.shape[1] columns; see _LoRALinearAug."""
+    K = w.shape[1]
+    meta, ab = [], []
+    for sl in slices:
+        c0, n, A, B = sl[:4]
+        p = float(sl[4]) if len(sl) > 4 else 0.0
+        salt = int(sl[5]) if len(sl) > 5 else 0
+        if not (training and torch.is_grad_enabled()):
+            p = 0.0
+        meta.append((int(c0), int(n), p, salt & 0xFFFFFFFF))
+        ab += [A, B]
+    return _LoRALinearAug.apply(xa, w, b, float(scale), tuple(meta), int(K), waug, *ab)
 
 
 def lora_linear(x, w, b, slices, scale, training: bool = True):

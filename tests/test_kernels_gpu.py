@@ -132,6 +132,56 @@ def test_gemm_mfma(M, K, N, nn, bm):
     _close(acc, 1 + 2 * ref_, 0.05, 0.01, msg="gemm f32 acc")
 
 
+@pytest.mark.parametrize("dropout", [0.0, 0.2])
+def test_lora_augmented_k_matches_plain(dropout):
+    """_LoRALinearAug ([x | u] . [W | sB^T] single GEMM) == _LoRALinear (GEMM + rank-r update)."""
+    from mobilefinetuner_amd.models.layers import Linear
+    from mobilefinetuner_amd.ops import functional as Fx
+    from mobilefinetuner_amd.utils.params import FlatParams
+    M, K, N = 300, 256, 384
+    lin = Linear(K, N, device=DEV)
+    with torch.no_grad():
+        lin.weight.copy_(torch.randn(N, K) * 0.05)
+        lin.bias.copy_(torch.randn(N) * 0.1)
+    for i, (c0, n) in enumerate([(0, 128), (128, 128), (256, 128)]):
+        A, B = lin.add_lora(c0, n, 8, 2.0, torch.randn(8, K) * 0.05, name=f"s{i}")
+        with torch.no_grad():
+            B.copy_(torch.randn_like(B) * 0.05)
+    lin.lora_dropout = dropout
+    flat = FlatParams([(f"p{i}", p) for i, p in enumerate(lin._lora_params)], DEV)
+    ka = lin.aug_cols()
+    assert ka == Fx.lora_aug_cols(K, [8, 8, 8]) == 320
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    g = torch.randn(M, N, device=DEV).bfloat16()
+    ctr = Fx.dropout_counter(DEV)
+    outs = []
+    for aug in (False, True):
+        flat.zero_grad()
+        if aug:
+            xa = torch.zeros(M, ka, device=DEV).bfloat16()  # producers hand over zeroed padding
+            xa[:, :K] = x
+            xa.requires_grad_()
+            y = lin(xa)
+        else:
+            xa = x.clone().requires_grad_()
+            y = lin(xa)
+        (y.float() * g.float()).sum().backward()
+        outs.append((y.float(), xa.grad[:, :K].float(), flat.grad.clone()))
+    (y0, dx0, gw0), (y1, dx1, gw1) = outs
+    assert torch.isfinite(y1).all() and torch.isfinite(dx1).all()
+    # producers honour the zero-padding contract even on recycled (garbage) memory
+    from mobilefinetuner_amd.ops import functional as F2
+    junk = torch.full((M, ka), float("nan"), device=DEV).bfloat16()
+    del junk
+    xn = F2.layer_norm(torch.randn(M, K, device=DEV).bfloat16(), torch.ones(K, device=DEV),
+                       torch.zeros(K, device=DEV), 1e-5, ka)
+    assert xn.shape[-1] == ka and (xn[:, K:] == 0).all()
+    _close(y1, y0, 0.03, 0.01, msg="aug y")
+    _close(dx1, dx0, 0.03, 0.01, msg="aug dx")
+    _close(gw1, gw0, 0.05, 0.02, msg="aug lora grads")
+    del ctr
+
+
 @pytest.mark.parametrize("trainable", [False, True])
 def test_fused_mlp_gelu_epilogues(trainable, monkeypatch):
     """gemm.hip BIAS_GELU / DGELU epilogue MLP vs the fp32 reference (tanh GELU)."""
@@ -209,7 +259,7 @@ def test_flash_attention_lse_and_spike():
     v = torch.randn(B, S, H, D, device=DEV)
     k[0, 200] *= 30.0
     q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
-    o, lse = native().attn_fwd(q, k, v, 0.125, True, 0, None)
+    o, lse, _ = native().attn_fwd(q, k, v, 0.125, True, 0, None, 0)
     orf, lser = _attn_ref(q.float(), k.float(), v.float(), 0.125, True, 0)
     _close(o, orf, 0.03, msg="spike o")
     _close(lse, lser, 0.05, msg="spike lse")
@@ -229,6 +279,11 @@ def test_flash_attention_packed_and_kvlens():
     # rows >= kv_len of batch 1 still attend to keys < 77 (causal + padding)
     _close(o, orf, 0.03, msg="packed o")
     _close(qkv.grad, r.grad, 0.06, 0.02, msg="packed dqkv")
+    # widened output for an augmented-K consumer: O in the first H*D columns, zeros after
+    with torch.no_grad():
+        ow = Fx.flash_attention_qkvpacked(qkv, 0.125, True, 0, kv, out_cols=H * D + 64)
+    assert ow.shape == (B, S, H * D + 64)
+    assert torch.equal(ow[..., :H * D], o.reshape(B, S, H * D)) and (ow[..., H * D:] == 0).all()
 
 
 @pytest.mark.parametrize("V,C", [(50257, 768), (1000, 128)])
