@@ -420,7 +420,8 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
   a.bias = bias.has_value() ? bp(*bias) : nullptr;
   a.aux = X.defined() ? bp(X) : nullptr; a.ldaux = X.defined() ? X.stride(0) : 0;
   a.M = M; a.N = N; a.K = K; a.alpha = (float)alpha;
-  mft::gemm(a, b_nn, (int)epi, (int)bm, stream());
+  if (bm == 8 && !b_nn) mft::gemm8(a, (int)epi, stream());  // cfg 8: 8-phase pipelined 256x256 NT kernel
+  else mft::gemm(a, b_nn, (int)epi, (int)bm, stream());
   return {C, X};
 }
 

@@ -69,6 +69,8 @@ struct GemmArgs {
 bool gemm_supported(int M, int N, int K);
 // cfg: tile configuration (gemm.hip launch_e): 0 = 256x256, 1 = 128x256, 2 = 128x128, 3 = 256x128
 void gemm(const GemmArgs& g, bool b_nn, int epi, int cfg, hipStream_t st);
+// 256x256 8-phase pipelined NT GEMM (gemm8.hip); same epilogues
+void gemm8(const GemmArgs& g, int epi, hipStream_t st);
 
 // ---------------------------------------------------------------- activations (act.hip)
 void gelu_fwd(const bf16_t* x, bf16_t* y, long n, hipStream_t st);

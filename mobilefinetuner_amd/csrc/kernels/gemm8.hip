@@ -1,0 +1,320 @@
+// 256 x 256 x 64 bf16 MFMA GEMM with an 8-phase software pipeline (gfx950), NT operand layout:
+//
+//   C[M, N] = epi(alpha * A[M, K] . B[N, K]^T)          A, B row-major, K contiguous
+//
+// (data-gradient GEMMs use the same layout through a transposed weight copy, ops.functional
+// weight_t).  Structure after the CDNA HIP guide §5 "256² 8-phase template" (T1 XCD remap, T2 LDS
+// XOR swizzle, T3+T4 8-phase interleave with counted vmcnt, T5 setprio):
+//
+//   * 8 waves; each 64-wide ds_read/MFMA phase works on ONE 128 x 128 quadrant of the block tile
+//     (every wave a 64 x 32 piece of it: 4 x 2 fragments x 2 k-steps = 16 MFMAs).  Quadrants are
+//     visited (A0,B0) (A0,B1) (A1,B1) (A1,B0) so consecutive phases reuse either the A or the B
+//     fragments in registers.  A K-tile = 4 phases; an iteration = 2 K-tiles (even/odd LDS
+//     buffer) = 8 phases.
+//   * LDS: 2 buffers x {A0, A1, B0, B1} half-tiles of 128 x 64 bf16 (16 KB each) = 128 KB, filled
+//     by global_load_lds_dwordx4 (2 per thread per half-tile) straight from HBM/L2; the 16-B chunk
+//     index is XOR-swizzled with (row & 7) on the SOURCE address so the lane-linear LDS image reads
+//     back conflict-light with ds_read_b128.
+//   * Each half-tile is restaged ONE phase after its last read (every phase ends its reads with
+//     lgkmcnt(0) before the barrier), one half-tile per phase, so the next K-tile of a buffer streams
+//     in while the other buffer is multiplied; the waits are counted (vmcnt(4): two half-tiles stay
+//     in flight across the barrier), never vmcnt(0) inside the loop, and the barriers are raw
+//     s_barrier (a __syncthreads() would drain the LDS-DMA queue).
+//
+// Half-tile staging schedule (phase -> half-tile, K-tile of iteration i):
+//   1: O.A1 (2i+1)  2: O.B0 (2i+1)  3: E.A0 (2i+2)  4: E.B1 (2i+2)
+//   5: E.A1 (2i+2)  6: E.B0 (2i+2)  7: O.A0 (2i+3)  8: O.B1 (2i+3)
+// with vmcnt(4) before the barriers of phases 4 (retires O for phases 5-8) and 8 (retires E for
+// the next phases 1-4).  Loads of K-tiles past the end are clamped onto the last tile (harmless
+// re-reads) so every wave issues the same count and the counted waits stay exact.
+#include "mfma.h"
+#include "kernels.h"
+
+namespace mft {
+
+namespace {
+
+constexpr int kHalf = 128 * 64;  // elements in a half-tile
+
+typedef __attribute__((address_space(3))) void lds_void8;
+typedef const __attribute__((address_space(1))) void g_void8;
+
+__device__ __forceinline__ void glds16_8(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((g_void8*)src, (lds_void8*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// stage one 128 x 64 half-tile: rows r0.. of src (clamped to rmax-1), columns k0..k0+63
+__device__ __forceinline__ void stage_half(bf16_t* lds, const bf16_t* src, long ld, int r0, int rmax, int k0) {
+  const int tid = threadIdx.x, w = tid >> 6;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int c = t * 512 + tid;
+    const int r = c >> 3, s = c & 7;
+    const int gr = min(r0 + r, rmax - 1);
+    glds16_8(src + (long)gr * ld + k0 + ((s ^ (r & 7)) << 3), lds + (t * 512 + w * 64) * 8);
+  }
+}
+
+// fragment of a swizzled half-tile: lane holds T[r0 + (l&15)][8*kc + 8*(l>>4) + j]
+__device__ __forceinline__ bf16x8_t frag8(const bf16_t* t, int r0, int kc) {
+  const int l = threadIdx.x & 63;
+  const int r = r0 + (l & 15), q = kc + (l >> 4);
+  return *reinterpret_cast<const bf16x8_t*>(t + r * 64 + ((q ^ (r & 7)) << 3));
+}
+
+}  // namespace
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  // buffer b (0 = even, 1 = odd): half-tiles A0, A1, B0, B1 at smem + (b * 4 + h) * kHalf
+  const int tiles_n = (g.N + 255) / 256;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / tiles_n) * 256, n0 = (tile % tiles_n) * 256;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 2, wn = w & 3;  // wave's 64 x 32 piece inside each 128 x 128 quadrant
+  const int nk = g.K / 64;
+  const int last = nk - 1;
+
+  auto half_ptr = [&](int buf, int h) { return smem + (buf * 4 + h) * kHalf; };
+  // h: 0 = A0, 1 = A1, 2 = B0, 3 = B1
+  auto stage = [&](int buf, int h, int kt) {
+    const int k0 = min(kt, last) * 64;
+    if (h < 2) stage_half(half_ptr(buf, h), g.A, g.lda, m0 + h * 128, g.M, k0);
+    else stage_half(half_ptr(buf, h), g.B, g.ldb, n0 + (h - 2) * 128, g.N, k0);
+  };
+
+  f32x4_t acc[4][4][2];  // [quadrant][i][j]
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[q][i][j] = zero4();
+
+  bf16x8_t af[4][2], bfr[2][2];
+  auto read_a = [&](int buf, int ah) {
+    const bf16_t* t = half_ptr(buf, ah);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag8(t, wm * 64 + i * 16, ks * 4);
+  };
+  auto read_b = [&](int buf, int bh) {
+    const bf16_t* t = half_ptr(buf, 2 + bh);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag8(t, wn * 32 + j * 16, ks * 4);
+  };
+  auto mma = [&](int q) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[q][i][j] = mfma16(af[i][ks], bfr[j][ks], acc[q][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: E <- K-tile 0 (all halves), O <- K-tile 1 (A0, B1); retire E
+  stage(0, 0, 0);
+  stage(0, 3, 0);
+  stage(0, 1, 0);
+  stage(0, 2, 0);
+  stage(1, 0, 1);
+  stage(1, 3, 1);
+  vm_wait<4>();
+  raw_barrier();
+
+  for (int kt = 0; kt < nk; kt += 2) {
+    const bool odd_ok = kt + 1 < nk;  // the odd K-tile of this iteration exists
+    // ---- phases 1-4: even buffer, K-tile kt
+    // phase 1: quadrant (A0, B0); stage O.A1 (kt+1)
+    read_a(0, 0);
+    read_b(0, 0);
+    stage(1, 1, kt + 1);
+    lgkm_wait0();
+    raw_barrier();
+    mma(0);
+    raw_barrier();
+    // phase 2: (A0, B1); stage O.B0 (kt+1)
+    read_b(0, 1);
+    stage(1, 2, kt + 1);
+    lgkm_wait0();
+    raw_barrier();
+    mma(1);
+    raw_barrier();
+    // phase 3: (A1, B1); stage E.A0 (kt+2)
+    read_a(0, 1);
+    stage(0, 0, kt + 2);
+    lgkm_wait0();
+    raw_barrier();
+    mma(2);
+    raw_barrier();
+    // phase 4: (A1, B0); stage E.B1 (kt+2); retire the odd buffer
+    read_b(0, 0);
+    stage(0, 3, kt + 2);
+    lgkm_wait0();
+    vm_wait<4>();
+    raw_barrier();
+    mma(3);
+    raw_barrier();
+    // ---- phases 5-8: odd buffer, K-tile kt+1 (MFMAs skipped past the end; loads/waits stay uniform)
+    // phase 5: (A0, B0); stage E.A1 (kt+2)
+    read_a(1, 0);
+    read_b(1, 0);
+    stage(0, 1, kt + 2);
+    lgkm_wait0();
+    raw_barrier();
+    if (odd_ok) mma(0);
+    raw_barrier();
+    // phase 6: (A0, B1); stage E.B0 (kt+2)
+    read_b(1, 1);
+    stage(0, 2, kt + 2);
+    lgkm_wait0();
+    raw_barrier();
+    if (odd_ok) mma(1);
+    raw_barrier();
+    // phase 7: (A1, B1); stage O.A0 (kt+3)
+    read_a(1, 1);
+    stage(1, 0, kt + 3);
+    lgkm_wait0();
+    raw_barrier();
+    if (odd_ok) mma(2);
+    raw_barrier();
+    // phase 8: (A1, B0); stage O.B1 (kt+3); retire the even buffer
+    read_b(1, 0);
+    stage(1, 3, kt + 3);
+    lgkm_wait0();
+    vm_wait<4>();
+    raw_barrier();
+    if (odd_ok) mma(3);
+    raw_barrier();
+  }
+  vm_wait<0>();  // drain the clamped tail prefetches before LDS is reused by the epilogue
+  raw_barrier();
+
+  // ------------------------------------------------------------------ epilogue
+  // per wave and quadrant: a 64 x 32 piece staged through LDS (stride 40) -> 16-B row stores
+  constexpr int LDT = 40;
+  bf16_t* T = smem + w * 64 * LDT;
+  auto sync_wave = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int qa = (q == 2 || q == 3) ? 1 : 0, qb = (q == 1 || q == 2) ? 1 : 0;
+    const int rbase = m0 + qa * 128 + wm * 64, cbase = n0 + qb * 128 + wn * 32;
+    auto to_global = [&](bf16_t* dst, long ldd) {
+      sync_wave();
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {  // 64 rows x 4 chunks = 256 pieces / 64 lanes
+        const int c = it * 64 + lane;
+        const int r = c >> 2, ch = c & 3;
+        const int row = rbase + r, col = cbase + ch * 8;
+        if (row < g.M && col < g.N)
+          *reinterpret_cast<u16x8_t*>(dst + (long)row * ldd + col) = *reinterpret_cast<const u16x8_t*>(T + r * LDT + ch * 8);
+      }
+      sync_wave();
+    };
+    if constexpr (EPI == GEMM_EPI_F32ACC) {
+      float* C = reinterpret_cast<float*>(g.C);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = rbase + i * 16 + 4 * (lane >> 4) + r, col = cbase + j * 16 + (lane & 15);
+            if (row < g.M && col < g.N) C[(long)row * g.ldc + col] += g.alpha * acc[q][i][j][r];
+          }
+      continue;
+    }
+    if constexpr (EPI == GEMM_EPI_DGELU) {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int c = it * 64 + lane;
+        const int r = c >> 2, ch = c & 3;
+        const int row = min(rbase + r, g.M - 1), col = min(cbase + ch * 8, g.N - 8);
+        *reinterpret_cast<u16x8_t*>(T + r * LDT + ch * 8) = *reinterpret_cast<const u16x8_t*>(g.aux + (long)row * g.ldaux + col);
+      }
+      sync_wave();
+    }
+    float bias_v[2] = {0.f, 0.f};
+    if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bias_v[j] = bf2f(g.bias[min(cbase + j * 16 + (lane & 15), g.N - 1)]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int tr = i * 16 + 4 * (lane >> 4) + r, tc = j * 16 + (lane & 15);
+          float v = acc[q][i][j][r] * g.alpha + bias_v[j];
+          if constexpr (EPI == GEMM_EPI_DGELU) v *= gelu_tanh_grad(bf2f(T[tr * LDT + tc]));
+          if constexpr (EPI == GEMM_EPI_BIAS_GELU) acc[q][i][j][r] = v;
+          T[tr * LDT + tc] = f2bf(v);
+        }
+    if constexpr (EPI == GEMM_EPI_BIAS_GELU) {
+      to_global(g.aux, g.ldaux);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int tr = i * 16 + 4 * (lane >> 4) + r, tc = j * 16 + (lane & 15);
+            T[tr * LDT + tc] = f2bf(gelu_tanh(acc[q][i][j][r]));
+          }
+    }
+    to_global(reinterpret_cast<bf16_t*>(g.C), g.ldc);
+  }
+}
+
+template <int EPI>
+static void launch8(const GemmArgs& g, hipStream_t st) {
+  constexpr size_t shm = sizeof(bf16_t) * 8 * kHalf;  // 128 KB
+  static bool attr = false;
+  if (!attr) {
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    attr = true;
+  }
+  const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+  gemm8_kernel<EPI><<<tiles, 512, shm, st>>>(g);
+}
+
+void gemm8(const GemmArgs& g, int epi, hipStream_t st) {
+  if (!gemm_supported(g.M, g.N, g.K)) {
+    fprintf(stderr, "mft::gemm8: unsupported shape M=%d N=%d K=%d\n", g.M, g.N, g.K);
+    abort();
+  }
+  switch (epi) {
+    case GEMM_EPI_NONE: launch8<GEMM_EPI_NONE>(g, st); break;
+    case GEMM_EPI_BIAS: launch8<GEMM_EPI_BIAS>(g, st); break;
+    case GEMM_EPI_BIAS_GELU: launch8<GEMM_EPI_BIAS_GELU>(g, st); break;
+    case GEMM_EPI_DGELU: launch8<GEMM_EPI_DGELU>(g, st); break;
+    case GEMM_EPI_F32ACC: launch8<GEMM_EPI_F32ACC>(g, st); break;
+    default: fprintf(stderr, "mft::gemm8: bad epilogue %d\n", epi); abort();
+  }
+}
+
+}  // namespace mft

@@ -453,7 +453,7 @@ class _MLPGelu(Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         w1c, b1c, w2c, b2c = cw(w1), cw(b1), cw(w2), cw(b2)
-        h, pre = C.gemm(x2, w1c, False, GEMM_EPI_BIAS_GELU, b1c, None, 1.0, 0, None)
+        h, pre = C.gemm(x2, w1c, False, GEMM_EPI_BIAS_GELU, b1c, None, 1.0, 8, None)
         y = torch.addmm(b2c, h, w2c.t())
         ctx.save_for_backward(x2 if _needs(w1) else None, pre, h if _needs(w2) else None)
         ctx.params = (w1, b1, w2, b2)
@@ -470,7 +470,7 @@ class _MLPGelu(Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dpre = C.gemm(dy2, weight_t(w2), False, GEMM_EPI_DGELU, None, pre, 1.0, 0, None)[0]
+        dpre = C.gemm(dy2, weight_t(w2), False, GEMM_EPI_DGELU, None, pre, 1.0, 8, None)[0]
         grads = [None] * 5
         if ctx.needs_input_grad[0]:
             grads[0] = torch.mm(dpre, w1c).view(ctx.shape)
@@ -491,9 +491,10 @@ class _MLPGelu(Function):
 
 
 def fused_mlp_available() -> bool:
-    """Fused-epilogue MLP (MFT_FUSED_MLP=1).  Off by default: measured in the GPT-2 bench step on
-    MI355X the gemm.hip main loop (~0.8-0.9 PF/s at these shapes) still trails hipBLASLt
-    (0.9-1.3 PF/s) by more than the GELU passes it removes (1.198M vs 1.221M tok/s)."""
+    """Fused-epilogue MLP (MFT_FUSED_MLP=1) on the 8-phase gemm8.hip kernel.  Off by default: in
+    the GPT-2 bench step on MI355X it is break-even (1.318M vs 1.320M tok/s, A/B in one call) --
+    the GELU passes it removes are paid back by gemm8's main loop (0.83-0.99 PF/s at these shapes)
+    trailing hipBLASLt (0.91-1.32 PF/s)."""
     import os
     return os.environ.get("MFT_FUSED_MLP", "0") == "1"
 

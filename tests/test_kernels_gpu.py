@@ -105,7 +105,9 @@ def test_gelu_and_gated():
 @pytest.mark.parametrize("M,K,N,nn,bm", [(300, 128, 264, False, 0), (1000, 192, 512, True, 0),
                                           (777, 256, 136, False, 1), (64, 64, 8, True, 1),
                                           (517, 320, 392, False, 2), (517, 320, 392, True, 2),
-                                          (300, 128, 264, False, 3), (300, 128, 264, True, 3)])
+                                          (300, 128, 264, False, 3), (300, 128, 264, True, 3),
+                                          (300, 128, 264, False, 8), (777, 320, 520, False, 8),
+                                          (64, 64, 8, False, 8), (1000, 704, 1024, False, 8)])
 def test_gemm_mfma(M, K, N, nn, bm):
     """gemm.hip (NT and NN operand layouts, M/N tails) and its epilogues vs fp32 torch."""
     from mobilefinetuner_amd._ext import native
