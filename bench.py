@@ -7,7 +7,8 @@ Synthetic token data + random-init GPT-2-124M weights (no network); one process 
 training step: forward, fused LM-head cross-entropy, backward through all 12 blocks, gradient
 all-reduce (N > 1), global grad-norm clip and the fused AdamW update.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--seq 128] [--no-graph]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config gpt2-lora|gemma3-270m-lora|gpt2-full|gpt2-xl-zero]
+                  [--batch B] [--seq S] [--no-graph]
 
 Prints ONE JSON line on rank 0.
 """
@@ -30,25 +31,92 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 BASELINE_TOKENS_PER_SEC = 170.0
 
 
+# BASELINE.json "configs" -> (model preset, mode, default micro-batch, seq, metric label)
+CONFIGS = {
+    # headline: GPT-2 small LoRA r=8 seq 128 (BASELINE.json "metric")
+    "gpt2-lora": dict(model="gpt2", mode="lora", batch=256, seq=128, targets="AttnQKV,AttnProj",
+                      metric="tokens/sec GPT-2-124M LoRA r=8 seq128 (training, whole job)"),
+    # Gemma-3 270M LoRA r=8 seq 256 (RMSNorm / QK-norm+RoPE / GQA / sliding-window kernels)
+    "gemma3-270m-lora": dict(model="gemma3-270m", mode="lora", batch=64, seq=256, targets="full",
+                             metric="tokens/sec Gemma-3-270M LoRA r=8 seq256 (training, whole job)"),
+    # GPT-2 small full fine-tuning, DP over RCCL (bucketed, backward-overlapped all-reduce)
+    "gpt2-full": dict(model="gpt2", mode="full", batch=64, seq=128, zero=0,
+                      metric="tokens/sec GPT-2-124M full fine-tune seq128 (training, whole job)"),
+    # GPT-2 XL (1.5B) full fine-tuning with ZeRO-2 partitioned optimizer / reduce-scattered grads
+    "gpt2-xl-zero": dict(model="gpt2-xl", mode="full", batch=16, seq=128, zero=2,
+                         metric="tokens/sec GPT-2-XL full fine-tune ZeRO-2 seq128 (training, whole job)"),
+}
+
+
+def build(a, cfgd, dev, world):
+    from mobilefinetuner_amd.optim.adamw import FusedAdamW
+    from mobilefinetuner_amd.parallel.ddp import DataParallel
+    from mobilefinetuner_amd.train.engine import TrainStep
+    from mobilefinetuner_amd.utils.params import FlatParams
+
+    name = cfgd["model"]
+    if name.startswith("gemma"):
+        from mobilefinetuner_amd.models.gemma3 import Gemma3Config, Gemma3Model
+        mcfg = Gemma3Config.preset(name)
+        model = Gemma3Model(mcfg, dtype=torch.bfloat16, device=dev, seed=1234)
+        vocab = mcfg.vocab_size
+    else:
+        from mobilefinetuner_amd.models.gpt2 import GPT2Config, GPT2Model
+        mcfg = GPT2Config.preset(name)
+        model = GPT2Model(mcfg, dtype=torch.bfloat16, device=dev, seed=1234)  # identical on every rank
+        vocab = mcfg.vocab_size
+    if cfgd["mode"] == "lora":
+        from mobilefinetuner_amd.peft import lora as L
+        if name.startswith("gemma"):
+            spec = L.LoraSpec(rank=a.rank, alpha=a.alpha, targets=L.parse_gemma_targets(a.targets or cfgd["targets"]))
+            L.inject_gemma(model, spec)
+        else:
+            spec = L.LoraSpec(rank=a.rank, alpha=a.alpha, targets=L.parse_gpt2_targets(a.targets or cfgd["targets"]))
+            L.inject_gpt2(model, spec)
+        flat = FlatParams(L.lora_parameters(model), dev)
+        opt = FusedAdamW(flat, lr=2e-4, weight_decay=0.0, max_grad_norm=1.0)
+        dp = DataParallel(flat) if world > 1 else None
+        desc = f"{name} LoRA r={a.rank} alpha={a.alpha:g} targets={a.targets or cfgd['targets']}"
+    else:
+        model.set_full_finetune()
+        zero = cfgd.get("zero", 0) if world > 1 else 0
+        flat = FlatParams(model.named_parameters(), dev, pad_multiple=max(1, world))
+        if zero:
+            from mobilefinetuner_amd.parallel.zero import ZeroOptimizer, ZeroReducer
+            opt = ZeroOptimizer(flat, zero, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0)
+            dp = ZeroReducer(opt)
+        else:
+            opt = FusedAdamW(flat, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0)
+            dp = DataParallel(flat) if world > 1 else None
+        desc = f"{name} full fine-tune" + (f" ZeRO-{zero}" if zero else "")
+    step = TrainStep(model, flat, opt, grad_accum=a.grad_accum, dp=dp, use_graph=not a.no_graph)
+    nparams = sum(p.numel() for p in model.parameters())
+    return model, step, vocab, desc, nparams
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    # 256 x 128 = 32k tokens per GPU per step: the M dimension every block GEMM sees.  Measured on
-    # 1x MI355X: B=64 0.89M tok/s, B=128 1.02M, B=256 1.09M (block GEMMs reach higher MFMA
-    # utilisation at M=32k; 288 GB HBM makes the activation footprint irrelevant).
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("MFT_BENCH_BATCH", 256)),
-                    help="micro-batch (sequences) per GPU")
-    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--config", default="gpt2-lora", choices=sorted(CONFIGS),
+                    help="benchmark configuration (BASELINE.json configs); default = the headline metric")
+    # micro-batch default per config; for the headline 256 x 128 = 32k tokens per GPU per step: the
+    # M dimension every block GEMM sees.  Measured on 1x MI355X: B=64 0.89M tok/s, B=128 1.02M,
+    # B=256 1.09M (block GEMMs reach higher MFMA utilisation at M=32k; 288 GB HBM makes the
+    # activation footprint irrelevant).
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("MFT_BENCH_BATCH", 0)),
+                    help="micro-batch (sequences) per GPU (0 = the config's default)")
+    ap.add_argument("--seq", type=int, default=0)
     ap.add_argument("--rank", type=int, default=8)
     ap.add_argument("--alpha", type=float, default=16.0)
-    ap.add_argument("--targets", default="AttnQKV,AttnProj")
-    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--targets", default="")
     ap.add_argument("--grad_accum", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--profile", action="store_true", help="print a per-phase breakdown to stderr")
     a = ap.parse_args()
+    cfgd = CONFIGS[a.config]
+    a.batch = a.batch or cfgd["batch"]
+    a.seq = a.seq or cfgd["seq"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -59,21 +127,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
-    from mobilefinetuner_amd.models.gpt2 import GPT2Config, GPT2Model
-    from mobilefinetuner_amd.optim.adamw import FusedAdamW
-    from mobilefinetuner_amd.parallel.ddp import DataParallel
-    from mobilefinetuner_amd.peft.lora import LoraSpec, inject_gpt2, lora_parameters, parse_gpt2_targets
-    from mobilefinetuner_amd.train.engine import TrainStep
-    from mobilefinetuner_amd.utils.params import FlatParams
-
-    cfg = GPT2Config.preset(a.model)
-    model = GPT2Model(cfg, dtype=torch.bfloat16, device=dev, seed=1234)  # identical on every rank
-    spec = LoraSpec(rank=a.rank, alpha=a.alpha, targets=parse_gpt2_targets(a.targets))
-    inject_gpt2(model, spec)
-    flat = FlatParams(lora_parameters(model), dev)
-    opt = FusedAdamW(flat, lr=2e-4, weight_decay=0.0, max_grad_norm=1.0)
-    dp = DataParallel(flat) if world > 1 else None
-    step = TrainStep(model, flat, opt, grad_accum=a.grad_accum, dp=dp, use_graph=not a.no_graph)
+    model, step, vocab, desc, nparams = build(a, cfgd, dev, world)
 
     # synthetic WikiText-shaped data: per-rank disjoint random token streams, labels = next token
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
@@ -82,7 +136,7 @@ def main():
     for _ in range(nbuf):
         mb = []
         for _ in range(a.grad_accum):
-            toks = torch.randint(0, cfg.vocab_size, (a.batch, a.seq + 1), generator=g)
+            toks = torch.randint(0, vocab, (a.batch, a.seq + 1), generator=g)
             mb.append((toks[:, :-1].contiguous().to(dev), toks[:, 1:].contiguous().to(dev)))
         data.append(mb)
 
@@ -108,7 +162,7 @@ def main():
     value = tokens / dt
     if rank == 0:
         out = {
-            "metric": "tokens/sec GPT-2-124M LoRA r=8 seq128 (training, whole job)",
+            "metric": cfgd["metric"],
             "value": round(value, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -117,18 +171,19 @@ def main():
             "ms_per_step": round(1000 * dt / a.steps, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_TOKENS_PER_SEC, 1),
+            # the reference publishes no throughput; only the GPT-2 small figure can be derived
+            "vs_baseline": round(value / BASELINE_TOKENS_PER_SEC, 1) if a.config == "gpt2-lora" else None,
             "dtype": "bf16",
             "data": "synthetic (random tokens, random-init weights)",
             "config": {
-                "model": f"{a.model} (124M) LoRA r={a.rank} alpha={a.alpha:g} targets={a.targets}",
+                "model": f"{desc} ({nparams / 1e6:.0f}M params)",
                 "global_batch": world * a.batch * a.grad_accum,
                 "micro_batch_per_gpu": a.batch,
                 "seq_len": a.seq,
                 "parallelism": f"dp{world}",
                 "hipgraph": not a.no_graph,
                 "final_loss": round(final_loss, 4),
-                "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC,
+                "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC if a.config == "gpt2-lora" else None,
             },
         }
         print(json.dumps(out), flush=True)

@@ -15,8 +15,11 @@ import torch.distributed as dist
 from ..utils.logging import log0
 
 
-def init_distributed(device_pref: str = "auto"):
-    """One process per GPU (torchrun env).  Backend nccl (= RCCL over xGMI) on GPUs, gloo on CPU."""
+def init_distributed(device_pref: str = "auto", timeout_s: float = 600.0):
+    """One process per GPU (mft_launch / torchrun env).  Backend nccl (= RCCL over xGMI) on GPUs,
+    gloo on CPU.  ``timeout_s`` bounds every collective: with TORCH_NCCL_ASYNC_ERROR_HANDLING the
+    RCCL watchdog aborts a rank whose peer died instead of hanging, and mft_launch
+    then stops the job."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -25,10 +28,13 @@ def init_distributed(device_pref: str = "auto"):
     if use_cuda:
         torch.cuda.set_device(dev)
     if world > 1 and not dist.is_initialized():
+        import datetime
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        to = datetime.timedelta(seconds=float(timeout_s))
         if use_cuda:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=to)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=to)
     return rank, world, local, dev
 
 
@@ -73,6 +79,17 @@ def add_runtime_args(ap):
     g.add_argument("--state_dir", default="", help="full training-state checkpoint dir (resume target)")
     g.add_argument("--metrics_out", default="")
     g.add_argument("--activation_checkpointing", action="store_true")
+    g.add_argument("--profile_steps", default="", help="a:b — hipProfilerStart/Stop + roctx ranges for steps a..b "
+                   "(rocprofv3 --selected-regions)")
+    g.add_argument("--trace", action="store_true", help="roctx ranges around every step phase (MFT_TRACE=1)")
+    g.add_argument("--inject_fault", default="", help="step:rank — raise on that rank at that step (failure tests)")
+    g.add_argument("--dist_timeout_s", type=float, default=600.0, help="collective timeout (RCCL watchdog)")
+
+
+def runtime_train_kwargs(a) -> dict:
+    """TrainConfig fields fed from the runtime flag block."""
+    return dict(profile_steps=getattr(a, "profile_steps", ""),
+                extra={"inject_fault": getattr(a, "inject_fault", ""), "trace": bool(getattr(a, "trace", False))})
 
 
 def build_power_monitor(a):

@@ -67,7 +67,7 @@ def main(argv=None):
     from ..io.lora_checkpoint import attach_lora, load_lora
     from ..peft.lora import merge_all, set_lora_enabled
     from ..utils.logging import log0
-    rank, world, _, dev = common.init_distributed(a.device)
+    rank, world, _, dev = common.init_distributed(a.device, getattr(a, 'dist_timeout_s', 600.0))
     dt = common.dtype_of(a)
     if a.model_type == "gpt2":
         model = common.load_gpt2(a.pretrained_dir, a.model, a.random_init, dev, dt)

@@ -63,7 +63,7 @@ def main(argv=None):
     from ..utils.logging import log0
     from ..utils.params import FlatParams
 
-    rank, world, _, dev = common.init_distributed(a.device)
+    rank, world, _, dev = common.init_distributed(a.device, getattr(a, 'dist_timeout_s', 600.0))
     torch.manual_seed(a.seed)
     log0("\n========== GPT-2 Full Finetune (MI355X) ==========\n")
     model = common.load_gpt2(a.pretrained_dir, a.model, a.random_init, dev, common.dtype_of(a), seed=1234)
@@ -94,7 +94,8 @@ def main(argv=None):
                      clip_grad_norm=a.clip_grad_norm, l2_coupled=a.compat_l2_adam, log_interval=a.log_interval,
                      eval_interval=a.eval_interval, eval_batches=a.eval_batches, eval_batch_size=a.eval_batch_size,
                      eval_out=a.eval_out, save_every=a.save_every, ema_beta=a.ema_beta,
-                     use_graph=not a.no_graph, state_dir=a.state_dir, metrics_out=a.metrics_out)
+                     use_graph=not a.no_graph, state_dir=a.state_dir, metrics_out=a.metrics_out,
+                     **common.runtime_train_kwargs(a))
 
     trainer = None
 

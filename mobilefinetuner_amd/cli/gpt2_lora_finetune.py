@@ -67,7 +67,7 @@ def main(argv=None):
     from ..utils.logging import log0
     from ..utils.params import FlatParams
 
-    rank, world, _, dev = common.init_distributed(a.device)
+    rank, world, _, dev = common.init_distributed(a.device, getattr(a, 'dist_timeout_s', 600.0))
     torch.manual_seed(a.seed)
     log0("\n========== GPT-2 LoRA Finetune (MI355X) ==========\n")
     log0("[Config]")
@@ -123,7 +123,8 @@ def main(argv=None):
                      clip_grad_norm=a.clip_grad_norm, l2_coupled=a.compat_l2_adam, log_interval=a.log_interval,
                      eval_interval=a.eval_interval, eval_batches=a.eval_batches, eval_batch_size=a.eval_batch_size,
                      eval_out=a.eval_out, save_every=a.save_every, ema_beta=a.ema_beta, use_graph=not a.no_graph,
-                     state_dir=a.state_dir, metrics_out=a.metrics_out)
+                     state_dir=a.state_dir, metrics_out=a.metrics_out,
+                     **common.runtime_train_kwargs(a))
 
     def save(step):
         if a.lora_out:

@@ -155,7 +155,7 @@ def main(argv=None):
     from ..utils.params import FlatParams
     if unknown:
         log0(f"[train_lora_gemma] ignoring unknown arguments: {unknown}")
-    rank, world, _, dev = common.init_distributed(a.device)
+    rank, world, _, dev = common.init_distributed(a.device, getattr(a, 'dist_timeout_s', 600.0))
     torch.manual_seed(a.seed)
     log0("\n========== Gemma-3 LoRA Finetune (MI355X) ==========")
     model = common.load_gemma(a.model_dir, a.model, a.random_init, dev, common.dtype_of(a), seed=1234)
@@ -201,7 +201,7 @@ def main(argv=None):
                      clip_grad_norm=a.max_grad_norm, l2_coupled=a.compat_l2_adam, log_interval=a.log_interval,
                      eval_interval=a.eval_steps, eval_batches=a.eval_batches, eval_batch_size=a.batch,
                      save_every=a.save_every, use_graph=not a.no_graph, log_style="gemma", state_dir=a.state_dir,
-                     metrics_out=a.metrics_out)
+                     metrics_out=a.metrics_out, **common.runtime_train_kwargs(a))
     out = os.path.join(a.output_dir, "gemma_lora.safetensors")
 
     def save(step):

@@ -14,8 +14,10 @@ from __future__ import annotations
 import torch
 
 from ..optim.adamw import FusedAdamW
+from ..utils.trace import trace_range
 from ..parallel.ddp import DataParallel, allreduce_mean_
 from ..utils.params import FlatParams
+
 
 
 class TrainStep:
@@ -57,9 +59,12 @@ class TrainStep:
     def _eager_step(self, batches):
         if self.dp is not None:
             self.dp.begin_step()
-        self._fwd_bwd(batches)
-        self._reduce()
-        self._opt()
+        with trace_range("fwd_bwd"):
+            self._fwd_bwd(batches)
+        with trace_range("grad_allreduce"):
+            self._reduce()
+        with trace_range("optimizer"):
+            self._opt()
 
     # ----------------------------------------------------------------- graph capture
     def _capture(self, batches):
@@ -104,8 +109,11 @@ class TrainStep:
                 slab.copy_(lab, non_blocking=True)
         if self.dp is not None:
             self.dp.begin_step()
-        self.graph.replay()
+        with trace_range("fwd_bwd_graph"):
+            self.graph.replay()
         if not self.graph_comm:
-            self._reduce()
-            self._opt()
+            with trace_range("grad_allreduce"):
+                self._reduce()
+            with trace_range("optimizer"):
+                self._opt()
         return self.loss_dev

@@ -28,6 +28,7 @@ from ..optim.adamw import FusedAdamW
 from ..parallel.ddp import DataParallel, allreduce_sum_, is_dist
 from ..utils.logging import log0, rank0
 from ..utils.params import FlatParams
+from ..utils.trace import PhaseTimer, ProfileWindow, enable_tracing, trace_range
 from .engine import TrainStep
 
 
@@ -191,7 +192,17 @@ class Trainer:
         accum = max(1, c.grad_accum)
         t_last = time.perf_counter()
         tok_last = self.total_tokens
+        window = ProfileWindow(c.profile_steps)
+        if c.extra.get("trace"):
+            enable_tracing(True)
+        timer = PhaseTimer(enabled=self.device.type == "cuda")
+        fault = c.extra.get("inject_fault", "")
+        fault_step, fault_rank = (int(v) for v in fault.split(":")) if fault else (-1, -1)
+        my_rank = dist.get_rank() if is_dist() else 0
         for step in range(self.global_step, self.total_steps):
+            window.before_step(step + 1)
+            if step + 1 == fault_step and my_rank == fault_rank:
+                raise RuntimeError(f"injected fault at step {step + 1} on rank {my_rank} (--inject_fault)")
             cur_epoch = step // self.steps_per_epoch + 1
             step_in_epoch = step % self.steps_per_epoch + 1
             lr = self.lr_at(step)
@@ -201,7 +212,9 @@ class Trainer:
                 ids, tg, nt = self._next_micro()
                 batches.append((ids, tg))
                 ntok += nt
-            loss_dev = self.step_fn(batches)
+            with timer.phase("train_step"):
+                loss_dev = self.step_fn(batches)
+            window.after_step(step + 1)
             self.global_step = step + 1
             ntok_all = ntok * self.world
             self.total_tokens += ntok_all
@@ -218,6 +231,7 @@ class Trainer:
                     beta = max(0.0, min(0.9999, c.ema_beta))
                     self.ema_loss = loss if self.ema_loss is None else beta * self.ema_loss + (1 - beta) * loss
             if do_log:
+                step_ms = timer.report().get("train_step", 0.0)
                 gn = self.opt.grad_norm()
                 gn_clip = min(gn, c.clip_grad_norm) if c.clip_grad_norm > 0 else gn
                 now = time.perf_counter()
@@ -232,9 +246,9 @@ class Trainer:
                     log0(f"[Train] epoch {cur_epoch}/{c.epochs} | step {step_in_epoch}/{self.steps_per_epoch} "
                          f"(global {step + 1}/{self.total_steps}) | lr {lr:.6f} | loss {loss:.4f} | ppl {ppl:.2f} "
                          f"| grad_norm {gn_clip:.3f} | tokens {ntok_all} | tokens_per_sec {tps:.0f} "
-                         f"| hbm_peak_gb {mem:.2f}" + (" | skipped_nonfinite" if skipped else ""))
+                         f"| hbm_peak_gb {mem:.2f} | step_ms {step_ms:.2f}" + (" | skipped_nonfinite" if skipped else ""))
                 rec = {"step": step + 1, "epoch": cur_epoch, "loss": loss, "lr": lr, "grad_norm": gn,
-                       "tokens_per_sec": tps, "hbm_peak_gb": mem}
+                       "tokens_per_sec": tps, "hbm_peak_gb": mem, "step_ms": step_ms, "skipped_total": self.skipped}
                 self.history.append(rec)
                 if c.metrics_out and rank0():
                     with open(c.metrics_out, "a") as f:

@@ -129,3 +129,35 @@ def test_zero_matches_ddp(stage):
     n = ddp[0][0].numel()
     assert torch.allclose(ddp[0][0], zero[0][0][:n], atol=1e-5), (ddp[0][0] - zero[0][0][:n]).abs().max()
     assert torch.allclose(zero[0][0], zero[1][0])
+
+
+def test_mft_launch_propagates_rank_failure(tmp_path):
+    """a failing rank stops the job (peers blocked in a collective are terminated)."""
+    import time
+    from mobilefinetuner_amd.launch import launch
+    script = tmp_path / "job.py"
+    script.write_text(
+        "import os, sys, time\n"
+        "import torch.distributed as dist\n"
+        "dist.init_process_group('gloo')\n"
+        "if int(os.environ['RANK']) == 1:\n"
+        "    sys.exit(3)\n"
+        "dist.barrier()  # rank 0 would wait here forever\n"
+        "time.sleep(600)\n")
+    t0 = time.time()
+    code = launch([str(script)], 2, grace=2.0)
+    assert code == 3 and time.time() - t0 < 60
+    ok = tmp_path / "ok.py"
+    ok.write_text("import os\nassert os.environ['WORLD_SIZE'] == '2' and os.environ['MASTER_ADDR'] == '127.0.0.1'\n")
+    assert launch([str(ok)], 2) == 0
+
+
+def test_cli_inject_fault_under_launcher(tmp_path):
+    """--inject_fault step:rank raises on that rank; mft_launch reports the failure and stops rank 0."""
+    from mobilefinetuner_amd.launch import launch
+    code = launch(["-m", "mobilefinetuner_amd.cli.gpt2_lora_finetune", "--model", "gpt2-tiny", "--device", "cpu",
+                   "--dtype", "fp32", "--random_init", "--synthetic_data", "--synthetic_tokens", "20000",
+                   "--steps", "6", "--batch_size", "2", "--seq_len", "32", "--lora_out",
+                   str(tmp_path / "l.safetensors"), "--inject_fault", "3:1", "--dist_timeout_s", "60"],
+                  2, grace=2.0, extra_env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "1"})
+    assert code != 0

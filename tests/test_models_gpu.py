@@ -170,3 +170,20 @@ def test_gemma270m_lora_step():
     l1 = float(st(b).item())
     assert l0 == l0 and abs(l0 - 12.48) < 1.0 and opt.grad_norm() > 0
     del l1
+
+
+def test_trace_profile_window_and_phase_timer():
+    """roctx ranges + hipProfilerStart/Stop window + hipEvent phase timers run on the GPU."""
+    from mobilefinetuner_amd.utils.trace import PhaseTimer, ProfileWindow, enable_tracing, trace_range
+    enable_tracing(True)
+    w = ProfileWindow("1:2")
+    t = PhaseTimer()
+    x = torch.randn(512, 512, device=DEV)
+    for step in (1, 2, 3):
+        w.before_step(step)
+        with t.phase("mm"), trace_range("inner"):
+            x = (x @ x).tanh()
+        w.after_step(step)
+    r = t.report()
+    enable_tracing(False)
+    assert r["mm"] > 0 and not w.active
