@@ -35,6 +35,16 @@ class ZeroOptimizer:
         self.shard = n // self.world
         self.lo, self.hi = self.rank * self.shard, (self.rank + 1) * self.shard
         self.inner = FusedAdamW(flat, param_range=(self.lo, self.hi), **adamw_kwargs)
+        # parameters that compute straight from the fp32 master (norm weights/biases: no bf16
+        # shadow) are not covered by the shadow all-gather; their owned slices are re-assembled
+        # with one masked all-reduce of a packed index list (tiny: LN/RMSNorm parameters only)
+        self._fp32_idx = self._fp32_own = None
+        if flat.shadow is not None:
+            loose = [s for s in flat.slots if getattr(s.param, "shadow", None) is None]
+            if loose:
+                idx = torch.cat([torch.arange(s.offset, s.offset + s.numel) for s in loose]).to(flat.master.device)
+                self._fp32_idx = idx
+                self._fp32_own = ((idx >= self.lo) & (idx < self.hi)).to(flat.master.dtype)
         if self.world > 1:  # identical starting weights everywhere
             dist.broadcast(flat.master, src=0, group=group)
             flat.refresh_shadow()
@@ -75,6 +85,10 @@ class ZeroOptimizer:
             # them for checkpointing
             sh = self.flat.shadow if self.flat.shadow is not None else self.flat.master
             dist.all_gather_into_tensor(sh, sh[self.lo:self.hi].clone(), group=self.group)
+            if self._fp32_idx is not None:
+                v = self.flat.master.index_select(0, self._fp32_idx) * self._fp32_own
+                dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.group)
+                self.flat.master.index_copy_(0, self._fp32_idx, v)
 
     def gather_master(self):
         """All-gather the fp32 master (for checkpointing on every rank)."""

@@ -161,3 +161,36 @@ def test_cli_inject_fault_under_launcher(tmp_path):
                    str(tmp_path / "l.safetensors"), "--inject_fault", "3:1", "--dist_timeout_s", "60"],
                   2, grace=2.0, extra_env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "1"})
     assert code != 0
+
+
+def _worker_zero_shadow(rank, world, port, q):
+    _init(rank, world, port)
+    from mobilefinetuner_amd.models.gpt2 import GPT2Config, GPT2Model
+    from mobilefinetuner_amd.parallel.zero import ZeroOptimizer
+    from mobilefinetuner_amd.utils.params import FlatParams
+    m = GPT2Model(GPT2Config.preset("gpt2-tiny"), dtype=torch.float32, device="cpu", seed=5)
+    m.set_full_finetune()
+    # a bf16 shadow as on the GPU: norm weights (no shadow) must still be synchronised across ranks
+    flat = FlatParams(m.named_parameters(), "cpu", shadow=True, pad_multiple=world)
+    opt = ZeroOptimizer(flat, 2, lr=1e-2, weight_decay=0.0, max_grad_norm=None)
+    for _ in range(2):
+        flat.grad.normal_(0, 1.0, generator=torch.Generator().manual_seed(rank + 1))
+        opt.reduce_gradients()
+        opt.step()
+    ln = torch.cat([m.blocks[0].ln_1.weight.detach().flatten(), m.ln_f.bias.detach().flatten()])
+    q.put((rank, ln.clone()))
+    dist.destroy_process_group()
+
+
+def test_zero_syncs_fp32_compute_params():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_zero_shadow, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=600) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert not torch.equal(out[0], torch.ones_like(out[0]))  # updated
+    assert torch.equal(out[0], out[1])
