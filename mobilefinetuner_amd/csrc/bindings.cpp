@@ -426,6 +426,21 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
 }
 
 
+// out[N] (fp32) (+)= column sums of x[M, N] (bf16, row stride ld): bias gradients accumulated
+// straight into the flat fp32 grad buffer (deterministic two-stage reduction, no fp32 copy of x).
+void colsum_acc(Tensor x, Tensor out, bool accumulate) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_F32(out);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.size(1) % 8 == 0 && out.numel() == x.size(1),
+              "colsum_acc: x [M, N] row-contiguous (N, ld multiples of 8), out [N]");
+  c10::DeviceGuard g(x.device());
+  const long M = x.size(0);
+  const int N = x.size(1);
+  const int nb = mft::colsum_partial_blocks(M);
+  auto part = torch::empty({(long)nb * N}, out.options());
+  mft::colsum_partial(bp(x), x.stride(0), M, N, fp(part), stream());
+  mft::reduce_rows(fp(part), fp(out), nb, N, accumulate ? 1 : 0, stream());
+}
+
 // Zero columns [c0, ncols) of a row-strided 2-D bf16 tensor (one small kernel, graph-capturable).
 // Deliberately outside autograd: the padding columns of augmented LoRA inputs are read by no
 // autograd-visible op (an in-place torch op there would trip the view/version checks).
@@ -466,6 +481,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_merge", &lora_merge);
   m.def("gemm", &gemm_op);
   m.def("zero_cols", &zero_cols);
+  m.def("colsum_acc", &colsum_acc);
   m.def("rope_apply", &rope_apply);
   m.def("qknorm_rope_fwd", &qknorm_rope_fwd);
   m.def("qknorm_rope_bwd", &qknorm_rope_bwd);

@@ -4,12 +4,16 @@
 // the hand-written kernels/gemm.hip because this ROCm build's gfx950 hipBLASLt has NO solutions for
 // the GELU_AUX(_BIAS) / DGELU(_BGRAD) epilogues in bf16 (scripts/probe_lt.py: 0 solutions for
 // every layout, while DEFAULT / BIAS / GELU / GELU_BIAS have 8).  lt_solutions() keeps that
-// check reproducible on any box; Plan/run() below are the cached-algorithm plumbing it shares.
+// check reproducible on any box.  lt_wgrad_acc() is the one hipBLASLt call made directly: weight
+// gradients accumulated in place into the fp32 grad buffer (beta = 1), which torch.mm cannot do
+// for bf16 inputs.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 #include <hipblaslt/hipblaslt.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -50,15 +54,17 @@ hipblasLtHandle_t handle_for(int dev) {
 struct Problem {
   int dev, ta, tb, epi, has_bias;
   long m, n, k, lda, ldb, ldd, ldaux;
+  int d_f32 = 0;  // C/D in fp32 (weight-gradient accumulation) instead of bf16
   std::string key() const {
     char buf[256];
-    snprintf(buf, sizeof(buf), "%d|%d|%d|%d|%d|%ld|%ld|%ld|%ld|%ld|%ld|%ld", dev, ta, tb, epi, has_bias, m, n, k, lda,
-             ldb, ldd, ldaux);
+    snprintf(buf, sizeof(buf), "%d|%d|%d|%d|%d|%ld|%ld|%ld|%ld|%ld|%ld|%ld|%d", dev, ta, tb, epi, has_bias, m, n, k, lda,
+             ldb, ldd, ldaux, d_f32);
     return buf;
   }
 };
 
-Plan& plan_for(const Problem& p, hipblasLtHandle_t h) {
+// A/B: the operands of the first call (timing candidates when the plan is created).
+Plan& plan_for(const Problem& p, hipblasLtHandle_t h, const void* A = nullptr, const void* B = nullptr) {
   static std::mutex mu;
   static std::unordered_map<std::string, Plan> plans;
   std::lock_guard<std::mutex> g(mu);
@@ -85,26 +91,70 @@ Plan& plan_for(const Problem& p, hipblasLtHandle_t h) {
   // A is (m x k) after op; stored (rows x cols) = ta ? (k x m) : (m x k)
   LT_CHECK(hipblasLtMatrixLayoutCreate(&pl.a, HIP_R_16BF, p.ta ? p.k : p.m, p.ta ? p.m : p.k, p.lda));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&pl.b, HIP_R_16BF, p.tb ? p.n : p.k, p.tb ? p.k : p.n, p.ldb));
-  LT_CHECK(hipblasLtMatrixLayoutCreate(&pl.d, HIP_R_16BF, p.m, p.n, p.ldd));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&pl.d, p.d_f32 ? HIP_R_32F : HIP_R_16BF, p.m, p.n, p.ldd));
   hipblasLtMatmulPreference_t pref;
   LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
   uint64_t ws = kWorkspace;
   LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws)));
-  hipblasLtMatmulHeuristicResult_t res[4];
+  constexpr int kCand = 16;
+  hipblasLtMatmulHeuristicResult_t res[kCand];
   int got = 0;
-  hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(h, pl.op, pl.a, pl.b, pl.d, pl.d, pref, 4, res, &got);
+  hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(h, pl.op, pl.a, pl.b, pl.d, pl.d, pref, kCand, res, &got);
   hipblasLtMatmulPreferenceDestroy(pref);
   TORCH_CHECK(st == HIPBLAS_STATUS_SUCCESS && got > 0, "hipBLASLt: no algorithm for epilogue ", p.epi, " m=", p.m,
               " n=", p.n, " k=", p.k);
-  pl.algo = res[0].algo;
-  pl.ws = res[0].workspaceSize;
+  int best = 0;
+  // Autotune: the heuristic's first pick is poor for some skinny shapes (weight gradients reduce
+  // over M = B*S with few output tiles); time every candidate once on the real operands into a
+  // scratch output.  Skipped while a hipGraph is being captured and with MFT_LT_TUNE=0.
+  hipStream_t stream = c10::hip::getCurrentHIPStream().stream();
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(stream, &cap);
+  const char* tune_env = getenv("MFT_LT_TUNE");
+  if (got > 1 && A && B && cap == hipStreamCaptureStatusNone && !(tune_env && tune_env[0] == '0')) {
+    const size_t esz = p.d_f32 ? 4 : 2;
+    auto opts = torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, p.dev);
+    Tensor scratch = torch::empty({(long)(p.ldd * p.n * esz)}, opts);
+    size_t wmax = 0;
+    for (int i = 0; i < got; ++i) wmax = std::max(wmax, (size_t)res[i].workspaceSize);
+    Tensor wsb = torch::empty({(long)std::max<size_t>(wmax, 1)}, opts);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    const float alpha = 1.f, beta = 0.f;
+    float best_ms = 1e30f;
+    for (int i = 0; i < got; ++i) {
+      bool ok = true;
+      for (int rep = 0; rep < 2 && ok; ++rep)
+        ok = hipblasLtMatmul(h, pl.op, &alpha, A, pl.a, B, pl.b, &beta, scratch.data_ptr(), pl.d, scratch.data_ptr(),
+                             pl.d, &res[i].algo, wsb.data_ptr(), res[i].workspaceSize, stream) == HIPBLAS_STATUS_SUCCESS;
+      if (!ok) continue;
+      (void)hipEventRecord(e0, stream);
+      for (int rep = 0; rep < 5; ++rep)
+        (void)hipblasLtMatmul(h, pl.op, &alpha, A, pl.a, B, pl.b, &beta, scratch.data_ptr(), pl.d, scratch.data_ptr(),
+                              pl.d, &res[i].algo, wsb.data_ptr(), res[i].workspaceSize, stream);
+      (void)hipEventRecord(e1, stream);
+      (void)hipEventSynchronize(e1);
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (ms < best_ms) {
+        best_ms = ms;
+        best = i;
+      }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
+  pl.algo = res[best].algo;
+  pl.ws = res[best].workspaceSize;
   return plans.emplace(key, pl).first->second;
 }
 
-void run(const Problem& p, const void* A, const void* B, void* D, const void* bias, void* aux) {
+void run(const Problem& p, const void* A, const void* B, void* D, const void* bias, void* aux, float alpha = 1.f,
+         float beta = 0.f) {
   const int dev = p.dev;
   hipblasLtHandle_t h = handle_for(dev);
-  Plan& pl = plan_for(p, h);
+  Plan& pl = plan_for(p, h, A, B);
   if (bias) LT_CHECK(hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
   if (aux) LT_CHECK(hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux)));
   Tensor ws;
@@ -113,7 +163,6 @@ void run(const Problem& p, const void* A, const void* B, void* D, const void* bi
     ws = torch::empty({(long)pl.ws}, torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, dev));
     wsp = ws.data_ptr();
   }
-  const float alpha = 1.f, beta = 0.f;
   LT_CHECK(hipblasLtMatmul(h, pl.op, &alpha, A, pl.a, B, pl.b, &beta, D, pl.d, D, pl.d, &pl.algo, wsp, pl.ws,
                            c10::hip::getCurrentHIPStream().stream()));
 }
@@ -161,8 +210,57 @@ int lt_solutions(int64_t m, int64_t n, int64_t k, bool ta, bool tb, int64_t epi,
   return st == HIPBLAS_STATUS_SUCCESS ? got : -(int)st;
 }
 
+// out[N, K] (fp32) += alpha * dy[M, N]^T x[M, K]   (bf16 inputs, fp32 accumulate, beta = 1):
+// weight gradients straight into the flat fp32 grad buffer -- no fp32 temporary + add pass.
+void lt_wgrad_acc(Tensor x, Tensor dy, Tensor out, double alpha) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && dy.scalar_type() == torch::kBFloat16 &&
+                  out.scalar_type() == torch::kFloat32, "lt_wgrad_acc: bf16 x/dy, fp32 out");
+  TORCH_CHECK(x.dim() == 2 && dy.dim() == 2 && out.dim() == 2 && x.stride(1) == 1 && dy.stride(1) == 1 &&
+                  out.stride(1) == 1, "lt_wgrad_acc: row-contiguous 2-D tensors");
+  const long M = x.size(0), K = x.size(1), N = dy.size(1);
+  TORCH_CHECK(dy.size(0) == M && out.size(0) == N && out.size(1) == K, "lt_wgrad_acc: shapes");
+  c10::DeviceGuard g(x.device());
+  // col-major: out^T [K, N] = x^T [K, M] . dy [M, N];  x row-major == col-major (K x M, ld K),
+  // dy row-major == col-major (N x M, ld N) -> op(B) = T
+  Problem p{x.get_device(), 0, 1, HIPBLASLT_EPILOGUE_DEFAULT, 0, K, N, M, x.stride(0), dy.stride(0), out.stride(0), 0};
+  p.d_f32 = 1;
+  run(p, x.data_ptr(), dy.data_ptr(), out.data_ptr(), nullptr, nullptr, (float)alpha, 1.f);
+}
+
+// y[M, N] = x[M, K] W[N, K]^T (+ bias[N])  -- autotuned hipBLASLt, bf16 out (BIAS epilogue)
+Tensor lt_linear(Tensor x, Tensor w, c10::optional<Tensor> bias) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16 &&
+                  x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1, "lt_linear: bf16 2-D row-major");
+  const long M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "lt_linear: shapes");
+  const bool hb = bias.has_value() && bias->defined();
+  if (hb) TORCH_CHECK(bias->scalar_type() == torch::kBFloat16 && bias->numel() == N && bias->is_contiguous(), "bias");
+  c10::DeviceGuard g(x.device());
+  auto y = torch::empty({M, N}, x.options());
+  Problem p{x.get_device(), 1, 0, hb ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT, hb ? 1 : 0, N, M, K,
+            w.stride(0), x.stride(0), N, 0};
+  run(p, w.data_ptr(), x.data_ptr(), y.data_ptr(), hb ? bias->data_ptr() : nullptr, nullptr);
+  return y;
+}
+
+// dx[M, K] = dy[M, N] W[N, K]  (data gradient of a Linear; W may be a row-strided view)
+Tensor lt_mm_dx(Tensor dy, Tensor w) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16 &&
+                  dy.dim() == 2 && w.dim() == 2 && dy.stride(1) == 1 && w.stride(1) == 1, "lt_mm_dx: bf16 2-D row-major");
+  const long M = dy.size(0), N = dy.size(1), K = w.size(1);
+  TORCH_CHECK(w.size(0) == N, "lt_mm_dx: shapes");
+  c10::DeviceGuard g(dy.device());
+  auto dx = torch::empty({M, K}, dy.options());
+  Problem p{dy.get_device(), 0, 0, HIPBLASLT_EPILOGUE_DEFAULT, 0, K, M, N, w.stride(0), dy.stride(0), K, 0};
+  run(p, w.data_ptr(), dy.data_ptr(), dx.data_ptr(), nullptr, nullptr);
+  return dx;
+}
+
 }  // namespace
 
 void register_gemm_lt(py::module_& m) {
+  m.def("lt_linear", &lt_linear, "y = x W^T (+ b), autotuned hipBLASLt");
+  m.def("lt_mm_dx", &lt_mm_dx, "dx = dy W, autotuned hipBLASLt");
+  m.def("lt_wgrad_acc", &lt_wgrad_acc, "out[N,K] (fp32) += alpha * dy^T x (hipBLASLt, beta = 1)");
   m.def("lt_solutions", &lt_solutions, "number of hipBLASLt solutions for (m, n, k, ta, tb, epilogue, bias, ldaux, aux_dtype)");
 }

@@ -10,6 +10,8 @@ typedef uint16_t bf16_t;
 
 // ---------------------------------------------------------------- norms (norm.hip)
 int norm_bwd_partial_blocks(int M);
+// out[i] (+)= sum_b part[b * N + i]  (deterministic partial-row reduction for weight grads)
+void reduce_rows(const float* part, float* out, int nb, int N, int accumulate, hipStream_t st);
 // ldy / lddy: row stride of the normalised output / of its gradient (0 = N).  A wider output row
 // leaves room for appended columns (the LoRA augmented-K input [x | u], lora.hip).
 void layernorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, const float* b,
@@ -162,6 +164,9 @@ void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t st);
 void cast_bf16_f32(const bf16_t* x, float* y, long n, hipStream_t st);
 void scale_bf16(const bf16_t* x, bf16_t* y, long n, const float* scale_dev, float scale, hipStream_t st);
 void add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, hipStream_t st);
+// bias gradients: part[b][n] = column sums of row block b (then reduce_rows into the fp32 grad)
+int colsum_partial_blocks(long M);
+void colsum_partial(const bf16_t* x, long ld, long M, int N, float* part, hipStream_t st);
 // p[row, c0 : c0 + ncols] = 0 for every row (c0, ncols, ld multiples of 8)
 void zero_cols(bf16_t* p, long ld, long M, int c0, int ncols, hipStream_t st);
 }  // namespace mft

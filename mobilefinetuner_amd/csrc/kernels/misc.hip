@@ -81,6 +81,48 @@ __global__ void zero_cols_kernel(bf16_t* __restrict__ p, long ld, long M, int c0
   *reinterpret_cast<u16x8_t*>(p + row * ld + c0 + ch * 8) = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
 }
 
+// part[blockIdx.y][n] = sum over this block's rows of x[m, n]  (bias gradients; 32 x 8-column chunks x
+// 8 row lanes per block, combined through LDS; finished by reduce_rows)
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __restrict__ x, long ld, long M, int N,
+                                                             long rows_per_block, float* __restrict__ part) {
+  __shared__ float red[8][32 * 8 + 1];
+  const int cc = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int n = (blockIdx.x * 32 + cc) * 8;
+  const long m0 = (long)blockIdx.y * rows_per_block, m1 = min(M, m0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (n < N) {
+    for (long m = m0 + rl; m < m1; m += 8) {
+      float v[8];
+      load8(x + m * ld + n, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cc * 8 + j] = acc[j];
+  __syncthreads();
+  for (int t = threadIdx.x; t < 256; t += 256) {
+    const int col = blockIdx.x * 256 + t;
+    if (col < N) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += red[k][t];
+      part[(long)blockIdx.y * N + col] = s;
+    }
+  }
+}
+
+int colsum_partial_blocks(long M) {
+  const long nb = (M + 255) / 256;
+  return (int)(nb < 128 ? nb : 128);
+}
+
+void colsum_partial(const bf16_t* x, long ld, long M, int N, float* part, hipStream_t st) {
+  const int nb = colsum_partial_blocks(M);
+  const long rows = (M + nb - 1) / nb;
+  colsum_partial_kernel<<<dim3(cdiv(N, 256), nb), 256, 0, st>>>(x, ld, M, N, rows, part);
+}
+
 void zero_cols(bf16_t* p, long ld, long M, int c0, int ncols, hipStream_t st) {
   const int nch = ncols / 8;
   if (M <= 0 || nch <= 0) return;

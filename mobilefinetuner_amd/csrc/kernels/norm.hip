@@ -183,14 +183,27 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// out[i] (+)= sum_b part[b][i]
-__global__ void reduce_rows_kernel(const float* __restrict__ part, float* __restrict__ out, int nb, int N,
-                                   int accumulate) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
+// out[i] (+)= sum_b part[b][i].  256 threads = 32 columns x 8 row-lanes: each row-lane strides over
+// the partial rows (coalesced 128-B column segments), the 8 lanes are combined through LDS.  (A
+// thread-per-column loop over 512 partial rows was a 512-deep dependent chain: ~120 us per call.)
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, float* __restrict__ out, int nb,
+                                                          int N, int accumulate) {
+  __shared__ float red[8][33];
+  const int c = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int i = blockIdx.x * 32 + c;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(long)b * N + i];
-  out[i] = accumulate ? out[i] + s : s;
+  if (i < N) {
+#pragma unroll 4
+    for (int b = rl; b < nb; b += 8) s += part[(long)b * N + i];
+  }
+  red[rl][c] = s;
+  __syncthreads();
+  if (rl == 0 && i < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][c];
+    out[i] = accumulate ? out[i] + t : t;
+  }
 }
 
 template <bool RMS>
@@ -234,9 +247,13 @@ static void norm_bwd_dispatch(const bf16_t* x, const bf16_t* dy, const float* w,
   else { MFT_NB(8) }
 #undef MFT_NB
   if (wgrad) {
-    reduce_rows_kernel<<<cdiv(N, 256), 256, 0, st>>>(dw_part, dw, nb, N, accumulate);
-    if (!RMS && db) reduce_rows_kernel<<<cdiv(N, 256), 256, 0, st>>>(db_part, db, nb, N, accumulate);
+    reduce_rows_kernel<<<cdiv(N, 32), 256, 0, st>>>(dw_part, dw, nb, N, accumulate);
+    if (!RMS && db) reduce_rows_kernel<<<cdiv(N, 32), 256, 0, st>>>(db_part, db, nb, N, accumulate);
   }
+}
+
+void reduce_rows(const float* part, float* out, int nb, int N, int accumulate, hipStream_t st) {
+  reduce_rows_kernel<<<cdiv(N, 32), 256, 0, st>>>(part, out, nb, N, accumulate);
 }
 
 int norm_bwd_partial_blocks(int M) {

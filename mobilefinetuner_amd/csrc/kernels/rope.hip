@@ -159,15 +159,6 @@ __global__ __launch_bounds__(256) void qknorm_rope_bwd_kernel(const bf16_t* __re
   }
 }
 
-__global__ void reduce_rows_kernel2(const float* __restrict__ part, float* __restrict__ out, int nb, int N,
-                                    int accumulate) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(long)b * N + i];
-  out[i] = accumulate ? out[i] + s : s;
-}
-
 #define MFT_PPL_DISPATCH(D, ...)                                      \
   do {                                                                \
     const int ppl = ((D) / 2 + 63) / 64;                              \
@@ -206,7 +197,7 @@ void qknorm_rope_bwd(const bf16_t* x, const long* st, const bf16_t* dy, const fl
   MFT_PPL_DISPATCH(D, qknorm_rope_bwd_kernel<P><<<nb, 256, shm, stream>>>(
                           x, st[0], st[1], st[2], dy, rstd, w, dx, dst[0], dst[1], dst[2], part, B, S, H, D, cos_t,
                           sin_t, pos0, off, interleaved));
-  if (dw) reduce_rows_kernel2<<<cdiv(D, 256), 256, 0, stream>>>(part, dw, nb, D, accumulate);
+  if (dw) reduce_rows(part, dw, nb, D, accumulate, stream);
 }
 
 }  // namespace mft

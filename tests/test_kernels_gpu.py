@@ -489,3 +489,20 @@ def test_lora_dropout_consistent_fwd_bwd():
     um2 = torch.empty_like(um)
     C.lora_rowdot(ones, eye, um2, 1.0, p, salt, ctr)
     assert not torch.equal(um, um2), "a new step must draw a new mask"
+
+
+def test_colsum_and_wgrad_accumulate():
+    """Bias-grad column sums and hipBLASLt beta=1 weight-grad accumulation into fp32 buffers."""
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    M, N, K = 1000, 264, 200
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    out = torch.full((N,), 2.0, device=DEV)
+    C.colsum_acc(dy, out, True)
+    _close(out, 2.0 + dy.float().sum(0), 0.02, 1e-3, msg="colsum")
+    C.colsum_acc(dy[:, :256], out[:256], False)
+    _close(out[:256], dy[:, :256].float().sum(0), 0.02, 1e-3, msg="colsum strided")
+    w = torch.ones(N, K, device=DEV)
+    C.lt_wgrad_acc(x, dy, w, 0.5)
+    _close(w, 1.0 + 0.5 * dy.float().t() @ x.float(), 0.05, 1e-3, msg="wgrad acc")
