@@ -84,7 +84,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   const int tiles_n = (g.N + 255) / 256;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (tile / tiles_n) * 256, n0 = (tile % tiles_n) * 256;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = w >> 2, wn = w & 3;  // wave's 64 x 32 piece inside each 128 x 128 quadrant
   const int nk = g.K / 64;
   const int last = nk - 1;
@@ -140,6 +140,12 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   stage(1, 3, 1);
   vm_wait<4>();
   raw_barrier();
+  // Ping-pong the two wave groups (wm = 0 / 1; each SIMD holds one wave of each): group 1 runs one
+  // barrier behind, so on every SIMD one wave issues its ds_reads + glds while the other one runs
+  // its MFMA cluster (guide §5 template, "if(wr==1) s_barrier").  Staging stays correct: a half-tile
+  // is restaged >= 1 phase after its last read and read >= 1 phase after the wait that retires it,
+  // which holds for both groups with a one-barrier offset.
+  if (wm == 1) raw_barrier();
 
   for (int kt = 0; kt < nk; kt += 2) {
     const bool odd_ok = kt + 1 < nk;  // the odd K-tile of this iteration exists
@@ -206,6 +212,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     if (odd_ok) mma(3);
     raw_barrier();
   }
+  if (wm == 0) raw_barrier();  // re-align the groups' barrier counts
   vm_wait<0>();  // drain the clamped tail prefetches before LDS is reused by the epilogue
   raw_barrier();
 

@@ -534,12 +534,12 @@ class _MLPGelu(Function):
 
 
 def fused_mlp_available() -> bool:
-    """Fused-epilogue MLP (MFT_FUSED_MLP=1) on the 8-phase gemm8.hip kernel.  Off by default: in
-    the GPT-2 bench step on MI355X it is break-even (1.318M vs 1.320M tok/s, A/B in one call) --
-    the GELU passes it removes are paid back by gemm8's main loop (0.83-0.99 PF/s at these shapes)
-    trailing hipBLASLt (0.91-1.32 PF/s)."""
+    """Fused-epilogue MLP on the 8-phase gemm8.hip kernel (MFT_FUSED_MLP=0 disables).  Measured in
+    the GPT-2 LoRA bench step on MI355X (A/B in one call): 1.338M vs 1.321M tok/s unfused; isolated
+    at M=32k: fc+GELU 198 us vs 215 (hipBLASLt addmm + GELU kernel), mlp_proj dx+dGELU 209 us vs
+    275 (hipBLASLt mm + GELU-backward kernel)."""
     import os
-    return os.environ.get("MFT_FUSED_MLP", "0") == "1"
+    return os.environ.get("MFT_FUSED_MLP", "1") != "0"
 
 
 def mlp_gelu(x, fc, proj):
