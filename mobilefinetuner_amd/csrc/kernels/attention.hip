@@ -18,6 +18,8 @@
 // of 64 keys are staged row-major in LDS with 16-B vector copies; S = Q K^T takes K by rows, and
 // O += P V takes V through ds_read_b64_tr_b16 transposed reads (no transposed copy of V).
 // Online softmax in base 2 with the scale folded into one multiplier.
+#include <cstdlib>
+
 #include "mfma.h"
 #include "kernels.h"
 
@@ -374,8 +376,6 @@ __global__ void gqa_reduce_kernel(const bf16_t* __restrict__ in, bf16_t* __restr
 // ============================================================================================
 constexpr int kShortS = 128;
 
-__host__ __device__ constexpr int short_ldp() { return kShortS + 8; }
-
 // per-wave [16][D] C-layout tile (acc[n][i] = row 4(l>>4)+i, col n*16+(l&15)) -> 16 global rows
 template <int D>
 __device__ __forceinline__ void store_tile16(bf16_t* scratch, int ld, const f32x4_t* acc, const float* rs,
@@ -400,22 +400,26 @@ __device__ __forceinline__ void store_tile16(bf16_t* scratch, int ld, const f32x
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---- v2: P (fwd) / P^T, dS^T (bwd) stay in registers -------------------------------------------
+// Scores are computed transposed (S^T = K Q^T: keys in C rows, queries in C columns), so two
+// 16-key C blocks ARE the A operand of the next MFMA over keys (pack_c2a / frag_tr_perm, mfma.h):
+// no LDS round trip for P, less LDS per workgroup -> several workgroups per CU overlap their loads.
+// Forward LDS = K + V (32 KB) + a 2.3 KB output staging tile per wave.
 template <int D>
-__global__ __launch_bounds__(512) void attn_fwd_short_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
-                                                             const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
-                                                             float* __restrict__ lse, AttnStrides qs, AttnStrides ks,
-                                                             AttnStrides vs, AttnStrides os, int H, int Hkv, int S,
-                                                             float scale, int causal, const int* __restrict__ kv_lens) {
-  constexpr int SM = kShortS, LDP = short_ldp(), NB = SM / 16, CPR = D / 8;
+__global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                              const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+                                                              float* __restrict__ lse, AttnStrides qs, AttnStrides ks,
+                                                              AttnStrides vs, AttnStrides os, int H, int Hkv, int S,
+                                                              float scale, int causal, const int* __restrict__ kv_lens) {
+  constexpr int SM = kShortS, NB = SM / 16, CPR = D / 8, LDO = D + 8;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  bf16_t* Ks = smem;            // [SM][D]
-  bf16_t* Vs = Ks + SM * D;     // [SM][D]
-  bf16_t* Pw = Vs + SM * D + (threadIdx.x >> 6) * 16 * LDP;  // per-wave [16][LDP]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  bf16_t* Ks = smem;                                      // [SM][D]
+  bf16_t* Vs = Ks + SM * D;                               // [SM][D]
+  bf16_t* Ow = Vs + SM * D + (threadIdx.x >> 6) * 16 * LDO;  // per-wave [16][LDO] output staging
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int h = blockIdx.x, b = blockIdx.y, hk = h / (H / Hkv);
   const int kv_len = kv_lens ? min(kv_lens[b], S) : S;
   const float c2 = scale * kLog2e;
-  // issue every global load first (K, V pieces and this wave's Q fragments), then fill LDS
   constexpr int PER = SM * CPR / 512;
   u16x8_t kr[PER], vr[PER];
 #pragma unroll
@@ -425,12 +429,13 @@ __global__ __launch_bounds__(512) void attn_fwd_short_kernel(const bf16_t* __res
     kr[j] = ok ? *reinterpret_cast<const u16x8_t*>(k + b * ks.sb + (long)r * ks.ss + hk * ks.sh + ch * 8) : u16x8_t{};
     vr[j] = ok ? *reinterpret_cast<const u16x8_t*>(v + b * vs.sb + (long)r * vs.ss + hk * vs.sh + ch * 8) : u16x8_t{};
   }
+  // this wave's 16 queries as the B operand of S^T = K Q^T (lane: Q[16w + (l&15)][8g + j + 32s])
   bf16x8_t qf[D / 32];
   {
     const int qr = 16 * w + (lane & 15);
 #pragma unroll
     for (int s = 0; s < D / 32; ++s)
-      qf[s] = qr < S ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qr * qs.ss + h * qs.sh + s * 32 + 8 * (lane >> 4))
+      qf[s] = qr < S ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qr * qs.ss + h * qs.sh + s * 32 + 8 * g)
                      : bf16x8_t{};
   }
 #pragma unroll
@@ -440,96 +445,88 @@ __global__ __launch_bounds__(512) void attn_fwd_short_kernel(const bf16_t* __res
     *reinterpret_cast<u16x8_t*>(Vs + r * D + ch * 8) = vr[j];
   }
   __syncthreads();
-  if (16 * w >= S) return;  // no query rows for this wave (after the only barrier)
-  const int nbmax = causal ? w + 1 : NB;  // key blocks of 16 visible to rows 16w..16w+15
-  f32x4_t sacc[NB];
+  if (16 * w >= S) return;
+  const int nbmax = causal ? w + 1 : NB;
+  const int qi = 16 * w + (lane & 15);  // this lane's query (C column)
+  f32x4_t st[NB];                        // st[kb][i] = S^T[key = 16 kb + 4g + i][qi]
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb) {
-    sacc[nb] = zero4();
-    if (nb < nbmax) {
+  for (int kb = 0; kb < NB; ++kb) {
+    st[kb] = zero4();
+    if (kb < nbmax) {
 #pragma unroll
-      for (int s = 0; s < D / 32; ++s) sacc[nb] = mfma16(qf[s], frag_row(Ks, D, nb * 16, s * 32), sacc[nb]);
+      for (int s = 0; s < D / 32; ++s) st[kb] = mfma16(frag_row(Ks, D, kb * 16, s * 32), qf[s], st[kb]);
     }
   }
-  float mrow[4], lrow[4];
+  float mx = -INFINITY;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int qi = 16 * w + 4 * (lane >> 4) + i;
-    float mx = -INFINITY;
+  for (int kb = 0; kb < NB; ++kb)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const int kj = nb * 16 + (lane & 15);
-      const bool ok = nb < nbmax && kj < kv_len && (!causal || kj <= qi);
-      const float sv = ok ? sacc[nb][i] * c2 : -INFINITY;
-      sacc[nb][i] = sv;
+    for (int i = 0; i < 4; ++i) {
+      const int kj = 16 * kb + 4 * g + i;
+      const bool ok = kb < nbmax && kj < kv_len && (!causal || kj <= qi);
+      const float sv = ok ? st[kb][i] * c2 : -INFINITY;
+      st[kb][i] = sv;
       mx = fmaxf(mx, sv);
     }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float ms = mx == -INFINITY ? 0.f : mx;
+  float rs = 0.f;
 #pragma unroll
-    for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
-    const float ms = mx == -INFINITY ? 0.f : mx;
-    float rs = 0.f;
+  for (int kb = 0; kb < NB; ++kb)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const float p = exp2f(sacc[nb][i] - ms);
-      sacc[nb][i] = p;
+    for (int i = 0; i < 4; ++i) {
+      const float p = exp2f(st[kb][i] - ms);
+      st[kb][i] = p;
       rs += p;
     }
-#pragma unroll
-    for (int o2 = 1; o2 < 16; o2 <<= 1) rs += __shfl_xor(rs, o2, 64);
-    mrow[i] = mx;
-    lrow[i] = rs;
-  }
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) Pw[(4 * (lane >> 4) + i) * LDP + nb * 16 + (lane & 15)] = f2bf(sacc[nb][i]);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  rs += __shfl_xor(rs, 16, 64);
+  rs += __shfl_xor(rs, 32, 64);
+  // O = P V over 32-key steps; P's A fragment comes straight from two S^T blocks
   f32x4_t acc[D / 16];
 #pragma unroll
   for (int n = 0; n < D / 16; ++n) acc[n] = zero4();
-  const int ksmax = causal ? (16 * w + 15) / 32 + 1 : SM / 32;
 #pragma unroll
   for (int kk = 0; kk < SM / 32; ++kk) {
-    if (kk < ksmax) {
-      const bf16x8_t pa = frag_row(Pw, LDP, 0, kk * 32);
+    if (2 * kk < nbmax) {
+      const bf16x8_t pa = pack_c2a(st[2 * kk], st[2 * kk + 1]);
 #pragma unroll
-      for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr(Vs, D, kk * 32, n * 16), acc[n]);
+      for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr_perm(Vs, D, kk * 32, n * 16), acc[n]);
     }
   }
+  // acc rows are queries 4g+i: fetch their 1/l from the lane that owns that query column
+  const float inv_own = rs > 0.f ? 1.f / rs : 0.f;
+  if (g == 0 && qi < S)
+    lse[((long)b * H + h) * S + qi] = rs > 0.f ? (mx + log2f(rs)) / kLog2e : 1e30f;
   float inv[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    inv[i] = lrow[i] > 0.f ? 1.f / lrow[i] : 0.f;
-    const int qi = 16 * w + 4 * (lane >> 4) + i;
-    if ((lane & 15) == 0 && qi < S)
-      lse[((long)b * H + h) * S + qi] = lrow[i] > 0.f ? (mrow[i] + log2f(lrow[i])) / kLog2e : 1e30f;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  store_tile16<D>(Pw, LDP, acc, inv, o, os, b, h, 16 * w, min(16, S - 16 * w));
+  for (int i = 0; i < 4; ++i) inv[i] = __shfl(inv_own, 4 * g + i, 64);
+  store_tile16<D>(Ow, LDO, acc, inv, o, os, b, h, 16 * w, min(16, S - 16 * w));
 }
 
+// Backward v2.  Phase 1 (wave w owns keys 16w..16w+15): per pair of 16-query blocks, S = Q K^T and
+// dP = dO V^T land in C layout with queries in rows and this wave's keys in columns -- exactly the
+// A operand (m = key, k = query) of dV += P^T dO and dK += dS^T Q after pack_c2a, with the B rows
+// permuted to match (frag_tr_perm).  dS is kept packed in registers; after a block barrier (V and
+// dO dead) it is written to a swizzled [query][key] image that aliases them, and phase 2 (wave w
+// owns queries 16w..) forms dQ = dS K.  LDS = K, V, Q, dO (64 KB) + lse/delta: two workgroups per CU.
 template <int D>
-__global__ __launch_bounds__(512) void attn_bwd_short_kernel(
+__global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     bf16_t* __restrict__ dq, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, AttnStrides qs, AttnStrides ks,
     AttnStrides vs, AttnStrides ost, AttnStrides dos, AttnStrides dqs, AttnStrides dks, AttnStrides dvs, int H, int Hkv,
     int S, float scale, int causal, const int* __restrict__ kv_lens, int dkv_per_qhead) {
-  constexpr int SM = kShortS, LDT = short_ldp(), NB = SM / 16, CPR = D / 8;
+  constexpr int SM = kShortS, CPR = D / 8;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  bf16_t* Ks = smem;              // [SM][D]
-  bf16_t* Vs = Ks + SM * D;       // [SM][D]
-  bf16_t* Qs = Vs + SM * D;       // [SM][D]
-  bf16_t* dOs = Qs + SM * D;      // [SM][D]
-  bf16_t* DST = dOs + SM * D;     // [SM keys][LDT]  dS^T * scale
-  bf16_t* PTw = DST + SM * LDT + (threadIdx.x >> 6) * 16 * LDT;  // per-wave [16][LDT]
-  float* lse_s = reinterpret_cast<float*>(DST + SM * LDT + 8 * 16 * LDT);  // [SM]
-  float* del_s = lse_s + SM;                                             // [SM]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  bf16_t* Ks = smem;           // [SM][D]
+  bf16_t* Vs = Ks + SM * D;    // [SM][D]   } phase 2: dS image [SM q][SM keys], 16-B chunks
+  bf16_t* dOs = Vs + SM * D;   // [SM][D]   }   swizzled chunk ^ (q & 15)
+  bf16_t* Qs = dOs + SM * D;   // [SM][D]   (after phase 1: per-wave [16][D] output staging)
+  bf16_t* DS = Vs;
+  float* lse_s = reinterpret_cast<float*>(Qs + SM * D);  // [SM]
+  float* del_s = lse_s + SM;                             // [SM]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
   const int h = blockIdx.x, b = blockIdx.y, hk = h / (H / Hkv);
   const int kv_len = kv_lens ? min(kv_lens[b], S) : S;
   const float c2 = scale * kLog2e;
@@ -566,82 +563,84 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(
   }
   __syncthreads();
 
-  // ---- phase 1: wave w owns keys 16w..16w+15: P^T, dS^T rows, dV and dK
+  // ---- phase 1: keys 16w..16w+15
+  const int key = 16 * w + c16;  // this lane's key (C column)
   f32x4_t dKa[D / 16], dVa[D / 16];
 #pragma unroll
   for (int n = 0; n < D / 16; ++n) { dKa[n] = zero4(); dVa[n] = zero4(); }
-  const int nbmin = causal ? w : 0;  // query blocks of 16 that can see these keys
-  {
-    f32x4_t st[NB], dpt[NB];
+  uint32_t dsp[SM / 16][2];  // dS (bf16 pairs) per 16-query block, kept for the phase-2 image
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      st[nb] = zero4();
-      dpt[nb] = zero4();
-      if (nb >= nbmin) {
+  for (int kk = 0; kk < SM / 32; ++kk) {
+    const bool live = !causal || 32 * kk + 31 >= 16 * w;  // some query of this step sees these keys
+    f32x4_t sc[2], dp[2];
 #pragma unroll
-        for (int s = 0; s < D / 32; ++s) {
-          st[nb] = mfma16(frag_row(Ks, D, 16 * w, s * 32), frag_row(Qs, D, nb * 16, s * 32), st[nb]);
-          dpt[nb] = mfma16(frag_row(Vs, D, 16 * w, s * 32), frag_row(dOs, D, nb * 16, s * 32), dpt[nb]);
+    for (int t = 0; t < 2; ++t) {
+      sc[t] = zero4();
+      dp[t] = zero4();
+      if (live) {
+#pragma unroll
+        for (int s2 = 0; s2 < D / 32; ++s2) {
+          sc[t] = mfma16(frag_row(Qs, D, 32 * kk + 16 * t, s2 * 32), frag_row(Ks, D, 16 * w, s2 * 32), sc[t]);
+          dp[t] = mfma16(frag_row(dOs, D, 32 * kk + 16 * t, s2 * 32), frag_row(Vs, D, 16 * w, s2 * 32), dp[t]);
         }
       }
-    }
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const int qi = nb * 16 + (lane & 15);
-      const float lq = lse_s[qi], dq_ = del_s[qi];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int kr = 16 * w + 4 * (lane >> 4) + i;
-        const bool ok = nb >= nbmin && qi < S && kr < kv_len && (!causal || kr <= qi);
-        const float p = ok ? exp2f(st[nb][i] * c2 - lq) : 0.f;
-        const float ds = p * (dpt[nb][i] - dq_) * scale;
-        PTw[(4 * (lane >> 4) + i) * LDT + qi] = f2bf(p);
-        DST[kr * LDT + qi] = f2bf(ds);
+        const int qi = 32 * kk + 16 * t + 4 * g + i;
+        const bool ok = live && qi < S && key < kv_len && (!causal || key <= qi);
+        const float p = ok ? exp2f(sc[t][i] * c2 - lse_s[qi]) : 0.f;
+        sc[t][i] = p;                                     // P
+        dp[t][i] = p * (dp[t][i] - del_s[qi]) * scale;    // dS
+      }
+      dsp[2 * kk + t][0] = pack_bf2(dp[t][0], dp[t][1]);
+      dsp[2 * kk + t][1] = pack_bf2(dp[t][2], dp[t][3]);
+    }
+    if (live) {
+      const bf16x8_t pa = pack_c2a(sc[0], sc[1]);
+      const bf16x8_t da = pack_c2a(dp[0], dp[1]);
+#pragma unroll
+      for (int n = 0; n < D / 16; ++n) {
+        dVa[n] = mfma16(pa, frag_tr_perm(dOs, D, 32 * kk, n * 16), dVa[n]);
+        dKa[n] = mfma16(da, frag_tr_perm(Qs, D, 32 * kk, n * 16), dKa[n]);
       }
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  {
-    const int ksmin = causal ? (16 * w) / 32 : 0;
+  __syncthreads();  // V, dO (and Q) are dead from here on
+  // dS image [q][key]: element (q, key) at q*SM + ((key/8 ^ (q&15)) * 8) + key%8
 #pragma unroll
-    for (int kk = 0; kk < SM / 32; ++kk) {
-      if (kk >= ksmin) {
-        const bf16x8_t pa = frag_row(PTw, LDT, 0, kk * 32);
-        const bf16x8_t da = frag_row(DST, LDT, 16 * w, kk * 32);
+  for (int qb = 0; qb < SM / 16; ++qb)
 #pragma unroll
-        for (int n = 0; n < D / 16; ++n) {
-          dVa[n] = mfma16(pa, frag_tr(dOs, D, kk * 32, n * 16), dVa[n]);
-          dKa[n] = mfma16(da, frag_tr(Qs, D, kk * 32, n * 16), dKa[n]);
-        }
-      }
+    for (int i = 0; i < 4; ++i) {
+      const int qi = 16 * qb + 4 * g + i;
+      const uint32_t pr = dsp[qb][i >> 1];
+      const bf16_t val = (i & 1) ? (bf16_t)(pr >> 16) : (bf16_t)(pr & 0xFFFF);
+      DS[qi * SM + (((key >> 3) ^ (qi & 15)) << 3) + (key & 7)] = val;
     }
+  // dK, dV of this wave's keys (staging tile in the dead Q region)
+  const int hout = dkv_per_qhead ? h : hk;
+  const float one[4] = {1.f, 1.f, 1.f, 1.f};
+  bf16_t* T = Qs + w * 16 * D;
+  if (16 * w < S) {
+    store_tile16<D>(T, D, dKa, one, dk, dks, b, hout, 16 * w, min(16, S - 16 * w));
+    store_tile16<D>(T, D, dVa, one, dv, dvs, b, hout, 16 * w, min(16, S - 16 * w));
   }
-  __syncthreads();  // every wave's dS^T rows are in LDS
+  __syncthreads();
 
-  // ---- phase 2: wave w owns queries 16w..16w+15: dQ = dS K
+  // ---- phase 2: queries 16w..16w+15: dQ = dS K
   f32x4_t dQa[D / 16];
 #pragma unroll
   for (int n = 0; n < D / 16; ++n) dQa[n] = zero4();
-  {
-    const int ksmax = causal ? (16 * w + 15) / 32 + 1 : SM / 32;
+  const int ksmax = causal ? (16 * w + 15) / 32 + 1 : SM / 32;
 #pragma unroll
-    for (int kk = 0; kk < SM / 32; ++kk) {
-      if (kk < ksmax) {
-        const bf16x8_t a = frag_tr(DST, LDT, kk * 32, 16 * w);
+  for (int kk = 0; kk < SM / 32; ++kk) {
+    if (kk < ksmax) {
+      const int qr = 16 * w + c16, ch = 4 * kk + g;
+      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(DS + qr * SM + ((ch ^ (qr & 15)) << 3));
 #pragma unroll
-        for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(a, frag_tr(Ks, D, kk * 32, n * 16), dQa[n]);
-      }
+      for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(a, frag_tr(Ks, D, kk * 32, n * 16), dQa[n]);
     }
   }
-  if (16 * w >= S) return;
-  const float one[4] = {1.f, 1.f, 1.f, 1.f};
-  const int nrows = min(16, S - 16 * w);
-  const int hout = dkv_per_qhead ? h : hk;
-  store_tile16<D>(PTw, LDT, dQa, one, dq, dqs, b, h, 16 * w, nrows);
-  store_tile16<D>(PTw, LDT, dKa, one, dk, dks, b, hout, 16 * w, nrows);
-  store_tile16<D>(PTw, LDT, dVa, one, dv, dvs, b, hout, 16 * w, nrows);
+  if (16 * w < S) store_tile16<D>(T, D, dQa, one, dq, dqs, b, h, 16 * w, min(16, S - 16 * w));
 }
 
 bool attn_short_path(int D, int Sq, int Sk, int window) {
@@ -654,16 +653,16 @@ template <int D>
 static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
   if constexpr (D == 64) {
     if (attn_short_path(D, a.Sq, a.Sk, a.window)) {
-      const size_t shm = sizeof(bf16_t) * (2 * kShortS * D + 8 * 16 * short_ldp());
+      const size_t shm = sizeof(bf16_t) * (2 * kShortS * D + 8 * 16 * (D + 8));
       static bool attr = false;
       if (!attr) {
-        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_short_kernel<D>,
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_short2_kernel<D>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
       }
-      attn_fwd_short_kernel<D><<<dim3(a.H, a.B), 512, shm, stream>>>(a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st),
-                                                                      mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.scale,
-                                                                      a.causal, a.kv_lens);
+      attn_fwd_short2_kernel<D><<<dim3(a.H, a.B), 512, shm, stream>>>(a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st),
+                                                                       mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.scale,
+                                                                       a.causal, a.kv_lens);
       return;
     }
   }
@@ -679,15 +678,15 @@ template <int D>
 static void bwd_launch(const AttnBwdArgs& a, hipStream_t stream) {
   if constexpr (D == 64) {
     if (attn_short_path(D, a.Sq, a.Sk, a.window)) {
-      const size_t shm = sizeof(bf16_t) * (4 * kShortS * D + 2 * kShortS * short_ldp()) + sizeof(float) * 2 * kShortS;
+      const size_t shm = sizeof(bf16_t) * 4 * kShortS * D + sizeof(float) * 2 * kShortS;
       static bool attr = false;
       if (!attr) {
-        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_short_kernel<D>,
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_short2_kernel<D>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
       }
       const int per_qhead = a.H != a.Hkv;
-      attn_bwd_short_kernel<D><<<dim3(a.H, a.B), 512, shm, stream>>>(
+      attn_bwd_short2_kernel<D><<<dim3(a.H, a.B), 512, shm, stream>>>(
           a.q, a.k, a.v, a.o, a.dout, a.lse, a.dq, per_qhead ? a.dk_tmp : a.dk, per_qhead ? a.dv_tmp : a.dv,
           mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.o_st), mk(a.do_st), mk(a.dq_st),
           per_qhead ? mk(a.tmp_st) : mk(a.dk_st), per_qhead ? mk(a.tmp_st) : mk(a.dv_st), a.H, a.Hkv, a.Sq, a.scale,

@@ -42,6 +42,33 @@ __device__ __forceinline__ bf16x8_t frag_tr(const bf16_t* base, int ld, int r0, 
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
+// Register-to-register operand reuse: two 16x16 C/D blocks c0, c1 whose COLUMNS index the next
+// MFMA's m and whose ROWS index its k (k 0..15 in c0, 16..31 in c1) become an A operand without an
+// LDS round trip if the k index is permuted consistently in both operands (the MFMA sums over k):
+//   A lane l, element j  <-  k = 4*(l>>4) + j (j < 4, from c0) | 16 + 4*(l>>4) + (j - 4) (j >= 4, c1)
+// pack_c2a builds that A fragment; frag_tr_perm reads the matching B fragment (rows permuted the
+// same way) from a row-major LDS image with two ds_read_b64_tr_b16.
+__device__ __forceinline__ bf16x8_t pack_c2a(f32x4_t c0, f32x4_t c1) {
+  u16x8_t u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u[i] = f2bf(c0[i]);
+    u[4 + i] = f2bf(c1[i]);
+  }
+  return __builtin_bit_cast(bf16x8_t, u);
+}
+
+// lane holds M[r0 + 4*(l>>4) + j][c0 + (l&15)] (j < 4) and M[r0 + 16 + 4*(l>>4) + j - 4][c0 + (l&15)] (j >= 4)
+__device__ __forceinline__ bf16x8_t frag_tr_perm(const bf16_t* base, int ld, int r0, int c0) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const bf16_t* a0 = base + (r0 + 4 * g + q) * ld + c0 + 4 * p;
+  s16x4_t lo = ds_tr16(a0);
+  s16x4_t hi = ds_tr16(a0 + 16 * ld);
+  s16x8_t r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
 __device__ __forceinline__ f32x4_t zero4() { return f32x4_t{0.f, 0.f, 0.f, 0.f}; }
 
 }  // namespace mft
