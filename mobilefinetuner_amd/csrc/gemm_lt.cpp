@@ -244,14 +244,21 @@ Tensor lt_linear(Tensor x, Tensor w, c10::optional<Tensor> bias) {
 }
 
 // dx[M, K] = dy[M, N] W[N, K]  (data gradient of a Linear; W may be a row-strided view)
-Tensor lt_mm_dx(Tensor dy, Tensor w) {
+Tensor lt_mm_dx(Tensor dy, Tensor w, c10::optional<Tensor> out) {
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16 &&
                   dy.dim() == 2 && w.dim() == 2 && dy.stride(1) == 1 && w.stride(1) == 1, "lt_mm_dx: bf16 2-D row-major");
   const long M = dy.size(0), N = dy.size(1), K = w.size(1);
   TORCH_CHECK(w.size(0) == N, "lt_mm_dx: shapes");
   c10::DeviceGuard g(dy.device());
-  auto dx = torch::empty({M, K}, dy.options());
-  Problem p{dy.get_device(), 0, 0, HIPBLASLT_EPILOGUE_DEFAULT, 0, K, M, N, w.stride(0), dy.stride(0), K, 0};
+  Tensor dx;
+  if (out.has_value() && out->defined()) {
+    dx = *out;
+    TORCH_CHECK(dx.size(0) == M && dx.size(1) == K && dx.stride(1) == 1 && dx.scalar_type() == torch::kBFloat16,
+                "lt_mm_dx: out must be [M, K] bf16 row-major");
+  } else {
+    dx = torch::empty({M, K}, dy.options());
+  }
+  Problem p{dy.get_device(), 0, 0, HIPBLASLT_EPILOGUE_DEFAULT, 0, K, M, N, w.stride(0), dy.stride(0), dx.stride(0), 0};
   run(p, w.data_ptr(), dy.data_ptr(), dx.data_ptr(), nullptr, nullptr);
   return dx;
 }
