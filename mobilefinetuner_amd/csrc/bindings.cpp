@@ -384,7 +384,8 @@ Tensor add_bf16(Tensor a, Tensor b) {
 // C = epi(alpha * A op(B)); A [M,K]; B [N,K] (b_nn = false) or [K,N] (b_nn = true).
 // Returns {C, aux}: aux is the pre-activation written by GEMM_EPI_BIAS_GELU.
 std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::optional<Tensor> bias,
-                            c10::optional<Tensor> aux, double alpha, int64_t bm, c10::optional<Tensor> out) {
+                            c10::optional<Tensor> aux, double alpha, int64_t bm, c10::optional<Tensor> out,
+                            c10::optional<Tensor> lora_u, c10::optional<Tensor> lora_w) {
   CHECK_CUDA(A); CHECK_BF16(A); CHECK_BF16(B);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "gemm: row-contiguous 2-D operands");
   const int M = A.size(0), K = A.size(1);
@@ -420,6 +421,15 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
   a.bias = bias.has_value() ? bp(*bias) : nullptr;
   a.aux = X.defined() ? bp(X) : nullptr; a.ldaux = X.defined() ? X.stride(0) : 0;
   a.M = M; a.N = N; a.K = K; a.alpha = (float)alpha;
+  if (epi == mft::GEMM_EPI_LORA) {
+    TORCH_CHECK(bm == 8 && !b_nn && lora_u.has_value() && lora_w.has_value(), "gemm: LoRA epilogue = cfg 8, NT, u and w");
+    CHECK_BF16((*lora_u)); CHECK_BF16((*lora_w));
+    TORCH_CHECK(lora_u->size(0) == M && lora_w->size(1) == N && lora_u->size(1) == lora_w->size(0) &&
+                lora_u->stride(1) == 1 && lora_w->stride(1) == 1, "gemm: LoRA u [M, r], w [r, N]");
+    a.lora_u = bp(*lora_u); a.ld_lu = lora_u->stride(0);
+    a.lora_w = bp(*lora_w); a.ld_lw = lora_w->stride(0);
+    a.lora_r = lora_u->size(1);
+  }
   if (bm == 8 && !b_nn) mft::gemm8(a, (int)epi, stream());  // cfg 8: 8-phase pipelined 256x256 NT kernel
   else mft::gemm(a, b_nn, (int)epi, (int)bm, stream());
   return {C, X};
@@ -479,7 +489,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_update", &lora_update);
   m.def("lora_wgrad", &lora_wgrad);
   m.def("lora_merge", &lora_merge);
-  m.def("gemm", &gemm_op);
+  m.def("gemm", &gemm_op, py::arg("A"), py::arg("B"), py::arg("b_nn"), py::arg("epi"), py::arg("bias"), py::arg("aux"),
+        py::arg("alpha"), py::arg("cfg"), py::arg("out"), py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none());
   m.def("zero_cols", &zero_cols);
   m.def("colsum_acc", &colsum_acc);
   m.def("rope_apply", &rope_apply);

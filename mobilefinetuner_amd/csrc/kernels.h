@@ -54,7 +54,8 @@ void attn_bwd(const AttnBwdArgs& a, hipStream_t s);
 bool attn_short_path(int D, int Sq, int Sk, int window);
 
 // ---------------------------------------------------------------- GEMM (gemm.hip)
-enum GemmEpi { GEMM_EPI_NONE = 0, GEMM_EPI_BIAS = 1, GEMM_EPI_BIAS_GELU = 2, GEMM_EPI_DGELU = 3, GEMM_EPI_F32ACC = 4 };
+enum GemmEpi { GEMM_EPI_NONE = 0, GEMM_EPI_BIAS = 1, GEMM_EPI_BIAS_GELU = 2, GEMM_EPI_DGELU = 3, GEMM_EPI_F32ACC = 4,
+               GEMM_EPI_LORA = 5 };
 struct GemmArgs {
   const bf16_t* A;
   long lda;  // A [M, K] row-major
@@ -67,6 +68,13 @@ struct GemmArgs {
   long ldaux;  // BIAS_GELU: pre-activation out; DGELU: pre-activation in
   int M, N, K;
   float alpha;
+  // GEMM_EPI_LORA (gemm8 only): C += lora_u[M, lora_r] . lora_w[lora_r, N] (rank-r update fused
+  // into the epilogue, e.g. dx = dy W + v A of a LoRA Linear's backward)
+  const bf16_t* lora_u;
+  long ld_lu;
+  const bf16_t* lora_w;
+  long ld_lw;
+  int lora_r;
 };
 bool gemm_supported(int M, int N, int K);
 // cfg: tile configuration (gemm.hip launch_e): 0 = 256x256, 1 = 128x256, 2 = 128x128, 3 = 256x128

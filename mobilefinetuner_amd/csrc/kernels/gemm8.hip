@@ -293,6 +293,41 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
             T[tr * LDT + tc] = f2bf(gelu_tanh(acc[q][i][j][r]));
           }
     }
+    if constexpr (EPI == GEMM_EPI_LORA) {
+      // rank-r update while moving the staged tile out: each lane owns one 8-column chunk of 4 rows
+      // (the to_global mapping), so its 8 x r slice of lora_w is loaded once per 8 ranks and each
+      // row of lora_u is one 16-B load per 8 ranks (r <= 32, multiple of 8)
+      sync_wave();
+      const int ch = lane & 3, col = cbase + ch * 8, colc = min(col, g.N - 8);
+      float o[4][8];
+#pragma unroll
+      for (int it = 0; it < 4; ++it)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[it][e] = bf2f(T[(it * 16 + (lane >> 2)) * LDT + ch * 8 + e]);
+#pragma unroll 1
+      for (int t8 = 0; t8 < g.lora_r; t8 += 8) {
+        u16x8_t w[8];  // kept packed (32 VGPRs; the accumulators of later quadrants are still live)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) w[t] = *reinterpret_cast<const u16x8_t*>(g.lora_w + (long)(t8 + t) * g.ld_lw + colc);
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int row = min(rbase + it * 16 + (lane >> 2), g.M - 1);
+          float u[8];
+          load8(g.lora_u + (long)row * g.ld_lu + t8, u);
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[it][e] += u[t] * bf2f(w[t][e]);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int row = rbase + it * 16 + (lane >> 2);
+        if (row < g.M && col < g.N) store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, o[it]);
+      }
+      sync_wave();
+      continue;
+    }
     to_global(reinterpret_cast<bf16_t*>(g.C), g.ldc);
   }
 }
@@ -320,6 +355,13 @@ void gemm8(const GemmArgs& g, int epi, hipStream_t st) {
     case GEMM_EPI_BIAS_GELU: launch8<GEMM_EPI_BIAS_GELU>(g, st); break;
     case GEMM_EPI_DGELU: launch8<GEMM_EPI_DGELU>(g, st); break;
     case GEMM_EPI_F32ACC: launch8<GEMM_EPI_F32ACC>(g, st); break;
+    case GEMM_EPI_LORA:
+      if (g.lora_r <= 0 || g.lora_r > 32 || g.lora_r % 8 || g.ld_lu % 8) {
+        fprintf(stderr, "mft::gemm8: LoRA epilogue needs rank %% 8 == 0, <= 32 (got %d)\n", g.lora_r);
+        abort();
+      }
+      launch8<GEMM_EPI_LORA>(g, st);
+      break;
     default: fprintf(stderr, "mft::gemm8: bad epilogue %d\n", epi); abort();
   }
 }

@@ -13,6 +13,7 @@ engines can launch bucket all-reduces while backward is still running.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch.autograd import Function
@@ -457,7 +458,7 @@ def linear(x, w, b=None):
     return _Linear.apply(x, w, b)
 
 
-GEMM_EPI_NONE, GEMM_EPI_BIAS, GEMM_EPI_BIAS_GELU, GEMM_EPI_DGELU, GEMM_EPI_F32ACC = 0, 1, 2, 3, 4
+GEMM_EPI_NONE, GEMM_EPI_BIAS, GEMM_EPI_BIAS_GELU, GEMM_EPI_DGELU, GEMM_EPI_F32ACC, GEMM_EPI_LORA = 0, 1, 2, 3, 4, 5
 
 
 def weight_t(p):
@@ -666,7 +667,7 @@ class _LoRALinearAug(Function):
         y = gemm_linear(xa2, waug, bc)
         ctx.save_for_backward(xa)  # the input itself (a no-grad view of it must not be saved)
         ctx.params = ab
-        ctx.slices, ctx.waug, ctx.K = slices, waug, K
+        ctx.slices, ctx.waug, ctx.K, ctx.w = slices, waug, K, w
         ctx.s, ctx.shape = float(s), shape
         return y.view(*shape[:-1], y.shape[-1])
 
@@ -683,11 +684,26 @@ class _LoRALinearAug(Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dxa = None
+        ranks = [cw(ab[2 * i]).shape[0] for i in range(len(ctx.slices))]
+        fused = ctx.needs_input_grad[0] and _lora_epi_ok(ctx.slices, ranks, dy2, K)
         if ctx.needs_input_grad[0]:
-            dx = gemm_dx(dy2, ctx.waug[:, :K])
             # columns [K, Ka) of the input gradient are never read (the producers' backward reads
             # only their own K columns through the row stride), so they are left unwritten
             dxa = torch.empty(M, Ka, device=dy.device, dtype=dy.dtype)
+            if not fused:
+                dx = gemm_dx(dy2, ctx.waug[:, :K])
+        vs = []
+        if fused:
+            # every v_i = s dy_i B_i^T into one [M, sum r] buffer, then ONE gemm8 launch computes
+            # dx = dy W + [v_1 .. v_n] [A_1; ..; A_n] with the rank-r update in its epilogue
+            vall = torch.empty(M, sum(ranks), device=dy.device, dtype=dy.dtype)
+            o = 0
+            for i, (c0, n, dp, salt) in enumerate(ctx.slices):
+                C.lora_rowdot(dy2[:, c0:c0 + n], cw(ab[2 * i + 1]), vall[:, o:o + ranks[i]], s, 0.0, 0, None)
+                vs.append(vall[:, o:o + ranks[i]])
+                o += ranks[i]
+            acat = torch.cat([cw(ab[2 * i]) for i in range(len(ranks))]) if len(ranks) > 1 else cw(ab[0])
+            C.gemm(dy2, weight_t(ctx.w), False, GEMM_EPI_LORA, None, None, 1.0, 8, dxa[:, :K], vall, acat)
         grads = []
         ctr = dropout_counter(dy.device)
         off = K
@@ -697,9 +713,12 @@ class _LoRALinearAug(Function):
             Ac, Bc = cw(A), cw(B)
             R = Ac.shape[0]
             dys = dy2[:, c0:c0 + n]
-            v = torch.empty(M, R, device=dy.device, dtype=dy.dtype)
-            C.lora_rowdot(dys, Bc, v, s, 0.0, 0, None)  # v = s dy B^T
-            if dxa is not None:
+            if fused:
+                v = vs[i]
+            else:
+                v = torch.empty(M, R, device=dy.device, dtype=dy.dtype)
+                C.lora_rowdot(dys, Bc, v, s, 0.0, 0, None)  # v = s dy B^T
+            if dxa is not None and not fused:
                 # dx (+)= mask * (v A); the first slice also moves dx into the wide gradient buffer
                 C.lora_update(dx if first else dxa[:, :K], v, Ac, dxa[:, :K], 1.0, dp, salt, ctr)
                 first = False
@@ -722,11 +741,21 @@ class _LoRALinearAug(Function):
                     gB = tgt
             grads += [gA, gB]
             off += R
-        if dxa is not None and first:  # no slices (cannot happen via Linear, kept for safety)
+        if dxa is not None and first and not fused:  # no slices (cannot happen via Linear)
             dxa[:, :K].copy_(dx)
         if dxa is not None:
             dxa = dxa.view(ctx.shape)
         return (dxa, None, None, None, None, None, None, *grads)
+
+
+def _lora_epi_ok(slices, ranks, dy2, K) -> bool:
+    """The fused dx path (gemm8 GEMM_EPI_LORA) needs no LoRA dropout (the mask would apply to v A
+    only), sum(r) a multiple of 8 up to 32, and gemm8's shape contract (reduction dim % 64)."""
+    if os.environ.get("MFT_LORA_EPI", "1") == "0" or not dy2.is_cuda or dy2.dtype != torch.bfloat16:
+        return False
+    rt = sum(ranks)
+    return (all(sl[2] == 0.0 for sl in slices) and 0 < rt <= 32 and rt % 8 == 0 and dy2.shape[1] % 64 == 0
+            and K % 8 == 0)
 
 
 def lora_aug_cols(in_features: int, ranks) -> int:

@@ -134,6 +134,23 @@ def test_gemm_mfma(M, K, N, nn, bm):
     _close(acc, 1 + 2 * ref_, 0.05, 0.01, msg="gemm f32 acc")
 
 
+@pytest.mark.parametrize("M,N,K,R", [(300, 768, 2304, 8), (512, 256, 128, 24), (1000, 200, 320, 32)])
+def test_gemm8_lora_epilogue(M, N, K, R):
+    """gemm8 GEMM_EPI_LORA: C = A B^T + U W (the fused LoRA data-grad) vs fp32 torch; strided C."""
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    u = torch.randn(M, R, device=DEV).bfloat16()
+    w = (torch.randn(R, N, device=DEV) * 0.1).bfloat16()
+    wide = torch.full((M, N + 64), 7.0, device=DEV).bfloat16()
+    out = wide[:, :N]
+    C.gemm(a, b, False, 5, None, None, 1.0, 8, out, u, w)
+    ref_ = a.float() @ b.float().t() + u.float() @ w.float()
+    _close(out, ref_, 0.03, 0.01, msg="gemm8 lora")
+    assert (wide[:, N:].float() == 7.0).all()
+
+
 @pytest.mark.parametrize("dropout", [0.0, 0.2])
 def test_lora_augmented_k_matches_plain(dropout):
     """_LoRALinearAug ([x | u] . [W | sB^T] single GEMM) == _LoRALinear (GEMM + rank-r update)."""
