@@ -7,7 +7,7 @@ Synthetic token data + random-init GPT-2-124M weights (no network); one process 
 training step: forward, fused LM-head cross-entropy, backward through all 12 blocks, gradient
 all-reduce (N > 1), global grad-norm clip and the fused AdamW update.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config gpt2-lora|gemma3-270m-lora|gpt2-full|gpt2-xl-zero]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config gpt2-lora|gemma3-270m-lora|gpt2-full|gpt2-xl-zero|gpt2-xl-zero3] [--zero S]
                   [--batch B] [--seq S] [--no-graph]
 
 Prints ONE JSON line on rank 0.
@@ -45,6 +45,10 @@ CONFIGS = {
     # GPT-2 XL (1.5B) full fine-tuning with ZeRO-2 partitioned optimizer / reduce-scattered grads
     "gpt2-xl-zero": dict(model="gpt2-xl", mode="full", batch=16, seq=128, zero=2,
                          metric="tokens/sec GPT-2-XL full fine-tune ZeRO-2 seq128 (training, whole job)"),
+    # same with ZeRO-3: parameters partitioned too, all-gathered per block (prefetched one block
+    # ahead on a communication stream), gradients reduce-scattered per block during backward
+    "gpt2-xl-zero3": dict(model="gpt2-xl", mode="full", batch=16, seq=128, zero=3,
+                          metric="tokens/sec GPT-2-XL full fine-tune ZeRO-3 seq128 (training, whole job)"),
 }
 
 
@@ -80,6 +84,14 @@ def build(a, cfgd, dev, world):
     else:
         model.set_full_finetune()
         zero = cfgd.get("zero", 0) if world > 1 else 0
+        if a.zero >= 0:  # explicit override (e.g. measure ZeRO-3's gather/scatter cost on 1 GPU)
+            zero = a.zero
+        if zero == 3:
+            from mobilefinetuner_amd.parallel.zero3 import attach_zero3
+            z3 = attach_zero3(model, dev, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0)
+            desc = f"{name} full fine-tune ZeRO-3"
+            step = TrainStep(model, z3.flat, z3, grad_accum=a.grad_accum, dp=z3, use_graph=False)
+            return model, step, vocab, desc, sum(p.numel() for p in model.parameters())
         flat = FlatParams(model.named_parameters(), dev, pad_multiple=max(1, world))
         if zero:
             from mobilefinetuner_amd.parallel.zero import ZeroOptimizer, ZeroReducer
@@ -108,6 +120,8 @@ def main():
     ap.add_argument("--batch", type=int, default=int(os.environ.get("MFT_BENCH_BATCH", 0)),
                     help="micro-batch (sequences) per GPU (0 = the config's default)")
     ap.add_argument("--seq", type=int, default=0)
+    ap.add_argument("--zero", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
+                    help="full fine-tune configs: ZeRO stage override (-1 = the config's, used when N > 1)")
     ap.add_argument("--rank", type=int, default=8)
     ap.add_argument("--alpha", type=float, default=16.0)
     ap.add_argument("--targets", default="")

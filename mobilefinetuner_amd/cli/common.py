@@ -62,8 +62,9 @@ def add_shard_args(ap):
     g.add_argument("--shard_dir", default="")
     g.add_argument("--shard_budget_mb", type=int, default=512)
     g.add_argument("--shard_fp16_disk", type=int, default=1)
-    g.add_argument("--zero_stage", type=int, default=0, choices=[0, 1, 2],
-                   help="ZeRO partitioning of optimizer state (1) and gradients (2) across ranks")
+    g.add_argument("--zero_stage", type=int, default=0, choices=[0, 1, 2, 3],
+                   help="ZeRO partitioning across ranks: optimizer state (1), + gradients (2), + parameters "
+                        "with per-block all-gather / reduce-scatter (3)")
 
 
 def add_runtime_args(ap):

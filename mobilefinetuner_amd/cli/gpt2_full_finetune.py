@@ -2,7 +2,8 @@
 251-583; the reference never wired it into CMake).  All parameters train: fp32 masters + bf16 compute
 shadows in one flat buffer, fused AdamW (weight decay 0.01 default like the reference), gradients
 averaged over ranks with bucketed RCCL all-reduce overlapped with backward, or partitioned with
-``--zero_stage 1|2`` (reduce-scatter + all-gather over xGMI).  Saves an HF-keyed safetensors
+``--zero_stage 1|2|3`` (reduce-scatter + all-gather over xGMI; 3 also partitions the parameters,
+gathered per block, parallel/zero3.py).  Saves an HF-keyed safetensors
 checkpoint (Conv1D [in,out] layout) at ``--save_every`` and at the end.
 """
 from __future__ import annotations
@@ -73,7 +74,14 @@ def main(argv=None):
     a.seq_len = min(a.seq_len, model.cfg.n_positions)
     model.activation_checkpointing = a.activation_checkpointing
     model.set_full_finetune()
-    flat = FlatParams(model.named_parameters(), dev, pad_multiple=world if a.zero_stage else 1)
+    z3 = None
+    if a.zero_stage == 3:
+        from ..parallel.zero3 import attach_zero3
+        z3 = attach_zero3(model, dev, lr=a.lr, weight_decay=a.weight_decay, max_grad_norm=a.clip_grad_norm,
+                          l2_coupled=a.compat_l2_adam)
+        flat = z3.flat
+    else:
+        flat = FlatParams(model.named_parameters(), dev, pad_multiple=world if a.zero_stage else 1)
     log0(f"  trainable params: {model.num_parameters(True):,}  (flat buffer {flat.numel:,}, "
          f"zero_stage={a.zero_stage}, ranks={world})")
     dcfg = WT2Config(data_dir=a.data_dir, seq_len=a.seq_len, seed=a.seed, data_fraction=a.data_fraction,
@@ -99,20 +107,28 @@ def main(argv=None):
 
     trainer = None
 
+    def save_final(path):
+        """Collective for ZeRO (every rank calls it); rank 0 writes."""
+        if z3 is not None:
+            with z3.materialize():
+                if rank == 0:
+                    save_full(path, model)
+            return
+        if a.zero_stage:
+            trainer.opt.gather_master()
+        if rank == 0:
+            save_full(path, model)
+
     def save(step):
         if a.output_path:
-            if a.zero_stage:
-                trainer.opt.gather_master()
-            save_full(make_checkpoint_path(a.output_path, step), model)
+            save_final(make_checkpoint_path(a.output_path, step))
 
     trainer = Trainer(model, flat, train, valid, tc, dev, save_fn=save, power_monitor=common.build_power_monitor(a),
                       dp=dp, zero_stage=a.zero_stage)
     log0(f"[Training plan] steps_per_epoch={trainer.steps_per_epoch} total_steps={trainer.total_steps}\n")
     trainer.train()
-    if a.zero_stage:
-        trainer.opt.gather_master()
-    if a.output_path and rank == 0:
-        save_full(a.output_path, model)
+    if a.output_path:
+        save_final(a.output_path)
         log0(f"  ✓ Full model saved to {a.output_path}")
     log0(f"✅ Training complete! total_tokens={trainer.total_tokens} final_ema_loss={(trainer.ema_loss or 0):.4f}")
     if dp is not None:

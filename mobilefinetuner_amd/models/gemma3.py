@@ -218,8 +218,11 @@ class Gemma3Model(nn.Module):
         gcos, gsin = self.rope("global", S, dev)
         lcos, lsin = self.rope("local", S, dev)
         sh = getattr(self, "sharder", None)
+        z3 = getattr(self, "zero3", None)  # parallel/zero3.py: per-layer gather / reduce-scatter
         if sh is not None:
             sh.require("embed")
+        if z3 is not None:
+            z3.begin_forward()
         x = Fx.embedding(input_ids, self.embed, None, self.embed_scale)
         h = self.layers[0].input_layernorm(x)
         n = len(self.layers)
@@ -228,11 +231,15 @@ class Gemma3Model(nn.Module):
             cos, sin = (lcos, lsin) if L.sliding else (gcos, gsin)
             if sh is not None:
                 sh.require(f"block{i}")
+            if z3 is not None:
+                x, h = z3.pre_block(i, x, h)
             if self.activation_checkpointing and self.training and torch.is_grad_enabled():
                 x, h = torch.utils.checkpoint.checkpoint(self._layer, L, nxt, x, h, B, S, cos, sin, kv_lens,
                                                          use_reentrant=False)
             else:
                 x, h = self._layer(L, nxt, x, h, B, S, cos, sin, kv_lens)
+            if z3 is not None:
+                x, h = z3.post_block(i, x, h)
             if sh is not None:
                 x, h = gate(x, sh, f"block{i}"), gate(h, sh, f"block{i}")
         if sh is not None:

@@ -153,8 +153,11 @@ class GPT2Model(nn.Module):
         B, S = input_ids.shape
         assert S <= self.cfg.n_positions, f"sequence {S} exceeds n_positions {self.cfg.n_positions}"
         sh = getattr(self, "sharder", None)
+        z3 = getattr(self, "zero3", None)  # parallel/zero3.py: per-block gather / reduce-scatter
         if sh is not None:
             sh.require("embed")
+        if z3 is not None:
+            z3.begin_forward()
         x = Fx.embedding(input_ids, self.wte, self.wpe)  # [B*S, C]
         h = self.blocks[0].ln_1(x)
         n = len(self.blocks)
@@ -162,11 +165,15 @@ class GPT2Model(nn.Module):
             nxt = self.blocks[i + 1].ln_1 if i + 1 < n else self.ln_f
             if sh is not None:
                 sh.require(f"block{i}")
+            if z3 is not None:
+                x, h = z3.pre_block(i, x, h)
             if self.activation_checkpointing and self.training and torch.is_grad_enabled():
                 x, h = torch.utils.checkpoint.checkpoint(self._block, blk, nxt, x, h, B, S, kv_lens,
                                                          use_reentrant=False)
             else:
                 x, h = self._block(blk, nxt, x, h, B, S, kv_lens)
+            if z3 is not None:
+                x, h = z3.post_block(i, x, h)
             if sh is not None:  # backward re-fetches this block's weights before its dgrad
                 x, h = gate(x, sh, f"block{i}"), gate(h, sh, f"block{i}")
         if sh is not None:

@@ -50,7 +50,8 @@ class TrainStep:
             self.loss_dev.add_(loss.detach().float().reshape(1), alpha=scale)
 
     def _reduce(self):
-        if self.dp is not None and self.dp.world > 1:
+        # ZeRO-3 must always finish (its outer-unit grads reach the shard there, even on 1 rank)
+        if self.dp is not None and (self.dp.world > 1 or getattr(self.dp, "always_finish", False)):
             self.dp.finish()
 
     def _opt(self):

@@ -70,7 +70,17 @@ class Trainer:
         self.save_fn = save_fn
         self.pm = power_monitor
         self.dp = dp
-        if zero_stage > 0:
+        if zero_stage == 3:
+            # parallel/zero3.py: attach_zero3(model, ...) already partitioned the model; ``flat`` is
+            # its rank-local shard view.  The Zero3 object is both the optimizer and the reducer.
+            z3 = model.zero3
+            z3.opt.set_lr(cfg.lr)
+            z3.opt.weight_decay = cfg.weight_decay
+            z3.opt.max_grad_norm = cfg.clip_grad_norm if (cfg.clip_grad_norm or 0) > 0 else None
+            z3.opt.l2_coupled = cfg.l2_coupled
+            self.opt = z3
+            dp = self.dp = z3
+        elif zero_stage > 0:
             from ..parallel.zero import ZeroOptimizer, ZeroReducer
             self.opt = ZeroOptimizer(flat, zero_stage, lr=cfg.lr, weight_decay=cfg.weight_decay,
                                      max_grad_norm=cfg.clip_grad_norm, l2_coupled=cfg.l2_coupled)
@@ -79,8 +89,10 @@ class Trainer:
         else:
             self.opt = FusedAdamW(flat, lr=cfg.lr, weight_decay=cfg.weight_decay,
                                   max_grad_norm=cfg.clip_grad_norm, l2_coupled=cfg.l2_coupled)
+        # ZeRO-3 frees / refills parameter storage between blocks: eager steps only
         self.step_fn = TrainStep(model, flat, self.opt, grad_accum=cfg.grad_accum, dp=dp,
-                                 use_graph=cfg.use_graph and device.type == "cuda", loss_fn=loss_fn)
+                                 use_graph=cfg.use_graph and device.type == "cuda" and zero_stage != 3,
+                                 loss_fn=loss_fn)
         world = dist.get_world_size() if is_dist() else 1
         micro, accum = cfg.batch_size, max(1, cfg.grad_accum)
         n_local = train_ds.num_local()
@@ -148,7 +160,18 @@ class Trainer:
         from ..io import safetensors as st
         os.makedirs(path, exist_ok=True)
         r = dist.get_rank() if is_dist() else 0
-        if r == 0:
+        if getattr(self.opt, "sharded", False):
+            # ZeRO-3: every rank writes its own partition (master shard + AdamW moments)
+            st.save_file(os.path.join(path, f"trainable.rank{r}.safetensors"),
+                         {n: p.detach() for n, p in self.flat.named()})
+            st.save_file(os.path.join(path, f"optimizer.rank{r}.safetensors"), {"m": self.opt.m, "v": self.opt.v})
+        elif hasattr(self.opt, "stage"):
+            # ZeRO-1/2: masters are replicated (rank 0 writes them), moments are per-rank shards
+            if r == 0:
+                st.save_file(os.path.join(path, "trainable.safetensors"),
+                             {n: p.detach() for n, p in self.flat.named()})
+            st.save_file(os.path.join(path, f"optimizer.rank{r}.safetensors"), {"m": self.opt.m, "v": self.opt.v})
+        elif r == 0:
             st.save_file(os.path.join(path, "trainable.safetensors"),
                          {n: p.detach() for n, p in self.flat.named()})
             st.save_file(os.path.join(path, "optimizer.safetensors"),
@@ -165,11 +188,18 @@ class Trainer:
     def load_state(self, path: str):
         from ..io import safetensors as st
         r = dist.get_rank() if is_dist() else 0
-        w = st.load_file(os.path.join(path, "trainable.safetensors"))
+        def pick(stem):
+            per_rank = os.path.join(path, f"{stem}.rank{r}.safetensors")
+            return per_rank if os.path.exists(per_rank) else os.path.join(path, f"{stem}.safetensors")
+
+        w = st.load_file(pick("trainable"))
         for n, p in self.flat.named():
             p.data.copy_(w[n].to(p.device, p.dtype))
         self.flat.refresh_shadow()
-        o = st.load_file(os.path.join(path, "optimizer.safetensors"))
+        if getattr(self.opt, "sharded", False):
+            for u in self.model.zero3.units:  # gathered copies are stale now
+                self.model.zero3._release(u)
+        o = st.load_file(pick("optimizer"))
         sp = os.path.join(path, f"trainer_state.rank{r}.json")
         if not os.path.exists(sp):
             sp = os.path.join(path, "trainer_state.rank0.json")
@@ -262,7 +292,10 @@ class Trainer:
                         f.write(json.dumps({"step": step + 1, "epoch": cur_epoch, "valid_ppl": ev["ppl"],
                                             "ema_loss": self.ema_loss, "total_tokens": self.total_tokens}) + "\n")
             if c.save_every > 0 and (step + 1) % c.save_every == 0:
-                if self.save_fn is not None and rank0():
+                # ZeRO checkpoints consolidate with collectives: every rank enters save_fn (which
+                # writes on rank 0 only); otherwise only rank 0 calls it
+                collective = hasattr(self.opt, "gather_master") or getattr(self.opt, "sharded", False)
+                if self.save_fn is not None and (collective or rank0()):
                     self.save_fn(step + 1)
                 if c.state_dir:
                     self.save_state(c.state_dir)

@@ -84,7 +84,7 @@ def test_ddp_grads_equal_single_process_large_batch():
     assert torch.allclose(res[0][0], flat.grad, atol=1e-6, rtol=1e-4), (res[0][0] - flat.grad).abs().max()
 
 
-def _worker_train(rank, world, port, stage, q):
+def _worker_train(rank, world, port, stage, q, accum=1, ckpt=False):
     _init(rank, world, port)
     from mobilefinetuner_amd.data.wikitext2 import LMDataset, WT2Config
     from mobilefinetuner_amd.models.gpt2 import GPT2Config, GPT2Model
@@ -93,42 +93,58 @@ def _worker_train(rank, world, port, stage, q):
     from mobilefinetuner_amd.utils.params import FlatParams
     m = GPT2Model(GPT2Config.preset("gpt2-tiny"), dtype=torch.float32, device="cpu", seed=11)
     m.set_full_finetune()
-    flat = FlatParams(m.named_parameters(), "cpu", shadow=False, pad_multiple=world)
+    m.activation_checkpointing = ckpt
+    if stage == 3:
+        from mobilefinetuner_amd.parallel.zero3 import attach_zero3
+        flat = attach_zero3(m, "cpu").flat
+    else:
+        flat = FlatParams(m.named_parameters(), "cpu", shadow=False, pad_multiple=world)
     toks = torch.randint(0, 1000, (8000,), generator=torch.Generator().manual_seed(0), dtype=torch.int64).int()
     ds = LMDataset(WT2Config(seq_len=32, seed=1, rank=rank, world=world), "train", toks)
     dp = DataParallel(flat, bucket_mb=0.05) if stage == 0 else None
-    tc = TrainConfig(steps=4, batch_size=2, lr=1e-3, weight_decay=0.01, clip_grad_norm=0.5, log_interval=1,
-                     use_graph=False, ema_beta=0.0)
+    tc = TrainConfig(steps=4, batch_size=2, grad_accum=accum, lr=1e-3, weight_decay=0.01, clip_grad_norm=0.5,
+                     log_interval=1, use_graph=False, ema_beta=0.0)
     tr = Trainer(m, flat, ds, None, tc, torch.device("cpu"), dp=dp, zero_stage=stage)
     tr.train()
-    if stage:
-        tr.opt.gather_master()
-    q.put((rank, flat.master.clone(), [h["loss"] for h in tr.history]))
+    if stage == 3:
+        # gathered block copies and gradient buffers are released between uses
+        assert all(u.full.untyped_storage().nbytes() == 0 and u.gwork.untyped_storage().nbytes() == 0
+                   for u in m.zero3.units)
+        params = m.zero3.full_state()
+    else:
+        if stage:
+            tr.opt.gather_master()
+        params = {n: p.detach().clone() for n, p in m.named_parameters()}
+    # numpy arrays pickle by value (shared-memory tensors would die with this process)
+    q.put((rank, {n: t.float().numpy().copy() for n, t in params.items()}, [h["loss"] for h in tr.history]))
     dist.destroy_process_group()
 
 
-def _run_train(stage):
+def _run_train(stage, accum=1, ckpt=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker_train, args=(r, 2, port, stage, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker_train, args=(r, 2, port, stage, q, accum, ckpt)) for r in range(2)]
     for p in ps:
         p.start()
-    out = dict((r, (w, l)) for r, w, l in [q.get(timeout=600) for _ in ps])
+    out = dict((r, ({n: torch.from_numpy(a) for n, a in w.items()}, l)) for r, w, l in [q.get(timeout=600) for _ in ps])
     for p in ps:
         p.join(60)
     return out
 
 
-@pytest.mark.parametrize("stage", [1, 2])
-def test_zero_matches_ddp(stage):
-    ddp = _run_train(0)
-    zero = _run_train(stage)
-    assert torch.allclose(ddp[0][0], ddp[1][0])
+@pytest.mark.parametrize("stage,accum,ckpt", [(1, 1, False), (2, 1, False), (3, 1, False), (3, 2, True)])
+def test_zero_matches_ddp(stage, accum, ckpt):
+    """ZeRO-1/2/3 training (4 steps, clipping + weight decay; ZeRO-3 also with grad accumulation and
+    activation checkpointing) == DDP training, on every rank."""
+    ddp = _run_train(0, accum)
+    zero = _run_train(stage, accum, ckpt)
     assert ddp[0][1] == pytest.approx(zero[0][1], rel=1e-4)
-    n = ddp[0][0].numel()
-    assert torch.allclose(ddp[0][0], zero[0][0][:n], atol=1e-5), (ddp[0][0] - zero[0][0][:n]).abs().max()
-    assert torch.allclose(zero[0][0], zero[1][0])
+    assert set(zero[0][0]) == set(ddp[0][0])
+    for n, w in ddp[0][0].items():
+        assert torch.allclose(w, ddp[1][0][n])
+        assert torch.allclose(w, zero[0][0][n], atol=1e-5), (n, (w - zero[0][0][n]).abs().max())
+        assert torch.allclose(zero[0][0][n], zero[1][0][n])
 
 
 def test_mft_launch_propagates_rank_failure(tmp_path):
