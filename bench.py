@@ -49,6 +49,11 @@ CONFIGS = {
     # ahead on a communication stream), gradients reduce-scattered per block during backward
     "gpt2-xl-zero3": dict(model="gpt2-xl", mode="full", batch=16, seq=128, zero=3,
                           metric="tokens/sec GPT-2-XL full fine-tune ZeRO-3 seq128 (training, whole job)"),
+    # BASELINE config 5: ZeRO partition + host-DRAM tier (AdamW moments in pinned host memory,
+    # streamed through the GPU per chunk on the native HostTier's copy stream)
+    "gpt2-xl-zero3-offload": dict(model="gpt2-xl", mode="full", batch=16, seq=128, zero=3, offload=True,
+                                  metric="tokens/sec GPT-2-XL full fine-tune ZeRO-3 + host-offloaded AdamW "
+                                         "seq128 (training, whole job)"),
 }
 
 
@@ -86,21 +91,22 @@ def build(a, cfgd, dev, world):
         zero = cfgd.get("zero", 0) if world > 1 else 0
         if a.zero >= 0:  # explicit override (e.g. measure ZeRO-3's gather/scatter cost on 1 GPU)
             zero = a.zero
+        offload = bool(cfgd.get("offload", False) or a.offload_optimizer)
         if zero == 3:
             from mobilefinetuner_amd.parallel.zero3 import attach_zero3
-            z3 = attach_zero3(model, dev, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0)
-            desc = f"{name} full fine-tune ZeRO-3"
+            z3 = attach_zero3(model, dev, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0, offload=offload)
+            desc = f"{name} full fine-tune ZeRO-3" + (" + host-offloaded AdamW" if offload else "")
             step = TrainStep(model, z3.flat, z3, grad_accum=a.grad_accum, dp=z3, use_graph=False)
             return model, step, vocab, desc, sum(p.numel() for p in model.parameters())
         flat = FlatParams(model.named_parameters(), dev, pad_multiple=max(1, world))
         if zero:
             from mobilefinetuner_amd.parallel.zero import ZeroOptimizer, ZeroReducer
-            opt = ZeroOptimizer(flat, zero, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0)
+            opt = ZeroOptimizer(flat, zero, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0, offload=offload)
             dp = ZeroReducer(opt)
         else:
-            opt = FusedAdamW(flat, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0)
+            opt = FusedAdamW(flat, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0, offload=offload)
             dp = DataParallel(flat) if world > 1 else None
-        desc = f"{name} full fine-tune" + (f" ZeRO-{zero}" if zero else "")
+        desc = f"{name} full fine-tune" + (f" ZeRO-{zero}" if zero else "") + (" + host-offloaded AdamW" if offload else "")
     step = TrainStep(model, flat, opt, grad_accum=a.grad_accum, dp=dp, use_graph=not a.no_graph)
     nparams = sum(p.numel() for p in model.parameters())
     return model, step, vocab, desc, nparams
@@ -120,6 +126,7 @@ def main():
     ap.add_argument("--batch", type=int, default=int(os.environ.get("MFT_BENCH_BATCH", 0)),
                     help="micro-batch (sequences) per GPU (0 = the config's default)")
     ap.add_argument("--seq", type=int, default=0)
+    ap.add_argument("--offload_optimizer", action="store_true", help="full fine-tune: AdamW state in pinned host DRAM")
     ap.add_argument("--zero", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
                     help="full fine-tune configs: ZeRO stage override (-1 = the config's, used when N > 1)")
     ap.add_argument("--rank", type=int, default=8)

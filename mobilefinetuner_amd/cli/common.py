@@ -58,7 +58,11 @@ def add_energy_args(ap):
 
 def add_shard_args(ap):
     g = ap.add_argument_group("parameter sharding / offload")
-    g.add_argument("--shard_enable", action="store_true")
+    g.add_argument("--shard_enable", action="store_true",
+                   help="LoRA: frozen weights in a pinned host tier, fetched per block under --shard_budget_mb; "
+                        "full fine-tune: AdamW state in pinned host DRAM (same as --offload_optimizer)")
+    g.add_argument("--offload_optimizer", action="store_true",
+                   help="AdamW moments in pinned host DRAM, streamed through the GPU per chunk on a copy stream")
     g.add_argument("--shard_dir", default="")
     g.add_argument("--shard_budget_mb", type=int, default=512)
     g.add_argument("--shard_fp16_disk", type=int, default=1)

@@ -75,10 +75,13 @@ def main(argv=None):
     model.activation_checkpointing = a.activation_checkpointing
     model.set_full_finetune()
     z3 = None
+    # full fine-tuning has no frozen weights to shard: --shard_enable moves the optimizer state to
+    # the pinned host tier instead (BASELINE config "ZeRO-style param shard + host-DRAM offload")
+    offload = bool(a.offload_optimizer or a.shard_enable) and dev.type == "cuda"
     if a.zero_stage == 3:
         from ..parallel.zero3 import attach_zero3
         z3 = attach_zero3(model, dev, lr=a.lr, weight_decay=a.weight_decay, max_grad_norm=a.clip_grad_norm,
-                          l2_coupled=a.compat_l2_adam)
+                          l2_coupled=a.compat_l2_adam, offload=offload)
         flat = z3.flat
     else:
         flat = FlatParams(model.named_parameters(), dev, pad_multiple=world if a.zero_stage else 1)
@@ -103,6 +106,7 @@ def main(argv=None):
                      eval_interval=a.eval_interval, eval_batches=a.eval_batches, eval_batch_size=a.eval_batch_size,
                      eval_out=a.eval_out, save_every=a.save_every, ema_beta=a.ema_beta,
                      use_graph=not a.no_graph, state_dir=a.state_dir, metrics_out=a.metrics_out,
+                     offload_optimizer=offload,
                      **common.runtime_train_kwargs(a))
 
     trainer = None

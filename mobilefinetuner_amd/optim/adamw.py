@@ -24,7 +24,8 @@ from ..utils.params import FlatParams
 class FusedAdamW:
     def __init__(self, flat: FlatParams, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  max_grad_norm: float | None = 1.0, l2_coupled: bool = False, skip_nonfinite: bool = True,
-                 param_range: tuple[int, int] | None = None):
+                 param_range: tuple[int, int] | None = None, offload: bool = False,
+                 offload_chunk: int = 1 << 25):
         self.flat = flat
         self.beta1, self.beta2 = betas
         self.eps, self.weight_decay = eps, weight_decay
@@ -35,8 +36,27 @@ class FusedAdamW:
         # optional sub-range (ZeRO-1/2: this rank owns [lo, hi) of the flat buffer)
         self.lo, self.hi = param_range if param_range is not None else (0, flat.numel)
         n = self.hi - self.lo
-        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
+        # offload: the AdamW moments live in pinned host DRAM (native HostTier, csrc/runtime/
+        # offload.cpp) and stream through two device slots per chunk -- H2D of chunk c+1 and D2H
+        # of chunk c-1 on the tier's copy stream overlap the update of chunk c (SURVEY §2.13 "host-
+        # DRAM offload tier for optimizer state"; the reference's analogue is the disk sharder)
+        self.offload = bool(offload) and dev.type == "cuda"
+        if self.offload:
+            self._tier = native().runtime.HostTier(0, "", 0)
+            self._chunks = []
+            for c0 in range(0, n, offload_chunk):
+                c1 = min(n, c0 + offload_chunk)
+                for k in ("m", "v"):
+                    self._tier.add(f"{k}#{c0}", (c1 - c0) * 4)
+                    self._tier.host_tensor(f"{k}#{c0}", torch.float32, [c1 - c0]).zero_()
+                self._chunks.append((c0, c1))
+            cmax = min(n, offload_chunk)
+            self._slots = [(torch.empty(cmax, dtype=torch.float32, device=dev),
+                            torch.empty(cmax, dtype=torch.float32, device=dev)) for _ in range(2)]
+            self.m = self.v = None
+        else:
+            self.m = torch.zeros(n, dtype=torch.float32, device=dev)
+            self.v = torch.zeros(n, dtype=torch.float32, device=dev)
         self.lr_dev = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
         self.step_dev = torch.zeros(1, dtype=torch.float32, device=dev)
         self.sumsq_dev = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -79,6 +99,9 @@ class FusedAdamW:
                 self.nonfinite_dev.zero_()
                 C.nonfinite_check(g, self.nonfinite_dev)
             sh = self.flat.shadow[self.lo:self.hi] if self.flat.shadow is not None else None
+            if self.offload:
+                self._step_offloaded(C, p, g, sh)
+                return
             C.adamw_step(p, g, self.m, self.v, self.lr_dev, self.step_dev,
                          self.sumsq_dev if self.max_grad_norm is not None else None,
                          self.beta1, self.beta2, self.eps, self.weight_decay,
@@ -86,6 +109,55 @@ class FusedAdamW:
                          self.nonfinite_dev if self.skip_nonfinite else None)
         else:
             self._step_reference(p, g)
+
+    def _step_offloaded(self, C, p, g, sh):
+        """Chunk c: H2D on one copy stream, update on the compute stream, D2H on another copy
+        stream (PCIe is full duplex: write-back of chunk c-1 and fetch of chunk c+1 run at once).
+        A device slot is refilled only after its previous chunk's write-back (slot_free event)."""
+        cur = torch.cuda.current_stream(p.device)
+        if not hasattr(self, "_h2d"):
+            self._h2d = torch.cuda.Stream(device=p.device)
+            self._d2h = torch.cuda.Stream(device=p.device)
+            self._free = [torch.cuda.Event(), torch.cuda.Event()]
+            for e in self._free:
+                e.record(cur)
+            self._host = [(self._tier.host_tensor(f"m#{c0}", torch.float32, [c1 - c0]),
+                           self._tier.host_tensor(f"v#{c0}", torch.float32, [c1 - c0])) for c0, c1 in self._chunks]
+        fetched = [torch.cuda.Event(), torch.cuda.Event()]
+
+        def fetch(i):
+            c0, c1 = self._chunks[i]
+            mb, vb = self._slots[i % 2]
+            self._h2d.wait_event(self._free[i % 2])
+            with torch.cuda.stream(self._h2d):
+                mb[:c1 - c0].copy_(self._host[i][0], non_blocking=True)
+                vb[:c1 - c0].copy_(self._host[i][1], non_blocking=True)
+            fetched[i % 2].record(self._h2d)
+
+        fetch(0)
+        for i, (c0, c1) in enumerate(self._chunks):
+            mb, vb = self._slots[i % 2]
+            if i + 1 < len(self._chunks):
+                fetch(i + 1)
+            cur.wait_event(fetched[i % 2])
+            C.adamw_step(p[c0:c1], g[c0:c1], mb[:c1 - c0], vb[:c1 - c0], self.lr_dev, self.step_dev,
+                         self.sumsq_dev if self.max_grad_norm is not None else None,
+                         self.beta1, self.beta2, self.eps, self.weight_decay,
+                         float(self.max_grad_norm or 0.0), self.l2_coupled,
+                         sh[c0:c1] if sh is not None else None,
+                         self.nonfinite_dev if self.skip_nonfinite else None)
+            self._d2h.wait_stream(cur)
+            with torch.cuda.stream(self._d2h):
+                self._host[i][0].copy_(mb[:c1 - c0], non_blocking=True)
+                self._host[i][1].copy_(vb[:c1 - c0], non_blocking=True)
+            self._free[i % 2].record(self._d2h)
+
+    def _moments_host(self):
+        if hasattr(self, "_d2h"):
+            self._d2h.synchronize()
+        m = torch.cat([self._tier.host_tensor(f"m#{c0}", torch.float32, [c1 - c0]) for c0, c1 in self._chunks])
+        v = torch.cat([self._tier.host_tensor(f"v#{c0}", torch.float32, [c1 - c0]) for c0, c1 in self._chunks])
+        return m, v
 
     @torch.no_grad()
     def _step_reference(self, p, g):
@@ -116,13 +188,24 @@ class FusedAdamW:
 
     # ---- state (full training-state checkpoint)
     def state_dict(self):
-        return {"m": self.m.detach().cpu(), "v": self.v.detach().cpu(), "step": self.step_count,
+        if self.offload:
+            m, v = self._moments_host()
+        else:
+            m, v = self.m.detach().cpu(), self.v.detach().cpu()
+        return {"m": m, "v": v, "step": self.step_count,
                 "lr": self.lr, "betas": (self.beta1, self.beta2), "eps": self.eps,
                 "weight_decay": self.weight_decay, "range": (self.lo, self.hi)}
 
     def load_state_dict(self, sd):
-        self.m.copy_(sd["m"].to(self.m.device))
-        self.v.copy_(sd["v"].to(self.v.device))
+        if self.offload:
+            if hasattr(self, "_d2h"):
+                self._d2h.synchronize()
+            for c0, c1 in self._chunks:
+                self._tier.host_tensor(f"m#{c0}", torch.float32, [c1 - c0]).copy_(sd["m"][c0:c1])
+                self._tier.host_tensor(f"v#{c0}", torch.float32, [c1 - c0]).copy_(sd["v"][c0:c1])
+        else:
+            self.m.copy_(sd["m"].to(self.m.device))
+            self.v.copy_(sd["v"].to(self.v.device))
         self.step_count = int(sd["step"])
         self.step_dev.fill_(float(self.step_count))
         self.set_lr(sd.get("lr", self.lr))

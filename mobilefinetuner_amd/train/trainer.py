@@ -46,6 +46,7 @@ class TrainConfig:
     schedule: str = "gpt2"          # gpt2 (warmup + cosine to 10%) | linear | cosine | constant
     clip_grad_norm: float = 1.0
     l2_coupled: bool = False        # reference Adam semantics (coupled L2)
+    offload_optimizer: bool = False  # AdamW moments in pinned host DRAM, streamed per chunk
     log_interval: int = 1
     eval_interval: int = 0
     eval_batches: int = 50
@@ -83,12 +84,14 @@ class Trainer:
         elif zero_stage > 0:
             from ..parallel.zero import ZeroOptimizer, ZeroReducer
             self.opt = ZeroOptimizer(flat, zero_stage, lr=cfg.lr, weight_decay=cfg.weight_decay,
-                                     max_grad_norm=cfg.clip_grad_norm, l2_coupled=cfg.l2_coupled)
+                                     max_grad_norm=cfg.clip_grad_norm, l2_coupled=cfg.l2_coupled,
+                                     offload=cfg.offload_optimizer)
             dp = ZeroReducer(self.opt)
             self.dp = dp
         else:
             self.opt = FusedAdamW(flat, lr=cfg.lr, weight_decay=cfg.weight_decay,
-                                  max_grad_norm=cfg.clip_grad_norm, l2_coupled=cfg.l2_coupled)
+                                  max_grad_norm=cfg.clip_grad_norm, l2_coupled=cfg.l2_coupled,
+                                  offload=cfg.offload_optimizer)
         # ZeRO-3 frees / refills parameter storage between blocks: eager steps only
         self.step_fn = TrainStep(model, flat, self.opt, grad_accum=cfg.grad_accum, dp=dp,
                                  use_graph=cfg.use_graph and device.type == "cuda" and zero_stage != 3,
@@ -156,6 +159,10 @@ class Trainer:
         return {"nll": nll, "ppl": math.exp(min(nll, 50.0)), "tokens": int(tot[1])}
 
     # ------------------------------------------------------------------ checkpoint / resume
+    def _moments(self):
+        sd = self.opt.state_dict()  # host copies (also for host-offloaded moments)
+        return {"m": sd["m"], "v": sd["v"]}
+
     def save_state(self, path: str):
         from ..io import safetensors as st
         os.makedirs(path, exist_ok=True)
@@ -164,18 +171,18 @@ class Trainer:
             # ZeRO-3: every rank writes its own partition (master shard + AdamW moments)
             st.save_file(os.path.join(path, f"trainable.rank{r}.safetensors"),
                          {n: p.detach() for n, p in self.flat.named()})
-            st.save_file(os.path.join(path, f"optimizer.rank{r}.safetensors"), {"m": self.opt.m, "v": self.opt.v})
+            st.save_file(os.path.join(path, f"optimizer.rank{r}.safetensors"), self._moments())
         elif hasattr(self.opt, "stage"):
             # ZeRO-1/2: masters are replicated (rank 0 writes them), moments are per-rank shards
             if r == 0:
                 st.save_file(os.path.join(path, "trainable.safetensors"),
                              {n: p.detach() for n, p in self.flat.named()})
-            st.save_file(os.path.join(path, f"optimizer.rank{r}.safetensors"), {"m": self.opt.m, "v": self.opt.v})
+            st.save_file(os.path.join(path, f"optimizer.rank{r}.safetensors"), self._moments())
         elif r == 0:
             st.save_file(os.path.join(path, "trainable.safetensors"),
                          {n: p.detach() for n, p in self.flat.named()})
             st.save_file(os.path.join(path, "optimizer.safetensors"),
-                         {"m": self.opt.m, "v": self.opt.v})
+                         self._moments())
         state = {"global_step": self.global_step, "opt_step": self.opt.step_count, "lr": self.opt.lr,
                  "ema_loss": self.ema_loss, "total_tokens": self.total_tokens, "skipped": self.skipped,
                  "data": self.train_ds.state(), "world": self.world, "total_steps": self.total_steps,
