@@ -34,24 +34,24 @@ BASELINE_TOKENS_PER_SEC = 170.0
 # BASELINE.json "configs" -> (model preset, mode, default micro-batch, seq, metric label)
 CONFIGS = {
     # headline: GPT-2 small LoRA r=8 seq 128 (BASELINE.json "metric")
-    "gpt2-lora": dict(model="gpt2", mode="lora", batch=256, seq=128, targets="AttnQKV,AttnProj",
+    "gpt2-lora": dict(model="gpt2", mode="lora", batch=512, seq=128, targets="AttnQKV,AttnProj",
                       metric="tokens/sec GPT-2-124M LoRA r=8 seq128 (training, whole job)"),
     # Gemma-3 270M LoRA r=8 seq 256 (RMSNorm / QK-norm+RoPE / GQA / sliding-window kernels)
-    "gemma3-270m-lora": dict(model="gemma3-270m", mode="lora", batch=64, seq=256, targets="full",
+    "gemma3-270m-lora": dict(model="gemma3-270m", mode="lora", batch=128, seq=256, targets="full",
                              metric="tokens/sec Gemma-3-270M LoRA r=8 seq256 (training, whole job)"),
     # GPT-2 small full fine-tuning, DP over RCCL (bucketed, backward-overlapped all-reduce)
-    "gpt2-full": dict(model="gpt2", mode="full", batch=64, seq=128, zero=0,
+    "gpt2-full": dict(model="gpt2", mode="full", batch=512, seq=128, zero=0,
                       metric="tokens/sec GPT-2-124M full fine-tune seq128 (training, whole job)"),
     # GPT-2 XL (1.5B) full fine-tuning with ZeRO-2 partitioned optimizer / reduce-scattered grads
-    "gpt2-xl-zero": dict(model="gpt2-xl", mode="full", batch=16, seq=128, zero=2,
+    "gpt2-xl-zero": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=2,
                          metric="tokens/sec GPT-2-XL full fine-tune ZeRO-2 seq128 (training, whole job)"),
     # same with ZeRO-3: parameters partitioned too, all-gathered per block (prefetched one block
     # ahead on a communication stream), gradients reduce-scattered per block during backward
-    "gpt2-xl-zero3": dict(model="gpt2-xl", mode="full", batch=16, seq=128, zero=3,
+    "gpt2-xl-zero3": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=3,
                           metric="tokens/sec GPT-2-XL full fine-tune ZeRO-3 seq128 (training, whole job)"),
     # BASELINE config 5: ZeRO partition + host-DRAM tier (AdamW moments in pinned host memory,
     # streamed through the GPU per chunk on the native HostTier's copy stream)
-    "gpt2-xl-zero3-offload": dict(model="gpt2-xl", mode="full", batch=16, seq=128, zero=3, offload=True,
+    "gpt2-xl-zero3-offload": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=3, offload=True,
                                   metric="tokens/sec GPT-2-XL full fine-tune ZeRO-3 + host-offloaded AdamW "
                                          "seq128 (training, whole job)"),
 }
@@ -119,10 +119,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="gpt2-lora", choices=sorted(CONFIGS),
                     help="benchmark configuration (BASELINE.json configs); default = the headline metric")
-    # micro-batch default per config; for the headline 256 x 128 = 32k tokens per GPU per step: the
-    # M dimension every block GEMM sees.  Measured on 1x MI355X: B=64 0.89M tok/s, B=128 1.02M,
-    # B=256 1.09M (block GEMMs reach higher MFMA utilisation at M=32k; 288 GB HBM makes the
-    # activation footprint irrelevant).
+    # micro-batch default per config; for the headline 512 x 128 = 64k tokens per GPU per step: the
+    # M dimension every block GEMM sees.  Measured on 1x MI355X (same build, one call): B=256 1.32M
+    # tok/s, B=384 1.37M, B=512 1.44M, B=768 1.40M, B=1024 1.47M -- at M = 64k the N = 768 GEMMs
+    # (qkv / proj / fc data-grads, mlp_proj) tile into whole waves of 256 CUs; 288 GB HBM makes the
+    # activation footprint irrelevant.
     ap.add_argument("--batch", type=int, default=int(os.environ.get("MFT_BENCH_BATCH", 0)),
                     help="micro-batch (sequences) per GPU (0 = the config's default)")
     ap.add_argument("--seq", type=int, default=0)
