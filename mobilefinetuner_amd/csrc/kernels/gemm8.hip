@@ -77,9 +77,18 @@ __device__ __forceinline__ bf16x8_t frag8(const bf16_t* t, int r0, int kc) {
 
 }  // namespace
 
+#ifdef MFT_G8_STAMPS  // diagnostic build only (scripts/g8_stamps.hip): s_memtime per phase per WG
+__device__ unsigned long long* g8_stamps;
+#define G8_STAMP(k) \
+  if (threadIdx.x == 0) g8_stamps[blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memtime()
+#else
+#define G8_STAMP(k)
+#endif
+
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  G8_STAMP(0);
   // buffer b (0 = even, 1 = odd): half-tiles A0, A1, B0, B1 at smem + (b * 4 + h) * kHalf
   const int tiles_n = (g.N + 255) / 256;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
@@ -127,7 +136,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[q][i][j] = mfma16(af[i][ks], bfr[j][ks], acc[q][i][j]);
+        for (int j = 0; j < 2; ++j) acc[q][i][j] = mfma16(bfr[j][ks], af[i][ks], acc[q][i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -140,6 +149,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   stage(1, 3, 1);
   vm_wait<4>();
   raw_barrier();
+  G8_STAMP(1);
   // Ping-pong the two wave groups (wm = 0 / 1; each SIMD holds one wave of each): group 1 runs one
   // barrier behind, so on every SIMD one wave issues its ds_reads + glds while the other one runs
   // its MFMA cluster (guide §5 template, "if(wr==1) s_barrier").  Staging stays correct: a half-tile
@@ -213,123 +223,101 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     raw_barrier();
   }
   if (wm == 0) raw_barrier();  // re-align the groups' barrier counts
-  vm_wait<0>();  // drain the clamped tail prefetches before LDS is reused by the epilogue
-  raw_barrier();
+  vm_wait<0>();  // drain the clamped tail prefetches (LDS-DMA must not outlive the workgroup)
+  G8_STAMP(2);
 
-  // ------------------------------------------------------------------ epilogue
-  // per wave and quadrant: a 64 x 32 piece staged through LDS (stride 40) -> 16-B row stores
-  constexpr int LDT = 40;
-  bf16_t* T = smem + w * 64 * LDT;
-  auto sync_wave = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
+  // ------------------------------------------------------------------ epilogue (registers only)
+  // The MFMAs ran with the operands swapped, so each 16 x 16 accumulator block is C^T: lane l holds
+  // row (l & 15) of the block, columns 4 * (l >> 4) .. +3.  One v_permlane16_swap per dword pairs
+  // the two column blocks of the wave's 32-column piece so every lane then owns EIGHT CONTIGUOUS
+  // columns of one row: lane group g = l >> 4 -> column offset {0, 16, 8, 24}[g].  Every epilogue
+  // is then 16-B vector loads/stores straight from registers (no LDS staging, no wave syncs).
+  const int g4 = lane >> 4;
+  const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int qa = (q == 2 || q == 3) ? 1 : 0, qb = (q == 1 || q == 2) ? 1 : 0;
-    const int rbase = m0 + qa * 128 + wm * 64, cbase = n0 + qb * 128 + wn * 32;
-    auto to_global = [&](bf16_t* dst, long ldd) {
-      sync_wave();
+    const int rbase = m0 + qa * 128 + wm * 64, col = n0 + qb * 128 + wn * 32 + cofs;
+    const bool col_ok = col < g.N;
+    const int colc = min(col, g.N - 8);
+    float bias_v[8];
+    if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU) load8(g.bias + colc, bias_v);
+    float o[4][8];
 #pragma unroll
-      for (int it = 0; it < 4; ++it) {  // 64 rows x 4 chunks = 256 pieces / 64 lanes
-        const int c = it * 64 + lane;
-        const int r = c >> 2, ch = c & 3;
-        const int row = rbase + r, col = cbase + ch * 8;
-        if (row < g.M && col < g.N)
-          *reinterpret_cast<u16x8_t*>(dst + (long)row * ldd + col) = *reinterpret_cast<const u16x8_t*>(T + r * LDT + ch * 8);
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[q][i][0][r]),
+                                                         __float_as_uint(acc[q][i][1][r]), false, false);
+        o[i][r] = __uint_as_float(sw[0]);
+        o[i][4 + r] = __uint_as_float(sw[1]);
       }
-      sync_wave();
-    };
-    if constexpr (EPI == GEMM_EPI_F32ACC) {
-      float* C = reinterpret_cast<float*>(g.C);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = rbase + i * 16 + 4 * (lane >> 4) + r, col = cbase + j * 16 + (lane & 15);
-            if (row < g.M && col < g.N) C[(long)row * g.ldc + col] += g.alpha * acc[q][i][j][r];
-          }
-      continue;
-    }
-    if constexpr (EPI == GEMM_EPI_DGELU) {
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int c = it * 64 + lane;
-        const int r = c >> 2, ch = c & 3;
-        const int row = min(rbase + r, g.M - 1), col = min(cbase + ch * 8, g.N - 8);
-        *reinterpret_cast<u16x8_t*>(T + r * LDT + ch * 8) = *reinterpret_cast<const u16x8_t*>(g.aux + (long)row * g.ldaux + col);
-      }
-      sync_wave();
-    }
-    float bias_v[2] = {0.f, 0.f};
-    if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bias_v[j] = bf2f(g.bias[min(cbase + j * 16 + (lane & 15), g.N - 1)]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int tr = i * 16 + 4 * (lane >> 4) + r, tc = j * 16 + (lane & 15);
-          float v = acc[q][i][j][r] * g.alpha + bias_v[j];
-          if constexpr (EPI == GEMM_EPI_DGELU) v *= gelu_tanh_grad(bf2f(T[tr * LDT + tc]));
-          if constexpr (EPI == GEMM_EPI_BIAS_GELU) acc[q][i][j][r] = v;
-          T[tr * LDT + tc] = f2bf(v);
-        }
-    if constexpr (EPI == GEMM_EPI_BIAS_GELU) {
-      to_global(g.aux, g.ldaux);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int tr = i * 16 + 4 * (lane >> 4) + r, tc = j * 16 + (lane & 15);
-            T[tr * LDT + tc] = f2bf(gelu_tanh(acc[q][i][j][r]));
-          }
     }
     if constexpr (EPI == GEMM_EPI_LORA) {
-      // rank-r update while moving the staged tile out: each lane owns one 8-column chunk of 4 rows
-      // (the to_global mapping), so its 8 x r slice of lora_w is loaded once per 8 ranks and each
-      // row of lora_u is one 16-B load per 8 ranks (r <= 32, multiple of 8)
-      sync_wave();
-      const int ch = lane & 3, col = cbase + ch * 8, colc = min(col, g.N - 8);
-      float o[4][8];
+      // rank-r update: the lane's 8 x r slice of lora_w is loaded once per 8 ranks per quadrant,
+      // each row of lora_u is one 16-B load per 8 ranks (r <= 32, multiple of 8)
 #pragma unroll
-      for (int it = 0; it < 4; ++it)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[it][e] = bf2f(T[(it * 16 + (lane >> 2)) * LDT + ch * 8 + e]);
+        for (int e = 0; e < 8; ++e) o[i][e] *= g.alpha;
 #pragma unroll 1
       for (int t8 = 0; t8 < g.lora_r; t8 += 8) {
-        u16x8_t w[8];  // kept packed (32 VGPRs; the accumulators of later quadrants are still live)
+        u16x8_t wv[8];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) w[t] = *reinterpret_cast<const u16x8_t*>(g.lora_w + (long)(t8 + t) * g.ld_lw + colc);
+        for (int t = 0; t < 8; ++t) wv[t] = *reinterpret_cast<const u16x8_t*>(g.lora_w + (long)(t8 + t) * g.ld_lw + colc);
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
-          const int row = min(rbase + it * 16 + (lane >> 2), g.M - 1);
+        for (int i = 0; i < 4; ++i) {
+          const int row = min(rbase + i * 16 + (lane & 15), g.M - 1);
           float u[8];
           load8(g.lora_u + (long)row * g.ld_lu + t8, u);
 #pragma unroll
           for (int t = 0; t < 8; ++t)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[it][e] += u[t] * bf2f(w[t][e]);
+            for (int e = 0; e < 8; ++e) o[i][e] += u[t] * bf2f(wv[t][e]);
         }
       }
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int row = rbase + it * 16 + (lane >> 2);
-        if (row < g.M && col < g.N) store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, o[it]);
-      }
-      sync_wave();
-      continue;
     }
-    to_global(reinterpret_cast<bf16_t*>(g.C), g.ldc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rbase + i * 16 + (lane & 15);
+      const bool ok = col_ok && row < g.M;
+      float* v = o[i];
+      if constexpr (EPI == GEMM_EPI_F32ACC) {
+        if (ok) {
+          float* C = reinterpret_cast<float*>(g.C) + (long)row * g.ldc + col;
+          f32x4_t c0 = *reinterpret_cast<f32x4_t*>(C), c1 = *reinterpret_cast<f32x4_t*>(C + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            c0[e] += g.alpha * v[e];
+            c1[e] += g.alpha * v[4 + e];
+          }
+          *reinterpret_cast<f32x4_t*>(C) = c0;
+          *reinterpret_cast<f32x4_t*>(C + 4) = c1;
+        }
+        continue;
+      }
+      if constexpr (EPI != GEMM_EPI_LORA) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] *= g.alpha;
+          if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU) v[e] += bias_v[e];
+        }
+      }
+      if constexpr (EPI == GEMM_EPI_DGELU) {
+        float pre[8];
+        load8(g.aux + (long)min(row, g.M - 1) * g.ldaux + colc, pre);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(pre[e]);
+      }
+      if constexpr (EPI == GEMM_EPI_BIAS_GELU) {
+        if (ok) store8(g.aux + (long)row * g.ldaux + col, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+      }
+      if (ok) store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, v);
+    }
   }
+  G8_STAMP(3);
 }
 
 template <int EPI>
