@@ -315,6 +315,24 @@ void lora_wgrad(Tensor X, Tensor Y, Tensor out, int64_t osk, int64_t osr, double
   mft::lora_wgrad(bp(X), X.stride(-2), bp(Y), Y.stride(-2), fp(out), osk, osr, M, K, R, (float)scale,
                   mkdrop(drop_p, salt, ctr), stream());
 }
+// rank 8: v = s dy B^T (bf16 [M, 8]) and dB += s u^T dy (fp32 [8, N] grad buffer) in one pass over dy
+void lora_dy(Tensor dy, Tensor B, Tensor u, Tensor dB, Tensor vpart, Tensor v, double s) {
+  CHECK_BF16(dy); CHECK_BF16(B); CHECK_BF16(u); CHECK_BF16(v); CHECK_F32(dB); CHECK_F32(vpart);
+  TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1, "lora_dy: dy must be a row-contiguous 2-D view");
+  const long M = dy.size(0);
+  const int N = dy.size(1);
+  TORCH_CHECK(B.dim() == 2 && B.size(0) == 8 && B.size(1) == N && B.stride(1) == 1, "lora_dy: B must be [8, N]");
+  TORCH_CHECK(u.dim() == 2 && u.size(0) == M && u.size(1) == 8 && u.stride(1) == 1, "lora_dy: u must be [M, 8]");
+  TORCH_CHECK(v.dim() == 2 && v.size(0) == M && v.size(1) == 8 && v.stride(1) == 1, "lora_dy: v must be [M, 8]");
+  TORCH_CHECK(dB.is_contiguous() && dB.numel() == 8L * N, "lora_dy: dB must be a contiguous [8, N] buffer");
+  TORCH_CHECK(vpart.is_contiguous() && vpart.numel() >= (long)((N + 255) / 256) * M * 8, "lora_dy: vpart too small");
+  TORCH_CHECK(N % 8 == 0 && dy.stride(0) % 8 == 0 && B.stride(0) % 8 == 0 && u.stride(0) % 8 == 0 &&
+              reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(u.data_ptr()) % 16 == 0,
+              "lora_dy: alignment (N and row strides % 8, 16-B aligned rows)");
+  mft::lora_dy(bp(dy), dy.stride(0), bp(B), B.stride(0), bp(u), u.stride(0), fp(dB), N, fp(vpart), bp(v), v.stride(0),
+               M, N, (float)s, stream());
+}
 void lora_merge(Tensor W, int64_t wsk, int64_t wsn, Tensor A, Tensor B, double s) {
   CHECK_F32(A); CHECK_F32(B); CHECK_CONTIG(A); CHECK_CONTIG(B);
   const int R = A.size(0), K = A.size(1), N = B.size(1);
@@ -489,6 +507,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_update", &lora_update);
   m.def("lora_wgrad", &lora_wgrad);
   m.def("lora_merge", &lora_merge);
+  m.def("lora_dy", &lora_dy);
   m.def("gemm", &gemm_op, py::arg("A"), py::arg("B"), py::arg("b_nn"), py::arg("epi"), py::arg("bias"), py::arg("aux"),
         py::arg("alpha"), py::arg("cfg"), py::arg("out"), py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none());
   m.def("zero_cols", &zero_cols);

@@ -150,6 +150,10 @@ void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const 
 // out[k*osk + r*osr] += scale * sum_m X[m, k] * Y[m, r]   (fp32 atomics into the grad buffer)
 void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out, long osk, long osr, long M, int K, int R,
                 float scale, LoraDrop drop, hipStream_t st);
+// rank 8, one pass over dy [M, N]:  dB[r*ldd + n] += s * sum_m u[m, r] dy[m, n]  (fp32 atomics) and
+// v[m*ldv + r] = s * sum_n dy[m, n] B[r, n]  (bf16); vpart = fp32 scratch of cdiv(N, 256) * M * 8
+void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,
+             float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st);
 // W[k*wsk + n*wsn] += s * sum_r A[r, k] * B[r, n]   (A [R,K], B [R,N] fp32)
 void lora_merge(void* W, int w_is_bf16, long wsk, long wsn, const float* A, const float* B, int K, int N, int R, float s,
                 hipStream_t st);

@@ -260,6 +260,149 @@ __global__ __launch_bounds__(1024) void lora_wgrad_kernel(const bf16_t* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------ dy pass
+// lora_dy (rank 8): ONE streaming pass over dy [M, N] for both rank-r products that read it
+//   v[m, r]   = s * sum_n dy[m, n] B[r, n]    (reduction over N)
+//   dB[r, n] += s * sum_m u[m, r] dy[m, n]    (reduction over M)
+// replacing lora_rowdot(dy, B) + lora_wgrad(dy, u), which each streamed dy (the largest LoRA operand:
+// M x 2304 for the fused qkv projection) from HBM.
+//
+// Both products run on MFMA (v_mfma_f32_16x16x32_bf16).  A wave owns 32-row tiles of one 256-column
+// strip.  Its dy tile is loaded ONCE from HBM with 16-B loads straight into A-operand fragments
+// (lane: row l&15, 8 contiguous columns), which
+//   * feed v += dy B^T directly (B^T fragments of the strip stay in registers), and
+//   * are written to the wave's own padded LDS image, read back transposed (ds_read_b64_tr_b16) as
+//     the B operand of dB^T-tile += u^T dy, with u^T staged through a tiny [32][16] LDS image.
+// dB accumulates over the wave's tiles in 16 f32x4 registers; the 4 waves of the block fold through
+// LDS and issue one fp32 atomic per (rank, column) per block (256-B contiguous per wave instruction).
+// v partial sums per 256-column strip go to an fp32 scratch [strip][M][8] summed by lora_dy_finish.
+constexpr int kDyLd = 256 + 8;  // padded LDS row (elements): transposed reads conflict-free
+
+__global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restrict__ dy, long ldy,
+                                                         const bf16_t* __restrict__ B, long ldb,
+                                                         const bf16_t* __restrict__ u, long ldu, float* __restrict__ dB,
+                                                         long ldd, float* __restrict__ vpart, long M, int N, long chunk,
+                                                         float s) {
+  // per wave: dy image [32][kDyLd] + u^T image [32][16]; block reduction buffer aliases the images
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4][32 * kDyLd + 32 * 16];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int n0 = blockIdx.x * 256;
+  bf16_t* img = lds[w];
+  bf16_t* uimg = lds[w] + 32 * kDyLd;
+  // B^T fragments of the strip: lane holds B[r = l&15][n0 + 32 cg + 8g + j] (zero for r >= 8 / n >= N)
+  bf16x8_t bt[8];
+#pragma unroll
+  for (int cg = 0; cg < 8; ++cg) {
+    const int n = n0 + 32 * cg + 8 * g;
+    bt[cg] = (c16 < 8 && n < N) ? *reinterpret_cast<const bf16x8_t*>(B + (long)c16 * ldb + n) : bf16x8_t{};
+  }
+  // zero ranks 8..15 of the u^T image once (rows are rewritten per tile, ranks 0..7 only)
+  if (lane < 32) *reinterpret_cast<u16x8_t*>(uimg + lane * 16 + 8) = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  f32x4_t db[16];
+#pragma unroll
+  for (int cb = 0; cb < 16; ++cb) db[cb] = zero4();
+  const long mbeg = (long)blockIdx.y * chunk;
+  const long mend = min(M, mbeg + chunk);
+  for (long t0 = mbeg + 32 * w; t0 < mend; t0 += 128) {
+    // ---- loads: dy A fragments (2 row blocks x 8 column groups) and this tile's u rows
+    bf16x8_t a[2][8];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const long m = t0 + 16 * rb + c16;
+      const bool rok = m < mend;
+      const bf16_t* rowp = dy + (rok ? m : mbeg) * ldy;
+#pragma unroll
+      for (int cg = 0; cg < 8; ++cg) {
+        const int n = n0 + 32 * cg + 8 * g;
+        a[rb][cg] = (rok && n < N) ? *reinterpret_cast<const bf16x8_t*>(rowp + n) : bf16x8_t{};
+      }
+    }
+    u16x8_t ur{0, 0, 0, 0, 0, 0, 0, 0};
+    if (lane < 32 && t0 + lane < mend) ur = *reinterpret_cast<const u16x8_t*>(u + (t0 + lane) * ldu);
+    // ---- v partials: D[row][rank] += dy[row][32 cols] . B^T[32 cols][rank]
+    f32x4_t vacc[2] = {zero4(), zero4()};
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int cg = 0; cg < 8; ++cg) vacc[rb] = mfma16(a[rb][cg], bt[cg], vacc[rb]);
+    // ---- dy tile -> LDS (row-major, padded), u rows -> u^T image
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int cg = 0; cg < 8; ++cg)
+        *reinterpret_cast<bf16x8_t*>(img + (16 * rb + c16) * kDyLd + 32 * cg + 8 * g) = a[rb][cg];
+    if (lane < 32) *reinterpret_cast<u16x8_t*>(uimg + lane * 16) = ur;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- dB^T tiles: D[rank][16 cols] += u^T[rank][32 rows] . dy[32 rows][16 cols]
+    const bf16x8_t ua = frag_tr(uimg, 16, 0, 0);  // lane: u[row 8g + j][rank l&15]
+#pragma unroll
+    for (int cb = 0; cb < 16; ++cb) db[cb] = mfma16(ua, frag_tr(img, kDyLd, 0, 16 * cb), db[cb]);
+    // v partial rows 4g+i of each 16-row block, rank l&15 (< 8)
+    if (c16 < 8) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const long m = t0 + 16 * rb + 4 * g + i;
+          if (m < mend) vpart[((long)blockIdx.x * M + m) * 8 + c16] = vacc[rb][i];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // tr-reads done before the next tile's writes
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // ---- block fold of dB (ranks 0..7 live in lane groups g = 0, 1) and one atomic per element
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(&lds[0][0]);  // [4 waves][8 ranks][256 cols] fp32 = 32 KB
+  if (g < 2) {
+#pragma unroll
+    for (int cb = 0; cb < 16; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(w * 8 + 4 * g + i) * 256 + 16 * cb + c16] = db[cb][i];
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < 8 * 256; o += 256) {
+    const int r = o >> 8, c = o & 255;
+    if (n0 + c >= N) continue;
+    const float v = red[r * 256 + c] + red[(8 + r) * 256 + c] + red[(16 + r) * 256 + c] + red[(24 + r) * 256 + c];
+    atomicAdd(dB + (long)r * ldd + n0 + c, v * s);
+  }
+}
+
+// v[m, r] = s * sum over strips of vpart[strip, m, r]   (bf16 out, row stride ldv)
+__global__ void lora_dy_finish_kernel(const float* __restrict__ vpart, int nstrip, long M, float s, bf16_t* __restrict__ v,
+                                      long ldv) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= M * 8) return;
+  float a = 0.f;
+  for (int k = 0; k < nstrip; ++k) a += vpart[(long)k * M * 8 + t];
+  v[(t >> 3) * ldv + (t & 7)] = f2bf(a * s);
+}
+
+void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,
+             float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st) {
+  if ((N % 8) || (ldy % 8) || (ldb % 8) || (ldu % 8) || (reinterpret_cast<uintptr_t>(dy) % 16) ||
+      (reinterpret_cast<uintptr_t>(B) % 16) || (reinterpret_cast<uintptr_t>(u) % 16)) {
+    fprintf(stderr, "lora_dy: N and the row strides must be multiples of 8, dy/B/u 16-B aligned\n");
+    abort();
+  }
+  if (M <= 0 || N <= 0) return;
+  const int gx = cdiv(N, 256);
+  // 2 resident blocks per CU (68 KB LDS each): ~512 blocks in total, >= 4 tiles per wave
+  long ny = cdiv(512, gx);
+  const long max_ny = cdiv(M, 512);
+  if (ny > max_ny) ny = max_ny;
+  if (ny < 1) ny = 1;
+  long chunk = cdiv(M, ny);
+  chunk = cdiv(chunk, 128) * 128;
+  dim3 grid(gx, (unsigned)cdiv(M, chunk));
+  lora_dy_kernel<<<grid, 256, 0, st>>>(dy, ldy, B, ldb, u, ldu, dB, ldd, vpart, M, N, chunk, s);
+  lora_dy_finish_kernel<<<cdiv(M * 8, 256), 256, 0, st>>>(vpart, gx, M, s, v, ldv);
+}
+
 template <typename T>
 __global__ void lora_merge_kernel(T* W, long wsk, long wsn, const float* __restrict__ A, const float* __restrict__ B, int K,
                                   int N, int R, float s) {

@@ -607,7 +607,7 @@ class _LoRALinear(Function):
             R = Ac.shape[0]
             dys = dy2[:, c0:c0 + n]
             v = torch.empty(dy2.shape[0], R, device=dy.device, dtype=dy.dtype)
-            C.lora_rowdot(dys, Bc, v, s, 0.0, 0, None)        # v = s dy B^T
+            db_done = _dy_pass(C, dy2, c0, n, B, us[i], 0, R, v, s)  # v = s dy B^T (+ dB in the same pass)
             if dx is not None:
                 C.lora_update(dx, v, Ac, dx, 1.0, dp, salt, ctr)  # dx += mask * (v A)
             gA = gB = None
@@ -622,7 +622,8 @@ class _LoRALinear(Function):
             if _needs(B):
                 buf = _grad_buf(B)
                 tgt = buf if buf is not None else torch.zeros(R, n, device=dy.device)
-                C.lora_wgrad(dys, us[i], tgt, 1, n, s, 0.0, 0, None)  # dB[r, n] += s sum_m u[m, r] dy[m, n]
+                if not db_done:
+                    C.lora_wgrad(dys, us[i], tgt, 1, n, s, 0.0, 0, None)  # dB[r, n] += s sum_m u[m, r] dy[m, n]
                 if buf is not None:
                     grad_ready(B)
                 else:
@@ -693,13 +694,15 @@ class _LoRALinearAug(Function):
             if not fused:
                 dx = gemm_dx(dy2, ctx.waug[:, :K])
         vs = []
+        db_done = set()
         if fused:
             # every v_i = s dy_i B_i^T into one [M, sum r] buffer, then ONE gemm8 launch computes
             # dx = dy W + [v_1 .. v_n] [A_1; ..; A_n] with the rank-r update in its epilogue
             vall = torch.empty(M, sum(ranks), device=dy.device, dtype=dy.dtype)
             o = 0
             for i, (c0, n, dp, salt) in enumerate(ctx.slices):
-                C.lora_rowdot(dy2[:, c0:c0 + n], cw(ab[2 * i + 1]), vall[:, o:o + ranks[i]], s, 0.0, 0, None)
+                if _dy_pass(C, dy2, c0, n, ab[2 * i + 1], xa2, K + o, ranks[i], vall[:, o:o + ranks[i]], s):
+                    db_done.add(i)  # dB_i came out of the same pass over dy_i (lora_dy)
                 vs.append(vall[:, o:o + ranks[i]])
                 o += ranks[i]
             acat = torch.cat([cw(ab[2 * i]) for i in range(len(ranks))]) if len(ranks) > 1 else cw(ab[0])
@@ -734,7 +737,8 @@ class _LoRALinearAug(Function):
             if _needs(B):
                 buf = _grad_buf(B)
                 tgt = buf if buf is not None else torch.zeros(R, n, device=dy.device)
-                C.lora_wgrad(dys, xa2[:, off:off + R], tgt, 1, n, s, 0.0, 0, None)  # dB += s u^T dy
+                if i not in db_done:
+                    C.lora_wgrad(dys, xa2[:, off:off + R], tgt, 1, n, s, 0.0, 0, None)  # dB += s u^T dy
                 if buf is not None:
                     grad_ready(B)
                 else:
@@ -746,6 +750,23 @@ class _LoRALinearAug(Function):
         if dxa is not None:
             dxa = dxa.view(ctx.shape)
         return (dxa, None, None, None, None, None, None, *grads)
+
+
+def _dy_pass(C, dy2, c0, n, B, xa2, uoff, R, v, s) -> bool:
+    """v = s dy[:, c0:c0+n] B^T into ``v``; when B's fp32 grad buffer exists and the shapes meet
+    lora_dy's contract (rank 8, 8-column aligned slice, u columns 16-B aligned), dB += s u^T dy is
+    produced by the SAME pass over dy (returns True); otherwise lora_rowdot only (False).
+    MFT_LORA_DY=0 disables the fused pass (A/B switch)."""
+    buf = _grad_buf(B)
+    M, N = dy2.shape
+    ok = (buf is not None and os.environ.get("MFT_LORA_DY", "1") != "0" and R == 8 and n % 8 == 0 and c0 % 8 == 0
+          and N % 8 == 0 and uoff % 8 == 0 and xa2.stride(0) % 8 == 0)
+    if ok:
+        vpart = torch.empty(((n + 255) // 256) * M * 8, device=dy2.device, dtype=torch.float32)
+        C.lora_dy(dy2[:, c0:c0 + n], cw(B), xa2[:, uoff:uoff + 8], buf, vpart, v, s)
+        return True
+    C.lora_rowdot(dy2[:, c0:c0 + n], cw(B), v, s, 0.0, 0, None)
+    return False
 
 
 def _lora_epi_ok(slices, ranks, dy2, K) -> bool:
