@@ -37,7 +37,7 @@ CONFIGS = {
     "gpt2-lora": dict(model="gpt2", mode="lora", batch=512, seq=128, targets="AttnQKV,AttnProj",
                       metric="tokens/sec GPT-2-124M LoRA r=8 seq128 (training, whole job)"),
     # Gemma-3 270M LoRA r=8 seq 256 (RMSNorm / QK-norm+RoPE / GQA / sliding-window kernels)
-    "gemma3-270m-lora": dict(model="gemma3-270m", mode="lora", batch=128, seq=256, targets="full",
+    "gemma3-270m-lora": dict(model="gemma3-270m", mode="lora", batch=256, seq=256, targets="full",
                              metric="tokens/sec Gemma-3-270M LoRA r=8 seq256 (training, whole job)"),
     # GPT-2 small full fine-tuning, DP over RCCL (bucketed, backward-overlapped all-reduce)
     "gpt2-full": dict(model="gpt2", mode="full", batch=512, seq=128, zero=0,

@@ -853,15 +853,18 @@ def dropout_counter(device):
 def default_ce_chunk(vpad: int) -> int:
     """Rows of bf16 logits materialised at once (the rest of the vocab-chunked CE never exists).
 
-    Measured on MI355X (profiles/): hipBLASLt's LM-head GEMM is far more efficient at M = 8192
-    than at 1024 (the L3-resident 96 MiB chunk lost 20% end-to-end), so we cap by a 2 GiB logits
-    budget instead — 8192 rows for GPT-2 (50304 cols), 4096 for Gemma-3 (262144 cols)."""
+    Sized for 288 GB of HBM: a 16 GiB logits budget (MFT_CE_BUDGET_GB), at most 65536 rows, i.e. the
+    whole GPT-2 bench step (512 x 128 tokens, 6.6 GB) in ONE LM-head GEMM / CE / dgrad triple and
+    Gemma-3 (262144 columns) in 32768-row chunks.  Measured on MI355X (one call, GPT-2 LoRA bench):
+    4096 rows 47.2 ms/step, 8192 44.5, 16384 44.1, 32768 44.0, 65536 43.3 -- fewer, larger GEMMs win
+    and the L3-resident small chunks lose (profiles/)."""
     import os
     env = os.environ.get("MFT_CE_CHUNK")
     if env:
         return int(env)
-    rows = (2 << 30) // (2 * vpad)
-    return max(64, min(8192, rows // 64 * 64))
+    budget = float(os.environ.get("MFT_CE_BUDGET_GB", "16")) * (1 << 30)
+    rows = int(budget // (2 * vpad))
+    return max(64, min(65536, rows // 64 * 64))
 
 
 def _lt_lm_ok(h, wc) -> bool:
