@@ -102,10 +102,16 @@ class Linear(nn.Module):
     def merge_lora(self, sign: float = 1.0):
         """W[col0:col0+n, :] += sign * s * B^T A  (merge; sign=-1 unmerges) — K10."""
         for sl in self.lora_slices:
-            A, B = sl.A.detach().float(), sl.B.detach().float()   # [r, in], [r, n]
-            delta = (B.t() @ A) * (sign * self.lora_scale)          # [n, in]
+            A, B = sl.A.detach().float().contiguous(), sl.B.detach().float().contiguous()   # [r, in], [r, n]
             w = self.weight.data
-            w[sl.col0:sl.col0 + sl.ncols] = (w[sl.col0:sl.col0 + sl.ncols].float() + delta).to(w.dtype)
+            if w.is_cuda and w.is_contiguous() and w.dtype in (torch.bfloat16, torch.float32):
+                # K10 lora_merge kernel (lora.hip): W[col0 + n, k] += sign * s * sum_r A[r, k] B[r, n]
+                from .._ext import native
+                native().lora_merge(w[sl.col0:sl.col0 + sl.ncols], 1, self.in_features, A, B,
+                                    float(sign * self.lora_scale))
+            else:
+                delta = (B.t() @ A) * (sign * self.lora_scale)          # [n, in]
+                w[sl.col0:sl.col0 + sl.ncols] = (w[sl.col0:sl.col0 + sl.ncols].float() + delta).to(w.dtype)
             if getattr(self.weight, "shadow", None) is not None:
                 self.weight.shadow.copy_(self.weight.data.to(self.weight.shadow.dtype))
         Fx.drop_weight_t(self.weight)

@@ -35,3 +35,33 @@ def test_lora_dy_matches_fp32(M, N):
     dBr = dB0 + 0.5 * u.float().t() @ dy.float()
     _close(v, vr, 0.02, 0.01, msg="v")
     _close(dB, dBr, 1e-3 * M ** 0.5, 1e-4, msg="dB")
+
+
+def test_lora_merge_kernel_matches_adapter_forward():
+    """K10: Linear.merge_lora on GPU runs the lora_merge kernel; merged W x == adapter forward, and
+    unmerge restores W (reference graph/test_lora_correctness.cpp:101-187)."""
+    from mobilefinetuner_amd.models.layers import Linear
+    torch.manual_seed(1)
+    K, N = 256, 384
+    lin = Linear(K, N, device=DEV)
+    with torch.no_grad():
+        lin.weight.copy_(torch.randn(N, K) * 0.05)
+        lin.bias.copy_(torch.randn(N) * 0.1)
+    for c0, n in ((0, 128), (128, 256)):
+        A, B = lin.add_lora(c0, n, 8, 2.0, torch.randn(8, K) * 0.05, name=f"m{c0}")
+        with torch.no_grad():
+            B.copy_(torch.randn_like(B) * 0.05)
+    x = torch.randn(64, K, device=DEV).bfloat16()
+    with torch.no_grad():
+        y_adapter = lin(x).float()
+        w0 = lin.weight.detach().float().clone()
+        lin.merge_lora(1.0)
+        lin.lora_enabled = False
+        y_merged = lin(x).float()
+        ref = w0.clone()
+        for sl in lin.lora_slices:
+            ref[sl.col0:sl.col0 + sl.ncols] += 2.0 * sl.B.float().t() @ sl.A.float()
+        _close(lin.weight, ref, 2e-3, 1e-2, msg="merged W")
+        _close(y_merged, y_adapter, 0.03, 0.01, msg="merged forward")
+        lin.merge_lora(-1.0)
+        _close(lin.weight, w0, 2e-3, 1e-2, msg="unmerge")
