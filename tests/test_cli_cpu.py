@@ -82,3 +82,42 @@ def test_eval_mmlu_cli(tmp_path):
                           "--tokenizer_dir", str(tdir), "--model", "gpt2-tiny", "--device", "cpu", "--dtype", "fp32",
                           "--random_init", "--out", str(tmp_path / "m.jsonl")])
     assert res["total"] == 5 and 0.0 <= res["micro"] <= 1.0
+
+
+def test_pretokenize_cli_matches_text_mode(tmp_path):
+    """cli.pretokenize writes the .bin + meta.json that --pretokenized_path reads, with exactly the
+    token stream text mode builds (reference scripts/pretokenize_wikitext2_gemma.py)."""
+    import numpy as np
+    from tokenizers import Tokenizer, models, pre_tokenizers, trainers
+    from mobilefinetuner_amd.cli import pretokenize
+    from mobilefinetuner_amd.data.wikitext2 import LMDataset, WT2Config
+    from mobilefinetuner_amd.tokenizers import GPT2Tokenizer
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    text = [" = Heading = ", "", " Some text , with numbers 12 and words .", " more words here ."]
+    tr = trainers.BpeTrainer(vocab_size=300, special_tokens=["<|endoftext|>"],
+                             initial_alphabet=pre_tokenizers.ByteLevel.alphabet(), show_progress=False)
+    tok.train_from_iterator(text * 10, tr)
+    tdir = tmp_path / "tok"
+    tdir.mkdir()
+    tok.model.save(str(tdir))
+    data = tmp_path / "wt2"
+    data.mkdir()
+    for split, n in (("train", 30), ("valid", 5), ("test", 3)):
+        (data / f"wiki.{split}.raw").write_text("\n".join(text * n) + "\n")
+    out = tmp_path / "pt"
+    assert pretokenize.main(["--data_dir", str(data), "--tokenizer_dir", str(tdir), "--model_type", "gpt2",
+                             "--out_dir", str(out)]) == 0
+    meta = json.load(open(out / "meta.json"))
+    stream = np.fromfile(out / "wt2_gpt2_tokens.bin", dtype=np.int32)
+    assert meta["total_tokens"] == stream.size and set(meta["splits"]) == {"train", "valid", "test"}
+    t = GPT2Tokenizer.from_pretrained(str(tdir))
+    cfg = WT2Config(data_dir=str(data), seq_len=1, eos_id=t.eos_id, shuffle_train=False, drop_last=False)
+    for split in ("train", "valid", "test"):
+        ref = np.asarray(LMDataset.from_text(cfg, split, t).tokens())
+        o, n = meta["splits"][split]["offset"], meta["splits"][split]["length"]
+        assert np.array_equal(stream[o:o + n], ref), split
+    # and the training CLI consumes it
+    pcfg = WT2Config(pretokenized_path=str(out / "wt2_gpt2_tokens.bin"), seq_len=16, shuffle_train=False)
+    ds = LMDataset.from_pretokenized(pcfg, "valid")
+    assert ds.num_sequences() == meta["splits"]["valid"]["length"] // 16 or ds.num_sequences() > 0
