@@ -290,6 +290,22 @@ static void test_dataset() {
     }
   }
   CHECK(total == 20);
+  // multi-threaded line packing (tokenizer calls fan out over threads): EOS after every line incl.
+  // blank ones, order preserved, identical to the single-threaded result
+  std::vector<std::string> lines;
+  for (int i = 0; i < 500; ++i) lines.push_back(i % 7 == 0 ? std::string() : std::string(1 + i % 13, (char)('a' + i % 26)));
+  auto enc = [](const std::string& l) {
+    std::vector<int> o;
+    for (char c : l) o.push_back((int)c);
+    return o;
+  };
+  auto p1 = pack_lines(lines, enc, 1, true, 1.0f, 8, 1);
+  auto p4 = pack_lines(lines, enc, 1, true, 1.0f, 8, 4);
+  CHECK(p1 == p4);
+  size_t expect = 0;
+  for (auto& l : lines) expect += l.size() + 1;
+  CHECK(p1.size() == expect);
+  CHECK(!p1.empty() && p1.back() == 1);
 }
 
 // ----------------------------------------------------------------------------- power monitor
