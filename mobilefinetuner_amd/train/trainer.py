@@ -309,5 +309,10 @@ class Trainer:
             if self.pm is not None:
                 ms = self.pm.suggest_sleep_ms(step + 1)
                 if ms > 0:
+                    # the step is queued asynchronously: drain it first so the GPU really idles for
+                    # the whole pause (a host-only sleep would overlap the running kernels and save
+                    # no energy -- the reference's CPU engine slept after finishing its step)
+                    if self.device.type == "cuda":
+                        torch.cuda.synchronize(self.device)
                     time.sleep(ms / 1000.0)
         return self.history
