@@ -88,8 +88,10 @@ def build(a, cfgd, dev, world):
         desc = f"{name} LoRA r={a.rank} alpha={a.alpha:g} targets={a.targets or cfgd['targets']}"
     else:
         model.set_full_finetune()
-        zero = cfgd.get("zero", 0) if world > 1 else 0
-        if a.zero >= 0:  # explicit override (e.g. measure ZeRO-3's gather/scatter cost on 1 GPU)
+        # the config's ZeRO stage also on 1 GPU (the stage's own collectives / gather-release work
+        # is then measured even with nothing to shard across), so a config's label is what ran
+        zero = cfgd.get("zero", 0)
+        if a.zero >= 0:  # explicit override
             zero = a.zero
         offload = bool(cfgd.get("offload", False) or a.offload_optimizer)
         if zero == 3:

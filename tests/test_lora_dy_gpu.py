@@ -51,6 +51,7 @@ def test_lora_merge_kernel_matches_adapter_forward():
         A, B = lin.add_lora(c0, n, 8, 2.0, torch.randn(8, K) * 0.05, name=f"m{c0}")
         with torch.no_grad():
             B.copy_(torch.randn_like(B) * 0.05)
+        A.shadow, B.shadow = A.detach().bfloat16(), B.detach().bfloat16()  # what FlatParams provides
     x = torch.randn(64, K, device=DEV).bfloat16()
     with torch.no_grad():
         y_adapter = lin(x).float()
