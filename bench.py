@@ -205,7 +205,7 @@ def main():
                 "micro_batch_per_gpu": a.batch,
                 "seq_len": a.seq,
                 "parallelism": f"dp{world}",
-                "hipgraph": not a.no_graph,
+                "hipgraph": bool(getattr(step, "use_graph", False)),
                 "final_loss": round(final_loss, 4),
                 "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC if a.config == "gpt2-lora" else None,
             },
