@@ -151,15 +151,14 @@ void attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, T
   const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
   const int Sk = k.size(1), Hkv = k.size(2);
   c10::DeviceGuard g(q.device());
-  const bool short_path = mft::attn_short_path(D, Sq, Sk, (int)window);
+  const int path = mft::attn_bwd_path(D, Sq, Sk, (int)window);
+  const bool short_path = path == 0;
   Tensor delta, dq_acc;
-  if (!short_path) {
-    delta = torch::empty({B, H, Sq}, q.options().dtype(torch::kFloat32));
-    dq_acc = torch::empty({B, Sq, H, D}, q.options().dtype(torch::kFloat32));
-  }
+  if (!short_path) delta = torch::empty({B, H, Sq}, q.options().dtype(torch::kFloat32));
+  if (path == 1) dq_acc = torch::empty({B, Sq, H, D}, q.options().dtype(torch::kFloat32));
   Tensor dk_tmp, dv_tmp;
   mft::AttnBwdArgs a{};
-  if (H != Hkv) {
+  if (H != Hkv && path != 2) {
     dk_tmp = torch::empty({B, Sk, H, D}, q.options());
     dv_tmp = torch::empty({B, Sk, H, D}, q.options());
     a.dk_tmp = bp(dk_tmp); a.dv_tmp = bp(dv_tmp);
@@ -167,7 +166,7 @@ void attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, T
   }
   a.q = bp(q); a.k = bp(k); a.v = bp(v); a.o = bp(o); a.dout = bp(dout); a.lse = fp(lse);
   a.delta = short_path ? nullptr : fp(delta);
-  a.dq_acc = short_path ? nullptr : fp(dq_acc);
+  a.dq_acc = path == 1 ? fp(dq_acc) : nullptr;
   a.dq = bp(dq); a.dk = bp(dk); a.dv = bp(dv);
   fill_st(a.q_st, q); fill_st(a.k_st, k); fill_st(a.v_st, v); fill_st(a.o_st, o); fill_st(a.do_st, dout);
   fill_st(a.dq_st, dq); fill_st(a.dk_st, dk); fill_st(a.dv_st, dv);
@@ -190,21 +189,36 @@ Tensor gelu_bwd(Tensor x, Tensor dy) {
   mft::gelu_bwd(bp(x), bp(dy), bp(dx), x.numel(), stream());
   return dx;
 }
-Tensor gated_fwd(Tensor gu, int64_t act) {
-  CHECK_BF16(gu); CHECK_CONTIG(gu);
+// out_cols > I: y is [M, out_cols] with the activation in the first I columns and the rest zeroed
+// (augmented-K input of the LoRA down projection); gated_bwd then reads that wide dy row-strided.
+Tensor gated_fwd(Tensor gu, int64_t act, int64_t out_cols) {
+  CHECK_CUDA(gu); CHECK_BF16(gu); CHECK_CONTIG(gu);
   const int I = gu.size(-1) / 2;
   TORCH_CHECK(I % 8 == 0, "gated: intermediate size must be a multiple of 8");
+  const long M = gu.numel() / (2 * I);
+  if (out_cols > I) {
+    TORCH_CHECK(out_cols % 8 == 0, "gated: out_cols must be a multiple of 8");
+    auto y = torch::empty({M, out_cols}, gu.options());
+    mft::gated_fwd(bp(gu), bp(y), M, I, out_cols, (int)act, stream());
+    mft::zero_cols(bp(y), out_cols, M, I, (int)(out_cols - I), stream());
+    return y;
+  }
   auto sizes = gu.sizes().vec();
   sizes.back() = I;
   auto y = torch::empty(sizes, gu.options());
-  mft::gated_fwd(bp(gu), bp(y), gu.numel() / (2 * I), I, (int)act, stream());
+  mft::gated_fwd(bp(gu), bp(y), M, I, I, (int)act, stream());
   return y;
 }
 Tensor gated_bwd(Tensor gu, Tensor dy, int64_t act) {
-  CHECK_CONTIG(gu); CHECK_CONTIG(dy);
+  CHECK_CONTIG(gu); CHECK_BF16(gu); CHECK_BF16(dy);
   const int I = gu.size(-1) / 2;
+  const long M = gu.numel() / (2 * I);
+  TORCH_CHECK(dy.stride(-1) == 1 && dy.size(-1) >= I && dy.numel() / dy.size(-1) == M, "gated_bwd: dy shape");
+  const long ldd = dy.dim() >= 2 ? dy.stride(-2) : I;
+  TORCH_CHECK(dy.dim() <= 2 || dy.is_contiguous(), "gated_bwd: dy must be 2-D row-strided or contiguous");
+  TORCH_CHECK(ldd % 8 == 0 && ldd >= I, "gated_bwd: dy row stride");
   auto dgu = torch::empty_like(gu);
-  mft::gated_bwd(bp(gu), bp(dy), bp(dgu), gu.numel() / (2 * I), I, (int)act, stream());
+  mft::gated_bwd(bp(gu), bp(dy), ldd, bp(dgu), M, I, (int)act, stream());
   return dgu;
 }
 

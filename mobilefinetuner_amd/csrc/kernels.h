@@ -52,6 +52,9 @@ void attn_fwd(const AttnArgs& a, hipStream_t s);
 void attn_bwd(const AttnBwdArgs& a, hipStream_t s);
 // true when the single-workgroup-per-(batch, head) kernels run (no delta / dq_acc workspaces)
 bool attn_short_path(int D, int Sq, int Sk, int window);
+// 0: short path; 1: long-sequence kernels with fp32 dQ atomics (needs delta + dq_acc, and the
+// dk_tmp/dv_tmp workspaces under GQA); 2: split dK/dV + dQ kernels (needs delta only)
+int attn_bwd_path(int D, int Sq, int Sk, int window);
 
 // ---------------------------------------------------------------- GEMM (gemm.hip)
 enum GemmEpi { GEMM_EPI_NONE = 0, GEMM_EPI_BIAS = 1, GEMM_EPI_BIAS_GELU = 2, GEMM_EPI_DGELU = 3, GEMM_EPI_F32ACC = 4,
@@ -86,8 +89,8 @@ void gemm8(const GemmArgs& g, int epi, hipStream_t st);
 void gelu_fwd(const bf16_t* x, bf16_t* y, long n, hipStream_t st);
 void gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, long n, hipStream_t st);
 // gu: [M, 2I] (gate | up); y: [M, I]; act 0 = gelu_tanh (GeGLU), 1 = silu (SwiGLU)
-void gated_fwd(const bf16_t* gu, bf16_t* y, long M, int I, int act, hipStream_t st);
-void gated_bwd(const bf16_t* gu, const bf16_t* dy, bf16_t* dgu, long M, int I, int act, hipStream_t st);
+void gated_fwd(const bf16_t* gu, bf16_t* y, long M, int I, long ldy, int act, hipStream_t st);
+void gated_bwd(const bf16_t* gu, const bf16_t* dy, long ldd, bf16_t* dgu, long M, int I, int act, hipStream_t st);
 
 // ---------------------------------------------------------------- embedding (embed.hip)
 // out[m] = wte[ids[m]] * scale (+ wpe[pos0 + m % S])

@@ -48,7 +48,7 @@ __global__ void gelu_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __re
 }
 
 template <int ACT>
-__global__ void gated_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ y, long M, int I) {
+__global__ void gated_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ y, long M, int I, long ldy) {
   const int c8 = I / 8;
   const long n8 = M * c8;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += (long)gridDim.x * blockDim.x) {
@@ -59,13 +59,13 @@ __global__ void gated_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restri
     load8(gu + m * 2 * I + I + c, u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = (ACT == 0 ? gelu_tanh(g[j]) : silu(g[j])) * u[j];
-    store8(y + m * I + c, g);
+    store8(y + m * ldy + c, g);
   }
 }
 
 template <int ACT>
 __global__ void gated_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dy, bf16_t* __restrict__ dgu,
-                                 long M, int I) {
+                                 long M, int I, long ldd) {
   const int c8 = I / 8;
   const long n8 = M * c8;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += (long)gridDim.x * blockDim.x) {
@@ -74,7 +74,7 @@ __global__ void gated_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* __
     float g[8], u[8], d[8], dg[8], du[8];
     load8(gu + m * 2 * I + c, g);
     load8(gu + m * 2 * I + I + c, u);
-    load8(dy + m * I + c, d);
+    load8(dy + m * ldd + c, d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float a = ACT == 0 ? gelu_tanh(g[j]) : silu(g[j]);
@@ -93,15 +93,17 @@ void gelu_fwd(const bf16_t* x, bf16_t* y, long n, hipStream_t st) {
 void gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, long n, hipStream_t st) {
   gelu_bwd_kernel<<<ew_grid(n / 8), 256, 0, st>>>(x, dy, dx, n);
 }
-void gated_fwd(const bf16_t* gu, bf16_t* y, long M, int I, int act, hipStream_t st) {
+// ldy / ldd: row strides of y / dy (> I when y is the widened augmented-K input of a LoRA
+// consumer, see bindings.cpp alloc_wide)
+void gated_fwd(const bf16_t* gu, bf16_t* y, long M, int I, long ldy, int act, hipStream_t st) {
   const int g = ew_grid(M * (I / 8));
-  if (act == 0) gated_fwd_kernel<0><<<g, 256, 0, st>>>(gu, y, M, I);
-  else gated_fwd_kernel<1><<<g, 256, 0, st>>>(gu, y, M, I);
+  if (act == 0) gated_fwd_kernel<0><<<g, 256, 0, st>>>(gu, y, M, I, ldy);
+  else gated_fwd_kernel<1><<<g, 256, 0, st>>>(gu, y, M, I, ldy);
 }
-void gated_bwd(const bf16_t* gu, const bf16_t* dy, bf16_t* dgu, long M, int I, int act, hipStream_t st) {
+void gated_bwd(const bf16_t* gu, const bf16_t* dy, long ldd, bf16_t* dgu, long M, int I, int act, hipStream_t st) {
   const int g = ew_grid(M * (I / 8));
-  if (act == 0) gated_bwd_kernel<0><<<g, 256, 0, st>>>(gu, dy, dgu, M, I);
-  else gated_bwd_kernel<1><<<g, 256, 0, st>>>(gu, dy, dgu, M, I);
+  if (act == 0) gated_bwd_kernel<0><<<g, 256, 0, st>>>(gu, dy, dgu, M, I, ldd);
+  else gated_bwd_kernel<1><<<g, 256, 0, st>>>(gu, dy, dgu, M, I, ldd);
 }
 
 }  // namespace mft

@@ -18,6 +18,7 @@
 // of 64 keys are staged row-major in LDS with 16-B vector copies; S = Q K^T takes K by rows, and
 // O += P V takes V through ds_read_b64_tr_b16 transposed reads (no transposed copy of V).
 // Online softmax in base 2 with the scale folded into one multiplier.
+#include <algorithm>
 #include <cstdlib>
 
 #include "mfma.h"
@@ -643,11 +644,369 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
   if (16 * w < S) store_tile16<D>(T, D, dQa, one, dq, dqs, b, h, 16 * w, min(16, S - 16 * w));
 }
 
+// ============================================================================================
+// Split path (every shape the short path does not take; Gemma-3: D = 256, GQA 4:1, S = 256..):
+// scores are computed TRANSPOSED as in the short path, so P / dS become the A operand of the next
+// MFMA straight from registers (pack_c2a + frag_tr_perm) -- no LDS round trip, no scalar LDS
+// writes.  32-row K/V (or Q/dO) tiles are staged through LDS with rows padded to D + 8 elements
+// (conflict-free ds_read_b128 row fragments).
+//   * forward: a workgroup owns 16*NW queries of one head (each wave 16, Q in registers as the B
+//     operand of S^T = K Q^T); online softmax stats are per C column, reduced over the 4 lane groups.
+//   * backward dK/dV: a workgroup owns 16*NW keys of one KV head and sweeps every query of EVERY
+//     q-head of its GQA group, so dK/dV are summed over the group in registers (no expanded
+//     per-q-head buffer, no reduction pass).
+//   * backward dQ: a workgroup owns 16*NW queries and recomputes S and dP per key tile; dQ is
+//     written once in bf16 (no fp32 atomics, workspace memset or conversion pass).
+// ============================================================================================
+constexpr int kSplitBK = 32;  // rows per staged tile
+
+// two 32-row tiles (rows >= nvalid zero-filled) -> lds0/lds1 [32][D + 8]; all loads issue first
+template <int D, int NT>
+__device__ __forceinline__ void stage32x2(bf16_t* lds0, bf16_t* lds1, const bf16_t* src0, const bf16_t* src1,
+                                          AttnStrides s0, AttnStrides s1, int b, int h, int row0, int nvalid) {
+  constexpr int CPR = D / 8, LD = D + 8, PER = (kSplitBK * CPR + NT - 1) / NT;
+  u16x8_t r0[PER], r1[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = threadIdx.x + j * NT, r = c / CPR, ch = c % CPR;
+    const bool ok = c < kSplitBK * CPR && r < nvalid;
+    r0[j] = ok ? *reinterpret_cast<const u16x8_t*>(src0 + b * s0.sb + (long)(row0 + r) * s0.ss + h * s0.sh + ch * 8)
+               : u16x8_t{};
+    r1[j] = ok ? *reinterpret_cast<const u16x8_t*>(src1 + b * s1.sb + (long)(row0 + r) * s1.ss + h * s1.sh + ch * 8)
+               : u16x8_t{};
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = threadIdx.x + j * NT, r = c / CPR, ch = c % CPR;
+    if (c < kSplitBK * CPR) {
+      *reinterpret_cast<u16x8_t*>(lds0 + r * LD + ch * 8) = r0[j];
+      *reinterpret_cast<u16x8_t*>(lds1 + r * LD + ch * 8) = r1[j];
+    }
+  }
+}
+
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+    float* __restrict__ lse, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides os, int H, int Hkv, int Sq,
+    int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
+  constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + 8;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* Ks = smem;        // [BK][LD]
+  bf16_t* Vs = Ks + BK * LD;  // [BK][LD]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * BQ, hk = h / (H / Hkv);
+  const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
+  const int coff = Sk - Sq;
+  const float c2 = scale * kLog2e;
+  const int wq_lo = q0 + 16 * w, wq_hi = wq_lo + 15;
+  const int qi = wq_lo + c16;  // this lane's query (C column)
+  bf16x8_t qf[D / 32];         // B operand of S^T = K Q^T: Q[qi][32 s + 8 g + j]
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s)
+    qf[s] = qi < Sq ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qi * qs.ss + h * qs.sh + s * 32 + 8 * g)
+                    : bf16x8_t{};
+  f32x4_t acc[D / 16];
+#pragma unroll
+  for (int n = 0; n < D / 16; ++n) acc[n] = zero4();
+  float m = -INFINITY, l = 0.f;  // running stats of query qi (identical in the 4 lane groups)
+  int kend = kv_len;
+  if (causal) kend = min(kend, q0 + BQ + coff);
+  int kstart = 0;
+  if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
+  for (int kb = kstart; kb < kend; kb += BK) {
+    __syncthreads();
+    stage32x2<D, NT>(Ks, Vs, k, v, ks, vs, b, hk, kb, min(BK, kv_len - kb));
+    __syncthreads();
+    const bool live = wq_lo < Sq && (!causal || kb <= wq_hi + coff) &&
+                      (window <= 0 || wq_lo + coff - (kb + BK - 1) < window);
+    if (!live) continue;  // wave-uniform; the next barrier is at the loop head
+    f32x4_t st[2];        // st[t][i] = S[key kb + 16 t + 4 g + i][qi]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      st[t] = zero4();
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) st[t] = mfma16(frag_row(Ks, LD, 16 * t, s * 32), qf[s], st[t]);
+    }
+    const bool need_mask = kb + BK > kv_len || (causal && kb + BK - 1 > wq_lo + coff) ||
+                           (window > 0 && wq_hi + coff - kb >= window) || wq_hi >= Sq;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sv = st[t][i] * c2;
+        if (need_mask && !(qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window)))
+          sv = -INFINITY;
+        st[t][i] = sv;
+        mx = fmaxf(mx, sv);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float msafe = mnew == -INFINITY ? 0.f : mnew;
+    const float alpha = exp2f(m - msafe);
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = exp2f(st[t][i] - msafe);
+        st[t][i] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mnew;
+    // acc rows are queries 4 g + i: their alpha lives in lane 4 g + i (C column = that query)
+    float ar[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ar[i] = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+    for (int n = 0; n < D / 16; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[n][i] *= ar[i];
+    const bf16x8_t pa = pack_c2a(st[0], st[1]);
+#pragma unroll
+    for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr_perm(Vs, LD, 0, n * 16), acc[n]);
+  }
+  const float inv_own = l > 0.f ? 1.f / l : 0.f;
+  if (g == 0 && qi < Sq) lse[((long)b * H + h) * Sq + qi] = l > 0.f ? (m + log2f(l)) / kLog2e : 1e30f;
+  float inv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) inv[i] = __shfl(inv_own, 4 * g + i, 64);
+  __syncthreads();  // K/V tiles dead: reuse LDS as per-wave output staging
+  if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * LD, LD, acc, inv, o, os, b, h, wq_lo, min(16, Sq - wq_lo));
+}
+
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
+    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides dos,
+    AttnStrides dks, AttnStrides dvs, int H, int Hkv, int Sq, int Sk, float scale, int causal, int window,
+    const int* __restrict__ kv_lens) {
+  constexpr int NT = 64 * NW, BKEY = 16 * NW, BQ = kSplitBK, LD = D + 8;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* Qs = smem;            // [BQ][LD]
+  bf16_t* dOs = Qs + BQ * LD;   // [BQ][LD]
+  float* ls = reinterpret_cast<float*>(dOs + BQ * LD);  // [BQ] lse * log2 e
+  float* dl = ls + BQ;                                  // [BQ] delta
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  const int b = blockIdx.z, hk = blockIdx.y, kb = blockIdx.x * BKEY, G = H / Hkv;
+  const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
+  const int coff = Sk - Sq;
+  const float c2 = scale * kLog2e;
+  const int wk_lo = kb + 16 * w, wk_hi = wk_lo + 15;
+  const int key = wk_lo + c16;  // this lane's key (C column of S = Q K^T)
+  bf16x8_t kf[D / 32], vf[D / 32];  // B operands: K[key][32 s + 8 g + j], V[key][...]
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    const bool ok = key < Sk;
+    kf[s] = ok ? *reinterpret_cast<const bf16x8_t*>(k + b * ks.sb + (long)key * ks.ss + hk * ks.sh + s * 32 + 8 * g)
+               : bf16x8_t{};
+    vf[s] = ok ? *reinterpret_cast<const bf16x8_t*>(v + b * vs.sb + (long)key * vs.ss + hk * vs.sh + s * 32 + 8 * g)
+               : bf16x8_t{};
+  }
+  f32x4_t dKa[D / 16], dVa[D / 16];
+#pragma unroll
+  for (int n = 0; n < D / 16; ++n) { dKa[n] = zero4(); dVa[n] = zero4(); }
+  int qstart = 0, qend = Sq;
+  if (causal) qstart = max(0, kb - coff) / BQ * BQ;
+  if (window > 0) qend = min(Sq, kb + BKEY - 1 - coff + window);
+  if (kb >= kv_len) qend = qstart;  // fully padded key block: grads are zero
+  const bool wave_keys = wk_lo < kv_len;
+  for (int gi = 0; gi < G; ++gi) {
+    const int h = hk * G + gi;
+    for (int q0 = qstart; q0 < qend; q0 += BQ) {
+      __syncthreads();
+      stage32x2<D, NT>(Qs, dOs, q, dout, qs, dos, b, h, q0, min(BQ, Sq - q0));
+      if (threadIdx.x < BQ) {
+        const int qi = q0 + threadIdx.x;
+        ls[threadIdx.x] = qi < Sq ? lse[((long)b * H + h) * Sq + qi] * kLog2e : 1e30f;
+        dl[threadIdx.x] = qi < Sq ? delta[((long)b * H + h) * Sq + qi] : 0.f;
+      }
+      __syncthreads();
+      const bool live = wave_keys && (!causal || q0 + BQ - 1 + coff >= wk_lo) &&
+                        (window <= 0 || q0 + coff - wk_hi < window);
+      if (!live) continue;
+      f32x4_t sc[2], dp[2];  // [t][i] = S / dP [query q0 + 16 t + 4 g + i][key]
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        sc[t] = zero4();
+        dp[t] = zero4();
+#pragma unroll
+        for (int s = 0; s < D / 32; ++s) {
+          sc[t] = mfma16(frag_row(Qs, LD, 16 * t, s * 32), kf[s], sc[t]);
+          dp[t] = mfma16(frag_row(dOs, LD, 16 * t, s * 32), vf[s], dp[t]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qr = 16 * t + 4 * g + i, qi = q0 + qr;
+          const bool ok = qi < Sq && attn_allowed(qi, key, kv_len, coff, causal, window);
+          const float p = ok ? exp2f(sc[t][i] * c2 - ls[qr]) : 0.f;
+          sc[t][i] = p;
+          dp[t][i] = p * (dp[t][i] - dl[qr]) * scale;
+        }
+      }
+      const bf16x8_t pa = pack_c2a(sc[0], sc[1]);  // A: m = key, k = query (permuted)
+      const bf16x8_t da = pack_c2a(dp[0], dp[1]);
+#pragma unroll
+      for (int n = 0; n < D / 16; ++n) {
+        dVa[n] = mfma16(pa, frag_tr_perm(dOs, LD, 0, n * 16), dVa[n]);
+        dKa[n] = mfma16(da, frag_tr_perm(Qs, LD, 0, n * 16), dKa[n]);
+      }
+    }
+  }
+  __syncthreads();  // Q/dO tiles dead: reuse LDS as per-wave output staging
+  const float one[4] = {1.f, 1.f, 1.f, 1.f};
+  if (wk_lo < Sk) {
+    bf16_t* T = smem + w * 16 * LD;
+    store_tile16<D>(T, LD, dKa, one, dk, dks, b, hk, wk_lo, min(16, Sk - wk_lo));
+    store_tile16<D>(T, LD, dVa, one, dv, dvs, b, hk, wk_lo, min(16, Sk - wk_lo));
+  }
+}
+
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
+    bf16_t* __restrict__ dq, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides dos, AttnStrides dqs, int H,
+    int Hkv, int Sq, int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
+  constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + 8;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* Ks = smem;          // [BK][LD]
+  bf16_t* Vs = Ks + BK * LD;  // [BK][LD]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * BQ, hk = h / (H / Hkv);
+  const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
+  const int coff = Sk - Sq;
+  const float c2 = scale * kLog2e;
+  const int wq_lo = q0 + 16 * w, wq_hi = wq_lo + 15;
+  const int qi = wq_lo + c16;
+  bf16x8_t qf[D / 32], df[D / 32];  // B operands: Q[qi][32 s + 8 g + j], dO[qi][...]
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    const bool ok = qi < Sq;
+    qf[s] = ok ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qi * qs.ss + h * qs.sh + s * 32 + 8 * g)
+               : bf16x8_t{};
+    df[s] = ok ? *reinterpret_cast<const bf16x8_t*>(dout + b * dos.sb + (long)qi * dos.ss + h * dos.sh + s * 32 + 8 * g)
+               : bf16x8_t{};
+  }
+  const float lq = qi < Sq ? lse[((long)b * H + h) * Sq + qi] * kLog2e : 1e30f;
+  const float dlq = qi < Sq ? delta[((long)b * H + h) * Sq + qi] : 0.f;
+  f32x4_t dQa[D / 16];
+#pragma unroll
+  for (int n = 0; n < D / 16; ++n) dQa[n] = zero4();
+  int kend = kv_len;
+  if (causal) kend = min(kend, q0 + BQ + coff);
+  int kstart = 0;
+  if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
+  for (int kb = kstart; kb < kend; kb += BK) {
+    __syncthreads();
+    stage32x2<D, NT>(Ks, Vs, k, v, ks, vs, b, hk, kb, min(BK, kv_len - kb));
+    __syncthreads();
+    const bool live = wq_lo < Sq && (!causal || kb <= wq_hi + coff) &&
+                      (window <= 0 || wq_lo + coff - (kb + BK - 1) < window);
+    if (!live) continue;
+    f32x4_t st[2], dpt[2];  // [t][i] = S^T / dP^T [key kb + 16 t + 4 g + i][qi]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      st[t] = zero4();
+      dpt[t] = zero4();
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) {
+        st[t] = mfma16(frag_row(Ks, LD, 16 * t, s * 32), qf[s], st[t]);
+        dpt[t] = mfma16(frag_row(Vs, LD, 16 * t, s * 32), df[s], dpt[t]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window);
+        const float p = ok ? exp2f(st[t][i] * c2 - lq) : 0.f;
+        dpt[t][i] = p * (dpt[t][i] - dlq) * scale;
+      }
+    }
+    const bf16x8_t da = pack_c2a(dpt[0], dpt[1]);  // A: m = query, k = key (permuted)
+#pragma unroll
+    for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(da, frag_tr_perm(Ks, LD, 0, n * 16), dQa[n]);
+  }
+  __syncthreads();
+  const float one[4] = {1.f, 1.f, 1.f, 1.f};
+  if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * LD, LD, dQa, one, dq, dqs, b, h, wq_lo, min(16, Sq - wq_lo));
+}
+
+static AttnStrides mk(const long* st) { return AttnStrides{st[0], st[1], st[2]}; }
+
 bool attn_short_path(int D, int Sq, int Sk, int window) {
   return D == 64 && Sq == Sk && Sq <= kShortS && window <= 0;
 }
 
-static AttnStrides mk(const long* st) { return AttnStrides{st[0], st[1], st[2]}; }
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+
+// MFT_ATTN_V1=1 keeps the previous long-sequence kernels (fp32 dQ atomics, per-q-head GQA dK/dV)
+// for A/B measurements.
+int attn_bwd_path(int D, int Sq, int Sk, int window) {
+  if (attn_short_path(D, Sq, Sk, window)) return 0;
+  static const int v1 = env_int("MFT_ATTN_V1", 0);
+  return v1 == 1 ? 1 : 2;
+}
+
+// waves per workgroup of the split kernels (4 or 8): MFT_ATTN_NW_{FWD,DKDV,DQ}
+static int split_nw(const char* name, int dflt) {
+  const int v = env_int(name, dflt);
+  return v == 4 || v == 8 ? v : dflt;
+}
+
+template <int D, int NW>
+static void fwd_split_launch(const AttnArgs& a, hipStream_t stream) {
+  constexpr int LD = D + 8;
+  const size_t shm = sizeof(bf16_t) * std::max(2 * kSplitBK * LD, NW * 16 * LD);
+  static bool attr = false;
+  if (!attr) {
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_split_kernel<D, NW>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  attn_fwd_split_kernel<D, NW><<<dim3(cdiv(a.Sq, 16 * NW), a.H, a.B), 64 * NW, shm, stream>>>(
+      a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale,
+      a.causal, a.window, a.kv_lens);
+}
+
+template <int D, int NW>
+static void dkdv_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
+  constexpr int LD = D + 8;
+  const size_t shm = std::max(sizeof(bf16_t) * 2 * kSplitBK * LD + sizeof(float) * 2 * kSplitBK,
+                              sizeof(bf16_t) * NW * 16 * LD);
+  static bool attr = false;
+  if (!attr) {
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<D, NW>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  attn_bwd_dkdv_kernel<D, NW><<<dim3(cdiv(a.Sk, 16 * NW), a.Hkv, a.B), 64 * NW, shm, stream>>>(
+      a.q, a.k, a.v, a.dout, a.lse, a.delta, a.dk, a.dv, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.do_st),
+      mk(a.dk_st), mk(a.dv_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale, a.causal, a.window, a.kv_lens);
+}
+
+template <int D, int NW>
+static void dq_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
+  constexpr int LD = D + 8;
+  const size_t shm = sizeof(bf16_t) * std::max(2 * kSplitBK * LD, NW * 16 * LD);
+  static bool attr = false;
+  if (!attr) {
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, NW>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  attn_bwd_dq_kernel<D, NW><<<dim3(cdiv(a.Sq, 16 * NW), a.H, a.B), 64 * NW, shm, stream>>>(
+      a.q, a.k, a.v, a.dout, a.lse, a.delta, a.dq, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.do_st), mk(a.dq_st), a.H,
+      a.Hkv, a.Sq, a.Sk, a.scale, a.causal, a.window, a.kv_lens);
+}
+
 
 template <int D>
 static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
@@ -665,6 +1024,11 @@ static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
                                                                        a.causal, a.kv_lens);
       return;
     }
+  }
+  if (attn_bwd_path(D, a.Sq, a.Sk, a.window) == 2) {
+    if (split_nw("MFT_ATTN_NW_FWD", 8) == 8) fwd_split_launch<D, 8>(a, stream);
+    else fwd_split_launch<D, 4>(a, stream);
+    return;
   }
   constexpr int BQ = 64, BK = 64, LDP = BK + 8;
   const size_t shm = sizeof(bf16_t) * (2 * BK * D + 4 * 16 * LDP);
@@ -704,6 +1068,13 @@ static void bwd_launch(const AttnBwdArgs& a, hipStream_t stream) {
     const long rows = (long)a.B * a.H * a.Sq;
     attn_bwd_delta_kernel<D><<<cdiv(rows * (D / 8), 256), 256, 0, stream>>>(a.o, a.dout, a.delta, mk(a.o_st),
                                                                             mk(a.do_st), a.B, a.H, a.Sq);
+  }
+  if (attn_bwd_path(D, a.Sq, a.Sk, a.window) == 2) {
+    if (split_nw("MFT_ATTN_NW_DKDV", 4) == 8) dkdv_split_launch<D, 8>(a, stream);
+    else dkdv_split_launch<D, 4>(a, stream);
+    if (split_nw("MFT_ATTN_NW_DQ", 8) == 8) dq_split_launch<D, 8>(a, stream);
+    else dq_split_launch<D, 4>(a, stream);
+    return;
   }
   MFT_HIP_CHECK(hipMemsetAsync(a.dq_acc, 0, sizeof(float) * (size_t)a.B * a.Sq * a.H * D, stream));
   const size_t shm = sizeof(bf16_t) * (2 * BK * D + 2 * BQ * D + 2 * BK * LDT) + sizeof(float) * 2 * BQ;

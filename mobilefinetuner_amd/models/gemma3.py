@@ -149,16 +149,14 @@ class Gemma3Layer(nn.Module):
 
     def attn(self, h, B, S, cos, sin, kv_lens):
         qkv = self.qkv_proj(h).view(B, S, self.nq + 2 * self.nkv, self.D)
-        q = Fx.qk_norm_rope(qkv[:, :, :self.nq], self.q_norm.weight, cos, sin, self.q_norm.eps, 1.0,
-                            self.interleaved_rope)
-        k = Fx.qk_norm_rope(qkv[:, :, self.nq:self.nq + self.nkv], self.k_norm.weight, cos, sin, self.k_norm.eps,
-                            1.0, self.interleaved_rope)
-        v = qkv[:, :, self.nq + self.nkv:]
-        o = Fx.flash_attention(q, k, v, self.scale, True, self.window, kv_lens)
-        return self.o_proj(o.view(B * S, self.nq * self.D))
+        # O goes straight into o_proj's augmented-K input when it carries a LoRA adapter
+        o = Fx.qk_norm_rope_attention(qkv, self.nq, self.nkv, self.q_norm.weight, self.k_norm.weight, cos, sin,
+                                      self.q_norm.eps, self.k_norm.eps, 1.0, self.interleaved_rope, self.scale,
+                                      self.window, kv_lens, self.o_proj.aug_cols())
+        return self.o_proj(o.view(B * S, -1))
 
     def mlp(self, h):
-        return self.down_proj(Fx.gated_act(self.gate_up_proj(h), self.act))
+        return self.down_proj(Fx.gated_act(self.gate_up_proj(h), self.act, self.down_proj.aug_cols()))
 
 
 class Gemma3Model(nn.Module):

@@ -190,16 +190,18 @@ class _Gelu(Function):
 
 class _Gated(Function):
     @staticmethod
-    def forward(ctx, gu, act):
+    def forward(ctx, gu, act, out_cols):
         gu = gu.contiguous()
         ctx.save_for_backward(gu)
         ctx.act = act
-        return native().gated_fwd(gu, act)
+        return native().gated_fwd(gu, act, out_cols)
 
     @staticmethod
     def backward(ctx, dy):
         (gu,) = ctx.saved_tensors
-        return native().gated_bwd(gu, dy.contiguous(), ctx.act), None
+        if dy.dim() != 2 or dy.stride(-1) != 1:
+            dy = dy.contiguous()
+        return native().gated_bwd(gu, dy, ctx.act), None, None
 
 
 def gelu(x):
@@ -208,12 +210,18 @@ def gelu(x):
     return _Gelu.apply(x)
 
 
-def gated_act(gu, act="gelu"):
-    """gelu_tanh(gate) * up (GeGLU, Gemma) or silu(gate) * up (SwiGLU); gu = [gate | up]."""
+def gated_act(gu, act="gelu", out_cols=0):
+    """gelu_tanh(gate) * up (GeGLU, Gemma) or silu(gate) * up (SwiGLU); gu = [gate | up].
+    out_cols > I (GPU): returns [M, out_cols] with the activation in the first I columns and zeros
+    after, the augmented-K input of a LoRA consumer (Linear.aug_cols)."""
     a = 0 if act in ("gelu", "gelu_tanh", "gelu_pytorch_tanh") else 1
     if not gu.is_cuda:
         return ref.gated(gu, a).to(gu.dtype)
-    return _Gated.apply(gu, a)
+    I = gu.shape[-1] // 2
+    oc = int(out_cols) if out_cols and out_cols > I else 0
+    if oc:
+        gu = gu.reshape(-1, 2 * I)
+    return _Gated.apply(gu, a, oc)
 
 
 # ---------------------------------------------------------------- embedding
@@ -362,6 +370,73 @@ def qk_norm_rope(x, w, cos, sin, eps=1e-6, offset=1.0, interleaved=False):
         y = ref.rms_norm(x, rw(w), eps, offset).to(x.dtype)
         return ref.rope(y, cos, sin, 0, interleaved).to(x.dtype)
     return _QKNormRoPE.apply(x, w, cos, sin, float(eps), float(offset), bool(interleaved))
+
+
+# ---------------------------------------------------------------- Gemma attention block
+class _QKNormRoPEAttn(Function):
+    """Gemma-3 attention core on the packed qkv GEMM output [B, S, nq + 2 nkv, D]: per-head q/k
+    RMSNorm + RoPE, then causal (sliding-window) GQA flash attention.  Replaces the reference's
+    separate q_norm / k_norm / rope / attention graph nodes (models/gemma_model.cpp attention
+    block).  One Function owns all three slices of qkv so the backward writes a single packed
+    dqkv: the attention backward stores dV straight into its slice and the q/k norm-RoPE backward
+    kernels store dQ / dK into theirs -- no zero-filled per-view gradients summed by autograd.
+    out_cols > nq*D: O is written into a [B, S, out_cols] buffer (augmented-K input of o_proj)."""
+
+    @staticmethod
+    def forward(ctx, qkv, wq, wk, cos, sin, eps_q, eps_k, offset, interleaved, nq, nkv, scale, window, kv_lens,
+                out_cols):
+        C = native()
+        wqc, wkc = cw(wq), cw(wk)
+        q, rq = C.qknorm_rope_fwd(qkv[:, :, :nq], wqc, cos, sin, 0, eps_q, offset, interleaved)
+        k, rk = C.qknorm_rope_fwd(qkv[:, :, nq:nq + nkv], wkc, cos, sin, 0, eps_k, offset, interleaved)
+        o_full, lse, o = C.attn_fwd(q, k, qkv[:, :, nq + nkv:], scale, True, window, kv_lens, out_cols)
+        ctx.save_for_backward(qkv, q, k, o, lse, rq, rk, wqc, wkc, cos, sin)
+        ctx.w = (wq, wk)
+        ctx.cfg = (offset, interleaved, nq, nkv, scale, window, kv_lens)
+        ctx.wide = out_cols > 0 and o_full.dim() == 3
+        return o_full
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, q, k, o, lse, rq, rk, wqc, wkc, cos, sin = ctx.saved_tensors
+        offset, interleaved, nq, nkv, scale, window, kv_lens = ctx.cfg
+        C = native()
+        B, S, _, D = qkv.shape
+        if ctx.wide:
+            do = do[..., :nq * D].view(B, S, nq, D)
+        if do.stride(-1) != 1 or not ctx.wide:
+            do = do.contiguous()
+        dqkv = torch.empty_like(qkv)
+        dq = torch.empty_like(q)
+        dk = torch.empty_like(k)
+        C.attn_bwd(q, k, qkv[:, :, nq + nkv:], o, do, lse, dq, dk, dqkv[:, :, nq + nkv:], scale, True, window,
+                   kv_lens)
+        grads = []
+        for w, wc, x, dy, r, dst in ((ctx.w[0], wqc, qkv[:, :, :nq], dq, rq, dqkv[:, :, :nq]),
+                                     (ctx.w[1], wkc, qkv[:, :, nq:nq + nkv], dk, rk, dqkv[:, :, nq:nq + nkv])):
+            buf = _grad_buf(w)
+            tmp = torch.zeros(w.shape, device=qkv.device) if (_needs(w) and buf is None) else None
+            C.qknorm_rope_bwd(x, dy, r, wc, dst, buf if buf is not None else tmp, cos, sin, 0, offset, interleaved)
+            if buf is not None:
+                grad_ready(w)
+            grads.append(tmp.to(w.dtype) if tmp is not None else None)
+        return (dqkv, grads[0], grads[1]) + (None,) * 12
+
+
+def qk_norm_rope_attention(qkv, nq, nkv, wq, wk, cos, sin, eps_q, eps_k, offset=1.0, interleaved=False, scale=None,
+                           window=0, kv_lens=None, out_cols=0):
+    """qkv [B,S,nq+2nkv,D] -> o [B,S,nq,D] = attention(rope(rmsnorm_q(q)), rope(rmsnorm_k(k)), v);
+    with out_cols > nq*D (GPU) -> [B,S,out_cols] whose first nq*D columns hold O."""
+    D = qkv.shape[-1]
+    if scale is None:
+        scale = 1.0 / math.sqrt(D)
+    if not qkv.is_cuda:
+        q = qk_norm_rope(qkv[:, :, :nq], wq, cos, sin, eps_q, offset, interleaved)
+        k = qk_norm_rope(qkv[:, :, nq:nq + nkv], wk, cos, sin, eps_k, offset, interleaved)
+        return flash_attention(q, k, qkv[:, :, nq + nkv:], scale, True, window, kv_lens)
+    oc = int(out_cols) if out_cols and out_cols > nq * D else 0
+    return _QKNormRoPEAttn.apply(qkv, wq, wk, cos, sin, float(eps_q), float(eps_k), float(offset), bool(interleaved),
+                                 int(nq), int(nkv), float(scale), int(window or 0), kv_lens, oc)
 
 
 # ---------------------------------------------------------------- linear layers

@@ -250,6 +250,9 @@ def _attn_ref(q, k, v, scale, causal, window, kv_lens=None):
     (1, 320, 4, 1, 256, True, 64),
     (2, 64, 4, 2, 128, False, 0),
     (1, 1024, 2, 2, 64, True, 0),
+    (2, 200, 4, 1, 256, True, 0),    # split path, partial tile
+    (1, 300, 4, 2, 128, True, 100),  # split path, sliding window
+    (2, 96, 2, 1, 256, False, 0),    # split path, non-causal
 ])
 def test_flash_attention(B, S, H, Hkv, D, causal, window):
     from mobilefinetuner_amd.ops import functional as Fx
@@ -267,6 +270,34 @@ def test_flash_attention(B, S, H, Hkv, D, causal, window):
     _close(q.grad, qr.grad, 0.06, 0.02, msg="attn dq")
     _close(k.grad, kr.grad, 0.06, 0.02, msg="attn dk")
     _close(v.grad, vr.grad, 0.06, 0.02, msg="attn dv")
+
+
+@pytest.mark.parametrize("nw", ["4", "8"])
+def test_flash_attention_split_kvlens_rect(nw, monkeypatch):
+    """Split kernels (D = 256, GQA 4:1) with right padding and Sq < Sk (bottom-right causal), at
+    both workgroup sizes (MFT_ATTN_NW_*)."""
+    from mobilefinetuner_amd._ext import native
+    for var in ("MFT_ATTN_NW_FWD", "MFT_ATTN_NW_DKDV", "MFT_ATTN_NW_DQ"):
+        monkeypatch.setenv(var, nw)
+    B, Sq, Sk, H, Hkv, D = 2, 90, 210, 4, 1, 256
+    q = torch.randn(B, Sq, H, D, device=DEV).bfloat16()
+    k = torch.randn(B, Sk, Hkv, D, device=DEV).bfloat16()
+    v = torch.randn(B, Sk, Hkv, D, device=DEV).bfloat16()
+    kv = torch.tensor([210, 150], dtype=torch.int32, device=DEV)
+    scale = D ** -0.5
+    o, lse, _ = native().attn_fwd(q, k, v, scale, True, 0, kv, 0)
+    go = torch.randn_like(o)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    native().attn_bwd(q, k, v, o, go, lse, dq, dk, dv, scale, True, 0, kv)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    orf, lser = _attn_ref(qr, kr, vr, scale, True, 0, kv)
+    (orf * go.float()).sum().backward()
+    valid = torch.isfinite(lser) & (lser < 1e29)
+    _close(o, orf, 0.03, msg="split o")
+    _close(lse[valid], lser[valid], 0.05, msg="split lse")
+    _close(dq, qr.grad, 0.06, 0.02, msg="split dq")
+    _close(dk, kr.grad, 0.06, 0.02, msg="split dk")
+    _close(dv, vr.grad, 0.06, 0.02, msg="split dv")
 
 
 def test_flash_attention_lse_and_spike():
@@ -402,6 +433,56 @@ def test_qknorm_rope():
     _close(y, yr, 0.06, msg="qkrope y")
     _close(big.grad, r.grad, 0.1, 0.01, msg="qkrope dx")
     _close(w.grad, wr.grad, 0.5, 0.01, msg="qkrope dw")
+
+
+def test_gated_widened_output():
+    """gated_act(out_cols): activation in the first I columns, zeros after; wide row-strided dy."""
+    from mobilefinetuner_amd.ops import functional as Fx
+    I, OC = 256, 288
+    gu = torch.randn(91, 2 * I, device=DEV).bfloat16().requires_grad_()
+    y = Fx.gated_act(gu, "gelu", OC)
+    assert y.shape == (91, OC)
+    assert y[:, I:].abs().max().item() == 0
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    r = gu.detach().float().requires_grad_()
+    a, u = r.chunk(2, -1)
+    yr = torch.nn.functional.gelu(a, approximate="tanh") * u
+    (yr * g[:, :I].float()).sum().backward()
+    _close(y[:, :I], yr, 0.05, msg="gated wide y")
+    _close(gu.grad, r.grad, 0.1, 0.01, msg="gated wide grad")
+
+
+@pytest.mark.parametrize("nq,nkv,window,oc", [(4, 1, 0, 0), (4, 1, 48, 1056), (2, 2, 0, 544)])
+def test_qknorm_rope_attention_fused(nq, nkv, window, oc):
+    """Fused Gemma attention core (packed qkv -> O, one packed dqkv) vs the fp32 composition."""
+    from mobilefinetuner_amd.ops import functional as Fx
+    from mobilefinetuner_amd.ops import reference as ref
+    B, S, D = 2, 128, 256
+    qkv = (torch.randn(B, S, nq + 2 * nkv, D, device=DEV)).bfloat16().requires_grad_()
+    wq = torch.nn.Parameter(torch.randn(D, device=DEV) * 0.1)
+    wk = torch.nn.Parameter(torch.randn(D, device=DEV) * 0.1)
+    cos, sin = ref.rope_tables(S, D, 10000.0, DEV)
+    scale = 256 ** -0.5
+    o = Fx.qk_norm_rope_attention(qkv, nq, nkv, wq, wk, cos, sin, 1e-6, 1e-6, 1.0, False, scale, window, None, oc)
+    if oc:
+        assert o.shape == (B, S, oc) and o[..., nq * D:].abs().max().item() == 0
+        o = o[..., :nq * D].reshape(B, S, nq, D)
+    g = torch.randn_like(o)
+    (o.float() * g.float()).sum().backward()
+    r = qkv.detach().float().requires_grad_()
+    wqr, wkr = wq.detach().clone().requires_grad_(), wk.detach().clone().requires_grad_()
+
+    def nr(x, w):
+        return ref.rope(x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + w), cos, sin)
+
+    q, k, v = nr(r[:, :, :nq], wqr), nr(r[:, :, nq:nq + nkv], wkr), r[:, :, nq + nkv:]
+    orf = ref.attention(q, k, v, scale, True, window, None)[0]
+    (orf * g.float()).sum().backward()
+    _close(o, orf, 0.03, msg="fused attn o")
+    _close(qkv.grad, r.grad, 0.05, 0.02, msg="fused attn dqkv")
+    _close(wq.grad, wqr.grad, 0.5, 0.02, msg="fused attn dwq")
+    _close(wk.grad, wkr.grad, 0.5, 0.02, msg="fused attn dwk")
 
 
 def test_adamw_matches_reference():
