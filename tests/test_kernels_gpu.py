@@ -413,22 +413,23 @@ def test_embedding():
     _close(wpe.grad[:S], dwpe, 0.05, msg="emb dwpe")
 
 
-def test_qknorm_rope():
+@pytest.mark.parametrize("D,interleaved", [(256, False), (128, False), (64, False), (256, True)])
+def test_qknorm_rope(D, interleaved):
     from mobilefinetuner_amd.ops import functional as Fx
     from mobilefinetuner_amd.ops import reference as ref
-    B, S, H, D = 2, 64, 4, 256
+    B, S, H = 2, 67, 3
     big = torch.randn(B, S, H + 2, D, device=DEV).bfloat16().requires_grad_()
     x = big[:, :, 1:1 + H]
     w = torch.nn.Parameter(torch.randn(D, device=DEV) * 0.1)
     cos, sin = ref.rope_tables(S, D, 10000.0, DEV)
-    y = Fx.qk_norm_rope(x, w, cos, sin, 1e-6, 1.0)
+    y = Fx.qk_norm_rope(x, w, cos, sin, 1e-6, 1.0, interleaved)
     g = torch.randn_like(y)
     (y.float() * g.float()).sum().backward()
     r = big.detach().float().requires_grad_()
     wr = w.detach().clone().requires_grad_()
     xr = r[:, :, 1:1 + H]
     yn = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + wr)
-    yr = ref.rope(yn, cos, sin)
+    yr = ref.rope(yn, cos, sin, 0, interleaved)
     (yr * g.float()).sum().backward()
     _close(y, yr, 0.06, msg="qkrope y")
     _close(big.grad, r.grad, 0.1, 0.01, msg="qkrope dx")
