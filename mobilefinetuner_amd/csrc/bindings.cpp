@@ -329,6 +329,25 @@ void lora_wgrad(Tensor X, Tensor Y, Tensor out, int64_t osk, int64_t osr, double
   mft::lora_wgrad(bp(X), X.stride(-2), bp(Y), Y.stride(-2), fp(out), osk, osr, M, K, R, (float)scale,
                   mkdrop(drop_p, salt, ctr), stream());
 }
+// dA_z += scale * X^T Y[:, 8z:8z+8] for every rank-8 adapter z sharing the input X (one pass over X);
+// outs[z] are contiguous fp32 [8, K] grad buffers
+void lora_wgrad_multi(Tensor X, Tensor Y, std::vector<Tensor> outs, double scale) {
+  CHECK_BF16(X); CHECK_BF16(Y);
+  TORCH_CHECK(X.stride(-1) == 1 && X.stride(-2) % 8 == 0, "lora_wgrad_multi: X rows must be contiguous, stride % 8 == 0");
+  const int K = X.size(-1), R = Y.size(-1);
+  TORCH_CHECK(K % 8 == 0 && Y.stride(-1) == 1, "lora_wgrad_multi: K % 8, Y rows contiguous");
+  TORCH_CHECK(!outs.empty() && outs.size() <= 8 && R == 8 * (int)outs.size(), "lora_wgrad_multi: R must be 8 per output");
+  mft::WgradOuts o{};
+  o.n = (int)outs.size();
+  for (size_t i = 0; i < outs.size(); ++i) {
+    CHECK_F32(outs[i]);
+    TORCH_CHECK(outs[i].is_contiguous() && outs[i].numel() == 8L * K, "lora_wgrad_multi: outputs must be contiguous [8, K]");
+    o.p[i] = fp(outs[i]);
+  }
+  const long M = X.numel() / K;
+  mft::lora_wgrad(bp(X), X.stride(-2), bp(Y), Y.stride(-2), nullptr, 1, K, M, K, R, (float)scale, mft::LoraDrop{nullptr, 0, 0.f},
+                  stream(), &o);
+}
 // rank 8: v = s dy B^T (bf16 [M, 8]) and dB += s u^T dy (fp32 [8, N] grad buffer) in one pass over dy
 void lora_dy(Tensor dy, Tensor B, Tensor u, Tensor dB, Tensor vpart, Tensor v, double s) {
   CHECK_BF16(dy); CHECK_BF16(B); CHECK_BF16(u); CHECK_BF16(v); CHECK_F32(dB); CHECK_F32(vpart);
@@ -520,6 +539,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_rowdot", &lora_rowdot);
   m.def("lora_update", &lora_update);
   m.def("lora_wgrad", &lora_wgrad);
+  m.def("lora_wgrad_multi", &lora_wgrad_multi);
   m.def("lora_merge", &lora_merge);
   m.def("lora_dy", &lora_dy);
   m.def("gemm", &gemm_op, py::arg("A"), py::arg("B"), py::arg("b_nn"), py::arg("epi"), py::arg("bias"), py::arg("aux"),

@@ -151,8 +151,14 @@ void lora_rowdot(const bf16_t* X, long ldx, const bf16_t* Wt, long ldw, bf16_t* 
 void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const bf16_t* W, long ldw, bf16_t* Y, long ldy,
                  long M, int N, int R, float s, LoraDrop drop, hipStream_t st);
 // out[k*osk + r*osr] += scale * sum_m X[m, k] * Y[m, r]   (fp32 atomics into the grad buffer)
+// Segmented form (outs != null, outs->n = R / 8): ranks 8z..8z+7 accumulate into outs->p[z] (rank
+// index restarting at 0) -- dA of several rank-8 adapters that share one input, one pass over X.
+struct WgradOuts {
+  float* p[8];
+  int n;
+};
 void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out, long osk, long osr, long M, int K, int R,
-                float scale, LoraDrop drop, hipStream_t st);
+                float scale, LoraDrop drop, hipStream_t st, const WgradOuts* outs = nullptr);
 // rank 8, one pass over dy [M, N]:  dB[r*ldd + n] += s * sum_m u[m, r] dy[m, n]  (fp32 atomics) and
 // v[m*ldv + r] = s * sum_n dy[m, n] B[r, n]  (bf16); vpart = fp32 scratch of cdiv(N, 256) * M * 8
 void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void lora_update_kernel(const bf16_t* base, lo
 template <int RB, bool YVEC, bool DROP>
 __global__ __launch_bounds__(1024) void lora_wgrad_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Y,
                                                           long ldy, float* __restrict__ out, long osk, long osr, long M, int K,
-                                                          int R, long chunk, float scale, LoraDrop drop) {
+                                                          int R, long chunk, float scale, LoraDrop drop, WgradOuts outs) {
   constexpr int U = DROP ? 6 : 12;
   __shared__ __attribute__((aligned(16))) float red[8][RB][256];
   __shared__ __attribute__((aligned(16))) bf16_t ysh[2][16 * U][RB];
@@ -247,6 +247,8 @@ __global__ __launch_bounds__(1024) void lora_wgrad_kernel(const bf16_t* __restri
   }
   __syncthreads();
   // final 8-way sum over RB x 256 outputs; lane order follows the unit-stride output axis
+  float* const dst = outs.n ? outs.p[blockIdx.z] : out;  // segmented: this rank block's own buffer
+  const int rdst = outs.n ? 0 : r0;
   for (int o = threadIdx.x; o < RB * 256; o += 1024) {
     int r, c;
     if (osk == 1) { r = o >> 8; c = o & 255; }
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(1024) void lora_wgrad_kernel(const bf16_t* __restri
     float v = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) v += red[i][r][c];
-    atomicAdd(out + (long)kk * osk + (long)(r0 + r) * osr, v * scale);
+    atomicAdd(dst + (long)kk * osk + (long)(rdst + r) * osr, v * scale);
   }
 }
 
@@ -453,7 +455,15 @@ void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const 
 }
 
 void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out, long osk, long osr, long M, int K, int R,
-                float scale, LoraDrop drop, hipStream_t st) {
+                float scale, LoraDrop drop, hipStream_t st, const WgradOuts* outs) {
+  WgradOuts so{};
+  if (outs) {
+    if (outs->n < 1 || outs->n > 8 || R != 8 * outs->n) {
+      fprintf(stderr, "lora_wgrad: segmented output needs R == 8 * n (R=%d, n=%d)\n", R, outs ? outs->n : 0);
+      abort();
+    }
+    so = *outs;
+  }
   if ((K % 4) || (ldx % 4) || (reinterpret_cast<uintptr_t>(X) % 8)) {
     fprintf(stderr, "lora_wgrad: K (%d) and ldx (%ld) must be multiples of 4 and X 8-byte aligned\n", K, ldx);
     abort();
@@ -477,9 +487,9 @@ void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out
 #define MFT_WG(RBV, YV)                                                                                         \
   do {                                                                                                          \
     if (drop.p > 0.f)                                                                                           \
-      lora_wgrad_kernel<RBV, YV, true><<<grid, 1024, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop);  \
+      lora_wgrad_kernel<RBV, YV, true><<<grid, 1024, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop, so);  \
     else                                                                                                        \
-      lora_wgrad_kernel<RBV, YV, false><<<grid, 1024, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop); \
+      lora_wgrad_kernel<RBV, YV, false><<<grid, 1024, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop, so); \
   } while (0)
   switch (rb) {
     case 1: MFT_WG(1, false); break;

@@ -733,11 +733,18 @@ class _LoRALinearAug(Function):
         x2 = xa2[:, :K]
         ctr = dropout_counter(xa.device)
         off = K
+        # several adapters on one input without dropout (q|k|v, gate|up): ONE pass over x for all
+        # u_i (the u columns of consecutive slices are adjacent in xa)
+        batched = len(slices) > 1 and all(dp == 0 for (_, _, dp, _) in slices)
+        if batched:
+            acat = torch.cat([cw(ab[2 * i]) for i in range(len(slices))])
+            C.lora_rowdot(x2, acat, xa2[:, K:K + acat.shape[0]], 1.0, 0.0, 0, None)
         for i, (c0, n, dp, salt) in enumerate(slices):
             Ac, Bc = cw(ab[2 * i]), cw(ab[2 * i + 1])
             R = Ac.shape[0]
-            C.lora_rowdot(x2, Ac, xa2[:, off:off + R], 1.0, dp, salt, ctr)  # u_i -> appended columns
-            torch.mul(Bc.t(), s, out=waug[c0:c0 + n, off:off + R])          # s B_i^T -> W' rows of slice i
+            if not batched:
+                C.lora_rowdot(x2, Ac, xa2[:, off:off + R], 1.0, dp, salt, ctr)  # u_i -> appended columns
+            torch.mul(Bc.t(), s, out=waug[c0:c0 + n, off:off + R])              # s B_i^T -> W' rows of slice i
             off += R
         bc = cw(b)
         y = gemm_linear(xa2, waug, bc)
@@ -786,6 +793,14 @@ class _LoRALinearAug(Function):
         ctr = dropout_counter(dy.device)
         off = K
         first = True
+        # dA of every rank-8 adapter in ONE pass over x (segmented lora_wgrad) when all of them have
+        # grad buffers and no dropout
+        da_done = False
+        if fused and len(ctx.slices) > 1 and all(r == 8 for r in ranks) and len(ranks) <= 8:
+            bufs = [_grad_buf(ab[2 * i]) for i in range(len(ranks))]
+            if all(b is not None for b in bufs) and all(dp == 0 for (_, _, dp, _) in ctx.slices):
+                C.lora_wgrad_multi(x2, vall, bufs, 1.0)
+                da_done = True
         for i, (c0, n, dp, salt) in enumerate(ctx.slices):
             A, B = ab[2 * i], ab[2 * i + 1]
             Ac, Bc = cw(A), cw(B)
@@ -801,7 +816,9 @@ class _LoRALinearAug(Function):
                 C.lora_update(dx if first else dxa[:, :K], v, Ac, dxa[:, :K], 1.0, dp, salt, ctr)
                 first = False
             gA = gB = None
-            if _needs(A):
+            if da_done:
+                grad_ready(A)
+            elif _needs(A):
                 buf = _grad_buf(A)
                 tgt = buf if buf is not None else torch.zeros(R, K, device=dy.device)
                 C.lora_wgrad(x2, v, tgt, 1, K, 1.0, dp, salt, ctr)
