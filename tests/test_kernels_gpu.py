@@ -336,7 +336,7 @@ def test_flash_attention_packed_and_kvlens():
     assert torch.equal(ow[..., :H * D], o.reshape(B, S, H * D)) and (ow[..., H * D:] == 0).all()
 
 
-@pytest.mark.parametrize("V,C", [(50257, 768), (1000, 128)])
+@pytest.mark.parametrize("V,C", [(50257, 768), (1000, 128), (70001, 64), (262144, 64)])
 def test_lm_head_ce(V, C):
     from mobilefinetuner_amd.ops import functional as Fx
     M = 300
