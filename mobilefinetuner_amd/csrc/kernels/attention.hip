@@ -660,6 +660,162 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
 // ============================================================================================
 constexpr int kSplitBK = 32;  // rows per staged tile
 
+// Two 32-row tiles (rows >= nvalid zero-filled) held in registers between the global load and the
+// LDS store, so the NEXT tile's loads are in flight while the current one is multiplied
+// (double-buffered LDS, one barrier per step).  LDS rows are padded to D + 8 elements.
+template <int D, int NT>
+struct Tile2 {
+  static constexpr int CPR = D / 8, LD = D + 8, PER = (kSplitBK * CPR + NT - 1) / NT;
+  u16x8_t r0[PER], r1[PER];
+  __device__ __forceinline__ void load(const bf16_t* src0, const bf16_t* src1, AttnStrides s0, AttnStrides s1, int b,
+                                       int h, int row0, int nvalid) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = threadIdx.x + j * NT, r = c / CPR, ch = c % CPR;
+      const bool ok = c < kSplitBK * CPR && r < nvalid;
+      r0[j] = ok ? *reinterpret_cast<const u16x8_t*>(src0 + b * s0.sb + (long)(row0 + r) * s0.ss + h * s0.sh + ch * 8)
+                 : u16x8_t{};
+      r1[j] = ok ? *reinterpret_cast<const u16x8_t*>(src1 + b * s1.sb + (long)(row0 + r) * s1.ss + h * s1.sh + ch * 8)
+                 : u16x8_t{};
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* lds0, bf16_t* lds1) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = threadIdx.x + j * NT, r = c / CPR, ch = c % CPR;
+      if (c < kSplitBK * CPR) {
+        *reinterpret_cast<u16x8_t*>(lds0 + r * LD + ch * 8) = r0[j];
+        *reinterpret_cast<u16x8_t*>(lds1 + r * LD + ch * 8) = r1[j];
+      }
+    }
+  }
+};
+
+// XCD-aware task order for the split kernels: the dispatcher deals workgroups round-robin over the
+// 8 XCDs (each with its own L2); renumbered, the consecutive tasks of one batch row (the q-blocks /
+// key blocks and heads that re-read the same K/V or Q/dO rows) run on ONE XCD and share its L2.
+__device__ __forceinline__ void split_task(int& x, int& y, int& z) {
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int n = nx * ny * gridDim.z;
+  const int t = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), n);
+  x = t % nx;
+  y = (t / nx) % ny;
+  z = t / (nx * ny);
+}
+
+// dynamic LDS of the split kernels: two {tile0, tile1} buffers (+ per-row floats), or the per-wave
+// output staging of the epilogue, whichever is larger
+template <int D, int NW>
+constexpr size_t split_shm(int row_floats) {
+  return std::max(sizeof(bf16_t) * 4 * kSplitBK * (D + 8) + sizeof(float) * 2 * row_floats * kSplitBK,
+                  sizeof(bf16_t) * NW * 16 * (D + 8));
+}
+
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+    float* __restrict__ lse, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides os, int H, int Hkv, int Sq,
+    int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
+  constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + 8;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // buffer j: K at smem + 2 j BK LD, V after it
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  int tx, h, b;
+  split_task(tx, h, b);
+  const int q0 = tx * BQ, hk = h / (H / Hkv);
+  const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
+  const int coff = Sk - Sq;
+  const float c2 = scale * kLog2e;
+  const int wq_lo = q0 + 16 * w, wq_hi = wq_lo + 15;
+  const int qi = wq_lo + c16;  // this lane's query (C column)
+  int kend = kv_len;
+  if (causal) kend = min(kend, q0 + BQ + coff);
+  int kstart = 0;
+  if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
+  Tile2<D, NT> tl;
+  if (kstart < kend) tl.load(k, v, ks, vs, b, hk, kstart, min(BK, kv_len - kstart));
+  bf16x8_t qf[D / 32];  // B operand of S^T = K Q^T: Q[qi][32 s + 8 g + j]
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s)
+    qf[s] = qi < Sq ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qi * qs.ss + h * qs.sh + s * 32 + 8 * g)
+                    : bf16x8_t{};
+  if (kstart < kend) tl.store(smem, smem + BK * LD);
+  f32x4_t acc[D / 16];
+#pragma unroll
+  for (int n = 0; n < D / 16; ++n) acc[n] = zero4();
+  float m = -INFINITY, l = 0.f;  // running stats of query qi (identical in the 4 lane groups)
+  for (int kb = kstart, j = 0; kb < kend; kb += BK, ++j) {
+    const bool more = kb + BK < kend;
+    if (more) tl.load(k, v, ks, vs, b, hk, kb + BK, min(BK, kv_len - kb - BK));
+    __syncthreads();
+    const bf16_t* Ks = smem + (j & 1) * 2 * BK * LD;
+    const bf16_t* Vs = Ks + BK * LD;
+    const bool live = wq_lo < Sq && (!causal || kb <= wq_hi + coff) &&
+                      (window <= 0 || wq_lo + coff - (kb + BK - 1) < window);
+    if (live) {           // wave-uniform
+      f32x4_t st[2];      // st[t][i] = S[key kb + 16 t + 4 g + i][qi]
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        st[t] = zero4();
+#pragma unroll
+        for (int s = 0; s < D / 32; ++s) st[t] = mfma16(frag_row(Ks, LD, 16 * t, s * 32), qf[s], st[t]);
+      }
+      const bool need_mask = kb + BK > kv_len || (causal && kb + BK - 1 > wq_lo + coff) ||
+                             (window > 0 && wq_hi + coff - kb >= window) || wq_hi >= Sq;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float sv = st[t][i] * c2;
+          if (need_mask && !(qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window)))
+            sv = -INFINITY;
+          st[t][i] = sv;
+          mx = fmaxf(mx, sv);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float msafe = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = exp2f(m - msafe);
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(st[t][i] - msafe);
+          st[t][i] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mnew;
+      // acc rows are queries 4 g + i: their alpha lives in lane 4 g + i (C column = that query)
+      float ar[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ar[i] = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+      for (int n = 0; n < D / 16; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[n][i] *= ar[i];
+      const bf16x8_t pa = pack_c2a(st[0], st[1]);
+#pragma unroll
+      for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr_perm(Vs, LD, 0, n * 16), acc[n]);
+    }
+    if (more) {  // the other buffer was last read in step j - 1: every wave passed this step's barrier
+      bf16_t* nb = smem + ((j + 1) & 1) * 2 * BK * LD;
+      tl.store(nb, nb + BK * LD);
+    }
+  }
+  const float inv_own = l > 0.f ? 1.f / l : 0.f;
+  if (g == 0 && qi < Sq) lse[((long)b * H + h) * Sq + qi] = l > 0.f ? (m + log2f(l)) / kLog2e : 1e30f;
+  float inv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) inv[i] = __shfl(inv_own, 4 * g + i, 64);
+  __syncthreads();  // K/V tiles dead: reuse LDS as per-wave output staging
+  if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * LD, LD, acc, inv, o, os, b, h, wq_lo, min(16, Sq - wq_lo));
+}
+
 // two 32-row tiles (rows >= nvalid zero-filled) -> lds0/lds1 [32][D + 8]; all loads issue first
 template <int D, int NT>
 __device__ __forceinline__ void stage32x2(bf16_t* lds0, bf16_t* lds1, const bf16_t* src0, const bf16_t* src1,
@@ -686,101 +842,6 @@ __device__ __forceinline__ void stage32x2(bf16_t* lds0, bf16_t* lds1, const bf16
 }
 
 template <int D, int NW>
-__global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
-    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
-    float* __restrict__ lse, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides os, int H, int Hkv, int Sq,
-    int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
-  constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + 8;
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  bf16_t* Ks = smem;        // [BK][LD]
-  bf16_t* Vs = Ks + BK * LD;  // [BK][LD]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * BQ, hk = h / (H / Hkv);
-  const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
-  const int coff = Sk - Sq;
-  const float c2 = scale * kLog2e;
-  const int wq_lo = q0 + 16 * w, wq_hi = wq_lo + 15;
-  const int qi = wq_lo + c16;  // this lane's query (C column)
-  bf16x8_t qf[D / 32];         // B operand of S^T = K Q^T: Q[qi][32 s + 8 g + j]
-#pragma unroll
-  for (int s = 0; s < D / 32; ++s)
-    qf[s] = qi < Sq ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qi * qs.ss + h * qs.sh + s * 32 + 8 * g)
-                    : bf16x8_t{};
-  f32x4_t acc[D / 16];
-#pragma unroll
-  for (int n = 0; n < D / 16; ++n) acc[n] = zero4();
-  float m = -INFINITY, l = 0.f;  // running stats of query qi (identical in the 4 lane groups)
-  int kend = kv_len;
-  if (causal) kend = min(kend, q0 + BQ + coff);
-  int kstart = 0;
-  if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
-  for (int kb = kstart; kb < kend; kb += BK) {
-    __syncthreads();
-    stage32x2<D, NT>(Ks, Vs, k, v, ks, vs, b, hk, kb, min(BK, kv_len - kb));
-    __syncthreads();
-    const bool live = wq_lo < Sq && (!causal || kb <= wq_hi + coff) &&
-                      (window <= 0 || wq_lo + coff - (kb + BK - 1) < window);
-    if (!live) continue;  // wave-uniform; the next barrier is at the loop head
-    f32x4_t st[2];        // st[t][i] = S[key kb + 16 t + 4 g + i][qi]
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      st[t] = zero4();
-#pragma unroll
-      for (int s = 0; s < D / 32; ++s) st[t] = mfma16(frag_row(Ks, LD, 16 * t, s * 32), qf[s], st[t]);
-    }
-    const bool need_mask = kb + BK > kv_len || (causal && kb + BK - 1 > wq_lo + coff) ||
-                           (window > 0 && wq_hi + coff - kb >= window) || wq_hi >= Sq;
-    float mx = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float sv = st[t][i] * c2;
-        if (need_mask && !(qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window)))
-          sv = -INFINITY;
-        st[t][i] = sv;
-        mx = fmaxf(mx, sv);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx);
-    const float msafe = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = exp2f(m - msafe);
-    float rs = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(st[t][i] - msafe);
-        st[t][i] = p;
-        rs += p;
-      }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mnew;
-    // acc rows are queries 4 g + i: their alpha lives in lane 4 g + i (C column = that query)
-    float ar[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ar[i] = __shfl(alpha, 4 * g + i, 64);
-#pragma unroll
-    for (int n = 0; n < D / 16; ++n)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[n][i] *= ar[i];
-    const bf16x8_t pa = pack_c2a(st[0], st[1]);
-#pragma unroll
-    for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr_perm(Vs, LD, 0, n * 16), acc[n]);
-  }
-  const float inv_own = l > 0.f ? 1.f / l : 0.f;
-  if (g == 0 && qi < Sq) lse[((long)b * H + h) * Sq + qi] = l > 0.f ? (m + log2f(l)) / kLog2e : 1e30f;
-  float inv[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) inv[i] = __shfl(inv_own, 4 * g + i, 64);
-  __syncthreads();  // K/V tiles dead: reuse LDS as per-wave output staging
-  if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * LD, LD, acc, inv, o, os, b, h, wq_lo, min(16, Sq - wq_lo));
-}
-
-template <int D, int NW>
 __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
@@ -794,7 +855,9 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
   float* ls = reinterpret_cast<float*>(dOs + BQ * LD);  // [BQ] lse * log2 e
   float* dl = ls + BQ;                                  // [BQ] delta
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
-  const int b = blockIdx.z, hk = blockIdx.y, kb = blockIdx.x * BKEY, G = H / Hkv;
+  int tx, hk, b;
+  split_task(tx, hk, b);
+  const int kb = tx * BKEY, G = H / Hkv;
   const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
   const int coff = Sk - Sq;
   const float c2 = scale * kLog2e;
@@ -875,16 +938,22 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
     bf16_t* __restrict__ dq, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides dos, AttnStrides dqs, int H,
     int Hkv, int Sq, int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
   constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + 8;
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  bf16_t* Ks = smem;          // [BK][LD]
-  bf16_t* Vs = Ks + BK * LD;  // [BK][LD]
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // buffer j: K, V tiles at smem + 2 j BK LD
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * BQ, hk = h / (H / Hkv);
+  int tx, h, b;
+  split_task(tx, h, b);
+  const int q0 = tx * BQ, hk = h / (H / Hkv);
   const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
   const int coff = Sk - Sq;
   const float c2 = scale * kLog2e;
   const int wq_lo = q0 + 16 * w, wq_hi = wq_lo + 15;
   const int qi = wq_lo + c16;
+  int kend = kv_len;
+  if (causal) kend = min(kend, q0 + BQ + coff);
+  int kstart = 0;
+  if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
+  Tile2<D, NT> tl;
+  if (kstart < kend) tl.load(k, v, ks, vs, b, hk, kstart, min(BK, kv_len - kstart));
   bf16x8_t qf[D / 32], df[D / 32];  // B operands: Q[qi][32 s + 8 g + j], dO[qi][...]
 #pragma unroll
   for (int s = 0; s < D / 32; ++s) {
@@ -896,40 +965,44 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
   }
   const float lq = qi < Sq ? lse[((long)b * H + h) * Sq + qi] * kLog2e : 1e30f;
   const float dlq = qi < Sq ? delta[((long)b * H + h) * Sq + qi] : 0.f;
+  if (kstart < kend) tl.store(smem, smem + BK * LD);
   f32x4_t dQa[D / 16];
 #pragma unroll
   for (int n = 0; n < D / 16; ++n) dQa[n] = zero4();
-  int kend = kv_len;
-  if (causal) kend = min(kend, q0 + BQ + coff);
-  int kstart = 0;
-  if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
-  for (int kb = kstart; kb < kend; kb += BK) {
+  for (int kb = kstart, j = 0; kb < kend; kb += BK, ++j) {
+    const bool more = kb + BK < kend;
+    if (more) tl.load(k, v, ks, vs, b, hk, kb + BK, min(BK, kv_len - kb - BK));
     __syncthreads();
-    stage32x2<D, NT>(Ks, Vs, k, v, ks, vs, b, hk, kb, min(BK, kv_len - kb));
-    __syncthreads();
+    const bf16_t* Ks = smem + (j & 1) * 2 * BK * LD;
+    const bf16_t* Vs = Ks + BK * LD;
     const bool live = wq_lo < Sq && (!causal || kb <= wq_hi + coff) &&
                       (window <= 0 || wq_lo + coff - (kb + BK - 1) < window);
-    if (!live) continue;
-    f32x4_t st[2], dpt[2];  // [t][i] = S^T / dP^T [key kb + 16 t + 4 g + i][qi]
+    if (live) {
+      f32x4_t st[2], dpt[2];  // [t][i] = S^T / dP^T [key kb + 16 t + 4 g + i][qi]
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      st[t] = zero4();
-      dpt[t] = zero4();
+      for (int t = 0; t < 2; ++t) {
+        st[t] = zero4();
+        dpt[t] = zero4();
 #pragma unroll
-      for (int s = 0; s < D / 32; ++s) {
-        st[t] = mfma16(frag_row(Ks, LD, 16 * t, s * 32), qf[s], st[t]);
-        dpt[t] = mfma16(frag_row(Vs, LD, 16 * t, s * 32), df[s], dpt[t]);
+        for (int s = 0; s < D / 32; ++s) {
+          st[t] = mfma16(frag_row(Ks, LD, 16 * t, s * 32), qf[s], st[t]);
+          dpt[t] = mfma16(frag_row(Vs, LD, 16 * t, s * 32), df[s], dpt[t]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window);
+          const float p = ok ? exp2f(st[t][i] * c2 - lq) : 0.f;
+          dpt[t][i] = p * (dpt[t][i] - dlq) * scale;
+        }
       }
+      const bf16x8_t da = pack_c2a(dpt[0], dpt[1]);  // A: m = query, k = key (permuted)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool ok = qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window);
-        const float p = ok ? exp2f(st[t][i] * c2 - lq) : 0.f;
-        dpt[t][i] = p * (dpt[t][i] - dlq) * scale;
-      }
+      for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(da, frag_tr_perm(Ks, LD, 0, n * 16), dQa[n]);
     }
-    const bf16x8_t da = pack_c2a(dpt[0], dpt[1]);  // A: m = query, k = key (permuted)
-#pragma unroll
-    for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(da, frag_tr_perm(Ks, LD, 0, n * 16), dQa[n]);
+    if (more) {
+      bf16_t* nb = smem + ((j + 1) & 1) * 2 * BK * LD;
+      tl.store(nb, nb + BK * LD);
+    }
   }
   __syncthreads();
   const float one[4] = {1.f, 1.f, 1.f, 1.f};
@@ -963,8 +1036,7 @@ static int split_nw(const char* name, int dflt) {
 
 template <int D, int NW>
 static void fwd_split_launch(const AttnArgs& a, hipStream_t stream) {
-  constexpr int LD = D + 8;
-  const size_t shm = sizeof(bf16_t) * std::max(2 * kSplitBK * LD, NW * 16 * LD);
+  const size_t shm = split_shm<D, NW>(0);
   static bool attr = false;
   if (!attr) {
     MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_split_kernel<D, NW>,
@@ -994,8 +1066,7 @@ static void dkdv_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
 
 template <int D, int NW>
 static void dq_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
-  constexpr int LD = D + 8;
-  const size_t shm = sizeof(bf16_t) * std::max(2 * kSplitBK * LD, NW * 16 * LD);
+  const size_t shm = split_shm<D, NW>(0);
   static bool attr = false;
   if (!attr) {
     MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, NW>,
