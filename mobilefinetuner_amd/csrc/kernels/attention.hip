@@ -648,7 +648,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
 // Split path (every shape the short path does not take; Gemma-3: D = 256, GQA 4:1, S = 256..):
 // scores are computed TRANSPOSED as in the short path, so P / dS become the A operand of the next
 // MFMA straight from registers (pack_c2a + frag_tr_perm) -- no LDS round trip, no scalar LDS
-// writes.  32-row K/V (or Q/dO) tiles are staged through LDS with rows padded to D + 8 elements
+// writes.  32-row K/V (or Q/dO) tiles are staged through LDS with rows padded to D + kSplitPad elements
 // (conflict-free ds_read_b128 row fragments).
 //   * forward: a workgroup owns 16*NW queries of one head (each wave 16, Q in registers as the B
 //     operand of S^T = K Q^T); online softmax stats are per C column, reduced over the 4 lane groups.
@@ -659,13 +659,20 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
 //     written once in bf16 (no fp32 atomics, workspace memset or conversion pass).
 // ============================================================================================
 constexpr int kSplitBK = 32;  // rows per staged tile
+// LDS row pitch D + 16 elements (row stride = 8 banks mod 64): conflict-free for BOTH operand reads
+// of these kernels -- ds_read_b128 row fragments (16-lane groups {0-3,12-15,20-27}, ...) and the
+// ds_read_b64_tr_b16 pairs of frag_tr_perm (32-lane groups) -- where a D + 8 pitch left ~2 extra
+// LDS cycles per instruction (SQ_LDS_BANK_CONFLICT, profiles/r1_attn_split_pmc.txt).  Measured at
+// the Gemma-3 shape: conflict cycles -90 %, kernel time only -2..5 % -- the waves spend ~65 % of
+// their cycles in SQ_WAIT_ANY (tile staging latency), not in LDS.
+constexpr int kSplitPad = 16;
 
 // Two 32-row tiles (rows >= nvalid zero-filled) held in registers between the global load and the
 // LDS store, so the NEXT tile's loads are in flight while the current one is multiplied
-// (double-buffered LDS, one barrier per step).  LDS rows are padded to D + 8 elements.
+// (double-buffered LDS, one barrier per step).  LDS rows are padded to D + kSplitPad elements.
 template <int D, int NT>
 struct Tile2 {
-  static constexpr int CPR = D / 8, LD = D + 8, PER = (kSplitBK * CPR + NT - 1) / NT;
+  static constexpr int CPR = D / 8, LD = D + kSplitPad, PER = (kSplitBK * CPR + NT - 1) / NT;
   u16x8_t r0[PER], r1[PER];
   __device__ __forceinline__ void load(const bf16_t* src0, const bf16_t* src1, AttnStrides s0, AttnStrides s1, int b,
                                        int h, int row0, int nvalid) {
@@ -707,8 +714,8 @@ __device__ __forceinline__ void split_task(int& x, int& y, int& z) {
 // output staging of the epilogue, whichever is larger
 template <int D, int NW>
 constexpr size_t split_shm(int row_floats) {
-  return std::max(sizeof(bf16_t) * 4 * kSplitBK * (D + 8) + sizeof(float) * 2 * row_floats * kSplitBK,
-                  sizeof(bf16_t) * NW * 16 * (D + 8));
+  return std::max(sizeof(bf16_t) * 4 * kSplitBK * (D + kSplitPad) + sizeof(float) * 2 * row_floats * kSplitBK,
+                  sizeof(bf16_t) * NW * 16 * (D + kSplitPad));
 }
 
 template <int D, int NW>
@@ -716,7 +723,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
     float* __restrict__ lse, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides os, int H, int Hkv, int Sq,
     int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
-  constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + 8;
+  constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + kSplitPad;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // buffer j: K at smem + 2 j BK LD, V after it
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
   int tx, h, b;
@@ -816,11 +823,11 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
   if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * LD, LD, acc, inv, o, os, b, h, wq_lo, min(16, Sq - wq_lo));
 }
 
-// two 32-row tiles (rows >= nvalid zero-filled) -> lds0/lds1 [32][D + 8]; all loads issue first
+// two 32-row tiles (rows >= nvalid zero-filled) -> lds0/lds1 [32][D + kSplitPad]; all loads issue first
 template <int D, int NT>
 __device__ __forceinline__ void stage32x2(bf16_t* lds0, bf16_t* lds1, const bf16_t* src0, const bf16_t* src1,
                                           AttnStrides s0, AttnStrides s1, int b, int h, int row0, int nvalid) {
-  constexpr int CPR = D / 8, LD = D + 8, PER = (kSplitBK * CPR + NT - 1) / NT;
+  constexpr int CPR = D / 8, LD = D + kSplitPad, PER = (kSplitBK * CPR + NT - 1) / NT;
   u16x8_t r0[PER], r1[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -848,7 +855,7 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
     bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides dos,
     AttnStrides dks, AttnStrides dvs, int H, int Hkv, int Sq, int Sk, float scale, int causal, int window,
     const int* __restrict__ kv_lens) {
-  constexpr int NT = 64 * NW, BKEY = 16 * NW, BQ = kSplitBK, LD = D + 8;
+  constexpr int NT = 64 * NW, BKEY = 16 * NW, BQ = kSplitBK, LD = D + kSplitPad;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   bf16_t* Qs = smem;            // [BQ][LD]
   bf16_t* dOs = Qs + BQ * LD;   // [BQ][LD]
@@ -937,7 +944,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dq, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides dos, AttnStrides dqs, int H,
     int Hkv, int Sq, int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
-  constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + 8;
+  constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + kSplitPad;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // buffer j: K, V tiles at smem + 2 j BK LD
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
   int tx, h, b;
@@ -1050,7 +1057,7 @@ static void fwd_split_launch(const AttnArgs& a, hipStream_t stream) {
 
 template <int D, int NW>
 static void dkdv_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
-  constexpr int LD = D + 8;
+  constexpr int LD = D + kSplitPad;
   const size_t shm = std::max(sizeof(bf16_t) * 2 * kSplitBK * LD + sizeof(float) * 2 * kSplitBK,
                               sizeof(bf16_t) * NW * 16 * LD);
   static bool attr = false;
