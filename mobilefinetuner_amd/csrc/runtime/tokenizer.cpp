@@ -1,5 +1,7 @@
 #include "tokenizer.h"
 
+#include <atomic>
+
 #include <algorithm>
 #include <cstring>
 #include <fstream>
@@ -272,10 +274,17 @@ std::vector<std::string> ByteLevelBPE::pretokenize(const std::string& text) cons
   return out;
 }
 
+uint64_t ByteLevelBPE::next_uid() {
+  static std::atomic<uint64_t> n{1};
+  return n.fetch_add(1, std::memory_order_relaxed);
+}
+
 void ByteLevelBPE::encode_word(const std::string& w, std::vector<int>& out) const {
-  // per-thread word cache (the dataset tokenises WikiText lines on several threads)
-  static thread_local std::unordered_map<const void*, std::unordered_map<std::string, std::vector<int>>> tl;
-  auto& cache_ = tl[this];
+  // per-thread word cache (the dataset tokenises WikiText lines on several threads), keyed by the
+  // tokenizer's serial; caches of tokenizers that no longer exist are dropped wholesale
+  static thread_local std::unordered_map<uint64_t, std::unordered_map<std::string, std::vector<int>>> tl;
+  if (tl.size() > 8 && !tl.count(uid_)) tl.clear();
+  auto& cache_ = tl[uid_];
   auto it = cache_.find(w);
   if (it != cache_.end()) {
     out.insert(out.end(), it->second.begin(), it->second.end());

@@ -54,6 +54,10 @@ class ByteLevelBPE : public BPECore {
   std::string byte_to_uni_[256];
   std::unordered_map<uint32_t, uint8_t> uni_to_byte_;
   void encode_word(const std::string& w, std::vector<int>& out) const;
+  // identity of this vocabulary for the per-thread word cache: a process-unique serial, NOT the
+  // object address (a new tokenizer allocated where a destroyed one lived must not see its cache)
+  uint64_t uid_ = next_uid();
+  static uint64_t next_uid();
 };
 
 class SentencePieceBPE : public BPECore {

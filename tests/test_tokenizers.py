@@ -104,3 +104,31 @@ def test_sentencepiece_bpe_matches_hf(sp_file):
         assert got == exp, (s, got, exp)
         assert ours.decode(got) == hf.decode(exp)
     assert ours.encode("hi", add_bos=True)[0] == ours.bos_id
+
+
+def test_gpt2_word_cache_not_shared_by_recycled_tokenizers(tmp_path):
+    """The native BPE keeps a per-thread word cache; a tokenizer created after another one was freed
+    (often at the same address) must not see the old vocabulary's cached words."""
+    import gc
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+    from mobilefinetuner_amd.tokenizers import GPT2Tokenizer
+    texts = ["first line of text .", "second line , with more words .", "= Title ="]
+    hfs = []
+    for i, (size, corpus) in enumerate(((300, texts), (400, CORPUS[:14]), (280, texts[::-1] * 3))):
+        tok = Tokenizer(models.BPE())
+        tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+        tok.decoder = decoders.ByteLevel()
+        tr = trainers.BpeTrainer(vocab_size=size, special_tokens=["<|endoftext|>"],
+                                 initial_alphabet=pre_tokenizers.ByteLevel.alphabet(), show_progress=False)
+        tok.train_from_iterator(corpus, tr)
+        d = tmp_path / f"t{i}"
+        d.mkdir()
+        tok.model.save(str(d))
+        hfs.append((d, tok))
+    for rep in range(12):
+        d, hf = hfs[rep % len(hfs)]
+        ours = GPT2Tokenizer.from_files(str(d / "vocab.json"), str(d / "merges.txt"))
+        for s in texts + ["with more words", "line of text"]:
+            assert ours.encode(s) == hf.encode(s).ids, (rep, s)
+        del ours
+        gc.collect()
