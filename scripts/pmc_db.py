@@ -7,7 +7,7 @@ from collections import defaultdict
 
 db = sys.argv[1]
 flts = sys.argv[2:]
-c = sqlite3.connect(db)
+c = sqlite3.connect(f"file:{db}?mode=ro", uri=True)  # never creates a file
 rows = c.execute("select dispatch_id, kernel_name, counter_name, value, duration, lds_block_size, vgpr_count, "
                  "accum_vgpr_count, scratch_size from counters_collection")
 per = defaultdict(lambda: defaultdict(float))

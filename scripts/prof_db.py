@@ -10,7 +10,7 @@ import sys
 
 
 def rows(db):
-    c = sqlite3.connect(db)
+    c = sqlite3.connect(f"file:{db}?mode=ro", uri=True)  # never creates a file
     q = ("select name, start, end, grid_x*grid_y*grid_z, workgroup_x*workgroup_y*workgroup_z, "
          "lds_size, vgpr_count, accum_vgpr_count from kernels order by start")
     return list(c.execute(q))
@@ -42,6 +42,9 @@ def step(db, marker="adamw_kernel", which=-2):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) < 2 or sys.argv[1].startswith("-"):
+        print(__doc__)
+        sys.exit(0)
     db, mode = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "stats"
     if mode == "stats":
         stats(db, float(sys.argv[3]) if len(sys.argv) > 3 else 1.0, int(sys.argv[4]) if len(sys.argv) > 4 else 40)
