@@ -393,9 +393,10 @@ void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t
   }
   if (M <= 0 || N <= 0) return;
   const int gx = cdiv(N, 256);
-  // 2 resident blocks per CU (68 KB LDS each): ~512 blocks in total, >= 4 tiles per wave
+  // 2 resident blocks per CU (68 KB LDS each): ~512 blocks in total, >= 2 tiles per wave (a 256-column
+  // slice such as Gemma's k / v projections then still fills every CU: 256 row chunks at M = 64k)
   long ny = cdiv(512, gx);
-  const long max_ny = cdiv(M, 512);
+  const long max_ny = cdiv(M, 256);
   if (ny > max_ny) ny = max_ny;
   if (ny < 1) ny = 1;
   long chunk = cdiv(M, ny);

@@ -113,6 +113,10 @@ class DataParallel:
             self._works.append(w)
 
     def _on_ready(self, p):
+        # inside a hipGraph capture (TrainStep use_graph) no collective may be enqueued: the bucket
+        # stays pending and finish() reduces every bucket after the replay
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return
         bi = self.param_bucket.get(id(p))
         if bi is None:
             return
