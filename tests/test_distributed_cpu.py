@@ -210,3 +210,25 @@ def test_zero_syncs_fp32_compute_params():
         p.join(60)
     assert not torch.equal(out[0], torch.ones_like(out[0]))  # updated
     assert torch.equal(out[0], out[1])
+
+
+def test_ddp_hook_defers_inside_graph_capture(monkeypatch):
+    """A bucket's grad-ready hook must not enqueue a collective while a hipGraph is being captured
+    (TrainStep use_graph): the bucket stays pending and finish() reduces it after the replay."""
+    sys.path.insert(0, ROOT)
+    from mobilefinetuner_amd.parallel.ddp import DataParallel
+    from mobilefinetuner_amd.utils.params import FlatParams
+    ps = [("a", torch.nn.Parameter(torch.randn(4000))), ("b", torch.nn.Parameter(torch.randn(3000)))]
+    flat = FlatParams(ps, "cpu", shadow=False)
+    dp = DataParallel(flat, bucket_mb=0.01)
+    dp.begin_step()
+    s = flat.slots[0]
+    bi = dp.param_bucket[id(s.param)]
+    before = list(dp._pending)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+    dp._on_ready(s.param)
+    assert dp._pending == before and not any(dp._launched)
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+    dp._on_ready(s.param)
+    assert dp._pending[bi] == before[bi] - 1
