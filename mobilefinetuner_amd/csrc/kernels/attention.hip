@@ -823,6 +823,178 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
   if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * LD, LD, acc, inv, o, os, b, h, wq_lo, min(16, Sq - wq_lo));
 }
 
+// ---- LDS-DMA ring variant of the split forward (D >= 128) -------------------------------------
+// The register-staged pipeline above prefetches one tile ahead, which the measured kernels show is
+// not enough (~65 % of wave cycles in SQ_WAIT_ANY, profiles/r1_attn_split_pmc.txt).  Here K/V tiles
+// go global -> LDS by global_load_lds_dwordx4 (no VGPRs) into a 3-deep ring: tile j+2 streams in
+// while tile j is multiplied.  LDS rows are unpadded (D elements) with the 16-B chunk index XORed
+// by 2 (row & 7) on the SOURCE side (the DMA writes lane-linear), which keeps both the ds_read_b128
+// row fragments and the ds_read_b64_tr_b16 pairs conflict-free (same bank algebra as the D + 16
+// pitch).  Waits are counted (vmcnt) and barriers raw, so the DMA queue is never drained mid-loop.
+constexpr int kRing = 3;
+
+__device__ __forceinline__ void dma16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row & 7) << 1); }
+
+// one 32-row tile, rows clamped into [0, rmax): LDS chunk c (lane-linear) <- global chunk swz(c)
+template <int D, int NW>
+__device__ __forceinline__ void dma_tile32(bf16_t* lds, const bf16_t* src, AttnStrides st, int b, int h, int row0,
+                                           int rmax) {
+  constexpr int CPR = D / 8, OPS = kSplitBK * CPR / 64;  // 1-KB DMA ops per tile
+  static_assert(OPS % NW == 0, "every wave issues the same number of DMA ops");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < OPS / NW; ++k) {
+    const int o = w + k * NW;
+    const int c = o * 64 + lane, r = c / CPR, pos = c % CPR;
+    const int gr = min(row0 + r, rmax - 1);
+    dma16(src + b * st.sb + (long)gr * st.ss + h * st.sh + swz_chunk(r, pos) * 8, lds + o * 512);
+  }
+}
+
+// lane holds T[r0 + (l&15)][c0 + 8 (l>>4) + j] of a swizzled [rows][D] image
+template <int D>
+__device__ __forceinline__ bf16x8_t frag_row_sw(const bf16_t* t, int r0, int c0) {
+  const int l = threadIdx.x & 63;
+  const int r = r0 + (l & 15), ch = (c0 >> 3) + (l >> 4);
+  return *reinterpret_cast<const bf16x8_t*>(t + r * D + (swz_chunk(r, ch) << 3));
+}
+// frag_tr_perm (mfma.h) on a swizzled image
+template <int D>
+__device__ __forceinline__ bf16x8_t frag_tr_perm_sw(const bf16_t* t, int r0, int c0) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const int ra = r0 + 4 * g + q, rb = ra + 16;
+  const int col = c0 + 4 * p, ch = col >> 3, off = col & 7;
+  s16x4_t lo = ds_tr16(t + ra * D + (swz_chunk(ra, ch) << 3) + off);
+  s16x4_t hi = ds_tr16(t + rb * D + (swz_chunk(rb, ch) << 3) + off);
+  s16x8_t rr = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, rr);
+}
+
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+    float* __restrict__ lse, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides os, int H, int Hkv, int Sq,
+    int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
+  constexpr int BQ = 16 * NW, BK = kSplitBK, TILE = BK * D, LDO = D + kSplitPad;
+  constexpr int OPW = 2 * (BK * D / 8 / 64) / NW;  // DMA ops per wave per ring stage (K + V)
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // ring stage s: K at smem + 2 s TILE, V after
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  int tx, h, b;
+  split_task(tx, h, b);
+  const int q0 = tx * BQ, hk = h / (H / Hkv);
+  const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
+  const int coff = Sk - Sq;
+  const float c2 = scale * kLog2e;
+  const int wq_lo = q0 + 16 * w, wq_hi = wq_lo + 15;
+  const int qi = wq_lo + c16;
+  int kend = kv_len;
+  if (causal) kend = min(kend, q0 + BQ + coff);
+  int kstart = 0;
+  if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
+  const int nt = kend > kstart ? (kend - kstart + BK - 1) / BK : 0;  // WG-uniform
+  bf16x8_t qf[D / 32];
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s)
+    qf[s] = qi < Sq ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qi * qs.ss + h * qs.sh + s * 32 + 8 * g)
+                    : bf16x8_t{};
+  auto issue = [&](int j) {  // ring stage j % 3 <- tile min(j, nt - 1) (tail re-reads keep counts uniform)
+    const int kb = kstart + min(j, nt - 1) * BK;
+    bf16_t* st = smem + (j % kRing) * 2 * TILE;
+    dma_tile32<D, NW>(st, k, ks, b, hk, kb, kv_len);
+    dma_tile32<D, NW>(st + TILE, v, vs, b, hk, kb, kv_len);
+  };
+  f32x4_t acc[D / 16];
+#pragma unroll
+  for (int n = 0; n < D / 16; ++n) acc[n] = zero4();
+  float m = -INFINITY, l = 0.f;
+  if (nt > 0) {
+    issue(0);
+    issue(1);
+  }
+  for (int j = 0; j < nt; ++j) {
+    vmcnt_wait<OPW>();  // this wave's ops for stage j are done (stage j + 1 may still fly)
+    lds_barrier();      // ... and every other wave's; stage (j + 2) % 3 was last read in step j - 1
+    issue(j + 2);
+    const int kb = kstart + j * BK;
+    const bf16_t* Ks = smem + (j % kRing) * 2 * TILE;
+    const bf16_t* Vs = Ks + TILE;
+    const bool live = wq_lo < Sq && (!causal || kb <= wq_hi + coff) &&
+                      (window <= 0 || wq_lo + coff - (kb + BK - 1) < window);
+    if (live) {
+      f32x4_t st[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        st[t] = zero4();
+#pragma unroll
+        for (int s = 0; s < D / 32; ++s) st[t] = mfma16(frag_row_sw<D>(Ks, 16 * t, s * 32), qf[s], st[t]);
+      }
+      const bool need_mask = kb + BK > kv_len || (causal && kb + BK - 1 > wq_lo + coff) ||
+                             (window > 0 && wq_hi + coff - kb >= window) || wq_hi >= Sq;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float sv = st[t][i] * c2;
+          if (need_mask && !(qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window)))
+            sv = -INFINITY;
+          st[t][i] = sv;
+          mx = fmaxf(mx, sv);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float msafe = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = exp2f(m - msafe);
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(st[t][i] - msafe);
+          st[t][i] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mnew;
+      float ar[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ar[i] = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+      for (int n = 0; n < D / 16; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[n][i] *= ar[i];
+      const bf16x8_t pa = pack_c2a(st[0], st[1]);
+#pragma unroll
+      for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr_perm_sw<D>(Vs, 0, n * 16), acc[n]);
+    }
+  }
+  vmcnt_wait<0>();  // the tail's re-read DMA must land before the LDS is reused / the WG exits
+  __syncthreads();
+  const float inv_own = l > 0.f ? 1.f / l : 0.f;
+  if (g == 0 && qi < Sq) lse[((long)b * H + h) * Sq + qi] = l > 0.f ? (m + log2f(l)) / kLog2e : 1e30f;
+  float inv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) inv[i] = __shfl(inv_own, 4 * g + i, 64);
+  if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * LDO, LDO, acc, inv, o, os, b, h, wq_lo, min(16, Sq - wq_lo));
+}
+
 // two 32-row tiles (rows >= nvalid zero-filled) -> lds0/lds1 [32][D + kSplitPad]; all loads issue first
 template <int D, int NT>
 __device__ __forceinline__ void stage32x2(bf16_t* lds0, bf16_t* lds1, const bf16_t* src0, const bf16_t* src1,
@@ -1055,6 +1227,21 @@ static void fwd_split_launch(const AttnArgs& a, hipStream_t stream) {
       a.causal, a.window, a.kv_lens);
 }
 
+template <int D>
+static void fwd_dma_launch(const AttnArgs& a, hipStream_t stream) {
+  constexpr int NW = 8;
+  const size_t shm = std::max(sizeof(bf16_t) * kRing * 2 * kSplitBK * D, sizeof(bf16_t) * NW * 16 * (D + kSplitPad));
+  static bool attr = false;
+  if (!attr) {
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_dma_kernel<D, NW>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  attn_fwd_dma_kernel<D, NW><<<dim3(cdiv(a.Sq, 16 * NW), a.H, a.B), 64 * NW, shm, stream>>>(
+      a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale,
+      a.causal, a.window, a.kv_lens);
+}
+
 template <int D, int NW>
 static void dkdv_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
   constexpr int LD = D + kSplitPad;
@@ -1104,6 +1291,13 @@ static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
     }
   }
   if (attn_bwd_path(D, a.Sq, a.Sk, a.window) == 2) {
+    if constexpr (D >= 128) {
+      static const int dma = env_int("MFT_ATTN_DMA", 1);
+      if (dma) {
+        fwd_dma_launch<D>(a, stream);
+        return;
+      }
+    }
     if (split_nw("MFT_ATTN_NW_FWD", 8) == 8) fwd_split_launch<D, 8>(a, stream);
     else fwd_split_launch<D, 4>(a, stream);
     return;
