@@ -884,6 +884,17 @@ __device__ __forceinline__ bf16x8_t frag_tr_perm_sw(const bf16_t* t, int r0, int
   return __builtin_bit_cast(bf16x8_t, rr);
 }
 
+// cross-row-group exchanges as VALU permlane swaps (no LDS round trip, unlike ds_bpermute shuffles):
+// value of lane l ^ 16 / l ^ 32
+__device__ __forceinline__ float xor16_pl(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(((threadIdx.x >> 4) & 1) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xor32_pl(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(((threadIdx.x >> 5) & 1) ? r[0] : r[1]);
+}
+
 template <int D, int NW>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
@@ -955,8 +966,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
           st[t][i] = sv;
           mx = fmaxf(mx, sv);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = fmaxf(mx, xor16_pl(mx));
+      mx = fmaxf(mx, xor32_pl(mx));
       const float mnew = fmaxf(m, mx);
       const float msafe = mnew == -INFINITY ? 0.f : mnew;
       const float alpha = exp2f(m - msafe);
@@ -969,17 +980,19 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
           st[t][i] = p;
           rs += p;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs += xor16_pl(rs);
+      rs += xor32_pl(rs);
       l = l * alpha + rs;
       m = mnew;
-      float ar[4];
+      if (__any(alpha != 1.f)) {  // wave-uniform: skip the rescale when no running max moved
+        float ar[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ar[i] = __shfl(alpha, 4 * g + i, 64);
+        for (int i = 0; i < 4; ++i) ar[i] = __shfl(alpha, 4 * g + i, 64);
 #pragma unroll
-      for (int n = 0; n < D / 16; ++n)
+        for (int n = 0; n < D / 16; ++n)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[n][i] *= ar[i];
+          for (int i = 0; i < 4; ++i) acc[n][i] *= ar[i];
+      }
       const bf16x8_t pa = pack_c2a(st[0], st[1]);
 #pragma unroll
       for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr_perm_sw<D>(Vs, 0, n * 16), acc[n]);
