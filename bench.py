@@ -182,8 +182,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     final_loss = float(loss.item())
+    from mobilefinetuner_amd.utils import trace
+    n_train = sum(p.numel() for p in model.parameters() if p.requires_grad)
+    fpt = trace.model_flops_per_token_cfg(model.cfg, a.seq, nparams, n_train)
     tokens = world * a.batch * a.seq * a.grad_accum * a.steps
     value = tokens / dt
+    tflops, mfu = trace.mfu(value / world, fpt)
     if rank == 0:
         out = {
             "metric": cfgd["metric"],
@@ -207,6 +211,8 @@ def main():
                 "parallelism": f"dp{world}",
                 "hipgraph": bool(getattr(step, "use_graph", False)),
                 "final_loss": round(final_loss, 4),
+                "model_tflops_per_gpu": round(tflops, 1),
+                "mfu_bf16_dense": round(mfu, 4),
                 "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC if a.config == "gpt2-lora" else None,
             },
         }

@@ -28,6 +28,7 @@ from ..optim.adamw import FusedAdamW
 from ..parallel.ddp import DataParallel, allreduce_sum_, is_dist
 from ..utils.logging import log0, rank0
 from ..utils.params import FlatParams
+from ..utils import trace
 from ..utils.trace import PhaseTimer, ProfileWindow, enable_tracing, trace_range
 from .engine import TrainStep
 
@@ -221,6 +222,17 @@ class Trainer:
         log0(f"[Resume] restored full training state from {path} at global step {self.global_step}")
 
     # ------------------------------------------------------------------ loop
+    def _mfu(self, tps_per_gpu: float, seq: int):
+        """Model TFLOP/s per GPU and MFU vs the MI355X bf16 dense peak (SURVEY §5.1 counters)."""
+        cfg = getattr(self.model, "cfg", None)
+        if cfg is None:
+            return 0.0, 0.0
+        if getattr(self, "_fpt", None) is None or self._fpt[0] != seq:
+            n_params = sum(p.numel() for p in self.model.parameters())
+            n_train = sum(p.numel() for p in self.model.parameters() if p.requires_grad)
+            self._fpt = (seq, trace.model_flops_per_token_cfg(cfg, seq, n_params, n_train))
+        return trace.mfu(tps_per_gpu, self._fpt[1])
+
     def train(self):
         c = self.cfg
         if self.total_steps <= 0:
@@ -276,6 +288,7 @@ class Trainer:
                 t_last, tok_last = now, self.total_tokens
                 ppl = math.exp(min(loss, 50.0))
                 mem = torch.cuda.max_memory_allocated(self.device) / 2 ** 30 if self.device.type == "cuda" else 0.0
+                tflops, mfu_frac = self._mfu(tps / self.world, batches[0][0].shape[1])
                 if c.log_style == "gemma":
                     log0(f"[Step {step + 1}] Loss={loss:.4f} PPL={ppl:.2f} LR={lr:.6g} "
                          f"grad_norm={gn_clip:.3f} tokens/s={tps:.0f}")
@@ -283,9 +296,10 @@ class Trainer:
                     log0(f"[Train] epoch {cur_epoch}/{c.epochs} | step {step_in_epoch}/{self.steps_per_epoch} "
                          f"(global {step + 1}/{self.total_steps}) | lr {lr:.6f} | loss {loss:.4f} | ppl {ppl:.2f} "
                          f"| grad_norm {gn_clip:.3f} | tokens {ntok_all} | tokens_per_sec {tps:.0f} "
-                         f"| hbm_peak_gb {mem:.2f} | step_ms {step_ms:.2f}" + (" | skipped_nonfinite" if skipped else ""))
+                         f"| hbm_peak_gb {mem:.2f} | step_ms {step_ms:.2f} | tflops {tflops:.1f} | mfu {mfu_frac:.3f}" + (" | skipped_nonfinite" if skipped else ""))
                 rec = {"step": step + 1, "epoch": cur_epoch, "loss": loss, "lr": lr, "grad_norm": gn,
-                       "tokens_per_sec": tps, "hbm_peak_gb": mem, "step_ms": step_ms, "skipped_total": self.skipped}
+                       "tokens_per_sec": tps, "hbm_peak_gb": mem, "step_ms": step_ms, "skipped_total": self.skipped,
+                       "tflops_per_gpu": tflops, "mfu": mfu_frac}
                 self.history.append(rec)
                 if c.metrics_out and rank0():
                     with open(c.metrics_out, "a") as f:

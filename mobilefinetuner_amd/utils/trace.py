@@ -104,3 +104,24 @@ def model_flops_per_token(n_params: int, n_trainable: int, n_layer: int, seq: in
     the attention score/value matmuls (causal: half of 4 * S * d per layer each direction)."""
     attn = n_layer * 2 * seq * d_model * 3  # fwd (QK^T, PV; causal half of 4Sd) + bwd (2x)
     return 4.0 * n_params + 2.0 * n_trainable + attn
+
+
+# CDNA4 dense bf16 matrix peak of one MI355X (no 2:1 sparsity), the MFU denominator
+MI355X_BF16_DENSE_TFLOPS = 2500.0
+
+
+def model_flops_per_token_cfg(cfg, seq: int, n_params: int, n_trainable: int) -> float:
+    """`model_flops_per_token` from a GPT2Config / Gemma3Config (attention width = heads x head_dim,
+    so Gemma-3's 4 x 256 query width is counted, not its 640 residual width)."""
+    n_layer = getattr(cfg, "n_layer", None) or cfg.num_hidden_layers
+    if hasattr(cfg, "n_embd"):
+        d_attn = cfg.n_embd
+    else:
+        d_attn = cfg.num_attention_heads * cfg.head_dim
+    return model_flops_per_token(n_params, n_trainable, n_layer, seq, d_attn)
+
+
+def mfu(tokens_per_sec_per_gpu: float, flops_per_token: float) -> tuple[float, float]:
+    """(achieved model TFLOP/s per GPU, fraction of the bf16 dense peak)."""
+    tf = tokens_per_sec_per_gpu * flops_per_token / 1e12
+    return tf, tf / MI355X_BF16_DENSE_TFLOPS

@@ -18,3 +18,25 @@ def test_runtime_selftest_asan_ubsan(tmp_path):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "sanitized runtime selftest OK" in r.stdout
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error:" not in r.stderr
+
+
+def test_energy_module_policy():
+    """`mobilefinetuner_amd.energy` facade over the native PowerMonitor (reference power_monitor.cpp:70-112)."""
+    from mobilefinetuner_amd import energy
+    c = energy.PowerConfig()
+    c.check_interval_steps = 1
+    m = energy.PowerMonitor(c)
+    m.set_manual_readings(100, 30)
+    cool = m.suggest_sleep_ms(1)
+    m.set_manual_readings(10, 50)  # low battery + hot -> slower target frequency -> longer sleep
+    assert m.suggest_sleep_ms(2) > cool
+
+
+def test_mfu_counters():
+    from mobilefinetuner_amd.models.gpt2 import GPT2Config
+    from mobilefinetuner_amd.utils import trace
+    fpt = trace.model_flops_per_token_cfg(GPT2Config.preset("gpt2"), 128, 124_439_808, 442_368)
+    # 4N + 2N_trainable + attention (12 layers x 2 x 128 x 768 x 3)
+    assert abs(fpt - (4 * 124_439_808 + 2 * 442_368 + 12 * 2 * 128 * 768 * 3)) < 1
+    tf, frac = trace.mfu(1e6, fpt)
+    assert abs(tf - fpt * 1e6 / 1e12) < 1e-9 and abs(frac - tf / 2500.0) < 1e-12
