@@ -8,7 +8,13 @@ training step: forward, fused LM-head cross-entropy, backward through all 12 blo
 all-reduce (N > 1), global grad-norm clip and the fused AdamW update.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config gpt2-lora|gemma3-270m-lora|gpt2-full|gpt2-xl-zero|gpt2-xl-zero3] [--zero S]
-                  [--batch B] [--seq S] [--no-graph]
+                  [--batch B] [--seq S] [--no-graph] [--cpu_smoke]
+
+``--gpus N`` with N > 1 and no ``WORLD_SIZE`` in the environment: this process becomes a launcher
+(``mobilefinetuner_amd.launch``) that starts N fresh rank processes (one per GPU, RCCL) and exits
+with their exit code; it never touches the GPU itself.  Under ``torch.distributed.run`` (WORLD_SIZE
+set) every process is one rank and ``--gpus`` must equal the world size.
+``--cpu_smoke``: gpt2-tiny on the CPU over gloo, for the GPU-less multi-rank test of this path.
 
 Prints ONE JSON line on rank 0.
 """
@@ -72,7 +78,8 @@ def build(a, cfgd, dev, world):
     else:
         from mobilefinetuner_amd.models.gpt2 import GPT2Config, GPT2Model
         mcfg = GPT2Config.preset(name)
-        model = GPT2Model(mcfg, dtype=torch.bfloat16, device=dev, seed=1234)  # identical on every rank
+        model = GPT2Model(mcfg, dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32, device=dev,
+                          seed=1234)  # identical on every rank
         vocab = mcfg.vocab_size
     if cfgd["mode"] == "lora":
         from mobilefinetuner_amd.peft import lora as L
@@ -114,6 +121,13 @@ def build(a, cfgd, dev, world):
     return model, step, vocab, desc, nparams
 
 
+def _spawn_ranks(n: int) -> int:
+    """Parent of an N-rank run started without torch.distributed.run: fresh subprocesses (never
+    exec, never a GPU call here), rank-failure propagation by the launcher."""
+    from mobilefinetuner_amd.launch import launch
+    return launch([os.path.abspath(__file__)] + sys.argv[1:], n, timeout=float(os.environ.get("MFT_BENCH_TIMEOUT", 0)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,19 +151,36 @@ def main():
     ap.add_argument("--targets", default="")
     ap.add_argument("--grad_accum", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu_smoke", action="store_true",
+                    help="gpt2-tiny on the CPU over gloo (tests the multi-rank bench path without a GPU)")
     a = ap.parse_args()
-    cfgd = CONFIGS[a.config]
-    a.batch = a.batch or cfgd["batch"]
-    a.seq = a.seq or cfgd["seq"]
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(_spawn_ranks(a.gpus))
+    cfgd = dict(CONFIGS[a.config])
+    if a.cpu_smoke:
+        cfgd["model"] = "gpt2-tiny"
+    a.batch = a.batch or (4 if a.cpu_smoke else cfgd["batch"])
+    a.seq = a.seq or (32 if a.cpu_smoke else cfgd["seq"])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if a.cpu_smoke:
+        dev = torch.device("cpu")
+        a.no_graph = True
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        if world > 1:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
+        assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
+    sync = (lambda: None) if a.cpu_smoke else torch.cuda.synchronize
 
     model, step, vocab, desc, nparams = build(a, cfgd, dev, world)
 
@@ -166,16 +197,16 @@ def main():
 
     for i in range(a.warmup):
         step(data[i % nbuf])
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(data[i % nbuf])
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], device=dev)
     if world > 1:
@@ -200,9 +231,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             # the reference publishes no throughput; only the GPT-2 small figure can be derived
-            "vs_baseline": round(value / BASELINE_TOKENS_PER_SEC, 1) if a.config == "gpt2-lora" else None,
-            "dtype": "bf16",
-            "data": "synthetic (random tokens, random-init weights)",
+            "vs_baseline": round(value / BASELINE_TOKENS_PER_SEC, 1) if (a.config == "gpt2-lora" and not a.cpu_smoke) else None,
+            "dtype": "fp32" if a.cpu_smoke else "bf16",
+            "data": "synthetic (random tokens, random-init weights)" + (" [cpu smoke]" if a.cpu_smoke else ""),
             "config": {
                 "model": f"{desc} ({nparams / 1e6:.0f}M params)",
                 "global_batch": world * a.batch * a.grad_accum,

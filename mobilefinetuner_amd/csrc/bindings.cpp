@@ -286,6 +286,10 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor step, 
   a.nonfinite = optp<int>(nonfinite);
   mft::adamw_step(a, stream());
 }
+void adamw_commit(Tensor step, c10::optional<Tensor> nonfinite, c10::optional<Tensor> sumsq_t) {
+  CHECK_F32(step);
+  mft::adamw_commit(fp(step), optp<int>(nonfinite), optp<float>(sumsq_t), stream());
+}
 
 // ------------------------------------------------------------------ LoRA
 // U = s * X Wt^T   (X [.., K] rows contiguous, Wt [R, K] contiguous rows)
@@ -536,6 +540,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sumsq", &sumsq);
   m.def("nonfinite_check", &nonfinite_check);
   m.def("adamw_step", &adamw_step);
+  m.def("adamw_commit", &adamw_commit);
   m.def("lora_rowdot", &lora_rowdot);
   m.def("lora_update", &lora_update);
   m.def("lora_wgrad", &lora_wgrad);

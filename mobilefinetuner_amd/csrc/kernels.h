@@ -125,7 +125,7 @@ struct AdamWArgs {
   long n;
   const float* lr_ptr;
   float beta1, beta2, eps, weight_decay;
-  const float* step_ptr;  // device step count (float, already incremented)
+  const float* step_ptr;  // device count of applied steps (this update uses t = *step_ptr + 1)
   const float* sumsq;     // device grad-norm^2 (or null)
   float max_norm;
   int l2_coupled;         // reference-compat: g += wd*p instead of decoupled decay
@@ -133,6 +133,8 @@ struct AdamWArgs {
   const int* nonfinite;   // optional device flag: skip the step when set
 };
 void adamw_step(const AdamWArgs& a, hipStream_t st);
+// after every adamw_step launch of one update: *step += 1 unless the update was skipped
+void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStream_t st);
 // flag[0] = any(!isfinite(x))  (accumulates with OR)
 void nonfinite_check(const float* x, long n, int* flag, hipStream_t st);
 

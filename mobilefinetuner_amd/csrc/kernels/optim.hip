@@ -57,10 +57,16 @@ void nonfinite_check(const float* x, long n, int* flag, hipStream_t st) {
   nonfinite_kernel<<<(int)(g < 1024 ? (g > 0 ? g : 1) : 1024), 256, 0, st>>>(x, n, flag);
 }
 
+// A step is skipped when any grad is non-finite (the flag, all-reduced over ranks by the ZeRO
+// optimizers so every rank skips together) or when the global grad norm itself is non-finite.
+__device__ __forceinline__ bool adamw_skip(const int* nonfinite, const float* sumsq) {
+  return (nonfinite && *nonfinite) || (sumsq && !isfinite(*sumsq));
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
-  if (a.nonfinite && *a.nonfinite) return;  // skip-step on NaN/Inf grads (fault tolerance)
+  if (adamw_skip(a.nonfinite, a.sumsq)) return;  // skip-step on NaN/Inf grads (fault tolerance)
   const float lr = *a.lr_ptr;
-  const float t = *a.step_ptr;
+  const float t = *a.step_ptr + 1.f;  // *step_ptr counts APPLIED steps; adamw_commit advances it
   const float bc1 = 1.f - powf(a.beta1, t);
   const float bc2 = 1.f - powf(a.beta2, t);
   float clip = 1.f;
@@ -112,6 +118,15 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
       if (a.shadow) a.shadow[i] = f2bf(pj);
     }
   }
+}
+
+// step += 1 only when the update was applied (a skipped step must not advance bias correction)
+__global__ void adamw_commit_kernel(float* step, const int* nonfinite, const float* sumsq) {
+  if (threadIdx.x == 0 && !adamw_skip(nonfinite, sumsq)) step[0] += 1.f;
+}
+
+void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStream_t st) {
+  adamw_commit_kernel<<<1, 64, 0, st>>>(step, nonfinite, sumsq);
 }
 
 void adamw_step(const AdamWArgs& a, hipStream_t st) {

@@ -166,6 +166,7 @@ class Gemma3Model(nn.Module):
         self.cfg, self.dtype = cfg, dtype
         self.embed = nn.Parameter(torch.zeros(cfg.vocab_padded, cfg.hidden_size, dtype=dtype, device=device),
                                   requires_grad=False)
+        self.embed._mft_tied = True  # embedding + LM head (ops.functional grad_ready ordering)
         self.layers = nn.ModuleList([Gemma3Layer(cfg, i, dtype, device) for i in range(cfg.num_hidden_layers)])
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, 1.0, device)
         s = math.sqrt(cfg.hidden_size)

@@ -114,6 +114,7 @@ class GPT2Model(nn.Module):
         C = cfg.n_embd
         self.wte = nn.Parameter(torch.zeros(cfg.vocab_padded, C, dtype=dtype, device=device), requires_grad=False)
         self.wpe = nn.Parameter(torch.zeros(cfg.n_positions, C, dtype=dtype, device=device), requires_grad=False)
+        self.wte._mft_tied = True  # embedding + LM head (ops.functional grad_ready ordering)
         self.blocks = nn.ModuleList([GPT2Block(cfg, dtype, device) for _ in range(cfg.n_layer)])
         self.ln_f = LayerNorm(C, cfg.layer_norm_epsilon, device)
         self.activation_checkpointing = False

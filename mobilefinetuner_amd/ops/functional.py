@@ -996,7 +996,9 @@ class _LMHeadCE(Function):
                 if wbuf is not None or wtmp is not None:
                     tgt = wbuf if wbuf is not None else wtmp
                     _mm_wgrad_into(tgt, logits, hc, w_grad_scale)
-        if wbuf is not None:
+        # a tied weight (GPT-2 wte) receives its final contribution later, from the embedding
+        # backward, which fires the hook; announcing it here would let a DP bucket reduce early
+        if wbuf is not None and not getattr(w, "_mft_tied", False):
             grad_ready(w)
         loss = loss_rows.sum() * scale
         ctx.save_for_backward(dh if dh is not None else torch.empty(0))

@@ -58,11 +58,17 @@ class FusedAdamW:
             self.m = torch.zeros(n, dtype=torch.float32, device=dev)
             self.v = torch.zeros(n, dtype=torch.float32, device=dev)
         self.lr_dev = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
+        # step_dev counts APPLIED updates (a NaN/Inf-skipped step does not advance the bias
+        # correction); the kernel uses t = step_dev + 1 and adamw_commit advances it
         self.step_dev = torch.zeros(1, dtype=torch.float32, device=dev)
         self.sumsq_dev = torch.zeros(1, dtype=torch.float32, device=dev)
         self.nonfinite_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        # running count of skipped updates, kept on device (read only when a log line is due)
+        self.skipped_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.lr = float(lr)
-        self.step_count = 0
+        self.attempts = 0
+        # set by the ZeRO optimizers: all-reduces the skip flag (MAX) so every rank skips together
+        self.reduce_flag = None
 
     # ---- host-side control (outside any captured graph)
     def set_lr(self, lr: float):
@@ -76,6 +82,11 @@ class FusedAdamW:
     def skipped_last(self) -> bool:
         return bool(self.nonfinite_dev.item())
 
+    @property
+    def step_count(self) -> int:
+        """Applied (non-skipped) updates (host sync)."""
+        return int(self.step_dev.item())
+
     # ---- device work (graph-capturable)
     def compute_grad_sumsq(self, extra_sumsq=None):
         g = self.flat.grad[self.lo:self.hi]
@@ -87,28 +98,35 @@ class FusedAdamW:
             extra_sumsq(self.sumsq_dev)
 
     def step(self, sumsq_ready: bool = False):
-        self.step_count += 1
-        self.step_dev.add_(1.0)
+        self.attempts += 1
         p = self.flat.master[self.lo:self.hi]
         g = self.flat.grad[self.lo:self.hi]
         if (self.max_grad_norm is not None) and not sumsq_ready:
             self.compute_grad_sumsq()
+        if self.skip_nonfinite:
+            self.nonfinite_dev.zero_()
+            if p.is_cuda:
+                native().nonfinite_check(g, self.nonfinite_dev)
+            else:
+                self.nonfinite_dev.fill_(int(not bool(torch.isfinite(g).all())))
+            if self.reduce_flag is not None:
+                self.reduce_flag(self.nonfinite_dev)
+        sumsq = self.sumsq_dev if self.max_grad_norm is not None else None
+        nonfinite = self.nonfinite_dev if self.skip_nonfinite else None
         if p.is_cuda:
             C = native()
-            if self.skip_nonfinite:
-                self.nonfinite_dev.zero_()
-                C.nonfinite_check(g, self.nonfinite_dev)
             sh = self.flat.shadow[self.lo:self.hi] if self.flat.shadow is not None else None
             if self.offload:
                 self._step_offloaded(C, p, g, sh)
-                return
-            C.adamw_step(p, g, self.m, self.v, self.lr_dev, self.step_dev,
-                         self.sumsq_dev if self.max_grad_norm is not None else None,
-                         self.beta1, self.beta2, self.eps, self.weight_decay,
-                         float(self.max_grad_norm or 0.0), self.l2_coupled, sh,
-                         self.nonfinite_dev if self.skip_nonfinite else None)
+            else:
+                C.adamw_step(p, g, self.m, self.v, self.lr_dev, self.step_dev, sumsq,
+                             self.beta1, self.beta2, self.eps, self.weight_decay,
+                             float(self.max_grad_norm or 0.0), self.l2_coupled, sh, nonfinite)
+            C.adamw_commit(self.step_dev, nonfinite, sumsq)
         else:
             self._step_reference(p, g)
+        if nonfinite is not None:
+            self.skipped_dev.add_(self.nonfinite_dev)
 
     def _step_offloaded(self, C, p, g, sh):
         """Chunk c: H2D on one copy stream, update on the compute stream, D2H on another copy
@@ -161,15 +179,14 @@ class FusedAdamW:
 
     @torch.no_grad()
     def _step_reference(self, p, g):
-        if self.skip_nonfinite and not torch.isfinite(g).all():
-            self.nonfinite_dev.fill_(1)
+        if self.skip_nonfinite and (bool(self.nonfinite_dev.item()) or not math.isfinite(float(self.sumsq_dev))):
             return
-        self.nonfinite_dev.fill_(0)
         clip = 1.0
         if self.max_grad_norm is not None:
             norm = float(self.sumsq_dev.sqrt())
             if norm > self.max_grad_norm:
                 clip = self.max_grad_norm / (norm + 1e-6)
+        self.step_dev.add_(1.0)
         t = float(self.step_dev)
         lr = float(self.lr_dev)
         gg = g * clip
@@ -206,6 +223,5 @@ class FusedAdamW:
         else:
             self.m.copy_(sd["m"].to(self.m.device))
             self.v.copy_(sd["v"].to(self.v.device))
-        self.step_count = int(sd["step"])
-        self.step_dev.fill_(float(self.step_count))
+        self.step_dev.fill_(float(int(sd["step"])))
         self.set_lr(sd.get("lr", self.lr))

@@ -85,6 +85,10 @@ class DataParallel:
         self._works = []
         self._pending = [0] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
+        self._seen = set()
+        # with gradient accumulation a bucket may only be reduced once its params received the
+        # LAST micro-batch's contribution: TrainStep clears this flag for earlier micro-batches
+        self.last_micro = True
         self._hook = None
         if self.overlap and len(self.buckets) > 1:
             self._hook = Fx.register_grad_ready_hook(self._on_ready)
@@ -101,6 +105,7 @@ class DataParallel:
     def begin_step(self):
         self._pending = [b["n"] for b in self.buckets]
         self._launched = [False] * len(self.buckets)
+        self._seen = set()
         self._works = []
 
     def _launch(self, bi):
@@ -117,9 +122,12 @@ class DataParallel:
         # stays pending and finish() reduces every bucket after the replay
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
             return
-        bi = self.param_bucket.get(id(p))
-        if bi is None:
+        if not self.last_micro:
             return
+        bi = self.param_bucket.get(id(p))
+        if bi is None or id(p) in self._seen:
+            return
+        self._seen.add(id(p))  # a param counts once per step (its LAST contribution fires the hook)
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._launch(bi)

@@ -35,6 +35,9 @@ class ZeroOptimizer:
         self.shard = n // self.world
         self.lo, self.hi = self.rank * self.shard, (self.rank + 1) * self.shard
         self.inner = FusedAdamW(flat, param_range=(self.lo, self.hi), **adamw_kwargs)
+        if self.world > 1:
+            # each rank scans only its shard for NaN/Inf: OR the flags so all ranks skip together
+            self.inner.reduce_flag = lambda f: dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
         # parameters that compute straight from the fp32 master (norm weights/biases: no bf16
         # shadow) are not covered by the shadow all-gather; their owned slices are re-assembled
         # with one masked all-reduce of a packed index list (tiny: LN/RMSNorm parameters only)

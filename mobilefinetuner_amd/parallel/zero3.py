@@ -313,6 +313,8 @@ class Zero3:
                 dist.all_reduce(o.sumsq_dev, op=dist.ReduceOp.SUM, group=self.group)
             if self.rep_off < self.flat.numel:  # replicated part: identical everywhere, count once
                 o.sumsq_dev.add_(g[self.rep_off:].double().pow(2).sum().float().reshape(1))
+        if self.world > 1 and o.reduce_flag is None:
+            o.reduce_flag = lambda f: dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
         o.step(sumsq_ready=True)
 
     def __getattr__(self, k):  # set_lr, grad_norm, skipped_last, lr, step_count, m, v, ...

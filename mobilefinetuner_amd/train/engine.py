@@ -44,7 +44,9 @@ class TrainStep:
         self.flat.grad.zero_()
         from ..ops.functional import dropout_counter
         dropout_counter(self.flat.grad.device).add_(1)  # fresh LoRA-dropout masks every step
-        for ids, lab in batches:
+        for i, (ids, lab) in enumerate(batches):
+            if self.dp is not None and hasattr(self.dp, "last_micro"):
+                self.dp.last_micro = i == len(batches) - 1
             loss = self.loss_fn(self.model, ids, lab, scale)
             (loss * scale).backward()
             self.loss_dev.add_(loss.detach().float().reshape(1), alpha=scale)

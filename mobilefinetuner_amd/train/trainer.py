@@ -63,6 +63,26 @@ class TrainConfig:
     extra: dict = field(default_factory=dict)
 
 
+def rng_state(device) -> dict:
+    """Every RNG stream a resumed run must continue: torch CPU / HIP generators and the device
+    step counter that keys the counter-based LoRA dropout masks."""
+    from ..ops.functional import dropout_counter
+    st = {"cpu": torch.get_rng_state().tolist()}
+    if device.type == "cuda":
+        st["cuda"] = torch.cuda.get_rng_state(device).tolist()
+        st["dropout_ctr"] = int(dropout_counter(device).item())
+    return st
+
+
+def set_rng_state(st: dict, device):
+    from ..ops.functional import dropout_counter
+    if "cpu" in st:
+        torch.set_rng_state(torch.tensor(st["cpu"], dtype=torch.uint8))
+    if device.type == "cuda" and "cuda" in st:
+        torch.cuda.set_rng_state(torch.tensor(st["cuda"], dtype=torch.uint8), device)
+        dropout_counter(device).fill_(int(st.get("dropout_ctr", 0)))
+
+
 class Trainer:
     def __init__(self, model, flat: FlatParams, train_ds, valid_ds, cfg: TrainConfig, device,
                  save_fn=None, power_monitor=None, dp: DataParallel | None = None, loss_fn=None,
@@ -111,6 +131,10 @@ class Trainer:
         self.ema_loss = None
         self.total_tokens = 0
         self.skipped = 0
+        self._skipped_base = 0
+        # EMA of the loss kept on device (no per-step host sync); read at log time only
+        self._ema_dev = torch.zeros(1, dtype=torch.float32, device=device)
+        self._ema_init = torch.zeros(1, dtype=torch.float32, device=device)
         self.history = []
 
     # ------------------------------------------------------------------ schedule
@@ -174,7 +198,10 @@ class Trainer:
                          {n: p.detach() for n, p in self.flat.named()})
             st.save_file(os.path.join(path, f"optimizer.rank{r}.safetensors"), self._moments())
         elif hasattr(self.opt, "stage"):
-            # ZeRO-1/2: masters are replicated (rank 0 writes them), moments are per-rank shards
+            # ZeRO-1/2: every rank updated only its shard of the fp32 master (other shards reach it
+            # only through the bf16 shadow all-gather): consolidate the masters first (collective,
+            # all ranks), then rank 0 writes them; moments are per-rank shards
+            self.opt.gather_master()
             if r == 0:
                 st.save_file(os.path.join(path, "trainable.safetensors"),
                              {n: p.detach() for n, p in self.flat.named()})
@@ -184,10 +211,11 @@ class Trainer:
                          {n: p.detach() for n, p in self.flat.named()})
             st.save_file(os.path.join(path, "optimizer.safetensors"),
                          self._moments())
+        self._sync_metrics()
         state = {"global_step": self.global_step, "opt_step": self.opt.step_count, "lr": self.opt.lr,
                  "ema_loss": self.ema_loss, "total_tokens": self.total_tokens, "skipped": self.skipped,
                  "data": self.train_ds.state(), "world": self.world, "total_steps": self.total_steps,
-                 "torch_rng": torch.get_rng_state().tolist()[:0]}
+                 "rng": rng_state(self.device)}
         with open(os.path.join(path, f"trainer_state.rank{r}.json"), "w") as f:
             json.dump(state, f)
         if is_dist():
@@ -218,8 +246,40 @@ class Trainer:
         self.ema_loss = s["ema_loss"]
         self.total_tokens = int(s["total_tokens"])
         self.skipped = int(s.get("skipped", 0))
+        self._skipped_base = self.skipped
+        if getattr(self.opt, "skipped_dev", None) is not None:
+            self.opt.skipped_dev.zero_()
+        if self.ema_loss is not None:
+            self._ema_dev.fill_(float(self.ema_loss))
+            self._ema_init.fill_(1.0)
+        if "rng" in s:
+            set_rng_state(s["rng"], self.device)
         self.train_ds.restore(s["data"])
         log0(f"[Resume] restored full training state from {path} at global step {self.global_step}")
+
+    # ------------------------------------------------------------------ device-side metrics
+    def _ema_update(self, loss_dev, beta):
+        """ema = beta * ema + (1 - beta) * loss on device; a non-finite loss leaves it unchanged.
+        Each rank keeps the EMA of its local loss; the EMA is linear, so the all-reduced mean of the
+        per-rank EMAs (taken at log time) equals the EMA of the rank-mean loss."""
+        beta = max(0.0, min(0.9999, float(beta)))
+        l = loss_dev.detach().float().reshape(1)
+        ok = torch.isfinite(l)
+        new = torch.where(self._ema_init > 0, beta * self._ema_dev + (1 - beta) * l, l)
+        self._ema_dev.copy_(torch.where(ok, new, self._ema_dev))
+        self._ema_init.copy_(torch.where(ok, torch.ones_like(self._ema_init), self._ema_init))
+
+    def _sync_metrics(self):
+        """Host copies of the device-side EMA and skipped-step counter (one sync, log time)."""
+        if self.cfg.ema_beta > 0 and float(self._ema_init.item()) > 0:
+            e = self._ema_dev.clone()
+            if is_dist():
+                allreduce_sum_(e)
+                e /= self.world
+            self.ema_loss = float(e.item())
+        sk = getattr(self.opt, "skipped_dev", None)
+        if sk is not None:
+            self.skipped = self._skipped_base + int(sk.item())
 
     # ------------------------------------------------------------------ loop
     def _mfu(self, tps_per_gpu: float, seq: int):
@@ -268,18 +328,16 @@ class Trainer:
             ntok_all = ntok * self.world
             self.total_tokens += ntok_all
             do_log = (step + 1) % max(1, c.log_interval) == 0 or step + 1 == self.total_steps
-            if do_log or c.ema_beta > 0:
+            if c.ema_beta > 0:
+                self._ema_update(loss_dev, c.ema_beta)
+            if do_log:
                 lt = loss_dev.detach().clone()
                 if is_dist():
                     allreduce_sum_(lt)
                     lt /= self.world
                 loss = float(lt.item())
                 skipped = self.opt.skipped_last()
-                self.skipped += int(skipped)
-                if math.isfinite(loss):
-                    beta = max(0.0, min(0.9999, c.ema_beta))
-                    self.ema_loss = loss if self.ema_loss is None else beta * self.ema_loss + (1 - beta) * loss
-            if do_log:
+                self._sync_metrics()
                 step_ms = timer.report().get("train_step", 0.0)
                 gn = self.opt.grad_norm()
                 gn_clip = min(gn, c.clip_grad_norm) if c.clip_grad_norm > 0 else gn
@@ -306,6 +364,7 @@ class Trainer:
                         f.write(json.dumps(rec) + "\n")
             if c.eval_interval > 0 and (step + 1) % c.eval_interval == 0:
                 ev = self.evaluate()
+                self._sync_metrics()
                 log0(f"\n[Eval] epoch {cur_epoch} | step {step + 1} | valid_ppl {ev['ppl']:.2f} | ema_loss "
                      f"{(self.ema_loss or 0):.4f} | total_tokens {self.total_tokens}\n")
                 if c.eval_out and rank0():

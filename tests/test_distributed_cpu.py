@@ -232,3 +232,139 @@ def test_ddp_hook_defers_inside_graph_capture(monkeypatch):
     monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
     dp._on_ready(s.param)
     assert dp._pending[bi] == before[bi] - 1
+
+
+def _worker_ddp_accum_hooks(rank, world, port, q):
+    """grad_ready fires per micro-batch (via the ops' _sink); with accum=2 the overlapped buckets
+    must reduce only after the last micro-batch, and a param announced twice counts once."""
+    _init(rank, world, port)
+    from mobilefinetuner_amd.ops import functional as Fx
+    from mobilefinetuner_amd.parallel.ddp import DataParallel
+    from mobilefinetuner_amd.utils.params import FlatParams
+    ps = [(f"p{i}", torch.nn.Parameter(torch.zeros(3000 + 100 * i))) for i in range(4)]
+    flat = FlatParams(ps, "cpu", shadow=False)
+    dp = DataParallel(flat, bucket_mb=0.01)
+    assert len(dp.buckets) > 1 and dp._hook is not None
+    dp.begin_step()
+    flat.grad.zero_()
+    gen = torch.Generator().manual_seed(100 + rank)
+    total = torch.zeros_like(flat.grad)
+    for micro in range(2):
+        dp.last_micro = micro == 1
+        for sl in flat.slots:
+            p = sl.param
+            g = torch.randn(p.shape, generator=gen)
+            total[sl.offset:sl.offset + sl.numel] += g
+            Fx._sink(p, g)  # accumulates into p.grad and calls grad_ready(p)
+            if micro == 1:
+                Fx.grad_ready(p)  # a second announcement (tied weights) must not double count
+    dp.finish()
+    q.put((rank, flat.grad.clone(), total.clone()))
+    dist.destroy_process_group()
+
+
+def test_ddp_overlap_with_grad_accumulation():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_ddp_accum_hooks, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict((r, (g, t)) for r, g, t in [q.get(timeout=300) for _ in ps])
+    for p in ps:
+        p.join(60)
+    want = (out[0][1] + out[1][1]) / 2  # mean over ranks of the summed micro-batch grads
+    assert torch.allclose(out[0][0], want, atol=1e-6) and torch.allclose(out[1][0], want, atol=1e-6)
+
+
+def _worker_zero_nonfinite(rank, world, port, q):
+    """A NaN in the shard of ONE rank: every rank must skip the step, and the applied-step counter
+    (bias correction) must not advance."""
+    _init(rank, world, port)
+    from mobilefinetuner_amd.parallel.zero import ZeroOptimizer
+    from mobilefinetuner_amd.utils.params import FlatParams
+    ps = [("w", torch.nn.Parameter(torch.ones(4096)))]
+    flat = FlatParams(ps, "cpu", shadow=False, pad_multiple=world)
+    opt = ZeroOptimizer(flat, 2, lr=1e-2, weight_decay=0.0, max_grad_norm=1.0)
+    flat.grad.fill_(0.1)
+    opt.reduce_gradients()
+    opt.step()
+    after1 = flat.master.clone()
+    flat.grad.fill_(0.1)
+    if rank == 1:
+        flat.grad[flat.numel - 5] = float("nan")  # lands in rank 1's shard only
+    opt.reduce_gradients()
+    opt.step()
+    opt.gather_master()
+    q.put((rank, torch.equal(after1, flat.master), opt.step_count, int(opt.skipped_dev.item())))
+    dist.destroy_process_group()
+
+
+def test_zero_nonfinite_skip_is_global():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_zero_nonfinite, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict((r, rest) for r, *rest in [q.get(timeout=300) for _ in ps])
+    for p in ps:
+        p.join(60)
+    for r in (0, 1):
+        unchanged, steps, skipped = out[r]
+        assert unchanged, f"rank {r} applied a step the other rank skipped"
+        assert steps == 1 and skipped == 1
+
+
+def _worker_zero_save(rank, world, port, path, q):
+    _init(rank, world, port)
+    from mobilefinetuner_amd.data.wikitext2 import LMDataset, WT2Config
+    from mobilefinetuner_amd.io import safetensors as st
+    from mobilefinetuner_amd.models.gpt2 import GPT2Config, GPT2Model
+    from mobilefinetuner_amd.train.trainer import TrainConfig, Trainer
+    from mobilefinetuner_amd.utils.params import FlatParams
+    m = GPT2Model(GPT2Config.preset("gpt2-tiny"), dtype=torch.float32, device="cpu", seed=11)
+    m.set_full_finetune()
+    flat = FlatParams(m.named_parameters(), "cpu", shadow=True, pad_multiple=world)
+    toks = torch.randint(0, 1000, (8000,), generator=torch.Generator().manual_seed(0), dtype=torch.int64).int()
+    ds = LMDataset(WT2Config(seq_len=32, seed=1, rank=rank, world=world), "train", toks)
+    tc = TrainConfig(steps=3, batch_size=2, lr=1e-3, log_interval=1, use_graph=False)
+    tr = Trainer(m, flat, ds, None, tc, torch.device("cpu"), zero_stage=2)
+    tr.train()
+    tr.save_state(path)
+    tr.opt.gather_master()
+    full = {n: p.detach().clone() for n, p in m.named_parameters()}
+    dist.barrier()
+    saved = st.load_file(os.path.join(path, "trainable.safetensors"))
+    ok = all(torch.equal(saved[n].float(), full[n].float()) for n in full)
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_zero2_checkpoint_has_every_shard(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_zero_save, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=600) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert out[0] and out[1]
+
+
+def test_bench_spawns_ranks_cpu_smoke():
+    """bench.py --gpus 2 without a launcher spawns 2 rank processes itself (no re-exec) and reports
+    the launched world size."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--cpu_smoke"], capture_output=True, text=True, timeout=600,
+                       env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 2 * out["config"]["micro_batch_per_gpu"]
