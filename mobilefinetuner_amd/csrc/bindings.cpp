@@ -477,7 +477,7 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
   a.aux = X.defined() ? bp(X) : nullptr; a.ldaux = X.defined() ? X.stride(0) : 0;
   a.M = M; a.N = N; a.K = K; a.alpha = (float)alpha;
   if (epi == mft::GEMM_EPI_LORA) {
-    TORCH_CHECK(bm == 8 && !b_nn && lora_u.has_value() && lora_w.has_value(), "gemm: LoRA epilogue = cfg 8, NT, u and w");
+    TORCH_CHECK(bm == 8 && lora_u.has_value() && lora_w.has_value(), "gemm: LoRA epilogue = cfg 8, u and w");
     CHECK_BF16((*lora_u)); CHECK_BF16((*lora_w));
     TORCH_CHECK(lora_u->size(0) == M && lora_w->size(1) == N && lora_u->size(1) == lora_w->size(0) &&
                 lora_u->stride(1) == 1 && lora_w->stride(1) == 1, "gemm: LoRA u [M, r], w [r, N]");
@@ -485,11 +485,73 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
     a.lora_w = bp(*lora_w); a.ld_lw = lora_w->stride(0);
     a.lora_r = lora_u->size(1);
   }
-  if (bm == 8 && !b_nn) mft::gemm8(a, (int)epi, stream());  // cfg 8: 8-phase pipelined 256x256 NT kernel
+  if (bm == 8) mft::gemm8x(a, (int)epi, false, b_nn, stream());  // cfg 8: 8-phase pipelined 256x256 kernel
   else mft::gemm(a, b_nn, (int)epi, (int)bm, stream());
   return {C, X};
 }
 
+// General 8-phase GEMM, every operand layout (gemm8.hip):
+//   A: a_t ? [K, M] : [M, K];  B: b_t ? [K, N] : [N, K];  C [M, N] (bf16, or fp32 += for F32ACC)
+// F32ACC with a_t && b_t is the TN weight gradient: split over K into fp32 slabs + deterministic
+// reduce when the output has few 256x256 tiles.
+std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, c10::optional<Tensor> bias,
+                           c10::optional<Tensor> aux, double alpha, c10::optional<Tensor> out,
+                           c10::optional<Tensor> lora_u, c10::optional<Tensor> lora_w) {
+  CHECK_CUDA(A); CHECK_BF16(A); CHECK_BF16(B);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "gemm_t: row-contiguous 2-D operands");
+  const int M = a_t ? A.size(1) : A.size(0), K = a_t ? A.size(0) : A.size(1);
+  const int N = b_t ? B.size(1) : B.size(0);
+  TORCH_CHECK((b_t ? B.size(0) : B.size(1)) == K, "gemm_t: inner dimensions differ");
+  TORCH_CHECK(mft::gemm8_supported(M, N, K, a_t, b_t), "gemm_t: needs K % 64 == 0, N % 8 == 0 (and M % 8 for a_t)");
+  TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "gemm_t: leading dimensions must be multiples of 8");
+  c10::DeviceGuard g(A.device());
+  const bool f32 = epi == mft::GEMM_EPI_F32ACC;
+  Tensor C;
+  if (out.has_value()) {
+    C = *out;
+    TORCH_CHECK(C.size(0) == M && C.size(1) == N && C.stride(1) == 1 && C.stride(0) % 8 == 0, "gemm_t: out shape");
+    TORCH_CHECK(C.scalar_type() == (f32 ? torch::kFloat32 : torch::kBFloat16), "gemm_t: out dtype");
+  } else {
+    TORCH_CHECK(!f32, "gemm_t: fp32 accumulate needs out=");
+    C = torch::empty({M, N}, A.options());
+  }
+  Tensor X;
+  if (epi == mft::GEMM_EPI_BIAS_GELU) {
+    X = aux.has_value() ? *aux : torch::empty({M, N}, A.options());
+  } else if (epi == mft::GEMM_EPI_DGELU) {
+    TORCH_CHECK(aux.has_value(), "gemm_t: dGELU needs aux (pre-activation)");
+    X = *aux;
+  }
+  if (X.defined()) TORCH_CHECK(X.size(0) == M && X.size(1) == N && X.stride(1) == 1 && X.stride(0) % 8 == 0, "gemm_t: aux shape");
+  if (epi == mft::GEMM_EPI_BIAS || epi == mft::GEMM_EPI_BIAS_GELU)
+    TORCH_CHECK(bias.has_value() && bias->numel() == N && bias->scalar_type() == torch::kBFloat16, "gemm_t: bf16 bias [N]");
+  mft::GemmArgs a{};
+  a.A = bp(A); a.lda = A.stride(0);
+  a.B = bp(B); a.ldb = B.stride(0);
+  a.C = C.data_ptr(); a.ldc = C.stride(0);
+  a.bias = bias.has_value() ? bp(*bias) : nullptr;
+  a.aux = X.defined() ? bp(X) : nullptr; a.ldaux = X.defined() ? X.stride(0) : 0;
+  a.M = M; a.N = N; a.K = K; a.alpha = (float)alpha;
+  Tensor ws;
+  if (f32) {
+    a.ksplit = mft::gemm8_pick_ksplit(M, N, K);
+    if (a.ksplit > 1) {
+      ws = torch::empty({(long)a.ksplit * M * N}, A.options().dtype(torch::kFloat32));
+      a.ws = fp(ws);
+    }
+  }
+  if (epi == mft::GEMM_EPI_LORA) {
+    TORCH_CHECK(lora_u.has_value() && lora_w.has_value(), "gemm_t: LoRA epilogue needs u and w");
+    CHECK_BF16((*lora_u)); CHECK_BF16((*lora_w));
+    TORCH_CHECK(lora_u->size(0) == M && lora_w->size(1) == N && lora_u->size(1) == lora_w->size(0) &&
+                lora_u->stride(1) == 1 && lora_w->stride(1) == 1, "gemm_t: LoRA u [M, r], w [r, N]");
+    a.lora_u = bp(*lora_u); a.ld_lu = lora_u->stride(0);
+    a.lora_w = bp(*lora_w); a.ld_lw = lora_w->stride(0);
+    a.lora_r = lora_u->size(1);
+  }
+  mft::gemm8x(a, (int)epi, a_t, b_t, stream());
+  return {C, X};
+}
 
 // out[N] (fp32) (+)= column sums of x[M, N] (bf16, row stride ld): bias gradients accumulated
 // straight into the flat fp32 grad buffer (deterministic two-stage reduction, no fp32 copy of x).
@@ -547,6 +609,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_wgrad_multi", &lora_wgrad_multi);
   m.def("lora_merge", &lora_merge);
   m.def("lora_dy", &lora_dy);
+  m.def("gemm_t", &gemm_t, py::arg("A"), py::arg("B"), py::arg("a_t"), py::arg("b_t"), py::arg("epi"),
+        py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("alpha") = 1.0, py::arg("out") = py::none(),
+        py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none());
   m.def("gemm", &gemm_op, py::arg("A"), py::arg("B"), py::arg("b_nn"), py::arg("epi"), py::arg("bias"), py::arg("aux"),
         py::arg("alpha"), py::arg("cfg"), py::arg("out"), py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none());
   m.def("zero_cols", &zero_cols);

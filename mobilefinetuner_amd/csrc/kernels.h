@@ -58,7 +58,7 @@ int attn_bwd_path(int D, int Sq, int Sk, int window);
 
 // ---------------------------------------------------------------- GEMM (gemm.hip)
 enum GemmEpi { GEMM_EPI_NONE = 0, GEMM_EPI_BIAS = 1, GEMM_EPI_BIAS_GELU = 2, GEMM_EPI_DGELU = 3, GEMM_EPI_F32ACC = 4,
-               GEMM_EPI_LORA = 5 };
+               GEMM_EPI_LORA = 5, GEMM_EPI_F32PART = 6 /* internal: split-K fp32 slab */ };
 struct GemmArgs {
   const bf16_t* A;
   long lda;  // A [M, K] row-major
@@ -78,12 +78,22 @@ struct GemmArgs {
   const bf16_t* lora_w;
   long ld_lw;
   int lora_r;
+  // split-K (GEMM_EPI_F32ACC only): ksplit > 1 splits K into slabs ws[ksplit][M][N] (fp32) that
+  // gemm_splitk_reduce adds into C in a fixed order (deterministic, no atomics)
+  int ksplit;
+  float* ws;
 };
 bool gemm_supported(int M, int N, int K);
 // cfg: tile configuration (gemm.hip launch_e): 0 = 256x256, 1 = 128x256, 2 = 128x128, 3 = 256x128
 void gemm(const GemmArgs& g, bool b_nn, int epi, int cfg, hipStream_t st);
-// 256x256 8-phase pipelined NT GEMM (gemm8.hip); same epilogues
-void gemm8(const GemmArgs& g, int epi, hipStream_t st);
+// 256x256 8-phase pipelined GEMM (gemm8.hip); same epilogues.  a_t: A stored [K, M]; b_t: B stored
+// [K, N] (NN data-grad); both: TN weight-grad (use GEMM_EPI_F32ACC with gemm8_pick_ksplit / ws)
+void gemm8(const GemmArgs& g, int epi, hipStream_t st);  // NT
+void gemm8x(const GemmArgs& g, int epi, bool a_t, bool b_t, hipStream_t st);
+bool gemm8_supported(int M, int N, int K, bool a_t, bool b_t);
+int gemm8_pick_ksplit(int M, int N, int K);
+void gemm_splitk_reduce(const float* ws, int ksplit, int M, int N, float* C, long ldc, float alpha, int accumulate,
+                        hipStream_t st);
 
 // ---------------------------------------------------------------- activations (act.hip)
 void gelu_fwd(const bf16_t* x, bf16_t* y, long n, hipStream_t st);

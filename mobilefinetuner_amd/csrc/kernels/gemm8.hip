@@ -1,9 +1,14 @@
-// 256 x 256 x 64 bf16 MFMA GEMM with an 8-phase software pipeline (gfx950), NT operand layout:
+// 256 x 256 x 64 bf16 MFMA GEMM with an 8-phase software pipeline (gfx950), every operand layout:
 //
-//   C[M, N] = epi(alpha * A[M, K] . B[N, K]^T)          A, B row-major, K contiguous
+//   C[M, N] = epi(alpha * op(A) . op(B))
+//   A: AT = false  [M, K] K-contiguous (activations)      AT = true  [K, M] M-contiguous
+//   B: BT = false  [N, K] K-contiguous ("NT": y = x W^T)  BT = true  [K, N] N-contiguous ("NN": dx = dy W)
+//   TN weight gradient dW[N_out, K_in] = dy^T x: AT = BT = true (both operands token-major), split
+//   over the token (K) dimension into fp32 slabs reduced deterministically by gemm_splitk_reduce.
 //
-// (data-gradient GEMMs use the same layout through a transposed weight copy, ops.functional
-// weight_t).  Structure after the CDNA HIP guide §5 "256² 8-phase template" (T1 XCD remap, T2 LDS
+// K-contiguous half-tiles are [128 rows][64 k] (ds_read_b128 fragments); token-major half-tiles are
+// [64 k][128 rows] read with ds_read_b64_tr_b16 (CDNA HIP guide T10) -- no transposed copies of any
+// operand (the weight_t copies of round 1 are gone).  Structure after the CDNA HIP guide §5 "256² 8-phase template" (T1 XCD remap, T2 LDS
 // XOR swizzle, T3+T4 8-phase interleave with counted vmcnt, T5 setprio):
 //
 //   * 8 waves; each 64-wide ds_read/MFMA phase works on ONE 128 x 128 quadrant of the block tile
@@ -43,6 +48,7 @@ __device__ __forceinline__ void glds16_8(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((g_void8*)src, (lds_void8*)lds_wave_base, 16, 0, 0);
 }
 
+
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -68,6 +74,55 @@ __device__ __forceinline__ void stage_half(bf16_t* lds, const bf16_t* src, long 
   }
 }
 
+// stage one [64 k][128 cols] half-tile of a k-major operand: rows k0..k0+63 of src, columns
+// c0..c0+127 (clamped to cmax-8; cmax % 8 == 0).  256-B rows; the 16-B chunk index is XOR-swizzled
+// with tsw(k) (even, so 32-B pairs stay together) on the SOURCE address: the 8 rows one 32-lane half
+// of ds_read_b64_tr_b16 touches ({0..3, 8..11} or {4..7, 12..15} mod 16) land in 8 distinct 32-B
+// bank slots -> conflict-free transposed reads.
+__device__ __forceinline__ int tsw(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+
+__device__ __forceinline__ void stage_half_t(bf16_t* lds, const bf16_t* src, long ld, int c0, int cmax, int k0) {
+  const int tid = threadIdx.x, w = tid >> 6;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int c = t * 512 + tid;
+    const int r = c >> 4, s = c & 15;
+    const int gc = min(c0 + ((s ^ tsw(r)) << 3), cmax - 8);
+    glds16_8(src + (long)(k0 + r) * ld + gc, lds + (t * 512 + w * 64) * 8);
+  }
+}
+
+// ds_read_b64_tr_b16 as inline asm: the builtin makes hipcc (ROCm 7.2) assume it may alias the
+// in-flight LDS-DMA and emit s_waitcnt vmcnt(0) before every transposed read, draining the
+// 8-phase prefetch (measured: NN 2.6x the wave-cycles of NT).  The asm result is only valid after
+// the explicit lgkmcnt(0) + sched_barrier of each phase (lds_sync below, guide §5.4 rule 18).
+// ds_read_b64_tr_b16 as inline asm: the builtin makes hipcc (ROCm 7.2) assume it may alias the
+// in-flight LDS-DMA and emit s_waitcnt vmcnt(0) before every transposed read, draining the
+// 8-phase prefetch (measured: NN 2.6x the wave-cycles of NT).  The asm result is only valid after
+// the explicit lgkmcnt(0) + sched_barrier of each phase (lds_sync below, guide §5.4 rule 18).
+__device__ __forceinline__ s16x4_t ds_tr16_asm(const bf16_t* p) {
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+  s16x4_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+
+// fragment of a swizzled [64 k][128] half-tile: lane holds T[k = 8*kc + 8*(l>>4) + j][c = r0 + (l&15)]
+// (the same register image frag8 produces from a K-contiguous tile)
+__device__ __forceinline__ bf16x8_t frag8_t(const bf16_t* t, int r0, int kc) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const int k = 8 * kc + 8 * g + q;        // rows k (lo) and k + 4 (hi)
+  const int col = r0 + 4 * p;              // 4 columns per lane of the 16-lane group
+  const int ch = col >> 3, off = col & 7;  // logical 16-B chunk, element offset inside it
+  const bf16_t* a0 = t + k * 128 + ((ch ^ tsw(k)) << 3) + off;
+  const bf16_t* a1 = t + (k + 4) * 128 + ((ch ^ tsw(k + 4)) << 3) + off;
+  s16x4_t lo = ds_tr16_asm(a0);
+  s16x4_t hi = ds_tr16_asm(a1);
+  s16x8_t r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
 // fragment of a swizzled half-tile: lane holds T[r0 + (l&15)][8*kc + 8*(l>>4) + j]
 __device__ __forceinline__ bf16x8_t frag8(const bf16_t* t, int r0, int kc) {
   const int l = threadIdx.x & 63;
@@ -85,25 +140,35 @@ __device__ unsigned long long* g8_stamps;
 #define G8_STAMP(k)
 #endif
 
-template <int EPI>
+template <int EPI, bool AT, bool BT>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   G8_STAMP(0);
   // buffer b (0 = even, 1 = odd): half-tiles A0, A1, B0, B1 at smem + (b * 4 + h) * kHalf
   const int tiles_n = (g.N + 255) / 256;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int ksplit = g.ksplit > 1 ? g.ksplit : 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid / ksplit, split = bid % ksplit;  // a tile's K-splits are neighbours (same XCD)
   const int m0 = (tile / tiles_n) * 256, n0 = (tile % tiles_n) * 256;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = w >> 2, wn = w & 3;  // wave's 64 x 32 piece inside each 128 x 128 quadrant
-  const int nk = g.K / 64;
-  const int last = nk - 1;
+  const int nk_all = g.K / 64;
+  const int kps = (nk_all + ksplit - 1) / ksplit;  // K-tiles per split
+  const int kbase = split * kps;
+  const int nk = max(0, min(nk_all - kbase, kps));
+  const int last = max(nk - 1, 0);
 
   auto half_ptr = [&](int buf, int h) { return smem + (buf * 4 + h) * kHalf; };
   // h: 0 = A0, 1 = A1, 2 = B0, 3 = B1
   auto stage = [&](int buf, int h, int kt) {
-    const int k0 = min(kt, last) * 64;
-    if (h < 2) stage_half(half_ptr(buf, h), g.A, g.lda, m0 + h * 128, g.M, k0);
-    else stage_half(half_ptr(buf, h), g.B, g.ldb, n0 + (h - 2) * 128, g.N, k0);
+    const int k0 = min(kbase + min(kt, last), nk_all - 1) * 64;  // an empty split still stores zeros
+    if (h < 2) {
+      if constexpr (AT) stage_half_t(half_ptr(buf, h), g.A, g.lda, m0 + h * 128, g.M, k0);
+      else stage_half(half_ptr(buf, h), g.A, g.lda, m0 + h * 128, g.M, k0);
+    } else {
+      if constexpr (BT) stage_half_t(half_ptr(buf, h), g.B, g.ldb, n0 + (h - 2) * 128, g.N, k0);
+      else stage_half(half_ptr(buf, h), g.B, g.ldb, n0 + (h - 2) * 128, g.N, k0);
+    }
   };
 
   f32x4_t acc[4][4][2];  // [quadrant][i][j]
@@ -120,14 +185,20 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) af[i][ks] = frag8(t, wm * 64 + i * 16, ks * 4);
+      for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (AT) af[i][ks] = frag8_t(t, wm * 64 + i * 16, ks * 4);
+        else af[i][ks] = frag8(t, wm * 64 + i * 16, ks * 4);
+      }
   };
   auto read_b = [&](int buf, int bh) {
     const bf16_t* t = half_ptr(buf, 2 + bh);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = frag8(t, wn * 32 + j * 16, ks * 4);
+      for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (BT) bfr[j][ks] = frag8_t(t, wn * 32 + j * 16, ks * 4);
+        else bfr[j][ks] = frag8(t, wn * 32 + j * 16, ks * 4);
+      }
   };
   auto mma = [&](int q) {
     __builtin_amdgcn_s_setprio(1);
@@ -138,6 +209,13 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[q][i][j] = mfma16(bfr[j][ks], af[i][ks], acc[q][i][j]);
     __builtin_amdgcn_s_setprio(0);
+  };
+
+  // end of a phase's fragment reads: every ds_read retired; with asm transposed reads the compiler
+  // must not move the MFMAs that consume them above this point
+  auto lds_sync = [&]() {
+    lgkm_wait0();
+    if constexpr (AT || BT) __builtin_amdgcn_sched_barrier(0);
   };
 
   // prologue: E <- K-tile 0 (all halves), O <- K-tile 1 (A0, B1); retire E
@@ -164,28 +242,28 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     read_a(0, 0);
     read_b(0, 0);
     stage(1, 1, kt + 1);
-    lgkm_wait0();
+    lds_sync();
     raw_barrier();
     mma(0);
     raw_barrier();
     // phase 2: (A0, B1); stage O.B0 (kt+1)
     read_b(0, 1);
     stage(1, 2, kt + 1);
-    lgkm_wait0();
+    lds_sync();
     raw_barrier();
     mma(1);
     raw_barrier();
     // phase 3: (A1, B1); stage E.A0 (kt+2)
     read_a(0, 1);
     stage(0, 0, kt + 2);
-    lgkm_wait0();
+    lds_sync();
     raw_barrier();
     mma(2);
     raw_barrier();
     // phase 4: (A1, B0); stage E.B1 (kt+2); retire the odd buffer
     read_b(0, 0);
     stage(0, 3, kt + 2);
-    lgkm_wait0();
+    lds_sync();
     vm_wait<4>();
     raw_barrier();
     mma(3);
@@ -195,28 +273,28 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     read_a(1, 0);
     read_b(1, 0);
     stage(0, 1, kt + 2);
-    lgkm_wait0();
+    lds_sync();
     raw_barrier();
     if (odd_ok) mma(0);
     raw_barrier();
     // phase 6: (A0, B1); stage E.B0 (kt+2)
     read_b(1, 1);
     stage(0, 2, kt + 2);
-    lgkm_wait0();
+    lds_sync();
     raw_barrier();
     if (odd_ok) mma(1);
     raw_barrier();
     // phase 7: (A1, B1); stage O.A0 (kt+3)
     read_a(1, 1);
     stage(1, 0, kt + 3);
-    lgkm_wait0();
+    lds_sync();
     raw_barrier();
     if (odd_ok) mma(2);
     raw_barrier();
     // phase 8: (A1, B0); stage O.B1 (kt+3); retire the even buffer
     read_b(1, 0);
     stage(1, 3, kt + 3);
-    lgkm_wait0();
+    lds_sync();
     vm_wait<4>();
     raw_barrier();
     if (odd_ok) mma(3);
@@ -282,6 +360,14 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
       const int row = rbase + i * 16 + (lane & 15);
       const bool ok = col_ok && row < g.M;
       float* v = o[i];
+      if constexpr (EPI == GEMM_EPI_F32PART) {  // split-K slab: plain fp32 store, reduced later
+        if (ok) {
+          float* P = g.ws + ((long)split * g.M + row) * g.N + col;
+          *reinterpret_cast<f32x4_t*>(P) = f32x4_t{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4_t*>(P + 4) = f32x4_t{v[4], v[5], v[6], v[7]};
+        }
+        continue;
+      }
       if constexpr (EPI == GEMM_EPI_F32ACC) {
         if (ok) {
           float* C = reinterpret_cast<float*>(g.C) + (long)row * g.ldc + col;
@@ -320,38 +406,101 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   G8_STAMP(3);
 }
 
-template <int EPI>
+template <int EPI, bool AT, bool BT>
 static void launch8(const GemmArgs& g, hipStream_t st) {
   constexpr size_t shm = sizeof(bf16_t) * 8 * kHalf;  // 128 KB
   static bool attr = false;
   if (!attr) {
-    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI, AT, BT>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     attr = true;
   }
   const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
-  gemm8_kernel<EPI><<<tiles, 512, shm, st>>>(g);
+  const int ks = g.ksplit > 1 ? g.ksplit : 1;
+  gemm8_kernel<EPI, AT, BT><<<tiles * ks, 512, shm, st>>>(g);
 }
 
-void gemm8(const GemmArgs& g, int epi, hipStream_t st) {
-  if (!gemm_supported(g.M, g.N, g.K)) {
-    fprintf(stderr, "mft::gemm8: unsupported shape M=%d N=%d K=%d\n", g.M, g.N, g.K);
+template <int EPI>
+static void launch8_layout(const GemmArgs& g, bool a_t, bool b_t, hipStream_t st) {
+  if (a_t && b_t) launch8<EPI, true, true>(g, st);
+  else if (b_t) launch8<EPI, false, true>(g, st);
+  else if (a_t) launch8<EPI, true, false>(g, st);
+  else launch8<EPI, false, false>(g, st);
+}
+
+// C (+)= alpha * sum_s ws[s]   (fp32, [M, N] slabs; deterministic split order)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int ksplit, long MN, int N,
+                                                            float* __restrict__ C, long ldc, float alpha, int accumulate) {
+  const long i4 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i4 * 4 >= MN) return;
+  const long i = i4 * 4;
+  f32x4_t s = *reinterpret_cast<const f32x4_t*>(ws + i);
+  for (int k = 1; k < ksplit; ++k) s += *reinterpret_cast<const f32x4_t*>(ws + (long)k * MN + i);
+  const long row = i / N, col = i % N;
+  float* c = C + row * ldc + col;
+  f32x4_t o = s * alpha;
+  if (accumulate) o += *reinterpret_cast<f32x4_t*>(c);
+  *reinterpret_cast<f32x4_t*>(c) = o;
+}
+
+void gemm_splitk_reduce(const float* ws, int ksplit, int M, int N, float* C, long ldc, float alpha, int accumulate,
+                        hipStream_t st) {
+  const long MN = (long)M * N;
+  splitk_reduce_kernel<<<(int)((MN / 4 + 255) / 256), 256, 0, st>>>(ws, ksplit, MN, N, C, ldc, alpha, accumulate);
+}
+
+int gemm8_pick_ksplit(int M, int N, int K) {
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int nk = K / 64;
+  int ks = 1;
+  // fill the 256 CUs: split the K (token) dimension while tiles are few and each split keeps >= 16
+  // K-tiles (the 8-phase pipeline's prologue/epilogue amortised)
+  while (tiles * ks * 2 <= 320 && nk / (ks * 2) >= 16) ks *= 2;
+  return ks;
+}
+
+bool gemm8_supported(int M, int N, int K, bool a_t, bool b_t) {
+  if (K % 64 || K <= 0 || M <= 0 || N < 8 || N % 8) return false;
+  if (a_t && (M % 8 || M < 8)) return false;
+  return true;
+}
+
+void gemm8x(const GemmArgs& g0, int epi, bool a_t, bool b_t, hipStream_t st) {
+  GemmArgs g = g0;
+  if (!gemm8_supported(g.M, g.N, g.K, a_t, b_t)) {
+    fprintf(stderr, "mft::gemm8: unsupported shape M=%d N=%d K=%d (a_t=%d b_t=%d)\n", g.M, g.N, g.K, a_t, b_t);
     abort();
   }
   switch (epi) {
-    case GEMM_EPI_NONE: launch8<GEMM_EPI_NONE>(g, st); break;
-    case GEMM_EPI_BIAS: launch8<GEMM_EPI_BIAS>(g, st); break;
-    case GEMM_EPI_BIAS_GELU: launch8<GEMM_EPI_BIAS_GELU>(g, st); break;
-    case GEMM_EPI_DGELU: launch8<GEMM_EPI_DGELU>(g, st); break;
-    case GEMM_EPI_F32ACC: launch8<GEMM_EPI_F32ACC>(g, st); break;
+    case GEMM_EPI_NONE: launch8_layout<GEMM_EPI_NONE>(g, a_t, b_t, st); break;
+    case GEMM_EPI_BIAS: launch8_layout<GEMM_EPI_BIAS>(g, a_t, b_t, st); break;
+    case GEMM_EPI_BIAS_GELU: launch8_layout<GEMM_EPI_BIAS_GELU>(g, a_t, b_t, st); break;
+    case GEMM_EPI_DGELU: launch8_layout<GEMM_EPI_DGELU>(g, a_t, b_t, st); break;
+    case GEMM_EPI_F32ACC:
+      // fp32 weight-gradient accumulate: split over K into slabs (g.ws, ksplit * M * N floats) when
+      // the output has few tiles, then one deterministic reduce into C; else accumulate in place
+      if (g.ksplit > 1) {
+        if (!g.ws) {
+          fprintf(stderr, "mft::gemm8: split-K needs a workspace\n");
+          abort();
+        }
+        launch8_layout<GEMM_EPI_F32PART>(g, a_t, b_t, st);
+        gemm_splitk_reduce(g.ws, g.ksplit, g.M, g.N, reinterpret_cast<float*>(g.C), g.ldc, g.alpha, 1, st);
+      } else {
+        launch8_layout<GEMM_EPI_F32ACC>(g, a_t, b_t, st);
+      }
+      break;
     case GEMM_EPI_LORA:
       if (g.lora_r <= 0 || g.lora_r > 32 || g.lora_r % 8 || g.ld_lu % 8) {
         fprintf(stderr, "mft::gemm8: LoRA epilogue needs rank %% 8 == 0, <= 32 (got %d)\n", g.lora_r);
         abort();
       }
-      launch8<GEMM_EPI_LORA>(g, st);
+      launch8_layout<GEMM_EPI_LORA>(g, a_t, b_t, st);
       break;
     default: fprintf(stderr, "mft::gemm8: bad epilogue %d\n", epi); abort();
   }
 }
+
+void gemm8(const GemmArgs& g, int epi, hipStream_t st) { gemm8x(g, epi, false, false, st); }
 
 }  // namespace mft
