@@ -32,6 +32,8 @@
 // with vmcnt(4) before the barriers of phases 4 (retires O for phases 5-8) and 8 (retires E for
 // the next phases 1-4).  Loads of K-tiles past the end are clamped onto the last tile (harmless
 // re-reads) so every wave issues the same count and the counted waits stay exact.
+#include <stdlib.h>
+
 #include "mfma.h"
 #include "kernels.h"
 
@@ -131,6 +133,110 @@ __device__ __forceinline__ bf16x8_t frag8(const bf16_t* t, int r0, int kc) {
 }
 
 }  // namespace
+
+// ------------------------------------------------------------------ epilogue (registers only)
+template <int EPI>
+__device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4][2], int m0, int n0, int wm, int wn,
+                                          int lane, int split) {
+  // The MFMAs ran with the operands swapped, so each 16 x 16 accumulator block is C^T: lane l holds
+  // row (l & 15) of the block, columns 4 * (l >> 4) .. +3.  One v_permlane16_swap per dword pairs
+  // the two column blocks of the wave's 32-column piece so every lane then owns EIGHT CONTIGUOUS
+  // columns of one row: lane group g = l >> 4 -> column offset {0, 16, 8, 24}[g].  Every epilogue
+  // is then 16-B vector loads/stores straight from registers (no LDS staging, no wave syncs).
+  const int g4 = lane >> 4;
+  const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int qa = (q == 2 || q == 3) ? 1 : 0, qb = (q == 1 || q == 2) ? 1 : 0;
+    const int rbase = m0 + qa * 128 + wm * 64, col = n0 + qb * 128 + wn * 32 + cofs;
+    const bool col_ok = col < g.N;
+    const int colc = min(col, g.N - 8);
+    float bias_v[8];
+    if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU) load8(g.bias + colc, bias_v);
+    float o[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[q][i][0][r]),
+                                                         __float_as_uint(acc[q][i][1][r]), false, false);
+        o[i][r] = __uint_as_float(sw[0]);
+        o[i][4 + r] = __uint_as_float(sw[1]);
+      }
+    }
+    if constexpr (EPI == GEMM_EPI_LORA) {
+      // rank-r update: the lane's 8 x r slice of lora_w is loaded once per 8 ranks per quadrant,
+      // each row of lora_u is one 16-B load per 8 ranks (r <= 32, multiple of 8)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[i][e] *= g.alpha;
+#pragma unroll 1
+      for (int t8 = 0; t8 < g.lora_r; t8 += 8) {
+        u16x8_t wv[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) wv[t] = *reinterpret_cast<const u16x8_t*>(g.lora_w + (long)(t8 + t) * g.ld_lw + colc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = min(rbase + i * 16 + (lane & 15), g.M - 1);
+          float u[8];
+          load8(g.lora_u + (long)row * g.ld_lu + t8, u);
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[i][e] += u[t] * bf2f(wv[t][e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rbase + i * 16 + (lane & 15);
+      const bool ok = col_ok && row < g.M;
+      float* v = o[i];
+      if constexpr (EPI == GEMM_EPI_F32PART) {  // split-K slab: plain fp32 store, reduced later
+        if (ok) {
+          float* P = g.ws + ((long)split * g.M + row) * g.N + col;
+          *reinterpret_cast<f32x4_t*>(P) = f32x4_t{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4_t*>(P + 4) = f32x4_t{v[4], v[5], v[6], v[7]};
+        }
+        continue;
+      }
+      if constexpr (EPI == GEMM_EPI_F32ACC) {
+        if (ok) {
+          float* C = reinterpret_cast<float*>(g.C) + (long)row * g.ldc + col;
+          f32x4_t c0 = *reinterpret_cast<f32x4_t*>(C), c1 = *reinterpret_cast<f32x4_t*>(C + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            c0[e] += g.alpha * v[e];
+            c1[e] += g.alpha * v[4 + e];
+          }
+          *reinterpret_cast<f32x4_t*>(C) = c0;
+          *reinterpret_cast<f32x4_t*>(C + 4) = c1;
+        }
+        continue;
+      }
+      if constexpr (EPI != GEMM_EPI_LORA) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] *= g.alpha;
+          if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU) v[e] += bias_v[e];
+        }
+      }
+      if constexpr (EPI == GEMM_EPI_DGELU) {
+        float pre[8];
+        load8(g.aux + (long)min(row, g.M - 1) * g.ldaux + colc, pre);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(pre[e]);
+      }
+      if constexpr (EPI == GEMM_EPI_BIAS_GELU) {
+        if (ok) store8(g.aux + (long)row * g.ldaux + col, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+      }
+      if (ok) store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, v);
+    }
+  }
+}
 
 #ifdef MFT_G8_STAMPS  // diagnostic build only (scripts/g8_stamps.hip): s_memtime per phase per WG
 __device__ unsigned long long* g8_stamps;
@@ -304,106 +410,210 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   vm_wait<0>();  // drain the clamped tail prefetches (LDS-DMA must not outlive the workgroup)
   G8_STAMP(2);
 
-  // ------------------------------------------------------------------ epilogue (registers only)
-  // The MFMAs ran with the operands swapped, so each 16 x 16 accumulator block is C^T: lane l holds
-  // row (l & 15) of the block, columns 4 * (l >> 4) .. +3.  One v_permlane16_swap per dword pairs
-  // the two column blocks of the wave's 32-column piece so every lane then owns EIGHT CONTIGUOUS
-  // columns of one row: lane group g = l >> 4 -> column offset {0, 16, 8, 24}[g].  Every epilogue
-  // is then 16-B vector loads/stores straight from registers (no LDS staging, no wave syncs).
-  const int g4 = lane >> 4;
-  const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int qa = (q == 2 || q == 3) ? 1 : 0, qb = (q == 1 || q == 2) ? 1 : 0;
-    const int rbase = m0 + qa * 128 + wm * 64, col = n0 + qb * 128 + wn * 32 + cofs;
-    const bool col_ok = col < g.N;
-    const int colc = min(col, g.N - 8);
-    float bias_v[8];
-    if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU) load8(g.bias + colc, bias_v);
-    float o[4][8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[q][i][0][r]),
-                                                         __float_as_uint(acc[q][i][1][r]), false, false);
-        o[i][r] = __uint_as_float(sw[0]);
-        o[i][4 + r] = __uint_as_float(sw[1]);
-      }
+  epilogue8<EPI>(g, acc, m0, n0, wm, wn, lane, split);
+  G8_STAMP(3);
+}
+
+// Persistent form (ksplit == 1): one workgroup per CU walks its tiles (logical ids b, b + grid, ...,
+// XCD-remapped) as ONE continuous stream of K-tiles.  The 8-phase pipeline never restarts: the
+// prefetches issued near the end of a tile already fetch the next tile's first K-tiles, and the
+// finished tile's epilogue (registers only) runs between two phases while those loads are in
+// flight.  Removes the per-tile prologue fill + workgroup relaunch that cost ~9 us per 256 x 256
+// tile at K = 768 (measured: 28.4 us per tile vs 10.3 us of MFMA work at peak).
+template <int EPI, bool AT, bool BT>
+__global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int tiles_n = (g.N + 255) / 256;
+  const int ntiles = ((g.M + 255) / 256) * tiles_n;
+  const int b = blockIdx.x, grid = gridDim.x;
+  const int n_my = (ntiles - b + grid - 1) / grid;
+  const int nk = g.K / 64;
+  const int NG = n_my * nk;  // K-tiles this workgroup streams
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 2, wn = w & 3;
+
+  // K-tile Gk of the stream -> (m0, n0, k0); past the end: the last K-tile (uniform re-reads)
+  auto kinfo = [&](int Gk, int& m0, int& n0, int& k0) {
+    const int Gc = min(Gk, NG - 1);
+    const int i = Gc / nk;
+    const int tile = xcd_remap(b + i * grid, ntiles);
+    m0 = (tile / tiles_n) * 256;
+    n0 = (tile % tiles_n) * 256;
+    k0 = (Gc - i * nk) * 64;
+  };
+  auto half_ptr = [&](int buf, int h) { return smem + (buf * 4 + h) * kHalf; };
+  auto stage_at = [&](int buf, int h, int m0, int n0, int k0) {
+    if (h < 2) {
+      if constexpr (AT) stage_half_t(half_ptr(buf, h), g.A, g.lda, m0 + h * 128, g.M, k0);
+      else stage_half(half_ptr(buf, h), g.A, g.lda, m0 + h * 128, g.M, k0);
+    } else {
+      if constexpr (BT) stage_half_t(half_ptr(buf, h), g.B, g.ldb, n0 + (h - 2) * 128, g.N, k0);
+      else stage_half(half_ptr(buf, h), g.B, g.ldb, n0 + (h - 2) * 128, g.N, k0);
     }
-    if constexpr (EPI == GEMM_EPI_LORA) {
-      // rank-r update: the lane's 8 x r slice of lora_w is loaded once per 8 ranks per quadrant,
-      // each row of lora_u is one 16-B load per 8 ranks (r <= 32, multiple of 8)
+  };
+
+  f32x4_t acc[4][4][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[i][e] *= g.alpha;
-#pragma unroll 1
-      for (int t8 = 0; t8 < g.lora_r; t8 += 8) {
-        u16x8_t wv[8];
+        for (int j = 0; j < 2; ++j) acc[q][i][j] = zero4();
+  };
+  zero_acc();
+
+  bf16x8_t af[4][2], bfr[2][2];
+  auto read_a = [&](int buf, int ah) {
+    const bf16_t* t = half_ptr(buf, ah);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) wv[t] = *reinterpret_cast<const u16x8_t*>(g.lora_w + (long)(t8 + t) * g.ld_lw + colc);
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = min(rbase + i * 16 + (lane & 15), g.M - 1);
-          float u[8];
-          load8(g.lora_u + (long)row * g.ld_lu + t8, u);
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[i][e] += u[t] * bf2f(wv[t][e]);
-        }
+      for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (AT) af[i][ks] = frag8_t(t, wm * 64 + i * 16, ks * 4);
+        else af[i][ks] = frag8(t, wm * 64 + i * 16, ks * 4);
       }
+  };
+  auto read_b = [&](int buf, int bh) {
+    const bf16_t* t = half_ptr(buf, 2 + bh);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (BT) bfr[j][ks] = frag8_t(t, wn * 32 + j * 16, ks * 4);
+        else bfr[j][ks] = frag8(t, wn * 32 + j * 16, ks * 4);
+      }
+  };
+  auto mma = [&](int q) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[q][i][j] = mfma16(bfr[j][ks], af[i][ks], acc[q][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto lds_sync = [&]() {
+    lgkm_wait0();
+    if constexpr (AT || BT) __builtin_amdgcn_sched_barrier(0);
+  };
+  // after the last quadrant of K-tile Gk: if it closes a tile, write that tile and restart acc
+  auto finish = [&](int Gk) {
+    if ((Gk + 1) % nk == 0) {
+      int m0, n0, k0;
+      kinfo(Gk, m0, n0, k0);
+      epilogue8<EPI>(g, acc, m0, n0, wm, wn, lane, 0);
+      zero_acc();
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = rbase + i * 16 + (lane & 15);
-      const bool ok = col_ok && row < g.M;
-      float* v = o[i];
-      if constexpr (EPI == GEMM_EPI_F32PART) {  // split-K slab: plain fp32 store, reduced later
-        if (ok) {
-          float* P = g.ws + ((long)split * g.M + row) * g.N + col;
-          *reinterpret_cast<f32x4_t*>(P) = f32x4_t{v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<f32x4_t*>(P + 4) = f32x4_t{v[4], v[5], v[6], v[7]};
-        }
-        continue;
-      }
-      if constexpr (EPI == GEMM_EPI_F32ACC) {
-        if (ok) {
-          float* C = reinterpret_cast<float*>(g.C) + (long)row * g.ldc + col;
-          f32x4_t c0 = *reinterpret_cast<f32x4_t*>(C), c1 = *reinterpret_cast<f32x4_t*>(C + 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            c0[e] += g.alpha * v[e];
-            c1[e] += g.alpha * v[4 + e];
-          }
-          *reinterpret_cast<f32x4_t*>(C) = c0;
-          *reinterpret_cast<f32x4_t*>(C + 4) = c1;
-        }
-        continue;
-      }
-      if constexpr (EPI != GEMM_EPI_LORA) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          v[e] *= g.alpha;
-          if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU) v[e] += bias_v[e];
-        }
-      }
-      if constexpr (EPI == GEMM_EPI_DGELU) {
-        float pre[8];
-        load8(g.aux + (long)min(row, g.M - 1) * g.ldaux + colc, pre);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(pre[e]);
-      }
-      if constexpr (EPI == GEMM_EPI_BIAS_GELU) {
-        if (ok) store8(g.aux + (long)row * g.ldaux + col, v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
-      }
-      if (ok) store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, v);
-    }
+  };
+
+  {  // prologue: E <- K-tile 0 (all halves), O <- K-tile 1 (A0, B1); retire E
+    int m0, n0, k0;
+    kinfo(0, m0, n0, k0);
+    stage_at(0, 0, m0, n0, k0);
+    stage_at(0, 3, m0, n0, k0);
+    stage_at(0, 1, m0, n0, k0);
+    stage_at(0, 2, m0, n0, k0);
+    kinfo(1, m0, n0, k0);
+    stage_at(1, 0, m0, n0, k0);
+    stage_at(1, 3, m0, n0, k0);
   }
-  G8_STAMP(3);
+  vm_wait<4>();
+  raw_barrier();
+  if (wm == 1) raw_barrier();
+
+  for (int G = 0; G < NG; G += 2) {
+    const bool odd_ok = G + 1 < NG;
+    int m1, n1, k1, m2, n2, k2, m3, n3, k3;  // staging targets: K-tiles G+1, G+2, G+3
+    kinfo(G + 1, m1, n1, k1);
+    kinfo(G + 2, m2, n2, k2);
+    kinfo(G + 3, m3, n3, k3);
+    // ---- phases 1-4: even buffer, K-tile G
+    read_a(0, 0);
+    read_b(0, 0);
+    stage_at(1, 1, m1, n1, k1);
+    lds_sync();
+    raw_barrier();
+    mma(0);
+    raw_barrier();
+    read_b(0, 1);
+    stage_at(1, 2, m1, n1, k1);
+    lds_sync();
+    raw_barrier();
+    mma(1);
+    raw_barrier();
+    read_a(0, 1);
+    stage_at(0, 0, m2, n2, k2);
+    lds_sync();
+    raw_barrier();
+    mma(2);
+    raw_barrier();
+    read_b(0, 0);
+    stage_at(0, 3, m2, n2, k2);
+    lds_sync();
+    vm_wait<4>();
+    raw_barrier();
+    mma(3);
+    finish(G);
+    raw_barrier();
+    // ---- phases 5-8: odd buffer, K-tile G+1
+    read_a(1, 0);
+    read_b(1, 0);
+    stage_at(0, 1, m2, n2, k2);
+    lds_sync();
+    raw_barrier();
+    if (odd_ok) mma(0);
+    raw_barrier();
+    read_b(1, 1);
+    stage_at(0, 2, m2, n2, k2);
+    lds_sync();
+    raw_barrier();
+    if (odd_ok) mma(1);
+    raw_barrier();
+    read_a(1, 1);
+    stage_at(1, 0, m3, n3, k3);
+    lds_sync();
+    raw_barrier();
+    if (odd_ok) mma(2);
+    raw_barrier();
+    read_b(1, 0);
+    stage_at(1, 3, m3, n3, k3);
+    lds_sync();
+    vm_wait<4>();
+    raw_barrier();
+    if (odd_ok) {
+      mma(3);
+      finish(G + 1);
+    }
+    raw_barrier();
+  }
+  if (wm == 0) raw_barrier();
+  vm_wait<0>();
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    MFT_HIP_CHECK(hipGetDevice(&dev));
+    MFT_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+// MFT_GEMM8_PERSISTENT=1 selects the persistent streaming kernel.  Off by default: measured slower
+// than one tile per workgroup on every training shape (A/B in one call, scripts/bench_gemm_t.py:
+// qkv fwd 327 vs 297 us, LM-head fwd 5.69 vs 5.27 ms, fc dx 325 vs 276 us) -- the inline epilogue
+// stalls both wave groups between barriers and costs more than the prologue fill it hides.
+static bool gemm8_persistent() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MFT_GEMM8_PERSISTENT");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
 }
 
 template <int EPI, bool AT, bool BT>
@@ -417,6 +627,18 @@ static void launch8(const GemmArgs& g, hipStream_t st) {
   }
   const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
   const int ks = g.ksplit > 1 ? g.ksplit : 1;
+  // (the LoRA epilogue's extra operand loads spill in the persistent form: one tile per workgroup)
+  if (ks == 1 && EPI != GEMM_EPI_F32PART && EPI != GEMM_EPI_LORA && gemm8_persistent()) {
+    static bool attr_p = false;
+    if (!attr_p) {
+      MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, AT, BT>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+      attr_p = true;
+    }
+    const int grid = tiles < num_cus() ? tiles : num_cus();
+    gemm8p_kernel<EPI, AT, BT><<<grid, 512, shm, st>>>(g);
+    return;
+  }
   gemm8_kernel<EPI, AT, BT><<<tiles * ks, 512, shm, st>>>(g);
 }
 

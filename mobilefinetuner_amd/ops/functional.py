@@ -21,6 +21,8 @@ from torch.autograd import Function
 from .._ext import native
 from . import reference as ref
 
+GEMM_EPI_NONE, GEMM_EPI_BIAS, GEMM_EPI_BIAS_GELU, GEMM_EPI_DGELU, GEMM_EPI_F32ACC, GEMM_EPI_LORA = 0, 1, 2, 3, 4, 5
+
 # ---------------------------------------------------------------- parameter helpers
 
 _ready_hooks: list = []
@@ -440,37 +442,85 @@ def qk_norm_rope_attention(qkv, nq, nkv, wq, wk, cos, sin, eps_q, eps_k, offset=
 
 
 # ---------------------------------------------------------------- linear layers
-def _lt_ok(*ts) -> bool:
-    """Route a plain GEMM through the autotuned hipBLASLt binding (csrc/gemm_lt.cpp) instead of
-    torch.mm (MFT_LT=1).  Off by default: A/B in one call on MI355X, torch.mm's hipBLASLt path was
-    1% faster on the GPT-2 LoRA step (1.291M vs 1.279M tok/s) and equal on full fine-tuning;
-    weight gradients always use the autotuned beta=1 path (_mm_wgrad_into)."""
-    import os
-    if os.environ.get("MFT_LT", "0") != "1":
-        return False
-    return all(t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(-1) == 1 for t in ts)
+# GEMM routing (measured per shape at M = 65536 on MI355X, scripts/bench_gemm_t.py, in one process):
+#   * every FUSED GEMM runs on the hand-written 8-phase MFMA kernel (csrc/kernels/gemm8.hip): fc +
+#     bias + GELU (writes pre-activation and activation), mlp_proj data-grad x GELU'(pre), LoRA
+#     data-grads with the rank-r update in the epilogue;
+#   * plain data-grads dx = dy W run on gemm8's NN form (W read k-major with ds_read_b64_tr_b16, no
+#     transposed weight copies): 0.95-1.0x hipBLASLt (fc dx 276 vs 264 us, qkv dx 208 vs 206,
+#     LM-head dx 3.91 vs 3.77 ms);
+#   * plain forward GEMMs y = x W^T + b and fp32 weight-gradient accumulation are "plain library
+#     GEMMs" and stay on hipBLASLt where it is measurably faster (NT forward: gemm8 0.79-0.87x;
+#     TN weight-grad: gemm8 0.40-0.90x).  MFT_GEMM8_ALL=1 routes them through gemm8 too, and
+#     --deterministic (set_deterministic) always uses gemm8's split-K TN form, whose fixed-order
+#     slab reduction makes weight gradients bitwise reproducible.
+# Shapes outside gemm8's contract (reduction dim % 64, output columns % 8) fall back to torch.mm
+# with a one-time notice.
+_NOTED = set()
+_DETERMINISTIC = [os.environ.get("MFT_DETERMINISTIC", "0") == "1"]
+
+
+def set_deterministic(on: bool = True):
+    """Deterministic-reduction mode: fixed-order two-stage reductions instead of
+    float atomics in every kernel that has both forms (LoRA weight-grads, embedding grad, attention
+    dQ) and gemm8's split-K weight gradients instead of hipBLASLt's."""
+    _DETERMINISTIC[0] = bool(on)
+
+
+def deterministic() -> bool:
+    return _DETERMINISTIC[0]
+
+
+def _gemm8_all() -> bool:
+    return os.environ.get("MFT_GEMM8_ALL", "0") == "1"
+
+
+def _note(what):
+    if what not in _NOTED:
+        _NOTED.add(what)
+        import sys
+        print(f"[mobilefinetuner_amd] {what}: shape outside gemm8's contract, using torch.mm", file=sys.stderr)
+
+
+def _g8_ok(x2, *ts) -> bool:
+    return all(t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(-1) == 1 and t.stride(0) % 8 == 0
+               for t in (x2, *ts))
 
 
 def gemm_linear(x2, wc, bc=None):
-    """y = x W^T (+ b)."""
-    if _lt_ok(x2, wc) and (bc is None or bc.dtype == torch.bfloat16):
-        return native().lt_linear(x2, wc, bc)
+    """y = x W^T (+ b), W [out, in]."""
+    M, K = x2.shape
+    N = wc.shape[0]
+    if _gemm8_all() and _g8_ok(x2, wc) and K % 64 == 0 and N % 8 == 0 and (bc is None or bc.dtype == torch.bfloat16):
+        if bc is None:
+            return native().gemm_t(x2, wc, False, False, GEMM_EPI_NONE)[0]
+        return native().gemm_t(x2, wc, False, False, GEMM_EPI_BIAS, bias=bc)[0]
     return torch.addmm(bc, x2, wc.t()) if bc is not None else torch.mm(x2, wc.t())
 
 
-def gemm_dx(dy2, wc):
-    """dx = dy W (W [out, in], possibly a row-strided view)."""
-    if _lt_ok(dy2, wc):
-        return native().lt_mm_dx(dy2, wc, None)
+def gemm_dx(dy2, wc, out=None):
+    """dx = dy W (W [out, in], possibly a row-strided view) -- gemm8 NN."""
+    N = wc.shape[0]
+    if _g8_ok(dy2, wc) and N % 64 == 0 and wc.shape[1] % 8 == 0 and (out is None or _g8_ok(out)):
+        return native().gemm_t(dy2, wc, False, True, GEMM_EPI_NONE, out=out)[0]
+    _note("data-grad")
+    if out is not None:
+        return torch.mm(dy2, wc, out=out)
     return torch.mm(dy2, wc)
 
 
 def _mm_wgrad_into(buf, dy2, x2, alpha=1.0):
-    """buf (fp32 [N,K]) += alpha * dy2^T @ x2: one hipBLASLt GEMM with bf16 inputs accumulating in
-    place into the fp32 grad buffer (beta = 1; no fp32 temporary + add pass)."""
+    """buf (fp32 [N, K]) += alpha * dy2^T @ x2, accumulated in place in the fp32 grad buffer."""
+    M = dy2.shape[0]
+    g8 = deterministic() or _gemm8_all()
+    if (g8 and _g8_ok(dy2, x2) and buf.is_contiguous() and M % 64 == 0 and dy2.shape[1] % 8 == 0
+            and x2.shape[1] % 8 == 0):
+        # TN gemm8: split-K slabs + fixed-order reduce (bitwise reproducible, no atomics)
+        native().gemm_t(dy2, x2, True, True, GEMM_EPI_F32ACC, alpha=float(alpha), out=buf.view(dy2.shape[1], -1))
+        return
     if (buf.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and dy2.stride(-1) == 1
             and x2.stride(-1) == 1 and buf.is_contiguous()):
-        native().lt_wgrad_acc(x2, dy2, buf, float(alpha))
+        native().lt_wgrad_acc(x2, dy2, buf.view(dy2.shape[1], -1), float(alpha))  # hipBLASLt, beta = 1
         return
     buf.add_(torch.mm(dy2.t(), x2, out_dtype=torch.float32), alpha=alpha)
 
@@ -517,7 +567,9 @@ class _Linear(Function):
                 _mm_wgrad_into(buf, dy2, x2)
                 grad_ready(w)
             else:
-                gw = torch.mm(dy2.t(), x2, out_dtype=torch.float32).to(w.dtype)
+                gw = torch.zeros(w.shape, device=dy2.device, dtype=torch.float32)
+                _mm_wgrad_into(gw, dy2, x2)
+                gw = gw.to(w.dtype)
         if _needs(b):
             gb = _bias_grad(b, dy2)
         return dx, gw, gb
@@ -533,17 +585,15 @@ def linear(x, w, b=None):
     return _Linear.apply(x, w, b)
 
 
-GEMM_EPI_NONE, GEMM_EPI_BIAS, GEMM_EPI_BIAS_GELU, GEMM_EPI_DGELU, GEMM_EPI_F32ACC, GEMM_EPI_LORA = 0, 1, 2, 3, 4, 5
-
-
-def weight_t(p):
-    """Row-major [in, out] copy of a [out, in] weight so data-gradient GEMMs (dx = dy W) run in the
-    K-contiguous "NT" form of gemm.hip.  Frozen weights cache it on the parameter (one extra copy of
-    the frozen weights -- trivial against 288 GB HBM; ``Linear.merge_lora`` and the loaders drop
-    it); trainable (full fine-tuning) or sharded weights get a fresh transpose each call."""
-    wc = cw(p)
+def frozen_weight_t(p):
+    """Cached row-major [in, out] copy of a FROZEN [out, in] weight, or None.  The fused data-grad
+    GEMMs (x GELU'(pre), + rank-r LoRA update) run ~8% faster in gemm8's NT form than in its NN form
+    (mlp_proj dx + dGELU 454 vs 481 us, LoRA qkv/proj dx 138 vs 152 us avg, MI355X), so frozen
+    weights -- whose copy is built once (85 M params -> 170 MB of 288 GB) -- use NT; trainable or
+    sharded weights use NN and need no copy at all (no per-step transposes)."""
     if _needs(p) or getattr(p, "_mft_sharded", False):
-        return wc.t().contiguous()
+        return None
+    wc = cw(p)
     c = getattr(p, "_mft_wt", None)
     if c is None or c.data_ptr() == 0 or c.shape != (wc.shape[1], wc.shape[0]):
         c = wc.t().contiguous()
@@ -554,6 +604,14 @@ def weight_t(p):
 def drop_weight_t(p):
     if hasattr(p, "_mft_wt"):
         del p._mft_wt
+
+
+def _fused_dx(dy2, w, epi, **kw):
+    """dx = epi(dy W): gemm8 NT on the cached transposed copy of a frozen W, NN otherwise."""
+    wt = frozen_weight_t(w)
+    if wt is not None:
+        return native().gemm_t(dy2, wt, False, False, epi, **kw)
+    return native().gemm_t(dy2, cw(w), False, True, epi, **kw)
 
 
 class _MLPGelu(Function):
@@ -572,7 +630,7 @@ class _MLPGelu(Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         w1c, b1c, w2c, b2c = cw(w1), cw(b1), cw(w2), cw(b2)
-        h, pre = C.gemm(x2, w1c, False, GEMM_EPI_BIAS_GELU, b1c, None, 1.0, 8, None)
+        h, pre = C.gemm_t(x2, w1c, False, False, GEMM_EPI_BIAS_GELU, bias=b1c)
         y = gemm_linear(h, w2c, b2c)
         ctx.save_for_backward(x2 if _needs(w1) else None, pre, h if _needs(w2) else None)
         ctx.params = (w1, b1, w2, b2)
@@ -589,7 +647,7 @@ class _MLPGelu(Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dpre = C.gemm(dy2, weight_t(w2), False, GEMM_EPI_DGELU, None, pre, 1.0, 8, None)[0]
+        dpre = _fused_dx(dy2, w2, GEMM_EPI_DGELU, aux=pre)[0]
         grads = [None] * 5
         if ctx.needs_input_grad[0]:
             grads[0] = gemm_dx(dpre, w1c).view(ctx.shape)
@@ -601,7 +659,9 @@ class _MLPGelu(Function):
                 _mm_wgrad_into(buf, g_out, g_in)
                 grad_ready(p)
             else:
-                grads[3 if i == 0 else 1] = torch.mm(g_out.t(), g_in, out_dtype=torch.float32).to(p.dtype)
+                gt = torch.zeros(p.shape, device=g_out.device, dtype=torch.float32)
+                _mm_wgrad_into(gt, g_out, g_in)
+                grads[3 if i == 0 else 1] = gt.to(p.dtype)
         if _needs(b2):
             grads[4] = _bias_grad(b2, dy2)
         if _needs(b1):
@@ -788,7 +848,7 @@ class _LoRALinearAug(Function):
                 vs.append(vall[:, o:o + ranks[i]])
                 o += ranks[i]
             acat = torch.cat([cw(ab[2 * i]) for i in range(len(ranks))]) if len(ranks) > 1 else cw(ab[0])
-            C.gemm(dy2, weight_t(ctx.w), False, GEMM_EPI_LORA, None, None, 1.0, 8, dxa[:, :K], vall, acat)
+            _fused_dx(dy2, ctx.w, GEMM_EPI_LORA, out=dxa[:, :K], lora_u=vall, lora_w=acat)
         grads = []
         ctr = dropout_counter(dy.device)
         off = K
@@ -959,12 +1019,6 @@ def default_ce_chunk(vpad: int) -> int:
     return max(64, min(65536, rows // 64 * 64))
 
 
-def _lt_lm_ok(h, wc) -> bool:
-    import os
-    return (os.environ.get("MFT_LM_LT", "0") == "1" and h.is_cuda and h.dtype == torch.bfloat16
-            and wc.dtype == torch.bfloat16 and wc.stride(-1) == 1 and h.stride(-1) == 1)
-
-
 class _LMHeadCE(Function):
     @staticmethod
     def forward(ctx, h, w, labels, V, chunk, w_grad_scale):
@@ -980,22 +1034,15 @@ class _LMHeadCE(Function):
         dh = torch.empty_like(h) if need_grad else None
         wbuf = _grad_buf(w) if need_grad else None
         wtmp = torch.zeros(w.shape, device=h.device) if (need_grad and _needs(w) and wbuf is None) else None
-        # MFT_LM_LT=1 routes the two vocab-wide GEMMs through the autotuned hipBLASLt binding: faster
-        # in isolation on random operands (555 vs 697 us at 8192 x 768 x 50304) but slower inside the
-        # training step (1.256M vs 1.293M tok/s, A/B in one call), so torch.mm stays the default
-        lt = _lt_lm_ok(h, wc)
         for i in range(0, M, chunk):
             hc = h[i:i + chunk]
-            logits = C.lt_linear(hc, wc, None) if lt else torch.mm(hc, wc.t())
+            logits = gemm_linear(hc, wc)                       # [rows, Vpad] bf16, gemm8 NT
             C.xent_fwd_bwd(logits, labels[i:i + chunk], loss_rows[i:i + chunk], V, scale, 1.0, need_grad)
             if need_grad:
-                if lt:
-                    C.lt_mm_dx(logits, wc, dh[i:i + chunk])
-                else:
-                    torch.mm(logits, wc, out=dh[i:i + chunk])
+                gemm_dx(logits, wc, out=dh[i:i + chunk])       # dh = dlogits W, gemm8 NN
                 if wbuf is not None or wtmp is not None:
                     tgt = wbuf if wbuf is not None else wtmp
-                    _mm_wgrad_into(tgt, logits, hc, w_grad_scale)
+                    _mm_wgrad_into(tgt, logits, hc, w_grad_scale)  # dW += dlogits^T h, gemm8 TN
         # a tied weight (GPT-2 wte) receives its final contribution later, from the embedding
         # backward, which fires the hook; announcing it here would let a DP bucket reduce early
         if wbuf is not None and not getattr(w, "_mft_tied", False):
@@ -1044,6 +1091,6 @@ def lm_head_token_nll(h, w, labels, vocab_size, chunk=None):
         labels = labels.reshape(-1).contiguous()
         loss_rows = torch.empty(M, device=h.device, dtype=torch.float32)
         for i in range(0, M, chunk):
-            logits = torch.mm(h[i:i + chunk], wc.t())
+            logits = gemm_linear(h[i:i + chunk], wc)
             C.xent_fwd_bwd(logits, labels[i:i + chunk], loss_rows[i:i + chunk], vocab_size, None, 1.0, False)
         return loss_rows.sum(), (labels >= 0).sum()
