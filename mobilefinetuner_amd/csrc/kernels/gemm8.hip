@@ -240,8 +240,13 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4
 
 #ifdef MFT_G8_STAMPS  // diagnostic build only (scripts/g8_stamps.hip): s_memtime per phase per WG
 __device__ unsigned long long* g8_stamps;
+#ifdef MFT_G8_STAMPS_RT  // 100 MHz constant clock instead of the shader clock
+#define G8_STAMP(k) \
+  if (threadIdx.x == 0) g8_stamps[blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
 #define G8_STAMP(k) \
   if (threadIdx.x == 0) g8_stamps[blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memtime()
+#endif
 #else
 #define G8_STAMP(k)
 #endif
@@ -252,9 +257,13 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   G8_STAMP(0);
   // buffer b (0 = even, 1 = odd): half-tiles A0, A1, B0, B1 at smem + (b * 4 + h) * kHalf
   const int tiles_n = (g.N + 255) / 256;
+  const int ntiles = ((g.M + 255) / 256) * tiles_n;
   const int ksplit = g.ksplit > 1 ? g.ksplit : 1;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = bid / ksplit, split = bid % ksplit;  // a tile's K-splits are neighbours (same XCD)
+  // split-major: the workgroups an XCD holds at once work on the SAME K (token) slab for different
+  // output tiles, so each slab of both operands is fetched into that XCD's L2 once and shared (a
+  // tile's splits share no data; tile-major ordering measured 2.8x the cycles per K-tile in TN)
+  const int tile = bid % ntiles, split = bid / ntiles;
   const int m0 = (tile / tiles_n) * 256, n0 = (tile % tiles_n) * 256;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = w >> 2, wn = w & 3;  // wave's 64 x 32 piece inside each 128 x 128 quadrant
@@ -674,11 +683,23 @@ void gemm_splitk_reduce(const float* ws, int ksplit, int M, int N, float* C, lon
 int gemm8_pick_ksplit(int M, int N, int K) {
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int nk = K / 64;
-  int ks = 1;
-  // fill the 256 CUs: split the K (token) dimension while tiles are few and each split keeps >= 16
-  // K-tiles (the 8-phase pipeline's prologue/epilogue amortised)
-  while (tiles * ks * 2 <= 320 && nk / (ks * 2) >= 16) ks *= 2;
-  return ks;
+  const int cus = num_cus();
+  // split the K (token) dimension so tiles * ks fills the CUs in as few, as full waves as possible,
+  // each split keeping >= 16 K-tiles (the 8-phase prologue/epilogue amortised); near-ties -> fewer splits
+  int best = 1;
+  double best_eff = 0.0;
+  for (int ks = 1; ks <= 32 && nk / ks >= 16; ++ks) {
+    const int wgs = tiles * ks;
+    const int waves = (wgs + cus - 1) / cus;
+    // a wave of workgroups costs ~ nk / ks K-tiles; minimise total time ~ waves * nk / ks
+    const double t = (double)waves * ((nk + ks - 1) / ks);
+    const double eff = 1.0 / t;
+    if (eff > best_eff * 1.05) {  // more splits cost fp32 slab traffic: only for a clear win
+      best_eff = eff;
+      best = ks;
+    }
+  }
+  return best;
 }
 
 bool gemm8_supported(int M, int N, int K, bool a_t, bool b_t) {

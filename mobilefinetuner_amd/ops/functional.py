@@ -451,7 +451,8 @@ def qk_norm_rope_attention(qkv, nq, nkv, wq, wk, cos, sin, eps_q, eps_k, offset=
 #     LM-head dx 3.91 vs 3.77 ms);
 #   * plain forward GEMMs y = x W^T + b and fp32 weight-gradient accumulation are "plain library
 #     GEMMs" and stay on hipBLASLt where it is measurably faster (NT forward: gemm8 0.79-0.87x;
-#     TN weight-grad: gemm8 0.40-0.90x).  MFT_GEMM8_ALL=1 routes them through gemm8 too, and
+#     wide TN weight-grads: gemm8 0.69-0.79x; small ones (<= 2304 x 768 outputs) run on gemm8,
+#     1.03-1.40x).  MFT_GEMM8_ALL=1 routes them through gemm8 too, and
 #     --deterministic (set_deterministic) always uses gemm8's split-K TN form, whose fixed-order
 #     slab reduction makes weight gradients bitwise reproducible.
 # Shapes outside gemm8's contract (reduction dim % 64, output columns % 8) fall back to torch.mm
@@ -512,7 +513,10 @@ def gemm_dx(dy2, wc, out=None):
 def _mm_wgrad_into(buf, dy2, x2, alpha=1.0):
     """buf (fp32 [N, K]) += alpha * dy2^T @ x2, accumulated in place in the fp32 grad buffer."""
     M = dy2.shape[0]
-    g8 = deterministic() or _gemm8_all()
+    # gemm8's split-major split-K TN form beats hipBLASLt on small outputs (qkv dW 540 vs 556 us,
+    # proj dW 195 vs 273 us at 65536 tokens); hipBLASLt keeps the wide ones (fc / mlp_proj dW 0.7-0.8x)
+    small = dy2.shape[1] * x2.shape[1] <= 2304 * 768
+    g8 = deterministic() or _gemm8_all() or small
     if (g8 and _g8_ok(dy2, x2) and buf.is_contiguous() and M % 64 == 0 and dy2.shape[1] % 8 == 0
             and x2.shape[1] % 8 == 0):
         # TN gemm8: split-K slabs + fixed-order reduce (bitwise reproducible, no atomics)
