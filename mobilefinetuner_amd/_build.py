@@ -59,6 +59,24 @@ def _sources():
     return hip, cpp, binding
 
 
+def _engine_sources():
+    """libmft engine (csrc/engine: tensor, allocator, autograd, ops, models, trainer -- no torch) and
+    the native CLI mains (csrc/apps)."""
+    hip = sorted(glob.glob(os.path.join(CSRC, "engine", "*.hip")))
+    cpp = sorted(glob.glob(os.path.join(CSRC, "engine", "*.cpp")))
+    apps = sorted(glob.glob(os.path.join(CSRC, "apps", "*.cpp")))
+    return hip, cpp, apps
+
+
+BIN_DIR = os.path.join(PKG_DIR, "bin")
+# executable -> (main source, extra defines)
+APPS = {
+    "gpt2_lora_finetune": ("gpt2_finetune.cpp", []),
+    "gpt2_full_finetune": ("gpt2_finetune.cpp", ["-DMFT_FULL_FT=1"]),
+    "engine_selftest": ("engine_selftest.cpp", []),
+}
+
+
 def _flags(kind: str, incs, abi):
     common = ["-O3", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{CSRC}",
               "-Wno-unused-result", "-Wno-deprecated-declarations"]
@@ -75,8 +93,8 @@ def _flags(kind: str, incs, abi):
     return common + [f"-I{ROCM}/include", "-D__HIP_PLATFORM_AMD__=1"]
 
 
-def _compile_one(src: str, kind: str, flags, hdr_digest: str, verbose: bool):
-    rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
+def _compile_one(src: str, kind: str, flags, hdr_digest: str, verbose: bool, tag: str = ""):
+    rel = os.path.relpath(src, CSRC).replace(os.sep, "__") + (f"__{tag}" if tag else "")
     obj = os.path.join(BUILD_DIR, rel + ".o")
     stamp = obj + ".sha1"
     with open(src, "rb") as f:
@@ -124,7 +142,46 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, OUT_SO)
+    build_engine(objs_kernels=[o for (src, k), o in zip(work, objs) if k == "hip"],
+                 objs_runtime=[o for (src, k), o in zip(work, objs) if k == "cpp"], abi=abi, hdr=hdr,
+                 verbose=verbose, jobs=jobs)
     return OUT_SO
+
+
+def build_engine(objs_kernels, objs_runtime, abi, hdr, verbose=False, jobs=None) -> list:
+    """Compile the torch-free libmft engine and link the native CLIs into mobilefinetuner_amd/bin/
+    against the same kernel / runtime objects as _C.so (hipBLASLt + HIP runtime from ROCm)."""
+    os.makedirs(BIN_DIR, exist_ok=True)
+    ehip, ecpp, apps = _engine_sources()
+    work = [(s, "hip", []) for s in ehip] + [(s, "cpp", []) for s in ecpp]
+    app_work = []
+    for exe, (main, defs) in APPS.items():
+        src = os.path.join(CSRC, "apps", main)
+        if os.path.exists(src):
+            app_work.append((exe, src, defs))
+    jobs = jobs or min(8, max(1, (os.cpu_count() or 4)))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = [ex.submit(_compile_one, s, k, _flags(k, [], abi) + d, hdr, verbose) for s, k, d in work]
+        app_futs = {exe: ex.submit(_compile_one, src, "cpp", _flags("cpp", [], abi) + defs, hdr, verbose, exe)
+                    for exe, src, defs in app_work}
+        eobjs = [f.result() for f in futs]
+        aobjs = {exe: f.result() for exe, f in app_futs.items()}
+    changed = any(c for _, c in eobjs) or any(c for _, c in aobjs.values())
+    libs = [o for o, _ in eobjs] + list(objs_kernels) + list(objs_runtime)
+    out = []
+    for exe, (obj, _) in aobjs.items():
+        path = os.path.join(BIN_DIR, exe)
+        if changed or not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(o) for o in libs):
+            cmd = [HIPCC, "-fPIC", obj, *libs, "-o", path + ".tmp", f"-L{ROCM}/lib", "-lhipblaslt", "-lamdhip64",
+                   f"-Wl,-rpath,{ROCM}/lib", "-ldl", "-lpthread"]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+            os.replace(path + ".tmp", path)
+        out.append(path)
+    return out
 
 
 def main(argv=None):

@@ -1,0 +1,367 @@
+// Native CLIs `gpt2_lora_finetune` and `gpt2_full_finetune` on the libmft engine (C++ tensor,
+// caching allocator, autograd tape, hipGraph-captured step; no Python, no torch).
+//
+// Reference: gpt2_lora_finetune/main.cpp:32-710 (CmdArgs :32-78, parse :114-171, LoRA on the fused
+// c_attn + attn.c_proj :382-399, resume :361-381, train loop :561-684, periodic `<stem>_stepN`
+// checkpoints :180-187) and gpt2_full_finetune/main.cpp:25-583 (all params trainable, full
+// HF-keyed safetensors output).  Flag names and defaults are the reference's; extras:
+//   --model P --random_init         random-init weights of preset P (no checkpoint needed)
+//   --synthetic_data [--synthetic_tokens N]   counter-hash token stream (no dataset needed)
+//   --pretokenized_path F [--pretokenized_meta M]   int32 token stream + meta.json
+//   --lora_targets AttnQKV,AttnProj[,MlpFcIn,MlpFcOut] --split_qkv
+//   --no_graph --compat_l2_adam --metrics_out F --deterministic
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <sstream>
+#include <string>
+#include <sys/stat.h>
+#include <thread>
+#include <vector>
+
+#include "engine/allocator.h"
+#include "engine/gemm.h"
+#include "engine/gpt2.h"
+#include "engine/optim.h"
+#include "engine/trainer.h"
+#include "runtime/dataset.h"
+#include "runtime/power_monitor.h"
+#include "runtime/tokenizer.h"
+
+using namespace mft;
+using namespace mft::eng;
+
+#ifdef MFT_FULL_FT
+static const char* kProg = "gpt2_full_finetune";
+#else
+static const char* kProg = "gpt2_lora_finetune";
+#endif
+
+namespace {
+
+struct Args {
+  std::map<std::string, std::string> kv;
+  std::set<std::string> flags;
+  std::string get(const std::string& k, const std::string& d = "") const {
+    auto it = kv.find(k);
+    return it == kv.end() ? d : it->second;
+  }
+  int i(const std::string& k, int d) const { return kv.count(k) ? std::stoi(kv.at(k)) : d; }
+  int64_t l(const std::string& k, int64_t d) const { return kv.count(k) ? std::stoll(kv.at(k)) : d; }
+  float f(const std::string& k, float d) const { return kv.count(k) ? std::stof(kv.at(k)) : d; }
+  bool b(const std::string& k) const { return flags.count(k) || (kv.count(k) && kv.at(k) != "0" && kv.at(k) != "false"); }
+};
+
+const std::set<std::string> kBool = {"split_qkv", "random_init", "synthetic_data", "no_graph", "compat_l2_adam",
+                                     "shard_enable", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
+                                     "deterministic", "help"};
+const std::set<std::string> kValued = {
+    "data_dir", "pretrained_dir", "lora_out", "resume_from", "eval_out", "output_path", "epochs", "steps",
+    "batch_size", "grad_accum_steps", "seq_len", "rank", "alpha", "lr", "weight_decay", "warmup_steps",
+    "clip_grad_norm", "lora_dropout", "data_fraction", "log_interval", "eval_interval", "eval_batches",
+    "eval_batch_size", "save_every", "ema_beta", "seed", "pm_interval", "pm_batt_thresh", "pm_temp_thresh",
+    "pm_fb_high", "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule",
+    "shard_dir", "shard_budget_mb", "shard_fp16_disk", "model", "synthetic_tokens", "pretokenized_path",
+    "pretokenized_meta", "lora_targets", "metrics_out", "device"};
+
+Args parse(int argc, char** argv) {
+  Args a;
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    if (s.rfind("--", 0) != 0) throw std::runtime_error("unexpected argument '" + s + "'");
+    s = s.substr(2);
+    std::string key = s, val;
+    bool has_val = false;
+    const size_t eq = s.find('=');
+    if (eq != std::string::npos) {
+      key = s.substr(0, eq);
+      val = s.substr(eq + 1);
+      has_val = true;
+    }
+    if (kBool.count(key)) {
+      if (has_val) a.kv[key] = val;
+      else a.flags.insert(key);
+      continue;
+    }
+    if (!kValued.count(key)) throw std::runtime_error("unknown flag --" + key + " (see --help)");
+    if (!has_val) {
+      if (i + 1 >= argc) throw std::runtime_error("flag --" + key + " needs a value");
+      val = argv[++i];
+    }
+    a.kv[key] = val;
+  }
+  return a;
+}
+
+bool file_exists(const std::string& p) {
+  struct stat st;
+  return stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode);
+}
+
+std::string checkpoint_path(const std::string& stem, int64_t step) {
+  const size_t dot = stem.rfind('.');
+  const size_t slash = stem.rfind('/');
+  std::string root = stem, ext = ".safetensors";
+  if (dot != std::string::npos && (slash == std::string::npos || dot > slash)) {
+    root = stem.substr(0, dot);
+    ext = stem.substr(dot);
+  }
+  return root + "_step" + std::to_string(step) + ext;
+}
+
+std::vector<std::string> split_csv(const std::string& s) {
+  std::vector<std::string> out;
+  std::stringstream ss(s);
+  std::string item;
+  while (std::getline(ss, item, ','))
+    if (!item.empty()) out.push_back(item);
+  return out;
+}
+
+std::string norm_target(std::string t) {
+  std::string l = t;
+  for (auto& c : l) c = (char)std::tolower(c);
+  if (l == "attnqkv" || l == "attn_qkv" || l == "c_attn" || l == "qkv") return "AttnQKV";
+  if (l == "attnproj" || l == "attn_proj" || l == "proj") return "AttnProj";
+  if (l == "mlpfcin" || l == "mlp_fc_in" || l == "c_fc" || l == "fc_in") return "MlpFcIn";
+  if (l == "mlpfcout" || l == "mlp_fc_out" || l == "fc_out") return "MlpFcOut";
+  throw std::runtime_error("unknown GPT-2 LoRA target '" + t + "'");
+}
+
+std::string split_file(const std::string& dir, const char* const* names) {
+  for (int i = 0; names[i]; ++i) {
+    const std::string p = dir + "/" + names[i];
+    if (file_exists(p)) return p;
+  }
+  return "";
+}
+
+void usage() {
+  std::printf(
+      "%s -- native MI355X engine (libmft)\n"
+      "  --data_dir D --pretrained_dir P [--lora_out F] [--resume_from F] [--eval_out F] [--output_path F]\n"
+      "  --epochs N --steps N --batch_size B --grad_accum_steps A --seq_len S --rank R --alpha A --lr LR\n"
+      "  --weight_decay W --warmup_steps W --clip_grad_norm C --lora_dropout P --data_fraction F --log_interval N\n"
+      "  --eval_interval N --eval_batches N --eval_batch_size B --save_every N --ema_beta B --seed S\n"
+      "  --pm_interval --pm_batt_thresh --pm_temp_thresh --pm_fb_high --pm_fb_low --pm_ft_high --pm_ft_low\n"
+      "  --pm_manual_batt --pm_manual_temp --pm_disable_batt --pm_disable_temp --pm_schedule --pm_gpu_telemetry\n"
+      "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --pretokenized_path F\n"
+      "          --pretokenized_meta F --lora_targets T --split_qkv --no_graph --compat_l2_adam --metrics_out F\n"
+      "          --deterministic\n",
+      kProg);
+}
+
+int run(int argc, char** argv) {
+  Args a = parse(argc, argv);
+  if (a.b("help")) {
+    usage();
+    return 0;
+  }
+#ifdef MFT_FULL_FT
+  const bool full = true;
+#else
+  const bool full = false;
+#endif
+  if (a.b("shard_enable"))
+    throw std::runtime_error("--shard_enable: the host/disk offload tier is driven from the Python CLI "
+                             "(python -m mobilefinetuner_amd.cli." + std::string(kProg) + "); the native CLI keeps "
+                             "every weight resident in HBM");
+  if (a.b("deterministic")) set_deterministic(true);
+  // one non-blocking stream for everything (graph capture target)
+  hipStream_t stream;
+  HIP_OK(hipSetDevice(0));
+  HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  set_current_stream(stream);
+
+  const int seq_len = a.i("seq_len", 128);
+  const uint64_t seed = (uint64_t)a.l("seed", 42);
+  std::printf("\n========== %s (MI355X native engine) ==========\n", kProg);
+
+  std::printf("\n[1/6] Loading model...\n");
+  const std::string pdir = a.get("pretrained_dir");
+  GPT2Config cfg;
+  const bool random_init = a.b("random_init") || pdir.empty();
+  if (!random_init && file_exists(pdir + "/config.json")) cfg = GPT2Config::from_json(pdir + "/config.json");
+  else cfg = GPT2Config::preset(a.get("model", "gpt2"));
+  auto model = std::make_unique<GPT2>(cfg);
+  if (random_init) {
+    model->init_random(1234);
+    std::printf("  random-init %s (%d layers, C=%d, H=%d)\n", a.get("model", "gpt2").c_str(), cfg.n_layer,
+                cfg.n_embd, cfg.n_head);
+  } else {
+    model->load_hf(pdir);
+    std::printf("  loaded %s/model.safetensors\n", pdir.c_str());
+  }
+  int seq = seq_len;
+  if (seq > cfg.n_positions) {
+    std::printf("  seq_len(%d) exceeds n_positions(%d), clamped\n", seq, cfg.n_positions);
+    seq = cfg.n_positions;
+  }
+
+  std::printf("\n[2/6] %s...\n", full ? "Full fine-tuning: every parameter trainable" : "LoRA adapters");
+  const std::string resume = a.get("resume_from");
+  if (full) {
+    model->set_full_finetune();
+  } else if (!resume.empty() && file_exists(resume)) {
+    model->load_lora(resume);
+    std::printf("  resumed adapter from %s (rank=%d)\n", resume.c_str(), model->lora_spec().rank);
+  } else {
+    LoraSpec spec;
+    spec.rank = a.i("rank", 8);
+    spec.alpha = a.f("alpha", 16.f);
+    spec.dropout = a.f("lora_dropout", 0.f);
+    spec.split_qkv = a.b("split_qkv");
+    spec.targets.clear();
+    for (auto& t : split_csv(a.get("lora_targets", "AttnQKV,AttnProj"))) spec.targets.push_back(norm_target(t));
+    model->inject_lora(spec);
+    std::printf("  injected adapters (rank=%d, alpha=%g, targets=%s)\n", spec.rank, spec.alpha,
+                a.get("lora_targets", "AttnQKV,AttnProj").c_str());
+  }
+  FlatParams flat(model->trainable());
+  std::printf("  trainable params: %lld (padded)  |  total: %zu\n", (long long)flat.numel, model->num_parameters());
+
+  std::printf("\n[3/6] Loading dataset...\n");
+  DataConfig dc;
+  dc.seq_len = seq;
+  dc.eos_id = 50256;
+  dc.seed = seed;
+  dc.data_fraction = a.f("data_fraction", 1.f);
+  DataConfig vc = dc;
+  vc.drop_last = false;
+  vc.shuffle = false;
+  TokenDataset train(dc), valid(vc);
+  bool have_valid = true;
+  const std::string ddir = a.get("data_dir"), pt = a.get("pretokenized_path");
+  if (!pt.empty()) {
+    std::string meta = a.get("pretokenized_meta");
+    if (meta.empty()) meta = pt.substr(0, pt.rfind('/') + 1) + "meta.json";
+    PretokMeta m = read_pretok_meta(meta);
+    train.set_tokens(read_pretok_split(pt, m, 0, dc.data_fraction, seq));
+    if (m.len[1] > 0) valid.set_tokens(read_pretok_split(pt, m, 1, 1.f, seq));
+    else have_valid = false;
+    std::printf("  pretokenized stream %s\n", pt.c_str());
+  } else if (a.b("synthetic_data") || ddir.empty()) {
+    const int64_t n = a.l("synthetic_tokens", 2000000);
+    auto gen = [&](int64_t count, uint64_t s) {
+      std::vector<int32_t> v(count);
+      uint64_t z = s;
+      for (int64_t i = 0; i < count; ++i) {
+        z += 0x9E3779B97F4A7C15ull;
+        uint64_t x = z;
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+        v[i] = (int32_t)((x ^ (x >> 31)) % (uint64_t)cfg.vocab_size);
+      }
+      return v;
+    };
+    train.set_tokens(gen(n, seed));
+    valid.set_tokens(gen(std::max<int64_t>(n / 20, 4 * seq), seed + 1));
+    std::printf("  (synthetic token data, %lld tokens)\n", (long long)n);
+  } else {
+    const char* tr_names[] = {"wiki.train.raw", "wiki.train.tokens", "train.txt", nullptr};
+    const char* va_names[] = {"wiki.valid.raw", "wiki.valid.tokens", "valid.txt", "validation.txt", nullptr};
+    auto tok = ByteLevelBPE::from_files(pdir + "/vocab.json", pdir + "/merges.txt");
+    auto enc = [&](const std::string& s) { return tok->encode(s); };
+    const int threads = std::max(1u, std::thread::hardware_concurrency());
+    const std::string ftr = split_file(ddir, tr_names), fva = split_file(ddir, va_names);
+    if (ftr.empty()) throw std::runtime_error("no train split under " + ddir);
+    train.set_tokens(pack_lines(read_lines(ftr, true), enc, dc.eos_id, true, dc.data_fraction, seq, threads));
+    if (!fva.empty()) valid.set_tokens(pack_lines(read_lines(fva, true), enc, dc.eos_id, true, 1.f, seq, threads));
+    else have_valid = false;
+  }
+  std::printf("  train: %zu sequences | valid: %zu sequences\n", train.num_sequences(),
+              have_valid ? valid.num_sequences() : (size_t)0);
+
+  AdamWConfig oc;
+  oc.lr = a.f("lr", full ? 5e-5f : 1e-4f);
+  oc.weight_decay = a.f("weight_decay", full ? 0.01f : 0.f);
+  oc.max_grad_norm = a.f("clip_grad_norm", 1.f);
+  oc.l2_coupled = a.b("compat_l2_adam");
+  AdamW opt(flat, oc);
+  TrainConfig tc;
+  tc.epochs = a.i("epochs", 0);
+  tc.steps = a.l("steps", 0);
+  tc.batch = a.i("batch_size", 1);
+  tc.accum = a.i("grad_accum_steps", 1);
+  tc.seq = seq;
+  tc.lr = oc.lr;
+  tc.warmup = a.i("warmup_steps", 0);
+  tc.log_interval = a.i("log_interval", 1);
+  tc.eval_interval = a.i("eval_interval", 0);
+  tc.eval_batches = a.i("eval_batches", 50);
+  tc.eval_batch_size = a.i("eval_batch_size", 2);
+  tc.save_every = a.i("save_every", 0);
+  tc.ema_beta = a.f("ema_beta", 0.9f);
+  tc.use_graph = !a.b("no_graph");
+  tc.eval_out = a.get("eval_out");
+  tc.metrics_out = a.get("metrics_out");
+  std::unique_ptr<PowerMonitor> pm;
+  if (a.i("pm_interval", 0) > 0 || !a.get("pm_schedule").empty()) {
+    PowerConfig pc;
+    pc.check_interval_steps = a.i("pm_interval", 0);
+    pc.battery_threshold = a.f("pm_batt_thresh", 20.f);
+    pc.temp_threshold = a.f("pm_temp_thresh", 42.f);
+    pc.freq_b_high = a.f("pm_fb_high", 2.f);
+    pc.freq_b_low = a.f("pm_fb_low", 0.5f);
+    pc.freq_t_high = a.f("pm_ft_high", 2.f);
+    pc.freq_t_low = a.f("pm_ft_low", 0.5f);
+    pc.enable_battery = !a.b("pm_disable_batt");
+    pc.enable_temp = !a.b("pm_disable_temp");
+    pc.use_gpu_telemetry = a.b("pm_gpu_telemetry");
+    pm = std::make_unique<PowerMonitor>(pc);
+    pm->set_manual_readings(a.f("pm_manual_batt", 100.f), a.f("pm_manual_temp", 30.f));
+    if (!a.get("pm_schedule").empty()) pm->set_step_schedule(PowerMonitor::parse_schedule(a.get("pm_schedule")));
+  }
+  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get());
+  const std::string lora_out = a.get("lora_out"), out_path = a.get("output_path");
+  auto save = [&](int64_t step) {
+    if (!full && !lora_out.empty()) {
+      const std::string p = checkpoint_path(lora_out, step);
+      model->save_lora(p);
+      std::printf("\n[Checkpoint] Saved %s\n\n", p.c_str());
+    }
+  };
+  std::printf("\n[Training plan]\n  epochs         : %d\n  steps_per_epoch: %lld\n  total_steps    : %lld\n"
+              "  effective_batch: %d (micro=%d x accum=%d)\n",
+              tc.epochs, (long long)trainer.steps_per_epoch(), (long long)trainer.total_steps(), tc.batch * tc.accum,
+              tc.batch, tc.accum);
+  std::printf("\n[4/6] Optimizer: fused AdamW (%s)\n", oc.l2_coupled ? "coupled L2, reference" : "decoupled");
+  std::printf("\n[5/6] Starting training (%s)...\n========================================\n",
+              tc.use_graph ? "hipGraph-captured step" : "eager");
+  const auto t0 = std::chrono::steady_clock::now();
+  trainer.train(save);
+  const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  std::printf("\n[6/6] Saving...\n");
+  if (!full && !lora_out.empty()) {
+    model->save_lora(lora_out);
+    std::printf("  LoRA saved to: %s\n", lora_out.c_str());
+  }
+  if (full && !out_path.empty()) {
+    model->save_hf(out_path);
+    std::printf("  model saved to: %s\n", out_path.c_str());
+  }
+  const AllocStats st = CachingAllocator::get(0).stats();
+  std::printf("\n========================================\nTraining complete!\n  Total steps: %lld\n"
+              "  Total tokens: %lld\n  Wall time: %.2f s (%.0f tokens/s)\n  Final EMA loss: %.4f\n"
+              "  HBM: peak allocated %.2f GB, reserved %.2f GB\n========================================\n",
+              (long long)trainer.global_step, (long long)trainer.total_tokens, secs, trainer.total_tokens / secs,
+              trainer.ema_loss, st.peak_allocated / 1e9, st.peak_reserved / 1e9);
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  try {
+    return run(argc, argv);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "%s: error: %s\n", kProg, e.what());
+    return 1;
+  }
+}

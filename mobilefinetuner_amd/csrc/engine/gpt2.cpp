@@ -1,0 +1,494 @@
+// libmft engine: GPT-2 model (see gpt2.h).
+#include "engine/gpt2.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <regex>
+#include <sstream>
+
+#include "engine/autograd.h"
+#include "engine/ops.h"
+#include "kernels.h"
+#include "runtime/json.h"
+#include "runtime/safetensors.h"
+
+namespace mft {
+namespace eng {
+
+GPT2Config GPT2Config::preset(const std::string& n0) {
+  std::string n = n0;
+  for (auto& c : n) c = (c == '_') ? '-' : (char)std::tolower(c);
+  GPT2Config c;
+  if (n == "gpt2" || n == "gpt2-small" || n == "gpt2-124m") return c;
+  if (n == "gpt2-medium") {
+    c.n_embd = 1024, c.n_layer = 24, c.n_head = 16;
+  } else if (n == "gpt2-large") {
+    c.n_embd = 1280, c.n_layer = 36, c.n_head = 20;
+  } else if (n == "gpt2-xl") {
+    c.n_embd = 1600, c.n_layer = 48, c.n_head = 25;
+  } else if (n == "gpt2-tiny") {
+    c.n_embd = 128, c.n_layer = 2, c.n_head = 2, c.vocab_size = 1000, c.n_positions = 256;
+  } else {
+    MFT_CHECK(false, "unknown GPT-2 preset '", n0, "'");
+  }
+  return c;
+}
+
+GPT2Config GPT2Config::from_json(const std::string& path) {
+  std::ifstream f(path);
+  MFT_CHECK(f.good(), "cannot open ", path);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  json::Value v = json::parse(ss.str());
+  GPT2Config c;
+  auto gi = [&](const char* k, int d) { return v.get(k) ? (int)v[k].as_int() : d; };
+  c.vocab_size = gi("vocab_size", c.vocab_size);
+  c.n_positions = v.get("n_positions") ? gi("n_positions", c.n_positions) : gi("n_ctx", c.n_positions);
+  c.n_embd = gi("n_embd", c.n_embd);
+  c.n_layer = gi("n_layer", c.n_layer);
+  c.n_head = gi("n_head", c.n_head);
+  if (v.get("layer_norm_epsilon")) c.eps = (float)v["layer_norm_epsilon"].as_double();
+  if (v.get("initializer_range")) c.init_range = (float)v["initializer_range"].as_double();
+  return c;
+}
+
+bool LoraSpec::has(const std::string& t) const { return std::find(targets.begin(), targets.end(), t) != targets.end(); }
+
+namespace {
+Param frozen(Tensor t) {
+  Param p;
+  p.leaf = t;
+  p.c = t;
+  return p;
+}
+}  // namespace
+
+GPT2::GPT2(const GPT2Config& cfg) : cfg_(cfg) { alloc(); }
+
+void GPT2::alloc() {
+  const int C = cfg_.n_embd;
+  NoGradGuard ng;
+  wte_ = frozen(zeros({cfg_.vocab_padded(), C}, DType::BF16));
+  wpe_ = frozen(zeros({cfg_.n_positions, C}, DType::BF16));
+  lnf_w_ = frozen(ones({C}, DType::F32));
+  lnf_b_ = frozen(zeros({C}, DType::F32));
+  blocks_.resize(cfg_.n_layer);
+  for (auto& b : blocks_) {
+    b.ln1_w = frozen(ones({C}, DType::F32));
+    b.ln1_b = frozen(zeros({C}, DType::F32));
+    b.ln2_w = frozen(ones({C}, DType::F32));
+    b.ln2_b = frozen(zeros({C}, DType::F32));
+    b.attn_w = frozen(zeros({3 * C, C}, DType::BF16));
+    b.attn_b = frozen(zeros({3 * C}, DType::BF16));
+    b.proj_w = frozen(zeros({C, C}, DType::BF16));
+    b.proj_b = frozen(zeros({C}, DType::BF16));
+    b.fc_w = frozen(zeros({4 * C, C}, DType::BF16));
+    b.fc_b = frozen(zeros({4 * C}, DType::BF16));
+    b.mproj_w = frozen(zeros({C, 4 * C}, DType::BF16));
+    b.mproj_b = frozen(zeros({C}, DType::BF16));
+  }
+  dropout_ctr = zeros({1}, DType::I64);
+  // LM-head CE chunk: rows of bf16 logits materialised at once, 16 GiB budget (MFT_CE_BUDGET_GB)
+  const char* env = std::getenv("MFT_CE_CHUNK");
+  if (env) {
+    ce_chunk = std::atoll(env);
+  } else {
+    const double gb = std::getenv("MFT_CE_BUDGET_GB") ? std::atof(std::getenv("MFT_CE_BUDGET_GB")) : 16.0;
+    const int64_t rows = (int64_t)(gb * (1ull << 30) / (2.0 * cfg_.vocab_padded()));
+    ce_chunk = std::max<int64_t>(64, std::min<int64_t>(65536, rows / 64 * 64));
+  }
+}
+
+void GPT2::init_random(uint64_t seed) {
+  NoGradGuard ng;
+  const float std0 = cfg_.init_range, std_proj = cfg_.init_range / std::sqrt(2.f * cfg_.n_layer);
+  uint64_t s = seed * 1000003ull + 17;
+  auto nrm = [&](Param& p, float sd) { p.c.copy_(randn(p.c.shape(), ++s, sd, DType::F32)); };
+  nrm(wte_, std0);
+  wte_.c.slice(0, cfg_.vocab_size, cfg_.vocab_padded()).zero_();
+  nrm(wpe_, 0.01f);
+  for (auto& b : blocks_) {
+    nrm(b.attn_w, std0);
+    nrm(b.fc_w, std0);
+    nrm(b.proj_w, std_proj);
+    nrm(b.mproj_w, std_proj);
+  }
+}
+
+// ------------------------------------------------------------------ HF checkpoint IO
+namespace {
+DType st_dtype(const std::string& d) {
+  if (d == "F32") return DType::F32;
+  if (d == "BF16") return DType::BF16;
+  if (d == "F16") return DType::F16;
+  MFT_CHECK(false, "safetensors: unsupported dtype ", d);
+  return DType::F32;
+}
+}  // namespace
+
+void GPT2::load_hf(const std::string& dir) {
+  NoGradGuard ng;
+  std::string path = dir;
+  if (path.size() < 12 || path.substr(path.size() - 12) != ".safetensors") path = dir + "/model.safetensors";
+  SafeTensorsFile f(path);
+  auto find = [&](const std::string& k) -> const TensorInfo* {
+    if (f.has(k)) return &f.info(k);
+    if (f.has("transformer." + k)) return &f.info("transformer." + k);
+    return nullptr;
+  };
+  auto load = [&](Param& p, const std::string& key, bool conv1d) {
+    const TensorInfo* ti = find(key);
+    MFT_CHECK(ti, "checkpoint ", path, " has no tensor '", key, "'");
+    Tensor host = from_blob(const_cast<void*>(f.data(ti->name)), ti->shape, st_dtype(ti->dtype), Device::cpu());
+    Tensor src = conv1d ? host.t() : host;  // HF Conv1D [in, out] -> [out, in]
+    Tensor dst = p.c;
+    if (key == "wte.weight") dst = p.c.slice(0, 0, ti->shape[0]);
+    MFT_CHECK(shape_numel(src.shape()) == dst.numel(), "checkpoint tensor '", key, "' ", shape_str(ti->shape),
+              " does not fit ", dst.str());
+    Tensor staged = empty(src.shape(), DType::F32, Device::cpu());
+    staged.copy_(src);  // host transpose + cast
+    dst.copy_(staged.view(dst.shape()));
+  };
+  load(wte_, "wte.weight", false);
+  load(wpe_, "wpe.weight", false);
+  load(lnf_w_, "ln_f.weight", false);
+  load(lnf_b_, "ln_f.bias", false);
+  for (int i = 0; i < cfg_.n_layer; ++i) {
+    auto& b = blocks_[i];
+    const std::string p = "h." + std::to_string(i) + ".";
+    load(b.ln1_w, p + "ln_1.weight", false);
+    load(b.ln1_b, p + "ln_1.bias", false);
+    load(b.attn_w, p + "attn.c_attn.weight", true);
+    load(b.attn_b, p + "attn.c_attn.bias", false);
+    load(b.proj_w, p + "attn.c_proj.weight", true);
+    load(b.proj_b, p + "attn.c_proj.bias", false);
+    load(b.ln2_w, p + "ln_2.weight", false);
+    load(b.ln2_b, p + "ln_2.bias", false);
+    load(b.fc_w, p + "mlp.c_fc.weight", true);
+    load(b.fc_b, p + "mlp.c_fc.bias", false);
+    load(b.mproj_w, p + "mlp.c_proj.weight", true);
+    load(b.mproj_b, p + "mlp.c_proj.bias", false);
+  }
+  synchronize();
+}
+
+std::vector<std::pair<std::string, Param*>> GPT2::all_params() {
+  std::vector<std::pair<std::string, Param*>> v{{"wte.weight", &wte_}, {"wpe.weight", &wpe_}};
+  for (int i = 0; i < cfg_.n_layer; ++i) {
+    auto& b = blocks_[i];
+    const std::string p = "h." + std::to_string(i) + ".";
+    v.push_back({p + "ln_1.weight", &b.ln1_w});
+    v.push_back({p + "ln_1.bias", &b.ln1_b});
+    v.push_back({p + "attn.c_attn.weight", &b.attn_w});
+    v.push_back({p + "attn.c_attn.bias", &b.attn_b});
+    v.push_back({p + "attn.c_proj.weight", &b.proj_w});
+    v.push_back({p + "attn.c_proj.bias", &b.proj_b});
+    v.push_back({p + "ln_2.weight", &b.ln2_w});
+    v.push_back({p + "ln_2.bias", &b.ln2_b});
+    v.push_back({p + "mlp.c_fc.weight", &b.fc_w});
+    v.push_back({p + "mlp.c_fc.bias", &b.fc_b});
+    v.push_back({p + "mlp.c_proj.weight", &b.mproj_w});
+    v.push_back({p + "mlp.c_proj.bias", &b.mproj_b});
+  }
+  v.push_back({"ln_f.weight", &lnf_w_});
+  v.push_back({"ln_f.bias", &lnf_b_});
+  return v;
+}
+
+void GPT2::save_hf(const std::string& path) {
+  std::vector<Tensor> keep;
+  std::vector<TensorBlob> blobs;
+  for (auto& kv : all_params()) {
+    const std::string& k = kv.first;
+    Tensor src = kv.second->trainable() ? kv.second->leaf.detach() : kv.second->c;
+    if (k == "wte.weight") src = src.slice(0, 0, cfg_.vocab_size);
+    const bool conv1d = k.find("attn.c_attn.weight") != std::string::npos ||
+                        k.find("attn.c_proj.weight") != std::string::npos ||
+                        k.find("mlp.c_fc.weight") != std::string::npos || k.find("mlp.c_proj.weight") != std::string::npos;
+    Tensor h = empty(conv1d ? Shape{src.size(1), src.size(0)} : src.shape(), DType::F32, Device::cpu());
+    h.copy_(conv1d ? src.t() : src);
+    keep.push_back(h);
+    blobs.push_back({k, "F32", h.shape(), h.data_ptr(), h.nbytes()});
+  }
+  safetensors_save(path, blobs, {{"format", "pt"}}, true, true);
+}
+
+// ------------------------------------------------------------------ parameters
+void GPT2::make_trainable(Param& p) {
+  if (p.trainable()) return;
+  NoGradGuard ng;
+  Tensor master = p.c.to(DType::F32);
+  if (master.impl() == p.c.impl()) master = p.c.clone();
+  master.requires_grad_(true);
+  p.leaf = master;
+  if (p.c.dtype() == DType::F32) p.c = master;  // fp32-compute (norm) weights read the master
+  p.wt = Tensor();
+}
+
+void GPT2::set_full_finetune() {
+  full_ = true;
+  for (auto& kv : all_params()) make_trainable(*kv.second);
+}
+
+std::vector<std::pair<std::string, Param*>> GPT2::trainable() {
+  std::vector<std::pair<std::string, Param*>> v;
+  if (full_) {
+    for (auto& kv : all_params())
+      if (kv.second->trainable()) v.push_back(kv);
+  }
+  for (int i = 0; i < cfg_.n_layer; ++i) {
+    auto& b = blocks_[i];
+    auto add = [&](std::vector<LoraAdapter>& ads, std::vector<std::string>& names) {
+      for (size_t j = 0; j < ads.size(); ++j) {
+        v.push_back({names[j] + ".lora_A", &ads[j].A});
+        v.push_back({names[j] + ".lora_B", &ads[j].B});
+      }
+    };
+    add(b.lqkv, b.names_qkv);
+    add(b.lproj, b.names_proj);
+    add(b.lfc, b.names_fc);
+    add(b.lfcout, b.names_fcout);
+  }
+  return v;
+}
+
+size_t GPT2::num_parameters() const {
+  size_t n = 0;
+  auto self = const_cast<GPT2*>(this);
+  for (auto& kv : self->all_params()) n += kv.second->c.numel();
+  return n - (size_t)(cfg_.vocab_padded() - cfg_.vocab_size) * cfg_.n_embd;
+}
+
+// ------------------------------------------------------------------ LoRA
+namespace {
+LoraAdapter make_adapter(int col0, int n, int in, int r, const Tensor& A_init, float dropout, const std::string& name) {
+  LoraAdapter a;
+  a.col0 = col0;
+  a.ncols = n;
+  a.rank = r;
+  a.dropout = dropout;
+  uint32_t h = 2166136261u;  // FNV-1a of the adapter name: stable dropout salt
+  for (char c : name) h = (h ^ (uint8_t)c) * 16777619u;
+  a.salt = h;
+  NoGradGuard ng;
+  Tensor A = A_init.to(DType::F32).contiguous().clone();
+  A.requires_grad_(true);
+  Tensor B = zeros({r, n}, DType::F32);
+  B.requires_grad_(true);
+  a.A.leaf = A;
+  a.A.c = A.to(DType::BF16);
+  a.B.leaf = B;
+  a.B.c = B.to(DType::BF16);
+  (void)in;
+  return a;
+}
+}  // namespace
+
+void GPT2::inject_lora(const LoraSpec& spec) {
+  spec_ = spec;
+  lora_ = true;
+  const int C = cfg_.n_embd;
+  std::vector<int> layers = spec.layers;
+  if (layers.empty())
+    for (int i = 0; i < cfg_.n_layer; ++i) layers.push_back(i);
+  for (int i : layers) {
+    auto& b = blocks_[i];
+    const std::string pre = "layer." + std::to_string(i) + ".";
+    auto add = [&](std::vector<LoraAdapter>& ads, std::vector<std::string>& names, int col0, int n, int in,
+                   const std::string& nm) {
+      // reference init (graph/lora_injector.cpp:70-85): A[in, r] ~ U(+-sqrt(6/(in+r))), seed 42+in+out
+      const float bound = std::sqrt(6.f / (float)(in + spec.rank));
+      Tensor A = rand_uniform({in, spec.rank}, spec.seed + in + n, -bound, bound, DType::F32).t();
+      ads.push_back(make_adapter(col0, n, in, spec.rank, A, spec.dropout, pre + nm));
+      names.push_back(pre + nm);
+    };
+    if (spec.has("AttnQKV")) {
+      if (spec.split_qkv) {
+        add(b.lqkv, b.names_qkv, 0, C, C, "attn.q");
+        add(b.lqkv, b.names_qkv, C, C, C, "attn.k");
+        add(b.lqkv, b.names_qkv, 2 * C, C, C, "attn.v");
+      } else {
+        add(b.lqkv, b.names_qkv, 0, 3 * C, C, "attn.qkv");
+      }
+    }
+    if (spec.has("AttnProj")) add(b.lproj, b.names_proj, 0, C, C, "attn.proj");
+    if (spec.has("MlpFcIn")) add(b.lfc, b.names_fc, 0, 4 * C, C, "mlp.fc_in");
+    if (spec.has("MlpFcOut")) add(b.lfcout, b.names_fcout, 0, C, 4 * C, "mlp.fc_out");
+  }
+}
+
+void GPT2::load_lora(const std::string& path) {
+  SafeTensorsFile f(path);
+  const auto& meta = f.metadata();
+  LoraSpec spec;
+  auto mget = [&](const char* k) -> std::string {
+    auto it = meta.find(k);
+    return it == meta.end() ? "" : it->second;
+  };
+  std::map<std::string, const TensorInfo*> A, B;
+  std::regex re(R"(layer\.(\d+)\.(attn\.qkv|attn\.q|attn\.k|attn\.v|attn\.proj|mlp\.fc_in|mlp\.fc_out)\.lora_(A|B))");
+  std::vector<int> layers;
+  for (auto& ti : f.tensors()) {
+    std::smatch m;
+    if (!std::regex_match(ti.name, m, re)) continue;
+    const std::string stem = "layer." + m[1].str() + "." + m[2].str();
+    (m[3].str() == "A" ? A : B)[stem] = &ti;
+    const int li = std::stoi(m[1].str());
+    if (std::find(layers.begin(), layers.end(), li) == layers.end()) layers.push_back(li);
+  }
+  MFT_CHECK(!A.empty(), "no LoRA tensors in ", path);
+  spec.rank = mget("rank").empty() ? (int)std::min(A.begin()->second->shape[0], A.begin()->second->shape[1])
+                                   : std::stoi(mget("rank"));
+  spec.alpha = mget("alpha").empty() ? 2.f * spec.rank : std::stof(mget("alpha"));
+  spec.dropout = mget("dropout").empty() ? 0.f : std::stof(mget("dropout"));
+  spec.split_qkv = mget("split_qkv") == "true";
+  spec.targets.clear();
+  for (auto& kv : A) {
+    const std::string part = kv.first.substr(kv.first.find('.', 6) + 1);
+    std::string t = part == "attn.proj" ? "AttnProj" : part == "mlp.fc_in" ? "MlpFcIn" : part == "mlp.fc_out" ? "MlpFcOut" : "AttnQKV";
+    if (part == "attn.q") spec.split_qkv = true;
+    if (!spec.has(t)) spec.targets.push_back(t);
+  }
+  std::sort(layers.begin(), layers.end());
+  spec.layers = layers;
+  for (auto& b : blocks_) {
+    b.lqkv.clear(), b.lproj.clear(), b.lfc.clear(), b.lfcout.clear();
+    b.names_qkv.clear(), b.names_proj.clear(), b.names_fc.clear(), b.names_fcout.clear();
+    b.waug_qkv = Tensor(), b.waug_proj = Tensor();
+  }
+  inject_lora(spec);
+  // overwrite the fresh adapters with the checkpoint's values: A [in, r] -> [r, in], B [r, out]
+  NoGradGuard ng;
+  for (auto& kv : trainable()) {
+    const std::string& name = kv.first;
+    const bool isA = name.size() > 7 && name.substr(name.size() - 7) == ".lora_A";
+    const std::string stem = name.substr(0, name.size() - 7);
+    auto& mp = isA ? A : B;
+    auto it = mp.find(stem);
+    MFT_CHECK(it != mp.end(), "LoRA checkpoint lacks ", name);
+    const TensorInfo* ti = it->second;
+    Tensor host = from_blob(const_cast<void*>(f.data(ti->name)), ti->shape, st_dtype(ti->dtype), Device::cpu());
+    Tensor src = isA ? host.t() : host;
+    Tensor staged = empty(src.shape(), DType::F32, Device::cpu());
+    staged.copy_(src);
+    Param* p = kv.second;
+    MFT_CHECK(staged.numel() == p->leaf.numel(), "LoRA tensor ", name, " shape mismatch");
+    p->leaf.copy_(staged.view(p->leaf.shape()));
+    p->c.copy_(p->leaf);
+  }
+}
+
+void GPT2::save_lora(const std::string& path) {
+  std::vector<Tensor> keep;
+  std::vector<TensorBlob> blobs;
+  for (auto& kv : trainable()) {
+    const std::string& name = kv.first;
+    if (name.find(".lora_") == std::string::npos) continue;
+    const bool isA = name.substr(name.size() - 7) == ".lora_A";
+    Tensor src = kv.second->leaf.detach();
+    if (isA) src = src.t();  // [r, in] -> reference [in, r]
+    Tensor h = empty(src.shape(), DType::F32, Device::cpu());
+    h.copy_(src);
+    keep.push_back(h);
+    blobs.push_back({name, "F32", h.shape(), h.data_ptr(), h.nbytes()});
+  }
+  auto fmt = [](double x) {
+    std::ostringstream os;
+    os << x;
+    return os.str();
+  };
+  std::string targets;
+  for (size_t i = 0; i < spec_.targets.size(); ++i) targets += (i ? "," : "") + spec_.targets[i];
+  safetensors_save(path, blobs,
+                   {{"rank", std::to_string(spec_.rank)},
+                    {"alpha", fmt(spec_.alpha)},
+                    {"dropout", fmt(spec_.dropout)},
+                    {"split_qkv", spec_.split_qkv ? "true" : "false"},
+                    {"targets", targets}},
+                   true, false);
+}
+
+void GPT2::merge_lora(float sign) {
+  NoGradGuard ng;
+  auto merge = [&](Param& w, std::vector<LoraAdapter>& ads) {
+    for (auto& a : ads) {
+      Tensor A = a.A.leaf.detach().contiguous(), B = a.B.leaf.detach().contiguous();
+      Tensor rows = w.c.slice(0, a.col0, a.col0 + a.ncols);
+      ::mft::lora_merge(rows.data_ptr(), 1, 1, w.c.size(1), A.data<float>(), B.data<float>(), (int)A.size(1), a.ncols,
+                        a.rank, sign * spec_.scale(), current_stream());
+    }
+    w.wt = Tensor();
+  };
+  for (auto& b : blocks_) {
+    merge(b.attn_w, b.lqkv);
+    merge(b.proj_w, b.lproj);
+    merge(b.fc_w, b.lfc);
+    merge(b.mproj_w, b.lfcout);
+    b.waug_qkv = Tensor();
+    b.waug_proj = Tensor();
+  }
+}
+
+// ------------------------------------------------------------------ forward
+Tensor GPT2::hidden(const Tensor& ids) {
+  const int64_t B = ids.size(0), S = ids.size(1);
+  MFT_CHECK(S <= cfg_.n_positions, "sequence ", S, " exceeds n_positions ", cfg_.n_positions);
+  const int C = cfg_.n_embd, H = cfg_.n_head, D = cfg_.head_dim();
+  const float scale = spec_.scale();
+  auto aug = [&](std::vector<LoraAdapter>& ads) { return ads.empty() ? 0 : lora_aug_cols(C, ads); };
+  Tensor x = embed(ids, wte_, &wpe_, 1.f);
+  auto n0 = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, aug(blocks_[0].lqkv));
+  Tensor h = n0.second;
+  for (int i = 0; i < cfg_.n_layer; ++i) {
+    auto& b = blocks_[i];
+    // attention
+    Tensor qkv = b.lqkv.empty()
+                     ? linear_p(h, b.attn_w, &b.attn_b)
+                     : lora_linear_aug(h, C, b.attn_w, &b.attn_b, b.lqkv, scale, b.waug_qkv, training, dropout_ctr);
+    Tensor o = attention_packed(qkv.view({B, S, 3, H, D}), 1.f / std::sqrt((float)D), true, 0, aug(b.lproj));
+    o = o.view({B * S, o.size(-1)});
+    Tensor a = b.lproj.empty()
+                   ? linear_p(o, b.proj_w, &b.proj_b)
+                   : lora_linear_aug(o, C, b.proj_w, &b.proj_b, b.lproj, scale, b.waug_proj, training, dropout_ctr);
+    auto r2 = add_norm(x, a, b.ln2_w, &b.ln2_b, cfg_.eps, false, 0.f, 0);
+    x = r2.first;
+    // MLP
+    Tensor f;
+    if (b.lfc.empty() && b.lfcout.empty()) {
+      f = mlp_gelu(r2.second, b.fc_w, b.fc_b, b.mproj_w, b.mproj_b);
+    } else {
+      Tensor u = b.lfc.empty() ? linear_p(r2.second, b.fc_w, &b.fc_b)
+                               : lora_linear(r2.second, b.fc_w, &b.fc_b, b.lfc, scale, training, dropout_ctr);
+      u = gelu(u, true);
+      f = b.lfcout.empty() ? linear_p(u, b.mproj_w, &b.mproj_b)
+                           : lora_linear(u, b.mproj_w, &b.mproj_b, b.lfcout, scale, training, dropout_ctr);
+    }
+    Param* nw = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_w : &lnf_w_;
+    Param* nb = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_b : &lnf_b_;
+    const int oc = i + 1 < cfg_.n_layer ? aug(blocks_[i + 1].lqkv) : 0;
+    auto r1 = add_norm(x, f, *nw, nb, cfg_.eps, false, 0.f, oc);
+    x = r1.first;
+    h = r1.second;
+  }
+  return h;
+}
+
+Tensor GPT2::loss(const Tensor& ids, const Tensor& labels, float w_grad_scale) {
+  Tensor h = hidden(ids);
+  return lm_head_ce(h, wte_, labels, cfg_.vocab_size, ce_chunk, w_grad_scale);
+}
+
+std::pair<Tensor, Tensor> GPT2::nll(const Tensor& ids, const Tensor& labels) {
+  NoGradGuard ng;
+  const bool t = training;
+  training = false;
+  Tensor h = hidden(ids);
+  training = t;
+  return lm_head_nll(h, wte_, labels, cfg_.vocab_size, ce_chunk);
+}
+
+}  // namespace eng
+}  // namespace mft

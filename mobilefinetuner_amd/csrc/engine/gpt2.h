@@ -1,0 +1,87 @@
+// libmft engine: GPT-2 (small ... XL) with LoRA adapters, on the fused ops of nn.h.
+//
+// Reference: GPT2Config / GPT2Model (operators/finetune_ops/graph/gpt2_model.h:50-186,
+// gpt2_model.cpp:121-861), LoraSpec / LoraInjector (graph/lora_injector.h:19-191,
+// lora_injector.cpp:48-148), LoraSaver (graph/lora_saver.cpp:123-452), GPT2KeyMapper
+// (graph/safetensors_loader.cpp:294-336).  Same graph as the Python package's models/gpt2.py:
+// embedding (+wpe) -> per block [LN1 -> c_attn (LoRA, augmented K) -> flash attention on the
+// packed qkv -> c_proj (LoRA) -> residual+LN2 -> fc+GELU -> proj] -> residual+LN_f -> tied LM head
+// + vocab-chunked CE.  Weights are [out, in] (HF Conv1D [in, out] transposed once at load).
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "engine/nn.h"
+
+namespace mft {
+namespace eng {
+
+struct GPT2Config {
+  int vocab_size = 50257, n_positions = 1024, n_embd = 768, n_layer = 12, n_head = 12;
+  float eps = 1e-5f, init_range = 0.02f;
+  int vocab_padded() const { return (vocab_size + 127) / 128 * 128; }
+  int head_dim() const { return n_embd / n_head; }
+  static GPT2Config preset(const std::string& name);
+  static GPT2Config from_json(const std::string& path);
+};
+
+struct LoraSpec {
+  int rank = 8;
+  float alpha = 16.f, dropout = 0.f;
+  bool split_qkv = false;
+  std::vector<std::string> targets{"AttnQKV", "AttnProj"};  // + MlpFcIn, MlpFcOut
+  std::vector<int> layers;                                  // empty = all
+  uint64_t seed = 42;
+  float scale() const { return alpha / (float)rank; }
+  bool has(const std::string& t) const;
+};
+
+struct GPT2Block {
+  Param ln1_w, ln1_b, attn_w, attn_b, proj_w, proj_b, ln2_w, ln2_b, fc_w, fc_b, mproj_w, mproj_b;
+  std::vector<LoraAdapter> lqkv, lproj, lfc, lfcout;
+  std::vector<std::string> names_qkv, names_proj, names_fc, names_fcout;  // checkpoint keys
+  Tensor waug_qkv, waug_proj;  // augmented weights of the LoRA'd attention projections
+};
+
+class GPT2 {
+ public:
+  explicit GPT2(const GPT2Config& cfg);
+  const GPT2Config& cfg() const { return cfg_; }
+  // HF init: N(0, 0.02), residual projections N(0, 0.02 / sqrt(2L)), zero biases, wpe N(0, 0.01);
+  // counter-based RNG (engine/tensor_kernels.hip) seeded per tensor
+  void init_random(uint64_t seed);
+  // <dir>/model.safetensors (+ config.json): HF GPT-2 keys (optional "transformer." prefix)
+  void load_hf(const std::string& dir);
+  void save_hf(const std::string& path);  // full-model writer (gpt2_full_finetune)
+  // LoRA: reference init A ~ U(+-sqrt(6/(in+r))) seeded 42+in+out, B = 0
+  void inject_lora(const LoraSpec& spec);
+  void load_lora(const std::string& path);  // reference checkpoint layout (attach_from_state)
+  void save_lora(const std::string& path);  // byte-compatible with graph/lora_saver.cpp
+  void set_full_finetune();                 // every parameter trainable (fp32 master + bf16 shadow)
+  // trainable parameters in a fixed order (name, param)
+  std::vector<std::pair<std::string, Param*>> trainable();
+  std::vector<std::pair<std::string, Param*>> all_params();
+  // mean token NLL of one micro-batch (ids / labels [B, S], labels already shifted, -100 ignored)
+  Tensor loss(const Tensor& ids, const Tensor& labels, float w_grad_scale = 1.f);
+  std::pair<Tensor, Tensor> nll(const Tensor& ids, const Tensor& labels);  // (sum, count), no grad
+  Tensor hidden(const Tensor& ids);
+  void merge_lora(float sign);
+  bool training = true;
+  Tensor dropout_ctr;  // device int64 step counter (fresh LoRA-dropout masks per step)
+  int64_t ce_chunk = 0;
+  const LoraSpec& lora_spec() const { return spec_; }
+  size_t num_parameters() const;
+
+ private:
+  void alloc();
+  GPT2Config cfg_;
+  LoraSpec spec_;
+  bool lora_ = false, full_ = false;
+  Param wte_, wpe_, lnf_w_, lnf_b_;
+  std::vector<GPT2Block> blocks_;
+  void make_trainable(Param& p);
+};
+
+}  // namespace eng
+}  // namespace mft

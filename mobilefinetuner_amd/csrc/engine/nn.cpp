@@ -1,0 +1,612 @@
+// libmft engine: fused transformer ops (see nn.h).
+#include "engine/nn.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+
+#include "engine/autograd.h"
+#include "engine/gemm.h"
+#include "engine/ops.h"
+#include "kernels.h"
+
+namespace mft {
+namespace eng {
+
+namespace {
+hipStream_t S() { return current_stream(); }
+inline ::mft::bf16_t* bp(const Tensor& t) { return (::mft::bf16_t*)t.data_ptr(); }
+inline float* fp(const Tensor& t) { return (float*)t.data_ptr(); }
+inline float* fp_or_null(const Tensor& t) { return t.defined() ? (float*)t.data_ptr() : nullptr; }
+
+Tensor f32_of(Param& p) {  // norm weights are fp32 compute
+  return p.c.dtype() == DType::F32 ? p.c : p.c.to(DType::F32);
+}
+// fp32 grad buffer of a trainable param (allocated on first use), or undefined
+Tensor gbuf(Param* p) {
+  if (!p || !p->trainable()) return Tensor();
+  return grad_buffer(p->leaf);
+}
+}  // namespace
+
+const Tensor& Param::transposed() {
+  if (!wt.defined()) {
+    NoGradGuard ng;
+    wt = c.t().contiguous();
+  }
+  return wt;
+}
+
+// ------------------------------------------------------------------ norms
+namespace {
+struct NormNode : Node {
+  Tensor xs, w32, mean, rstd;
+  Param* w = nullptr;
+  Param* b = nullptr;
+  bool rms = false, has_delta = false;
+  float offset = 0.f;
+  int N = 0;
+  std::vector<Tensor> apply(std::vector<Tensor>& g) override {
+    // outputs: {s, y}; inputs: {x, delta, w.leaf, b.leaf}
+    Tensor ds = has_delta ? g[0] : Tensor();
+    Tensor dy = g[1];
+    const long M = xs.numel() / N;
+    if (!dy.defined()) dy = zeros({M, (int64_t)N}, DType::BF16, xs.device());
+    Tensor dy2 = dy.reshape({M, dy.size(-1)});
+    if (dy2.stride(1) != 1 || dy2.stride(0) % 8) dy2 = dy2.contiguous();
+    Tensor ds2 = ds.defined() ? ds.reshape({M, (int64_t)N}).contiguous() : Tensor();
+    Tensor dx = empty(xs.shape(), DType::BF16, xs.device());
+    Tensor dw = gbuf(w), db = rms ? Tensor() : gbuf(b);
+    Tensor work;
+    if (dw.defined()) work = empty({2L * ::mft::norm_bwd_partial_blocks((int)M) * N}, DType::F32, xs.device());
+    if (rms) {
+      ::mft::rmsnorm_bwd(bp(xs), bp(dy2), fp(w32), fp(rstd), ds2.defined() ? bp(ds2) : nullptr, bp(dx),
+                         fp_or_null(dw), fp_or_null(work), (int)M, N, offset, 1, dy2.stride(0), S());
+    } else {
+      ::mft::layernorm_bwd(bp(xs), bp(dy2), fp(w32), fp(mean), fp(rstd), ds2.defined() ? bp(ds2) : nullptr, bp(dx),
+                           fp_or_null(dw), fp_or_null(db), fp_or_null(work), (int)M, N, 1, dy2.stride(0), S());
+    }
+    return {dx, has_delta ? dx : Tensor(), Tensor(), Tensor()};
+  }
+};
+}  // namespace
+
+std::pair<Tensor, Tensor> add_norm(const Tensor& x, const Tensor& delta, Param& w, Param* b, float eps, bool rms,
+                                   float offset, int out_cols) {
+  const int N = (int)x.size(-1);
+  MFT_CHECK(x.dtype() == DType::BF16 && N % 8 == 0 && N <= 4096, "norm: bf16 rows, width % 8, <= 4096");
+  const long M = x.numel() / N;
+  Tensor x2 = x.detach().reshape({M, (int64_t)N}).contiguous();
+  Tensor d2 = delta.defined() ? delta.detach().reshape({M, (int64_t)N}).contiguous() : Tensor();
+  Tensor w32 = f32_of(w);
+  Tensor b32 = (!rms && b) ? f32_of(*b) : Tensor();
+  const int oc = out_cols > N ? out_cols : N;
+  MFT_CHECK(oc % 8 == 0, "norm: out_cols % 8");
+  Tensor y = empty({M, (int64_t)oc}, DType::BF16, x.device());
+  Tensor mean = rms ? Tensor() : empty({M}, DType::F32, x.device());
+  Tensor rstd = empty({M}, DType::F32, x.device());
+  Tensor s = d2.defined() ? empty({M, (int64_t)N}, DType::BF16, x.device()) : Tensor();
+  if (rms) {
+    ::mft::rmsnorm_fwd(bp(x2), d2.defined() ? bp(d2) : nullptr, s.defined() ? bp(s) : nullptr, fp(w32), bp(y),
+                       fp(rstd), (int)M, N, eps, offset, oc, S());
+  } else {
+    ::mft::layernorm_fwd(bp(x2), d2.defined() ? bp(d2) : nullptr, s.defined() ? bp(s) : nullptr, fp(w32), fp(b32),
+                         bp(y), fp(mean), fp(rstd), (int)M, N, eps, oc, S());
+  }
+  Shape ys = x.shape();
+  ys.back() = oc;
+  y = y.detach().view(ys);
+  Tensor sv = s.defined() ? s.view(x.shape()) : x;
+  auto n = std::make_shared<NormNode>();
+  n->name = rms ? "RMSNormBackward" : "LayerNormBackward";
+  n->xs = s.defined() ? s : x2;
+  n->w32 = w32;
+  n->mean = mean;
+  n->rstd = rstd;
+  n->w = &w;
+  n->b = b;
+  n->rms = rms;
+  n->has_delta = d2.defined();
+  n->offset = offset;
+  n->N = N;
+  Tensor s_out = d2.defined() ? sv : Tensor();
+  // (grads of trainable w / b land in their flat buffers inside apply())
+  connect(n, {x, delta, w.leaf, b ? b->leaf : Tensor()}, {s_out, y});
+  return {d2.defined() ? s_out : x, y};
+}
+
+// ------------------------------------------------------------------ embedding
+Tensor embed(const Tensor& ids, Param& wte, Param* wpe, float scale) {
+  MFT_CHECK(ids.dim() == 2 && ids.dtype() == DType::I64, "embed: ids [B, S] int64");
+  const long M = ids.numel();
+  const int S_ = (int)ids.size(1);
+  const int C = (int)wte.c.size(1);
+  Tensor idc = ids.contiguous();
+  Tensor out = empty({M, (int64_t)C}, DType::BF16, ids.device());
+  ::mft::embed_fwd(idc.data<int64_t>(), bp(wte.c), wpe ? bp(wpe->c) : nullptr, bp(out), M, C, S_, 0, scale, S());
+  if (wte.trainable() || (wpe && wpe->trainable())) {
+    Param* pw = &wte;
+    auto n = lambda_node("EmbeddingBackward", [idc, pw, wpe, M, C, S_, scale](std::vector<Tensor>& g) {
+      if (!g[0].defined()) return std::vector<Tensor>{Tensor(), Tensor()};
+      Tensor d = g[0].contiguous();
+      Tensor bte = gbuf(pw), bpe = gbuf(wpe);
+      ::mft::embed_bwd(idc.data<int64_t>(), bp(d), fp_or_null(bte), fp_or_null(bpe), M, C, S_, 0, scale, S());
+      return std::vector<Tensor>{Tensor(), Tensor()};
+    });
+    connect(n, {wte.leaf, wpe ? wpe->leaf : Tensor()}, {out});
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ attention
+namespace {
+void fill_st(long* st, const Tensor& t) {
+  MFT_CHECK(t.dim() == 4 && t.stride(3) == 1 && t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0,
+            "attention: [B, S, H, D] views with unit D stride and 8-aligned strides");
+  st[0] = t.stride(0);
+  st[1] = t.stride(1);
+  st[2] = t.stride(2);
+}
+}  // namespace
+
+Tensor attention_packed(const Tensor& qkv, float scale, bool causal, int window, int out_cols) {
+  MFT_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.dtype() == DType::BF16, "attention: qkv [B, S, 3, H, D] bf16");
+  const int B = (int)qkv.size(0), Sq = (int)qkv.size(1), H = (int)qkv.size(3), D = (int)qkv.size(4);
+  MFT_CHECK(D == 64 || D == 128 || D == 256, "attention: head dim 64 / 128 / 256");
+  Tensor qd = qkv.detach();
+  Tensor q = qd.select(2, 0), k = qd.select(2, 1), v = qd.select(2, 2);
+  const int HD = H * D;
+  const int oc = out_cols > HD ? out_cols : HD;
+  Tensor o_full = empty({B, Sq, (int64_t)oc}, DType::BF16, qkv.device());
+  Tensor o = o_full.slice(2, 0, HD).view({B, Sq, H, D});
+  Tensor lse = empty({B, H, Sq}, DType::F32, qkv.device());
+  ::mft::AttnArgs a{};
+  a.q = bp(q);
+  a.k = bp(k);
+  a.v = bp(v);
+  a.o = bp(o);
+  a.lse = fp(lse);
+  fill_st(a.q_st, q);
+  fill_st(a.k_st, k);
+  fill_st(a.v_st, v);
+  fill_st(a.o_st, o);
+  a.B = B;
+  a.H = H;
+  a.Hkv = H;
+  a.Sq = Sq;
+  a.Sk = Sq;
+  a.D = D;
+  a.scale = scale;
+  a.causal = causal;
+  a.window = window;
+  ::mft::attn_fwd(a, S());
+  if (oc > HD) ::mft::zero_cols(bp(o_full), oc, (long)B * Sq, HD, oc - HD, S());
+  if (needs_grad(qkv)) {
+    auto n = lambda_node("FlashAttentionBackward", [qd, o, lse, scale, causal, window, B, Sq, H, D,
+                                                     HD](std::vector<Tensor>& g) {
+      if (!g[0].defined()) return std::vector<Tensor>{Tensor()};
+      Tensor dqkv = empty(qd.shape(), DType::BF16, qd.device());
+      Tensor dout = g[0].slice(2, 0, HD).view({B, Sq, H, D});
+      if (dout.stride(3) != 1 || dout.stride(1) % 8) dout = dout.contiguous();
+      const int path = ::mft::attn_bwd_path(D, Sq, Sq, window);
+      Tensor delta, dq_acc;
+      if (path != 0) delta = empty({B, H, Sq}, DType::F32, qd.device());
+      if (path == 1) dq_acc = empty({B, Sq, H, D}, DType::F32, qd.device());
+      ::mft::AttnBwdArgs b{};
+      Tensor q = qd.select(2, 0), k = qd.select(2, 1), v = qd.select(2, 2);
+      Tensor dq = dqkv.select(2, 0), dk = dqkv.select(2, 1), dv = dqkv.select(2, 2);
+      b.q = bp(q);
+      b.k = bp(k);
+      b.v = bp(v);
+      b.o = bp(o);
+      b.dout = bp(dout);
+      b.lse = fp(lse);
+      b.delta = path != 0 ? fp(delta) : nullptr;
+      b.dq_acc = path == 1 ? fp(dq_acc) : nullptr;
+      b.dq = bp(dq);
+      b.dk = bp(dk);
+      b.dv = bp(dv);
+      fill_st(b.q_st, q);
+      fill_st(b.k_st, k);
+      fill_st(b.v_st, v);
+      fill_st(b.o_st, o);
+      fill_st(b.do_st, dout);
+      fill_st(b.dq_st, dq);
+      fill_st(b.dk_st, dk);
+      fill_st(b.dv_st, dv);
+      b.B = B;
+      b.H = H;
+      b.Hkv = H;
+      b.Sq = Sq;
+      b.Sk = Sq;
+      b.D = D;
+      b.scale = scale;
+      b.causal = causal;
+      b.window = window;
+      ::mft::attn_bwd(b, S());
+      return std::vector<Tensor>{dqkv};
+    });
+    connect(n, {qkv}, {o_full});
+  }
+  return o_full;
+}
+
+// ------------------------------------------------------------------ linear / MLP
+static void bias_grad(Param* b, const Tensor& dy2) {
+  if (!b || !b->trainable()) return;
+  Tensor buf = grad_buffer(b->leaf);
+  const long M = dy2.size(0);
+  const int N = (int)dy2.size(1);
+  const int nb = ::mft::colsum_partial_blocks(M);
+  Tensor part = empty({(int64_t)nb * N}, DType::F32, dy2.device());
+  ::mft::colsum_partial(bp(dy2), dy2.stride(0), M, N, fp(part), S());
+  ::mft::reduce_rows(fp(part), fp(buf), nb, N, 1, S());
+}
+
+Tensor linear_p(const Tensor& x, Param& w, Param* b) {
+  const int64_t K = x.size(-1), N = w.c.size(0);
+  Tensor x2 = x.detach().reshape({-1, K});
+  if (x2.stride(1) != 1 || x2.stride(0) % 8) x2 = x2.contiguous();
+  Shape ys = x.shape();
+  ys.back() = N;
+  Tensor y = empty({x2.size(0), N}, DType::BF16, x.device());
+  gemm_nt(x2, w.c, b ? b->c : Tensor(), y);
+  if (any_needs_grad({x, w.leaf, b ? b->leaf : Tensor()})) {
+    Param* pw = &w;
+    auto n = lambda_node("LinearBackward", [x2, pw, b, K, N](std::vector<Tensor>& g) {
+      if (!g[0].defined()) return std::vector<Tensor>{Tensor(), Tensor(), Tensor()};
+      Tensor dy2 = g[0].reshape({-1, N});
+      if (dy2.stride(1) != 1 || dy2.stride(0) % 8) dy2 = dy2.contiguous();
+      Tensor dx = empty({dy2.size(0), K}, DType::BF16, dy2.device());
+      gemm_nn(dy2, pw->c, dx);
+      if (pw->trainable()) {
+        Tensor buf = grad_buffer(pw->leaf).view({N, K});
+        gemm_wgrad(buf, dy2, x2);
+      }
+      bias_grad(b, dy2);
+      return std::vector<Tensor>{dx, Tensor(), Tensor()};
+    });
+    connect(n, {x, w.leaf, b ? b->leaf : Tensor()}, {y});
+  }
+  return y.view(ys);
+}
+
+Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2) {
+  const int64_t K = x.size(-1), I = w1.c.size(0), N = w2.c.size(0);
+  Tensor x2 = x.detach().reshape({-1, K}).contiguous();
+  const int64_t M = x2.size(0);
+  Tensor h = empty({M, I}, DType::BF16, x.device()), pre = empty({M, I}, DType::BF16, x.device());
+  Gemm8Extra ex;
+  ex.bias = &b1.c;
+  ex.aux = &pre;
+  gemm8_call(x2, w1.c, false, ::mft::GEMM_EPI_BIAS_GELU, h, ex);
+  Tensor y = empty({M, N}, DType::BF16, x.device());
+  gemm_nt(h, w2.c, b2.c, y);
+  Shape ys = x.shape();
+  ys.back() = N;
+  if (any_needs_grad({x, w1.leaf, b1.leaf, w2.leaf, b2.leaf})) {
+    Param *p1 = &w1, *q1 = &b1, *p2 = &w2, *q2 = &b2;
+    auto n = lambda_node("MLPGeluBackward", [x2, h, pre, p1, q1, p2, q2, M, K, I, N](std::vector<Tensor>& g) {
+      if (!g[0].defined()) return std::vector<Tensor>(5);
+      Tensor dy2 = g[0].reshape({M, N}).contiguous();
+      Tensor dpre = empty({M, I}, DType::BF16, dy2.device());
+      Gemm8Extra e2;
+      Tensor aux = pre;
+      e2.aux = &aux;
+      if (!p2->trainable()) gemm8_call(dy2, p2->transposed(), false, ::mft::GEMM_EPI_DGELU, dpre, e2);
+      else gemm8_call(dy2, p2->c, true, ::mft::GEMM_EPI_DGELU, dpre, e2);
+      Tensor dx = empty({M, K}, DType::BF16, dy2.device());
+      gemm_nn(dpre, p1->c, dx);
+      if (p2->trainable()) {
+        Tensor b2v = grad_buffer(p2->leaf).view({N, I});
+        gemm_wgrad(b2v, dy2, h);
+      }
+      if (p1->trainable()) {
+        Tensor b1v = grad_buffer(p1->leaf).view({I, K});
+        gemm_wgrad(b1v, dpre, x2);
+      }
+      bias_grad(q2, dy2);
+      bias_grad(q1, dpre);
+      return std::vector<Tensor>{dx, Tensor(), Tensor(), Tensor(), Tensor()};
+    });
+    connect(n, {x, w1.leaf, b1.leaf, w2.leaf, b2.leaf}, {y});
+  }
+  return y.view(ys);
+}
+
+// ------------------------------------------------------------------ LoRA (augmented K)
+int lora_aug_cols(int in_features, const std::vector<LoraAdapter>& ads) {
+  int r = 0;
+  for (auto& a : ads) r += a.rank;
+  return (in_features + r + 63) / 64 * 64;
+}
+
+Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<LoraAdapter>& ads, float s,
+                       Tensor& waug, bool training, const Tensor& drop_ctr) {
+  MFT_CHECK(!w.trainable(), "lora_linear_aug: the base weight must be frozen");
+  const int64_t Ka = xa.size(-1), N = w.c.size(0);
+  Tensor xa2 = xa.detach().reshape({-1, Ka});
+  MFT_CHECK(xa2.stride(1) == 1, "lora_linear_aug: input rows must be contiguous");
+  const int64_t M = xa2.size(0);
+  Tensor x2 = xa2.slice(1, 0, K);
+  if (!waug.defined() || waug.size(1) != Ka) {
+    NoGradGuard ng;
+    waug = zeros({N, Ka}, DType::BF16, xa.device());
+    Tensor wl = waug.slice(1, 0, K);
+    wl.copy_(w.c);
+  }
+  bool nodrop = true;
+  for (auto& a : ads) nodrop = nodrop && (a.dropout <= 0.f || !training);
+  int off = K;
+  if (nodrop && ads.size() > 1) {  // one pass over x for every u_i (adjacent appended columns)
+    std::vector<Tensor> as;
+    for (auto& a : ads) as.push_back(a.A.c);
+    Tensor acat;
+    {
+      NoGradGuard ng;
+      acat = cat(as, 0);
+    }
+    const int R = (int)acat.size(0);
+    ::mft::lora_rowdot(bp(x2), x2.stride(0), bp(acat), acat.stride(0), bp(xa2) + K, xa2.stride(0), M, K, R, 1.f,
+                       ::mft::LoraDrop{nullptr, 0, 0.f}, S());
+  }
+  for (auto& a : ads) {
+    const int R = a.rank;
+    if (!(nodrop && ads.size() > 1)) {
+      ::mft::LoraDrop d{drop_ctr.defined() ? drop_ctr.data<int64_t>() : nullptr, a.salt, training ? a.dropout : 0.f};
+      ::mft::lora_rowdot(bp(x2), x2.stride(0), bp(a.A.c), a.A.c.stride(0), bp(xa2) + off, xa2.stride(0), M, K, R, 1.f,
+                         d, S());
+    }
+    // s B_i^T into the slice's rows of the augmented weight
+    Tensor dst = waug.slice(0, a.col0, a.col0 + a.ncols).slice(1, off, off + R);
+    k::unary(desc(dst), desc(a.B.c.t()), k::U_AFFINE, s, 0.f, S());
+    off += R;
+  }
+  Tensor y = empty({M, N}, DType::BF16, xa.device());
+  gemm_nt(xa2, waug, b ? b->c : Tensor(), y);
+  Shape ys = xa.shape();
+  ys.back() = N;
+  std::vector<Tensor> ins{xa};
+  for (auto& a : ads) {
+    ins.push_back(a.A.leaf);
+    ins.push_back(a.B.leaf);
+  }
+  if (any_needs_grad(ins)) {
+    Param* pw = &w;
+    std::vector<LoraAdapter>* pads = &ads;
+    Tensor wa = waug;
+    Shape xshape = xa.shape();
+    auto n = lambda_node("LoRALinearBackward", [xa2, xshape, K, Ka, M, N, pw, pads, s, wa, training, drop_ctr,
+                                                 nin = ins.size()](std::vector<Tensor>& g) {
+      std::vector<Tensor> out(nin);
+      if (!g[0].defined()) return out;
+      auto& ads = *pads;
+      Tensor dy2 = g[0].reshape({M, N});
+      if (dy2.stride(1) != 1 || dy2.stride(0) % 8) dy2 = dy2.contiguous();
+      Tensor x2 = xa2.slice(1, 0, K);
+      int rt = 0;
+      bool nodrop = true;
+      for (auto& a : ads) {
+        rt += a.rank;
+        nodrop = nodrop && (a.dropout <= 0.f || !training);
+      }
+      const bool fused = nodrop && rt > 0 && rt <= 32 && rt % 8 == 0 && N % 64 == 0 && K % 8 == 0;
+      Tensor dxa = empty({M, Ka}, DType::BF16, dy2.device());
+      Tensor dx = dxa.slice(1, 0, K);
+      Tensor vall = empty({M, (int64_t)std::max(rt, 8)}, DType::BF16, dy2.device());
+      int o = 0;
+      std::vector<bool> db_done(ads.size(), false);
+      for (size_t i = 0; i < ads.size(); ++i) {
+        auto& a = ads[i];
+        Tensor v = vall.slice(1, o, o + a.rank);
+        Tensor dys = dy2.slice(1, a.col0, a.col0 + a.ncols);
+        Tensor dB = a.B.trainable() ? grad_buffer(a.B.leaf) : Tensor();
+        if (dB.defined() && a.rank == 8 && a.ncols % 8 == 0 && a.col0 % 8 == 0 && (K + o) % 8 == 0) {
+          Tensor vpart = empty({(int64_t)((a.ncols + 255) / 256) * M * 8}, DType::F32, dy2.device());
+          ::mft::lora_dy(bp(dys), dys.stride(0), bp(a.B.c), a.B.c.stride(0), bp(xa2) + K + o, xa2.stride(0), fp(dB),
+                         a.ncols, fp(vpart), bp(v), v.stride(0), M, a.ncols, s, S());
+          db_done[i] = true;
+        } else {
+          ::mft::lora_rowdot(bp(dys), dys.stride(0), bp(a.B.c), a.B.c.stride(0), bp(v), v.stride(0), M, a.ncols,
+                             a.rank, s, ::mft::LoraDrop{nullptr, 0, 0.f}, S());
+        }
+        o += a.rank;
+      }
+      Tensor acat;
+      {
+        std::vector<Tensor> as;
+        for (auto& a : ads) as.push_back(a.A.c);
+        acat = as.size() == 1 ? as[0] : cat(as, 0);
+      }
+      if (fused) {
+        Gemm8Extra ex;
+        Tensor vu = vall.slice(1, 0, rt);
+        ex.lora_u = &vu;
+        ex.lora_w = &acat;
+        gemm8_call(dy2, pw->transposed(), false, ::mft::GEMM_EPI_LORA, dx, ex);
+      } else {
+        gemm_nn(dy2, wa.slice(1, 0, K), dx);
+        o = 0;
+        for (auto& a : ads) {
+          Tensor v = vall.slice(1, o, o + a.rank);
+          ::mft::LoraDrop d{drop_ctr.defined() ? drop_ctr.data<int64_t>() : nullptr, a.salt,
+                            training ? a.dropout : 0.f};
+          ::mft::lora_update(bp(dx), dx.stride(0), bp(v), v.stride(0), bp(a.A.c), a.A.c.stride(0), bp(dx),
+                             dx.stride(0), M, (int)K, a.rank, 1.f, d, S());
+          o += a.rank;
+        }
+      }
+      // dA (one pass over x for several rank-8 adapters) and the remaining dB
+      bool da_done = false;
+      if (nodrop && ads.size() > 1 && ads.size() <= 8) {
+        bool all8 = true;
+        for (auto& a : ads) all8 = all8 && a.rank == 8 && a.A.trainable();
+        if (all8) {
+          ::mft::WgradOuts wo{};
+          wo.n = (int)ads.size();
+          for (size_t i = 0; i < ads.size(); ++i) wo.p[i] = fp(grad_buffer(ads[i].A.leaf));
+          ::mft::lora_wgrad(bp(x2), x2.stride(0), bp(vall), vall.stride(0), nullptr, 1, K, M, K, rt, 1.f,
+                            ::mft::LoraDrop{nullptr, 0, 0.f}, S(), &wo);
+          da_done = true;
+        }
+      }
+      o = 0;
+      int off = K;
+      for (size_t i = 0; i < ads.size(); ++i) {
+        auto& a = ads[i];
+        Tensor v = vall.slice(1, o, o + a.rank);
+        if (!da_done && a.A.trainable()) {
+          ::mft::LoraDrop d{drop_ctr.defined() ? drop_ctr.data<int64_t>() : nullptr, a.salt,
+                            training ? a.dropout : 0.f};
+          ::mft::lora_wgrad(bp(x2), x2.stride(0), bp(v), v.stride(0), fp(grad_buffer(a.A.leaf)), 1, K, M, K, a.rank,
+                            1.f, d, S());
+        }
+        if (a.B.trainable() && !db_done[i]) {
+          Tensor dys = dy2.slice(1, a.col0, a.col0 + a.ncols);
+          ::mft::lora_wgrad(bp(dys), dys.stride(0), bp(xa2) + off, xa2.stride(0), fp(grad_buffer(a.B.leaf)), 1,
+                            a.ncols, M, a.ncols, a.rank, s, ::mft::LoraDrop{nullptr, 0, 0.f}, S());
+        }
+        o += a.rank;
+        off += a.rank;
+      }
+      out[0] = dxa.view(xshape);
+      return out;
+    });
+    connect(n, ins, {y});
+  }
+  return y.view(ys);
+}
+
+Tensor lora_linear(const Tensor& x, Param& w, Param* b, std::vector<LoraAdapter>& ads, float s, bool training,
+                   const Tensor& drop_ctr) {
+  MFT_CHECK(!w.trainable(), "lora_linear: the base weight must be frozen");
+  const int64_t K = x.size(-1), N = w.c.size(0);
+  Tensor x2 = x.detach().reshape({-1, K});
+  if (x2.stride(1) != 1 || x2.stride(0) % 8) x2 = x2.contiguous();
+  const int64_t M = x2.size(0);
+  Tensor y = empty({M, N}, DType::BF16, x.device());
+  gemm_nt(x2, w.c, b ? b->c : Tensor(), y);
+  std::vector<Tensor> us;
+  for (auto& a : ads) {
+    Tensor u = empty({M, (int64_t)a.rank}, DType::BF16, x.device());
+    ::mft::LoraDrop d{drop_ctr.defined() ? drop_ctr.data<int64_t>() : nullptr, a.salt, training ? a.dropout : 0.f};
+    ::mft::lora_rowdot(bp(x2), x2.stride(0), bp(a.A.c), a.A.c.stride(0), bp(u), u.stride(0), M, (int)K, a.rank, 1.f, d,
+                       S());
+    Tensor ys = y.slice(1, a.col0, a.col0 + a.ncols);
+    ::mft::lora_update(bp(ys), ys.stride(0), bp(u), u.stride(0), bp(a.B.c), a.B.c.stride(0), bp(ys), ys.stride(0), M,
+                       a.ncols, a.rank, s, ::mft::LoraDrop{nullptr, 0, 0.f}, S());
+    us.push_back(u);
+  }
+  Shape ys = x.shape();
+  ys.back() = N;
+  std::vector<Tensor> ins{x};
+  for (auto& a : ads) {
+    ins.push_back(a.A.leaf);
+    ins.push_back(a.B.leaf);
+  }
+  if (any_needs_grad(ins)) {
+    Param* pw = &w;
+    std::vector<LoraAdapter>* pads = &ads;
+    Shape xshape = x.shape();
+    auto n = lambda_node("LoRALinearBackward", [x2, xshape, us, K, M, N, pw, pads, s, training, drop_ctr,
+                                                 nin = ins.size()](std::vector<Tensor>& g) {
+      std::vector<Tensor> out(nin);
+      if (!g[0].defined()) return out;
+      Tensor dy2 = g[0].reshape({M, N});
+      if (dy2.stride(1) != 1 || dy2.stride(0) % 8) dy2 = dy2.contiguous();
+      Tensor dx = empty({M, K}, DType::BF16, dy2.device());
+      gemm_nn(dy2, pw->c, dx);
+      for (size_t i = 0; i < pads->size(); ++i) {
+        auto& a = (*pads)[i];
+        ::mft::LoraDrop d{drop_ctr.defined() ? drop_ctr.data<int64_t>() : nullptr, a.salt, training ? a.dropout : 0.f};
+        Tensor dys = dy2.slice(1, a.col0, a.col0 + a.ncols);
+        Tensor v = empty({M, (int64_t)a.rank}, DType::BF16, dy2.device());
+        ::mft::lora_rowdot(bp(dys), dys.stride(0), bp(a.B.c), a.B.c.stride(0), bp(v), v.stride(0), M, a.ncols, a.rank,
+                           s, ::mft::LoraDrop{nullptr, 0, 0.f}, S());
+        ::mft::lora_update(bp(dx), dx.stride(0), bp(v), v.stride(0), bp(a.A.c), a.A.c.stride(0), bp(dx), dx.stride(0),
+                           M, (int)K, a.rank, 1.f, d, S());
+        if (a.A.trainable())
+          ::mft::lora_wgrad(bp(x2), x2.stride(0), bp(v), v.stride(0), fp(grad_buffer(a.A.leaf)), 1, K, M, (int)K,
+                            a.rank, 1.f, d, S());
+        if (a.B.trainable())
+          ::mft::lora_wgrad(bp(dys), dys.stride(0), bp(us[i]), us[i].stride(0), fp(grad_buffer(a.B.leaf)), 1, a.ncols,
+                            M, a.ncols, a.rank, s, ::mft::LoraDrop{nullptr, 0, 0.f}, S());
+      }
+      out[0] = dx.view(xshape);
+      return out;
+    });
+    connect(n, ins, {y});
+  }
+  return y.view(ys);
+}
+
+// ------------------------------------------------------------------ LM head + cross entropy
+namespace {
+Tensor inv_valid(const Tensor& labels) {
+  NoGradGuard ng;
+  Tensor cnt = empty({1}, DType::F32, labels.device());
+  k::count_valid(labels.data<int64_t>(), labels.numel(), -100, fp(cnt), S());
+  Tensor one = ones({1}, DType::F32, labels.device());
+  return div(one, maximum(cnt, one));
+}
+}  // namespace
+
+Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk, float w_grad_scale) {
+  const int64_t M = h.size(0), C = h.size(1), Vp = w.c.size(0);
+  Tensor hc = h.detach().contiguous();
+  Tensor lab = labels.reshape({-1}).contiguous();
+  Tensor scale = inv_valid(lab);
+  Tensor loss_rows = empty({M}, DType::F32, h.device());
+  const bool need_h = needs_grad(h);
+  const bool need_w = w.trainable() && grad_enabled();
+  const bool need = need_h || need_w;
+  Tensor dh = need ? empty({M, C}, DType::BF16, h.device()) : Tensor();
+  Tensor wbuf = need_w ? grad_buffer(w.leaf).view({Vp, C}) : Tensor();
+  if (chunk <= 0) chunk = M;
+  for (int64_t i = 0; i < M; i += chunk) {
+    const int64_t r = std::min(chunk, M - i);
+    Tensor hi = hc.slice(0, i, i + r);
+    Tensor logits = empty({r, Vp}, DType::BF16, h.device());
+    gemm_nt(hi, w.c, Tensor(), logits);
+    ::mft::xent_fwd_bwd(bp(logits), lab.data<int64_t>() + i, fp(loss_rows) + i, r, V, Vp, fp(scale), 1.f, need ? 1 : 0,
+                        S());
+    if (need) {
+      Tensor dhi = dh.slice(0, i, i + r);
+      gemm_nn(logits, w.c, dhi);
+      if (need_w) gemm_wgrad(wbuf, logits, hi, w_grad_scale);
+    }
+  }
+  Tensor loss = mul(sum(loss_rows), scale);
+  if (need) {
+    auto n = lambda_node("LMHeadCEBackward", [dh, M](std::vector<Tensor>& g) {
+      if (!g[0].defined()) return std::vector<Tensor>{Tensor(), Tensor()};
+      Tensor gs = g[0].to(DType::F32).contiguous();
+      Tensor out = empty(dh.shape(), DType::BF16, dh.device());
+      ::mft::scale_bf16(bp(dh), bp(out), dh.numel(), fp(gs), 1.f, S());
+      return std::vector<Tensor>{out, Tensor()};
+    });
+    connect(n, {h, w.leaf}, {loss});
+  }
+  return loss;
+}
+
+std::pair<Tensor, Tensor> lm_head_nll(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk) {
+  NoGradGuard ng;
+  const int64_t M = h.size(0), Vp = w.c.size(0);
+  Tensor hc = h.detach().contiguous();
+  Tensor lab = labels.reshape({-1}).contiguous();
+  Tensor loss_rows = empty({M}, DType::F32, h.device());
+  if (chunk <= 0) chunk = M;
+  for (int64_t i = 0; i < M; i += chunk) {
+    const int64_t r = std::min(chunk, M - i);
+    Tensor logits = empty({r, Vp}, DType::BF16, h.device());
+    gemm_nt(hc.slice(0, i, i + r), w.c, Tensor(), logits);
+    ::mft::xent_fwd_bwd(bp(logits), lab.data<int64_t>() + i, fp(loss_rows) + i, r, V, Vp, nullptr, 1.f, 0, S());
+  }
+  Tensor cnt = empty({1}, DType::F32, h.device());
+  k::count_valid(lab.data<int64_t>(), lab.numel(), -100, fp(cnt), S());
+  return {sum(loss_rows), cnt};
+}
+
+}  // namespace eng
+}  // namespace mft

@@ -1,0 +1,68 @@
+// libmft engine: the fused transformer ops the models are built from (autograd-aware).
+//
+// Each op wraps one or two of the gfx950 kernels of csrc/kernels/*.hip and records ONE node:
+//   add_layer_norm   residual add + LayerNorm fwd/bwd (norm.hip)       reference ops.cpp:1404-1458
+//   embed            token + position embedding gather / scatter-add    gpt2_model.cpp:346-381,500-528
+//   attention_packed causal flash attention on the packed qkv GEMM output (attention.hip)
+//                    reference memory_efficient_attention.cpp:40-185 (forward only there)
+//   mlp_gelu         fc GEMM + bias + GELU epilogue, proj GEMM; backward dGELU fused (gemm8.hip)
+//   lora_linear_aug  base GEMM over the augmented K dim [x | u] . [W | s B^T]^T (lora.hip + GEMM)
+//                    reference LoRALinear nn/lora_linear.cpp:47-108
+//   lm_head_ce       tied LM head + vocab-chunked cross entropy fwd+bwd (xent.hip + gemm8)
+//                    reference lm_loss.cpp:19-210, gpt2_model.cpp:425-439
+// Trainable parameters are fp32 masters (autograd leaves; their .grad is a view into the
+// optimizer's flat fp32 buffer) with bf16 compute shadows; the kernels accumulate straight into
+// those grad buffers.  A `Param` pairs the leaf with its compute view.
+#pragma once
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+#include "engine/tensor.h"
+
+namespace mft {
+namespace eng {
+
+struct Param {
+  Tensor leaf;  // autograd leaf: fp32 master (trainable) or the frozen compute weight itself
+  Tensor c;     // compute view: bf16 shadow (trainable) or == leaf (frozen)
+  Tensor wt;    // cached [in, out] transposed copy of a FROZEN 2-D weight (NT data-grad GEMMs)
+  bool trainable() const { return leaf.defined() && leaf.requires_grad(); }
+  const Tensor& transposed();  // builds wt once (frozen weights only)
+};
+
+// s = x + delta (if delta defined), y = LayerNorm(s) (or RMSNorm(1+w) when rms); y allocated
+// [M, out_cols] when out_cols > N (appended columns zeroed, for a LoRA consumer's augmented input).
+// Returns {s, y} (s == x when no delta).
+std::pair<Tensor, Tensor> add_norm(const Tensor& x, const Tensor& delta, Param& w, Param* b, float eps, bool rms,
+                                   float offset, int out_cols);
+Tensor embed(const Tensor& ids, Param& wte, Param* wpe, float scale);
+// qkv [B, S, 3, H, D] -> o [B, S, H*D] (or [B, S, out_cols] with zeroed tail when out_cols > H*D)
+Tensor attention_packed(const Tensor& qkv, float scale, bool causal, int window, int out_cols);
+Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2);
+// y = x W^T + b on bf16 [M, K] rows (trainable or frozen W)
+Tensor linear_p(const Tensor& x, Param& w, Param* b);
+
+struct LoraAdapter {
+  int col0 = 0, ncols = 0, rank = 8;
+  Param A, B;  // A [r, in], B [r, ncols] (fp32 masters + bf16 shadows)
+  float dropout = 0.f;
+  uint32_t salt = 0;
+};
+// width of the augmented input [x | u_1..u_n | 0]: in + sum(r), rounded to 64
+int lora_aug_cols(int in_features, const std::vector<LoraAdapter>& ads);
+// xa [M, Ka] holds x in its first K columns (zero tail); waug [N, Ka] = [W | s B^T.. | 0] (owned by
+// the caller, W copied once); W frozen.
+Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<LoraAdapter>& ads, float scale,
+                       Tensor& waug, bool training, const Tensor& drop_ctr);
+// plain (non-augmented) LoRA Linear: y = x W^T + b + s * (drop(x) A_i^T) B_i in column slices
+Tensor lora_linear(const Tensor& x, Param& w, Param* b, std::vector<LoraAdapter>& ads, float scale, bool training,
+                   const Tensor& drop_ctr);
+// mean token NLL of logits = h W^T over the first V columns (labels -100 ignored); the W gradient
+// (tied embedding in full fine-tuning) is produced during forward scaled by w_grad_scale
+Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk, float w_grad_scale);
+// (sum of NLL over valid rows, number of valid rows) without gradients -- evaluation
+std::pair<Tensor, Tensor> lm_head_nll(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk);
+
+}  // namespace eng
+}  // namespace mft

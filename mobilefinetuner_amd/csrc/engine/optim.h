@@ -1,0 +1,65 @@
+// libmft engine: flat parameter storage, fused AdamW with global-norm clipping, LR schedules.
+//
+// Reference: Adam (operators/finetune_ops/optim/adam.h:23-104, adam.cpp:25-140: bias-corrected,
+// coupled L2 decay, per-tensor state map), the clip_grad_norm copies (gpt2_lora_finetune/main.cpp:
+// 491-516) and the three LR schedules (main.cpp:470-488, gemma_trainer.cpp:63-82,
+// trainer.cpp:44-64).  MI355X design (same as the Python package's utils/params.py + optim/adamw.py):
+// every trainable parameter lives in ONE fp32 master buffer with ONE fp32 grad buffer and ONE bf16
+// compute shadow; one sumsq reduction, one non-finite check and one fused AdamW launch per step,
+// lr / step / norm^2 in device memory so the whole optimizer step replays inside a hipGraph.
+#pragma once
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "engine/nn.h"
+
+namespace mft {
+namespace eng {
+
+class FlatParams {
+ public:
+  // re-homes every param: leaf -> view of `master` (requires grad, .grad = view of `grad`),
+  // compute view -> view of `shadow` (bf16) unless the param computes in fp32
+  explicit FlatParams(std::vector<std::pair<std::string, Param*>> params);
+  Tensor master, grad, shadow;
+  int64_t numel = 0;
+  std::vector<std::pair<std::string, Param*>> params;
+  std::vector<int64_t> offsets;
+  void zero_grad();
+  void refresh_shadow();
+};
+
+struct AdamWConfig {
+  float lr = 1e-4f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, weight_decay = 0.f;
+  float max_grad_norm = 1.f;  // <= 0: no clipping
+  bool l2_coupled = false;    // reference Adam (L2 added to the gradient)
+  bool skip_nonfinite = true;
+};
+
+class AdamW {
+ public:
+  AdamW(FlatParams& flat, const AdamWConfig& cfg);
+  void set_lr(float lr);  // host -> device scalar (outside graph capture)
+  void step();            // device-only work: capturable
+  float grad_norm() const;  // host sync
+  bool skipped_last() const;
+  int64_t applied_steps() const;
+  Tensor m, v, lr_dev, step_dev, sumsq_dev, nonfinite_dev, skipped_dev;
+  const AdamWConfig& config() const { return cfg_; }
+  void load_state(const Tensor& m_h, const Tensor& v_h, int64_t steps);
+
+ private:
+  FlatParams& flat_;
+  AdamWConfig cfg_;
+};
+
+// (a) GPT-2 CLIs: linear warmup (step+1)/W, then cosine to min_ratio of lr (0-indexed step)
+float gpt2_cli_lr(int64_t step, float base, int64_t warmup, int64_t total, float min_ratio = 0.1f);
+// (b) Gemma trainer: warmup = ceil(ratio * total), 1-indexed, then linear (or cosine) to 0
+float gemma_lr(int64_t step, float base, float warmup_ratio, int64_t total, bool cosine = false);
+// (c) LoRATrainer: linear / cosine after warmup
+float trainer_lr(int64_t step, float base, int64_t warmup, int64_t total, bool cosine = false);
+
+}  // namespace eng
+}  // namespace mft

@@ -1,0 +1,189 @@
+// libmft engine: training loop (see trainer.h).
+#include "engine/trainer.h"
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <thread>
+
+#include "engine/allocator.h"
+#include "engine/autograd.h"
+#include "engine/ops.h"
+
+namespace mft {
+namespace eng {
+
+Trainer::Trainer(GPT2& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid,
+                 const TrainConfig& cfg, PowerMonitor* pm)
+    : model_(model), flat_(flat), opt_(opt), train_(train), valid_(valid), cfg_(cfg), pm_(pm) {
+  stream_ = current_stream();
+  const int64_t micro = cfg.batch, accum = std::max(1, cfg.accum);
+  const int64_t n_local = (int64_t)train.num_local();
+  steps_per_epoch_ = std::max<int64_t>(1, (n_local + micro * accum - 1) / (micro * accum));
+  total_steps_ = cfg.steps;
+  if (cfg.epochs > 0) total_steps_ = steps_per_epoch_ * cfg.epochs;
+  for (int i = 0; i < accum; ++i) {
+    ids_.push_back(zeros({micro, cfg.seq}, DType::I64));
+    labels_.push_back(full({micro, cfg.seq}, -100.0, DType::I64));
+  }
+  loss_acc_ = zeros({1}, DType::F32);
+  one_ = ones({1}, DType::I64);
+}
+
+Trainer::~Trainer() {
+  if (exec_) (void)hipGraphExecDestroy(exec_);
+  if (graph_) (void)hipGraphDestroy(graph_);
+}
+
+void Trainer::eager_step() {
+  const float inv = 1.f / (float)ids_.size();
+  flat_.zero_grad();
+  loss_acc_.zero_();
+  {
+    // fresh LoRA-dropout masks every step (device counter, advanced inside the graph too)
+    k::Desc c = desc(model_.dropout_ctr);
+    k::binary(c, c, desc(one_), k::B_ADD, 1.f, current_stream());
+  }
+  for (size_t i = 0; i < ids_.size(); ++i) {
+    Tensor loss = model_.loss(ids_[i], labels_[i], inv);
+    Tensor scaled = mul_scalar(loss, inv);
+    backward({scaled});
+    add_(loss_acc_, loss.detach(), inv);
+  }
+  opt_.step();
+}
+
+void Trainer::capture() {
+  auto& al = CachingAllocator::get(0);
+  pool_ = al.new_pool();
+  CachingAllocator::set_current_pool(pool_);
+  HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
+  eager_step();
+  HIP_OK(hipStreamEndCapture(stream_, &graph_));
+  CachingAllocator::set_current_pool(0);
+  HIP_OK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+}
+
+Tensor Trainer::step(const std::vector<std::pair<const int64_t*, const int64_t*>>& micro) {
+  MFT_CHECK(micro.size() == ids_.size(), "trainer: expected ", ids_.size(), " micro-batches");
+  for (size_t i = 0; i < micro.size(); ++i) {
+    Tensor hi = from_blob(const_cast<int64_t*>(micro[i].first), ids_[i].shape(), DType::I64, Device::cpu());
+    Tensor hl = from_blob(const_cast<int64_t*>(micro[i].second), labels_[i].shape(), DType::I64, Device::cpu());
+    ids_[i].copy_(hi);
+    labels_[i].copy_(hl);
+  }
+  if (!cfg_.use_graph) {
+    eager_step();
+  } else if (!exec_) {
+    if (warm_ < 2) {
+      ++warm_;
+      eager_step();
+    } else {
+      capture();
+      HIP_OK(hipGraphLaunch(exec_, stream_));
+    }
+  } else {
+    HIP_OK(hipGraphLaunch(exec_, stream_));
+  }
+  return loss_acc_;
+}
+
+std::pair<double, double> Trainer::evaluate(int max_batches, int batch_size) {
+  if (!valid_) return {0.0, 0.0};
+  NoGradGuard ng;
+  valid_->reset_cursor();
+  const int S = cfg_.seq;
+  std::vector<int64_t> ids((size_t)batch_size * S), tg((size_t)batch_size * S);
+  std::vector<float> mk((size_t)batch_size * S);
+  double nll = 0.0, cnt = 0.0;
+  int done = 0;
+  const bool tr = model_.training;
+  model_.training = false;
+  while (max_batches <= 0 || done < max_batches) {
+    const int got = valid_->next_batch(batch_size, false, ids.data(), tg.data(), mk.data(), nullptr);
+    if (got == 0) break;
+    Tensor di = from_host(ids.data(), {batch_size, S}, DType::I64);
+    Tensor dl = from_host(tg.data(), {batch_size, S}, DType::I64);
+    auto r = model_.nll(di, dl);
+    nll += r.first.item();
+    cnt += r.second.item();
+    ++done;
+  }
+  model_.training = tr;
+  const double m = nll / std::max(1.0, cnt);
+  return {m, std::exp(std::min(m, 50.0))};
+}
+
+void Trainer::train(const std::function<void(int64_t)>& save_fn) {
+  if (total_steps_ <= 0) {
+    std::printf("[Train] nothing to do (steps=0)\n");
+    return;
+  }
+  const int B = cfg_.batch, S = cfg_.seq, A = (int)ids_.size();
+  std::vector<std::vector<int64_t>> hid(A, std::vector<int64_t>((size_t)B * S)),
+      htg(A, std::vector<int64_t>((size_t)B * S));
+  std::vector<float> mk((size_t)B * S);
+  std::ofstream metrics;
+  if (!cfg_.metrics_out.empty()) metrics.open(cfg_.metrics_out, std::ios::app);
+  auto t_last = std::chrono::steady_clock::now();
+  int64_t tok_since = 0, steps_since = 0;
+  for (int64_t it = 0; it < total_steps_; ++it) {
+    const float lr = gpt2_cli_lr(it, cfg_.lr, cfg_.warmup, total_steps_);
+    opt_.set_lr(lr);
+    std::vector<std::pair<const int64_t*, const int64_t*>> micro;
+    int64_t tokens = 0;
+    for (int a = 0; a < A; ++a) {
+      train_.next_batch(B, true, hid[a].data(), htg[a].data(), mk.data(), nullptr);
+      for (float m : mk) tokens += m > 0.f;
+      micro.push_back({hid[a].data(), htg[a].data()});
+    }
+    Tensor loss = step(micro);
+    ++global_step;
+    total_tokens += tokens;
+    tok_since += tokens;
+    ++steps_since;
+    const bool log_now = cfg_.log_interval > 0 && (global_step % cfg_.log_interval == 0 || it + 1 == total_steps_);
+    if (log_now) {
+      const float l = (float)loss.item();  // syncs the stream
+      const auto now = std::chrono::steady_clock::now();
+      const double dt = std::chrono::duration<double>(now - t_last).count();
+      t_last = now;
+      step_ms = dt * 1e3 / std::max<int64_t>(1, steps_since);
+      const double tps = tok_since / std::max(dt, 1e-9);
+      tok_since = 0;
+      steps_since = 0;
+      losses.push_back(l);
+      ema_loss = ema_init ? cfg_.ema_beta * ema_loss + (1.0 - cfg_.ema_beta) * l : l;
+      ema_init = true;
+      const float gn = opt_.grad_norm();
+      std::printf("[Step %lld/%lld] Loss=%.4f PPL=%.2f LR=%.6g GradNorm=%.4f EMA=%.4f tok/s=%.0f step_ms=%.2f\n",
+                  (long long)global_step, (long long)total_steps_, l, std::exp(std::min<double>(l, 50.0)), lr, gn,
+                  ema_loss, tps, step_ms);
+      std::fflush(stdout);
+      if (metrics.is_open()) {
+        metrics << "{\"step\": " << global_step << ", \"loss\": " << l << ", \"lr\": " << lr << ", \"grad_norm\": " << gn
+                << ", \"tokens_per_s\": " << tps << ", \"step_ms\": " << step_ms << "}\n";
+        metrics.flush();
+      }
+    }
+    if (cfg_.eval_interval > 0 && global_step % cfg_.eval_interval == 0 && valid_) {
+      auto ev = evaluate(cfg_.eval_batches, cfg_.eval_batch_size);
+      std::printf("\n[Eval] step %lld | valid_nll %.4f | valid_ppl %.2f\n\n", (long long)global_step, ev.first,
+                  ev.second);
+      if (!cfg_.eval_out.empty()) {
+        std::ofstream eo(cfg_.eval_out, std::ios::app);
+        eo << "{\"step\": " << global_step << ", \"nll\": " << ev.first << ", \"ppl\": " << ev.second << "}\n";
+      }
+    }
+    if (cfg_.save_every > 0 && global_step % cfg_.save_every == 0 && save_fn) save_fn(global_step);
+    if (pm_) {
+      const int ms = pm_->suggest_sleep_ms(global_step);
+      if (ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+    }
+  }
+  synchronize();
+}
+
+}  // namespace eng
+}  // namespace mft

@@ -1,0 +1,78 @@
+// libmft engine: the training loop (micro-batch accumulation, hipGraph-captured step, eval, logs).
+//
+// Reference call stack: gpt2_lora_finetune/main.cpp:561-684 -- per step `accum`
+// micro-batches of forward -> lm_cross_entropy -> loss/accum -> backward, clip_and_get_grad_norm,
+// lr schedule, Adam::step, zero_grad, force_cleanup; eval every eval_interval (JSONL), periodic
+// LoRA checkpoints, power-monitor sleep.  MI355X design: the whole step (zero-grad, every
+// micro-batch forward+backward, clip, AdamW) is captured ONCE into a hipGraph after two eager
+// warm-up steps (relaxed capture mode, private allocator pool) and replayed with the next batch
+// copied into the graph's static input buffers; the loss stays on the device and is read only when
+// a log line is due.
+#pragma once
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "engine/gpt2.h"
+#include "engine/optim.h"
+#include "runtime/dataset.h"
+#include "runtime/power_monitor.h"
+
+namespace mft {
+namespace eng {
+
+struct TrainConfig {
+  int epochs = 0;
+  int64_t steps = 0;
+  int batch = 1, accum = 1, seq = 128;
+  int warmup = 0;
+  float lr = 1e-4f;  // base learning rate of the schedule
+  int log_interval = 1, eval_interval = 0, eval_batches = 50, eval_batch_size = 2, save_every = 0;
+  float ema_beta = 0.9f;
+  bool use_graph = true;
+  std::string eval_out, metrics_out;
+  int pm_interval = 0;
+};
+
+class Trainer {
+ public:
+  Trainer(GPT2& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid, const TrainConfig& cfg,
+          PowerMonitor* pm = nullptr);
+  ~Trainer();
+  int64_t total_steps() const { return total_steps_; }
+  int64_t steps_per_epoch() const { return steps_per_epoch_; }
+  // one optimizer step on `accum` micro-batches (host int64 [B, S] ids / targets); returns the
+  // device loss (mean over micro-batches)
+  Tensor step(const std::vector<std::pair<const int64_t*, const int64_t*>>& micro);
+  void train(const std::function<void(int64_t)>& save_fn);
+  std::pair<double, double> evaluate(int max_batches, int batch_size);  // (nll, ppl)
+  double ema_loss = 0.0;
+  bool ema_init = false;
+  int64_t global_step = 0, total_tokens = 0;
+  std::vector<float> losses;  // per-step mean loss (read at log points)
+  double step_ms = 0.0;
+
+ private:
+  void eager_step();
+  void capture();
+  GPT2& model_;
+  FlatParams& flat_;
+  AdamW& opt_;
+  TokenDataset& train_;
+  TokenDataset* valid_;
+  TrainConfig cfg_;
+  PowerMonitor* pm_;
+  int64_t total_steps_ = 0, steps_per_epoch_ = 1;
+  // static device inputs (the graph reads these) + loss accumulator
+  std::vector<Tensor> ids_, labels_;
+  Tensor loss_acc_, one_;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  int warm_ = 0;
+  int pool_ = 0;
+};
+
+}  // namespace eng
+}  // namespace mft
