@@ -346,6 +346,24 @@ void GPT2::load_lora(const std::string& path) {
   spec.dropout = mget("dropout").empty() ? 0.f : std::stof(mget("dropout"));
   spec.split_qkv = mget("split_qkv") == "true";
   spec.targets.clear();
+  {  // metadata order wins (spec_from_metadata); else the canonical target order
+    const std::string t = mget("targets");
+    if (!t.empty() && t.find("attn.") == std::string::npos) {
+      std::stringstream ss(t);
+      std::string item;
+      while (std::getline(ss, item, ','))
+        if (!item.empty()) spec.targets.push_back(item);
+    }
+  }
+  for (const char* canon : {"attn.qkv", "attn.q", "attn.proj", "mlp.fc_in", "mlp.fc_out"}) {
+    const std::string part = canon;
+    bool present = false;
+    for (auto& kv : A) present = present || kv.first.substr(kv.first.find('.', 6) + 1) == part;
+    if (!present) continue;
+    std::string t = part == "attn.proj" ? "AttnProj" : part == "mlp.fc_in" ? "MlpFcIn" : part == "mlp.fc_out" ? "MlpFcOut" : "AttnQKV";
+    if (part == "attn.q") spec.split_qkv = true;
+    if (!spec.has(t)) spec.targets.push_back(t);
+  }
   for (auto& kv : A) {
     const std::string part = kv.first.substr(kv.first.find('.', 6) + 1);
     std::string t = part == "attn.proj" ? "AttnProj" : part == "mlp.fc_in" ? "MlpFcIn" : part == "mlp.fc_out" ? "MlpFcOut" : "AttnQKV";

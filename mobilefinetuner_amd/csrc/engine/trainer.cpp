@@ -125,7 +125,10 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
       htg(A, std::vector<int64_t>((size_t)B * S));
   std::vector<float> mk((size_t)B * S);
   std::ofstream metrics;
-  if (!cfg_.metrics_out.empty()) metrics.open(cfg_.metrics_out, std::ios::app);
+  if (!cfg_.metrics_out.empty()) {
+    metrics.open(cfg_.metrics_out, std::ios::app);
+    metrics.precision(9);
+  }
   auto t_last = std::chrono::steady_clock::now();
   int64_t tok_since = 0, steps_since = 0;
   for (int64_t it = 0; it < total_steps_; ++it) {
