@@ -181,6 +181,10 @@ def main():
     if world > 1:
         assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
     sync = (lambda: None) if a.cpu_smoke else torch.cuda.synchronize
+    if not a.cpu_smoke:
+        # library GEMMs with the offline-tuned solutions shipped in the package (no tuning here)
+        from mobilefinetuner_amd.utils.gemm_tuning import enable_tuned_gemms
+        enable_tuned_gemms()
 
     model, step, vocab, desc, nparams = build(a, cfgd, dev, world)
 

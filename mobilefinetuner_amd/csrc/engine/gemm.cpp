@@ -273,7 +273,8 @@ void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
   MFT_CHECK(buf.dtype() == DType::F32 && buf.is_contiguous(), "gemm_wgrad: fp32 contiguous grad buffer");
   const long M = dy2.size(0), N = dy2.size(1), K = x2.size(1);
   MFT_CHECK(x2.size(0) == M && buf.numel() == N * K, "gemm_wgrad: shapes");
-  const bool small = N * K <= 2304L * 768L;
+  // (gemm8 split-K wins small outputs in isolation but loses inside the full-FT step: opt-in only)
+  const bool small = N * K <= 2304L * 768L && std::getenv("MFT_G8_SMALL_WGRAD") && std::getenv("MFT_G8_SMALL_WGRAD")[0] == '1';
   if ((deterministic() || gemm8_all() || small) && M % 64 == 0 && N % 8 == 0 && K % 8 == 0 && dy2.stride(0) % 8 == 0 &&
       x2.stride(0) % 8 == 0 && ::mft::gemm8_supported((int)N, (int)K, (int)M, true, true)) {
     ::mft::GemmArgs g{};

@@ -451,8 +451,7 @@ def qk_norm_rope_attention(qkv, nq, nkv, wq, wk, cos, sin, eps_q, eps_k, offset=
 #     LM-head dx 3.91 vs 3.77 ms);
 #   * plain forward GEMMs y = x W^T + b and fp32 weight-gradient accumulation are "plain library
 #     GEMMs" and stay on hipBLASLt where it is measurably faster (NT forward: gemm8 0.79-0.87x;
-#     wide TN weight-grads: gemm8 0.69-0.79x; small ones (<= 2304 x 768 outputs) run on gemm8,
-#     1.03-1.40x).  MFT_GEMM8_ALL=1 routes them through gemm8 too, and
+#     TN weight-grads: gemm8 0.69-1.40x in isolation, slower inside the full-FT step).  MFT_GEMM8_ALL=1 routes them through gemm8 too, and
 #     --deterministic (set_deterministic) always uses gemm8's split-K TN form, whose fixed-order
 #     slab reduction makes weight gradients bitwise reproducible.
 # Shapes outside gemm8's contract (reduction dim % 64, output columns % 8) fall back to torch.mm
@@ -513,9 +512,11 @@ def gemm_dx(dy2, wc, out=None):
 def _mm_wgrad_into(buf, dy2, x2, alpha=1.0):
     """buf (fp32 [N, K]) += alpha * dy2^T @ x2, accumulated in place in the fp32 grad buffer."""
     M = dy2.shape[0]
-    # gemm8's split-major split-K TN form beats hipBLASLt on small outputs (qkv dW 540 vs 556 us,
-    # proj dW 195 vs 273 us at 65536 tokens); hipBLASLt keeps the wide ones (fc / mlp_proj dW 0.7-0.8x)
-    small = dy2.shape[1] * x2.shape[1] <= 2304 * 768
+    # gemm8's split-major split-K TN form beats hipBLASLt on small outputs IN ISOLATION (qkv dW 540 vs
+    # 556 us, proj dW 195 vs 273 us at 65536 tokens) but not inside the full-FT step (69.9 vs 72.1
+    # ms/step, A/B in one call: the fp32 slabs + reduce pass compete with the step's other traffic);
+    # hipBLASLt (beta = 1, in place) stays the default, MFT_G8_SMALL_WGRAD=1 opts in
+    small = dy2.shape[1] * x2.shape[1] <= 2304 * 768 and os.environ.get("MFT_G8_SMALL_WGRAD", "0") == "1"
     g8 = deterministic() or _gemm8_all() or small
     if (g8 and _g8_ok(dy2, x2) and buf.is_contiguous() and M % 64 == 0 and dy2.shape[1] % 8 == 0
             and x2.shape[1] % 8 == 0):
@@ -1040,7 +1041,12 @@ class _LMHeadCE(Function):
         wtmp = torch.zeros(w.shape, device=h.device) if (need_grad and _needs(w) and wbuf is None) else None
         for i in range(0, M, chunk):
             hc = h[i:i + chunk]
-            logits = gemm_linear(hc, wc)                       # [rows, Vpad] bf16, gemm8 NT
+            if wc.shape[0] > 65536:
+                from ..utils.gemm_tuning import no_tuning
+                with no_tuning():
+                    logits = gemm_linear(hc, wc)
+            else:
+                logits = gemm_linear(hc, wc)                   # [rows, Vpad] bf16
             C.xent_fwd_bwd(logits, labels[i:i + chunk], loss_rows[i:i + chunk], V, scale, 1.0, need_grad)
             if need_grad:
                 gemm_dx(logits, wc, out=dh[i:i + chunk])       # dh = dlogits W, gemm8 NN

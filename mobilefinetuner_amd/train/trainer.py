@@ -88,6 +88,9 @@ class Trainer:
                  save_fn=None, power_monitor=None, dp: DataParallel | None = None, loss_fn=None,
                  zero_stage: int = 0):
         self.model, self.flat, self.train_ds, self.valid_ds = model, flat, train_ds, valid_ds
+        if device.type == "cuda":
+            from ..utils.gemm_tuning import enable_tuned_gemms
+            enable_tuned_gemms()
         self.cfg, self.device = cfg, device
         self.save_fn = save_fn
         self.pm = power_monitor
