@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONPATH=$PWD
-export PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=0 PYTORCH_TUNABLEOP_FILENAME=$PWD/mobilefinetuner_amd/tuning/tunableop_gfx950.csv
+
 rm -rf gpurun_out/tprof
 timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/tprof -o run -- python3 bench.py --steps 10 --warmup 3 > gpurun_out/tprof.log 2>&1 || { tail gpurun_out/tprof.log; exit 1; }
 DB=$(find gpurun_out/tprof -name "*.db" | head -1)
