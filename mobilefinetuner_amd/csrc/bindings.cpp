@@ -16,6 +16,17 @@ namespace {
 
 inline hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// deterministic-reduction mode: the LoRA weight-gradient and embedding-gradient
+// kernels sum per-block partials in a fixed order instead of fp32 atomics (workspaces from torch's
+// caching allocator, so the mode is hipGraph-capturable).  MFT_DETERMINISTIC=1 or set_deterministic().
+bool g_det = [] {
+  const char* e = getenv("MFT_DETERMINISTIC");
+  return e && e[0] == '1';
+}();
+void set_deterministic(bool on) { g_det = on; }
+bool get_deterministic() { return g_det; }
+Tensor det_ws(const Tensor& like, long n) { return torch::empty({n}, like.options().dtype(torch::kFloat32)); }
+
 #define CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == torch::kBFloat16, #t " must be bf16")
 #define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == torch::kFloat32, #t " must be fp32")
@@ -239,8 +250,9 @@ void embed_bwd(Tensor ids, Tensor dout, c10::optional<Tensor> dwte, c10::optiona
   CHECK_CONTIG(dout);
   const long M = ids.numel();
   const int C = dout.size(-1);
+  const long det_vocab = (g_det && dwte.has_value() && dwte->defined()) ? dwte->numel() / C : 0;
   mft::embed_bwd(ids.data_ptr<int64_t>(), bp(dout), optp<float>(dwte), optp<float>(dwpe), M, C, (int)S, (int)pos0,
-                 (float)scale, stream());
+                 (float)scale, stream(), det_vocab);
 }
 
 // ------------------------------------------------------------------ cross entropy
@@ -331,7 +343,7 @@ void lora_wgrad(Tensor X, Tensor Y, Tensor out, int64_t osk, int64_t osr, double
   TORCH_CHECK(K % 8 == 0, "lora_wgrad: K must be a multiple of 8");
   const long M = X.numel() / K;
   mft::lora_wgrad(bp(X), X.stride(-2), bp(Y), Y.stride(-2), fp(out), osk, osr, M, K, R, (float)scale,
-                  mkdrop(drop_p, salt, ctr), stream());
+                  mkdrop(drop_p, salt, ctr), stream(), nullptr, g_det ? det_ws(X, mft::lora_wgrad_ws_floats(M, K, R)).data_ptr<float>() : nullptr);
 }
 // dA_z += scale * X^T Y[:, 8z:8z+8] for every rank-8 adapter z sharing the input X (one pass over X);
 // outs[z] are contiguous fp32 [8, K] grad buffers
@@ -350,7 +362,7 @@ void lora_wgrad_multi(Tensor X, Tensor Y, std::vector<Tensor> outs, double scale
   }
   const long M = X.numel() / K;
   mft::lora_wgrad(bp(X), X.stride(-2), bp(Y), Y.stride(-2), nullptr, 1, K, M, K, R, (float)scale, mft::LoraDrop{nullptr, 0, 0.f},
-                  stream(), &o);
+                  stream(), &o, g_det ? det_ws(X, mft::lora_wgrad_ws_floats(M, K, R)).data_ptr<float>() : nullptr);
 }
 // rank 8: v = s dy B^T (bf16 [M, 8]) and dB += s u^T dy (fp32 [8, N] grad buffer) in one pass over dy
 void lora_dy(Tensor dy, Tensor B, Tensor u, Tensor dB, Tensor vpart, Tensor v, double s) {
@@ -368,7 +380,7 @@ void lora_dy(Tensor dy, Tensor B, Tensor u, Tensor dB, Tensor vpart, Tensor v, d
               reinterpret_cast<uintptr_t>(u.data_ptr()) % 16 == 0,
               "lora_dy: alignment (N and row strides % 8, 16-B aligned rows)");
   mft::lora_dy(bp(dy), dy.stride(0), bp(B), B.stride(0), bp(u), u.stride(0), fp(dB), N, fp(vpart), bp(v), v.stride(0),
-               M, N, (float)s, stream());
+               M, N, (float)s, stream(), g_det ? det_ws(dy, mft::lora_dy_ws_floats(M, N)).data_ptr<float>() : nullptr);
 }
 void lora_merge(Tensor W, int64_t wsk, int64_t wsn, Tensor A, Tensor B, double s) {
   CHECK_F32(A); CHECK_F32(B); CHECK_CONTIG(A); CHECK_CONTIG(B);
@@ -615,6 +627,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm_op, py::arg("A"), py::arg("B"), py::arg("b_nn"), py::arg("epi"), py::arg("bias"), py::arg("aux"),
         py::arg("alpha"), py::arg("cfg"), py::arg("out"), py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none());
   m.def("zero_cols", &zero_cols);
+  m.def("set_deterministic", &set_deterministic);
+  m.def("get_deterministic", &get_deterministic);
   m.def("colsum_acc", &colsum_acc);
   m.def("rope_apply", &rope_apply);
   m.def("qknorm_rope_fwd", &qknorm_rope_fwd);

@@ -110,7 +110,9 @@ Plan& plan_for(const Problem& p, const void* A, const void* B) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (s) (void)hipStreamIsCapturing(s, &cap);
   const char* tune = std::getenv("MFT_LT_TUNE");
-  if (got > 1 && A && B && cap == hipStreamCaptureStatusNone && !(tune && tune[0] == '0')) {
+  // (deterministic mode keeps the heuristic's first pick: a timing-based choice can differ between
+  // processes, and different algorithms sum in different orders)
+  if (got > 1 && A && B && cap == hipStreamCaptureStatusNone && !(tune && tune[0] == '0') && !g_det) {
     auto& al = CachingAllocator::get(p.dev);
     size_t wmax = 1;
     for (int i = 0; i < got; ++i) wmax = std::max(wmax, (size_t)res[i].workspaceSize);

@@ -23,6 +23,9 @@ Tensor f32_of(Param& p) {  // norm weights are fp32 compute
   return p.c.dtype() == DType::F32 ? p.c : p.c.to(DType::F32);
 }
 // fp32 grad buffer of a trainable param (allocated on first use), or undefined
+// deterministic-mode workspace (fixed-order partial sums instead of fp32 atomics), else undefined
+Tensor det_ws(long n) { return deterministic() ? empty({(int64_t)n}, DType::F32) : Tensor(); }
+float* dptr(const Tensor& t) { return t.defined() ? (float*)t.data_ptr() : nullptr; }
 Tensor gbuf(Param* p) {
   if (!p || !p->trainable()) return Tensor();
   return grad_buffer(p->leaf);
@@ -130,7 +133,8 @@ Tensor embed(const Tensor& ids, Param& wte, Param* wpe, float scale) {
       if (!g[0].defined()) return std::vector<Tensor>{Tensor(), Tensor()};
       Tensor d = g[0].contiguous();
       Tensor bte = gbuf(pw), bpe = gbuf(wpe);
-      ::mft::embed_bwd(idc.data<int64_t>(), bp(d), fp_or_null(bte), fp_or_null(bpe), M, C, S_, 0, scale, S());
+      ::mft::embed_bwd(idc.data<int64_t>(), bp(d), fp_or_null(bte), fp_or_null(bpe), M, C, S_, 0, scale, S(),
+                       (deterministic() && bte.defined()) ? bte.numel() / C : 0);
       return std::vector<Tensor>{Tensor(), Tensor()};
     });
     connect(n, {wte.leaf, wpe ? wpe->leaf : Tensor()}, {out});
@@ -403,8 +407,9 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         Tensor dB = a.B.trainable() ? grad_buffer(a.B.leaf) : Tensor();
         if (dB.defined() && a.rank == 8 && a.ncols % 8 == 0 && a.col0 % 8 == 0 && (K + o) % 8 == 0) {
           Tensor vpart = empty({(int64_t)((a.ncols + 255) / 256) * M * 8}, DType::F32, dy2.device());
+          Tensor dw = det_ws(::mft::lora_dy_ws_floats(M, a.ncols));
           ::mft::lora_dy(bp(dys), dys.stride(0), bp(a.B.c), a.B.c.stride(0), bp(xa2) + K + o, xa2.stride(0), fp(dB),
-                         a.ncols, fp(vpart), bp(v), v.stride(0), M, a.ncols, s, S());
+                         a.ncols, fp(vpart), bp(v), v.stride(0), M, a.ncols, s, S(), dptr(dw));
           db_done[i] = true;
         } else {
           ::mft::lora_rowdot(bp(dys), dys.stride(0), bp(a.B.c), a.B.c.stride(0), bp(v), v.stride(0), M, a.ncols,
@@ -445,8 +450,9 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
           ::mft::WgradOuts wo{};
           wo.n = (int)ads.size();
           for (size_t i = 0; i < ads.size(); ++i) wo.p[i] = fp(grad_buffer(ads[i].A.leaf));
+          Tensor dw = det_ws(::mft::lora_wgrad_ws_floats(M, K, rt));
           ::mft::lora_wgrad(bp(x2), x2.stride(0), bp(vall), vall.stride(0), nullptr, 1, K, M, K, rt, 1.f,
-                            ::mft::LoraDrop{nullptr, 0, 0.f}, S(), &wo);
+                            ::mft::LoraDrop{nullptr, 0, 0.f}, S(), &wo, dptr(dw));
           da_done = true;
         }
       }
@@ -458,13 +464,15 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         if (!da_done && a.A.trainable()) {
           ::mft::LoraDrop d{drop_ctr.defined() ? drop_ctr.data<int64_t>() : nullptr, a.salt,
                             training ? a.dropout : 0.f};
+          Tensor dw = det_ws(::mft::lora_wgrad_ws_floats(M, K, a.rank));
           ::mft::lora_wgrad(bp(x2), x2.stride(0), bp(v), v.stride(0), fp(grad_buffer(a.A.leaf)), 1, K, M, K, a.rank,
-                            1.f, d, S());
+                            1.f, d, S(), nullptr, dptr(dw));
         }
         if (a.B.trainable() && !db_done[i]) {
           Tensor dys = dy2.slice(1, a.col0, a.col0 + a.ncols);
+          Tensor dw = det_ws(::mft::lora_wgrad_ws_floats(M, a.ncols, a.rank));
           ::mft::lora_wgrad(bp(dys), dys.stride(0), bp(xa2) + off, xa2.stride(0), fp(grad_buffer(a.B.leaf)), 1,
-                            a.ncols, M, a.ncols, a.rank, s, ::mft::LoraDrop{nullptr, 0, 0.f}, S());
+                            a.ncols, M, a.ncols, a.rank, s, ::mft::LoraDrop{nullptr, 0, 0.f}, S(), nullptr, dptr(dw));
         }
         o += a.rank;
         off += a.rank;
@@ -525,12 +533,16 @@ Tensor lora_linear(const Tensor& x, Param& w, Param* b, std::vector<LoraAdapter>
                            s, ::mft::LoraDrop{nullptr, 0, 0.f}, S());
         ::mft::lora_update(bp(dx), dx.stride(0), bp(v), v.stride(0), bp(a.A.c), a.A.c.stride(0), bp(dx), dx.stride(0),
                            M, (int)K, a.rank, 1.f, d, S());
-        if (a.A.trainable())
+        if (a.A.trainable()) {
+          Tensor dw = det_ws(::mft::lora_wgrad_ws_floats(M, (int)K, a.rank));
           ::mft::lora_wgrad(bp(x2), x2.stride(0), bp(v), v.stride(0), fp(grad_buffer(a.A.leaf)), 1, K, M, (int)K,
-                            a.rank, 1.f, d, S());
-        if (a.B.trainable())
+                            a.rank, 1.f, d, S(), nullptr, dptr(dw));
+        }
+        if (a.B.trainable()) {
+          Tensor dw = det_ws(::mft::lora_wgrad_ws_floats(M, a.ncols, a.rank));
           ::mft::lora_wgrad(bp(dys), dys.stride(0), bp(us[i]), us[i].stride(0), fp(grad_buffer(a.B.leaf)), 1, a.ncols,
-                            M, a.ncols, a.rank, s, ::mft::LoraDrop{nullptr, 0, 0.f}, S());
+                            M, a.ncols, a.rank, s, ::mft::LoraDrop{nullptr, 0, 0.f}, S(), nullptr, dptr(dw));
+        }
       }
       out[0] = dx.view(xshape);
       return out;

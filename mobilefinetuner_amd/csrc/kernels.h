@@ -106,9 +106,10 @@ void gated_bwd(const bf16_t* gu, const bf16_t* dy, long ldd, bf16_t* dgu, long M
 // out[m] = wte[ids[m]] * scale (+ wpe[pos0 + m % S])
 void embed_fwd(const int64_t* ids, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, long M, int C, int S, int pos0,
                float scale, hipStream_t st);
-// dwte[ids[m]] += dout[m]*scale (fp32 atomics); dwpe[p] += sum over batch
+// dwte[ids[m]] += dout[m]*scale (fp32 atomics); dwpe[p] += sum over batch.  det_vocab > 0: the
+// deterministic form (fixed summation order per table row, no float atomics; V = det_vocab rows)
 void embed_bwd(const int64_t* ids, const bf16_t* dout, float* dwte, float* dwpe, long M, int C, int S, int pos0,
-               float scale, hipStream_t st);
+               float scale, hipStream_t st, long det_vocab = 0);
 
 // ---------------------------------------------------------------- cross entropy (xent.hip)
 // logits [M, ld] bf16 (first V columns valid); labels [M] (-100 = ignore).  Writes per-row loss
@@ -169,12 +170,16 @@ struct WgradOuts {
   float* p[8];
   int n;
 };
+// det_ws != null: deterministic mode -- per-row-chunk partials (lora_wgrad_ws_floats(M, K, R) floats)
+// summed in a fixed order instead of fp32 atomics
 void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out, long osk, long osr, long M, int K, int R,
-                float scale, LoraDrop drop, hipStream_t st, const WgradOuts* outs = nullptr);
+                float scale, LoraDrop drop, hipStream_t st, const WgradOuts* outs = nullptr, float* det_ws = nullptr);
+long lora_wgrad_ws_floats(long M, int K, int R);
 // rank 8, one pass over dy [M, N]:  dB[r*ldd + n] += s * sum_m u[m, r] dy[m, n]  (fp32 atomics) and
 // v[m*ldv + r] = s * sum_n dy[m, n] B[r, n]  (bf16); vpart = fp32 scratch of cdiv(N, 256) * M * 8
 void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,
-             float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st);
+             float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st, float* det_ws = nullptr);
+long lora_dy_ws_floats(long M, int N);  // deterministic-mode workspace of lora_dy (det_ws)
 // W[k*wsk + n*wsn] += s * sum_r A[r, k] * B[r, n]   (A [R,K], B [R,N] fp32)
 void lora_merge(void* W, int w_is_bf16, long wsk, long wsn, const float* A, const float* B, int K, int N, int R, float s,
                 hipStream_t st);

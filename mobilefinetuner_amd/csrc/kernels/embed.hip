@@ -55,14 +55,52 @@ __global__ void embed_bwd_wpe_kernel(const bf16_t* __restrict__ dout, float* __r
   }
 }
 
+// Deterministic token-table gradient: block b owns vocab rows [b*16, b*16 + 16) and walks ALL token
+// rows in ascending order, adding the rows whose id it owns (fp32, LDS accumulators) -- every
+// dwte element is summed in the same order on every run.  Only for the deterministic mode (it reads
+// the id list once per block: V/16 passes over M int64 ids, L2-resident).
+constexpr int kDetRows = 16;
+__global__ __launch_bounds__(256) void embed_bwd_wte_det_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ dout,
+                                                                float* __restrict__ dwte, long M, int C, long V, float scale) {
+  extern __shared__ float acc[];  // [kDetRows][C]
+  const long v0 = (long)blockIdx.x * kDetRows;
+  for (int i = threadIdx.x; i < kDetRows * C; i += blockDim.x) acc[i] = 0.f;
+  __syncthreads();
+  for (long m0 = 0; m0 < M; m0 += 256) {
+    const long m = m0 + threadIdx.x;
+    const long id = m < M ? ids[m] : -1;
+    const bool mine = id >= v0 && id < v0 + kDetRows;
+    // the block's rows of this 256-token window, processed in token order (one row at a time)
+    __shared__ int hit[256];
+    hit[threadIdx.x] = mine ? (int)(id - v0) : -1;
+    __syncthreads();
+    for (int t = 0; t < 256 && m0 + t < M; ++t) {
+      const int r = hit[t];
+      if (r < 0) continue;
+      const bf16_t* src = dout + (m0 + t) * C;
+      for (int c = threadIdx.x; c < C; c += blockDim.x) acc[r * C + c] += bf2f(src[c]) * scale;
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < kDetRows * C; i += blockDim.x) {
+    const long v = v0 + i / C;
+    if (v < V) dwte[v * C + (i % C)] += acc[i];
+  }
+}
+
 void embed_fwd(const int64_t* ids, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, long M, int C, int S, int pos0,
                float scale, hipStream_t st) {
   embed_fwd_kernel<<<cdiv(M, 4), 256, 0, st>>>(ids, wte, wpe, out, M, C, S, pos0, scale);
 }
 
 void embed_bwd(const int64_t* ids, const bf16_t* dout, float* dwte, float* dwpe, long M, int C, int S, int pos0,
-               float scale, hipStream_t st) {
-  if (dwte) embed_bwd_wte_kernel<<<cdiv(M, 4), 256, 0, st>>>(ids, dout, dwte, M, C, scale);
+               float scale, hipStream_t st, long det_vocab) {
+  if (dwte && det_vocab > 0) {
+    const size_t shm = sizeof(float) * kDetRows * C;
+    embed_bwd_wte_det_kernel<<<cdiv(det_vocab, kDetRows), 256, shm, st>>>(ids, dout, dwte, M, C, det_vocab, scale);
+  } else if (dwte) {
+    embed_bwd_wte_kernel<<<cdiv(M, 4), 256, 0, st>>>(ids, dout, dwte, M, C, scale);
+  }
   if (dwpe) embed_bwd_wpe_kernel<<<S, 256, 0, st>>>(dout, dwpe, M, C, S, pos0);
 }
 

@@ -147,7 +147,8 @@ __global__ __launch_bounds__(256) void lora_update_kernel(const bf16_t* base, lo
 template <int RB, bool YVEC, bool DROP>
 __global__ __launch_bounds__(1024) void lora_wgrad_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Y,
                                                           long ldy, float* __restrict__ out, long osk, long osr, long M, int K,
-                                                          int R, long chunk, float scale, LoraDrop drop, WgradOuts outs) {
+                                                          int R, long chunk, float scale, LoraDrop drop, WgradOuts outs,
+                                                          float* __restrict__ det_ws, long det_kp) {
   constexpr int U = DROP ? 6 : 12;
   __shared__ __attribute__((aligned(16))) float red[8][RB][256];
   __shared__ __attribute__((aligned(16))) bf16_t ysh[2][16 * U][RB];
@@ -258,8 +259,26 @@ __global__ __launch_bounds__(1024) void lora_wgrad_kernel(const bf16_t* __restri
     float v = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) v += red[i][r][c];
+    if (det_ws) {  // deterministic mode: this row chunk's partial, summed in a fixed order later
+      det_ws[((long)blockIdx.y * R + r0 + r) * det_kp + kk] = v * scale;
+      continue;
+    }
     atomicAdd(dst + (long)kk * osk + (long)(rdst + r) * osr, v * scale);
   }
+}
+
+// deterministic-mode reduction of lora_wgrad partials: out(rank r, column k) += sum_y ws[y][r][k]
+// in ascending y (row-chunk) order; segmented outputs map rank r to outs.p[r / 8], local rank r % 8
+__global__ void lora_wgrad_reduce_kernel(const float* __restrict__ ws, int ny, int R, int K, long kp, float* out,
+                                         long osk, long osr, WgradOuts outs) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)R * K) return;
+  const int r = (int)(t / K), k = (int)(t % K);
+  float acc = 0.f;
+  for (int y = 0; y < ny; ++y) acc += ws[((long)y * R + r) * kp + k];
+  float* dst = outs.n ? outs.p[r >> 3] : out;
+  const int rl = outs.n ? (r & 7) : r;
+  dst[(long)k * osk + (long)rl * osr] += acc;
 }
 
 // ------------------------------------------------------------------------------------ dy pass
@@ -284,7 +303,7 @@ __global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restric
                                                          const bf16_t* __restrict__ B, long ldb,
                                                          const bf16_t* __restrict__ u, long ldu, float* __restrict__ dB,
                                                          long ldd, float* __restrict__ vpart, long M, int N, long chunk,
-                                                         float s) {
+                                                         float s, float* __restrict__ det_ws, long det_np) {
   // per wave: dy image [32][kDyLd] + u^T image [32][16]; block reduction buffer aliases the images
   __shared__ __attribute__((aligned(16))) bf16_t lds[4][32 * kDyLd + 32 * 16];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -370,6 +389,10 @@ __global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restric
     const int r = o >> 8, c = o & 255;
     if (n0 + c >= N) continue;
     const float v = red[r * 256 + c] + red[(8 + r) * 256 + c] + red[(16 + r) * 256 + c] + red[(24 + r) * 256 + c];
+    if (det_ws) {  // deterministic mode: per-row-chunk partial, fixed-order sum in lora_dy_reduce
+      det_ws[((long)blockIdx.y * 8 + r) * det_np + n0 + c] = v * s;
+      continue;
+    }
     atomicAdd(dB + (long)r * ldd + n0 + c, v * s);
   }
 }
@@ -384,14 +407,17 @@ __global__ void lora_dy_finish_kernel(const float* __restrict__ vpart, int nstri
   v[(t >> 3) * ldv + (t & 7)] = f2bf(a * s);
 }
 
-void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,
-             float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st) {
-  if ((N % 8) || (ldy % 8) || (ldb % 8) || (ldu % 8) || (reinterpret_cast<uintptr_t>(dy) % 16) ||
-      (reinterpret_cast<uintptr_t>(B) % 16) || (reinterpret_cast<uintptr_t>(u) % 16)) {
-    fprintf(stderr, "lora_dy: N and the row strides must be multiples of 8, dy/B/u 16-B aligned\n");
-    abort();
-  }
-  if (M <= 0 || N <= 0) return;
+__global__ void lora_dy_reduce_kernel(const float* __restrict__ ws, int ny, int N, long np, float* __restrict__ dB,
+                                      long ldd) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 8L * N) return;
+  const int r = (int)(t / N), n = (int)(t % N);
+  float acc = 0.f;
+  for (int y = 0; y < ny; ++y) acc += ws[((long)y * 8 + r) * np + n];
+  dB[(long)r * ldd + n] += acc;
+}
+
+static long dy_chunks(long M, int N, long* chunk_out) {
   const int gx = cdiv(N, 256);
   // 2 resident blocks per CU (68 KB LDS each): ~512 blocks in total, >= 2 tiles per wave (a 256-column
   // slice such as Gemma's k / v projections then still fills every CU: 256 row chunks at M = 64k)
@@ -401,9 +427,28 @@ void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t
   if (ny < 1) ny = 1;
   long chunk = cdiv(M, ny);
   chunk = cdiv(chunk, 128) * 128;
-  dim3 grid(gx, (unsigned)cdiv(M, chunk));
-  lora_dy_kernel<<<grid, 256, 0, st>>>(dy, ldy, B, ldb, u, ldu, dB, ldd, vpart, M, N, chunk, s);
+  if (chunk_out) *chunk_out = chunk;
+  return cdiv(M, chunk);
+}
+
+long lora_dy_ws_floats(long M, int N) { return dy_chunks(M, N, nullptr) * 8L * cdiv(N, 256) * 256; }
+
+void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,
+             float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st, float* det_ws) {
+  if ((N % 8) || (ldy % 8) || (ldb % 8) || (ldu % 8) || (reinterpret_cast<uintptr_t>(dy) % 16) ||
+      (reinterpret_cast<uintptr_t>(B) % 16) || (reinterpret_cast<uintptr_t>(u) % 16)) {
+    fprintf(stderr, "lora_dy: N and the row strides must be multiples of 8, dy/B/u 16-B aligned\n");
+    abort();
+  }
+  if (M <= 0 || N <= 0) return;
+  const int gx = cdiv(N, 256);
+  long chunk = 0;
+  const long ny = dy_chunks(M, N, &chunk);
+  const long np = (long)gx * 256;
+  dim3 grid(gx, (unsigned)ny);
+  lora_dy_kernel<<<grid, 256, 0, st>>>(dy, ldy, B, ldb, u, ldu, dB, ldd, vpart, M, N, chunk, s, det_ws, np);
   lora_dy_finish_kernel<<<cdiv(M * 8, 256), 256, 0, st>>>(vpart, gx, M, s, v, ldv);
+  if (det_ws) lora_dy_reduce_kernel<<<cdiv(8L * N, 256), 256, 0, st>>>(det_ws, (int)ny, N, np, dB, ldd);
 }
 
 template <typename T>
@@ -455,8 +500,27 @@ void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const 
   }
 }
 
+static long wgrad_chunks(long M, int K, int R, long* chunk_out) {
+  const int rb = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : 8;
+  const int gx = cdiv(K, 256);
+  const int gz = cdiv(R, rb);
+  // ~4 live waves per SIMD (4096 waves = 256 blocks of 16) but at least U=8 rows per wave; the
+  // chunk is a multiple of 16 rows so every wave streams the same number of rows
+  static const long target = getenv("MFT_WGRAD_BLOCKS") ? atol(getenv("MFT_WGRAD_BLOCKS")) : 256;
+  long nrc = cdiv(target, (long)gx * gz);
+  const long max_nrc = cdiv(M, 16 * 8);  // >= 8 rows per wave
+  if (nrc > max_nrc) nrc = max_nrc;
+  if (nrc < 1) nrc = 1;
+  long chunk = cdiv(M, nrc);
+  chunk = cdiv(chunk, 16) * 16;
+  if (chunk_out) *chunk_out = chunk;
+  return cdiv(M, chunk);
+}
+
+long lora_wgrad_ws_floats(long M, int K, int R) { return wgrad_chunks(M, K, R, nullptr) * R * (long)cdiv(K, 256) * 256; }
+
 void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out, long osk, long osr, long M, int K, int R,
-                float scale, LoraDrop drop, hipStream_t st, const WgradOuts* outs) {
+                float scale, LoraDrop drop, hipStream_t st, const WgradOuts* outs, float* det_ws) {
   WgradOuts so{};
   if (outs) {
     if (outs->n < 1 || outs->n > 8 || R != 8 * outs->n) {
@@ -472,25 +536,21 @@ void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out
   const int rb = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : 8;
   const int gx = cdiv(K, 256);
   const int gz = cdiv(R, rb);
-  // ~4 live waves per SIMD (4096 waves = 256 blocks of 16) but at least U=8 rows per wave; the
-  // chunk is a multiple of 16 rows so every wave streams the same number of rows
-  static const long target = getenv("MFT_WGRAD_BLOCKS") ? atol(getenv("MFT_WGRAD_BLOCKS")) : 256;
-  long nrc = cdiv(target, (long)gx * gz);
-  const long max_nrc = cdiv(M, 16 * 8);  // >= 8 rows per wave
-  if (nrc > max_nrc) nrc = max_nrc;
-  if (nrc < 1) nrc = 1;
-  long chunk = cdiv(M, nrc);
-  chunk = cdiv(chunk, 16) * 16;
-  dim3 grid(gx, (unsigned)cdiv(M, chunk), gz);
+  long chunk = 0;
+  const long ny = wgrad_chunks(M, K, R, &chunk);
+  const long kp = (long)gx * 256;
+  dim3 grid(gx, (unsigned)ny, gz);
   // vector Y loads need every rank block complete and 2*RB-byte aligned rows
   const bool yvec = (rb == 8 || rb == 4) && R % rb == 0 && ldy % rb == 0 &&
                     reinterpret_cast<uintptr_t>(Y) % (2 * rb) == 0;
 #define MFT_WG(RBV, YV)                                                                                         \
   do {                                                                                                          \
     if (drop.p > 0.f)                                                                                           \
-      lora_wgrad_kernel<RBV, YV, true><<<grid, 1024, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop, so);  \
+      lora_wgrad_kernel<RBV, YV, true><<<grid, 1024, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop, so, \
+                                                              det_ws, kp);                                     \
     else                                                                                                        \
-      lora_wgrad_kernel<RBV, YV, false><<<grid, 1024, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop, so); \
+      lora_wgrad_kernel<RBV, YV, false><<<grid, 1024, 0, st>>>(X, ldx, Y, ldy, out, osk, osr, M, K, R, chunk, scale, drop, \
+                                                               so, det_ws, kp);                                \
   } while (0)
   switch (rb) {
     case 1: MFT_WG(1, false); break;
@@ -499,6 +559,8 @@ void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out
     default: if (yvec) MFT_WG(8, true); else MFT_WG(8, false); break;
   }
 #undef MFT_WG
+  if (det_ws)
+    lora_wgrad_reduce_kernel<<<cdiv((long)R * K, 256), 256, 0, st>>>(det_ws, (int)ny, R, K, kp, out, osk, osr, so);
 }
 
 void lora_merge(void* W, int w_is_bf16, long wsk, long wsn, const float* A, const float* B, int K, int N, int R, float s,

@@ -465,6 +465,7 @@ def set_deterministic(on: bool = True):
     float atomics in every kernel that has both forms (LoRA weight-grads, embedding grad, attention
     dQ) and gemm8's split-K weight gradients instead of hipBLASLt's."""
     _DETERMINISTIC[0] = bool(on)
+    native().set_deterministic(bool(on))
 
 
 def deterministic() -> bool:

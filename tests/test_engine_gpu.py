@@ -142,8 +142,10 @@ def test_native_lora_checkpoint_bytes_match_python(tmp_path):
 
 
 def test_native_eager_and_graph_agree():
+    # --deterministic: fixed-order reductions instead of fp32 atomics, so eager and graph replay must
+    # agree to the last printed digit
     common = ["--random_init", "--model", "gpt2-tiny", "--synthetic_data", "--synthetic_tokens", "100000", "--steps",
-              "5", "--batch_size", "4", "--seq_len", "64", "--lr", "1e-3", "--log_interval", "1"]
+              "5", "--batch_size", "4", "--seq_len", "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic"]
     outs = []
     for extra in ([], ["--no_graph"]):
         r = subprocess.run([_bin("gpt2_lora_finetune"), *common, *extra], capture_output=True, text=True, timeout=120)
