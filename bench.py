@@ -168,6 +168,9 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if a.cpu_smoke:
+        # host tensors run through the test-suite's fp32 oracle (the op layer itself is GPU-only)
+        os.environ.setdefault("MFT_HOST_ORACLE", os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests",
+                                                              "oracle"))
         dev = torch.device("cpu")
         a.no_graph = True
         if world > 1:

@@ -1,8 +1,8 @@
 """Loader for the in-tree native extension ``mobilefinetuner_amd/_C.so``.
 
 GPU code paths call :func:`native` and FAIL LOUDLY when the extension is missing — there is no
-silent eager fallback for GPU tensors.  CPU tensors use the PyTorch reference implementations in
-``ops/reference.py`` (the numerics oracle of the test-suite).
+eager fallback.  The op layer has no host path of its own: host tensors are served only when the
+test-suite's fp32 oracle (``tests/oracle``) is installed, and raise otherwise.
 """
 from __future__ import annotations
 

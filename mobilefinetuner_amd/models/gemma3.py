@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import functional as Fx
-from ..ops import reference as ref
+from ..ops.rope_tables import rope_tables
 from ..parallel.sharder import gate
 from .layers import Linear, RMSNorm
 
@@ -183,9 +183,9 @@ class Gemma3Model(nn.Module):
         t = self._rope.get(key)
         if t is None or t[0].shape[0] < S:
             if kind == "global":
-                t = ref.rope_tables(n, self.cfg.head_dim, self.cfg.rope_theta, device, self.cfg.rope_scaling_factor)
+                t = rope_tables(n, self.cfg.head_dim, self.cfg.rope_theta, device, self.cfg.rope_scaling_factor)
             else:
-                t = ref.rope_tables(n, self.cfg.head_dim, self.cfg.rope_local_base_freq, device)
+                t = rope_tables(n, self.cfg.head_dim, self.cfg.rope_local_base_freq, device)
             self._rope[key] = t
         return t
 

@@ -1,7 +1,11 @@
-"""Autograd-aware fused ops.
+"""Autograd-aware fused ops -- ONE device path: the gfx950 HIP kernels of ``_C`` (no silent
+fallback: a missing extension raises).
 
-GPU tensors -> the gfx950 HIP kernels of ``_C`` (no silent fallback: a missing extension raises).
-CPU tensors -> the fp32 PyTorch reference (``ops/reference.py``).
+CPU tensors are not a second backend of this layer.  Every public op is wrapped by
+``_device_op``: a call on host tensors is routed to an externally installed host implementation
+(``install_host_ops``) or raises.  The only such implementation is the fp32 PyTorch oracle of the
+test-suite (``tests/oracle``), installed by ``tests/conftest.py`` / ``MFT_HOST_ORACLE`` for the
+GPU-less CI tests (HF parity, gloo data-parallel, CLI smoke runs).
 
 Gradient convention (replaces the reference's overwrite-on-backward): every trainable
 parameter's ``.grad`` is a persistent view into a flat fp32 grad buffer (see
@@ -12,6 +16,7 @@ engines can launch bucket all-reduces while backward is still running.
 """
 from __future__ import annotations
 
+import functools
 import math
 import os
 
@@ -19,9 +24,51 @@ import torch
 from torch.autograd import Function
 
 from .._ext import native
-from . import reference as ref
 
 GEMM_EPI_NONE, GEMM_EPI_BIAS, GEMM_EPI_BIAS_GELU, GEMM_EPI_DGELU, GEMM_EPI_F32ACC, GEMM_EPI_LORA = 0, 1, 2, 3, 4, 5
+
+# ---------------------------------------------------------------- host tensors (test oracle only)
+_HOST_OPS = [None]
+
+
+def install_host_ops(mod):
+    """Route public ops called on CPU tensors to ``mod`` (functions of the same names and
+    signatures).  Only the test-suite's fp32 oracle (tests/oracle) does this."""
+    _HOST_OPS[0] = mod
+
+
+def _load_env_oracle():
+    path = os.environ.get("MFT_HOST_ORACLE", "")
+    if not path or _HOST_OPS[0] is not None:
+        return
+    import importlib.util
+    import sys
+    init = os.path.join(path, "__init__.py")
+    spec = importlib.util.spec_from_file_location("mft_host_oracle", init, submodule_search_locations=[path])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["mft_host_oracle"] = mod
+    spec.loader.exec_module(mod)
+    install_host_ops(mod.host_ops)
+
+
+def _device_op(fn):
+    name = fn.__name__
+
+    @functools.wraps(fn)
+    def op(*args, **kwargs):
+        t = next((a for a in args if isinstance(a, torch.Tensor)), None)
+        if t is not None and not t.is_cuda:
+            if _HOST_OPS[0] is None:
+                _load_env_oracle()
+            if _HOST_OPS[0] is None:
+                raise RuntimeError(f"mobilefinetuner_amd.ops.{name}: the fused ops run on the GPU (gfx950 HIP "
+                                   f"kernels); host tensors need the test-suite oracle (tests/oracle, "
+                                   f"MFT_HOST_ORACLE=<repo>/tests/oracle)")
+            return getattr(_HOST_OPS[0], name)(*args, **kwargs)
+        return fn(*args, **kwargs)
+
+    return op
+
 
 # ---------------------------------------------------------------- parameter helpers
 
@@ -51,7 +98,7 @@ def cw(p):
 
 
 def rw(p):
-    """Weight view for the CPU reference path: the autograd-tracked parameter itself when trainable
+    """Weight view for the host oracle (tests/oracle): the autograd-tracked parameter itself when trainable
     (so AccumulateGrad fills p.grad), else its compute view."""
     if p is None:
         return None
@@ -149,30 +196,24 @@ class _Norm(Function):
 # out_cols > width: the GPU output is allocated [.., out_cols] with the normalised values in the first
 # `width` columns and the rest left for the consumer (a LoRA Linear appends its rank-r projections
 # there, _LoRALinearAug).  CPU paths ignore it.
+@_device_op
 def layer_norm(x, w, b, eps=1e-5, out_cols=0):
-    if not x.is_cuda:
-        return ref.layer_norm(x, rw(w), rw(b), eps).to(x.dtype)
     return _Norm.apply(x, None, w, b, eps, False, 0.0, int(out_cols))
 
 
+@_device_op
 def add_layer_norm(x, delta, w, b, eps=1e-5, out_cols=0):
     """s = x + delta; y = LayerNorm(s)  -> (s, y) (fused residual + norm)."""
-    if not x.is_cuda:
-        s = x + delta
-        return s, ref.layer_norm(s, rw(w), rw(b), eps).to(x.dtype)
     return _Norm.apply(x, delta, w, b, eps, False, 0.0, int(out_cols))
 
 
+@_device_op
 def rms_norm(x, w, eps=1e-6, offset=1.0, out_cols=0):
-    if not x.is_cuda:
-        return ref.rms_norm(x, rw(w), eps, offset).to(x.dtype)
     return _Norm.apply(x, None, w, None, eps, True, offset, int(out_cols))
 
 
+@_device_op
 def add_rms_norm(x, delta, w, eps=1e-6, offset=1.0, out_cols=0):
-    if not x.is_cuda:
-        s = x + delta
-        return s, ref.rms_norm(s, rw(w), eps, offset).to(x.dtype)
     return _Norm.apply(x, delta, w, None, eps, True, offset, int(out_cols))
 
 
@@ -206,19 +247,17 @@ class _Gated(Function):
         return native().gated_bwd(gu, dy, ctx.act), None, None
 
 
+@_device_op
 def gelu(x):
-    if not x.is_cuda:
-        return ref.gelu_tanh(x).to(x.dtype)
     return _Gelu.apply(x)
 
 
+@_device_op
 def gated_act(gu, act="gelu", out_cols=0):
     """gelu_tanh(gate) * up (GeGLU, Gemma) or silu(gate) * up (SwiGLU); gu = [gate | up].
     out_cols > I (GPU): returns [M, out_cols] with the activation in the first I columns and zeros
     after, the augmented-K input of a LoRA consumer (Linear.aug_cols)."""
     a = 0 if act in ("gelu", "gelu_tanh", "gelu_pytorch_tanh") else 1
-    if not gu.is_cuda:
-        return ref.gated(gu, a).to(gu.dtype)
     I = gu.shape[-1] // 2
     oc = int(out_cols) if out_cols and out_cols > I else 0
     if oc:
@@ -259,16 +298,10 @@ class _Embedding(Function):
         return None, gte, gpe, None, None
 
 
+@_device_op
 def embedding(ids, wte, wpe=None, scale=1.0):
     """ids [B,S] -> [B*S, C]: wte[ids]*scale (+ wpe[pos])."""
     B, S = ids.shape
-    if not ids.is_cuda:
-        e = rw(wte)[ids.reshape(-1)].float()
-        if scale != 1.0:
-            e = e * scale
-        if wpe is not None:
-            e = e + rw(wpe)[:S].float().repeat(B, 1)
-        return e.to(rw(wte).dtype)
     return _Embedding.apply(ids, wte, wpe, S, float(scale))
 
 
@@ -319,22 +352,20 @@ class _FlashAttnPacked(Function):
         return dqkv, None, None, None, None, None
 
 
+@_device_op
 def flash_attention(q, k, v, scale=None, causal=True, window=0, kv_lens=None):
     """q [B,Sq,H,D], k/v [B,Sk,Hkv,D] (strided views OK) -> o [B,Sq,H,D]."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
-    if not q.is_cuda:
-        return ref.attention(q, k, v, scale, causal, window, kv_lens)[0].to(q.dtype).contiguous()
     return _FlashAttn.apply(q, k, v, float(scale), bool(causal), int(window or 0), kv_lens)
 
 
+@_device_op
 def flash_attention_qkvpacked(qkv, scale=None, causal=True, window=0, kv_lens=None, out_cols=0):
     """qkv [B,S,3,H,D] -> o [B,S,H,D]; with out_cols > H*D (GPU) -> [B,S,out_cols] whose first H*D
     columns hold O (room for the consumer's appended LoRA columns, _LoRALinearAug)."""
     if scale is None:
         scale = 1.0 / math.sqrt(qkv.shape[-1])
-    if not qkv.is_cuda:
-        return ref.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], scale, causal, window, kv_lens)[0].to(qkv.dtype).contiguous()
     H, D = qkv.shape[3], qkv.shape[4]
     oc = int(out_cols) if out_cols and out_cols > H * D else 0
     return _FlashAttnPacked.apply(qkv, float(scale), bool(causal), int(window or 0), kv_lens, oc)
@@ -366,11 +397,9 @@ class _QKNormRoPE(Function):
         return dx, (tmp.to(w.dtype) if tmp is not None else None), None, None, None, None, None
 
 
+@_device_op
 def qk_norm_rope(x, w, cos, sin, eps=1e-6, offset=1.0, interleaved=False):
     """x [B,S,H,D] strided view -> rope(rmsnorm(x) * (w + offset)) contiguous [B,S,H,D]."""
-    if not x.is_cuda:
-        y = ref.rms_norm(x, rw(w), eps, offset).to(x.dtype)
-        return ref.rope(y, cos, sin, 0, interleaved).to(x.dtype)
     return _QKNormRoPE.apply(x, w, cos, sin, float(eps), float(offset), bool(interleaved))
 
 
@@ -425,6 +454,7 @@ class _QKNormRoPEAttn(Function):
         return (dqkv, grads[0], grads[1]) + (None,) * 12
 
 
+@_device_op
 def qk_norm_rope_attention(qkv, nq, nkv, wq, wk, cos, sin, eps_q, eps_k, offset=1.0, interleaved=False, scale=None,
                            window=0, kv_lens=None, out_cols=0):
     """qkv [B,S,nq+2nkv,D] -> o [B,S,nq,D] = attention(rope(rmsnorm_q(q)), rope(rmsnorm_k(k)), v);
@@ -432,10 +462,6 @@ def qk_norm_rope_attention(qkv, nq, nkv, wq, wk, cos, sin, eps_q, eps_k, offset=
     D = qkv.shape[-1]
     if scale is None:
         scale = 1.0 / math.sqrt(D)
-    if not qkv.is_cuda:
-        q = qk_norm_rope(qkv[:, :, :nq], wq, cos, sin, eps_q, offset, interleaved)
-        k = qk_norm_rope(qkv[:, :, nq:nq + nkv], wk, cos, sin, eps_k, offset, interleaved)
-        return flash_attention(q, k, qkv[:, :, nq + nkv:], scale, True, window, kv_lens)
     oc = int(out_cols) if out_cols and out_cols > nq * D else 0
     return _QKNormRoPEAttn.apply(qkv, wq, wk, cos, sin, float(eps_q), float(eps_k), float(offset), bool(interleaved),
                                  int(nq), int(nkv), float(scale), int(window or 0), kv_lens, oc)
@@ -581,13 +607,9 @@ class _Linear(Function):
         return dx, gw, gb
 
 
+@_device_op
 def linear(x, w, b=None):
     """y = x W^T + b with W [out, in] (nn.Linear layout)."""
-    if not x.is_cuda:
-        y = x.float() @ rw(w).float().t()
-        if b is not None:
-            y = y + rw(b).float()
-        return y.to(x.dtype)
     return _Linear.apply(x, w, b)
 
 
@@ -958,6 +980,7 @@ def lora_linear_aug(xa, w, b, slices, scale, waug, training: bool = True):
     return _LoRALinearAug.apply(xa, w, b, float(scale), tuple(meta), int(K), waug, *ab)
 
 
+@_device_op
 def lora_linear(x, w, b, slices, scale, training: bool = True):
     """slices: list of (col0, ncols, A, B[, dropout_p, salt]).  See _LoRALinear.  Dropout (PEFT
     semantics: on the LoRA input only) is active when ``training`` and grad mode are on."""
@@ -969,20 +992,6 @@ def lora_linear(x, w, b, slices, scale, training: bool = True):
         if not (training and torch.is_grad_enabled()):
             p = 0.0
         norm.append((c0, n, A, B, p, salt))
-    if not x.is_cuda:
-        xf = x.float()
-        y = xf @ rw(w).float().t()
-        if b is not None:
-            y = y + rw(b).float()
-        parts = []
-        for (c0, n, A, B, p, salt) in norm:
-            xd = torch.nn.functional.dropout(xf, p) if p > 0 else xf
-            parts.append((c0, n, scale * ((xd @ rw(A).float().t()) @ rw(B).float())))
-        if parts:
-            y = y.clone()
-            for c0, n, d in parts:
-                y[..., c0:c0 + n] = y[..., c0:c0 + n] + d
-        return y.to(x.dtype)
     meta = tuple((int(c0), int(n), float(p), int(salt) & 0xFFFFFFFF) for (c0, n, _, _, p, salt) in norm)
     ab = []
     for sl in norm:
@@ -1072,28 +1081,22 @@ class _LMHeadCE(Function):
         return dh, gw, None, None, None, None
 
 
+@_device_op
 def lm_head_cross_entropy(h, w, labels, vocab_size, chunk=None, w_grad_scale=1.0):
     """Mean token NLL of logits = h W^T (W [Vpad, C], first vocab_size rows real) vs labels
     (already shifted; -100 = ignore).  Never materialises the full logits: chunks of rows are
     GEMM'd, turned into dlogits in place and immediately multiplied back (dh, dW).
     NOTE: the W gradient is produced during forward and scaled by ``w_grad_scale`` (pass the
     same factor the loss is later multiplied by, e.g. 1/grad_accum); dh honours grad_output."""
-    if not h.is_cuda:
-        logits = h.float() @ rw(w).float().t()
-        logits = logits[:, :vocab_size]
-        return torch.nn.functional.cross_entropy(logits, labels.reshape(-1), ignore_index=-100)
     if chunk is None:
         chunk = default_ce_chunk(cw(w).shape[0])
     return _LMHeadCE.apply(h, w, labels, int(vocab_size), int(chunk), float(w_grad_scale))
 
 
+@_device_op
 def lm_head_token_nll(h, w, labels, vocab_size, chunk=None):
     """Per-row NLL (no grad) for evaluation: returns (sum_nll, n_valid) device scalars."""
     with torch.no_grad():
-        if not h.is_cuda:
-            logits = (h.float() @ rw(w).float().t())[:, :vocab_size]
-            nll = torch.nn.functional.cross_entropy(logits, labels.reshape(-1), ignore_index=-100, reduction="sum")
-            return nll, (labels >= 0).sum()
         C = native()
         wc = cw(w)
         M = h.shape[0]

@@ -4,6 +4,9 @@ import sys
 import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the fp32 host oracle (tests/oracle) serves host-tensor calls of the op layer in this process and,
+# through the environment, in every subprocess a test starts (gloo ranks, bench --cpu_smoke)
+os.environ.setdefault("MFT_HOST_ORACLE", os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle"))
 
 
 def pytest_configure(config):

@@ -1,9 +1,7 @@
-"""Plain-PyTorch fp32 reference implementations of every fused op.
-
-These are (1) the numerics oracle the HIP kernels are tested against and (2) the path taken
-for CPU tensors (CPU-only CI, tokenizer/data tooling).  They mirror the semantics of the
-reference engine's ops where SURVEY §8 says we keep them, and HF/PEFT semantics elsewhere.
-"""
+"""Plain-PyTorch fp32 reference implementations of every fused op: the numerics oracle the HIP
+kernels are tested against, and (through ``host_ops``) the host-tensor path of the GPU-less CI.
+They mirror the semantics of the reference engine's ops where SURVEY §8 says we keep them, and
+HF/PEFT semantics elsewhere."""
 from __future__ import annotations
 
 import math
@@ -59,12 +57,7 @@ def attention(q, k, v, scale, causal=True, window=0, kv_lens=None):
     return o, lse
 
 
-def rope_tables(seq_len, dim, theta, device=None, scaling_factor=1.0):
-    """cos/sin tables [seq_len, dim/2] fp32 (HF default rope; linear scaling divides positions)."""
-    inv = 1.0 / (theta ** (torch.arange(0, dim, 2, dtype=torch.float64) / dim))
-    pos = torch.arange(seq_len, dtype=torch.float64) / scaling_factor
-    f = torch.outer(pos, inv)
-    return f.cos().float().to(device), f.sin().float().to(device)
+from mobilefinetuner_amd.ops.rope_tables import rope_tables  # noqa: E402,F401  (model setup helper)
 
 
 def rope(x, cos, sin, pos0=0, interleaved=False):

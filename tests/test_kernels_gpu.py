@@ -207,7 +207,7 @@ def test_fused_mlp_gelu_epilogues(trainable, monkeypatch):
     monkeypatch.setenv("MFT_FUSED_MLP", "1")
     from mobilefinetuner_amd.models.layers import Linear
     from mobilefinetuner_amd.ops import functional as Fx
-    from mobilefinetuner_amd.ops import reference as ref
+    from oracle import reference as ref
     assert Fx.fused_mlp_available()
     M, C = 500, 256
     fc, proj = Linear(C, 4 * C, device=DEV), Linear(4 * C, C, device=DEV)
@@ -235,7 +235,7 @@ def test_fused_mlp_gelu_epilogues(trainable, monkeypatch):
 
 
 def _attn_ref(q, k, v, scale, causal, window, kv_lens=None):
-    from mobilefinetuner_amd.ops import reference as ref
+    from oracle import reference as ref
     return ref.attention(q, k, v, scale, causal, window, kv_lens)
 
 
@@ -416,7 +416,7 @@ def test_embedding():
 @pytest.mark.parametrize("D,interleaved", [(256, False), (128, False), (64, False), (256, True)])
 def test_qknorm_rope(D, interleaved):
     from mobilefinetuner_amd.ops import functional as Fx
-    from mobilefinetuner_amd.ops import reference as ref
+    from oracle import reference as ref
     B, S, H = 2, 67, 3
     big = torch.randn(B, S, H + 2, D, device=DEV).bfloat16().requires_grad_()
     x = big[:, :, 1:1 + H]
@@ -458,7 +458,7 @@ def test_gated_widened_output():
 def test_qknorm_rope_attention_fused(nq, nkv, window, oc):
     """Fused Gemma attention core (packed qkv -> O, one packed dqkv) vs the fp32 composition."""
     from mobilefinetuner_amd.ops import functional as Fx
-    from mobilefinetuner_amd.ops import reference as ref
+    from oracle import reference as ref
     B, S, D = 2, 128, 256
     qkv = (torch.randn(B, S, nq + 2 * nkv, D, device=DEV)).bfloat16().requires_grad_()
     wq = torch.nn.Parameter(torch.randn(D, device=DEV) * 0.1)
