@@ -265,6 +265,44 @@ void xent_fwd_bwd(Tensor logits, Tensor labels, Tensor loss, int64_t V, c10::opt
   mft::xent_fwd_bwd(bp(logits), labels.data_ptr<int64_t>(), fp(loss), logits.size(0), (int)V, logits.stride(0),
                     optp<float>(scale), (float)extra, write_grad, stream());
 }
+// Fused LM head + cross entropy over one chunk of rows (xent.hip lm_head_ce): logits = h W^T never
+// reach HBM.  E ([M, Vpad] bf16 workspace) receives exp(logit - tile max), or dlogits when
+// materialize (the caller then forms dW = E^T h); loss [M] fp32 per-row NLL; dh [M, K] bf16.
+void lm_head_ce(Tensor h, Tensor W, Tensor labels, int64_t V, c10::optional<Tensor> E, Tensor loss,
+                c10::optional<Tensor> scale, double extra, c10::optional<Tensor> dh, bool materialize) {
+  CHECK_CUDA(h); CHECK_BF16(h); CHECK_BF16(W); CHECK_F32(loss);
+  TORCH_CHECK(h.dim() == 2 && W.dim() == 2 && h.stride(1) == 1 && W.stride(1) == 1 && h.size(1) == W.size(1),
+              "lm_head_ce: h [M, K], W [Vpad, K] row-contiguous");
+  TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.is_contiguous() && labels.numel() == h.size(0),
+              "lm_head_ce: labels [M] contiguous int64");
+  const int M = h.size(0), K = h.size(1), Vpad = W.size(0);
+  TORCH_CHECK(K % 64 == 0 && Vpad % 64 == 0 && V > 0 && V <= Vpad, "lm_head_ce: K, Vpad multiples of 64, V <= Vpad");
+  TORCH_CHECK(h.stride(0) % 8 == 0 && W.stride(0) % 8 == 0, "lm_head_ce: leading dimensions must be multiples of 8");
+  TORCH_CHECK(loss.numel() == M && loss.is_contiguous(), "lm_head_ce: loss [M]");
+  if (E.has_value()) {
+    CHECK_BF16((*E));
+    TORCH_CHECK(E->size(0) == M && E->size(1) == Vpad && E->stride(1) == 1 && E->stride(0) % 8 == 0, "lm_head_ce: E [M, Vpad]");
+  }
+  if (dh.has_value()) {
+    CHECK_BF16((*dh));
+    TORCH_CHECK(E.has_value(), "lm_head_ce: the gradient needs E");
+    TORCH_CHECK(dh->size(0) == M && dh->size(1) == K && dh->stride(1) == 1 && dh->stride(0) % 8 == 0, "lm_head_ce: dh [M, K]");
+  }
+  c10::DeviceGuard g(h.device());
+  auto ws = torch::empty({mft::lm_head_ce_ws_floats(M, Vpad)}, h.options().dtype(torch::kFloat32));
+  mft::CeArgs a{};
+  a.h = bp(h); a.ldh = h.stride(0);
+  a.W = bp(W); a.ldw = W.stride(0);
+  a.labels = labels.data_ptr<int64_t>();
+  a.M = M; a.K = K; a.Vpad = Vpad; a.V = (int)V;
+  a.E = E.has_value() ? bp(*E) : nullptr; a.lde = E.has_value() ? E->stride(0) : 0;
+  a.loss = fp(loss);
+  a.scale = optp<float>(scale); a.extra = (float)extra;
+  a.dh = dh.has_value() ? bp(*dh) : nullptr; a.lddh = dh.has_value() ? dh->stride(0) : 0;
+  a.materialize = materialize;
+  a.ws = fp(ws);
+  mft::lm_head_ce(a, stream());
+}
 Tensor logsoftmax_gather(Tensor logits, Tensor idx, int64_t V) {
   CHECK_BF16(logits); TORCH_CHECK(logits.stride(1) == 1, "logits rows must be contiguous");
   auto out = torch::empty({logits.size(0), idx.numel()}, logits.options().dtype(torch::kFloat32));
@@ -610,6 +648,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("xent_fwd_bwd", &xent_fwd_bwd);
+  m.def("lm_head_ce", &lm_head_ce);
   m.def("logsoftmax_gather", &logsoftmax_gather);
   m.def("sumsq", &sumsq);
   m.def("nonfinite_check", &nonfinite_check);

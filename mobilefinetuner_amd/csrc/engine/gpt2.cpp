@@ -91,12 +91,12 @@ void GPT2::alloc() {
     b.mproj_b = frozen(zeros({C}, DType::BF16));
   }
   dropout_ctr = zeros({1}, DType::I64);
-  // LM-head CE chunk: rows of bf16 logits materialised at once, 16 GiB budget (MFT_CE_BUDGET_GB)
+  // LM-head CE chunk: rows per fused call (one [rows, Vpad] bf16 E workspace), 32 GiB budget (MFT_CE_BUDGET_GB)
   const char* env = std::getenv("MFT_CE_CHUNK");
   if (env) {
     ce_chunk = std::atoll(env);
   } else {
-    const double gb = std::getenv("MFT_CE_BUDGET_GB") ? std::atof(std::getenv("MFT_CE_BUDGET_GB")) : 16.0;
+    const double gb = std::getenv("MFT_CE_BUDGET_GB") ? std::atof(std::getenv("MFT_CE_BUDGET_GB")) : 32.0;
     const int64_t rows = (int64_t)(gb * (1ull << 30) / (2.0 * cfg_.vocab_padded()));
     ce_chunk = std::max<int64_t>(64, std::min<int64_t>(65536, rows / 64 * 64));
   }

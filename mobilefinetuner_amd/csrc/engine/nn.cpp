@@ -578,15 +578,23 @@ Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_
   for (int64_t i = 0; i < M; i += chunk) {
     const int64_t r = std::min(chunk, M - i);
     Tensor hi = hc.slice(0, i, i + r);
-    Tensor logits = empty({r, Vp}, DType::BF16, h.device());
-    gemm_nt(hi, w.c, Tensor(), logits);
-    ::mft::xent_fwd_bwd(bp(logits), lab.data<int64_t>() + i, fp(loss_rows) + i, r, V, Vp, fp(scale), 1.f, need ? 1 : 0,
-                        S());
-    if (need) {
-      Tensor dhi = dh.slice(0, i, i + r);
-      gemm_nn(logits, w.c, dhi);
-      if (need_w) gemm_wgrad(wbuf, logits, hi, w_grad_scale);
-    }
+    // fused forward (softmax statistics from the fp32 logits tile, E = exp(logit - tile max)) +
+    // per-tile-rescaled NN dgrad; E becomes dlogits in place only when W itself trains
+    Tensor E = need ? empty({r, Vp}, DType::BF16, h.device()) : Tensor();
+    Tensor ws = empty({::mft::lm_head_ce_ws_floats((int)r, (int)Vp)}, DType::F32, h.device());
+    ::mft::CeArgs a{};
+    a.h = bp(hi); a.ldh = C;
+    a.W = bp(w.c); a.ldw = C;
+    a.labels = lab.data<int64_t>() + i;
+    a.M = (int)r; a.K = (int)C; a.Vpad = (int)Vp; a.V = V;
+    a.E = need ? bp(E) : nullptr; a.lde = Vp;
+    a.loss = fp(loss_rows) + i;
+    a.scale = fp(scale); a.extra = 1.f;
+    a.dh = need ? bp(dh) + i * C : nullptr; a.lddh = C;
+    a.materialize = need_w ? 1 : 0;
+    a.ws = fp(ws);
+    ::mft::lm_head_ce(a, S());
+    if (need_w) gemm_wgrad(wbuf, E, hi, w_grad_scale);
   }
   Tensor loss = mul(sum(loss_rows), scale);
   if (need) {
@@ -611,9 +619,16 @@ std::pair<Tensor, Tensor> lm_head_nll(const Tensor& h, Param& w, const Tensor& l
   if (chunk <= 0) chunk = M;
   for (int64_t i = 0; i < M; i += chunk) {
     const int64_t r = std::min(chunk, M - i);
-    Tensor logits = empty({r, Vp}, DType::BF16, h.device());
-    gemm_nt(hc.slice(0, i, i + r), w.c, Tensor(), logits);
-    ::mft::xent_fwd_bwd(bp(logits), lab.data<int64_t>() + i, fp(loss_rows) + i, r, V, Vp, nullptr, 1.f, 0, S());
+    Tensor ws = empty({::mft::lm_head_ce_ws_floats((int)r, (int)Vp)}, DType::F32, h.device());
+    ::mft::CeArgs a{};  // loss only: no logits are stored
+    a.h = bp(hc) + i * hc.size(1); a.ldh = hc.size(1);
+    a.W = bp(w.c); a.ldw = w.c.size(1);
+    a.labels = lab.data<int64_t>() + i;
+    a.M = (int)r; a.K = (int)hc.size(1); a.Vpad = (int)Vp; a.V = V;
+    a.loss = fp(loss_rows) + i;
+    a.extra = 1.f;
+    a.ws = fp(ws);
+    ::mft::lm_head_ce(a, S());
   }
   Tensor cnt = empty({1}, DType::F32, h.device());
   k::count_valid(lab.data<int64_t>(), lab.numel(), -100, fp(cnt), S());

@@ -8,7 +8,7 @@
 //   mlp_gelu         fc GEMM + bias + GELU epilogue, proj GEMM; backward dGELU fused (gemm8.hip)
 //   lora_linear_aug  base GEMM over the augmented K dim [x | u] . [W | s B^T]^T (lora.hip + GEMM)
 //                    reference LoRALinear nn/lora_linear.cpp:47-108
-//   lm_head_ce       tied LM head + vocab-chunked cross entropy fwd+bwd (xent.hip + gemm8)
+//   lm_head_ce       tied LM head + fused cross entropy fwd+bwd (gemm8 CE epilogues, xent.hip)
 //                    reference lm_loss.cpp:19-210, gpt2_model.cpp:425-439
 // Trainable parameters are fp32 masters (autograd leaves; their .grad is a view into the
 // optimizer's flat fp32 buffer) with bf16 compute shadows; the kernels accumulate straight into

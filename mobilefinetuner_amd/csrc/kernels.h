@@ -58,7 +58,9 @@ int attn_bwd_path(int D, int Sq, int Sk, int window);
 
 // ---------------------------------------------------------------- GEMM (gemm.hip)
 enum GemmEpi { GEMM_EPI_NONE = 0, GEMM_EPI_BIAS = 1, GEMM_EPI_BIAS_GELU = 2, GEMM_EPI_DGELU = 3, GEMM_EPI_F32ACC = 4,
-               GEMM_EPI_LORA = 5, GEMM_EPI_F32PART = 6 /* internal: split-K fp32 slab */ };
+               GEMM_EPI_LORA = 5, GEMM_EPI_F32PART = 6 /* internal: split-K fp32 slab */,
+               // fused LM-head cross entropy (gemm8 only, driven by lm_head_ce in xent.hip)
+               GEMM_EPI_CE_FWD = 7, GEMM_EPI_CE_DGRAD = 8 };
 struct GemmArgs {
   const bf16_t* A;
   long lda;  // A [M, K] row-major
@@ -82,6 +84,19 @@ struct GemmArgs {
   // gemm_splitk_reduce adds into C in a fixed order (deterministic, no atomics)
   int ksplit;
   float* ws;
+  // GEMM_EPI_CE_FWD (NT, C = h W^T never stored as logits): per 256-column vocab tile and row the
+  // epilogue writes (tile max, tile sum-exp) to ce_stats [M][ceil(N/256)] (float pairs), the label
+  // logit to ce_lbl [M], and -- when C is set -- E = exp(logit - tile max) (bf16; columns >= ce_V
+  // are 0).  GEMM_EPI_CE_DGRAD (NN, dh = softmax(logits) W - onehot W from E): the accumulator is
+  // rescaled by ce_ratio at every vocab-tile start ([T][Mpad] in the tile-row order of
+  // lm_head_ce), the epilogue applies ce_fin [M] and subtracts ce_wlab [M] x W[label].
+  const int64_t* ce_labels;
+  float* ce_stats;
+  float* ce_lbl;
+  const float* ce_ratio;
+  const float* ce_fin;
+  const float* ce_wlab;
+  int ce_V;
 };
 bool gemm_supported(int M, int N, int K);
 // cfg: tile configuration (gemm.hip launch_e): 0 = 256x256, 1 = 128x256, 2 = 128x128, 3 = 256x128
@@ -117,6 +132,31 @@ void embed_bwd(const int64_t* ids, const bf16_t* dout, float* dwte, float* dwpe,
 // (columns >= V set to 0).  scale may be null (=> 1.0); extra multiplies it.
 void xent_fwd_bwd(bf16_t* logits, const int64_t* labels, float* loss, long M, int V, long ld, const float* scale,
                   float extra, int write_grad, hipStream_t st);
+// Fused LM head + cross entropy over a chunk of rows: logits = h W^T are never written to HBM.
+//   1. gemm8 NT with the CE_FWD epilogue: E = exp(logit - tile max) (bf16) + per-tile (max, sum-exp)
+//      + label logit from the fp32 accumulators;
+//   2. ce_finalize: row lse, loss, per-tile rescale factors;
+//   3. (grad) gemm8 NN with the CE_DGRAD main loop: dh = (softmax - onehot) W * scale from E with
+//      the per-(row, tile) softmax factor applied as an accumulator rescale at each vocab-tile
+//      boundary (no elementwise pass over the [M, V] operand), or -- when the W gradient is needed
+//      too (materialize) -- E is turned into dlogits in place and multiplied by a plain NN GEMM
+//      (the caller then forms dW = dlogits^T h from it).
+struct CeArgs {
+  const bf16_t* h; long ldh;   // [M, K]
+  const bf16_t* W; long ldw;   // [Vpad, K]
+  const int64_t* labels;       // [M] (-100 / out of range = ignored)
+  int M, K, Vpad, V;
+  bf16_t* E; long lde;         // [M, Vpad] workspace (null: loss only)
+  float* loss;                 // [M] per-row NLL (0 for ignored rows)
+  float* lse;                  // [M] (optional)
+  const float* scale;          // device scalar weight of a valid row (e.g. 1 / n_valid), null = 1
+  float extra;
+  bf16_t* dh; long lddh;       // [M, K] out (null: no gradient)
+  int materialize;             // E := dlogits (for a W gradient by the caller)
+  float* ws;                   // lm_head_ce_ws_floats(M, Vpad) floats
+};
+long lm_head_ce_ws_floats(int M, int Vpad);
+void lm_head_ce(const CeArgs& a, hipStream_t st);
 // log-softmax gather: out[m, c] = logits[m, idx[c]] - lse(logits[m])  (MMLU scoring)
 void logsoftmax_gather(const bf16_t* logits, const int64_t* idx, float* out, long M, int V, long ld, int nidx,
                        hipStream_t st);

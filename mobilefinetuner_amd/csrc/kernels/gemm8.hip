@@ -64,15 +64,24 @@ __device__ __forceinline__ void vm_wait() {
 
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Addresses are a wave-uniform base plus a 32-bit per-lane byte offset (the SGPR-base "saddr" form
+// of global_load_lds): 1 VGPR per load instead of a 64-bit VGPR pair, which keeps the 256-VGPR
+// budget of two waves per SIMD free for the epilogue variants.
+__device__ __forceinline__ void glds16_off(const bf16_t* base, uint32_t off_bytes, void* lds_wave_base) {
+  glds16_8(reinterpret_cast<const char*>(base) + off_bytes, lds_wave_base);
+}
+
 // stage one 128 x 64 half-tile: rows r0.. of src (clamped to rmax-1), columns k0..k0+63
 __device__ __forceinline__ void stage_half(bf16_t* lds, const bf16_t* src, long ld, int r0, int rmax, int k0) {
   const int tid = threadIdx.x, w = tid >> 6;
+  const int rb = min(r0, rmax - 1);
+  const bf16_t* base = src + (long)rb * ld + k0;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int c = t * 512 + tid;
     const int r = c >> 3, s = c & 7;
-    const int gr = min(r0 + r, rmax - 1);
-    glds16_8(src + (long)gr * ld + k0 + ((s ^ (r & 7)) << 3), lds + (t * 512 + w * 64) * 8);
+    const int gr = min(r0 + r, rmax - 1) - rb;
+    glds16_off(base, (uint32_t)((gr * (int)ld + ((s ^ (r & 7)) << 3)) * 2), lds + (t * 512 + w * 64) * 8);
   }
 }
 
@@ -85,12 +94,14 @@ __device__ __forceinline__ int tsw(int k) { return ((k & 3) | (((k >> 3) & 1) <<
 
 __device__ __forceinline__ void stage_half_t(bf16_t* lds, const bf16_t* src, long ld, int c0, int cmax, int k0) {
   const int tid = threadIdx.x, w = tid >> 6;
+  const int cb = min(c0, cmax - 8);
+  const bf16_t* base = src + (long)k0 * ld + cb;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int c = t * 512 + tid;
     const int r = c >> 4, s = c & 15;
-    const int gc = min(c0 + ((s ^ tsw(r)) << 3), cmax - 8);
-    glds16_8(src + (long)(k0 + r) * ld + gc, lds + (t * 512 + w * 64) * 8);
+    const int gc = min(c0 + ((s ^ tsw(r)) << 3), cmax - 8) - cb;
+    glds16_off(base, (uint32_t)((r * (int)ld + gc) * 2), lds + (t * 512 + w * 64) * 8);
   }
 }
 
@@ -238,6 +249,188 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4
   }
 }
 
+// ------------------------------------------------------------------ LM-head CE dgrad epilogue
+// dh = fin * acc - wlab * W[label] (B = W stored [Vpad, N]).  Every per-row operand of the lane's
+// 8 rows is loaded before the first store (the stores could alias them, so the compiler would
+// otherwise serialise 16 dependent load chains behind them).
+__device__ __forceinline__ void epilogue_ce_dgrad(const GemmArgs& g, f32x4_t (&acc)[4][4][2], int m0, int n0, int wm,
+                                                  int wn, int lane) {
+  const int g4 = lane >> 4;
+  const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
+  float fin[2][4], wl[2][4];
+  long lab[2][4];
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = min(m0 + qa * 128 + wm * 64 + i * 16 + (lane & 15), g.M - 1);
+      fin[qa][i] = g.ce_fin[rr];
+      wl[qa][i] = g.ce_wlab[rr];
+      lab[qa][i] = g.ce_labels[rr];
+    }
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa) {
+    u16x8_t wv[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int col = n0 + h * 128 + wn * 32 + cofs, colc = min(col, g.N - 8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long l = wl[qa][i] != 0.f ? lab[qa][i] : 0;
+        wv[h][i] = *reinterpret_cast<const u16x8_t*>(g.B + l * g.ldb + colc);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = qa ? (h ? 2 : 3) : (h ? 1 : 0);  // quadrant (qa, qb = h)
+      const int col = n0 + h * 128 + wn * 32 + cofs;
+      float o[4][8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[q][i][0][r]),
+                                                           __float_as_uint(acc[q][i][1][r]), false, false);
+          o[i][r] = __uint_as_float(sw[0]);
+          o[i][4 + r] = __uint_as_float(sw[1]);
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + qa * 128 + wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[i][e] = o[i][e] * fin[qa][i] - wl[qa][i] * bf2f(wv[h][i][e]);
+        if (col < g.N && row < g.M) store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, o[i]);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ LM-head CE forward epilogue
+// Logits tile (fp32 accumulators) -> per-row tile max and sum-exp, label logit, and (optionally)
+// E = exp(logit - tile max) in bf16.  A row's 256 tile columns are spread over the lane's 2 x 8
+// columns (quadrants qb = 0, 1), the 4 lane groups of the wave (shuffles) and the 4 wn-waves (LDS).
+// Numerics: the loss comes from fp32 logits; E is relative to its tile max, so every softmax term
+// keeps bf16's relative precision whatever the logit magnitude (raw bf16 logits of a pretrained
+// model, |logit| ~ 100, would be quantised to 0.5).
+__device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc)[4][4][2], int m0, int n0, int wm,
+                                                int wn, int lane, float* red) {
+  const int g4 = lane >> 4, r16 = lane & 15;
+  const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
+  const int T = (g.N + 255) / 256, tn = n0 >> 8;
+  float o[4][4][8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[q][i][0][r]),
+                                                         __float_as_uint(acc[q][i][1][r]), false, false);
+        o[q][i][r] = __uint_as_float(sw[0]);
+        o[q][i][4 + r] = __uint_as_float(sw[1]);
+      }
+  // quadrants: 0 = (A0, B0), 1 = (A0, B1), 2 = (A1, B1), 3 = (A1, B0); row half qa holds q = 2qa, 2qa+1
+  auto qcol = [&](int q) { return n0 + ((q == 1 || q == 2) ? 128 : 0) + wn * 32 + cofs; };
+  // only the last vocab tile has padding columns: the mask is a uniform branch elsewhere
+  const bool full = n0 + 256 <= g.ce_V;
+  float mt[2][4];
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = 2 * qa + h, c = qcol(q);
+        if (full) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m = fmaxf(m, o[q][i][e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (c + e < g.ce_V) m = fmaxf(m, o[q][i][e]);
+        }
+      }
+      m = fmaxf(m, __shfl_xor(m, 16));
+      m = fmaxf(m, __shfl_xor(m, 32));
+      mt[qa][i] = m;
+    }
+  const int rl0 = wm * 64 + r16;  // tile row = qa * 128 + rl0 + 16 i
+  if (g4 == 0) {
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(qa * 128 + rl0 + i * 16) * 4 + wn] = mt[qa][i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4_t v = *reinterpret_cast<const f32x4_t*>(red + (qa * 128 + rl0 + i * 16) * 4);
+      mt[qa][i] = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));  // -inf only for an all-padding tile
+    }
+  __syncthreads();  // red is reused for the sums
+  long labs[2][4];
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) labs[qa][i] = g.ce_labels[min(m0 + qa * 128 + rl0 + i * 16, g.M - 1)];
+  float st[2][4];
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int R = m0 + qa * 128 + rl0 + i * 16;
+      const bool rok = R < g.M;
+      const long lab = labs[qa][i];
+      const float mb = mt[qa][i] * 1.4426950408889634f;
+      float s = 0.f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = 2 * qa + h, c = qcol(q);
+        const long d = lab - c;
+        if (rok && d >= 0 && d < 8) {  // the label column: one select chain, one store
+          float xl = o[q][i][0];
+#pragma unroll
+          for (int e = 1; e < 8; ++e) xl = d == e ? o[q][i][e] : xl;
+          g.ce_lbl[R] = xl;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = exp2f(fmaf(o[q][i][e], 1.4426950408889634f, -mb));
+          if (!full && c + e >= g.ce_V) x = 0.f;
+          o[q][i][e] = x;
+          s += x;
+        }
+        if (g.C && rok && c < g.N) store8(reinterpret_cast<bf16_t*>(g.C) + (long)R * g.ldc + c, o[q][i]);
+      }
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      st[qa][i] = s;
+    }
+  if (g4 == 0) {
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(qa * 128 + rl0 + i * 16) * 4 + wn] = st[qa][i];
+  }
+  __syncthreads();
+  if (wn == 0 && g4 == 0) {
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int R = m0 + qa * 128 + rl0 + i * 16;
+        if (R >= g.M) continue;
+        const f32x4_t v = *reinterpret_cast<const f32x4_t*>(red + (qa * 128 + rl0 + i * 16) * 4);
+        float* p = g.ce_stats + ((long)R * T + tn) * 2;
+        p[0] = mt[qa][i];
+        p[1] = (v[0] + v[1]) + (v[2] + v[3]);
+      }
+  }
+}
+
 #ifdef MFT_G8_STAMPS  // diagnostic build only (scripts/g8_stamps.hip): s_memtime per phase per WG
 __device__ unsigned long long* g8_stamps;
 #ifdef MFT_G8_STAMPS_RT  // 100 MHz constant clock instead of the shader clock
@@ -333,6 +526,63 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     if constexpr (AT || BT) __builtin_amdgcn_sched_barrier(0);
   };
 
+  // CE_DGRAD: the A operand E holds exp(logit - tile max) per 256-column vocab tile (4 K-tiles); at
+  // each tile start the accumulator is rescaled by exp(m'_prev - m'_cur) (ratios precomputed per
+  // row by ce_finalize), so after the last tile acc = sum_t exp(m'_t - m'_last) E_t W_t and the
+  // epilogue's factor exp(m'_last - lse) turns it into softmax . W -- no elementwise pass over E.
+  // The 256 row factors of a tile arrive by one LDS-DMA of wave 0 (1 KB, 2 slots after the half-
+  // tile buffers), issued in phase 5 two iterations ahead: it is older than the 4 in-flight
+  // half-tiles at the phase-8 vm_wait, so the counted waits retire it with no extra wait.
+  float* const rslot = reinterpret_cast<float*>(smem + 8 * kHalf);
+  auto ce_dma = [&](int kt) {
+    if constexpr (EPI == GEMM_EPI_CE_DGRAD) {
+      const int tt = kt / 4 + 1;
+      if ((kt & 3) == 0 && tt * 4 < nk && w == 0) {
+        const long mpad = (long)((g.M + 255) / 256) * 256;
+        glds16_8(g.ce_ratio + (long)tt * mpad + m0 + lane * 4, rslot + (tt & 1) * 256);
+      }
+    }
+  };
+  // the phase's 4 row factors: read with its fragments (before lds_sync), applied after it
+  auto ce_read = [&](int q, int kt) -> f32x4_t {
+    if constexpr (EPI == GEMM_EPI_CE_DGRAD) {
+      if ((kt & 3) == 0 && kt > 0)
+        return *reinterpret_cast<const f32x4_t*>(rslot + ((kt / 4) & 1) * 256 + (q < 2 ? 0 : 128) + wm * 64 +
+                                                 (lane & 15) * 4);
+    }
+    return f32x4_t{1.f, 1.f, 1.f, 1.f};
+  };
+  // The rescale of each accumulator block is issued right before its first MFMA of the even
+  // K-tile, inside the MFMA cluster: 4 v_mul_f32 fit the 16-cycle issue gap of the MFMA before (the
+  // same multiplies placed in the load segment cost ~15% of the kernel: VALU there competes with
+  // the partner wave's prio-1 MFMA cluster).  Branch-free (factor 1 off the tile starts): a
+  // second MFMA code path for the tile starts spills.  Scalar asm multiplies: left to the
+  // compiler they become v_pk_mul_f32, which costs extra cycles beside MFMAs.
+  auto mma_ce = [&](int q, const f32x4_t& r) {
+    if constexpr (EPI == GEMM_EPI_CE_DGRAD) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if (ks == 0) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float x = acc[q][i][j][e];
+                asm("v_mul_f32 %0, %1, %2" : "=v"(x) : "v"(x), "v"(r[i]));
+                acc[q][i][j][e] = x;
+              }
+            }
+            acc[q][i][j] = mfma16(bfr[j][ks], af[i][ks], acc[q][i][j]);
+          }
+      __builtin_amdgcn_s_setprio(0);
+    } else {
+      mma(q);
+    }
+  };
+
   // prologue: E <- K-tile 0 (all halves), O <- K-tile 1 (A0, B1); retire E
   stage(0, 0, 0);
   stage(0, 3, 0);
@@ -356,37 +606,42 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     // phase 1: quadrant (A0, B0); stage O.A1 (kt+1)
     read_a(0, 0);
     read_b(0, 0);
+    const f32x4_t rq0 = ce_read(0, kt);
     stage(1, 1, kt + 1);
     lds_sync();
     raw_barrier();
-    mma(0);
+    mma_ce(0, rq0);
     raw_barrier();
     // phase 2: (A0, B1); stage O.B0 (kt+1)
     read_b(0, 1);
+    const f32x4_t rq1 = ce_read(1, kt);
     stage(1, 2, kt + 1);
     lds_sync();
     raw_barrier();
-    mma(1);
+    mma_ce(1, rq1);
     raw_barrier();
     // phase 3: (A1, B1); stage E.A0 (kt+2)
     read_a(0, 1);
+    const f32x4_t rq2 = ce_read(2, kt);
     stage(0, 0, kt + 2);
     lds_sync();
     raw_barrier();
-    mma(2);
+    mma_ce(2, rq2);
     raw_barrier();
     // phase 4: (A1, B0); stage E.B1 (kt+2); retire the odd buffer
     read_b(0, 0);
+    const f32x4_t rq3 = ce_read(3, kt);
     stage(0, 3, kt + 2);
     lds_sync();
     vm_wait<4>();
     raw_barrier();
-    mma(3);
+    mma_ce(3, rq3);
     raw_barrier();
     // ---- phases 5-8: odd buffer, K-tile kt+1 (MFMAs skipped past the end; loads/waits stay uniform)
     // phase 5: (A0, B0); stage E.A1 (kt+2)
     read_a(1, 0);
     read_b(1, 0);
+    ce_dma(kt);
     stage(0, 1, kt + 2);
     lds_sync();
     raw_barrier();
@@ -419,7 +674,9 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   vm_wait<0>();  // drain the clamped tail prefetches (LDS-DMA must not outlive the workgroup)
   G8_STAMP(2);
 
-  epilogue8<EPI>(g, acc, m0, n0, wm, wn, lane, split);
+  if constexpr (EPI == GEMM_EPI_CE_FWD) epilogue_ce_fwd(g, acc, m0, n0, wm, wn, lane, reinterpret_cast<float*>(smem));
+  else if constexpr (EPI == GEMM_EPI_CE_DGRAD) epilogue_ce_dgrad(g, acc, m0, n0, wm, wn, lane);
+  else epilogue8<EPI>(g, acc, m0, n0, wm, wn, lane, split);
   G8_STAMP(3);
 }
 
@@ -627,7 +884,8 @@ static bool gemm8_persistent() {
 
 template <int EPI, bool AT, bool BT>
 static void launch8(const GemmArgs& g, hipStream_t st) {
-  constexpr size_t shm = sizeof(bf16_t) * 8 * kHalf;  // 128 KB
+  // 128 KB of half-tile buffers (+ 2 KB of row-factor slots for the CE dgrad)
+  constexpr size_t shm = sizeof(bf16_t) * 8 * kHalf + (EPI == GEMM_EPI_CE_DGRAD ? 2048 : 0);
   static bool attr = false;
   if (!attr) {
     MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI, AT, BT>,
@@ -637,16 +895,19 @@ static void launch8(const GemmArgs& g, hipStream_t st) {
   const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
   const int ks = g.ksplit > 1 ? g.ksplit : 1;
   // (the LoRA epilogue's extra operand loads spill in the persistent form: one tile per workgroup)
-  if (ks == 1 && EPI != GEMM_EPI_F32PART && EPI != GEMM_EPI_LORA && gemm8_persistent()) {
-    static bool attr_p = false;
-    if (!attr_p) {
-      MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, AT, BT>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-      attr_p = true;
+  if constexpr (EPI != GEMM_EPI_F32PART && EPI != GEMM_EPI_LORA && EPI != GEMM_EPI_CE_FWD &&
+                EPI != GEMM_EPI_CE_DGRAD) {
+    if (ks == 1 && gemm8_persistent()) {
+      static bool attr_p = false;
+      if (!attr_p) {
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, AT, BT>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        attr_p = true;
+      }
+      const int grid = tiles < num_cus() ? tiles : num_cus();
+      gemm8p_kernel<EPI, AT, BT><<<grid, 512, shm, st>>>(g);
+      return;
     }
-    const int grid = tiles < num_cus() ? tiles : num_cus();
-    gemm8p_kernel<EPI, AT, BT><<<grid, 512, shm, st>>>(g);
-    return;
   }
   gemm8_kernel<EPI, AT, BT><<<tiles * ks, 512, shm, st>>>(g);
 }
@@ -710,7 +971,8 @@ bool gemm8_supported(int M, int N, int K, bool a_t, bool b_t) {
 
 void gemm8x(const GemmArgs& g0, int epi, bool a_t, bool b_t, hipStream_t st) {
   GemmArgs g = g0;
-  if (!gemm8_supported(g.M, g.N, g.K, a_t, b_t)) {
+  // per-lane staging offsets are 32-bit byte offsets from a uniform base (128 rows x ld x 2 B)
+  if (!gemm8_supported(g.M, g.N, g.K, a_t, b_t) || g.lda > (1L << 23) || g.ldb > (1L << 23)) {
     fprintf(stderr, "mft::gemm8: unsupported shape M=%d N=%d K=%d (a_t=%d b_t=%d)\n", g.M, g.N, g.K, a_t, b_t);
     abort();
   }
@@ -739,6 +1001,20 @@ void gemm8x(const GemmArgs& g0, int epi, bool a_t, bool b_t, hipStream_t st) {
         abort();
       }
       launch8_layout<GEMM_EPI_LORA>(g, a_t, b_t, st);
+      break;
+    case GEMM_EPI_CE_FWD:  // NT only (logits = h W^T)
+      if (a_t || b_t || g.ksplit > 1 || !g.ce_labels || !g.ce_stats || !g.ce_lbl || g.ce_V <= 0 || g.ce_V > g.N) {
+        fprintf(stderr, "mft::gemm8: CE forward epilogue needs the NT layout, labels/stats/lbl, 0 < V <= N\n");
+        abort();
+      }
+      launch8<GEMM_EPI_CE_FWD, false, false>(g, st);
+      break;
+    case GEMM_EPI_CE_DGRAD:  // NN only (dh = dlogits W, W stored [V, N])
+      if (a_t || !b_t || g.ksplit > 1 || !g.ce_labels || !g.ce_ratio || !g.ce_fin || !g.ce_wlab) {
+        fprintf(stderr, "mft::gemm8: CE dgrad needs the NN layout and ratio/fin/wlab/labels\n");
+        abort();
+      }
+      launch8<GEMM_EPI_CE_DGRAD, false, true>(g, st);
       break;
     default: fprintf(stderr, "mft::gemm8: bad epilogue %d\n", epi); abort();
   }

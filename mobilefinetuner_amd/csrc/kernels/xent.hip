@@ -162,6 +162,139 @@ __global__ __launch_bounds__(256) void logsoftmax_gather_kernel(const bf16_t* __
   for (int c = threadIdx.x; c < nidx; c += blockDim.x) out[row * nidx + c] = bf2f(x[idx[c]]) - lse;
 }
 
+// ------------------------------------------------------------------ fused LM head + CE (lm_head_ce)
+// Row positions inside a 256-row tile in the order the CE dgrad main loop reads its row factors:
+// lane (r16) of wave-row wm reads rows qa * 128 + wm * 64 + 16 i + r16 (i = 0..3) as one 16-B word.
+__device__ __forceinline__ int ce_row_pos(int R) {
+  const int rl = R & 255;
+  return (R & ~255) + (rl >> 6) * 64 + (rl & 15) * 4 + ((rl >> 4) & 3);
+}
+
+// 64 rows per block.  Pass 1 (a wave per row, lanes over vocab tiles): row max of the tile maxima,
+// lse = max + log sum_t s_t exp(m_t - max), loss, the dgrad's final factor and label weight.
+// Pass 2: ratio[t][pos(R)] = exp(m'_{t-1} - m'_t), m'_t = max(m_t, rowmax - 60) (a tile 60 below
+// the row max contributes < e^-60: clamping keeps every ratio and partial sum finite in fp32).
+__global__ __launch_bounds__(256) void ce_finalize_kernel(const float2* __restrict__ stats, const float* __restrict__ lbl,
+                                                          const int64_t* __restrict__ labels, int M, int T, int V,
+                                                          long mpad, const float* __restrict__ scale, float extra,
+                                                          float* __restrict__ loss, float* __restrict__ lse_out,
+                                                          float* __restrict__ ratio, float* __restrict__ fin,
+                                                          float* __restrict__ wlab) {
+  __shared__ float s_mx[64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r0 = blockIdx.x * 64;
+  for (int rr = w; rr < 64; rr += 4) {
+    const int R = r0 + rr;
+    if (R >= M) break;
+    const float2* st = stats + (long)R * T;
+    float m = -INFINITY;
+    for (int t = lane; t < T; t += 64) m = fmaxf(m, st[t].x);
+    m = wave_max(m);
+    float s = 0.f;
+    for (int t = lane; t < T; t += 64) {
+      const float2 v = st[t];
+      if (v.y > 0.f) s += v.y * __expf(v.x - m);
+    }
+    s = wave_sum(s);
+    if (lane == 0) {
+      const float l = m + __logf(s);
+      const int64_t lab = labels[R];
+      const bool valid = lab >= 0 && lab < V;
+      loss[R] = valid ? l - lbl[R] : 0.f;
+      if (lse_out) lse_out[R] = l;
+      if (fin) {
+        const float wv = valid ? (scale ? *scale : 1.f) * extra : 0.f;
+        wlab[R] = wv;
+        fin[R] = wv * __expf(fmaxf(st[T - 1].x, m - 60.f) - l);
+      }
+      s_mx[rr] = m;
+    }
+  }
+  if (!ratio) return;
+  __syncthreads();
+  const int rr = threadIdx.x & 63, R = r0 + rr;
+  if (R >= M) return;
+  const float2* st = stats + (long)R * T;
+  const float floor_m = s_mx[rr] - 60.f;
+  const long dst = ce_row_pos(R);
+  for (int t = 1 + w; t < T; t += 4)
+    ratio[(long)t * mpad + dst] = __expf(fmaxf(st[t - 1].x, floor_m) - fmaxf(st[t].x, floor_m));
+}
+
+// E (exp(logit - tile max)) -> dlogits = (softmax - onehot) * w in place; padding columns stay 0
+__global__ __launch_bounds__(256) void ce_materialize_kernel(bf16_t* __restrict__ E, long lde, int N,
+                                                             const float2* __restrict__ stats, int T,
+                                                             const float* __restrict__ lse,
+                                                             const int64_t* __restrict__ labels, int V,
+                                                             const float* __restrict__ scale, float extra) {
+  const long R = blockIdx.x;
+  const int64_t lab = labels[R];
+  const bool valid = lab >= 0 && lab < V;
+  const float wv = valid ? (scale ? *scale : 1.f) * extra : 0.f;
+  const float l = lse[R];
+  bf16_t* e = E + R * lde;
+  for (int c8 = threadIdx.x; c8 < N / 8; c8 += blockDim.x) {
+    const int c = c8 * 8;
+    const float f = wv * __expf(stats[R * T + (c >> 8)].x - l);
+    float v[8];
+    load8(e + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] *= f;
+      if (c + j == lab) v[j] -= wv;
+    }
+    store8(e + c, v);
+  }
+}
+
+long lm_head_ce_ws_floats(int M, int Vpad) {
+  const long T = (Vpad + 255) / 256, mpad = (long)((M + 255) / 256) * 256;
+  return 2 * (long)M * T + 4L * M + T * mpad + 64;
+}
+
+void lm_head_ce(const CeArgs& a, hipStream_t st) {
+  if (a.M <= 0) return;
+  const int T = (a.Vpad + 255) / 256;
+  const long mpad = (long)((a.M + 255) / 256) * 256;
+  float* p = a.ws;
+  float* stats = p; p += 2 * (long)a.M * T;
+  float* lbl = p; p += a.M;
+  float* lse = a.lse ? a.lse : p; p += a.M;
+  float* fin = p; p += a.M;
+  float* wlab = p; p += a.M;
+  float* ratio = a.ws + ((p - a.ws + 63) / 64) * 64;  // 256-B aligned: read by 16-B LDS-DMA
+  const bool grad = a.dh != nullptr;
+  if (grad && !a.E) {
+    fprintf(stderr, "mft::lm_head_ce: the gradient needs the E workspace\n");
+    abort();
+  }
+  GemmArgs f{};
+  f.A = a.h; f.lda = a.ldh;
+  f.B = a.W; f.ldb = a.ldw;
+  f.C = a.E; f.ldc = a.lde;
+  f.M = a.M; f.N = a.Vpad; f.K = a.K; f.alpha = 1.f;
+  f.ce_labels = a.labels; f.ce_stats = stats; f.ce_lbl = lbl; f.ce_V = a.V;
+  gemm8x(f, GEMM_EPI_CE_FWD, false, false, st);
+  const bool fused = grad && !a.materialize;
+  ce_finalize_kernel<<<(a.M + 63) / 64, 256, 0, st>>>(reinterpret_cast<const float2*>(stats), lbl, a.labels, a.M, T,
+                                                       a.V, mpad, a.scale, a.extra, a.loss, lse,
+                                                       fused ? ratio : nullptr, fused ? fin : nullptr, wlab);
+  if (!grad) return;
+  GemmArgs d{};
+  d.A = a.E; d.lda = a.lde;
+  d.B = a.W; d.ldb = a.ldw;
+  d.C = a.dh; d.ldc = a.lddh;
+  d.M = a.M; d.N = a.K; d.K = a.Vpad; d.alpha = 1.f;
+  if (a.materialize) {
+    ce_materialize_kernel<<<a.M, 256, 0, st>>>(a.E, a.lde, a.Vpad, reinterpret_cast<const float2*>(stats), T, lse,
+                                               a.labels, a.V, a.scale, a.extra);
+    gemm8x(d, GEMM_EPI_NONE, false, true, st);
+  } else {
+    d.ce_labels = a.labels; d.ce_ratio = ratio; d.ce_fin = fin; d.ce_wlab = wlab;
+    gemm8x(d, GEMM_EPI_CE_DGRAD, false, true, st);
+  }
+}
+
 void xent_fwd_bwd(bf16_t* logits, const int64_t* labels, float* loss, long M, int V, long ld, const float* scale,
                   float extra, int write_grad, hipStream_t st) {
   if (M <= 0) return;

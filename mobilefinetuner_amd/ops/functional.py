@@ -1018,23 +1018,31 @@ def dropout_counter(device):
 
 # ---------------------------------------------------------------- fused LM head + cross entropy
 def default_ce_chunk(vpad: int) -> int:
-    """Rows of bf16 logits materialised at once (the rest of the vocab-chunked CE never exists).
+    """Rows of the LM-head CE processed per fused call (each call holds one [rows, Vpad] bf16 E
+    workspace: exp(logit - tile max), the only vocab-wide tensor, never the logits themselves).
 
-    Sized for 288 GB of HBM: a 16 GiB logits budget (MFT_CE_BUDGET_GB), at most 65536 rows, i.e. the
-    whole GPT-2 bench step (512 x 128 tokens, 6.6 GB) in ONE LM-head GEMM / CE / dgrad triple and
-    Gemma-3 (262144 columns) in 32768-row chunks.  Measured on MI355X (one call, GPT-2 LoRA bench):
-    4096 rows 47.2 ms/step, 8192 44.5, 16384 44.1, 32768 44.0, 65536 43.3 -- fewer, larger GEMMs win
-    and the L3-resident small chunks lose (profiles/)."""
+    Sized for 288 GB of HBM: a 32 GiB budget (MFT_CE_BUDGET_GB), at most 65536 rows -- the whole
+    GPT-2 bench step (6.6 GB) and the whole Gemma-3 bench step (262144 columns, 32 GiB) in ONE
+    call: the NN dgrad has only ceil(C / 256) column tiles, so row chunks smaller than the step
+    leave CUs idle (Gemma, C = 640: 2 x 32768-row calls 57.5 ms vs one 65536-row call 52.9 ms;
+    GPT-2 4096-row chunks were 9% slower per step in round 1, profiles/)."""
     import os
     env = os.environ.get("MFT_CE_CHUNK")
     if env:
         return int(env)
-    budget = float(os.environ.get("MFT_CE_BUDGET_GB", "16")) * (1 << 30)
+    budget = float(os.environ.get("MFT_CE_BUDGET_GB", "32")) * (1 << 30)
     rows = int(budget // (2 * vpad))
     return max(64, min(65536, rows // 64 * 64))
 
 
 class _LMHeadCE(Function):
+    """Fused LM head + CE (xent.hip ``lm_head_ce``): per chunk of rows ONE gemm8 forward whose
+    epilogue reduces the fp32 logits tile to (max, sum-exp) and stores E = exp(logit - tile max),
+    a row finalize, and -- for dh -- one gemm8 NN whose main loop rescales its accumulator per
+    vocab tile, so neither logits nor dlogits are ever produced by an elementwise pass.  When the
+    LM-head weight itself trains (full fine-tune, tied wte) E is turned into dlogits in place and
+    also feeds the TN weight-gradient GEMM."""
+
     @staticmethod
     def forward(ctx, h, w, labels, V, chunk, w_grad_scale):
         C = native()
@@ -1049,20 +1057,15 @@ class _LMHeadCE(Function):
         dh = torch.empty_like(h) if need_grad else None
         wbuf = _grad_buf(w) if need_grad else None
         wtmp = torch.zeros(w.shape, device=h.device) if (need_grad and _needs(w) and wbuf is None) else None
+        want_w = wbuf is not None or wtmp is not None
         for i in range(0, M, chunk):
             hc = h[i:i + chunk]
-            if wc.shape[0] > 65536:
-                from ..utils.gemm_tuning import no_tuning
-                with no_tuning():
-                    logits = gemm_linear(hc, wc)
-            else:
-                logits = gemm_linear(hc, wc)                   # [rows, Vpad] bf16
-            C.xent_fwd_bwd(logits, labels[i:i + chunk], loss_rows[i:i + chunk], V, scale, 1.0, need_grad)
-            if need_grad:
-                gemm_dx(logits, wc, out=dh[i:i + chunk])       # dh = dlogits W, gemm8 NN
-                if wbuf is not None or wtmp is not None:
-                    tgt = wbuf if wbuf is not None else wtmp
-                    _mm_wgrad_into(tgt, logits, hc, w_grad_scale)  # dW += dlogits^T h, gemm8 TN
+            E = torch.empty(hc.shape[0], wc.shape[0], device=h.device, dtype=torch.bfloat16) if need_grad else None
+            C.lm_head_ce(hc, wc, labels[i:i + chunk], V, E, loss_rows[i:i + chunk], scale, 1.0,
+                         dh[i:i + chunk] if need_grad else None, want_w)
+            if want_w:
+                tgt = wbuf if wbuf is not None else wtmp
+                _mm_wgrad_into(tgt, E, hc, w_grad_scale)       # dW += dlogits^T h, gemm8 TN
         # a tied weight (GPT-2 wte) receives its final contribution later, from the embedding
         # backward, which fires the hook; announcing it here would let a DP bucket reduce early
         if wbuf is not None and not getattr(w, "_mft_tied", False):
@@ -1084,8 +1087,9 @@ class _LMHeadCE(Function):
 @_device_op
 def lm_head_cross_entropy(h, w, labels, vocab_size, chunk=None, w_grad_scale=1.0):
     """Mean token NLL of logits = h W^T (W [Vpad, C], first vocab_size rows real) vs labels
-    (already shifted; -100 = ignore).  Never materialises the full logits: chunks of rows are
-    GEMM'd, turned into dlogits in place and immediately multiplied back (dh, dW).
+    (already shifted; -100 = ignore).  Logits never reach HBM: per chunk of rows the gemm8 forward
+    epilogue reduces them to per-tile softmax statistics (+ E = exp(logit - tile max)) and the NN
+    dgrad consumes E with a per-tile accumulator rescale (see ``_LMHeadCE``).
     NOTE: the W gradient is produced during forward and scaled by ``w_grad_scale`` (pass the
     same factor the loss is later multiplied by, e.g. 1/grad_accum); dh honours grad_output."""
     if chunk is None:
@@ -1104,7 +1108,7 @@ def lm_head_token_nll(h, w, labels, vocab_size, chunk=None):
             chunk = default_ce_chunk(wc.shape[0])
         labels = labels.reshape(-1).contiguous()
         loss_rows = torch.empty(M, device=h.device, dtype=torch.float32)
-        for i in range(0, M, chunk):
-            logits = gemm_linear(h[i:i + chunk], wc)
-            C.xent_fwd_bwd(logits, labels[i:i + chunk], loss_rows[i:i + chunk], vocab_size, None, 1.0, False)
+        for i in range(0, M, chunk):  # loss only: the fused forward stores no logits at all
+            C.lm_head_ce(h[i:i + chunk].contiguous(), wc, labels[i:i + chunk], vocab_size, None, loss_rows[i:i + chunk],
+                         None, 1.0, None, False)
         return loss_rows.sum(), (labels >= 0).sum()
