@@ -63,6 +63,14 @@ CONFIGS = {
 }
 
 
+def _odesc(a):
+    return " + host-offloaded AdamW (" + ("fp32" if a.offload_fp32 else "bf16 stochastic-rounded") + " moments)"
+
+
+def _force_comm():
+    return dist.is_initialized() and os.environ.get("MFT_DP_FORCE_COMM", "0") == "1"
+
+
 def build(a, cfgd, dev, world):
     from mobilefinetuner_amd.optim.adamw import FusedAdamW
     from mobilefinetuner_amd.parallel.ddp import DataParallel
@@ -91,7 +99,7 @@ def build(a, cfgd, dev, world):
             L.inject_gpt2(model, spec)
         flat = FlatParams(L.lora_parameters(model), dev)
         opt = FusedAdamW(flat, lr=2e-4, weight_decay=0.0, max_grad_norm=1.0)
-        dp = DataParallel(flat) if world > 1 else None
+        dp = DataParallel(flat) if (world > 1 or _force_comm()) else None
         desc = f"{name} LoRA r={a.rank} alpha={a.alpha:g} targets={a.targets or cfgd['targets']}"
     else:
         model.set_full_finetune()
@@ -101,22 +109,28 @@ def build(a, cfgd, dev, world):
         if a.zero >= 0:  # explicit override
             zero = a.zero
         offload = bool(cfgd.get("offload", False) or a.offload_optimizer)
+        # host-offloaded AdamW moments in bf16 (the reference's --shard_fp16_disk default 1)
+        okw = dict(offload=offload, offload_dtype=torch.float32 if a.offload_fp32 else torch.bfloat16)
         if zero == 3:
             from mobilefinetuner_amd.parallel.zero3 import attach_zero3
-            z3 = attach_zero3(model, dev, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0, offload=offload)
-            desc = f"{name} full fine-tune ZeRO-3" + (" + host-offloaded AdamW" if offload else "")
-            step = TrainStep(model, z3.flat, z3, grad_accum=a.grad_accum, dp=z3, use_graph=False)
+            z3 = attach_zero3(model, dev, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0, **okw)
+            desc = f"{name} full fine-tune ZeRO-3" + (_odesc(a) if offload else "")
+            step = TrainStep(model, z3.flat, z3, grad_accum=a.grad_accum, dp=z3, use_graph=not (a.no_graph or offload))
             return model, step, vocab, desc, sum(p.numel() for p in model.parameters())
         flat = FlatParams(model.named_parameters(), dev, pad_multiple=max(1, world))
         if zero:
             from mobilefinetuner_amd.parallel.zero import ZeroOptimizer, ZeroReducer
-            opt = ZeroOptimizer(flat, zero, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0, offload=offload)
+            opt = ZeroOptimizer(flat, zero, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0, **okw)
             dp = ZeroReducer(opt)
         else:
-            opt = FusedAdamW(flat, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0, offload=offload)
-            dp = DataParallel(flat) if world > 1 else None
-        desc = f"{name} full fine-tune" + (f" ZeRO-{zero}" if zero else "") + (" + host-offloaded AdamW" if offload else "")
-    step = TrainStep(model, flat, opt, grad_accum=a.grad_accum, dp=dp, use_graph=not a.no_graph)
+            opt = FusedAdamW(flat, lr=1e-5, weight_decay=0.01, max_grad_norm=1.0, **okw)
+            dp = DataParallel(flat, reduce_dtype=torch.bfloat16 if a.bf16_grads else None) \
+                if (world > 1 or _force_comm()) else None
+        desc = f"{name} full fine-tune" + (f" ZeRO-{zero}" if zero else "") + (_odesc(a) if offload else "")
+    # a host-offloaded optimizer step is PCIe-bound: it runs eagerly (as graph memcpy nodes its
+    # chunk copies were slower, 369 vs 306 ms/step on GPT-2 XL ZeRO-3)
+    offload = cfgd["mode"] == "full" and bool(cfgd.get("offload", False) or a.offload_optimizer)
+    step = TrainStep(model, flat, opt, grad_accum=a.grad_accum, dp=dp, use_graph=not (a.no_graph or offload))
     nparams = sum(p.numel() for p in model.parameters())
     return model, step, vocab, desc, nparams
 
@@ -144,6 +158,7 @@ def main():
                     help="micro-batch (sequences) per GPU (0 = the config's default)")
     ap.add_argument("--seq", type=int, default=0)
     ap.add_argument("--offload_optimizer", action="store_true", help="full fine-tune: AdamW state in pinned host DRAM")
+    ap.add_argument("--offload_fp32", action="store_true", help="offloaded AdamW moments in fp32 (default bf16)")
     ap.add_argument("--zero", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
                     help="full fine-tune configs: ZeRO stage override (-1 = the config's, used when N > 1)")
     ap.add_argument("--rank", type=int, default=8)
@@ -151,6 +166,7 @@ def main():
     ap.add_argument("--targets", default="")
     ap.add_argument("--grad_accum", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--bf16_grads", action="store_true", help="full fine-tune DP: all-reduce gradients in bf16")
     ap.add_argument("--cpu_smoke", action="store_true",
                     help="gpt2-tiny on the CPU over gloo (tests the multi-rank bench path without a GPU)")
     a = ap.parse_args()
@@ -176,8 +192,14 @@ def main():
         if world > 1:
             dist.init_process_group("gloo")
     else:
-        if world > 1:
+        force_comm = os.environ.get("MFT_DP_FORCE_COMM", "0") == "1"
+        if world > 1 or force_comm:
             torch.cuda.set_device(local_rank)
+            if world == 1:  # 1-rank RCCL group: profile the reducer's collectives on one GPU
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 2000))
+                os.environ.setdefault("RANK", "0")
+                os.environ.setdefault("WORLD_SIZE", "1")
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         dev = torch.device("cuda", local_rank)
         torch.cuda.set_device(dev)
@@ -255,7 +277,8 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
+        dist.barrier()
         dist.destroy_process_group()
 
 

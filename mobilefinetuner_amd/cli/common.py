@@ -65,7 +65,9 @@ def add_shard_args(ap):
                    help="AdamW moments in pinned host DRAM, streamed through the GPU per chunk on a copy stream")
     g.add_argument("--shard_dir", default="")
     g.add_argument("--shard_budget_mb", type=int, default=512)
-    g.add_argument("--shard_fp16_disk", type=int, default=1)
+    g.add_argument("--shard_fp16_disk", type=int, default=1,
+                   help="16-bit host/disk copies: host-offloaded AdamW moments in bf16 with stochastic rounding "
+                        "(half the PCIe bytes); sharded frozen weights are bf16 already")
     g.add_argument("--zero_stage", type=int, default=0, choices=[0, 1, 2, 3],
                    help="ZeRO partitioning across ranks: optimizer state (1), + gradients (2), + parameters "
                         "with per-block all-gather / reduce-scatter (3)")

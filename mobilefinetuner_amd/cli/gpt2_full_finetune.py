@@ -81,7 +81,8 @@ def main(argv=None):
     if a.zero_stage == 3:
         from ..parallel.zero3 import attach_zero3
         z3 = attach_zero3(model, dev, lr=a.lr, weight_decay=a.weight_decay, max_grad_norm=a.clip_grad_norm,
-                          l2_coupled=a.compat_l2_adam, offload=offload)
+                          l2_coupled=a.compat_l2_adam, offload=offload,
+                          offload_dtype=torch.bfloat16 if a.shard_fp16_disk else torch.float32)
         flat = z3.flat
     else:
         flat = FlatParams(model.named_parameters(), dev, pad_multiple=world if a.zero_stage else 1)
@@ -106,7 +107,7 @@ def main(argv=None):
                      eval_interval=a.eval_interval, eval_batches=a.eval_batches, eval_batch_size=a.eval_batch_size,
                      eval_out=a.eval_out, save_every=a.save_every, ema_beta=a.ema_beta,
                      use_graph=not a.no_graph, state_dir=a.state_dir, metrics_out=a.metrics_out,
-                     offload_optimizer=offload,
+                     offload_optimizer=offload, offload_bf16=bool(a.shard_fp16_disk),
                      **common.runtime_train_kwargs(a))
 
     trainer = None

@@ -324,11 +324,16 @@ void nonfinite_check(Tensor x, Tensor flag) {
 void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor step, c10::optional<Tensor> sumsq_t,
                 double beta1, double beta2, double eps, double wd, double max_norm, bool l2_coupled,
                 c10::optional<Tensor> shadow, c10::optional<Tensor> nonfinite) {
-  CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v);
+  CHECK_F32(p); CHECK_F32(g);
   CHECK_CONTIG(p); CHECK_CONTIG(g); CHECK_CONTIG(m); CHECK_CONTIG(v);
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adamw: size mismatch");
+  const bool mb = m.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(m.scalar_type() == v.scalar_type() && (mb || m.scalar_type() == torch::kFloat32),
+              "adamw: moments must both be fp32 or both bf16");
   mft::AdamWArgs a{};
-  a.p = fp(p); a.g = fp(g); a.m = fp(m); a.v = fp(v); a.n = p.numel();
+  a.p = fp(p); a.g = fp(g); a.n = p.numel();
+  a.m = reinterpret_cast<float*>(m.data_ptr()); a.v = reinterpret_cast<float*>(v.data_ptr());
+  a.moments_bf16 = mb;
   a.lr_ptr = fp(lr); a.step_ptr = fp(step); a.sumsq = optp<float>(sumsq_t);
   a.beta1 = beta1; a.beta2 = beta2; a.eps = eps; a.weight_decay = wd; a.max_norm = max_norm; a.l2_coupled = l2_coupled;
   a.shadow = optp<bf16_t>(shadow);

@@ -182,6 +182,7 @@ struct AdamWArgs {
   int l2_coupled;         // reference-compat: g += wd*p instead of decoupled decay
   bf16_t* shadow;         // optional bf16 copy
   const int* nonfinite;   // optional device flag: skip the step when set
+  int moments_bf16;       // m / v are bf16 (stochastically rounded; host-offloaded optimizer state)
 };
 void adamw_step(const AdamWArgs& a, hipStream_t st);
 // after every adamw_step launch of one update: *step += 1 unless the update was skipped

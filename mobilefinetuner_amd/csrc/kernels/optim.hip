@@ -63,6 +63,35 @@ __device__ __forceinline__ bool adamw_skip(const int* nonfinite, const float* su
   return (nonfinite && *nonfinite) || (sumsq && !isfinite(*sumsq));
 }
 
+// bf16 moments (MB): stochastic rounding with a counter hash of (step, element) -- round-to-nearest
+// would freeze v under beta2 = 0.999 (a 0.1% change is below half a bf16 ulp) and bias m; SR keeps
+// both unbiased.  The fp32 master weights and the update itself stay fp32.
+__device__ __forceinline__ uint32_t sr_hash(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352DU;
+  x ^= x >> 15;
+  x *= 0x846CA68BU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint16_t f2bf_sr(float f, uint32_t r) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7F800000U) == 0x7F800000U) return (uint16_t)(u >> 16);  // inf / nan
+  return (uint16_t)((u + (r & 0xFFFFU)) >> 16);
+}
+
+template <bool MB>
+__device__ __forceinline__ float ld_mom(const void* p, long i) {
+  if constexpr (MB) return bf2f(reinterpret_cast<const uint16_t*>(p)[i]);
+  else return reinterpret_cast<const float*>(p)[i];
+}
+template <bool MB>
+__device__ __forceinline__ void st_mom(void* p, long i, float x, uint32_t r) {
+  if constexpr (MB) reinterpret_cast<uint16_t*>(p)[i] = f2bf_sr(x, r);
+  else reinterpret_cast<float*>(p)[i] = x;
+}
+
+template <bool MB>
 __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
   if (adamw_skip(a.nonfinite, a.sumsq)) return;  // skip-step on NaN/Inf grads (fault tolerance)
   const float lr = *a.lr_ptr;
@@ -78,13 +107,22 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
   const float rbc2 = 1.f / sqrtf(bc2);
   const float decay = a.l2_coupled ? 1.f : 1.f - lr * a.weight_decay;
   const long n4 = a.n / 4;
+  const uint32_t seed = sr_hash((uint32_t)t * 0x9E3779B9U);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 p = reinterpret_cast<float4*>(a.p)[i];
     float4 g = reinterpret_cast<const float4*>(a.g)[i];
-    float4 m = reinterpret_cast<float4*>(a.m)[i];
-    float4 v = reinterpret_cast<float4*>(a.v)[i];
-    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w}, mm[4] = {m.x, m.y, m.z, m.w},
-          vv[4] = {v.x, v.y, v.z, v.w};
+    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w}, mm[4], vv[4];
+    if constexpr (MB) {
+      const uint2 mb = reinterpret_cast<const uint2*>(a.m)[i], vb = reinterpret_cast<const uint2*>(a.v)[i];
+      mm[0] = __uint_as_float(mb.x << 16); mm[1] = __uint_as_float(mb.x & 0xFFFF0000U);
+      mm[2] = __uint_as_float(mb.y << 16); mm[3] = __uint_as_float(mb.y & 0xFFFF0000U);
+      vv[0] = __uint_as_float(vb.x << 16); vv[1] = __uint_as_float(vb.x & 0xFFFF0000U);
+      vv[2] = __uint_as_float(vb.y << 16); vv[3] = __uint_as_float(vb.y & 0xFFFF0000U);
+    } else {
+      const float4 m = reinterpret_cast<const float4*>(a.m)[i], v = reinterpret_cast<const float4*>(a.v)[i];
+      mm[0] = m.x; mm[1] = m.y; mm[2] = m.z; mm[3] = m.w;
+      vv[0] = v.x; vv[1] = v.y; vv[2] = v.z; vv[3] = v.w;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float gj = gg[j] * clip;
@@ -95,8 +133,20 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
       pp[j] = pp[j] * decay - step_size * mm[j] / denom;
     }
     reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-    reinterpret_cast<float4*>(a.m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
-    reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    if constexpr (MB) {
+      const uint32_t r = sr_hash(seed ^ (uint32_t)i), r2 = sr_hash(r);
+      uint2 mb, vb;
+      mb.x = (uint32_t)f2bf_sr(mm[0], r) | ((uint32_t)f2bf_sr(mm[1], r >> 16) << 16);
+      mb.y = (uint32_t)f2bf_sr(mm[2], r2) | ((uint32_t)f2bf_sr(mm[3], r2 >> 16) << 16);
+      const uint32_t r3 = sr_hash(r2), r4 = sr_hash(r3);
+      vb.x = (uint32_t)f2bf_sr(vv[0], r3) | ((uint32_t)f2bf_sr(vv[1], r3 >> 16) << 16);
+      vb.y = (uint32_t)f2bf_sr(vv[2], r4) | ((uint32_t)f2bf_sr(vv[3], r4 >> 16) << 16);
+      reinterpret_cast<uint2*>(a.m)[i] = mb;
+      reinterpret_cast<uint2*>(a.v)[i] = vb;
+    } else {
+      reinterpret_cast<float4*>(a.m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+      reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    }
     if (a.shadow) {
       uint2 sh;
       sh.x = pack_bf2(pp[0], pp[1]);
@@ -109,12 +159,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
       float gj = a.g[i] * clip;
       float pj = a.p[i];
       if (a.l2_coupled) gj += a.weight_decay * pj;
-      const float mj = a.beta1 * a.m[i] + (1.f - a.beta1) * gj;
-      const float vj = a.beta2 * a.v[i] + (1.f - a.beta2) * gj * gj;
+      const float mj = a.beta1 * ld_mom<MB>(a.m, i) + (1.f - a.beta1) * gj;
+      const float vj = a.beta2 * ld_mom<MB>(a.v, i) + (1.f - a.beta2) * gj * gj;
       pj = pj * decay - step_size * mj / (sqrtf(vj) * rbc2 + a.eps);
       a.p[i] = pj;
-      a.m[i] = mj;
-      a.v[i] = vj;
+      const uint32_t r = sr_hash(seed ^ 0x5bd1e995U ^ (uint32_t)i);
+      st_mom<MB>(a.m, i, mj, r);
+      st_mom<MB>(a.v, i, vj, r >> 16);
       if (a.shadow) a.shadow[i] = f2bf(pj);
     }
   }
@@ -132,7 +183,9 @@ void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStre
 void adamw_step(const AdamWArgs& a, hipStream_t st) {
   long g = (a.n / 4 + 255) / 256;
   if (g < 1) g = 1;
-  adamw_kernel<<<(int)(g < 2048 ? g : 2048), 256, 0, st>>>(a);
+  const int grid = (int)(g < 2048 ? g : 2048);
+  if (a.moments_bf16) adamw_kernel<true><<<grid, 256, 0, st>>>(a);
+  else adamw_kernel<false><<<grid, 256, 0, st>>>(a);
 }
 
 }  // namespace mft

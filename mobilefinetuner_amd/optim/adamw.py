@@ -25,7 +25,7 @@ class FusedAdamW:
     def __init__(self, flat: FlatParams, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  max_grad_norm: float | None = 1.0, l2_coupled: bool = False, skip_nonfinite: bool = True,
                  param_range: tuple[int, int] | None = None, offload: bool = False,
-                 offload_chunk: int = 1 << 25):
+                 offload_chunk: int = 1 << 26, offload_dtype=torch.float32, offload_slots: int = 3):
         self.flat = flat
         self.beta1, self.beta2 = betas
         self.eps, self.weight_decay = eps, weight_decay
@@ -40,19 +40,30 @@ class FusedAdamW:
         # offload.cpp) and stream through two device slots per chunk -- H2D of chunk c+1 and D2H
         # of chunk c-1 on the tier's copy stream overlap the update of chunk c (SURVEY §2.13 "host-
         # DRAM offload tier for optimizer state"; the reference's analogue is the disk sharder)
+        # offload_dtype=bf16 (the reference's --shard_fp16_disk default): the host copies of the
+        # moments are 16-bit -- half the PCIe bytes each way -- and the kernel updates them in
+        # place with stochastic rounding (optim.hip), the fp32 master weights stay fp32
         self.offload = bool(offload) and dev.type == "cuda"
+        import os
+        offload_chunk = int(os.environ.get("MFT_OFFLOAD_CHUNK", offload_chunk))
+        offload_slots = int(os.environ.get("MFT_OFFLOAD_SLOTS", offload_slots))
+        self.mdt = torch.bfloat16 if offload_dtype in (torch.bfloat16, torch.float16, "bf16", "fp16") else torch.float32
         if self.offload:
             self._tier = native().runtime.HostTier(0, "", 0)
             self._chunks = []
+            esz = torch.tensor([], dtype=self.mdt).element_size()
             for c0 in range(0, n, offload_chunk):
                 c1 = min(n, c0 + offload_chunk)
                 for k in ("m", "v"):
-                    self._tier.add(f"{k}#{c0}", (c1 - c0) * 4)
-                    self._tier.host_tensor(f"{k}#{c0}", torch.float32, [c1 - c0]).zero_()
+                    self._tier.add(f"{k}#{c0}", (c1 - c0) * esz)
+                    self._tier.host_tensor(f"{k}#{c0}", self.mdt, [c1 - c0]).zero_()
                 self._chunks.append((c0, c1))
             cmax = min(n, offload_chunk)
-            self._slots = [(torch.empty(cmax, dtype=torch.float32, device=dev),
-                            torch.empty(cmax, dtype=torch.float32, device=dev)) for _ in range(2)]
+            # K device slots: the fetch of chunk c+K-1 only waits for the write-back of chunk c-1,
+            # so H2D and D2H (PCIe is full duplex) stay busy together
+            self._ns = max(2, int(offload_slots))
+            self._slots = [(torch.empty(cmax, dtype=self.mdt, device=dev),
+                            torch.empty(cmax, dtype=self.mdt, device=dev)) for _ in range(self._ns)]
             self.m = self.v = None
         else:
             self.m = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -136,28 +147,35 @@ class FusedAdamW:
         if not hasattr(self, "_h2d"):
             self._h2d = torch.cuda.Stream(device=p.device)
             self._d2h = torch.cuda.Stream(device=p.device)
-            self._free = [torch.cuda.Event(), torch.cuda.Event()]
-            for e in self._free:
-                e.record(cur)
-            self._host = [(self._tier.host_tensor(f"m#{c0}", torch.float32, [c1 - c0]),
-                           self._tier.host_tensor(f"v#{c0}", torch.float32, [c1 - c0])) for c0, c1 in self._chunks]
-        fetched = [torch.cuda.Event(), torch.cuda.Event()]
+            self._free = [torch.cuda.Event() for _ in range(self._ns)]
+            self._host = [(self._tier.host_tensor(f"m#{c0}", self.mdt, [c1 - c0]),
+                           self._tier.host_tensor(f"v#{c0}", self.mdt, [c1 - c0])) for c0, c1 in self._chunks]
+        # every cross-stream dependency of the step is created inside it (hipGraph-capturable):
+        # the previous step's write-backs precede this step's refills, both copy streams fork
+        # from the compute stream, and a captured step joins its write-back stream at the end
+        cur.wait_stream(self._d2h)
+        for e in self._free:
+            e.record(cur)
+        self._h2d.wait_stream(cur)
+        ns = self._ns
+        fetched = [torch.cuda.Event() for _ in range(ns)]
 
         def fetch(i):
             c0, c1 = self._chunks[i]
-            mb, vb = self._slots[i % 2]
-            self._h2d.wait_event(self._free[i % 2])
+            mb, vb = self._slots[i % ns]
+            self._h2d.wait_event(self._free[i % ns])
             with torch.cuda.stream(self._h2d):
                 mb[:c1 - c0].copy_(self._host[i][0], non_blocking=True)
                 vb[:c1 - c0].copy_(self._host[i][1], non_blocking=True)
-            fetched[i % 2].record(self._h2d)
+            fetched[i % ns].record(self._h2d)
 
-        fetch(0)
+        for i in range(min(ns - 1, len(self._chunks))):
+            fetch(i)
         for i, (c0, c1) in enumerate(self._chunks):
-            mb, vb = self._slots[i % 2]
-            if i + 1 < len(self._chunks):
-                fetch(i + 1)
-            cur.wait_event(fetched[i % 2])
+            mb, vb = self._slots[i % ns]
+            if i + ns - 1 < len(self._chunks):
+                fetch(i + ns - 1)
+            cur.wait_event(fetched[i % ns])
             C.adamw_step(p[c0:c1], g[c0:c1], mb[:c1 - c0], vb[:c1 - c0], self.lr_dev, self.step_dev,
                          self.sumsq_dev if self.max_grad_norm is not None else None,
                          self.beta1, self.beta2, self.eps, self.weight_decay,
@@ -168,13 +186,15 @@ class FusedAdamW:
             with torch.cuda.stream(self._d2h):
                 self._host[i][0].copy_(mb[:c1 - c0], non_blocking=True)
                 self._host[i][1].copy_(vb[:c1 - c0], non_blocking=True)
-            self._free[i % 2].record(self._d2h)
+            self._free[i % ns].record(self._d2h)
+        if torch.cuda.is_current_stream_capturing():
+            cur.wait_stream(self._d2h)
 
     def _moments_host(self):
         if hasattr(self, "_d2h"):
             self._d2h.synchronize()
-        m = torch.cat([self._tier.host_tensor(f"m#{c0}", torch.float32, [c1 - c0]) for c0, c1 in self._chunks])
-        v = torch.cat([self._tier.host_tensor(f"v#{c0}", torch.float32, [c1 - c0]) for c0, c1 in self._chunks])
+        m = torch.cat([self._tier.host_tensor(f"m#{c0}", self.mdt, [c1 - c0]) for c0, c1 in self._chunks]).float()
+        v = torch.cat([self._tier.host_tensor(f"v#{c0}", self.mdt, [c1 - c0]) for c0, c1 in self._chunks]).float()
         return m, v
 
     @torch.no_grad()
@@ -218,8 +238,8 @@ class FusedAdamW:
             if hasattr(self, "_d2h"):
                 self._d2h.synchronize()
             for c0, c1 in self._chunks:
-                self._tier.host_tensor(f"m#{c0}", torch.float32, [c1 - c0]).copy_(sd["m"][c0:c1])
-                self._tier.host_tensor(f"v#{c0}", torch.float32, [c1 - c0]).copy_(sd["v"][c0:c1])
+                self._tier.host_tensor(f"m#{c0}", self.mdt, [c1 - c0]).copy_(sd["m"][c0:c1])
+                self._tier.host_tensor(f"v#{c0}", self.mdt, [c1 - c0]).copy_(sd["v"][c0:c1])
         else:
             self.m.copy_(sd["m"].to(self.m.device))
             self.v.copy_(sd["v"].to(self.v.device))

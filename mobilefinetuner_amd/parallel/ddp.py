@@ -1,4 +1,4 @@
-"""Data parallelism over RCCL (xGMI) / gloo: bucketed gradient all-reduce on the flat grad buffer.
+"""Data parallelism over RCCL (xGMI) / gloo: bucketed gradient reduction on the flat grad buffer.
 
 The reference has no parallelism at all.  Design for MI355X:
 
@@ -6,13 +6,26 @@ The reference has no parallelism at all.  Design for MI355X:
 * gradients live in ONE flat fp32 buffer (utils/params.py), so a bucket is just a contiguous
   slice — no packing/unpacking copies;
 * buckets are laid out in reverse-forward order and launched asynchronously from the
-  ``grad_ready`` hook that the fused backward kernels call, so the all-reduce of late layers
-  overlaps the backward of early layers;
+  ``grad_ready`` hook that the fused backward kernels call, so the reduction of late layers
+  overlaps the backward of early layers (eager steps); with ``MFT_GRAPH_COMM=1`` also inside the
+  step's hipGraph: the hooks enqueue their RCCL collectives while the step is being captured, so
+  the replay runs each bucket's collective on RCCL's stream as soon as the kernels producing it are
+  done (``capturable``; opt-in, see __init__);
+* two reductions: ``all_reduce`` (DDP, ZeRO-1) or, with ``shard`` (ZeRO-2), ``reduce`` of every
+  bucket segment to the rank whose optimizer shard owns it -- the reduce-scatter traffic, bucketed
+  and overlapped, while the owned shard stays one contiguous range for the fused AdamW;
+* optional bf16 reduction (``reduce_dtype=torch.bfloat16``): the bucket is cast into a bf16 comm
+  buffer, reduced at half the xGMI bytes and cast back (full fine-tuning: 498 MB -> 249 MB per
+  GPT-2 step);
 * bucket size defaults to 64 MiB: xGMI is point-to-point (7 links x ~153 GB/s per MI355X), ring
   collectives are per-link bound and latency-dominated below a few MB, so fewer, larger buckets
   win; LoRA grads (1.8-7.6 MB) always fit one bucket and are reduced once after backward.
+``MFT_DP_FORCE_COMM=1`` keeps the collectives on a 1-rank RCCL group (profiling the overlap on
+one GPU).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.distributed as dist
@@ -57,13 +70,23 @@ def allreduce_sum_(t: torch.Tensor, group=None):
 
 
 class DataParallel:
-    """Bucketed, overlapped gradient averaging for a FlatParams grad buffer."""
+    """Bucketed, overlapped gradient averaging for a FlatParams grad buffer (all-reduce, or reduce
+    to the owning rank of a ZeRO-2 shard of ``shard`` elements per rank)."""
 
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 64.0, overlap: bool = True,
-                 broadcast_from: int | None = 0):
+                 broadcast_from: int | None = 0, reduce_dtype=None, shard: int | None = None):
         self.flat, self.group = flat, group
         self.world = dist.get_world_size(group) if is_dist() else 1
-        self.overlap = overlap and self.world > 1
+        self.rank = dist.get_rank(group) if is_dist() else 0
+        self.force = is_dist() and os.environ.get("MFT_DP_FORCE_COMM", "0") == "1"
+        self.active = self.world > 1 or self.force
+        self.nccl = _supports_avg(group)
+        self.overlap = overlap and self.active
+        # collectives recorded into the step's hipGraph: opt-in (MFT_GRAPH_COMM=1).  On ROCm 7 /
+        # RCCL 2.26 capturing them aborted intermittently at capture end on a 1-rank group, so the
+        # default replays the captured fwd/bwd and reduces the buckets right after the replay
+        self.capturable = self.nccl and os.environ.get("MFT_GRAPH_COMM", "0") == "1"
+        self.shard = shard
         cap = int(bucket_mb * (1 << 20) / 4)
         # buckets over slots in REVERSE order (last layer's grads are ready first)
         self.buckets = []
@@ -78,10 +101,20 @@ class DataParallel:
                 cur, lo = [], None
         if cur:
             self.buckets.append(self._mk(cur))
+        if self.buckets:
+            # the buckets tile the whole buffer (alignment gaps and the padding tail included), so
+            # every element -- in particular every element of a ZeRO-2 shard -- is reduced once
+            self.buckets[0]["hi"] = flat.numel
+            self.buckets[-1]["lo"] = 0
+            for k in range(len(self.buckets) - 1):
+                self.buckets[k]["lo"] = self.buckets[k + 1]["hi"]
         self.param_bucket = {}
         for bi, b in enumerate(self.buckets):
             for s in b["slots"]:
                 self.param_bucket[id(s.param)] = bi
+        self.comm_buf = None
+        if reduce_dtype is not None and reduce_dtype != flat.grad.dtype and self.active:
+            self.comm_buf = torch.empty(flat.numel, dtype=reduce_dtype, device=flat.grad.device)
         self._works = []
         self._pending = [0] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
@@ -90,7 +123,7 @@ class DataParallel:
         # LAST micro-batch's contribution: TrainStep clears this flag for earlier micro-batches
         self.last_micro = True
         self._hook = None
-        if self.overlap and len(self.buckets) > 1:
+        if self.overlap and (len(self.buckets) > 1 or shard is not None):
             self._hook = Fx.register_grad_ready_hook(self._on_ready)
         if broadcast_from is not None and self.world > 1:
             dist.broadcast(flat.master, src=broadcast_from, group=group)
@@ -101,6 +134,19 @@ class DataParallel:
         lo = min(s.offset for s in slots)
         hi = max(s.offset + s.numel for s in slots)
         return {"slots": slots, "lo": lo, "hi": hi, "n": len(slots)}
+
+    def _owner_segments(self, lo, hi):
+        """[(owner rank, a, b)] cover [lo, hi) by the ranks' contiguous ZeRO-2 shards."""
+        out, a = [], lo
+        while a < hi:
+            r = min(a // self.shard, self.world - 1)
+            b = min(hi, (r + 1) * self.shard) if r < self.world - 1 else hi
+            out.append((r, a, b))
+            a = b
+        return out
+
+    def _dst(self, r):
+        return dist.get_global_rank(self.group, r) if self.group is not None else r
 
     def begin_step(self):
         self._pending = [b["n"] for b in self.buckets]
@@ -113,14 +159,26 @@ class DataParallel:
             return
         b = self.buckets[bi]
         self._launched[bi] = True
-        w = allreduce_mean_(self.flat.grad[b["lo"]:b["hi"]], self.group, async_op=True)
-        if w is not None:
-            self._works.append(w)
+        if not self.active:
+            return
+        lo, hi = b["lo"], b["hi"]
+        t = self.flat.grad[lo:hi]
+        if self.comm_buf is not None:
+            c = self.comm_buf[lo:hi]
+            c.copy_(t)
+            t = c
+        op = dist.ReduceOp.AVG if self.nccl else dist.ReduceOp.SUM
+        if self.shard is None:
+            self._works.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
+        else:
+            for r, a, z in self._owner_segments(lo, hi):
+                self._works.append(dist.reduce(t[a - lo:z - lo], dst=self._dst(r), op=op, group=self.group,
+                                               async_op=True))
 
     def _on_ready(self, p):
-        # inside a hipGraph capture (TrainStep use_graph) no collective may be enqueued: the bucket
-        # stays pending and finish() reduces every bucket after the replay
-        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        # while a hipGraph is captured the collective is recorded into it only if the backend can
+        # (RCCL); otherwise the bucket stays pending and finish() reduces it after the replay
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing() and not self.capturable:
             return
         if not self.last_micro:
             return
@@ -132,18 +190,35 @@ class DataParallel:
         if self._pending[bi] == 0:
             self._launch(bi)
 
+    def wants_graph_comm(self):
+        """Record the reduction (and the optimizer step) into the step's hipGraph: only when the
+        backward hooks overlap several buckets on RCCL; a single bucket (LoRA) is reduced by one
+        eager collective after the replay."""
+        return self.capturable and self._hook is not None
+
+    def owned(self):
+        """(lo, hi) of the reduced gradient this rank's optimizer reads."""
+        if self.shard is None:
+            return 0, self.flat.numel
+        lo = self.rank * self.shard
+        return lo, (self.flat.numel if self.rank == self.world - 1 else lo + self.shard)
+
     def finish(self):
-        """Make sure every bucket is reduced (launch the ones no hook completed) and wait."""
-        if self.world == 1:
-            return
-        if not self.overlap or len(self.buckets) == 1:
-            allreduce_mean_(self.flat.grad, self.group)
+        """Launch every bucket no hook completed, wait, and finish the average (gloo: /world;
+        bf16: cast back)."""
+        if not self.active:
             return
         for bi in range(len(self.buckets)):
             self._launch(bi)
         for w in self._works:
-            w.wait()
+            if w is not None:
+                w.wait()
         self._works = []
+        lo, hi = self.owned()
+        if self.comm_buf is not None:
+            self.flat.grad[lo:hi].copy_(self.comm_buf[lo:hi])
+        if not self.nccl:
+            self.flat.grad[lo:hi].div_(self.world)
 
     def close(self):
         if self._hook is not None:

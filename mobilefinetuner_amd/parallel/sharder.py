@@ -14,7 +14,9 @@ stream ordered with hipEvents; eviction frees the DEVICE STORAGE in place (``sto
 so tensors captured by autograd are released too and are re-filled in place before the backward of
 their block (a gate autograd node at each block boundary calls ``require`` on the way back).
 Frozen weights are bf16 already, so the host copy keeps the device dtype (the reference's
-fp16-on-disk quantisation of fp32 weights has nothing to halve here).
+fp16-on-disk quantisation of fp32 weights has nothing to halve here; ``--shard_fp16_disk`` instead
+halves the host-offloaded optimizer state, optim/adamw.py).  Eviction never synchronises the device
+(stream-ordered release, see _evict), and the backward prefetches the preceding block.
 """
 from __future__ import annotations
 
@@ -65,9 +67,11 @@ class ParameterSharder:
                 continue
             if self.tier.dirty(key):
                 self.tier.offload(key, t)
-                self.tier.synchronize(key)
-            # the storage may still be read by already-queued kernels: order the free after them
-            torch.cuda.current_stream().synchronize()
+                self.tier.synchronize(key)  # the write-back reads the storage on the copy stream
+            # No device sync: the storage returns to the caching allocator on the compute stream,
+            # which hands it out again only to later work of that stream (ordered after the
+            # already-queued kernels still reading it), and every refill's H2D copy is ordered
+            # after the compute stream by the tier (order event, csrc/runtime/offload.cpp).
             t.untyped_storage().resize_(0)
             self.tier.mark_resident(key, False)
         self.stats["evictions"] += 1
@@ -84,7 +88,9 @@ class ParameterSharder:
             self.tier.mark_resident(key, True)
         self.stats["fetches"] += 1
 
-    def require(self, name: str):
+    def require(self, name: str, backward: bool = False):
+        """Make ``name`` resident; prefetch the group used next -- the following block in the
+        forward, the preceding one in the backward."""
         g = self.groups.get(name)
         if g is None:
             return
@@ -99,8 +105,8 @@ class ParameterSharder:
                 self._evict(v)
         self._fetch(name)
         if self.prefetch:
-            idx = self.order.index(name)
-            nxt = self.order[idx + 1] if idx + 1 < len(self.order) else None
+            idx = self.order.index(name) + (-1 if backward else 1)
+            nxt = self.order[idx] if 0 <= idx < len(self.order) else None
             if nxt is not None and self._fits(nxt, exclude=name):
                 self._fetch(nxt)
 
@@ -127,7 +133,7 @@ class _Gate(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        ctx.sharder.require(ctx.name)
+        ctx.sharder.require(ctx.name, backward=True)
         return g, None, None
 
 

@@ -6,13 +6,15 @@ the real cross-GPU version for full fine-tuning (gpt2_full_finetune, GPT-2 XL on
 * the flat fp32 grad / master buffers are split into ``world`` equal contiguous shards (padded);
 * ZeRO-1: grads are all-reduced (averaged), each rank updates only its shard of the AdamW moments
   (optimizer memory / world);
-* ZeRO-2: grads are ``reduce_scatter``-ed — each rank receives only its averaged shard (half the
-  traffic of an all-reduce on the per-link-bound xGMI ring);
+* ZeRO-2: every gradient bucket is ``reduce``-d to the rank(s) owning its elements — the traffic of
+  a reduce-scatter (half an all-reduce on the per-link-bound xGMI ring), but bucketed and launched
+  from the backward's grad-ready hooks, so it overlaps the backward (and is recorded into the
+  step's hipGraph with RCCL; parallel/ddp.py);
 * the updated bf16 compute weights (the ``shadow``) are ``all_gather``-ed into every rank, so the
   next forward sees the full model;
 * the global grad norm for clipping is the all-reduced sum of per-shard squares.
 
-Collectives run on the flat buffers directly (no packing), one call each per step.
+Collectives run on the flat buffers directly (no packing).
 """
 from __future__ import annotations
 
@@ -21,11 +23,12 @@ import torch.distributed as dist
 
 from ..optim.adamw import FusedAdamW
 from ..utils.params import FlatParams
-from .ddp import is_dist
+from .ddp import DataParallel, is_dist
 
 
 class ZeroOptimizer:
-    def __init__(self, flat: FlatParams, stage: int, group=None, **adamw_kwargs):
+    def __init__(self, flat: FlatParams, stage: int, group=None, bucket_mb: float = 64.0, overlap: bool = True,
+                 reduce_dtype=None, **adamw_kwargs):
         assert stage in (1, 2)
         self.flat, self.stage, self.group = flat, stage, group
         self.world = dist.get_world_size(group) if is_dist() else 1
@@ -51,30 +54,20 @@ class ZeroOptimizer:
         if self.world > 1:  # identical starting weights everywhere
             dist.broadcast(flat.master, src=0, group=group)
             flat.refresh_shadow()
+        # bucketed, backward-overlapped gradient reduction (all-reduce for stage 1, reduce to the
+        # owning rank for stage 2)
+        self.reducer = DataParallel(flat, group=group, bucket_mb=bucket_mb, overlap=overlap, broadcast_from=None,
+                                    reduce_dtype=reduce_dtype, shard=self.shard if stage == 2 else None)
 
     # expose the FusedAdamW control surface used by Trainer/TrainStep
     def __getattr__(self, k):
         return getattr(self.inner, k)
 
-    def _avg(self, t):
-        if dist.get_backend(self.group) == "nccl":
-            return dist.ReduceOp.AVG
-        return dist.ReduceOp.SUM
-
     def reduce_gradients(self):
-        if self.world == 1:
-            return
-        g = self.flat.grad
-        op = self._avg(g)
-        if self.stage == 1:
-            dist.all_reduce(g, op=op, group=self.group)
-        else:
-            out = g[self.lo:self.hi]
-            tmp = torch.empty(self.shard, dtype=g.dtype, device=g.device)
-            dist.reduce_scatter_tensor(tmp, g, op=op, group=self.group)
-            out.copy_(tmp)
-        if op == dist.ReduceOp.SUM:
-            g[self.lo:self.hi].div_(self.world) if self.stage == 2 else g.div_(self.world)
+        """Finish this step's reduction (buckets the backward hooks did not launch are launched
+        now) and re-arm the reducer for the next step."""
+        self.reducer.finish()
+        self.reducer.begin_step()
 
     def step(self, sumsq_ready: bool = False):
         if self.inner.max_grad_norm is not None:
@@ -114,11 +107,26 @@ class ZeroReducer:
         self.world = zero.world
         self.group = zero.group
 
+    @property
+    def capturable(self):
+        return self.zero.reducer.capturable
+
+    def wants_graph_comm(self):
+        return self.zero.reducer.wants_graph_comm()
+
+    @property
+    def last_micro(self):
+        return self.zero.reducer.last_micro
+
+    @last_micro.setter
+    def last_micro(self, v):
+        self.zero.reducer.last_micro = v
+
     def begin_step(self):
-        pass
+        self.zero.reducer.begin_step()
 
     def finish(self):
-        self.zero.reduce_gradients()
+        self.zero.reducer.finish()
 
     def close(self):
-        pass
+        self.zero.reducer.close()

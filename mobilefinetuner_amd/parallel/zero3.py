@@ -17,9 +17,13 @@ next step's all-gathers read.  Norm weights/biases (which compute in fp32 straig
 
 Per step (GPU, bf16 compute):
   forward  block i : all_gather(shadow shards of unit i) -> unit's full bf16 buffer, prefetching
-                     unit i+1 on the communication stream; after the block the buffer's storage is
-                     released (``storage.resize_(0)``: views captured by autograd stay valid and
-                     are refilled in place later);
+                     unit i+1 on the communication stream; the gathered buffers are two fixed
+                     slots shared by the even / odd blocks (+ one for the outer unit): a block's
+                     slot is overwritten by the block two ahead, and views captured by autograd
+                     are refilled in place before the block's backward.  No allocation or
+                     storage resize ever happens inside a step, so the whole ZeRO-3 step --
+                     gathers, prefetches on the side stream, reduce-scatters, sharded AdamW --
+                     is recorded into ONE hipGraph like the other configurations;
   backward block i : an autograd gate at the block OUTPUT re-gathers unit i (prefetching i-1) and
                      materialises a zeroed fp32 gradient buffer that the kernels accumulate into;
                      a gate at the block INPUT fires once the whole block's backward is done:
@@ -28,8 +32,8 @@ Per step (GPU, bf16 compute):
                      all-reduced, then the sharded AdamW (grad norm = all-reduced sum of the
                      shard squares + the replicated part counted once).
 
-Peak parameter memory per rank = shards (1/world of everything) + at most three gathered blocks
-(current, prefetched, and the outer unit).  On the CPU (gloo, tests) the gathered copy is the fp32
+Peak parameter memory per rank = shards (1/world of everything) + three gathered units (two block
+slots and the outer unit) + their three fp32 gradient slots.  On the CPU (gloo, tests) the gathered copy is the fp32
 master itself and autograd accumulates straight into the gradient buffer views.
 """
 from __future__ import annotations
@@ -46,10 +50,6 @@ ALIGN = 64
 
 def _round(n, a):
     return (n + a - 1) // a * a
-
-
-def _resize(t: torch.Tensor, numel: int):
-    t.untyped_storage().resize_(numel * t.element_size())
 
 
 class _ShardFlat:
@@ -85,8 +85,9 @@ class _Unit:
             off += _round(p.numel(), ALIGN)
         self.used = off
         self.n = self.s = self.off = 0
-        self.full = None              # gathered compute copy (storage released between uses)
-        self.gwork = None             # full-size fp32 gradient buffer (backward only)
+        self.full = None              # gathered compute copy (a view of the unit's slot)
+        self.gwork = None             # full-size fp32 gradient buffer (backward only; slot view)
+        self.slot = None              # [owner] cell shared by the units of one slot
         self.gathered = False
         self.g_live = False
         self.event = None             # comm-stream event of an in-flight prefetch
@@ -115,13 +116,24 @@ class Zero3:
     always_finish = True  # TrainStep: run finish() even on a single rank
     sharded = True        # Trainer.save_state: optimizer + master are per-rank partitions
 
+    def wants_graph_comm(self):
+        # the step's Python bookkeeping (gathered / live flags) runs once, at capture: the
+        # reduction and the sharded optimizer step must be recorded into the same graph
+        return True
+
     def __init__(self, units, device, group=None, prefetch: bool = True, **adamw_kwargs):
         self.group = group
         self.world = dist.get_world_size(group) if is_dist() else 1
         self.rank = dist.get_rank(group) if is_dist() else 0
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
-        self.prefetch = prefetch and self.cuda
+        # one rank: the "shard" of every unit is the whole unit, so the compute copies alias the
+        # shard (shadow / master) and the kernels accumulate straight into the shard's gradient --
+        # no gather copies, no gradient buffers to zero and fold in (MFT_Z3_FORCE_COPY=1 keeps the
+        # multi-rank gather / slot / reduce path, for testing it on one GPU)
+        import os
+        self.direct = self.world == 1 and os.environ.get("MFT_Z3_FORCE_COPY", "0") != "1"
+        self.prefetch = prefetch and self.cuda and not self.direct
         self.comm = torch.cuda.Stream(device=self.device) if self.prefetch else None
         self.rep: list = []
         self.units: list[_Unit] = []
@@ -148,8 +160,16 @@ class Zero3:
             off += _round(p.numel(), ALIGN)
         self.flat = _ShardFlat(max(off, ALIGN), self.device, shadow=self.cuda)
         gdt = torch.bfloat16 if self.cuda else torch.float32
+        # slots: the outer unit's own, and two shared by the even / odd block units
+        slots = []
+        if not self.direct:
+            nb = max([u.n for u in self.units[1:]] + [ALIGN])
+            slots = [(torch.empty(self.units[0].n, dtype=gdt, device=self.device),
+                      torch.empty(self.units[0].n, dtype=torch.float32, device=self.device), [None])]
+            slots += [(torch.empty(nb, dtype=gdt, device=self.device),
+                       torch.empty(nb, dtype=torch.float32, device=self.device), [None]) for _ in range(2)]
         with torch.no_grad():
-            for u in self.units:
+            for ui, u in enumerate(self.units):
                 full32 = torch.zeros(u.n, dtype=torch.float32, device=self.device)
                 for (n, p), o in zip(u.params, u.offsets):
                     full32[o:o + p.numel()].copy_(p.data.reshape(-1).float())
@@ -157,8 +177,12 @@ class Zero3:
                     dist.broadcast(full32, src=0, group=group)
                 self.flat.master[u.off:u.off + u.s].copy_(full32[self.rank * u.s:(self.rank + 1) * u.s])
                 del full32
-                u.full = torch.empty(u.n, dtype=gdt, device=self.device)
-                u.gwork = torch.empty(u.n, dtype=torch.float32, device=self.device)
+                if self.direct:
+                    src = self.flat.shadow if self.cuda else self.flat.master
+                    u.full, u.gwork, u.slot = src[u.off:u.off + u.n], self.flat.grad[u.off:u.off + u.n], [None]
+                else:
+                    full, gwork, owner = slots[0] if ui == 0 else slots[1 + (ui & 1)]
+                    u.full, u.gwork, u.slot = full[:u.n], gwork[:u.n], owner
                 for (n, p), o in zip(u.params, u.offsets):
                     k = p.numel()
                     view = u.full[o:o + k].view(p.shape)
@@ -171,8 +195,6 @@ class Zero3:
                     else:
                         p.data = view
                     p.grad = u.gwork[o:o + k].view(p.shape)
-                _resize(u.full, 0)
-                _resize(u.gwork, 0)
             for (n, p), o in zip(self.rep, rep_offs):
                 mv = self.flat.master[o:o + p.numel()].view(p.shape)
                 mv.copy_(p.data.to(self.device, torch.float32))
@@ -189,17 +211,28 @@ class Zero3:
         src = self.flat.shadow if self.cuda else self.flat.master
         return src[u.off:u.off + u.s]
 
+    def _take_slot(self, u):
+        """u becomes the occupant of its slot; a previous occupant's gathered copy is gone."""
+        prev = u.slot[0]
+        if prev is not None and prev is not u:
+            self._release(prev)
+        u.slot[0] = u
+
     def _issue_gather(self, u, on_comm: bool):
         if u.gathered:
             return
+        self._take_slot(u)
         cur = torch.cuda.current_stream(self.device) if self.cuda else None
         if on_comm:
             self.comm.wait_stream(cur)  # the shard is current (optimizer step done)
             ctx = torch.cuda.stream(self.comm)
         else:
             ctx = torch.no_grad()
+        if self.direct:  # the compute copy IS the shard
+            self.stats["all_gather"] += 1
+            u.gathered = True
+            return
         with ctx, torch.no_grad():
-            _resize(u.full, u.n)
             if self.world > 1:
                 dist.all_gather_into_tensor(u.full, self._src(u), group=self.group)
             else:
@@ -215,9 +248,7 @@ class Zero3:
         if not u.gathered:
             self._issue_gather(u, False)
         if u.event is not None:
-            cur = torch.cuda.current_stream(self.device)
-            cur.wait_event(u.event)
-            u.full.record_stream(cur)  # storage allocated on the comm stream, read here
+            torch.cuda.current_stream(self.device).wait_event(u.event)
             u.event = None
 
     def _release(self, u):
@@ -225,7 +256,6 @@ class Zero3:
             if u.event is not None:  # prefetched but never consumed
                 torch.cuda.current_stream(self.device).wait_event(u.event)
                 u.event = None
-            _resize(u.full, 0)
             u.gathered = False
 
     def _prefetch(self, j):
@@ -255,8 +285,8 @@ class Zero3:
         self._ensure(u)
         self._prefetch(i)  # unit of block i-1 (index i in self.units)
         if not u.g_live:
-            _resize(u.gwork, u.n)
-            u.gwork.zero_()
+            if not self.direct:
+                u.gwork.zero_()
             u.g_live = True
 
     def _post_backward(self, i):
@@ -267,6 +297,10 @@ class Zero3:
     def _reduce_scatter(self, u):
         if not u.g_live:
             return
+        if self.direct:  # the kernels accumulated into the shard's gradient already
+            self.stats["reduce_scatter"] += 1
+            u.g_live = False
+            return
         with torch.no_grad():
             dst = self.flat.grad[u.off:u.off + u.s]
             if self.world > 1:
@@ -276,15 +310,14 @@ class Zero3:
             else:
                 dst.add_(u.gwork)
         self.stats["reduce_scatter"] += 1
-        _resize(u.gwork, 0)
         u.g_live = False
 
     # ------------------------------------------------------------------ DataParallel-style reducer
     def begin_step(self):
         u = self.units[0]
         if not u.g_live:
-            _resize(u.gwork, u.n)
-            u.gwork.zero_()
+            if not self.direct:
+                u.gwork.zero_()
             u.g_live = True
 
     def finish(self):

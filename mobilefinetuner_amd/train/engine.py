@@ -15,20 +15,25 @@ import torch
 
 from ..optim.adamw import FusedAdamW
 from ..utils.trace import trace_range
-from ..parallel.ddp import DataParallel, allreduce_mean_
+from ..parallel.ddp import DataParallel
 from ..utils.params import FlatParams
 
 
 
 class TrainStep:
     def __init__(self, model, flat: FlatParams, opt: FusedAdamW, grad_accum: int = 1,
-                 dp: DataParallel | None = None, use_graph: bool = False, graph_comm: bool = False,
+                 dp: DataParallel | None = None, use_graph: bool = False, graph_comm: bool | None = None,
                  loss_fn=None):
         self.model, self.flat, self.opt = model, flat, opt
         self.accum = max(1, int(grad_accum))
         self.dp = dp
         self.use_graph = use_graph
-        self.graph_comm = graph_comm
+        # graph_comm: the gradient reduction and the optimizer step are recorded into the hipGraph
+        # too (the reducer's collectives then overlap the captured backward); default: as the
+        # reducer asks (multi-bucket RCCL data parallelism, ZeRO-3)
+        if graph_comm is None:
+            graph_comm = dp is not None and hasattr(dp, "wants_graph_comm") and dp.wants_graph_comm()
+        self.graph_comm = bool(graph_comm)
         self.loss_fn = loss_fn or (lambda m, ids, lab, scale: m(ids, lab, loss_scale=scale))
         self.loss_dev = None
         self.graph = None
@@ -52,8 +57,9 @@ class TrainStep:
             self.loss_dev.add_(loss.detach().float().reshape(1), alpha=scale)
 
     def _reduce(self):
-        # ZeRO-3 must always finish (its outer-unit grads reach the shard there, even on 1 rank)
-        if self.dp is not None and (self.dp.world > 1 or getattr(self.dp, "always_finish", False)):
+        # ZeRO-3 must always finish (its outer-unit grads reach the shard there, even on 1 rank);
+        # a DataParallel reducer decides itself (1-rank profiling groups)
+        if self.dp is not None:
             self.dp.finish()
 
     def _opt(self):
@@ -79,16 +85,15 @@ class TrainStep:
         with torch.cuda.stream(side):
             if self.dp is not None:
                 self.dp.begin_step()
-            with torch.cuda.graph(self.graph, stream=side):
+            # thread_local: RCCL's watchdog thread keeps polling the events of earlier collectives
+            # while this thread captures; under the default "global" mode those hipEventQuery
+            # calls fail (hipErrorStreamCaptureUnsupported) and abort the process group
+            with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
                 self._fwd_bwd(self._static)
                 if self.graph_comm:
-                    self._reduce_flat()
+                    self._reduce()
                     self._opt()
         torch.cuda.current_stream(dev).wait_stream(side)
-
-    def _reduce_flat(self):
-        if self.dp is not None and self.dp.world > 1:
-            allreduce_mean_(self.flat.grad, self.dp.group)
 
     def __call__(self, batches):
         """batches: list (len = grad_accum) of (input_ids [B,S] int64, labels [B,S] int64) on device.

@@ -2,8 +2,8 @@
 """Summarise a rocprofv3 rocpd database (``--kernel-trace`` output ``*_results.db``).
 
   prof_db.py <db> stats [steps] [top]       per-kernel totals (ms/step, %, calls, avg us, VGPR/LDS)
-  prof_db.py <db> step [marker] [which]     kernel sequence of one step (located by a kernel that runs
-                                            once per step, default the AdamW update)
+  prof_db.py <db> step [marker] [which]     kernel sequence of one step (start offset, duration; located
+                                            by a kernel that runs once per step, default the AdamW update)
 """
 import sqlite3
 import sys
@@ -35,9 +35,11 @@ def step(db, marker="adamw_kernel", which=-2):
     idx = [i for i, x in enumerate(r) if marker in x[0]]
     a, b = idx[which - 1] + 1, idx[which] + 1
     tot = 0
+    t0 = r[a][1]
+    print(f"{'start_us':>9} {'dur_us':>8}")
     for name, s, e, grid, wg, lds, vg, ag in r[a:b]:
         tot += e - s
-        print(f"{(e - s) / 1e3:8.1f}  wg={grid // max(1, wg):6d}  {name[:110]}")
+        print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}  wg={grid // max(1, wg):6d}  {name[:110]}")
     print(f"sum {tot / 1e3:.1f} us, span {(r[b - 1][2] - r[a][1]) / 1e3:.1f} us, {b - a} kernels")
 
 

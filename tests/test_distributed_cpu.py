@@ -107,9 +107,12 @@ def _worker_train(rank, world, port, stage, q, accum=1, ckpt=False):
     tr = Trainer(m, flat, ds, None, tc, torch.device("cpu"), dp=dp, zero_stage=stage)
     tr.train()
     if stage == 3:
-        # gathered block copies and gradient buffers are released between uses
-        assert all(u.full.untyped_storage().nbytes() == 0 and u.gwork.untyped_storage().nbytes() == 0
-                   for u in m.zero3.units)
+        # between steps no unit is gathered or holds a live gradient buffer, and the blocks share
+        # two fixed slots (no allocation inside a step -> graph-capturable)
+        z3 = m.zero3
+        assert not any(u.gathered or u.g_live for u in z3.units)
+        blocks = z3.units[1:]
+        assert len({u.full.data_ptr() for u in blocks}) == min(2, len(blocks))
         params = m.zero3.full_state()
     else:
         if stage:
@@ -275,6 +278,57 @@ def test_ddp_overlap_with_grad_accumulation():
         p.join(60)
     want = (out[0][1] + out[1][1]) / 2  # mean over ranks of the summed micro-batch grads
     assert torch.allclose(out[0][0], want, atol=1e-6) and torch.allclose(out[1][0], want, atol=1e-6)
+
+
+def _worker_bucketed_reduce(rank, world, port, q, stage, bf16):
+    """Hook-driven bucketed reduction: ZeRO-2 reduces every bucket segment to its owner (the owned
+    shard must equal the rank mean), DDP/ZeRO-1 all-reduce; optionally through a bf16 comm buffer."""
+    _init(rank, world, port)
+    from mobilefinetuner_amd.ops import functional as Fx
+    from mobilefinetuner_amd.parallel.ddp import DataParallel
+    from mobilefinetuner_amd.utils.params import FlatParams
+    ps = [(f"p{i}", torch.nn.Parameter(torch.zeros(2000 + 333 * i))) for i in range(5)]
+    flat = FlatParams(ps, "cpu", shadow=False, pad_multiple=world)
+    shard = flat.numel // world if stage == 2 else None
+    dp = DataParallel(flat, bucket_mb=0.01, broadcast_from=None, shard=shard,
+                      reduce_dtype=torch.bfloat16 if bf16 else None)
+    assert len(dp.buckets) > 1 and dp._hook is not None
+    # the buckets tile the buffer exactly
+    spans = sorted((b["lo"], b["hi"]) for b in dp.buckets)
+    assert spans[0][0] == 0 and spans[-1][1] == flat.numel and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    dp.begin_step()
+    flat.grad.zero_()
+    gen = torch.Generator().manual_seed(7 + rank)
+    local = torch.zeros_like(flat.grad)
+    for sl in reversed(flat.slots):
+        g = torch.randn(sl.param.shape, generator=gen)
+        local[sl.offset:sl.offset + sl.numel] = g
+        Fx._sink(sl.param, g)
+    dp.finish()
+    lo, hi = dp.owned()
+    q.put((rank, lo, hi, flat.grad.clone(), local))
+    dp.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("stage,bf16", [(2, False), (2, True), (0, True)])
+def test_bucketed_reduce_owner_and_bf16(stage, bf16):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker_bucketed_reduce, args=(r, 2, port, q, stage, bf16)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = {r: (lo, hi, g, l) for r, lo, hi, g, l in [q.get(timeout=300) for _ in ps]}
+    for p in ps:
+        p.join(60)
+    want = (out[0][3] + out[1][3]) / 2
+    tol = 2e-2 if bf16 else 1e-6
+    covered = 0
+    for r, (lo, hi, g, _) in out.items():
+        assert torch.allclose(g[lo:hi], want[lo:hi], atol=tol), (r, (g[lo:hi] - want[lo:hi]).abs().max())
+        covered += hi - lo
+    assert covered == (want.numel() if stage == 2 else 2 * want.numel())
 
 
 def _worker_zero_nonfinite(rank, world, port, q):

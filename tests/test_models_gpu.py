@@ -83,10 +83,14 @@ def test_full_finetune_gpu_decreases_loss():
         assert p.grad is not None and p.grad.abs().sum() > 0, n
 
 
-@pytest.mark.parametrize("model_name", ["gpt2-tiny", "gemma3-tiny"])
-def test_zero3_single_gpu_matches_flat(model_name):
-    """ZeRO-3 (per-block gather into released/refilled storage, comm-stream prefetch, per-block
-    grad buffers) on one GPU == the plain flat-buffer full fine-tune, step for step."""
+@pytest.mark.parametrize("model_name,copy_path", [("gpt2-tiny", True), ("gemma3-tiny", True), ("gpt2-tiny", False)])
+def test_zero3_single_gpu_matches_flat(model_name, copy_path, monkeypatch):
+    """ZeRO-3 (per-block gathers into two shared slots, comm-stream prefetch, per-block grad
+    buffers) on one GPU == the plain flat-buffer full fine-tune, step for step -- eagerly and with
+    the whole ZeRO-3 step recorded into one hipGraph (2 eager warm-ups, capture, replays).
+    copy_path: the multi-rank gather / slot / gradient-fold path forced on one rank
+    (MFT_Z3_FORCE_COPY=1); otherwise the 1-rank aliasing fast path."""
+    monkeypatch.setenv("MFT_Z3_FORCE_COPY", "1" if copy_path else "0")
     from mobilefinetuner_amd.models import gemma3, gpt2
     from mobilefinetuner_amd.optim.adamw import FusedAdamW
     from mobilefinetuner_amd.parallel.zero3 import attach_zero3
@@ -104,17 +108,20 @@ def test_zero3_single_gpu_matches_flat(model_name):
     m0.set_full_finetune()
     flat = FlatParams(m0.named_parameters(), DEV)
     st0 = TrainStep(m0, flat, FusedAdamW(flat, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0), use_graph=False)
-    ref_losses = [float(st0(b).item()) for _ in range(3)]
-    m1 = make()
-    m1.set_full_finetune()
-    z3 = attach_zero3(m1, DEV, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0)
-    st1 = TrainStep(m1, z3.flat, z3, dp=z3, use_graph=False)
-    losses = [float(st1(b).item()) for _ in range(3)]
-    assert losses == pytest.approx(ref_losses, rel=2e-3, abs=2e-3)
-    full = z3.full_state()
-    for n, p in m0.named_parameters():
-        assert torch.allclose(full[n], p.detach().float().cpu(), atol=2e-3, rtol=1e-2), n
-    assert z3.stats["all_gather"] > 0 and z3.stats["reduce_scatter"] > 0
+    ref_losses = [float(st0(b).item()) for _ in range(5)]
+    for graph in (False, True):
+        m1 = make()
+        m1.set_full_finetune()
+        z3 = attach_zero3(m1, DEV, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0)
+        st1 = TrainStep(m1, z3.flat, z3, dp=z3, use_graph=graph)
+        assert st1.graph_comm and z3.direct == (not copy_path)
+        losses = [float(st1(b).item()) for _ in range(5)]
+        assert (st1.graph is not None) == graph
+        assert losses == pytest.approx(ref_losses, rel=2e-3, abs=2e-3), (graph, losses, ref_losses)
+        full = z3.full_state()
+        for n, p in m0.named_parameters():
+            assert torch.allclose(full[n], p.detach().float().cpu(), atol=2e-3, rtol=1e-2), (graph, n)
+        assert z3.stats["all_gather"] > 0 and z3.stats["reduce_scatter"] > 0
 
 
 def test_adamw_host_offload_matches_resident():
@@ -143,6 +150,34 @@ def test_adamw_host_offload_matches_resident():
     assert torch.allclose(sa["m"], sb["m"]) and torch.allclose(sa["v"], sb["v"])
     b.load_state_dict(sa)
     assert torch.allclose(b.state_dict()["v"], sa["v"])
+
+
+def test_adamw_offload_bf16_moments_track_fp32():
+    """Host-offloaded AdamW with bf16 moments (stochastic rounding, half the PCIe bytes) follows the
+    fp32 optimizer over many steps; round-to-nearest would freeze v under beta2 = 0.999."""
+    from mobilefinetuner_amd.optim.adamw import FusedAdamW
+    from mobilefinetuner_amd.utils.params import FlatParams
+    fl = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        fl.append(FlatParams([("p", torch.nn.Parameter(torch.randn(50_000, device=DEV)))], DEV))
+    a = FusedAdamW(fl[0], lr=1e-3, weight_decay=0.0, max_grad_norm=None)
+    b = FusedAdamW(fl[1], lr=1e-3, weight_decay=0.0, max_grad_norm=None, offload=True, offload_chunk=20_000,
+                   offload_dtype=torch.bfloat16)
+    assert b._slots[0][0].dtype == torch.bfloat16
+    start = fl[0].master.clone()
+    for it in range(60):
+        g = torch.randn(fl[0].numel, device=DEV, generator=torch.Generator(device=DEV).manual_seed(it)) * (1 + it % 3)
+        for f, o in zip(fl, (a, b)):
+            f.grad.copy_(g)
+            o.step()
+    torch.cuda.synchronize()
+    da, db = fl[0].master - start, fl[1].master - start
+    assert ((da - db).norm() / da.norm()).item() < 2e-2
+    m, v = b._moments_host()
+    sa = a.state_dict()
+    assert ((v - sa["v"]).norm() / sa["v"].norm()).item() < 2e-2
+    assert ((m - sa["m"]).norm() / sa["m"].norm()).item() < 3e-2
 
 
 def test_sharder_offload_matches_resident(monkeypatch):
