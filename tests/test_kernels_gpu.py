@@ -16,6 +16,14 @@ def _close(a, b, atol, rtol=0.0, msg=""):
     assert err <= tol, f"{msg} max abs err {err:.3e} > {tol:.3e}"
 
 
+def _rel(a, b, tol, msg=""):
+    """Relative L2 error: for reductions over many rows (weight / bias gradients), where a max-abs
+    bound would have to scale with the row count."""
+    a, b = a.float(), b.float()
+    err = ((a - b).norm() / b.norm().clamp(min=1e-12)).item()
+    assert err <= tol, f"{msg} rel L2 err {err:.3e} > {tol:.3e}"
+
+
 @pytest.fixture(autouse=True)
 def _seed():
     torch.manual_seed(0)
@@ -54,8 +62,9 @@ def test_layernorm(N, resid):
     lr_.backward()
     _close(y, yr, 0.05, msg="ln y")
     _close(x.grad, xr.grad, 0.08, 0.01, msg="ln dx")
-    _close(w.grad, wr.grad, 0.5, 0.01, msg="ln dw")
-    _close(b.grad, br.grad, 0.5, 0.01, msg="ln db")
+    _rel(w.grad, wr.grad, 2e-3, msg="ln dw")
+    _rel(b.grad, br.grad, 2e-3, msg="ln db")
+    _close(w.grad, wr.grad, 0.02, 2e-3, msg="ln dw")
     if resid:
         _close(d.grad, dr.grad, 0.08, 0.01, msg="ln ddelta")
 
@@ -75,7 +84,8 @@ def test_rmsnorm(N):
     (yr * gy.float()).sum().backward()
     _close(y, yr, 0.05, msg="rms y")
     _close(x.grad, xr.grad, 0.08, 0.01, msg="rms dx")
-    _close(w.grad, wr.grad, 0.5, 0.01, msg="rms dw")
+    _rel(w.grad, wr.grad, 2e-3, msg="rms dw")
+    _close(w.grad, wr.grad, 0.02, 2e-3, msg="rms dw")
 
 
 def test_gelu_and_gated():
@@ -433,7 +443,7 @@ def test_qknorm_rope(D, interleaved):
     (yr * g.float()).sum().backward()
     _close(y, yr, 0.06, msg="qkrope y")
     _close(big.grad, r.grad, 0.1, 0.01, msg="qkrope dx")
-    _close(w.grad, wr.grad, 0.5, 0.01, msg="qkrope dw")
+    _rel(w.grad, wr.grad, 5e-3, msg="qkrope dw")
 
 
 def test_gated_widened_output():
@@ -482,8 +492,8 @@ def test_qknorm_rope_attention_fused(nq, nkv, window, oc):
     (orf * g.float()).sum().backward()
     _close(o, orf, 0.03, msg="fused attn o")
     _close(qkv.grad, r.grad, 0.05, 0.02, msg="fused attn dqkv")
-    _close(wq.grad, wqr.grad, 0.5, 0.02, msg="fused attn dwq")
-    _close(wk.grad, wkr.grad, 0.5, 0.02, msg="fused attn dwk")
+    _rel(wq.grad, wqr.grad, 1e-2, msg="fused attn dwq")
+    _rel(wk.grad, wkr.grad, 1e-2, msg="fused attn dwk")
 
 
 def test_adamw_matches_reference():
