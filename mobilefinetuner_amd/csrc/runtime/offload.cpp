@@ -174,6 +174,19 @@ void* HostTier::host_ptr(const std::string& name) {
   return get(name).host;
 }
 
+void* HostTier::device_ptr(const std::string& name) {
+  std::lock_guard<std::mutex> g(mu_);
+  Entry& e = get(name);
+  if (!e.host) throw std::runtime_error("HostTier: " + name + " is not in host memory");
+  hipPointerAttribute_t at{};
+  HT_CHECK(hipPointerGetAttributes(&at, e.host));
+  if (at.type != hipMemoryTypeHost) throw std::runtime_error("HostTier: " + name + " is not pinned host memory");
+  void* d = nullptr;
+  HT_CHECK(hipHostGetDevicePointer(&d, e.host, 0));
+  if (!d) throw std::runtime_error("HostTier: " + name + " has no device mapping");
+  return d;
+}
+
 void HostTier::spill(const std::string& name) {
   synchronize(name);
   std::lock_guard<std::mutex> g(mu_);

@@ -51,6 +51,9 @@ class HostTier {
   size_t bytes(const std::string& name) const;
   // raw host pointer (pinned) for host-side inspection / quantised views
   void* host_ptr(const std::string& name);
+  // device-side address of the pinned host buffer (zero-copy access by kernels over PCIe); throws
+  // unless the runtime reports a mapped host allocation
+  void* device_ptr(const std::string& name);
   // disk tier
   void spill(const std::string& name);
   void unspill(const std::string& name);

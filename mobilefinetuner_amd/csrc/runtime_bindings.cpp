@@ -282,6 +282,15 @@ void register_runtime(py::module_& m) {
            [](mft::HostTier& h, const std::string& n, torch::Dtype dt, std::vector<int64_t> shape) {
              return torch::from_blob(h.host_ptr(n), shape, torch::TensorOptions().dtype(dt));
            })
+      .def("device_tensor",
+           [](mft::HostTier& h, const std::string& n, torch::Dtype dt, std::vector<int64_t> shape) {
+             int dev = 0;
+             TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "device_tensor: no HIP device");
+             // the pinned host bytes, addressed by kernels over PCIe (zero copy); tensor ops that
+             // need only the pointer (the fused AdamW) may use it like device memory
+             return torch::from_blob(h.device_ptr(n), shape,
+                                     torch::TensorOptions().dtype(dt).device(torch::kCUDA, dev));
+           })
       .def("synchronize", &mft::HostTier::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("synchronize_all", &mft::HostTier::synchronize_all, py::call_guard<py::gil_scoped_release>())
       .def("mark_resident", &mft::HostTier::mark_resident)

@@ -14,6 +14,7 @@ live in device memory so the whole optimizer step can be replayed from a hipGrap
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -37,18 +38,33 @@ class FusedAdamW:
         self.lo, self.hi = param_range if param_range is not None else (0, flat.numel)
         n = self.hi - self.lo
         # offload: the AdamW moments live in pinned host DRAM (native HostTier, csrc/runtime/
-        # offload.cpp) and stream through two device slots per chunk -- H2D of chunk c+1 and D2H
-        # of chunk c-1 on the tier's copy stream overlap the update of chunk c (SURVEY §2.13 "host-
-        # DRAM offload tier for optimizer state"; the reference's analogue is the disk sharder)
+        # offload.cpp; SURVEY §2.13 "host-DRAM offload tier for optimizer state", the reference's
+        # analogue is the disk sharder).  Default "zerocopy": the fused AdamW kernel reads and
+        # writes them in place over PCIe (both directions at once, nothing staged): GPT-2 XL
+        # ZeRO-3 offload 226.5 ms/step vs 314 ms streaming chunks through K device slots
+        # ("stream", MFT_OFFLOAD_MODE=stream; profiles/r2_offload_zerocopy_vs_stream.txt)
         # offload_dtype=bf16 (the reference's --shard_fp16_disk default): the host copies of the
         # moments are 16-bit -- half the PCIe bytes each way -- and the kernel updates them in
         # place with stochastic rounding (optim.hip), the fp32 master weights stay fp32
         self.offload = bool(offload) and dev.type == "cuda"
-        import os
         offload_chunk = int(os.environ.get("MFT_OFFLOAD_CHUNK", offload_chunk))
         offload_slots = int(os.environ.get("MFT_OFFLOAD_SLOTS", offload_slots))
         self.mdt = torch.bfloat16 if offload_dtype in (torch.bfloat16, torch.float16, "bf16", "fp16") else torch.float32
-        if self.offload:
+        # offload_mode: "stream" copies chunks through K device slots on two copy streams;
+        # "zerocopy" lets the AdamW kernel read and write the pinned host moments directly over
+        # PCIe (full duplex, no staging copies, no device slots)
+        self.zerocopy = self.offload and os.environ.get("MFT_OFFLOAD_MODE", "zerocopy") == "zerocopy"
+        if self.offload and self.zerocopy:
+            self._tier = native().runtime.HostTier(0, "", 0)
+            esz = torch.tensor([], dtype=self.mdt).element_size()
+            for k in ("m", "v"):
+                self._tier.add(f"{k}#0", n * esz)
+                self._tier.host_tensor(f"{k}#0", self.mdt, [n]).zero_()
+            self._chunks = [(0, n)]
+            self._zm = self._tier.device_tensor("m#0", self.mdt, [n])
+            self._zv = self._tier.device_tensor("v#0", self.mdt, [n])
+            self.m = self.v = None
+        elif self.offload:
             self._tier = native().runtime.HostTier(0, "", 0)
             self._chunks = []
             esz = torch.tensor([], dtype=self.mdt).element_size()
@@ -127,7 +143,13 @@ class FusedAdamW:
         if p.is_cuda:
             C = native()
             sh = self.flat.shadow[self.lo:self.hi] if self.flat.shadow is not None else None
-            if self.offload:
+            if self.offload and self.zerocopy:
+                C.adamw_step(p, g, self._zm, self._zv, self.lr_dev, self.step_dev,
+                             self.sumsq_dev if self.max_grad_norm is not None else None,
+                             self.beta1, self.beta2, self.eps, self.weight_decay,
+                             float(self.max_grad_norm or 0.0), self.l2_coupled, sh,
+                             self.nonfinite_dev if self.skip_nonfinite else None)
+            elif self.offload:
                 self._step_offloaded(C, p, g, sh)
             else:
                 C.adamw_step(p, g, self.m, self.v, self.lr_dev, self.step_dev, sumsq,
@@ -193,6 +215,8 @@ class FusedAdamW:
     def _moments_host(self):
         if hasattr(self, "_d2h"):
             self._d2h.synchronize()
+        if self.zerocopy:
+            torch.cuda.current_stream(self.flat.master.device).synchronize()
         m = torch.cat([self._tier.host_tensor(f"m#{c0}", self.mdt, [c1 - c0]) for c0, c1 in self._chunks]).float()
         v = torch.cat([self._tier.host_tensor(f"v#{c0}", self.mdt, [c1 - c0]) for c0, c1 in self._chunks]).float()
         return m, v
@@ -237,6 +261,7 @@ class FusedAdamW:
         if self.offload:
             if hasattr(self, "_d2h"):
                 self._d2h.synchronize()
+            torch.cuda.current_stream(self.flat.master.device).synchronize()
             for c0, c1 in self._chunks:
                 self._tier.host_tensor(f"m#{c0}", self.mdt, [c1 - c0]).copy_(sd["m"][c0:c1])
                 self._tier.host_tensor(f"v#{c0}", self.mdt, [c1 - c0]).copy_(sd["v"][c0:c1])

@@ -124,9 +124,12 @@ def test_zero3_single_gpu_matches_flat(model_name, copy_path, monkeypatch):
         assert z3.stats["all_gather"] > 0 and z3.stats["reduce_scatter"] > 0
 
 
-def test_adamw_host_offload_matches_resident():
-    """FusedAdamW with the moments in the pinned host tier (several chunks, double-buffered device
-    slots) == the resident optimizer, including clipping and state_dict round trip."""
+@pytest.mark.parametrize("mode", ["stream", "zerocopy"])
+def test_adamw_host_offload_matches_resident(mode, monkeypatch):
+    """FusedAdamW with the moments in the pinned host tier == the resident optimizer, including
+    clipping and state_dict round trip: streamed through K device slots in chunks, or read and
+    written in place by the kernel over PCIe (zero copy)."""
+    monkeypatch.setenv("MFT_OFFLOAD_MODE", mode)
     from mobilefinetuner_amd.optim.adamw import FusedAdamW
     from mobilefinetuner_amd.utils.params import FlatParams
     ps = []
@@ -137,7 +140,7 @@ def test_adamw_host_offload_matches_resident():
         ps.append(FlatParams([("p", p), ("q", q)], DEV))
     a = FusedAdamW(ps[0], lr=1e-2, weight_decay=0.1, max_grad_norm=0.5)
     b = FusedAdamW(ps[1], lr=1e-2, weight_decay=0.1, max_grad_norm=0.5, offload=True, offload_chunk=3000)
-    assert b.offload and len(b._chunks) > 3
+    assert b.offload and b.zerocopy == (mode == "zerocopy") and (mode == "zerocopy" or len(b._chunks) > 3)
     for it in range(4):
         g = torch.randn(ps[0].numel, device=DEV, generator=torch.Generator(device=DEV).manual_seed(it))
         for f, o in zip(ps, (a, b)):
@@ -152,9 +155,11 @@ def test_adamw_host_offload_matches_resident():
     assert torch.allclose(b.state_dict()["v"], sa["v"])
 
 
-def test_adamw_offload_bf16_moments_track_fp32():
+@pytest.mark.parametrize("mode", ["stream", "zerocopy"])
+def test_adamw_offload_bf16_moments_track_fp32(mode, monkeypatch):
     """Host-offloaded AdamW with bf16 moments (stochastic rounding, half the PCIe bytes) follows the
     fp32 optimizer over many steps; round-to-nearest would freeze v under beta2 = 0.999."""
+    monkeypatch.setenv("MFT_OFFLOAD_MODE", mode)
     from mobilefinetuner_amd.optim.adamw import FusedAdamW
     from mobilefinetuner_amd.utils.params import FlatParams
     fl = []
@@ -164,7 +169,7 @@ def test_adamw_offload_bf16_moments_track_fp32():
     a = FusedAdamW(fl[0], lr=1e-3, weight_decay=0.0, max_grad_norm=None)
     b = FusedAdamW(fl[1], lr=1e-3, weight_decay=0.0, max_grad_norm=None, offload=True, offload_chunk=20_000,
                    offload_dtype=torch.bfloat16)
-    assert b._slots[0][0].dtype == torch.bfloat16
+    assert b.mdt == torch.bfloat16
     start = fl[0].master.clone()
     for it in range(60):
         g = torch.randn(fl[0].numel, device=DEV, generator=torch.Generator(device=DEV).manual_seed(it)) * (1 + it % 3)
