@@ -100,6 +100,15 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return x * sigmoid_fast(2.f * u);
 }
 
+// GELU(x) and GELU'(x) from one sigmoid
+__device__ __forceinline__ void gelu_tanh_and_grad(float x, float& y, float& dy) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float s = sigmoid_fast(2.f * k0 * (x + k1 * x2 * x));
+  y = x * s;
+  dy = s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x2);
+}
+
 // d/dx: s + 2 x s (1 - s) k0 (1 + 3 k1 x^2), s = sigmoid(2u)   (0.5 (1 - tanh^2) = 2 s (1 - s))
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;

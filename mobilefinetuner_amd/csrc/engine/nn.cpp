@@ -283,7 +283,7 @@ Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2) {
   Gemm8Extra ex;
   ex.bias = &b1.c;
   ex.aux = &pre;
-  gemm8_call(x2, w1.c, false, ::mft::GEMM_EPI_BIAS_GELU, h, ex);
+  gemm8_call(x2, w1.c, false, ::mft::GEMM_EPI_BIAS_GELU_D, h, ex);  // aux = GELU'(pre)
   Tensor y = empty({M, N}, DType::BF16, x.device());
   gemm_nt(h, w2.c, b2.c, y);
   Shape ys = x.shape();
@@ -297,8 +297,8 @@ Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2) {
       Gemm8Extra e2;
       Tensor aux = pre;
       e2.aux = &aux;
-      if (!p2->trainable()) gemm8_call(dy2, p2->transposed(), false, ::mft::GEMM_EPI_DGELU, dpre, e2);
-      else gemm8_call(dy2, p2->c, true, ::mft::GEMM_EPI_DGELU, dpre, e2);
+      if (!p2->trainable()) gemm8_call(dy2, p2->transposed(), false, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
+      else gemm8_call(dy2, p2->c, true, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
       Tensor dx = empty({M, K}, DType::BF16, dy2.device());
       gemm_nn(dpre, p1->c, dx);
       if (p2->trainable()) {

@@ -60,7 +60,10 @@ int attn_bwd_path(int D, int Sq, int Sk, int window);
 enum GemmEpi { GEMM_EPI_NONE = 0, GEMM_EPI_BIAS = 1, GEMM_EPI_BIAS_GELU = 2, GEMM_EPI_DGELU = 3, GEMM_EPI_F32ACC = 4,
                GEMM_EPI_LORA = 5, GEMM_EPI_F32PART = 6 /* internal: split-K fp32 slab */,
                // fused LM-head cross entropy (gemm8 only, driven by lm_head_ce in xent.hip)
-               GEMM_EPI_CE_FWD = 7, GEMM_EPI_CE_DGRAD = 8 };
+               GEMM_EPI_CE_FWD = 7, GEMM_EPI_CE_DGRAD = 8,
+               // GELU MLP (gemm8 only): the forward stores GELU'(pre) -- not pre -- as aux (one
+               // sigmoid serves GELU and its derivative), the backward multiplies by it
+               GEMM_EPI_BIAS_GELU_D = 9, GEMM_EPI_MUL_AUX = 10 };
 struct GemmArgs {
   const bf16_t* A;
   long lda;  // A [M, K] row-major

@@ -156,6 +156,22 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4
   // is then 16-B vector loads/stores straight from registers (no LDS staging, no wave syncs).
   const int g4 = lane >> 4;
   const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
+  // epilogues that read an [M, N] operand: every load of the lane's 16 pieces is issued before the
+  // first store (the stores may alias it, so the compiler would otherwise wait on each load in turn)
+  constexpr bool kAux = EPI == GEMM_EPI_DGELU || EPI == GEMM_EPI_MUL_AUX;
+  u16x8_t auxv[4][4];
+  if constexpr (kAux) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int qa = (q == 2 || q == 3) ? 1 : 0, qb = (q == 1 || q == 2) ? 1 : 0;
+      const int colc = min(n0 + qb * 128 + wn * 32 + cofs, g.N - 8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = min(m0 + qa * 128 + wm * 64 + i * 16 + (lane & 15), g.M - 1);
+        auxv[q][i] = *reinterpret_cast<const u16x8_t*>(g.aux + (long)row * g.ldaux + colc);
+      }
+    }
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int qa = (q == 2 || q == 3) ? 1 : 0, qb = (q == 1 || q == 2) ? 1 : 0;
@@ -163,7 +179,8 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4
     const bool col_ok = col < g.N;
     const int colc = min(col, g.N - 8);
     float bias_v[8];
-    if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU) load8(g.bias + colc, bias_v);
+    if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU || EPI == GEMM_EPI_BIAS_GELU_D)
+      load8(g.bias + colc, bias_v);
     float o[4][8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -230,19 +247,28 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           v[e] *= g.alpha;
-          if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU) v[e] += bias_v[e];
+          if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU || EPI == GEMM_EPI_BIAS_GELU_D)
+            v[e] += bias_v[e];
         }
       }
       if constexpr (EPI == GEMM_EPI_DGELU) {
-        float pre[8];
-        load8(g.aux + (long)min(row, g.M - 1) * g.ldaux + colc, pre);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(pre[e]);
+        for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(bf2f(auxv[q][i][e]));
+      }
+      if constexpr (EPI == GEMM_EPI_MUL_AUX) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= bf2f(auxv[q][i][e]);
       }
       if constexpr (EPI == GEMM_EPI_BIAS_GELU) {
         if (ok) store8(g.aux + (long)row * g.ldaux + col, v);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+      }
+      if constexpr (EPI == GEMM_EPI_BIAS_GELU_D) {
+        float d[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gelu_tanh_and_grad(v[e], v[e], d[e]);
+        if (ok) store8(g.aux + (long)row * g.ldaux + col, d);
       }
       if (ok) store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, v);
     }
@@ -981,6 +1007,8 @@ void gemm8x(const GemmArgs& g0, int epi, bool a_t, bool b_t, hipStream_t st) {
     case GEMM_EPI_BIAS: launch8_layout<GEMM_EPI_BIAS>(g, a_t, b_t, st); break;
     case GEMM_EPI_BIAS_GELU: launch8_layout<GEMM_EPI_BIAS_GELU>(g, a_t, b_t, st); break;
     case GEMM_EPI_DGELU: launch8_layout<GEMM_EPI_DGELU>(g, a_t, b_t, st); break;
+    case GEMM_EPI_BIAS_GELU_D: launch8_layout<GEMM_EPI_BIAS_GELU_D>(g, a_t, b_t, st); break;
+    case GEMM_EPI_MUL_AUX: launch8_layout<GEMM_EPI_MUL_AUX>(g, a_t, b_t, st); break;
     case GEMM_EPI_F32ACC:
       // fp32 weight-gradient accumulate: split over K into slabs (g.ws, ksplit * M * N floats) when
       // the output has few tiles, then one deterministic reduce into C; else accumulate in place

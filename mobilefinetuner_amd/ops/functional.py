@@ -26,6 +26,7 @@ from torch.autograd import Function
 from .._ext import native
 
 GEMM_EPI_NONE, GEMM_EPI_BIAS, GEMM_EPI_BIAS_GELU, GEMM_EPI_DGELU, GEMM_EPI_F32ACC, GEMM_EPI_LORA = 0, 1, 2, 3, 4, 5
+GEMM_EPI_BIAS_GELU_D, GEMM_EPI_MUL_AUX = 9, 10
 
 # ---------------------------------------------------------------- host tensors (test oracle only)
 _HOST_OPS = [None]
@@ -644,10 +645,10 @@ def _fused_dx(dy2, w, epi, **kw):
 
 class _MLPGelu(Function):
     """y = GELU(x W1^T + b1) W2^T + b2 with both GELU passes fused into the hand-written MFMA GEMM
-    (csrc/kernels/gemm.hip): the fc GEMM's epilogue adds the bias and writes BOTH the
-    pre-activation (saved for backward) and GELU(pre); the mlp_proj data-grad GEMM's epilogue
-    multiplies by GELU'(pre), so no separate GELU pass touches the [M, 4C] activations in either
-    direction.  Reference MLP: graph/gpt2_model.cpp (c_fc matmul, gelu_new, c_proj matmul as three
+    (csrc/kernels/gemm8.hip): the fc GEMM's epilogue adds the bias and writes BOTH GELU(pre) and
+    GELU'(pre) (one sigmoid for both; saved for backward instead of pre); the mlp_proj data-grad
+    GEMM's epilogue multiplies by it, so no separate GELU pass touches the [M, 4C] activations in
+    either direction and the backward does no transcendental work.  Reference MLP: graph/gpt2_model.cpp (c_fc matmul, gelu_new, c_proj matmul as three
     separate ops)."""
 
     @staticmethod
@@ -658,9 +659,9 @@ class _MLPGelu(Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         w1c, b1c, w2c, b2c = cw(w1), cw(b1), cw(w2), cw(b2)
-        h, pre = C.gemm_t(x2, w1c, False, False, GEMM_EPI_BIAS_GELU, bias=b1c)
+        h, dgl = C.gemm_t(x2, w1c, False, False, GEMM_EPI_BIAS_GELU_D, bias=b1c)  # dgl = GELU'(pre)
         y = gemm_linear(h, w2c, b2c)
-        ctx.save_for_backward(x2 if _needs(w1) else None, pre, h if _needs(w2) else None)
+        ctx.save_for_backward(x2 if _needs(w1) else None, dgl, h if _needs(w2) else None)
         ctx.params = (w1, b1, w2, b2)
         ctx.wc = w1c
         ctx.shape = shape
@@ -669,13 +670,13 @@ class _MLPGelu(Function):
     @staticmethod
     def backward(ctx, dy):
         C = native()
-        x2, pre, h = ctx.saved_tensors
+        x2, dgl, h = ctx.saved_tensors
         w1, b1, w2, b2 = ctx.params
         w1c = ctx.wc
         dy2 = dy.reshape(-1, dy.shape[-1])
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dpre = _fused_dx(dy2, w2, GEMM_EPI_DGELU, aux=pre)[0]
+        dpre = _fused_dx(dy2, w2, GEMM_EPI_MUL_AUX, aux=dgl)[0]
         grads = [None] * 5
         if ctx.needs_input_grad[0]:
             grads[0] = gemm_dx(dpre, w1c).view(ctx.shape)

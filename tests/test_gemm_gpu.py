@@ -6,6 +6,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_DGELU, EPI_F32ACC, EPI_LORA = 0, 1, 2, 3, 4, 5
+EPI_BIAS_GELU_D, EPI_MUL_AUX = 9, 10
 
 
 def C():
@@ -68,3 +69,23 @@ def test_gemm8_tn_wgrad_splitk(T, P, Q):
     out2 = base.clone()
     C().gemm_t(dy, x, True, True, EPI_F32ACC, alpha=0.5, out=out2)
     assert torch.equal(out, out2), "split-K weight gradient must be deterministic"
+
+
+def _gelu_and_grad(pf):
+    t = torch.tanh(0.7978845608 * (pf + 0.044715 * pf ** 3))
+    return 0.5 * pf * (1 + t), 0.5 * (1 + t) + 0.5 * pf * (1 - t ** 2) * 0.7978845608 * (1 + 3 * 0.044715 * pf ** 2)
+
+
+def test_gemm8_gelu_mlp_epilogues():
+    """fc forward: GELU(xW^T + b) and GELU'(xW^T + b) (aux) from one epilogue; mlp_proj data-grad:
+    (dy W) * aux -- at the GPT-2 MLP shapes."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    M, K, N = 65536, 768, 3072
+    x, w, b = rnd(M, K, gen=g), rnd(N, K, s=0.1, gen=g), rnd(N, s=0.5, gen=g)
+    h, d = C().gemm_t(x, w, False, False, EPI_BIAS_GELU_D, bias=b)
+    pre = x.float() @ w.float().t() + b.float()
+    gl, dg = _gelu_and_grad(pre)
+    assert relerr(h, gl) < 1e-2 and relerr(d, dg) < 1e-2
+    dy, w2 = rnd(M, K, gen=g), rnd(K, N, s=0.05, gen=g)
+    y = C().gemm_t(dy, w2, False, True, EPI_MUL_AUX, aux=d)[0]
+    assert relerr(y, (dy.float() @ w2.float()) * d.float()) < 1e-2
