@@ -172,7 +172,7 @@ def build_engine(objs_kernels, objs_runtime, abi, hdr, verbose=False, jobs=None)
     for exe, (obj, _) in aobjs.items():
         path = os.path.join(BIN_DIR, exe)
         if changed or not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(o) for o in libs):
-            cmd = [HIPCC, "-fPIC", obj, *libs, "-o", path + ".tmp", f"-L{ROCM}/lib", "-lhipblaslt", "-lamdhip64",
+            cmd = [HIPCC, "-fPIC", obj, *libs, "-o", path + ".tmp", f"-L{ROCM}/lib", "-lhipblaslt", "-lrccl", "-lamdhip64",
                    f"-Wl,-rpath,{ROCM}/lib", "-ldl", "-lpthread"]
             if verbose:
                 print(" ".join(cmd), flush=True)

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "engine/allocator.h"
+#include "engine/comm.h"
 #include "engine/gemm.h"
 #include "engine/gpt2.h"
 #include "engine/optim.h"
@@ -173,15 +174,22 @@ int run(int argc, char** argv) {
                              "(python -m mobilefinetuner_amd.cli." + std::string(kProg) + "); the native CLI keeps "
                              "every weight resident in HBM");
   if (a.b("deterministic")) set_deterministic(true);
+  // data parallelism: one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK, e.g. under
+  // `python -m mobilefinetuner_amd.launch --nproc N`), native RCCL communicator; the communicator
+  // selects the device LOCAL_RANK.  MFT_DP_FORCE_COMM=1 builds a 1-rank one on a single GPU.
+  const char* fc = std::getenv("MFT_DP_FORCE_COMM");
+  std::unique_ptr<Communicator> comm = Communicator::from_env(fc && fc[0] == '1');
+  if (!comm) HIP_OK(hipSetDevice(0));
+  if (comm && comm->rank() != 0) std::setvbuf(stdout, nullptr, _IOFBF, 1 << 16);  // rank 0 reports
   // one non-blocking stream for everything (graph capture target)
   hipStream_t stream;
-  HIP_OK(hipSetDevice(0));
   HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   set_current_stream(stream);
 
   const int seq_len = a.i("seq_len", 128);
   const uint64_t seed = (uint64_t)a.l("seed", 42);
   std::printf("\n========== %s (MI355X native engine) ==========\n", kProg);
+  if (comm) std::printf("  data parallel: rank %d of %d (RCCL, device %d)\n", comm->rank(), comm->world(), comm->local_rank());
 
   std::printf("\n[1/6] Loading model...\n");
   const std::string pdir = a.get("pretrained_dir");
@@ -229,6 +237,10 @@ int run(int argc, char** argv) {
   std::printf("\n[3/6] Loading dataset...\n");
   DataConfig dc;
   dc.seq_len = seq;
+  if (comm) {  // this rank's shard of every epoch's shuffled order
+    dc.rank = comm->rank();
+    dc.world = comm->world();
+  }
   dc.eos_id = 50256;
   dc.seed = seed;
   dc.data_fraction = a.f("data_fraction", 1.f);
@@ -318,7 +330,7 @@ int run(int argc, char** argv) {
     pm->set_manual_readings(a.f("pm_manual_batt", 100.f), a.f("pm_manual_temp", 30.f));
     if (!a.get("pm_schedule").empty()) pm->set_step_schedule(PowerMonitor::parse_schedule(a.get("pm_schedule")));
   }
-  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get());
+  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get());
   const std::string lora_out = a.get("lora_out"), out_path = a.get("output_path");
   auto save = [&](int64_t step) {
     if (!full && !lora_out.empty()) {
@@ -337,12 +349,13 @@ int run(int argc, char** argv) {
   const auto t0 = std::chrono::steady_clock::now();
   trainer.train(save);
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const bool lead = !comm || comm->rank() == 0;
   std::printf("\n[6/6] Saving...\n");
-  if (!full && !lora_out.empty()) {
+  if (!full && !lora_out.empty() && lead) {
     model->save_lora(lora_out);
     std::printf("  LoRA saved to: %s\n", lora_out.c_str());
   }
-  if (full && !out_path.empty()) {
+  if (full && !out_path.empty() && lead) {
     model->save_hf(out_path);
     std::printf("  model saved to: %s\n", out_path.c_str());
   }

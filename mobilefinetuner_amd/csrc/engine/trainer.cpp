@@ -15,9 +15,13 @@ namespace mft {
 namespace eng {
 
 Trainer::Trainer(GPT2& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid,
-                 const TrainConfig& cfg, PowerMonitor* pm)
-    : model_(model), flat_(flat), opt_(opt), train_(train), valid_(valid), cfg_(cfg), pm_(pm) {
+                 const TrainConfig& cfg, PowerMonitor* pm, Communicator* comm)
+    : model_(model), flat_(flat), opt_(opt), train_(train), valid_(valid), cfg_(cfg), pm_(pm), comm_(comm) {
   stream_ = current_stream();
+  if (comm_) {  // every rank starts from rank 0's trainable weights
+    comm_->broadcast(flat_.master.data_ptr(), (size_t)flat_.numel * sizeof(float), 0, stream_);
+    flat_.refresh_shadow();
+  }
   const int64_t micro = cfg.batch, accum = std::max(1, cfg.accum);
   const int64_t n_local = (int64_t)train.num_local();
   steps_per_epoch_ = std::max<int64_t>(1, (n_local + micro * accum - 1) / (micro * accum));
@@ -37,6 +41,16 @@ Trainer::~Trainer() {
 }
 
 void Trainer::eager_step() {
+  fwd_bwd();
+  reduce_grads();
+  opt_.step();
+}
+
+void Trainer::reduce_grads() {
+  if (comm_) comm_->all_reduce_avg(static_cast<float*>(flat_.grad.data_ptr()), (size_t)flat_.numel, stream_);
+}
+
+void Trainer::fwd_bwd() {
   const float inv = 1.f / (float)ids_.size();
   flat_.zero_grad();
   loss_acc_.zero_();
@@ -51,7 +65,6 @@ void Trainer::eager_step() {
     backward({scaled});
     add_(loss_acc_, loss.detach(), inv);
   }
-  opt_.step();
 }
 
 void Trainer::capture() {
@@ -59,7 +72,10 @@ void Trainer::capture() {
   pool_ = al.new_pool();
   CachingAllocator::set_current_pool(pool_);
   HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
-  eager_step();
+  // with a communicator the collective and the optimizer run eagerly after each replay (one
+  // latency-bound all-reduce; no RCCL call is recorded into the graph)
+  if (comm_) fwd_bwd();
+  else eager_step();
   HIP_OK(hipStreamEndCapture(stream_, &graph_));
   CachingAllocator::set_current_pool(0);
   HIP_OK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
@@ -82,9 +98,17 @@ Tensor Trainer::step(const std::vector<std::pair<const int64_t*, const int64_t*>
     } else {
       capture();
       HIP_OK(hipGraphLaunch(exec_, stream_));
+      if (comm_) {
+        reduce_grads();
+        opt_.step();
+      }
     }
   } else {
     HIP_OK(hipGraphLaunch(exec_, stream_));
+    if (comm_) {
+      reduce_grads();
+      opt_.step();
+    }
   }
   return loss_acc_;
 }
@@ -111,6 +135,14 @@ std::pair<double, double> Trainer::evaluate(int max_batches, int batch_size) {
     ++done;
   }
   model_.training = tr;
+  if (comm_) {  // token-weighted over every rank's shard
+    float h2[2] = {(float)nll, (float)cnt};
+    Tensor d = from_host(h2, {2}, DType::F32);
+    comm_->all_reduce_sum(static_cast<float*>(d.data_ptr()), 2, current_stream());
+    Tensor back = d.to(Device::cpu());
+    nll = static_cast<const float*>(back.data_ptr())[0];
+    cnt = static_cast<const float*>(back.data_ptr())[1];
+  }
   const double m = nll / std::max(1.0, cnt);
   return {m, std::exp(std::min(m, 50.0))};
 }
@@ -148,6 +180,11 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
     ++steps_since;
     const bool log_now = cfg_.log_interval > 0 && (global_step % cfg_.log_interval == 0 || it + 1 == total_steps_);
     if (log_now) {
+      if (comm_) {  // mean over ranks (a copy: the graph keeps accumulating into loss_acc_)
+        Tensor lc = loss.clone();
+        comm_->all_reduce_avg(static_cast<float*>(lc.data_ptr()), 1, current_stream());
+        loss = lc;
+      }
       const float l = (float)loss.item();  // syncs the stream
       const auto now = std::chrono::steady_clock::now();
       const double dt = std::chrono::duration<double>(now - t_last).count();
@@ -160,11 +197,13 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
       ema_loss = ema_init ? cfg_.ema_beta * ema_loss + (1.0 - cfg_.ema_beta) * l : l;
       ema_init = true;
       const float gn = opt_.grad_norm();
-      std::printf("[Step %lld/%lld] Loss=%.4f PPL=%.2f LR=%.6g GradNorm=%.4f EMA=%.4f tok/s=%.0f step_ms=%.2f\n",
-                  (long long)global_step, (long long)total_steps_, l, std::exp(std::min<double>(l, 50.0)), lr, gn,
-                  ema_loss, tps, step_ms);
+      const int nr = comm_ ? comm_->world() : 1;
+      if (lead())
+        std::printf("[Step %lld/%lld] Loss=%.4f PPL=%.2f LR=%.6g GradNorm=%.4f EMA=%.4f tok/s=%.0f step_ms=%.2f\n",
+                    (long long)global_step, (long long)total_steps_, l, std::exp(std::min<double>(l, 50.0)), lr, gn,
+                    ema_loss, tps * nr, step_ms);
       std::fflush(stdout);
-      if (metrics.is_open()) {
+      if (metrics.is_open() && lead()) {
         metrics << "{\"step\": " << global_step << ", \"loss\": " << l << ", \"lr\": " << lr << ", \"grad_norm\": " << gn
                 << ", \"tokens_per_s\": " << tps << ", \"step_ms\": " << step_ms << "}\n";
         metrics.flush();
@@ -172,14 +211,15 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
     }
     if (cfg_.eval_interval > 0 && global_step % cfg_.eval_interval == 0 && valid_) {
       auto ev = evaluate(cfg_.eval_batches, cfg_.eval_batch_size);
-      std::printf("\n[Eval] step %lld | valid_nll %.4f | valid_ppl %.2f\n\n", (long long)global_step, ev.first,
-                  ev.second);
-      if (!cfg_.eval_out.empty()) {
+      if (lead())
+        std::printf("\n[Eval] step %lld | valid_nll %.4f | valid_ppl %.2f\n\n", (long long)global_step, ev.first,
+                    ev.second);
+      if (!cfg_.eval_out.empty() && lead()) {
         std::ofstream eo(cfg_.eval_out, std::ios::app);
         eo << "{\"step\": " << global_step << ", \"nll\": " << ev.first << ", \"ppl\": " << ev.second << "}\n";
       }
     }
-    if (cfg_.save_every > 0 && global_step % cfg_.save_every == 0 && save_fn) save_fn(global_step);
+    if (cfg_.save_every > 0 && global_step % cfg_.save_every == 0 && save_fn && lead()) save_fn(global_step);
     if (pm_) {
       const int ms = pm_->suggest_sleep_ms(global_step);
       if (ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(ms));

@@ -7,13 +7,18 @@
 // micro-batch forward+backward, clip, AdamW) is captured ONCE into a hipGraph after two eager
 // warm-up steps (relaxed capture mode, private allocator pool) and replayed with the next batch
 // copied into the graph's static input buffers; the loss stays on the device and is read only when
-// a log line is due.
+// a log line is due.  Data parallelism (native RCCL communicator, engine/comm.h): every rank
+// starts from rank 0's weights (broadcast), reads its own data shard, and the flat gradient is
+// averaged by ONE all-reduce on the compute stream between the replayed forward/backward graph
+// and the optimizer step (LoRA: 1.8 MB, latency-bound); logged losses and eval sums are reduced
+// over the ranks and only rank 0 prints and saves.
 #pragma once
 #include <functional>
 #include <memory>
 #include <string>
 #include <vector>
 
+#include "engine/comm.h"
 #include "engine/gpt2.h"
 #include "engine/optim.h"
 #include "runtime/dataset.h"
@@ -38,7 +43,7 @@ struct TrainConfig {
 class Trainer {
  public:
   Trainer(GPT2& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid, const TrainConfig& cfg,
-          PowerMonitor* pm = nullptr);
+          PowerMonitor* pm = nullptr, Communicator* comm = nullptr);
   ~Trainer();
   int64_t total_steps() const { return total_steps_; }
   int64_t steps_per_epoch() const { return steps_per_epoch_; }
@@ -55,7 +60,10 @@ class Trainer {
 
  private:
   void eager_step();
+  void fwd_bwd();
+  void reduce_grads();
   void capture();
+  bool lead() const { return !comm_ || comm_->rank() == 0; }
   GPT2& model_;
   FlatParams& flat_;
   AdamW& opt_;
@@ -63,6 +71,7 @@ class Trainer {
   TokenDataset* valid_;
   TrainConfig cfg_;
   PowerMonitor* pm_;
+  Communicator* comm_;
   int64_t total_steps_ = 0, steps_per_epoch_ = 1;
   // static device inputs (the graph reads these) + loss accumulator
   std::vector<Tensor> ids_, labels_;

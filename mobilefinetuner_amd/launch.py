@@ -4,7 +4,9 @@
     python -m mobilefinetuner_amd.launch --nproc 8 -m mobilefinetuner_amd.cli.gpt2_full_finetune [args...]
 
 One process per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in the
-environment; the ranks build their RCCL communicator through torch.distributed's TCP store).
+environment; the Python ranks build their RCCL communicator through torch.distributed's TCP store,
+the native CLIs (bin/gpt2_lora_finetune, bin/gpt2_full_finetune) through libmft's own TCP unique-id
+exchange, csrc/engine/comm.cpp).
 SURVEY §5.3 "failure detection": the launcher watches every rank; when one exits non-zero (crash,
 fault injection, RCCL watchdog abort) or the optional job timeout expires, the remaining ranks get
 SIGTERM, then SIGKILL after a grace period, and the launcher exits with the failing rank's code, so a

@@ -173,3 +173,25 @@ def test_native_full_finetune_runs(tmp_path):
     # every tensor kind was trained (weights, biases, norms, tied embedding)
     for k in ("wte.weight", "h.1.mlp.c_proj.weight", "h.0.ln_1.weight", "h.0.attn.c_attn.bias", "ln_f.bias"):
         assert not torch.equal(sd0[k], sd6[k]), k
+
+
+def test_native_cli_with_rccl_communicator():
+    """The native data-parallel path (engine/comm.h: RCCL communicator, rank-0 broadcast of the
+    trainable weights, gradient all-reduce between the replayed forward/backward graph and the
+    optimizer, reduced eval sums) on a 1-rank group (MFT_DP_FORCE_COMM=1): identical losses to the
+    single-process run (--deterministic; a 1-rank average is exact)."""
+    common = ["--random_init", "--model", "gpt2-tiny", "--synthetic_data", "--synthetic_tokens", "100000", "--steps",
+              "6", "--batch_size", "4", "--seq_len", "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic",
+              "--eval_interval", "3", "--eval_batches", "4"]
+    outs = []
+    for force in ("0", "1"):
+        env = dict(os.environ, MFT_DP_FORCE_COMM=force, MASTER_ADDR="127.0.0.1", MASTER_PORT="29611")
+        env.pop("WORLD_SIZE", None)
+        r = subprocess.run([_bin("gpt2_lora_finetune"), *common], capture_output=True, text=True, timeout=180, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        if force == "1":
+            assert "data parallel: rank 0 of 1" in r.stdout
+        steps = [ln.split("Loss=")[1].split()[0] for ln in r.stdout.splitlines() if ln.startswith("[Step")]
+        evals = [ln for ln in r.stdout.splitlines() if ln.startswith("[Eval]")]
+        outs.append((steps, evals))
+    assert outs[0] == outs[1] and len(outs[0][0]) == 6 and len(outs[0][1]) == 2, outs
