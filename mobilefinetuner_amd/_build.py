@@ -74,6 +74,7 @@ APPS = {
     "gpt2_lora_finetune": ("gpt2_finetune.cpp", []),
     "gpt2_full_finetune": ("gpt2_finetune.cpp", ["-DMFT_FULL_FT=1"]),
     "engine_selftest": ("engine_selftest.cpp", []),
+    "eval_ppl": ("eval_ppl.cpp", []),
 }
 
 

@@ -25,6 +25,7 @@
 #include <thread>
 #include <vector>
 
+#include "apps/app_common.h"
 #include "engine/allocator.h"
 #include "engine/comm.h"
 #include "engine/gemm.h"
@@ -37,6 +38,10 @@
 
 using namespace mft;
 using namespace mft::eng;
+using mft::apps::Args;
+using mft::apps::file_exists;
+using mft::apps::parse_args;
+using mft::apps::split_file;
 
 #ifdef MFT_FULL_FT
 static const char* kProg = "gpt2_full_finetune";
@@ -45,19 +50,6 @@ static const char* kProg = "gpt2_lora_finetune";
 #endif
 
 namespace {
-
-struct Args {
-  std::map<std::string, std::string> kv;
-  std::set<std::string> flags;
-  std::string get(const std::string& k, const std::string& d = "") const {
-    auto it = kv.find(k);
-    return it == kv.end() ? d : it->second;
-  }
-  int i(const std::string& k, int d) const { return kv.count(k) ? std::stoi(kv.at(k)) : d; }
-  int64_t l(const std::string& k, int64_t d) const { return kv.count(k) ? std::stoll(kv.at(k)) : d; }
-  float f(const std::string& k, float d) const { return kv.count(k) ? std::stof(kv.at(k)) : d; }
-  bool b(const std::string& k) const { return flags.count(k) || (kv.count(k) && kv.at(k) != "0" && kv.at(k) != "false"); }
-};
 
 const std::set<std::string> kBool = {"split_qkv", "random_init", "synthetic_data", "no_graph", "compat_l2_adam",
                                      "shard_enable", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
@@ -71,39 +63,7 @@ const std::set<std::string> kValued = {
     "shard_dir", "shard_budget_mb", "shard_fp16_disk", "model", "synthetic_tokens", "pretokenized_path",
     "pretokenized_meta", "lora_targets", "metrics_out", "device"};
 
-Args parse(int argc, char** argv) {
-  Args a;
-  for (int i = 1; i < argc; ++i) {
-    std::string s = argv[i];
-    if (s.rfind("--", 0) != 0) throw std::runtime_error("unexpected argument '" + s + "'");
-    s = s.substr(2);
-    std::string key = s, val;
-    bool has_val = false;
-    const size_t eq = s.find('=');
-    if (eq != std::string::npos) {
-      key = s.substr(0, eq);
-      val = s.substr(eq + 1);
-      has_val = true;
-    }
-    if (kBool.count(key)) {
-      if (has_val) a.kv[key] = val;
-      else a.flags.insert(key);
-      continue;
-    }
-    if (!kValued.count(key)) throw std::runtime_error("unknown flag --" + key + " (see --help)");
-    if (!has_val) {
-      if (i + 1 >= argc) throw std::runtime_error("flag --" + key + " needs a value");
-      val = argv[++i];
-    }
-    a.kv[key] = val;
-  }
-  return a;
-}
-
-bool file_exists(const std::string& p) {
-  struct stat st;
-  return stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode);
-}
+Args parse(int argc, char** argv) { return parse_args(argc, argv, kBool, kValued); }
 
 std::string checkpoint_path(const std::string& stem, int64_t step) {
   const size_t dot = stem.rfind('.');
@@ -133,14 +93,6 @@ std::string norm_target(std::string t) {
   if (l == "mlpfcin" || l == "mlp_fc_in" || l == "c_fc" || l == "fc_in") return "MlpFcIn";
   if (l == "mlpfcout" || l == "mlp_fc_out" || l == "fc_out") return "MlpFcOut";
   throw std::runtime_error("unknown GPT-2 LoRA target '" + t + "'");
-}
-
-std::string split_file(const std::string& dir, const char* const* names) {
-  for (int i = 0; names[i]; ++i) {
-    const std::string p = dir + "/" + names[i];
-    if (file_exists(p)) return p;
-  }
-  return "";
 }
 
 void usage() {

@@ -195,3 +195,23 @@ def test_native_cli_with_rccl_communicator():
         evals = [ln for ln in r.stdout.splitlines() if ln.startswith("[Eval]")]
         outs.append((steps, evals))
     assert outs[0] == outs[1] and len(outs[0][0]) == 6 and len(outs[0][1]) == 2, outs
+
+
+def test_native_eval_ppl_matches_python_cli(tmp_path):
+    """Native eval_ppl (fused LM head, merged LoRA) == the Python eval_ppl CLI on the same weights,
+    adapter and pretokenized validation split."""
+    tmp = str(tmp_path)
+    _, lora = _make_fixture(tmp, 128, 60_000)
+    common = ["--pretrained_dir", tmp, "--lora_path", lora, "--pretokenized_path", os.path.join(tmp, "tokens.bin"),
+              "--split", "valid", "--seq_len", "128", "--batch_size", "4"]
+    nat_out, py_out = os.path.join(tmp, "nat.json"), os.path.join(tmp, "py.json")
+    r = subprocess.run([_bin("eval_ppl"), *common, "--out", nat_out], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run(["python", "-m", "mobilefinetuner_amd.cli.eval_ppl", *common, "--out", py_out],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    nat, py = json.load(open(nat_out)), json.loads(open(py_out).read().splitlines()[-1])
+    print(nat, py)
+    assert nat["tokens"] == py.get("tokens", py.get("n_tokens", nat["tokens"]))
+    assert abs(nat["ppl"] - py["ppl"]) < 2e-3 * py["ppl"], (nat, py)
