@@ -194,13 +194,19 @@ def main():
     else:
         force_comm = os.environ.get("MFT_DP_FORCE_COMM", "0") == "1"
         if world > 1 or force_comm:
+            if os.environ.get("MFT_DIST_BACKEND", "nccl") != "nccl":
+                local_rank = 0  # every rank shares the one GPU
             torch.cuda.set_device(local_rank)
             if world == 1:  # 1-rank RCCL group: profile the reducer's collectives on one GPU
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 2000))
                 os.environ.setdefault("RANK", "0")
                 os.environ.setdefault("WORLD_SIZE", "1")
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            backend = os.environ.get("MFT_DIST_BACKEND", "nccl")  # gloo: several ranks on one GPU (tests)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            else:
+                dist.init_process_group(backend)
         dev = torch.device("cuda", local_rank)
         torch.cuda.set_device(dev)
     if world > 1:
