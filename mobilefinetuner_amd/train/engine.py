@@ -27,7 +27,8 @@ class TrainStep:
         self.model, self.flat, self.opt = model, flat, opt
         self.accum = max(1, int(grad_accum))
         self.dp = dp
-        self.use_graph = use_graph
+        # a reducer whose step can only be captured with its collectives (ZeRO-3) may veto the graph
+        self.use_graph = use_graph and (dp is None or not hasattr(dp, "graph_ok") or dp.graph_ok())
         # graph_comm: the gradient reduction and the optimizer step are recorded into the hipGraph
         # too (the reducer's collectives then overlap the captured backward); default: as the
         # reducer asks (multi-bucket RCCL data parallelism, ZeRO-3)
