@@ -75,6 +75,7 @@ APPS = {
     "gpt2_full_finetune": ("gpt2_finetune.cpp", ["-DMFT_FULL_FT=1"]),
     "engine_selftest": ("engine_selftest.cpp", []),
     "eval_ppl": ("eval_ppl.cpp", []),
+    "train_lora_gemma": ("train_lora_gemma.cpp", []),
 }
 
 

@@ -200,45 +200,10 @@ int run(int argc, char** argv) {
   vc.drop_last = false;
   vc.shuffle = false;
   TokenDataset train(dc), valid(vc);
-  bool have_valid = true;
-  const std::string ddir = a.get("data_dir"), pt = a.get("pretokenized_path");
-  if (!pt.empty()) {
-    std::string meta = a.get("pretokenized_meta");
-    if (meta.empty()) meta = pt.substr(0, pt.rfind('/') + 1) + "meta.json";
-    PretokMeta m = read_pretok_meta(meta);
-    train.set_tokens(read_pretok_split(pt, m, 0, dc.data_fraction, seq));
-    if (m.len[1] > 0) valid.set_tokens(read_pretok_split(pt, m, 1, 1.f, seq));
-    else have_valid = false;
-    std::printf("  pretokenized stream %s\n", pt.c_str());
-  } else if (a.b("synthetic_data") || ddir.empty()) {
-    const int64_t n = a.l("synthetic_tokens", 2000000);
-    auto gen = [&](int64_t count, uint64_t s) {
-      std::vector<int32_t> v(count);
-      uint64_t z = s;
-      for (int64_t i = 0; i < count; ++i) {
-        z += 0x9E3779B97F4A7C15ull;
-        uint64_t x = z;
-        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-        v[i] = (int32_t)((x ^ (x >> 31)) % (uint64_t)cfg.vocab_size);
-      }
-      return v;
-    };
-    train.set_tokens(gen(n, seed));
-    valid.set_tokens(gen(std::max<int64_t>(n / 20, 4 * seq), seed + 1));
-    std::printf("  (synthetic token data, %lld tokens)\n", (long long)n);
-  } else {
-    const char* tr_names[] = {"wiki.train.raw", "wiki.train.tokens", "train.txt", nullptr};
-    const char* va_names[] = {"wiki.valid.raw", "wiki.valid.tokens", "valid.txt", "validation.txt", nullptr};
-    auto tok = ByteLevelBPE::from_files(pdir + "/vocab.json", pdir + "/merges.txt");
-    auto enc = [&](const std::string& s) { return tok->encode(s); };
-    const int threads = std::max(1u, std::thread::hardware_concurrency());
-    const std::string ftr = split_file(ddir, tr_names), fva = split_file(ddir, va_names);
-    if (ftr.empty()) throw std::runtime_error("no train split under " + ddir);
-    train.set_tokens(pack_lines(read_lines(ftr, true), enc, dc.eos_id, true, dc.data_fraction, seq, threads));
-    if (!fva.empty()) valid.set_tokens(pack_lines(read_lines(fva, true), enc, dc.eos_id, true, 1.f, seq, threads));
-    else have_valid = false;
-  }
+  const bool have_valid = mft::apps::load_token_splits(a, dc, cfg.vocab_size, train, valid, [&]() -> mft::apps::Encoder {
+    std::shared_ptr<ByteLevelBPE> tok = ByteLevelBPE::from_files(pdir + "/vocab.json", pdir + "/merges.txt");
+    return [tok](const std::string& s) { return tok->encode(s); };
+  });
   std::printf("  train: %zu sequences | valid: %zu sequences\n", train.num_sequences(),
               have_valid ? valid.num_sequences() : (size_t)0);
 
@@ -265,23 +230,7 @@ int run(int argc, char** argv) {
   tc.use_graph = !a.b("no_graph");
   tc.eval_out = a.get("eval_out");
   tc.metrics_out = a.get("metrics_out");
-  std::unique_ptr<PowerMonitor> pm;
-  if (a.i("pm_interval", 0) > 0 || !a.get("pm_schedule").empty()) {
-    PowerConfig pc;
-    pc.check_interval_steps = a.i("pm_interval", 0);
-    pc.battery_threshold = a.f("pm_batt_thresh", 20.f);
-    pc.temp_threshold = a.f("pm_temp_thresh", 42.f);
-    pc.freq_b_high = a.f("pm_fb_high", 2.f);
-    pc.freq_b_low = a.f("pm_fb_low", 0.5f);
-    pc.freq_t_high = a.f("pm_ft_high", 2.f);
-    pc.freq_t_low = a.f("pm_ft_low", 0.5f);
-    pc.enable_battery = !a.b("pm_disable_batt");
-    pc.enable_temp = !a.b("pm_disable_temp");
-    pc.use_gpu_telemetry = a.b("pm_gpu_telemetry");
-    pm = std::make_unique<PowerMonitor>(pc);
-    pm->set_manual_readings(a.f("pm_manual_batt", 100.f), a.f("pm_manual_temp", 30.f));
-    if (!a.get("pm_schedule").empty()) pm->set_step_schedule(PowerMonitor::parse_schedule(a.get("pm_schedule")));
-  }
+  std::unique_ptr<PowerMonitor> pm = mft::apps::power_monitor_from(a);
   Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get());
   const std::string lora_out = a.get("lora_out"), out_path = a.get("output_path");
   auto save = [&](int64_t step) {

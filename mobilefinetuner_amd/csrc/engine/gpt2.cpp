@@ -91,15 +91,7 @@ void GPT2::alloc() {
     b.mproj_b = frozen(zeros({C}, DType::BF16));
   }
   dropout_ctr = zeros({1}, DType::I64);
-  // LM-head CE chunk: rows per fused call (one [rows, Vpad] bf16 E workspace), 32 GiB budget (MFT_CE_BUDGET_GB)
-  const char* env = std::getenv("MFT_CE_CHUNK");
-  if (env) {
-    ce_chunk = std::atoll(env);
-  } else {
-    const double gb = std::getenv("MFT_CE_BUDGET_GB") ? std::atof(std::getenv("MFT_CE_BUDGET_GB")) : 32.0;
-    const int64_t rows = (int64_t)(gb * (1ull << 30) / (2.0 * cfg_.vocab_padded()));
-    ce_chunk = std::max<int64_t>(64, std::min<int64_t>(65536, rows / 64 * 64));
-  }
+  ce_chunk = default_ce_chunk(cfg_.vocab_padded());
 }
 
 void GPT2::init_random(uint64_t seed) {
@@ -263,30 +255,6 @@ size_t GPT2::num_parameters() const {
 }
 
 // ------------------------------------------------------------------ LoRA
-namespace {
-LoraAdapter make_adapter(int col0, int n, int in, int r, const Tensor& A_init, float dropout, const std::string& name) {
-  LoraAdapter a;
-  a.col0 = col0;
-  a.ncols = n;
-  a.rank = r;
-  a.dropout = dropout;
-  uint32_t h = 2166136261u;  // FNV-1a of the adapter name: stable dropout salt
-  for (char c : name) h = (h ^ (uint8_t)c) * 16777619u;
-  a.salt = h;
-  NoGradGuard ng;
-  Tensor A = A_init.to(DType::F32).contiguous().clone();
-  A.requires_grad_(true);
-  Tensor B = zeros({r, n}, DType::F32);
-  B.requires_grad_(true);
-  a.A.leaf = A;
-  a.A.c = A.to(DType::BF16);
-  a.B.leaf = B;
-  a.B.c = B.to(DType::BF16);
-  (void)in;
-  return a;
-}
-}  // namespace
-
 void GPT2::inject_lora(const LoraSpec& spec) {
   spec_ = spec;
   lora_ = true;
@@ -302,7 +270,7 @@ void GPT2::inject_lora(const LoraSpec& spec) {
       // reference init (graph/lora_injector.cpp:70-85): A[in, r] ~ U(+-sqrt(6/(in+r))), seed 42+in+out
       const float bound = std::sqrt(6.f / (float)(in + spec.rank));
       Tensor A = rand_uniform({in, spec.rank}, spec.seed + in + n, -bound, bound, DType::F32).t();
-      ads.push_back(make_adapter(col0, n, in, spec.rank, A, spec.dropout, pre + nm));
+      ads.push_back(make_adapter(col0, n, spec.rank, A, spec.dropout, pre + nm));
       names.push_back(pre + nm);
     };
     if (spec.has("AttnQKV")) {

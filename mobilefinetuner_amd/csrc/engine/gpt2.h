@@ -12,7 +12,7 @@
 #include <string>
 #include <vector>
 
-#include "engine/nn.h"
+#include "engine/lm.h"
 
 namespace mft {
 namespace eng {
@@ -44,7 +44,7 @@ struct GPT2Block {
   Tensor waug_qkv, waug_proj;  // augmented weights of the LoRA'd attention projections
 };
 
-class GPT2 {
+class GPT2 : public LanguageModel {
  public:
   explicit GPT2(const GPT2Config& cfg);
   const GPT2Config& cfg() const { return cfg_; }
@@ -60,18 +60,15 @@ class GPT2 {
   void save_lora(const std::string& path);  // byte-compatible with graph/lora_saver.cpp
   void set_full_finetune();                 // every parameter trainable (fp32 master + bf16 shadow)
   // trainable parameters in a fixed order (name, param)
-  std::vector<std::pair<std::string, Param*>> trainable();
+  std::vector<std::pair<std::string, Param*>> trainable() override;
   std::vector<std::pair<std::string, Param*>> all_params();
   // mean token NLL of one micro-batch (ids / labels [B, S], labels already shifted, -100 ignored)
-  Tensor loss(const Tensor& ids, const Tensor& labels, float w_grad_scale = 1.f);
-  std::pair<Tensor, Tensor> nll(const Tensor& ids, const Tensor& labels);  // (sum, count), no grad
+  Tensor loss(const Tensor& ids, const Tensor& labels, float w_grad_scale = 1.f) override;
+  std::pair<Tensor, Tensor> nll(const Tensor& ids, const Tensor& labels) override;  // (sum, count), no grad
   Tensor hidden(const Tensor& ids);
   void merge_lora(float sign);
-  bool training = true;
-  Tensor dropout_ctr;  // device int64 step counter (fresh LoRA-dropout masks per step)
-  int64_t ce_chunk = 0;
   const LoraSpec& lora_spec() const { return spec_; }
-  size_t num_parameters() const;
+  size_t num_parameters() const override;
 
  private:
   void alloc();

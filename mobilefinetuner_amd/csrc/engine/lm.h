@@ -1,0 +1,43 @@
+// libmft engine: the interface the Trainer drives (GPT-2 and Gemma-3 implement it).
+//
+// Reference: the reference has one trainer per family (gpt2_lora_finetune/main.cpp:561-684 for
+// GPT-2, GemmaLoRATrainer optim/gemma_trainer.cpp:18-233 for Gemma); here one Trainer (engine/trainer.h)
+// runs either model through this interface: a mean-token-NLL loss with autograd, an eval NLL sum
+// without it, the trainable parameters in checkpoint order, the LoRA-dropout step counter.
+#pragma once
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "engine/nn.h"
+
+namespace mft {
+namespace eng {
+
+class LanguageModel {
+ public:
+  virtual ~LanguageModel() = default;
+  // mean token NLL of one micro-batch (ids / labels [B, S], labels already shifted, -100 ignored);
+  // a trainable tied embedding's gradient is produced inside the CE scaled by w_grad_scale
+  virtual Tensor loss(const Tensor& ids, const Tensor& labels, float w_grad_scale = 1.f) = 0;
+  // (sum of token NLL, number of valid tokens) without gradients -- evaluation
+  virtual std::pair<Tensor, Tensor> nll(const Tensor& ids, const Tensor& labels) = 0;
+  virtual std::vector<std::pair<std::string, Param*>> trainable() = 0;
+  virtual size_t num_parameters() const = 0;
+  bool training = true;
+  Tensor dropout_ctr;    // device int64 step counter (fresh LoRA-dropout masks per step)
+  int64_t ce_chunk = 0;  // LM-head CE rows per fused call (default_ce_chunk)
+};
+
+// rows of the fused LM-head CE per call: one [rows, Vpad] bf16 E workspace within a 32 GiB budget
+// (MFT_CE_BUDGET_GB; MFT_CE_CHUNK overrides), at most 65536 rows (ops/functional.default_ce_chunk)
+int64_t default_ce_chunk(int vocab_padded);
+
+// FNV-1a of an adapter's checkpoint name: its stable LoRA-dropout salt
+uint32_t adapter_salt(const std::string& name);
+// LoRA adapter over output columns [col0, col0 + n) of a frozen Linear: A [r, in] = A_init (fp32
+// master + bf16 shadow), B [r, n] = 0
+LoraAdapter make_adapter(int col0, int n, int r, const Tensor& A_init, float dropout, const std::string& name);
+
+}  // namespace eng
+}  // namespace mft

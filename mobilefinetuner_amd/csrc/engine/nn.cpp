@@ -1,12 +1,15 @@
 // libmft engine: fused transformer ops (see nn.h).
 #include "engine/nn.h"
 
+#include <cstring>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
 #include "engine/autograd.h"
 #include "engine/gemm.h"
+#include "engine/lm.h"
 #include "engine/ops.h"
 #include "kernels.h"
 
@@ -38,6 +41,40 @@ const Tensor& Param::transposed() {
     wt = c.t().contiguous();
   }
   return wt;
+}
+
+// ------------------------------------------------------------------ model helpers (lm.h)
+int64_t default_ce_chunk(int vocab_padded) {
+  if (const char* env = std::getenv("MFT_CE_CHUNK")) return std::atoll(env);
+  const char* gbs = std::getenv("MFT_CE_BUDGET_GB");
+  const double gb = gbs ? std::atof(gbs) : 32.0;
+  const int64_t rows = (int64_t)(gb * (1ull << 30) / (2.0 * vocab_padded));
+  return std::max<int64_t>(64, std::min<int64_t>(65536, rows / 64 * 64));
+}
+
+uint32_t adapter_salt(const std::string& name) {
+  uint32_t h = 2166136261u;
+  for (char c : name) h = (h ^ (uint8_t)c) * 16777619u;
+  return h;
+}
+
+LoraAdapter make_adapter(int col0, int n, int r, const Tensor& A_init, float dropout, const std::string& name) {
+  LoraAdapter a;
+  a.col0 = col0;
+  a.ncols = n;
+  a.rank = r;
+  a.dropout = dropout;
+  a.salt = adapter_salt(name);
+  NoGradGuard ng;
+  Tensor A = A_init.to(DType::F32).contiguous().clone();
+  A.requires_grad_(true);
+  Tensor B = zeros({r, n}, DType::F32);
+  B.requires_grad_(true);
+  a.A.leaf = A;
+  a.A.c = A.to(DType::BF16);
+  a.B.leaf = B;
+  a.B.c = B.to(DType::BF16);
+  return a;
 }
 
 // ------------------------------------------------------------------ norms
@@ -233,6 +270,157 @@ Tensor attention_packed(const Tensor& qkv, float scale, bool causal, int window,
     connect(n, {qkv}, {o_full});
   }
   return o_full;
+}
+
+// ------------------------------------------------------------------ Gemma-3 attention core
+Tensor qknorm_rope_attention(const Tensor& qkv, int nq, int nkv, Param& wq, Param& wk, const Tensor& cos_t,
+                             const Tensor& sin_t, float eps, float offset, bool interleaved, float scale, int window,
+                             int out_cols) {
+  MFT_CHECK(qkv.dim() == 4 && qkv.dtype() == DType::BF16 && qkv.size(2) == nq + 2 * nkv,
+            "qknorm_rope_attention: qkv [B, S, nq + 2 nkv, D] bf16");
+  MFT_CHECK(nkv > 0 && nq % nkv == 0, "qknorm_rope_attention: nq must be a multiple of nkv");
+  const int B = (int)qkv.size(0), Sq = (int)qkv.size(1), D = (int)qkv.size(3);
+  MFT_CHECK(D == 64 || D == 128 || D == 256, "qknorm_rope_attention: head dim 64 / 128 / 256");
+  MFT_CHECK(cos_t.size(0) >= Sq && cos_t.size(1) == D / 2, "qknorm_rope_attention: RoPE tables too short");
+  Tensor qd = qkv.detach();
+  Tensor xq = qd.slice(2, 0, nq), xk = qd.slice(2, nq, nq + nkv), v = qd.slice(2, nq + nkv, nq + 2 * nkv);
+  Tensor wq32 = f32_of(wq), wk32 = f32_of(wk);
+  // normalised + rotated q / k (contiguous [B, S, h, D]) and their per-(row, head) rstd
+  Tensor q = empty({B, Sq, nq, D}, DType::BF16, qkv.device()), k = empty({B, Sq, nkv, D}, DType::BF16, qkv.device());
+  Tensor rq = empty({(int64_t)B * Sq * nq}, DType::F32, qkv.device());
+  Tensor rk = empty({(int64_t)B * Sq * nkv}, DType::F32, qkv.device());
+  long st[3];
+  fill_st(st, xq);
+  ::mft::qknorm_rope_fwd(bp(xq), st, bp(q), fp(rq), fp(wq32), B, Sq, nq, D, fp(cos_t), fp(sin_t), 0, eps, offset,
+                         interleaved, S());
+  fill_st(st, xk);
+  ::mft::qknorm_rope_fwd(bp(xk), st, bp(k), fp(rk), fp(wk32), B, Sq, nkv, D, fp(cos_t), fp(sin_t), 0, eps, offset,
+                         interleaved, S());
+  const int HD = nq * D;
+  const int oc = out_cols > HD ? out_cols : HD;
+  Tensor o_full = empty({B, Sq, (int64_t)oc}, DType::BF16, qkv.device());
+  Tensor o = o_full.slice(2, 0, HD).view({B, Sq, nq, D});
+  Tensor lse = empty({B, nq, Sq}, DType::F32, qkv.device());
+  ::mft::AttnArgs a{};
+  a.q = bp(q);
+  a.k = bp(k);
+  a.v = bp(v);
+  a.o = bp(o);
+  a.lse = fp(lse);
+  fill_st(a.q_st, q);
+  fill_st(a.k_st, k);
+  fill_st(a.v_st, v);
+  fill_st(a.o_st, o);
+  a.B = B;
+  a.H = nq;
+  a.Hkv = nkv;
+  a.Sq = Sq;
+  a.Sk = Sq;
+  a.D = D;
+  a.scale = scale;
+  a.causal = 1;
+  a.window = window;
+  ::mft::attn_fwd(a, S());
+  if (oc > HD) ::mft::zero_cols(bp(o_full), oc, (long)B * Sq, HD, oc - HD, S());
+  if (any_needs_grad({qkv, wq.leaf, wk.leaf})) {
+    Param *pq = &wq, *pk = &wk;
+    auto n = lambda_node("QKNormRoPEAttentionBackward", [qd, q, k, o, lse, rq, rk, wq32, wk32, cos_t, sin_t, pq, pk,
+                                                         nq, nkv, B, Sq, D, HD, scale, window, offset,
+                                                         interleaved](std::vector<Tensor>& g) {
+      std::vector<Tensor> out(3);
+      if (!g[0].defined()) return out;
+      Tensor dqkv = empty(qd.shape(), DType::BF16, qd.device());
+      Tensor dout = g[0].slice(2, 0, HD).view({B, Sq, nq, D});
+      if (dout.stride(3) != 1 || dout.stride(1) % 8) dout = dout.contiguous();
+      const int path = ::mft::attn_bwd_path(D, Sq, Sq, window);
+      Tensor delta, dq_acc, dk_tmp, dv_tmp;
+      if (path != 0) delta = empty({B, nq, Sq}, DType::F32, qd.device());
+      if (path == 1) dq_acc = empty({B, Sq, nq, D}, DType::F32, qd.device());
+      // dQ / dK of the rotated normalised q / k (the norm-RoPE backward reads them), dV in place
+      Tensor dq = empty({B, Sq, nq, D}, DType::BF16, qd.device()), dk = empty({B, Sq, nkv, D}, DType::BF16, qd.device());
+      Tensor v = qd.slice(2, nq + nkv, nq + 2 * nkv), dv = dqkv.slice(2, nq + nkv, nq + 2 * nkv);
+      ::mft::AttnBwdArgs b{};
+      if (nq != nkv && path != 2) {
+        dk_tmp = empty({B, Sq, nq, D}, DType::BF16, qd.device());
+        dv_tmp = empty({B, Sq, nq, D}, DType::BF16, qd.device());
+        b.dk_tmp = bp(dk_tmp);
+        b.dv_tmp = bp(dv_tmp);
+        fill_st(b.tmp_st, dk_tmp);
+      }
+      b.q = bp(q);
+      b.k = bp(k);
+      b.v = bp(v);
+      b.o = bp(o);
+      b.dout = bp(dout);
+      b.lse = fp(lse);
+      b.delta = path != 0 ? fp(delta) : nullptr;
+      b.dq_acc = path == 1 ? fp(dq_acc) : nullptr;
+      b.dq = bp(dq);
+      b.dk = bp(dk);
+      b.dv = bp(dv);
+      fill_st(b.q_st, q);
+      fill_st(b.k_st, k);
+      fill_st(b.v_st, v);
+      fill_st(b.o_st, o);
+      fill_st(b.do_st, dout);
+      fill_st(b.dq_st, dq);
+      fill_st(b.dk_st, dk);
+      fill_st(b.dv_st, dv);
+      b.B = B;
+      b.H = nq;
+      b.Hkv = nkv;
+      b.Sq = Sq;
+      b.Sk = Sq;
+      b.D = D;
+      b.scale = scale;
+      b.causal = 1;
+      b.window = window;
+      ::mft::attn_bwd(b, S());
+      // q / k norm-RoPE backward straight into their dqkv slices (+ norm-weight grads if trainable)
+      auto nr_bwd = [&](int h0, int nh, const Tensor& dy, const Tensor& r, const Tensor& w32, Param* pw) {
+        Tensor x = qd.slice(2, h0, h0 + nh), dx = dqkv.slice(2, h0, h0 + nh);
+        Tensor dw = gbuf(pw), work;
+        if (dw.defined()) work = empty({(int64_t)::mft::qknorm_rope_bwd_blocks((long)B * Sq * nh) * D}, DType::F32, qd.device());
+        long xs[3], ds[3];
+        fill_st(xs, x);
+        fill_st(ds, dx);
+        ::mft::qknorm_rope_bwd(bp(x), xs, bp(dy), fp(r), fp(w32), bp(dx), ds, fp_or_null(dw), fp_or_null(work), B, Sq,
+                               nh, D, fp(cos_t), fp(sin_t), 0, offset, interleaved, 1, S());
+      };
+      nr_bwd(0, nq, dq, rq, wq32, pq);
+      nr_bwd(nq, nkv, dk, rk, wk32, pk);
+      out[0] = dqkv;
+      return out;
+    });
+    connect(n, {qkv, wq.leaf, wk.leaf}, {o_full});
+  }
+  return o_full;
+}
+
+// ------------------------------------------------------------------ gated MLP activation
+Tensor gated_act(const Tensor& gu, int act, int out_cols) {
+  const int64_t I2 = gu.size(-1), I = I2 / 2;
+  MFT_CHECK(gu.dtype() == DType::BF16 && I2 % 16 == 0, "gated_act: bf16 [M, 2I], I % 8 == 0");
+  Tensor g2 = gu.detach().reshape({-1, I2}).contiguous();
+  const int64_t M = g2.size(0);
+  const int64_t oc = out_cols > I ? out_cols : I;
+  MFT_CHECK(oc % 8 == 0, "gated_act: out_cols % 8");
+  Tensor y = empty({M, oc}, DType::BF16, gu.device());
+  ::mft::gated_fwd(bp(g2), bp(y), M, (int)I, oc, act, S());
+  if (oc > I) ::mft::zero_cols(bp(y), oc, M, (int)I, (int)(oc - I), S());
+  if (needs_grad(gu)) {
+    Shape gshape = gu.shape();
+    auto n = lambda_node("GatedActBackward", [g2, gshape, M, I, act](std::vector<Tensor>& g) {
+      if (!g[0].defined()) return std::vector<Tensor>{Tensor()};
+      Tensor dy = g[0];
+      if (dy.stride(1) != 1 || dy.stride(0) % 8) dy = dy.contiguous();
+      Tensor dgu = empty({M, 2 * I}, DType::BF16, dy.device());
+      ::mft::gated_bwd(bp(g2), bp(dy), dy.stride(0), bp(dgu), M, (int)I, act, S());
+      return std::vector<Tensor>{dgu.view(gshape)};
+    });
+    connect(n, {gu}, {y});
+  }
+  return y;
 }
 
 // ------------------------------------------------------------------ linear / MLP

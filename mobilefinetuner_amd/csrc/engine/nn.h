@@ -40,6 +40,17 @@ Tensor embed(const Tensor& ids, Param& wte, Param* wpe, float scale);
 // qkv [B, S, 3, H, D] -> o [B, S, H*D] (or [B, S, out_cols] with zeroed tail when out_cols > H*D)
 Tensor attention_packed(const Tensor& qkv, float scale, bool causal, int window, int out_cols);
 Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2);
+// Gemma-3 attention core on the packed q|k|v projection qkv [B, S, nq + 2 nkv, D]: per-head
+// RMSNorm(offset + w) of q and k + RoPE (cos / sin [>= S, D/2] fp32 tables), then causal GQA flash
+// attention (sliding window when window > 0).  O [B, S, nq*D] (or [B, S, out_cols], zeroed tail).
+// One node owns the three slices: its backward writes ONE packed dqkv (dV by the attention
+// backward, dQ / dK by the norm-RoPE backward kernels into their slices).
+Tensor qknorm_rope_attention(const Tensor& qkv, int nq, int nkv, Param& wq, Param& wk, const Tensor& cos_t,
+                             const Tensor& sin_t, float eps, float offset, bool interleaved, float scale, int window,
+                             int out_cols);
+// gated MLP activation on gu = [gate | up] [M, 2I]: act(gate) * up (act 0 GELU-tanh = GeGLU, 1 SiLU);
+// [M, out_cols] with zeroed tail when out_cols > I (augmented-K input of a LoRA consumer)
+Tensor gated_act(const Tensor& gu, int act, int out_cols);
 // y = x W^T + b on bf16 [M, K] rows (trainable or frozen W)
 Tensor linear_p(const Tensor& x, Param& w, Param* b);
 

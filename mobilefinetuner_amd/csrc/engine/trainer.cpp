@@ -14,7 +14,7 @@
 namespace mft {
 namespace eng {
 
-Trainer::Trainer(GPT2& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid,
+Trainer::Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid,
                  const TrainConfig& cfg, PowerMonitor* pm, Communicator* comm)
     : model_(model), flat_(flat), opt_(opt), train_(train), valid_(valid), cfg_(cfg), pm_(pm), comm_(comm) {
   stream_ = current_stream();
@@ -164,7 +164,7 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
   auto t_last = std::chrono::steady_clock::now();
   int64_t tok_since = 0, steps_since = 0;
   for (int64_t it = 0; it < total_steps_; ++it) {
-    const float lr = gpt2_cli_lr(it, cfg_.lr, cfg_.warmup, total_steps_);
+    const float lr = cfg_.lr_fn ? cfg_.lr_fn(it, total_steps_) : gpt2_cli_lr(it, cfg_.lr, cfg_.warmup, total_steps_);
     opt_.set_lr(lr);
     std::vector<std::pair<const int64_t*, const int64_t*>> micro;
     int64_t tokens = 0;

@@ -19,7 +19,7 @@
 #include <vector>
 
 #include "engine/comm.h"
-#include "engine/gpt2.h"
+#include "engine/lm.h"
 #include "engine/optim.h"
 #include "runtime/dataset.h"
 #include "runtime/power_monitor.h"
@@ -38,11 +38,13 @@ struct TrainConfig {
   bool use_graph = true;
   std::string eval_out, metrics_out;
   int pm_interval = 0;
+  // learning rate of 0-indexed update `it` of `total`; unset: the GPT-2 CLI schedule (gpt2_cli_lr)
+  std::function<float(int64_t it, int64_t total)> lr_fn;
 };
 
 class Trainer {
  public:
-  Trainer(GPT2& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid, const TrainConfig& cfg,
+  Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid, const TrainConfig& cfg,
           PowerMonitor* pm = nullptr, Communicator* comm = nullptr);
   ~Trainer();
   int64_t total_steps() const { return total_steps_; }
@@ -64,7 +66,7 @@ class Trainer {
   void reduce_grads();
   void capture();
   bool lead() const { return !comm_ || comm_->rank() == 0; }
-  GPT2& model_;
+  LanguageModel& model_;
   FlatParams& flat_;
   AdamW& opt_;
   TokenDataset& train_;

@@ -1,0 +1,143 @@
+"""Native Gemma-3 on the libmft engine (mobilefinetuner_amd/bin/train_lora_gemma) on the GPU.
+
+* Python-path parity: the native CLI and the PyTorch-driven package train the SAME random-init
+  Gemma-3 (gemma3-tiny shapes: GQA 4:2, D = 64, sliding + global layers) with LoRA on all seven
+  projections (weights / adapter exchanged through the HF and reference Gemma LoRA safetensors
+  layouts) on the SAME pretokenized batches; per-step losses and the applied adapter update agree.
+* The adapter the native CLI writes is byte-identical to the Python writer's file.
+* Real Gemma-3-270M shapes (D = 256, GQA 4:1, sliding 512, V = 262144, LoRA dropout on) train
+  natively: finite per-step losses starting near ln(V).
+"""
+import json
+import math
+import os
+import subprocess
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "mobilefinetuner_amd", "bin")
+
+
+def _bin(name):
+    p = os.path.join(BIN, name)
+    if not os.path.exists(p):
+        pytest.fail(f"{p} missing: run python -m mobilefinetuner_amd._build")
+    return p
+
+
+def _fixture(tmp, S=64, n_tokens=200_000):
+    from mobilefinetuner_amd.data.wikitext2 import write_pretokenized
+    from mobilefinetuner_amd.io import safetensors as st
+    from mobilefinetuner_amd.io.lora_checkpoint import save_lora
+    from mobilefinetuner_amd.models.gemma3 import Gemma3Config, Gemma3Model
+    from mobilefinetuner_amd.models.hf_io import export_gemma_state
+    from mobilefinetuner_amd.peft.lora import LoraSpec, inject_gemma, parse_gemma_targets
+
+    cfg = Gemma3Config.preset("gemma3-tiny")
+    model = Gemma3Model(cfg, device="cuda", seed=1234)
+    g = torch.Generator().manual_seed(5)
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            if p.dim() == 1:  # RMSNorm(1 + w) weights away from zero
+                p.copy_((torch.randn(p.shape, generator=g) * 0.1).to(p.device))
+    inject_gemma(model, LoraSpec(rank=8, alpha=32, dropout=0.0, targets=parse_gemma_targets("full"), init="peft"))
+    with torch.no_grad():
+        for m in model.modules():
+            for sl in getattr(m, "lora_slices", []):
+                sl.B.copy_(((torch.rand(sl.B.shape, generator=g) - 0.5) * 0.05).cuda())
+                if getattr(sl.B, "shadow", None) is not None:
+                    sl.B.shadow.copy_(sl.B.to(sl.B.shadow.dtype))
+    os.makedirs(tmp, exist_ok=True)
+    st.save_file(os.path.join(tmp, "model.safetensors"), export_gemma_state(model))
+    with open(os.path.join(tmp, "config.json"), "w") as f:
+        json.dump(cfg.to_dict(), f)
+    lora = os.path.join(tmp, "lora_init.safetensors")
+    save_lora(lora, model)
+    toks = torch.randint(0, 200, (n_tokens,), generator=g, dtype=torch.int32)  # learnable: 200 of 1024 ids
+    write_pretokenized(tmp, {"train": toks, "valid": toks[: 40 * (S + 1)]}, eos_id=cfg.eos_token_id,
+                       pad_id=cfg.pad_token_id, vocab_size=cfg.vocab_size)
+    return model, lora
+
+
+def _python_losses(model, tmp, steps, B, S, lr, ratio):
+    from mobilefinetuner_amd.data.wikitext2 import LMDataset, WT2Config
+    from mobilefinetuner_amd.optim.adamw import FusedAdamW
+    from mobilefinetuner_amd.optim.schedules import gemma_lr
+    from mobilefinetuner_amd.peft.lora import lora_parameters
+    from mobilefinetuner_amd.train.engine import TrainStep
+    from mobilefinetuner_amd.utils.params import FlatParams
+
+    ds = LMDataset.from_pretokenized(WT2Config(pretokenized_path=os.path.join(tmp, "tokens.bin"), seq_len=S,
+                                               seed=42), "train")
+    flat = FlatParams(lora_parameters(model), "cuda")
+    opt = FusedAdamW(flat, lr=lr, weight_decay=0.0, max_grad_norm=1.0)
+    step = TrainStep(model, flat, opt, use_graph=True)
+    out = []
+    for i in range(steps):
+        opt.set_lr(gemma_lr(i + 1, lr, ratio, steps))
+        b = ds.next_batch(B)
+        out.append(float(step([(b["input_ids"].cuda(), b["targets"].cuda())]).item()))
+    return out
+
+
+def test_native_gemma_matches_python_path(tmp_path):
+    S, B, steps, lr, ratio = 64, 8, 10, 2e-3, 0.2
+    tmp = str(tmp_path)
+    model, lora = _fixture(tmp, S)
+    py = _python_losses(model, tmp, steps, B, S, lr, ratio)
+    metrics = os.path.join(tmp, "native.jsonl")
+    out_dir = os.path.join(tmp, "native_out")
+    cmd = [_bin("train_lora_gemma"), "--model_dir", tmp, "--resume_from", lora, "--pretokenized_path",
+           os.path.join(tmp, "tokens.bin"), "--max_steps", str(steps), "--batch", str(B), "--seq_len", str(S),
+           "--lr", str(lr), "--warmup_ratio", str(ratio), "--log_interval", "1", "--metrics_out", metrics,
+           "--output_dir", out_dir, "--eval_batches", "4"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    print(r.stdout[-3000:], r.stderr[-2000:])
+    assert r.returncode == 0
+    nat = [json.loads(line)["loss"] for line in open(metrics)]
+    print("python:", py)
+    print("native:", nat)
+    assert len(nat) == steps
+    for a, b in zip(py, nat):
+        assert abs(a - b) < 3e-3, (py, nat)
+    assert nat[-1] < nat[0] - 0.02, nat
+    from mobilefinetuner_amd.io import safetensors as st
+    from mobilefinetuner_amd.io.lora_checkpoint import lora_state
+    init, mine = st.load_file(lora), lora_state(model)[0]
+    theirs = st.load_file(os.path.join(out_dir, "gemma_lora.safetensors"))
+    assert sorted(mine) == sorted(theirs) and len(mine) == 3 * 7 * 2
+    num = den = 0.0
+    for k in mine:
+        d_py, d_nat = mine[k].float() - init[k].float(), theirs[k].float() - init[k].float()
+        num += float((d_py - d_nat).pow(2).sum())
+        den += float(d_py.pow(2).sum())
+    assert den > 0 and (num / den) ** 0.5 < 0.05, (num / den) ** 0.5
+
+
+def test_native_gemma_lora_checkpoint_bytes_match_python(tmp_path):
+    tmp = str(tmp_path)
+    _, lora = _fixture(tmp, n_tokens=20_000)
+    out_dir = os.path.join(tmp, "o")
+    r = subprocess.run([_bin("train_lora_gemma"), "--model_dir", tmp, "--resume_from", lora, "--pretokenized_path",
+                        os.path.join(tmp, "tokens.bin"), "--epochs", "0", "--max_steps", "0", "--seq_len", "64",
+                        "--output_dir", out_dir, "--eval_batches", "1"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    with open(lora, "rb") as f, open(os.path.join(out_dir, "gemma_lora.safetensors"), "rb") as g:
+        assert f.read() == g.read()
+
+
+def test_native_gemma270m_trains():
+    V = 262144
+    r = subprocess.run([_bin("train_lora_gemma"), "--random_init", "--model", "gemma3-270m", "--synthetic_data",
+                        "--synthetic_tokens", "300000", "--max_steps", "6", "--batch", "8", "--seq_len", "256",
+                        "--lr", "2e-3", "--warmup_ratio", "0", "--lora_dropout", "0.1", "--log_interval", "1",
+                        "--eval_batches", "2"], capture_output=True, text=True, timeout=300)
+    print(r.stdout[-3000:], r.stderr[-2000:])
+    assert r.returncode == 0
+    losses = [float(line.split("Loss=")[1].split()[0]) for line in r.stdout.splitlines() if "Loss=" in line]
+    assert len(losses) == 6 and all(math.isfinite(x) for x in losses)
+    assert abs(losses[0] - math.log(V)) < 1.0, losses
