@@ -83,6 +83,11 @@ def main(argv=None):
             merge_all(model)
             set_lora_enabled(model, False)
             log0("  ✓ LoRA merged into base weights")
+        elif dev.type == "cuda":
+            # separate adapters: the fp32 A / B need their bf16 compute shadows (FlatParams)
+            from ..peft.lora import lora_parameters
+            from ..utils.params import FlatParams
+            model._lora_flat = FlatParams(lora_parameters(model), dev)
     if a.model_type == "gemma":
         eos = model.cfg.eos_token_id
     else:

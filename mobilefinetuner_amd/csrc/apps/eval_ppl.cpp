@@ -1,4 +1,4 @@
-// Native CLI `eval_ppl` (GPT-2) on the libmft engine: token-weighted perplexity of a WikiText-2
+// Native CLI `eval_ppl` (GPT-2, or Gemma-3 with --model_type gemma) on the libmft engine: token-weighted perplexity of a WikiText-2
 // split with the fused LM head (per-tile softmax statistics in the GEMM epilogue; no logits are
 // stored), optional LoRA adapter (merged into the weights by default), data-parallel over RCCL
 // ranks (each rank scores its shard; the sums are all-reduced).
@@ -6,7 +6,9 @@
 // Reference: gpt2_lora_finetune/eval_ppl.cpp:67-231 (flags --data_root --split --seq_len --batch_size
 // --pretrained_dir --lora_path --lora_merge --out --log_every; non-overlapping seq_len windows, mean
 // NLL over the predicted tokens, PPL = exp(NLL)).  Extras: --model P --random_init --synthetic_data
-// --synthetic_tokens N --pretokenized_path F --pretokenized_meta F --max_batches N.
+// --synthetic_tokens N --pretokenized_path F --pretokenized_meta F --max_batches N --model_type gpt2|gemma
+// (the Python CLI's flag; Gemma reads config.json / model.safetensors / tokenizer.json from
+// --pretrained_dir and the reference Gemma adapter layout).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -22,6 +24,7 @@
 #include "apps/app_common.h"
 #include "engine/autograd.h"
 #include "engine/comm.h"
+#include "engine/gemma3.h"
 #include "engine/gpt2.h"
 #include "runtime/dataset.h"
 #include "runtime/tokenizer.h"
@@ -35,7 +38,8 @@ namespace {
 const std::set<std::string> kBool = {"random_init", "synthetic_data", "debug", "help"};
 const std::set<std::string> kValued = {"data_root", "split", "seq_len", "batch_size", "pretrained_dir", "lora_path",
                                        "lora_merge", "out", "log_every", "model", "synthetic_tokens",
-                                       "pretokenized_path", "pretokenized_meta", "max_batches", "device"};
+                                       "pretokenized_path", "pretokenized_meta", "max_batches", "device",
+                                       "model_type"};
 
 int run(int argc, char** argv) {
   Args a = mft::apps::parse_args(argc, argv, kBool, kValued);
@@ -45,7 +49,7 @@ int run(int argc, char** argv) {
         "  --data_root D --split train|valid|test --seq_len S --batch_size B --pretrained_dir P\n"
         "  [--lora_path F --lora_merge 0|1] [--out F] [--log_every N]\n"
         "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --pretokenized_path F\n"
-        "          --pretokenized_meta F --max_batches N\n");
+        "          --pretokenized_meta F --max_batches N --model_type gpt2|gemma\n");
     return 0;
   }
   const char* fc = std::getenv("MFT_DP_FORCE_COMM");
@@ -58,20 +62,40 @@ int run(int argc, char** argv) {
 
   const std::string pdir = a.get("pretrained_dir");
   const bool random_init = a.b("random_init") || pdir.empty();
-  GPT2Config cfg = (!random_init && mft::apps::file_exists(pdir + "/config.json"))
-                       ? GPT2Config::from_json(pdir + "/config.json")
-                       : GPT2Config::preset(a.get("model", "gpt2"));
-  auto model = std::make_unique<GPT2>(cfg);
-  if (random_init) model->init_random(1234);
-  else model->load_hf(pdir);
-  model->training = false;
+  const std::string mtype = a.get("model_type", "gpt2");
+  if (mtype != "gpt2" && mtype != "gemma") throw std::runtime_error("--model_type must be gpt2 or gemma");
+  const bool cfg_file = !random_init && mft::apps::file_exists(pdir + "/config.json");
+  std::unique_ptr<LanguageModel> model;
+  int vocab = 0, max_pos = 0, eos = 50256;
   const std::string lora = a.get("lora_path");
-  if (!lora.empty()) {
-    model->load_lora(lora);
-    if (a.i("lora_merge", 1)) model->merge_lora(1.f);  // W += s A^T B^T: the adapter costs nothing
-    if (lead) std::printf("  LoRA %s %s\n", lora.c_str(), a.i("lora_merge", 1) ? "(merged)" : "(separate)");
+  const bool merge = a.i("lora_merge", 1) != 0;
+  if (mtype == "gpt2") {
+    GPT2Config cfg = cfg_file ? GPT2Config::from_json(pdir + "/config.json") : GPT2Config::preset(a.get("model", "gpt2"));
+    auto m = std::make_unique<GPT2>(cfg);
+    if (random_init) m->init_random(1234);
+    else m->load_hf(pdir);
+    if (!lora.empty()) {
+      m->load_lora(lora);
+      if (merge) m->merge_lora(1.f);  // W += s A^T B^T: the adapter costs nothing
+    }
+    vocab = cfg.vocab_size, max_pos = cfg.n_positions;
+    model = std::move(m);
+  } else {
+    Gemma3Config cfg = cfg_file ? Gemma3Config::from_json(pdir + "/config.json")
+                                : Gemma3Config::preset(a.get("model", "gemma3-270m"));
+    auto m = std::make_unique<Gemma3>(cfg);
+    if (random_init) m->init_random(1234);
+    else m->load_hf(pdir);
+    if (!lora.empty()) {
+      m->load_lora(lora);
+      if (merge) m->merge_lora(1.f);
+    }
+    vocab = cfg.vocab_size, max_pos = cfg.max_positions, eos = cfg.eos_id;
+    model = std::move(m);
   }
-  const int seq = std::min(a.i("seq_len", 1024), cfg.n_positions);
+  model->training = false;
+  if (!lora.empty() && lead) std::printf("  LoRA %s %s\n", lora.c_str(), merge ? "(merged)" : "(separate)");
+  const int seq = std::min(a.i("seq_len", 1024), max_pos);
   const int B = a.i("batch_size", 1);
   const std::string split = a.get("split", "valid");
   const int sidx = split == "train" ? 0 : split == "valid" ? 1 : split == "test" ? 2 : -1;
@@ -79,7 +103,7 @@ int run(int argc, char** argv) {
 
   DataConfig dc;
   dc.seq_len = seq;
-  dc.eos_id = 50256;
+  dc.eos_id = eos;
   dc.drop_last = false;
   dc.shuffle = false;
   if (comm) {
@@ -101,7 +125,7 @@ int run(int argc, char** argv) {
       uint64_t x = z;
       x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
       x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-      v[i] = (int32_t)((x ^ (x >> 31)) % (uint64_t)cfg.vocab_size);
+      v[i] = (int32_t)((x ^ (x >> 31)) % (uint64_t)vocab);
     }
     ds.set_tokens(std::move(v));
   } else {
@@ -110,8 +134,14 @@ int run(int argc, char** argv) {
     const char* names[] = {raw.c_str(), tokf.c_str(), txt.c_str(), nullptr};
     const std::string f = mft::apps::split_file(root, names);
     if (f.empty()) throw std::runtime_error("no " + split + " split under " + root);
-    auto tok = ByteLevelBPE::from_files(pdir + "/vocab.json", pdir + "/merges.txt");
-    auto enc = [&](const std::string& s) { return tok->encode(s); };
+    mft::apps::Encoder enc;
+    if (mtype == "gpt2") {
+      std::shared_ptr<ByteLevelBPE> tok = ByteLevelBPE::from_files(pdir + "/vocab.json", pdir + "/merges.txt");
+      enc = [tok](const std::string& s) { return tok->encode(s); };
+    } else {
+      std::shared_ptr<SentencePieceBPE> tok = SentencePieceBPE::from_tokenizer_json(pdir + "/tokenizer.json");
+      enc = [tok](const std::string& s) { return tok->encode(s, false); };
+    }
     const int threads = std::max(1u, std::thread::hardware_concurrency());
     ds.set_tokens(pack_lines(read_lines(f, true), enc, dc.eos_id, true, 1.f, seq, threads));
   }

@@ -406,6 +406,7 @@ void Gemma3::save_lora(const std::string& path) {
 
 void Gemma3::merge_lora(float sign) {
   NoGradGuard ng;
+  lora_enabled = sign < 0;
   auto merge = [&](Param& w, std::vector<LoraAdapter>& ads) {
     for (auto& a : ads) {
       Tensor A = a.A.leaf.detach().contiguous(), B = a.B.leaf.detach().contiguous();
@@ -458,27 +459,27 @@ Tensor Gemma3::hidden(const Tensor& ids) {
   };
   auto gl = rope(false, (int)S), lc = rope(true, (int)S);
   Tensor x = embed(ids, embed_, nullptr, embed_scale_);
-  Tensor h = add_norm(x, Tensor(), layers_[0].in_norm, nullptr, eps, true, 1.f, aug(layers_[0].lqkv, H)).second;
+  Tensor h = add_norm(x, Tensor(), layers_[0].in_norm, nullptr, eps, true, 1.f, aug(active(layers_[0].lqkv), H)).second;
   for (int i = 0; i < cfg_.n_layer; ++i) {
     auto& L = layers_[i];
     const auto& cs = L.sliding ? lc : gl;
     // attention
-    Tensor qkv = proj(h, H, L.qkv_w, L.lqkv, L.waug_qkv).view({B, S, nq + 2 * nkv, D});
+    Tensor qkv = proj(h, H, L.qkv_w, active(L.lqkv), L.waug_qkv).view({B, S, nq + 2 * nkv, D});
     Tensor o = qknorm_rope_attention(qkv, nq, nkv, L.q_norm, L.k_norm, cs.first, cs.second, eps, 1.f,
                                      interleaved_rope, attn_scale, L.sliding ? cfg_.sliding_window : 0,
-                                     aug(L.lo, nq * D));
+                                     aug(active(L.lo), nq * D));
     o = o.view({B * S, o.size(-1)});
-    Tensor a = proj(o, nq * D, L.o_w, L.lo, L.waug_o);
+    Tensor a = proj(o, nq * D, L.o_w, active(L.lo), L.waug_o);
     a = add_norm(a, Tensor(), L.post_attn_norm, nullptr, eps, true, 1.f, 0).second;
-    auto r = add_norm(x, a, L.pre_ff_norm, nullptr, eps, true, 1.f, aug(L.lgu, H));
+    auto r = add_norm(x, a, L.pre_ff_norm, nullptr, eps, true, 1.f, aug(active(L.lgu), H));
     x = r.first;
     // GeGLU MLP
-    Tensor gu = proj(r.second, H, L.gu_w, L.lgu, L.waug_gu);
-    Tensor g = gated_act(gu, cfg_.act, aug(L.ldown, I));
-    Tensor f = proj(g, I, L.down_w, L.ldown, L.waug_down);
+    Tensor gu = proj(r.second, H, L.gu_w, active(L.lgu), L.waug_gu);
+    Tensor g = gated_act(gu, cfg_.act, aug(active(L.ldown), I));
+    Tensor f = proj(g, I, L.down_w, active(L.ldown), L.waug_down);
     f = add_norm(f, Tensor(), L.post_ff_norm, nullptr, eps, true, 1.f, 0).second;
     Param& nw = i + 1 < cfg_.n_layer ? layers_[i + 1].in_norm : final_norm_;
-    const int oc = i + 1 < cfg_.n_layer ? aug(layers_[i + 1].lqkv, H) : 0;
+    const int oc = i + 1 < cfg_.n_layer ? aug(active(layers_[i + 1].lqkv), H) : 0;
     auto r1 = add_norm(x, f, nw, nullptr, eps, true, 1.f, oc);
     x = r1.first;
     h = r1.second;

@@ -399,6 +399,7 @@ void GPT2::save_lora(const std::string& path) {
 
 void GPT2::merge_lora(float sign) {
   NoGradGuard ng;
+  lora_enabled = sign < 0;
   auto merge = [&](Param& w, std::vector<LoraAdapter>& ads) {
     for (auto& a : ads) {
       Tensor A = a.A.leaf.detach().contiguous(), B = a.B.leaf.detach().contiguous();
@@ -426,35 +427,35 @@ Tensor GPT2::hidden(const Tensor& ids) {
   const float scale = spec_.scale();
   auto aug = [&](std::vector<LoraAdapter>& ads) { return ads.empty() ? 0 : lora_aug_cols(C, ads); };
   Tensor x = embed(ids, wte_, &wpe_, 1.f);
-  auto n0 = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, aug(blocks_[0].lqkv));
+  auto n0 = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, aug(active(blocks_[0].lqkv)));
   Tensor h = n0.second;
   for (int i = 0; i < cfg_.n_layer; ++i) {
     auto& b = blocks_[i];
     // attention
-    Tensor qkv = b.lqkv.empty()
+    Tensor qkv = active(b.lqkv).empty()
                      ? linear_p(h, b.attn_w, &b.attn_b)
-                     : lora_linear_aug(h, C, b.attn_w, &b.attn_b, b.lqkv, scale, b.waug_qkv, training, dropout_ctr);
-    Tensor o = attention_packed(qkv.view({B, S, 3, H, D}), 1.f / std::sqrt((float)D), true, 0, aug(b.lproj));
+                     : lora_linear_aug(h, C, b.attn_w, &b.attn_b, active(b.lqkv), scale, b.waug_qkv, training, dropout_ctr);
+    Tensor o = attention_packed(qkv.view({B, S, 3, H, D}), 1.f / std::sqrt((float)D), true, 0, aug(active(b.lproj)));
     o = o.view({B * S, o.size(-1)});
-    Tensor a = b.lproj.empty()
+    Tensor a = active(b.lproj).empty()
                    ? linear_p(o, b.proj_w, &b.proj_b)
-                   : lora_linear_aug(o, C, b.proj_w, &b.proj_b, b.lproj, scale, b.waug_proj, training, dropout_ctr);
+                   : lora_linear_aug(o, C, b.proj_w, &b.proj_b, active(b.lproj), scale, b.waug_proj, training, dropout_ctr);
     auto r2 = add_norm(x, a, b.ln2_w, &b.ln2_b, cfg_.eps, false, 0.f, 0);
     x = r2.first;
     // MLP
     Tensor f;
-    if (b.lfc.empty() && b.lfcout.empty()) {
+    if (active(b.lfc).empty() && active(b.lfcout).empty()) {
       f = mlp_gelu(r2.second, b.fc_w, b.fc_b, b.mproj_w, b.mproj_b);
     } else {
-      Tensor u = b.lfc.empty() ? linear_p(r2.second, b.fc_w, &b.fc_b)
-                               : lora_linear(r2.second, b.fc_w, &b.fc_b, b.lfc, scale, training, dropout_ctr);
+      Tensor u = active(b.lfc).empty() ? linear_p(r2.second, b.fc_w, &b.fc_b)
+                               : lora_linear(r2.second, b.fc_w, &b.fc_b, active(b.lfc), scale, training, dropout_ctr);
       u = gelu(u, true);
-      f = b.lfcout.empty() ? linear_p(u, b.mproj_w, &b.mproj_b)
-                           : lora_linear(u, b.mproj_w, &b.mproj_b, b.lfcout, scale, training, dropout_ctr);
+      f = active(b.lfcout).empty() ? linear_p(u, b.mproj_w, &b.mproj_b)
+                           : lora_linear(u, b.mproj_w, &b.mproj_b, active(b.lfcout), scale, training, dropout_ctr);
     }
     Param* nw = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_w : &lnf_w_;
     Param* nb = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_b : &lnf_b_;
-    const int oc = i + 1 < cfg_.n_layer ? aug(blocks_[i + 1].lqkv) : 0;
+    const int oc = i + 1 < cfg_.n_layer ? aug(active(blocks_[i + 1].lqkv)) : 0;
     auto r1 = add_norm(x, f, *nw, nb, cfg_.eps, false, 0.f, oc);
     x = r1.first;
     h = r1.second;

@@ -25,8 +25,15 @@ class LanguageModel {
   virtual std::vector<std::pair<std::string, Param*>> trainable() = 0;
   virtual size_t num_parameters() const = 0;
   bool training = true;
+  // false after merge_lora(+1): the adapters live in the base weights, the forward skips them
+  bool lora_enabled = true;
   Tensor dropout_ctr;    // device int64 step counter (fresh LoRA-dropout masks per step)
   int64_t ce_chunk = 0;  // LM-head CE rows per fused call (default_ce_chunk)
+
+ protected:
+  // the adapters of one projection as the forward sees them (none while merged)
+  std::vector<LoraAdapter>& active(std::vector<LoraAdapter>& ads) { return lora_enabled ? ads : no_adapters_; }
+  std::vector<LoraAdapter> no_adapters_;
 };
 
 // rows of the fused LM-head CE per call: one [rows, Vpad] bf16 E workspace within a 32 GiB budget

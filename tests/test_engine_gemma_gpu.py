@@ -141,3 +141,29 @@ def test_native_gemma270m_trains():
     losses = [float(line.split("Loss=")[1].split()[0]) for line in r.stdout.splitlines() if "Loss=" in line]
     assert len(losses) == 6 and all(math.isfinite(x) for x in losses)
     assert abs(losses[0] - math.log(V)) < 1.0, losses
+
+
+def test_native_gemma_eval_ppl_matches_python_cli(tmp_path):
+    """Native eval_ppl --model_type gemma (fused LM head) == the Python eval_ppl CLI on the same
+    Gemma weights, adapter and pretokenized validation split, with the adapter merged into the base
+    weights and kept separate (a merged adapter must not also run in the forward)."""
+    tmp = str(tmp_path)
+    _, lora = _fixture(tmp, 64, 20_000)
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    ppl = {}
+    for merge in ("1", "0"):
+        common = ["--model_type", "gemma", "--pretrained_dir", tmp, "--lora_path", lora, "--lora_merge", merge,
+                  "--pretokenized_path", os.path.join(tmp, "tokens.bin"), "--split", "valid", "--seq_len", "64",
+                  "--batch_size", "4"]
+        nat_out, py_out = os.path.join(tmp, f"nat{merge}.json"), os.path.join(tmp, f"py{merge}.json")
+        r = subprocess.run([_bin("eval_ppl"), *common, "--out", nat_out], capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        r = subprocess.run(["python", "-m", "mobilefinetuner_amd.cli.eval_ppl", *common, "--out", py_out],
+                           capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        nat, py = json.load(open(nat_out)), json.loads(open(py_out).read().splitlines()[-1])
+        print(merge, nat, py)
+        assert nat["tokens"] == py.get("tokens", py.get("n_tokens", nat["tokens"]))
+        assert abs(nat["ppl"] - py["ppl"]) < 2e-3 * py["ppl"], (merge, nat, py)
+        ppl[merge] = nat["ppl"]
+    assert abs(ppl["1"] - ppl["0"]) < 5e-3 * ppl["0"], ppl
