@@ -88,32 +88,38 @@ class ParameterSharder:
             self.tier.mark_resident(key, True)
         self.stats["fetches"] += 1
 
+    def _make_room(self, name, keep):
+        """Evict least-recently-used groups (never those in ``keep``) until ``name`` fits."""
+        g = self.groups[name]
+        need = sum(b for i, b in enumerate(g.nbytes) if not self.tier.resident(f"{name}#{i}"))
+        if not need:
+            return
+        victims = []
+        for key in self.tier.victims(need, ""):
+            gname = key.split("#")[0]
+            if gname not in keep and gname not in victims:
+                victims.append(gname)
+        for v in victims:
+            self._evict(v)
+
     def require(self, name: str, backward: bool = False):
         """Make ``name`` resident; prefetch the group used next -- the following block in the
-        forward, the preceding one in the backward."""
+        forward (after the last block: the embedding, which the tied LM head reads next), the
+        preceding one in the backward (before block 0: the embedding, which the next step's forward
+        reads first) -- evicting least-recently-used groups to make room, so the copy of the next
+        group always overlaps the compute of this one (the reference's require() loads on demand)."""
         g = self.groups.get(name)
         if g is None:
             return
-        need = sum(b for i, b in enumerate(g.nbytes) if not self.tier.resident(f"{name}#{i}"))
-        if need:
-            victims = set()
-            for key in self.tier.victims(need, ""):
-                gname = key.split("#")[0]
-                if gname != name:
-                    victims.add(gname)
-            for v in victims:
-                self._evict(v)
+        self._make_room(name, {name})
         self._fetch(name)
-        if self.prefetch:
-            idx = self.order.index(name) + (-1 if backward else 1)
-            nxt = self.order[idx] if 0 <= idx < len(self.order) else None
-            if nxt is not None and self._fits(nxt, exclude=name):
+        if self.prefetch and len(self.order) > 1:
+            idx = self.order.index(name)
+            nxt = self.order[(idx - 1) % len(self.order)] if backward else self.order[(idx + 1) % len(self.order)]
+            both = sum(self.groups[name].nbytes) + sum(self.groups[nxt].nbytes)
+            if nxt != name and (not self.tier.device_budget or both <= self.tier.device_budget):
+                self._make_room(nxt, {name, nxt})
                 self._fetch(nxt)
-
-    def _fits(self, name, exclude):
-        g = self.groups[name]
-        need = sum(b for i, b in enumerate(g.nbytes) if not self.tier.resident(f"{name}#{i}"))
-        return not self.tier.device_budget or self.tier.resident_bytes + need <= self.tier.device_budget
 
     def offload_all(self):
         for n in self.order:

@@ -43,8 +43,12 @@ def run_cli(args, metrics):
         raise RuntimeError(f"{' '.join(args)} failed:\n{open(log).read()[-4000:]}")
     recs = [json.loads(x) for x in open(metrics)] if os.path.exists(metrics) else []
     hbm = max((x.get("hbm_peak_gb", 0.0) for x in recs), default=0.0)
+    # steady-state throughput (setup -- model build, host-tier registration -- excluded): median
+    # tokens/s of the logged steps after the first three
+    tps = sorted(x["tokens_per_sec"] for x in recs[3:] if x.get("tokens_per_sec"))
+    med = tps[len(tps) // 2] if tps else 0.0
     return {"wall_s": round(wall, 2), "hbm_peak_gb": round(hbm, 3), "host_rss_peak_gb": round(ru.ru_maxrss / 2 ** 20, 3),
-            "steps_logged": len(recs)}
+            "steps_logged": len(recs), "steady_tokens_per_s": round(med, 1)}
 
 
 def cli_for(model):
