@@ -500,6 +500,108 @@ void lora_update(const bf16_t* base, long ldb, const bf16_t* U, long ldu, const 
   }
 }
 
+// lora_xty (weight-gradient of a rank-r factor on MFMA):  out[k, r] (+)= scale * sum_m X[m, k] Y[m, r]
+// for R % 8 == 0, R <= 32 -- dA = v^T x (X = the layer input, Y = v) and dB = u^T dy (X = dy, Y = u)
+// of every adapter sharing X in ONE pass over X.  The dB half of lora_dy with up to 32 ranks: a wave
+// owns 32-row tiles of one 256-column strip, loads its X tile once with 16-B loads, writes it to its
+// padded LDS image and reads it back transposed (ds_read_b64_tr_b16) as the B operand of
+// D[rank][16 cols] += Y^T[rank][32 rows] . X[32 rows][16 cols]; the Y rows of the tile go through a
+// [32][16 NR] image read back transposed as the A operand.  The VALU form (lora_wgrad_kernel) does
+// R fp32 FMAs per X element and was VALU-bound (Gemma q|k|v dA: 60 us for 84 MB).
+template <int NR>  // rank blocks of 16
+__global__ __launch_bounds__(256, 2) void lora_xty_kernel(const bf16_t* __restrict__ X, long ldx,
+                                                          const bf16_t* __restrict__ Y, long ldy, int R,
+                                                          float* __restrict__ out, long osk, long osr, WgradOuts outs,
+                                                          long M, int K, long chunk, float scale) {
+  constexpr int YL = 16 * NR;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4][32 * kDyLd + 32 * YL];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int k0 = blockIdx.x * 256;
+  bf16_t* img = lds[w];
+  bf16_t* yimg = lds[w] + 32 * kDyLd;
+  f32x4_t acc[NR][16];
+#pragma unroll
+  for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+    for (int cb = 0; cb < 16; ++cb) acc[nr][cb] = zero4();
+  const long mbeg = (long)blockIdx.y * chunk;
+  const long mend = min(M, mbeg + chunk);
+  for (long t0 = mbeg + 32 * w; t0 < mend; t0 += 128) {
+    bf16x8_t a[2][8];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const long m = t0 + 16 * rb + c16;
+      const bool rok = m < mend;
+      const bf16_t* rowp = X + (rok ? m : mbeg) * ldx;
+#pragma unroll
+      for (int cg = 0; cg < 8; ++cg) {
+        const int k = k0 + 32 * cg + 8 * g;
+        a[rb][cg] = (rok && k < K) ? *reinterpret_cast<const bf16x8_t*>(rowp + k) : bf16x8_t{};
+      }
+    }
+    // Y rows of the tile: lane < 32 -> row t0 + lane, 8 ranks per 16-B load (zero past R / mend)
+    u16x8_t yr[2 * NR];
+#pragma unroll
+    for (int j = 0; j < 2 * NR; ++j) {
+      yr[j] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      if (lane < 32 && t0 + lane < mend && 8 * j < R) yr[j] = *reinterpret_cast<const u16x8_t*>(Y + (t0 + lane) * ldy + 8 * j);
+    }
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int cg = 0; cg < 8; ++cg)
+        *reinterpret_cast<bf16x8_t*>(img + (16 * rb + c16) * kDyLd + 32 * cg + 8 * g) = a[rb][cg];
+    if (lane < 32) {
+#pragma unroll
+      for (int j = 0; j < 2 * NR; ++j) *reinterpret_cast<u16x8_t*>(yimg + lane * YL + 8 * j) = yr[j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr) {
+      const bf16x8_t ya = frag_tr(yimg, YL, 0, 16 * nr);  // lane: Y[row 8g + j][rank 16 nr + (l & 15)]
+#pragma unroll
+      for (int cb = 0; cb < 16; ++cb) acc[nr][cb] = mfma16(ya, frag_tr(img, kDyLd, 0, 16 * cb), acc[nr][cb]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // tr-reads done before the next tile's writes
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // block fold per 16-rank block through LDS ([4 waves][16 ranks][256 cols] fp32 = 64 KB), one fp32
+  // atomic per (rank, column) per block
+  float* red = reinterpret_cast<float*>(&lds[0][0]);
+#pragma unroll
+  for (int nr = 0; nr < NR; ++nr) {
+    __syncthreads();
+#pragma unroll
+    for (int cb = 0; cb < 16; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(w * 16 + 4 * g + i) * 256 + 16 * cb + c16] = acc[nr][cb][i];
+    __syncthreads();
+    for (int o = threadIdx.x; o < 16 * 256; o += 256) {
+      const int rl16 = o >> 8, c = o & 255;
+      const int r = 16 * nr + rl16;
+      if (r >= R || k0 + c >= K) continue;
+      const float v = red[rl16 * 256 + c] + red[(16 + rl16) * 256 + c] + red[(32 + rl16) * 256 + c] +
+                      red[(48 + rl16) * 256 + c];
+      float* dst = outs.n ? outs.p[r >> 3] : out;
+      const int rr = outs.n ? (r & 7) : r;
+      atomicAdd(dst + (long)(k0 + c) * osk + (long)rr * osr, v * scale);
+    }
+  }
+}
+
+// MFT_WGRAD_VALU=1: every lora_wgrad on the VALU kernel (A/B switch)
+static bool wgrad_valu() {
+  static const int v = [] {
+    const char* e = getenv("MFT_WGRAD_VALU");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v == 1;
+}
+
 static long wgrad_chunks(long M, int K, int R, long* chunk_out) {
   const int rb = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : 8;
   const int gx = cdiv(K, 256);
@@ -532,6 +634,19 @@ void lora_wgrad(const bf16_t* X, long ldx, const bf16_t* Y, long ldy, float* out
   if ((K % 4) || (ldx % 4) || (reinterpret_cast<uintptr_t>(X) % 8)) {
     fprintf(stderr, "lora_wgrad: K (%d) and ldx (%ld) must be multiples of 4 and X 8-byte aligned\n", K, ldx);
     abort();
+  }
+  // MFMA form: no dropout mask on X, ranks in whole 8-blocks up to 32, 16-B aligned rows, fp32 atomics
+  // (the deterministic mode keeps the VALU kernel's fixed-order partials)
+  if (!det_ws && drop.p <= 0.f && R % 8 == 0 && R <= 32 && K % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
+      reinterpret_cast<uintptr_t>(X) % 16 == 0 && reinterpret_cast<uintptr_t>(Y) % 16 == 0 && !wgrad_valu()) {
+    long chunk = 0;
+    const long ny = dy_chunks(M, K, &chunk);
+    dim3 grid(cdiv(K, 256), (unsigned)ny);
+    if (R <= 16)
+      lora_xty_kernel<1><<<grid, 256, 0, st>>>(X, ldx, Y, ldy, R, out, osk, osr, so, M, K, chunk, scale);
+    else
+      lora_xty_kernel<2><<<grid, 256, 0, st>>>(X, ldx, Y, ldy, R, out, osk, osr, so, M, K, chunk, scale);
+    return;
   }
   const int rb = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : 8;
   const int gx = cdiv(K, 256);
