@@ -89,6 +89,12 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// 2^x as ONE v_exp_f32.  exp2f() expands to a denormal-safe sequence (compare, select, add, exp,
+// select, ldexp: ~6 VALU ops + hazard nops per element), which dominated the CE forward epilogue
+// and the softmax of the attention kernels.  Every caller feeds x <= 0 (value minus a running or
+// final max) or -inf: results below 2^-126 flush to 0, which a softmax sum cannot see.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // GELU (tanh form, GPT-2 "gelu_new") via 0.5 (1 + tanh(u)) = sigmoid(2u): one v_exp_f32 and one
 // v_rcp_f32 instead of a libm tanhf (which dominated the fused GEMM epilogues).  Saturates
 // correctly: exp -> inf gives sigmoid 0, exp -> 0 gives 1.

@@ -130,11 +130,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
       for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
       const float mnew = fmaxf(m[i], mx);
       const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
-      alpha[i] = exp2f(m[i] - msafe);
+      alpha[i] = fast_exp2(m[i] - msafe);
       float rs = 0.f;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) {
-        const float p = exp2f(sacc[nb][i] - msafe);
+        const float p = fast_exp2(sacc[nb][i] - msafe);
         sacc[nb][i] = p;
         rs += p;
       }
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
       for (int i = 0; i < 4; ++i) {
         const int kr = 16 * w + 4 * (lane >> 4) + i;
         const bool ok = qi < Sq && attn_allowed(qi, kb + kr, kv_len, coff, causal, window);
-        const float p = ok ? exp2f(st[nb][i] * c2 - lq) : 0.f;
+        const float p = ok ? fast_exp2(st[nb][i] * c2 - lq) : 0.f;
         const float ds = p * (dpt[nb][i] - dq) * scale;
         PT[kr * LDT + qc] = f2bf(p);
         DST[kr * LDT + qc] = f2bf(ds);
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __re
   for (int kb = 0; kb < NB; ++kb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float p = exp2f(st[kb][i] - ms);
+      const float p = fast_exp2(st[kb][i] - ms);
       st[kb][i] = p;
       rs += p;
     }
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
       for (int i = 0; i < 4; ++i) {
         const int qi = 32 * kk + 16 * t + 4 * g + i;
         const bool ok = live && qi < S && key < kv_len && (!causal || key <= qi);
-        const float p = ok ? exp2f(sc[t][i] * c2 - lse_s[qi]) : 0.f;
+        const float p = ok ? fast_exp2(sc[t][i] * c2 - lse_s[qi]) : 0.f;
         sc[t][i] = p;                                     // P
         dp[t][i] = p * (dp[t][i] - del_s[qi]) * scale;    // dS
       }
@@ -783,13 +783,13 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m, mx);
       const float msafe = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = exp2f(m - msafe);
+      const float alpha = fast_exp2(m - msafe);
       float rs = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(st[t][i] - msafe);
+          const float p = fast_exp2(st[t][i] - msafe);
           st[t][i] = p;
           rs += p;
         }
@@ -970,13 +970,13 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
       mx = fmaxf(mx, xor32_pl(mx));
       const float mnew = fmaxf(m, mx);
       const float msafe = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = exp2f(m - msafe);
+      const float alpha = fast_exp2(m - msafe);
       float rs = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(st[t][i] - msafe);
+          const float p = fast_exp2(st[t][i] - msafe);
           st[t][i] = p;
           rs += p;
         }
@@ -1100,7 +1100,7 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
         for (int i = 0; i < 4; ++i) {
           const int qr = 16 * t + 4 * g + i, qi = q0 + qr;
           const bool ok = qi < Sq && attn_allowed(qi, key, kv_len, coff, causal, window);
-          const float p = ok ? exp2f(sc[t][i] * c2 - ls[qr]) : 0.f;
+          const float p = ok ? fast_exp2(sc[t][i] * c2 - ls[qr]) : 0.f;
           sc[t][i] = p;
           dp[t][i] = p * (dp[t][i] - dl[qr]) * scale;
         }
@@ -1183,7 +1183,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const bool ok = qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window);
-          const float p = ok ? exp2f(st[t][i] * c2 - lq) : 0.f;
+          const float p = ok ? fast_exp2(st[t][i] * c2 - lq) : 0.f;
           dpt[t][i] = p * (dpt[t][i] - dlq) * scale;
         }
       }

@@ -69,15 +69,28 @@ __global__ __launch_bounds__(256) void lora_rowdot_kernel(const bf16_t* __restri
   f32x4_t acc[RT];
 #pragma unroll
   for (int t = 0; t < RT; ++t) acc[t] = zero4();
-  for (int ks = ks0; ks < ks1; ++ks) {
-    const int k = ks * 32 + 8 * (lane >> 4);
-    bf16x8_t a = row_ok ? *reinterpret_cast<const bf16x8_t*>(X + mr * ldx + k) : bf16x8_t{};
-    if (drop.p > 0.f) a = apply_drop8(a, drop, dseed, mr, k, K);
+  // UNR k-steps per batch: every X / W load of the batch is issued before the first MFMA consumes
+  // one (a one-step loop exposed the full load latency on each of its few iterations: K / 128 per
+  // wave, e.g. 5 at Gemma's K = 640)
+  constexpr int UNR = 4;
+  for (int kb = ks0; kb < ks1; kb += UNR) {
+    bf16x8_t a[UNR], b[UNR][RT];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      const int r = t * 16 + (lane & 15);
-      bf16x8_t b = r < R ? *reinterpret_cast<const bf16x8_t*>(Wt + (long)r * ldw + k) : bf16x8_t{};
-      acc[t] = mfma16(a, b, acc[t]);
+    for (int u = 0; u < UNR; ++u) {
+      const bool ok = kb + u < ks1;
+      const int k = (kb + u) * 32 + 8 * (lane >> 4);
+      a[u] = (ok && row_ok) ? *reinterpret_cast<const bf16x8_t*>(X + mr * ldx + k) : bf16x8_t{};
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const int r = t * 16 + (lane & 15);
+        b[u][t] = (ok && r < R) ? *reinterpret_cast<const bf16x8_t*>(Wt + (long)r * ldw + k) : bf16x8_t{};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (drop.p > 0.f) a[u] = apply_drop8(a[u], drop, dseed, mr, (kb + u) * 32 + 8 * (lane >> 4), K);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) acc[t] = mfma16(a[u], b[u][t], acc[t]);
     }
   }
 #pragma unroll

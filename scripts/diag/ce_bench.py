@@ -30,6 +30,7 @@ def main():
     dh = torch.empty_like(h)
     scale = torch.full((1,), 1.0 / M, device="cuda")
     t_fwd = timeit(lambda: C.lm_head_ce(h, W, labels, V, E, loss, scale, 1.0, None, False))
+    t_nll = timeit(lambda: C.lm_head_ce(h, W, labels, V, None, loss, scale, 1.0, None, False))
     t_all = timeit(lambda: C.lm_head_ce(h, W, labels, V, E, loss, scale, 1.0, dh, False))
     t_mat = timeit(lambda: C.lm_head_ce(h, W, labels, V, E, loss, scale, 1.0, dh, True))
     t_g8_nt = timeit(lambda: C.gemm_t(h, W, False, False, 0, None, None, 1.0, E, None, None))
@@ -39,6 +40,7 @@ def main():
     fl = 2.0 * M * K * Vpad
     print(f"M={M} K={K} Vpad={Vpad}")
     print(f"fused fwd (CE_FWD + finalize)      {t_fwd:8.3f} ms  {fl / t_fwd / 1e9:7.1f} TF/s")
+    print(f"fused fwd, no E stores (NLL only)  {t_nll:8.3f} ms  {fl / t_nll / 1e9:7.1f} TF/s")
     print(f"fused fwd + dgrad (CE_DGRAD)       {t_all:8.3f} ms  (dgrad ~ {t_all - t_fwd:.3f} ms, {fl / (t_all - t_fwd) / 1e9:.1f} TF/s)")
     print(f"fused fwd + materialize + NN       {t_mat:8.3f} ms")
     print(f"gemm8 NT plain                     {t_g8_nt:8.3f} ms  {fl / t_g8_nt / 1e9:7.1f} TF/s")
