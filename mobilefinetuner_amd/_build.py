@@ -76,6 +76,7 @@ APPS = {
     "engine_selftest": ("engine_selftest.cpp", []),
     "eval_ppl": ("eval_ppl.cpp", []),
     "train_lora_gemma": ("train_lora_gemma.cpp", []),
+    "eval_mmlu": ("eval_mmlu.cpp", []),
 }
 
 

@@ -68,7 +68,9 @@ class Gemma3 : public LanguageModel {
   std::vector<std::pair<std::string, Param*>> trainable() override;
   Tensor loss(const Tensor& ids, const Tensor& labels, float w_grad_scale = 1.f) override;
   std::pair<Tensor, Tensor> nll(const Tensor& ids, const Tensor& labels) override;
-  Tensor hidden(const Tensor& ids);
+  Tensor hidden(const Tensor& ids) override;
+  Param& output_embedding() override { return embed_; }
+  int vocab() const override { return cfg_.vocab_size; }
   void merge_lora(float sign);
   size_t num_parameters() const override;
   const GemmaLoraSpec& lora_spec() const { return spec_; }

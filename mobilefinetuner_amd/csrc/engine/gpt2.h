@@ -65,7 +65,9 @@ class GPT2 : public LanguageModel {
   // mean token NLL of one micro-batch (ids / labels [B, S], labels already shifted, -100 ignored)
   Tensor loss(const Tensor& ids, const Tensor& labels, float w_grad_scale = 1.f) override;
   std::pair<Tensor, Tensor> nll(const Tensor& ids, const Tensor& labels) override;  // (sum, count), no grad
-  Tensor hidden(const Tensor& ids);
+  Tensor hidden(const Tensor& ids) override;
+  Param& output_embedding() override { return wte_; }
+  int vocab() const override { return cfg_.vocab_size; }
   void merge_lora(float sign);
   const LoraSpec& lora_spec() const { return spec_; }
   size_t num_parameters() const override;

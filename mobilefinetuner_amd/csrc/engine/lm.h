@@ -24,6 +24,10 @@ class LanguageModel {
   virtual std::pair<Tensor, Tensor> nll(const Tensor& ids, const Tensor& labels) = 0;
   virtual std::vector<std::pair<std::string, Param*>> trainable() = 0;
   virtual size_t num_parameters() const = 0;
+  // final hidden states [B*S, C] (after the last norm) and the tied output embedding [Vpad, C]
+  virtual Tensor hidden(const Tensor& ids) = 0;
+  virtual Param& output_embedding() = 0;
+  virtual int vocab() const = 0;
   bool training = true;
   // false after merge_lora(+1): the adapters live in the base weights, the forward skips them
   bool lora_enabled = true;
