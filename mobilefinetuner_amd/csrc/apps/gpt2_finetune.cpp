@@ -121,10 +121,9 @@ int run(int argc, char** argv) {
 #else
   const bool full = false;
 #endif
-  if (a.b("shard_enable"))
-    throw std::runtime_error("--shard_enable: the host/disk offload tier is driven from the Python CLI "
-                             "(python -m mobilefinetuner_amd.cli." + std::string(kProg) + "); the native CLI keeps "
-                             "every weight resident in HBM");
+  if (a.b("shard_enable") && full)
+    throw std::runtime_error("--shard_enable streams FROZEN weights; in full fine-tuning every weight trains "
+                             "(use the Python CLI's ZeRO-3 / host-offloaded optimizer for that)");
   if (a.b("deterministic")) set_deterministic(true);
   // data parallelism: one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK, e.g. under
   // `python -m mobilefinetuner_amd.launch --nproc N`), native RCCL communicator; the communicator
@@ -182,6 +181,17 @@ int run(int argc, char** argv) {
     model->inject_lora(spec);
     std::printf("  injected adapters (rank=%d, alpha=%g, targets=%s)\n", spec.rank, spec.alpha,
                 a.get("lora_targets", "AttnQKV,AttnProj").c_str());
+  }
+  if (a.b("shard_enable")) {
+    // reference ParameterSharder flags: --shard_budget_mb (device bytes for streamed weights);
+    // --shard_dir / --shard_fp16_disk name its disk tier, which pinned host memory replaces here
+    const size_t budget = (size_t)a.l("shard_budget_mb", 512) << 20;
+    model->enable_weight_streaming(budget);
+    const WeightStreamer* ws = model->streamer();
+    std::printf("  weight streaming ON: %d device slots (%.1f MB) for %.1f MB of frozen block weights in pinned host memory\n",
+                ws->slots(), ws->device_bytes() / 1048576.0, ws->host_bytes() / 1048576.0);
+    if (!a.get("shard_dir").empty() || a.kv.count("shard_fp16_disk"))
+      std::printf("  (--shard_dir / --shard_fp16_disk: no disk tier in the native engine, host DRAM holds the weights)\n");
   }
   FlatParams flat(model->trainable());
   std::printf("  trainable params: %lld (padded)  |  total: %zu\n", (long long)flat.numel, model->num_parameters());

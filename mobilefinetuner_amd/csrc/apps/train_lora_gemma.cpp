@@ -9,6 +9,7 @@
 // (cli/train_lora_gemma.py, which follows the reference); extras:
 //   --model P --random_init --synthetic_data [--synthetic_tokens N] --resume_from F (initial
 //   adapter) --no_graph --compat_l2_adam --metrics_out F --deterministic --interleaved_rope
+//   --shard_enable --shard_budget_mb N: frozen layer weights streamed from pinned host memory
 // The alignment-dump harness (--align_*) and the embedding dump stay in the Python CLI.
 #include <hip/hip_runtime.h>
 
@@ -41,14 +42,15 @@ const char* kProg = "train_lora_gemma";
 
 const std::set<std::string> kBool = {"random_init", "synthetic_data", "no_graph", "compat_l2_adam", "deterministic",
                                      "interleaved_rope", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
-                                     "help"};
+                                     "shard_enable", "help"};
 const std::set<std::string> kValued = {
     "model_dir", "data_dir", "pretokenized_path", "pretokenized_meta", "output_dir", "targets", "lora_targets",
     "epochs", "max_steps", "seq_len", "batch", "grad_accum", "lr", "learning_rate", "rank", "lora_r", "alpha",
     "lora_alpha", "lora_dropout", "warmup_ratio", "max_grad_norm", "weight_decay", "loss_reduction", "lr_schedule",
     "data_fraction", "log_interval", "eval_steps", "eval_batches", "save_every", "seed", "model", "synthetic_tokens",
     "resume_from", "metrics_out", "eval_out", "pm_interval", "pm_batt_thresh", "pm_temp_thresh", "pm_fb_high",
-    "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "device"};
+    "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "device",
+    "shard_budget_mb", "shard_dir", "shard_fp16_disk"};
 
 // first present of several alias flags
 std::string pick(const Args& a, std::initializer_list<const char*> keys, const std::string& d) {
@@ -132,6 +134,16 @@ int run(int argc, char** argv) {
     std::string t;
     for (auto& x : spec.targets) t += (t.empty() ? "" : ",") + x;
     std::printf("  LoRA rank=%d alpha=%g dropout=%g targets=%s\n", spec.rank, spec.alpha, spec.dropout, t.c_str());
+  }
+  if (a.b("shard_enable")) {
+    // --shard_budget_mb: device bytes for the streamed layer weights (the reference CLI raised its
+    // budget to the largest parameter, train_lora_gemma.cpp:431-441; here the tied embedding stays
+    // resident and every slot holds one whole layer)
+    const size_t budget = (size_t)a.l("shard_budget_mb", 512) << 20;
+    model->enable_weight_streaming(budget);
+    const WeightStreamer* ws = model->streamer();
+    std::printf("  weight streaming ON: %d device slots (%.1f MB) for %.1f MB of frozen layer weights in pinned host memory\n",
+                ws->slots(), ws->device_bytes() / 1048576.0, ws->host_bytes() / 1048576.0);
   }
   FlatParams flat(model->trainable());
   std::printf("  trainable params: %lld (padded)  |  total: %zu\n", (long long)flat.numel, model->num_parameters());

@@ -8,6 +8,7 @@
 #include <regex>
 #include <set>
 #include <sstream>
+#include <tuple>
 
 #include "engine/autograd.h"
 #include "engine/ops.h"
@@ -425,6 +426,15 @@ void Gemma3::merge_lora(float sign) {
   }
 }
 
+void Gemma3::enable_weight_streaming(size_t budget_bytes) {
+  std::vector<std::vector<Param*>> groups;
+  for (auto& L : layers_) {
+    groups.push_back({&L.qkv_w, &L.o_w, &L.gu_w, &L.down_w});
+    L.waug_qkv = L.waug_o = L.waug_gu = L.waug_down = Tensor();
+  }
+  streamer_ = std::make_unique<WeightStreamer>(groups, budget_bytes);
+}
+
 // ------------------------------------------------------------------ forward
 std::pair<Tensor, Tensor> Gemma3::rope(bool local, int S) {
   const int key = local ? 1 : 0;
@@ -452,10 +462,13 @@ Tensor Gemma3::hidden(const Tensor& ids) {
   const int H = cfg_.hidden, D = cfg_.head_dim, nq = cfg_.n_head, nkv = cfg_.n_kv, I = cfg_.intermediate;
   const float s = spec_.scale(), eps = cfg_.eps;
   const float attn_scale = 1.f / std::sqrt(cfg_.query_pre_attn_scalar);
-  auto aug = [&](std::vector<LoraAdapter>& ads, int in) { return ads.empty() ? 0 : lora_aug_cols(in, ads); };
+  // streamed weights: no resident augmented-K copy [W | s B^T], the adapters run beside the GEMM
+  const bool st = streamer_ != nullptr;
+  auto aug = [&](std::vector<LoraAdapter>& ads, int in) { return (ads.empty() || st) ? 0 : lora_aug_cols(in, ads); };
   auto proj = [&](const Tensor& x, int K, Param& w, std::vector<LoraAdapter>& ads, Tensor& waug) {
-    return ads.empty() ? linear_p(x, w, nullptr)
-                       : lora_linear_aug(x, K, w, nullptr, ads, s, waug, training, dropout_ctr);
+    if (ads.empty()) return linear_p(x, w, nullptr);
+    if (st) return lora_linear(x, w, nullptr, ads, s, training, dropout_ctr);
+    return lora_linear_aug(x, K, w, nullptr, ads, s, waug, training, dropout_ctr);
   };
   auto gl = rope(false, (int)S), lc = rope(true, (int)S);
   Tensor x = embed(ids, embed_, nullptr, embed_scale_);
@@ -463,6 +476,7 @@ Tensor Gemma3::hidden(const Tensor& ids) {
   for (int i = 0; i < cfg_.n_layer; ++i) {
     auto& L = layers_[i];
     const auto& cs = L.sliding ? lc : gl;
+    if (st) streamer_->ensure(i, i + 1);
     // attention
     Tensor qkv = proj(h, H, L.qkv_w, active(L.lqkv), L.waug_qkv).view({B, S, nq + 2 * nkv, D});
     Tensor o = qknorm_rope_attention(qkv, nq, nkv, L.q_norm, L.k_norm, cs.first, cs.second, eps, 1.f,
@@ -483,6 +497,7 @@ Tensor Gemma3::hidden(const Tensor& ids) {
     auto r1 = add_norm(x, f, nw, nullptr, eps, true, 1.f, oc);
     x = r1.first;
     h = r1.second;
+    if (st) std::tie(x, h) = streamer_->gate(x, h, i);
   }
   return h;
 }

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "engine/lm.h"
+#include "engine/weight_stream.h"
 
 namespace mft {
 namespace eng {
@@ -74,6 +75,10 @@ class Gemma3 : public LanguageModel {
   void merge_lora(float sign);
   size_t num_parameters() const override;
   const GemmaLoraSpec& lora_spec() const { return spec_; }
+  // --shard_enable: the layers' frozen projection weights streamed from pinned host memory through
+  // device slots within budget_bytes (weight_stream.h); LoRA projections take the plain path
+  void enable_weight_streaming(size_t budget_bytes);
+  const WeightStreamer* streamer() const { return streamer_.get(); }
   bool interleaved_rope = false;  // reference RoPE pairing
 
  private:
@@ -83,6 +88,7 @@ class Gemma3 : public LanguageModel {
   GemmaLoraSpec spec_;
   Param embed_, final_norm_;
   std::vector<Gemma3Layer> layers_;
+  std::unique_ptr<WeightStreamer> streamer_;
   float embed_scale_ = 1.f;
   std::map<int, std::pair<Tensor, Tensor>> rope_;  // key: local ? 1 : 0 -> (cos, sin) [n, D/2]
   int rope_len_ = 0;

@@ -8,6 +8,7 @@
 #include <map>
 #include <regex>
 #include <sstream>
+#include <tuple>
 
 #include "engine/autograd.h"
 #include "engine/ops.h"
@@ -419,27 +420,42 @@ void GPT2::merge_lora(float sign) {
   }
 }
 
+void GPT2::enable_weight_streaming(size_t budget_bytes) {
+  std::vector<std::vector<Param*>> groups;
+  for (auto& b : blocks_) {
+    std::vector<Param*> g;
+    for (Param* p : {&b.attn_w, &b.attn_b, &b.proj_w, &b.proj_b, &b.fc_w, &b.fc_b, &b.mproj_w, &b.mproj_b})
+      if (!p->trainable()) g.push_back(p);
+    groups.push_back(g);
+    b.waug_qkv = Tensor(), b.waug_proj = Tensor();
+  }
+  streamer_ = std::make_unique<WeightStreamer>(groups, budget_bytes);
+}
+
 // ------------------------------------------------------------------ forward
 Tensor GPT2::hidden(const Tensor& ids) {
   const int64_t B = ids.size(0), S = ids.size(1);
   MFT_CHECK(S <= cfg_.n_positions, "sequence ", S, " exceeds n_positions ", cfg_.n_positions);
   const int C = cfg_.n_embd, H = cfg_.n_head, D = cfg_.head_dim();
   const float scale = spec_.scale();
-  auto aug = [&](std::vector<LoraAdapter>& ads) { return ads.empty() ? 0 : lora_aug_cols(C, ads); };
+  // streamed weights: no resident augmented-K copy [W | s B^T], the adapters run beside the GEMM
+  const bool st = streamer_ != nullptr;
+  auto aug = [&](std::vector<LoraAdapter>& ads) { return (ads.empty() || st) ? 0 : lora_aug_cols(C, ads); };
   Tensor x = embed(ids, wte_, &wpe_, 1.f);
   auto n0 = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, aug(active(blocks_[0].lqkv)));
   Tensor h = n0.second;
   for (int i = 0; i < cfg_.n_layer; ++i) {
     auto& b = blocks_[i];
     // attention
-    Tensor qkv = active(b.lqkv).empty()
-                     ? linear_p(h, b.attn_w, &b.attn_b)
-                     : lora_linear_aug(h, C, b.attn_w, &b.attn_b, active(b.lqkv), scale, b.waug_qkv, training, dropout_ctr);
+    if (st) streamer_->ensure(i, i + 1);
+    Tensor qkv = active(b.lqkv).empty() ? linear_p(h, b.attn_w, &b.attn_b)
+                 : st ? lora_linear(h, b.attn_w, &b.attn_b, active(b.lqkv), scale, training, dropout_ctr)
+                      : lora_linear_aug(h, C, b.attn_w, &b.attn_b, active(b.lqkv), scale, b.waug_qkv, training, dropout_ctr);
     Tensor o = attention_packed(qkv.view({B, S, 3, H, D}), 1.f / std::sqrt((float)D), true, 0, aug(active(b.lproj)));
     o = o.view({B * S, o.size(-1)});
-    Tensor a = active(b.lproj).empty()
-                   ? linear_p(o, b.proj_w, &b.proj_b)
-                   : lora_linear_aug(o, C, b.proj_w, &b.proj_b, active(b.lproj), scale, b.waug_proj, training, dropout_ctr);
+    Tensor a = active(b.lproj).empty() ? linear_p(o, b.proj_w, &b.proj_b)
+               : st ? lora_linear(o, b.proj_w, &b.proj_b, active(b.lproj), scale, training, dropout_ctr)
+                    : lora_linear_aug(o, C, b.proj_w, &b.proj_b, active(b.lproj), scale, b.waug_proj, training, dropout_ctr);
     auto r2 = add_norm(x, a, b.ln2_w, &b.ln2_b, cfg_.eps, false, 0.f, 0);
     x = r2.first;
     // MLP
@@ -459,6 +475,7 @@ Tensor GPT2::hidden(const Tensor& ids) {
     auto r1 = add_norm(x, f, *nw, nb, cfg_.eps, false, 0.f, oc);
     x = r1.first;
     h = r1.second;
+    if (st) std::tie(x, h) = streamer_->gate(x, h, i);
   }
   return h;
 }

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "engine/lm.h"
+#include "engine/weight_stream.h"
 
 namespace mft {
 namespace eng {
@@ -71,6 +72,10 @@ class GPT2 : public LanguageModel {
   void merge_lora(float sign);
   const LoraSpec& lora_spec() const { return spec_; }
   size_t num_parameters() const override;
+  // --shard_enable: every block's frozen weights into the host tier, streamed through device slots
+  // within budget_bytes (weight_stream.h); LoRA projections then take the plain (non-augmented) path
+  void enable_weight_streaming(size_t budget_bytes);
+  const WeightStreamer* streamer() const { return streamer_.get(); }
 
  private:
   void alloc();
@@ -79,6 +84,7 @@ class GPT2 : public LanguageModel {
   bool lora_ = false, full_ = false;
   Param wte_, wpe_, lnf_w_, lnf_b_;
   std::vector<GPT2Block> blocks_;
+  std::unique_ptr<WeightStreamer> streamer_;
   void make_trainable(Param& p);
 };
 

@@ -36,6 +36,7 @@ Tensor gbuf(Param* p) {
 }  // namespace
 
 const Tensor& Param::transposed() {
+  MFT_CHECK(!streamed, "Param::transposed: a streamed weight has no resident transposed copy");
   if (!wt.defined()) {
     NoGradGuard ng;
     wt = c.t().contiguous();
@@ -485,7 +486,7 @@ Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2) {
       Gemm8Extra e2;
       Tensor aux = pre;
       e2.aux = &aux;
-      if (!p2->trainable()) gemm8_call(dy2, p2->transposed(), false, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
+      if (!p2->trainable() && !p2->streamed) gemm8_call(dy2, p2->transposed(), false, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
       else gemm8_call(dy2, p2->c, true, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
       Tensor dx = empty({M, K}, DType::BF16, dy2.device());
       gemm_nn(dpre, p1->c, dx);

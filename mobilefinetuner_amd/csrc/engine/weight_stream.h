@@ -1,0 +1,61 @@
+// libmft engine: frozen-weight streaming for `--shard_enable` (host-DRAM weight tier).
+//
+// Reference: ParameterSharder (operators/opt_ops/sharding/parameter_sharder.h:36-93, .cpp:86-276):
+// register_parameter drops the RAM copy to disk, require(name) reloads it under a byte budget with
+// LRU eviction, called from the model forward per block (graph/gpt2_model.cpp:536-554).
+//
+// MI355X design (native engine): each transformer block's frozen bf16 weights are ONE contiguous
+// pinned host buffer; K device slots (K = budget / largest block, at least 2) hold the blocks in
+// use, block i always in slot i % K, so every Param of a streamed block is a fixed view into its
+// slot and the whole schedule is static -- it records into the trainer's hipGraph like any other
+// work.  ensure(i, next) makes block i resident (one H2D copy on a dedicated copy stream, ordered
+// after every kernel that used the slot before through an event recorded on the compute stream)
+// and prefetches `next` into its own slot while block i computes.  The forward walks the blocks up,
+// a gate node at each block boundary re-loads the block on the way back down in the backward.
+// Embeddings, norms and trainable (LoRA) parameters stay resident.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "engine/nn.h"
+
+namespace mft {
+namespace eng {
+
+class WeightStreamer {
+ public:
+  // groups[i]: the frozen bf16 Params of block i (re-bound to slot views; their device copies freed)
+  WeightStreamer(const std::vector<std::vector<Param*>>& groups, size_t budget_bytes);
+  ~WeightStreamer();
+  WeightStreamer(const WeightStreamer&) = delete;
+  WeightStreamer& operator=(const WeightStreamer&) = delete;
+  // block g resident before the current stream's next kernel; prefetch block `next` (-1: none)
+  void ensure(int g, int next);
+  // identity on (x, h) whose backward calls ensure(g, g - 1) before block g's backward runs
+  std::pair<Tensor, Tensor> gate(const Tensor& x, const Tensor& h, int g);
+  int slots() const { return (int)slot_.size(); }
+  size_t device_bytes() const { return slot_bytes_ * slot_.size(); }
+  size_t host_bytes() const { return host_bytes_; }
+  int64_t copies = 0;  // H2D group copies issued (a graph replay repeats its recorded ones)
+
+ private:
+  void issue(int g);
+  struct Group {
+    std::vector<Param*> ps;
+    std::vector<int64_t> off;  // element offsets inside the slot
+    Tensor host;               // pinned bf16 [elems]
+    int64_t elems = 0;
+  };
+  std::vector<Group> groups_;
+  std::vector<Tensor> slot_;
+  std::vector<int> holder_;  // group whose copy was last issued into each slot (-1: none)
+  std::vector<hipEvent_t> ready_;
+  hipEvent_t order_ = nullptr;
+  hipStream_t copy_ = nullptr;
+  size_t slot_bytes_ = 0, host_bytes_ = 0;
+  bool capturing_ = false;
+};
+
+}  // namespace eng
+}  // namespace mft

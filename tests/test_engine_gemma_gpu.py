@@ -167,3 +167,22 @@ def test_native_gemma_eval_ppl_matches_python_cli(tmp_path):
         assert abs(nat["ppl"] - py["ppl"]) < 2e-3 * py["ppl"], (merge, nat, py)
         ppl[merge] = nat["ppl"]
     assert abs(ppl["1"] - ppl["0"]) < 5e-3 * ppl["0"], ppl
+
+
+def test_native_gemma_weight_streaming_matches_resident():
+    """train_lora_gemma --shard_enable: the layers' frozen projections stream from pinned host memory
+    through 2 device slots (3 layers), graph-captured and eager, with the resident run's losses."""
+    common = ["--random_init", "--model", "gemma3-tiny", "--synthetic_data", "--synthetic_tokens", "50000",
+              "--max_steps", "5", "--batch", "4", "--seq_len", "64", "--lr", "2e-3", "--warmup_ratio", "0",
+              "--lora_dropout", "0", "--log_interval", "1", "--deterministic", "--eval_batches", "1"]
+
+    def losses(extra):
+        r = subprocess.run([_bin("train_lora_gemma"), *common, *extra], capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        return [float(line.split("Loss=")[1].split()[0]) for line in r.stdout.splitlines() if "Loss=" in line], r.stdout
+
+    ref, _ = losses([])
+    for extra in ([], ["--no_graph"]):
+        got, out = losses(["--shard_enable", "--shard_budget_mb", "1", *extra])
+        assert "weight streaming ON: 2 device slots" in out, out[-2000:]
+        assert len(got) == 5 and got == pytest.approx(ref, abs=2e-3), (extra, got, ref)

@@ -215,3 +215,22 @@ def test_native_eval_ppl_matches_python_cli(tmp_path):
     print(nat, py)
     assert nat["tokens"] == py.get("tokens", py.get("n_tokens", nat["tokens"]))
     assert abs(nat["ppl"] - py["ppl"]) < 2e-3 * py["ppl"], (nat, py)
+
+
+def test_native_weight_streaming_matches_resident():
+    """--shard_enable in the native CLI: GPT-2's frozen block weights in pinned host memory, streamed
+    through 2 device slots (40 MB budget, 14 MB per block) with prefetch and backward re-loads, in the
+    hipGraph-captured step and eagerly -- the same per-step losses as the resident run."""
+    common = ["--random_init", "--model", "gpt2", "--synthetic_data", "--synthetic_tokens", "200000", "--steps", "6",
+              "--batch_size", "4", "--seq_len", "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic"]
+
+    def losses(extra):
+        r = subprocess.run([_bin("gpt2_lora_finetune"), *common, *extra], capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        return [float(line.split("Loss=")[1].split()[0]) for line in r.stdout.splitlines() if "Loss=" in line], r.stdout
+
+    ref, _ = losses([])
+    for extra in ([], ["--no_graph"]):
+        got, out = losses(["--shard_enable", "--shard_budget_mb", "40", *extra])
+        assert "weight streaming ON: 2 device slots" in out, out[-2000:]
+        assert len(got) == 6 and got == pytest.approx(ref, abs=2e-3), (extra, got, ref)
