@@ -407,6 +407,7 @@ void Gemma3::save_lora(const std::string& path) {
 
 void Gemma3::merge_lora(float sign) {
   NoGradGuard ng;
+  MFT_CHECK(!streamer_, "merge_lora: streamed weights are re-loaded from the host tier (merge before enable_weight_streaming)");
   lora_enabled = sign < 0;
   auto merge = [&](Param& w, std::vector<LoraAdapter>& ads) {
     for (auto& a : ads) {

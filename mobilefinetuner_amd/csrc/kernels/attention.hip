@@ -469,8 +469,8 @@ __global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __re
       st[kb][i] = sv;
       mx = fmaxf(mx, sv);
     }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = fmaxf(mx, xor16_pl(mx));
+  mx = fmaxf(mx, xor32_pl(mx));
   const float ms = mx == -INFINITY ? 0.f : mx;
   float rs = 0.f;
 #pragma unroll
@@ -481,8 +481,8 @@ __global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __re
       st[kb][i] = p;
       rs += p;
     }
-  rs += __shfl_xor(rs, 16, 64);
-  rs += __shfl_xor(rs, 32, 64);
+  rs += xor16_pl(rs);
+  rs += xor32_pl(rs);
   // O = P V over 32-key steps; P's A fragment comes straight from two S^T blocks
   f32x4_t acc[D / 16];
 #pragma unroll
@@ -779,8 +779,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
           st[t][i] = sv;
           mx = fmaxf(mx, sv);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = fmaxf(mx, xor16_pl(mx));
+      mx = fmaxf(mx, xor32_pl(mx));
       const float mnew = fmaxf(m, mx);
       const float msafe = mnew == -INFINITY ? 0.f : mnew;
       const float alpha = fast_exp2(m - msafe);
@@ -793,8 +793,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
           st[t][i] = p;
           rs += p;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs += xor16_pl(rs);
+      rs += xor32_pl(rs);
       l = l * alpha + rs;
       m = mnew;
       // acc rows are queries 4 g + i: their alpha lives in lane 4 g + i (C column = that query)
@@ -884,16 +884,6 @@ __device__ __forceinline__ bf16x8_t frag_tr_perm_sw(const bf16_t* t, int r0, int
   return __builtin_bit_cast(bf16x8_t, rr);
 }
 
-// cross-row-group exchanges as VALU permlane swaps (no LDS round trip, unlike ds_bpermute shuffles):
-// value of lane l ^ 16 / l ^ 32
-__device__ __forceinline__ float xor16_pl(float x) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(((threadIdx.x >> 4) & 1) ? r[0] : r[1]);
-}
-__device__ __forceinline__ float xor32_pl(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(((threadIdx.x >> 5) & 1) ? r[0] : r[1]);
-}
 
 template <int D, int NW>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(

@@ -382,8 +382,8 @@ __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc
             if (c + e < g.ce_V) m = fmaxf(m, o[q][i][e]);
         }
       }
-      m = fmaxf(m, __shfl_xor(m, 16));
-      m = fmaxf(m, __shfl_xor(m, 32));
+      m = fmaxf(m, xor16_pl(m));
+      m = fmaxf(m, xor32_pl(m));
       mt[qa][i] = m;
     }
   const int rl0 = wm * 64 + r16;  // tile row = qa * 128 + rl0 + 16 i
@@ -436,8 +436,8 @@ __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc
         }
         if (g.C && rok && c < g.N) store8(reinterpret_cast<bf16_t*>(g.C) + (long)R * g.ldc + c, o[q][i]);
       }
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
+      s += xor16_pl(s);
+      s += xor32_pl(s);
       st[qa][i] = s;
     }
   if (g4 == 0) {

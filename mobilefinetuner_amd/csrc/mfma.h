@@ -71,4 +71,15 @@ __device__ __forceinline__ bf16x8_t frag_tr_perm(const bf16_t* base, int ld, int
 
 __device__ __forceinline__ f32x4_t zero4() { return f32x4_t{0.f, 0.f, 0.f, 0.f}; }
 
+// cross-row-group exchanges as VALU permlane swaps (no LDS round trip, unlike ds_bpermute shuffles):
+// value of lane l ^ 16 / l ^ 32
+__device__ __forceinline__ float xor16_pl(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(((threadIdx.x >> 4) & 1) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xor32_pl(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(((threadIdx.x >> 5) & 1) ? r[0] : r[1]);
+}
+
 }  // namespace mft
