@@ -100,6 +100,9 @@ struct GemmArgs {
   const float* ce_fin;
   const float* ce_wlab;
   int ce_V;
+  // gemm8: 1 = compute the (A*, B1) quadrants of an N-tail tile anyway (set by gemm8x from
+  // MFT_GEMM8_NTAIL=0 for A/B runs; the CE dgrad never skips them)
+  int ntail_full;
 };
 bool gemm_supported(int M, int N, int K);
 // cfg: tile configuration (gemm.hip launch_e): 0 = 256x256, 1 = 128x256, 2 = 128x128, 3 = 256x128

@@ -630,6 +630,13 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   // is restaged >= 1 phase after its last read and read >= 1 phase after the wait that retires it,
   // which holds for both groups with a one-barrier offset.
   if (wm == 1) raw_barrier();
+  // N tail: when the tile's upper 128 columns lie wholly past N (N % 256 in (0, 128], e.g. Gemma-3's
+  // d_model 640 -> 3rd column tile, or GPT-2's 50304-wide LM head), the (A*, B1) quadrants only
+  // produce columns that are never stored: their B1 fragment reads and MFMAs are skipped (a
+  // workgroup-uniform branch; staging and the counted waits are unchanged).  Not in the CE dgrad:
+  // there the three column tiles of a row block stream the same 34 GB E operand in lockstep through
+  // L2, and a faster third tile breaks that sharing (measured 21.9 -> 23.2 ms at Gemma-3's shape).
+  const bool b1_ok = EPI == GEMM_EPI_CE_DGRAD || g.ntail_full || n0 + 128 < g.N;
 
   for (int kt = 0; kt < nk; kt += 2) {
     const bool odd_ok = kt + 1 < nk;  // the odd K-tile of this iteration exists
@@ -644,12 +651,12 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     mma_ce(0, rq0);
     raw_barrier();
     // phase 2: (A0, B1); stage O.B0 (kt+1)
-    read_b(0, 1);
+    if (b1_ok) read_b(0, 1);
     const f32x4_t rq1 = ce_read(1, kt);
     stage(1, 2, kt + 1);
     lds_sync();
     raw_barrier();
-    mma_ce(1, rq1);
+    if (b1_ok) mma_ce(1, rq1);
     raw_barrier();
     // phase 3: (A1, B1); stage E.A0 (kt+2)
     read_a(0, 1);
@@ -657,7 +664,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     stage(0, 0, kt + 2);
     lds_sync();
     raw_barrier();
-    mma_ce(2, rq2);
+    if (b1_ok) mma_ce(2, rq2);
     raw_barrier();
     // phase 4: (A1, B0); stage E.B1 (kt+2); retire the odd buffer
     read_b(0, 0);
@@ -679,18 +686,18 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     if (odd_ok) mma(0);
     raw_barrier();
     // phase 6: (A0, B1); stage E.B0 (kt+2)
-    read_b(1, 1);
+    if (b1_ok) read_b(1, 1);
     stage(0, 2, kt + 2);
     lds_sync();
     raw_barrier();
-    if (odd_ok) mma(1);
+    if (odd_ok && b1_ok) mma(1);
     raw_barrier();
     // phase 7: (A1, B1); stage O.A0 (kt+3)
     read_a(1, 1);
     stage(1, 0, kt + 3);
     lds_sync();
     raw_barrier();
-    if (odd_ok) mma(2);
+    if (odd_ok && b1_ok) mma(2);
     raw_barrier();
     // phase 8: (A1, B0); stage O.B1 (kt+3); retire the even buffer
     read_b(1, 0);
@@ -1000,8 +1007,19 @@ bool gemm8_supported(int M, int N, int K, bool a_t, bool b_t) {
   return true;
 }
 
+// MFT_GEMM8_NTAIL=0 turns the N-tail quadrant skip off (A/B runs)
+static int gemm8_ntail_full() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MFT_GEMM8_NTAIL");
+    v = (e && e[0] == '0') ? 1 : 0;
+  }
+  return v;
+}
+
 void gemm8x(const GemmArgs& g0, int epi, bool a_t, bool b_t, hipStream_t st) {
   GemmArgs g = g0;
+  g.ntail_full = gemm8_ntail_full();
   // per-lane staging offsets are 32-bit byte offsets from a uniform base (128 rows x ld x 2 B)
   if (!gemm8_supported(g.M, g.N, g.K, a_t, b_t) || g.lda > (1L << 23) || g.ldb > (1L << 23)) {
     fprintf(stderr, "mft::gemm8: unsupported shape M=%d N=%d K=%d (a_t=%d b_t=%d)\n", g.M, g.N, g.K, a_t, b_t);

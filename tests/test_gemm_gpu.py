@@ -1,5 +1,6 @@
 """gemm8 in every operand layout (NT forward, NN data-grad, TN split-K weight-grad) at the
-production M = 65536 GPT-2 shapes, against an fp32 PyTorch reference (relative tolerances)."""
+production M = 65536 GPT-2 and Gemma-3 shapes, against an fp32 PyTorch reference (relative
+tolerances).  N = 640 / 8 / 120 exercise the N-tail path that skips the (A*, B1) quadrants."""
 import pytest
 import torch
 
@@ -23,7 +24,7 @@ def relerr(a, b):
 
 
 @pytest.mark.parametrize("M,K,N", [(65536, 768, 2304), (65536, 3072, 768), (65536, 768, 50304), (1000, 832, 776),
-                                   (300, 64, 8)])
+                                   (300, 64, 8), (65536, 1024, 640), (777, 128, 120)])
 def test_gemm8_nt(M, K, N):
     g = torch.Generator(device="cuda").manual_seed(1)
     x, w, b = rnd(M, K, gen=g), rnd(N, K, s=0.05, gen=g), rnd(N, s=0.5, gen=g)
@@ -33,7 +34,7 @@ def test_gemm8_nt(M, K, N):
 
 
 @pytest.mark.parametrize("M,K,N", [(65536, 3072, 768), (65536, 768, 3072), (65536, 2304, 768), (8192, 50304, 768),
-                                   (1000, 832, 776)])
+                                   (1000, 832, 776), (65536, 2048, 640), (8192, 262144, 640)])
 def test_gemm8_nn(M, K, N):
     g = torch.Generator(device="cuda").manual_seed(2)
     dy, w = rnd(M, K, gen=g), rnd(K, N, s=0.05, gen=g)
@@ -56,7 +57,7 @@ def test_gemm8_nn_dgelu_and_lora():
 
 
 @pytest.mark.parametrize("T,P,Q", [(65536, 2304, 768), (65536, 768, 3072), (65536, 3072, 768), (4096, 776, 136),
-                                   (65536, 768, 50304)])
+                                   (65536, 768, 50304), (65536, 2048, 640)])
 def test_gemm8_tn_wgrad_splitk(T, P, Q):
     """dW[P, Q] += dy[T, P]^T x[T, Q] in fp32 (split-K slabs + deterministic reduce)."""
     g = torch.Generator(device="cuda").manual_seed(4)
@@ -89,3 +90,13 @@ def test_gemm8_gelu_mlp_epilogues():
     dy, w2 = rnd(M, K, gen=g), rnd(K, N, s=0.05, gen=g)
     y = C().gemm_t(dy, w2, False, True, EPI_MUL_AUX, aux=d)[0]
     assert relerr(y, (dy.float() @ w2.float()) * d.float()) < 1e-2
+
+
+def test_gemm8_lora_epilogue_n_tail():
+    """NT + fused rank-16 LoRA update at Gemma-3's d_model 640 output width (3rd column tile half empty)."""
+    g = torch.Generator(device="cuda").manual_seed(6)
+    M, K, N = 65536, 1024, 640
+    x, w = rnd(M, K, gen=g), rnd(N, K, s=0.05, gen=g)
+    u, lw = rnd(M, 16, gen=g), rnd(16, N, s=0.1, gen=g)
+    y = C().gemm_t(x, w, False, False, EPI_LORA, lora_u=u, lora_w=lw)[0]
+    assert relerr(y, x.float() @ w.float().t() + u.float() @ lw.float()) < 1e-2
