@@ -1088,9 +1088,10 @@ class _LMHeadCE(Function):
 @_device_op
 def lm_head_cross_entropy(h, w, labels, vocab_size, chunk=None, w_grad_scale=1.0):
     """Mean token NLL of logits = h W^T (W [Vpad, C], first vocab_size rows real) vs labels
-    (already shifted; -100 = ignore).  Logits never reach HBM: per chunk of rows the gemm8 forward
-    epilogue reduces them to per-tile softmax statistics (+ E = exp(logit - tile max)) and the NN
-    dgrad consumes E with a per-tile accumulator rescale (see ``_LMHeadCE``).
+    (already shifted; -100 = ignore).  No raw / fp32 logits reach HBM: per chunk of rows the gemm8
+    forward epilogue reduces them to per-tile softmax statistics and (training only) stores
+    E = exp(logit - tile max) in bf16 -- one [rows, Vpad] bf16 buffer, the size of bf16 logits --
+    which the NN dgrad consumes once with a per-tile accumulator rescale (see ``_LMHeadCE``).
     NOTE: the W gradient is produced during forward and scaled by ``w_grad_scale`` (pass the
     same factor the loss is later multiplied by, e.g. 1/grad_accum); dh honours grad_output."""
     if chunk is None:
