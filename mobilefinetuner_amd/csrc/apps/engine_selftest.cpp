@@ -72,6 +72,20 @@ std::vector<double> numgrad(const std::function<double(const std::vector<double>
   }
   return g;
 }
+// tape gradient of sum(f(x) * c) with respect to x vs central differences of the same device ops
+void gradcheck(const std::string& name, const std::vector<double>& x0, Shape shape,
+               const std::function<Tensor(const Tensor&)>& f, double tol = 3e-3) {
+  Tensor tx = dev(x0, shape);
+  tx.requires_grad_(true);
+  Tensor y = f(tx);
+  Tensor tc = dev(rnd((size_t)y.numel()), y.shape());
+  sum(mul(y, tc)).backward();
+  auto fn = [&](const std::vector<double>& xv) {
+    NoGradGuard ng;
+    return host(sum(mul(f(dev(xv, shape)), tc)))[0];
+  };
+  check(name, host(tx.grad()), numgrad(fn, x0), tol);
+}
 }  // namespace
 
 int main() {
@@ -279,6 +293,102 @@ int main() {
     check("linear backward dx", host(x2.grad()), gx, 1e-5);
     check("linear backward dW", host(w2.grad()), gw, 1e-5);
     check("linear backward db", host(b2.grad()), gb, 1e-5);
+  }
+  // ---------------------------------------------------------------- composite catalog layers
+  {
+    const int R = 5, C = 16;
+    auto x = rnd(R * C, -2, 2), w = rnd(C), b = rnd(C);
+    Tensor tw = dev(w, {C}), tb = dev(b, {C});
+    std::vector<double> ln(R * C), rms(R * C);
+    for (int r = 0; r < R; ++r) {
+      double mu = 0, ss = 0, ms = 0;
+      for (int j = 0; j < C; ++j) mu += x[r * C + j] / C;
+      for (int j = 0; j < C; ++j) ss += (x[r * C + j] - mu) * (x[r * C + j] - mu) / C;
+      for (int j = 0; j < C; ++j) ms += x[r * C + j] * x[r * C + j] / C;
+      for (int j = 0; j < C; ++j) {
+        ln[r * C + j] = (x[r * C + j] - mu) / std::sqrt(ss + 1e-5) * w[j] + b[j];
+        rms[r * C + j] = x[r * C + j] / std::sqrt(ms + 1e-6) * (1.0 + w[j]);
+      }
+    }
+    check("layer_norm (composite)", host(layer_norm(dev(x, {R, C}), tw, tb)), ln, 1e-5);
+    check("rms_norm(1 + w) (composite)", host(rms_norm(dev(x, {R, C}), tw)), rms, 1e-5);
+    gradcheck("layer_norm backward vs numeric", x, {R, C}, [&](const Tensor& t) { return layer_norm(t, tw, tb); });
+    gradcheck("rms_norm backward vs numeric", x, {R, C}, [&](const Tensor& t) { return rms_norm(t, tw); });
+    const int N = 8, F = 6;
+    auto bx = rnd(N * F, -2, 2), gm = rnd(F), bt = rnd(F);
+    Tensor tg = dev(gm, {F}), tbt = dev(bt, {F});
+    std::vector<double> bn(N * F);
+    for (int j = 0; j < F; ++j) {
+      double mu = 0, var = 0;
+      for (int i = 0; i < N; ++i) mu += bx[i * F + j] / N;
+      for (int i = 0; i < N; ++i) var += (bx[i * F + j] - mu) * (bx[i * F + j] - mu) / N;
+      for (int i = 0; i < N; ++i) bn[i * F + j] = (bx[i * F + j] - mu) / std::sqrt(var + 1e-5) * gm[j] + bt[j];
+    }
+    check("batch_norm (training stats)", host(batch_norm(dev(bx, {N, F}), tg, tbt)), bn, 1e-5);
+    gradcheck("batch_norm backward vs numeric", bx, {N, F}, [&](const Tensor& t) { return batch_norm(t, tg, tbt); });
+    auto gt = rnd(64, -3, 3), up = rnd(64);
+    Tensor tu = dev(up, {4, 16});
+    std::vector<double> sw(64), gg(64);
+    for (int i = 0; i < 64; ++i) {
+      const double v = gt[i];
+      sw[i] = v / (1 + std::exp(-v)) * up[i];
+      gg[i] = 0.5 * v * (1 + std::tanh(0.7978845608028654 * (v + 0.044715 * v * v * v))) * up[i];
+    }
+    check("swiglu", host(swiglu(dev(gt, {4, 16}), tu)), sw, 1e-4);
+    check("geglu", host(geglu(dev(gt, {4, 16}), tu)), gg, 1e-4);
+    gradcheck("swiglu backward (gate) vs numeric", gt, {4, 16}, [&](const Tensor& t) { return swiglu(t, tu); });
+    // masked softmax: causal + sliding window 3, Sq = 5 queries over Sk = 7 keys (2 cached)
+    const int Sq = 5, Sk = 7, Wn = 3;
+    auto sc = rnd(Sq * Sk, -2, 2);
+    std::vector<double> msm(Sq * Sk, 0.0);
+    for (int i = 0; i < Sq; ++i) {
+      double m = -1e30, z = 0;
+      auto ok = [&](int j) { return j <= i + (Sk - Sq) && i + (Sk - Sq) - j < Wn; };
+      for (int j = 0; j < Sk; ++j)
+        if (ok(j)) m = std::max(m, sc[i * Sk + j]);
+      for (int j = 0; j < Sk; ++j)
+        if (ok(j)) z += std::exp(sc[i * Sk + j] - m);
+      for (int j = 0; j < Sk; ++j) msm[i * Sk + j] = ok(j) ? std::exp(sc[i * Sk + j] - m) / z : 0.0;
+    }
+    check("causal_mask(window) + apply_mask + softmax",
+          host(softmax(apply_mask(dev(sc, {Sq, Sk}), causal_mask(Sq, Sk, Wn)))), msm, 1e-5);
+    // GQA repeat: [2, 3, 2, 4] -> [2, 3, 6, 4]
+    auto kv = rnd(2 * 3 * 2 * 4);
+    std::vector<double> rk(2 * 3 * 6 * 4);
+    for (int b = 0; b < 2; ++b)
+      for (int t = 0; t < 3; ++t)
+        for (int hq = 0; hq < 6; ++hq)
+          for (int d = 0; d < 4; ++d) rk[((b * 3 + t) * 6 + hq) * 4 + d] = kv[((b * 3 + t) * 2 + hq / 3) * 4 + d];
+    check("repeat_kv (GQA 3:1)", host(repeat_kv(dev(kv, {2, 3, 2, 4}), 3)), rk, 1e-6);
+    gradcheck("repeat_kv backward vs numeric", kv, {2, 3, 2, 4}, [&](const Tensor& t) { return repeat_kv(t, 3); });
+    // RoPE on [B = 2, S = 3, H = 2, D = 8], both pair layouts
+    const int RB = 2, RS = 3, RH = 2, RD = 8, hh = RD / 2;
+    auto rx = rnd(RB * RS * RH * RD);
+    std::vector<double> cs(RS * hh), sn(RS * hh);
+    for (int t = 0; t < RS; ++t)
+      for (int i = 0; i < hh; ++i) {
+        const double ang = t * std::pow(10000.0, -2.0 * i / RD);
+        cs[t * hh + i] = std::cos(ang);
+        sn[t * hh + i] = std::sin(ang);
+      }
+    Tensor tcs = dev(cs, {RS, hh}), tsn = dev(sn, {RS, hh});
+    std::vector<double> rh(rx.size()), ri(rx.size());
+    for (int b = 0; b < RB; ++b)
+      for (int t = 0; t < RS; ++t)
+        for (int hd = 0; hd < RH; ++hd) {
+          const int o = ((b * RS + t) * RH + hd) * RD;
+          for (int i = 0; i < hh; ++i) {
+            const double c = cs[t * hh + i], sv = sn[t * hh + i];
+            rh[o + i] = rx[o + i] * c - rx[o + i + hh] * sv;
+            rh[o + i + hh] = rx[o + i + hh] * c + rx[o + i] * sv;
+            ri[o + 2 * i] = rx[o + 2 * i] * c - rx[o + 2 * i + 1] * sv;
+            ri[o + 2 * i + 1] = rx[o + 2 * i + 1] * c + rx[o + 2 * i] * sv;
+          }
+        }
+    check("apply_rope rotate-half", host(apply_rope(dev(rx, {RB, RS, RH, RD}), tcs, tsn, false)), rh, 1e-5);
+    check("apply_rope interleaved", host(apply_rope(dev(rx, {RB, RS, RH, RD}), tcs, tsn, true)), ri, 1e-5);
+    gradcheck("apply_rope backward vs numeric", rx, {RB, RS, RH, RD},
+              [&](const Tensor& t) { return apply_rope(t, tcs, tsn, true); });
   }
   // ---------------------------------------------------------------- allocator
   {

@@ -511,6 +511,66 @@ Tensor where_mask(const Tensor& mask, const Tensor& a, float fill) {
   return r;
 }
 
+// ------------------------------------------------------------------ composite catalog layers
+Tensor layer_norm(const Tensor& x, const Tensor& w, const Tensor& b, float eps) {
+  Tensor xc = sub(x, mean(x, -1, true));
+  Tensor y = mul(mul(xc, rsqrt(add_scalar(mean(square(xc), -1, true), eps))), w);
+  return b.defined() ? add(y, b) : y;
+}
+
+Tensor rms_norm(const Tensor& x, const Tensor& w, float eps, float offset) {
+  Tensor y = mul(x, rsqrt(add_scalar(mean(square(x), -1, true), eps)));
+  return mul(y, offset != 0.f ? add_scalar(w, offset) : w);
+}
+
+Tensor batch_norm(const Tensor& x, const Tensor& gamma, const Tensor& beta, float eps) {
+  MFT_CHECK(x.dim() == 2, "batch_norm: x must be [N, C]");
+  Tensor xc = sub(x, mean(x, 0, true));
+  Tensor y = mul(mul(xc, rsqrt(add_scalar(mean(square(xc), 0, true), eps))), gamma);
+  return beta.defined() ? add(y, beta) : y;
+}
+
+Tensor swiglu(const Tensor& gate, const Tensor& up) { return mul(silu(gate), up); }
+Tensor geglu(const Tensor& gate, const Tensor& up) { return mul(gelu(gate, true), up); }
+
+Tensor causal_mask(int64_t Sq, int64_t Sk, int64_t window) {
+  std::vector<float> m((size_t)(Sq * Sk));
+  const int64_t coff = Sk - Sq;
+  for (int64_t i = 0; i < Sq; ++i)
+    for (int64_t j = 0; j < Sk; ++j)
+      m[(size_t)(i * Sk + j)] = (j <= i + coff && (window <= 0 || i + coff - j < window)) ? 1.f : 0.f;
+  return from_vector(m, {Sq, Sk}, DType::F32);
+}
+
+Tensor apply_mask(const Tensor& scores, const Tensor& mask) { return where_mask(mask, scores, -1e30f); }
+
+Tensor repeat_kv(const Tensor& x, int n_rep) {
+  MFT_CHECK(x.dim() == 4 && n_rep >= 1, "repeat_kv: x must be [B, S, Hkv, D]");
+  if (n_rep == 1) return x;
+  Tensor u = x.unsqueeze(3);  // [B, S, Hkv, 1, D]
+  std::vector<Tensor> parts((size_t)n_rep, u);
+  return cat(parts, 3).reshape({x.size(0), x.size(1), x.size(2) * n_rep, x.size(3)});
+}
+
+Tensor apply_rope(const Tensor& x, const Tensor& cos_t, const Tensor& sin_t, bool interleaved) {
+  MFT_CHECK(x.dim() >= 3, "apply_rope: x must be [.., S, H, D]");
+  const int nd = x.dim();
+  const int64_t S = x.size(nd - 3), D = x.size(nd - 1), h = D / 2;
+  MFT_CHECK(D % 2 == 0 && cos_t.numel() == S * h && sin_t.numel() == S * h, "apply_rope: cos / sin must be [S, D/2]");
+  if (!interleaved) {
+    Tensor c = cos_t.reshape({S, 1, h}), s = sin_t.reshape({S, 1, h});
+    Tensor x1 = x.slice(nd - 1, 0, h), x2 = x.slice(nd - 1, h, D);
+    return cat({sub(mul(x1, c), mul(x2, s)), add(mul(x2, c), mul(x1, s))}, nd - 1);
+  }
+  Shape ps = x.shape();
+  ps.back() = h;
+  ps.push_back(2);
+  Tensor xp = x.reshape(ps);  // [.., S, H, D/2, 2]
+  Tensor c = cos_t.reshape({S, 1, h, 1}), s = sin_t.reshape({S, 1, h, 1});
+  Tensor x1 = xp.slice(nd, 0, 1), x2 = xp.slice(nd, 1, 2);
+  return cat({sub(mul(x1, c), mul(x2, s)), add(mul(x2, c), mul(x1, s))}, nd).reshape(x.shape());
+}
+
 Tensor embedding(const Tensor& ids, const Tensor& table) {
   MFT_CHECK(ids.dtype() == DType::I64 && table.dim() == 2, "embedding: int64 ids, [V, C] table");
   const int64_t n = ids.numel(), C = table.size(1);

@@ -89,5 +89,26 @@ Tensor cat(const std::vector<Tensor>& ts, int dim);
 Tensor where_mask(const Tensor& mask, const Tensor& a, float fill);  // mask ? a : fill (no grad on mask)
 Tensor embedding(const Tensor& ids, const Tensor& table);           // gather rows (scatter-add backward)
 
+// ---- composite layers of the reference catalog, built from the ops above (the tape differentiates
+// them); the training models run the fused kernels of nn.h instead.  Reference: layer_norm
+// core/ops.cpp:1404-1458, rms_norm / rms_norm_affine :1489-1574, batch_norm, swiglu, causal mask /
+// apply_mask and repeat_kv_heads :2072-2149, apply_rope :2151-2225.
+Tensor layer_norm(const Tensor& x, const Tensor& w, const Tensor& b, float eps = 1e-5f);  // over the last dim
+// x / rms(x) * (offset + w): offset 1 = Gemma's RMSNorm(1 + w), 0 = the affine variant
+Tensor rms_norm(const Tensor& x, const Tensor& w, float eps = 1e-6f, float offset = 1.f);
+// training-mode batch norm of x [N, C]: batch mean / biased variance per channel, then gamma, beta
+Tensor batch_norm(const Tensor& x, const Tensor& gamma, const Tensor& beta, float eps = 1e-5f);
+Tensor swiglu(const Tensor& gate, const Tensor& up);  // silu(gate) * up
+Tensor geglu(const Tensor& gate, const Tensor& up);   // gelu_tanh(gate) * up
+// [Sq, Sk] fp32 keep-mask (1 = attend): key j <= query i + (Sk - Sq), and within `window` (> 0)
+Tensor causal_mask(int64_t Sq, int64_t Sk, int64_t window = 0);
+// scores where mask == 0 -> -1e30 (finite, so a fully-masked row stays NaN-free; softmax weight 0)
+Tensor apply_mask(const Tensor& scores, const Tensor& mask);
+// GQA: [B, S, Hkv, D] -> [B, S, Hkv * n_rep, D] (q head h reads kv head h / n_rep)
+Tensor repeat_kv(const Tensor& x, int n_rep);
+// RoPE on x [.., S, H, D] with cos / sin [S, D / 2]: rotate-half pairs (d, d + D/2), or interleaved
+// pairs (2d, 2d + 1) (the reference's layout)
+Tensor apply_rope(const Tensor& x, const Tensor& cos_t, const Tensor& sin_t, bool interleaved = false);
+
 }  // namespace eng
 }  // namespace mft
