@@ -498,7 +498,8 @@ Tensor cat(const std::vector<Tensor>& ts, int dim) {
 }
 
 Tensor where_mask(const Tensor& mask, const Tensor& a, float fill) {
-  // mask * a + (1 - mask) * fill
+  // mask * a + (1 - mask) * fill: `fill` must be finite (inf * 0 would be NaN); use -1e30 for -inf
+  MFT_CHECK(std::isfinite(fill), "where_mask: fill must be finite (use e.g. -1e30 instead of -inf)");
   Tensor m = mask.to(float_of(a));
   Tensor keep = mul(a, m);
   NoGradGuard ng;

@@ -86,7 +86,7 @@ Tensor linear(const Tensor& x, const Tensor& w, const Tensor& b = Tensor());
 // ---- misc
 Tensor dropout(const Tensor& x, float p, uint64_t seed, bool training = true);
 Tensor cat(const std::vector<Tensor>& ts, int dim);
-Tensor where_mask(const Tensor& mask, const Tensor& a, float fill);  // mask ? a : fill (no grad on mask)
+Tensor where_mask(const Tensor& mask, const Tensor& a, float fill);  // mask ? a : fill (no grad on mask; finite fill)
 Tensor embedding(const Tensor& ids, const Tensor& table);           // gather rows (scatter-add backward)
 
 // ---- composite layers of the reference catalog, built from the ops above (the tape differentiates
