@@ -282,6 +282,32 @@ def test_flash_attention(B, S, H, Hkv, D, causal, window):
     _close(v.grad, vr.grad, 0.06, 0.02, msg="attn dv")
 
 
+@pytest.mark.parametrize("B,S,H,Hkv,D,window", [
+    (512, 128, 12, 12, 64, 0),   # GPT-2 124M bench step (short path)
+    (256, 256, 4, 1, 256, 0),    # Gemma-3 270M bench step, global layer (split path, GQA 4:1)
+    (256, 256, 4, 1, 256, 128),  # ... sliding-window layer (window below S so the mask is exercised)
+])
+def test_flash_attention_production_shapes(B, S, H, Hkv, D, window):
+    """Attention forward + backward at the benchmarked shapes vs the fp32 oracle (relative L2 over
+    all elements plus a max-abs bound): the per-layer launch the training steps actually run."""
+    from mobilefinetuner_amd.ops import functional as Fx
+    g = torch.Generator(device=DEV).manual_seed(11)
+    q = torch.randn(B, S, H, D, device=DEV, generator=g).bfloat16().requires_grad_()
+    k = torch.randn(B, S, Hkv, D, device=DEV, generator=g).bfloat16().requires_grad_()
+    v = torch.randn(B, S, Hkv, D, device=DEV, generator=g).bfloat16().requires_grad_()
+    scale = 1.0 / math.sqrt(D)
+    o = Fx.flash_attention(q, k, v, scale, True, window)
+    go = torch.randn(o.shape, device=DEV, generator=g)
+    (o.float() * go).sum().backward()
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf, _ = _attn_ref(qr, kr, vr, scale, True, window)
+    (orf * go).sum().backward()
+    for name, a, b in (("o", o, orf), ("dq", q.grad, qr.grad), ("dk", k.grad, kr.grad), ("dv", v.grad, vr.grad)):
+        _rel(a, b, 1e-2, msg=f"attn {name}")
+    _close(o, orf, 0.03, msg="attn o")
+    _close(v.grad, vr.grad, 0.06, 0.02, msg="attn dv")
+
+
 @pytest.mark.parametrize("nw", ["4", "8"])
 def test_flash_attention_split_kvlens_rect(nw, monkeypatch):
     """Split kernels (D = 256, GQA 4:1) with right padding and Sq < Sk (bottom-right causal), at
