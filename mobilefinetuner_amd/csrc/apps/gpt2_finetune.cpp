@@ -55,7 +55,7 @@ const std::set<std::string> kBool = {"split_qkv", "random_init", "synthetic_data
                                      "shard_enable", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
                                      "deterministic", "help"};
 const std::set<std::string> kValued = {
-    "data_dir", "pretrained_dir", "lora_out", "resume_from", "eval_out", "output_path", "epochs", "steps",
+    "data_dir", "pretrained_dir", "lora_out", "resume_from", "state_dir", "eval_out", "output_path", "epochs", "steps",
     "batch_size", "grad_accum_steps", "seq_len", "rank", "alpha", "lr", "weight_decay", "warmup_steps",
     "clip_grad_norm", "lora_dropout", "data_fraction", "log_interval", "eval_interval", "eval_batches",
     "eval_batch_size", "save_every", "ema_beta", "seed", "pm_interval", "pm_batt_thresh", "pm_temp_thresh",
@@ -106,6 +106,7 @@ void usage() {
       "  --pm_manual_batt --pm_manual_temp --pm_disable_batt --pm_disable_temp --pm_schedule --pm_gpu_telemetry\n"
       "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --pretokenized_path F\n"
       "          --pretokenized_meta F --lora_targets T --split_qkv --no_graph --compat_l2_adam --metrics_out F\n"
+      "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"
       "          --deterministic\n",
       kProg);
 }
@@ -240,8 +241,12 @@ int run(int argc, char** argv) {
   tc.use_graph = !a.b("no_graph");
   tc.eval_out = a.get("eval_out");
   tc.metrics_out = a.get("metrics_out");
+  tc.state_dir = a.get("state_dir");
   std::unique_ptr<PowerMonitor> pm = mft::apps::power_monitor_from(a);
   Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get());
+  if (!tc.state_dir.empty() && trainer.load_state(tc.state_dir))
+    std::printf("  resumed full training state from %s at step %lld / %lld\n", tc.state_dir.c_str(),
+                (long long)trainer.global_step, (long long)trainer.total_steps());
   const std::string lora_out = a.get("lora_out"), out_path = a.get("output_path");
   auto save = [&](int64_t step) {
     if (!full && !lora_out.empty()) {

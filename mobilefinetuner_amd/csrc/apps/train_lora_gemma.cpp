@@ -48,7 +48,7 @@ const std::set<std::string> kValued = {
     "epochs", "max_steps", "seq_len", "batch", "grad_accum", "lr", "learning_rate", "rank", "lora_r", "alpha",
     "lora_alpha", "lora_dropout", "warmup_ratio", "max_grad_norm", "weight_decay", "loss_reduction", "lr_schedule",
     "data_fraction", "log_interval", "eval_steps", "eval_batches", "save_every", "seed", "model", "synthetic_tokens",
-    "resume_from", "metrics_out", "eval_out", "pm_interval", "pm_batt_thresh", "pm_temp_thresh", "pm_fb_high",
+    "resume_from", "state_dir", "metrics_out", "eval_out", "pm_interval", "pm_batt_thresh", "pm_temp_thresh", "pm_fb_high",
     "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "device",
     "shard_budget_mb", "shard_dir", "shard_fp16_disk"};
 
@@ -73,7 +73,8 @@ void usage() {
       "  --weight_decay W --lr_schedule linear|cosine|constant --data_fraction F --log_interval N --eval_steps N\n"
       "  --eval_batches N --save_every N --seed S --pm_* (energy)\n"
       "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --resume_from F --no_graph\n"
-      "          --compat_l2_adam --metrics_out F --deterministic --interleaved_rope\n",
+      "          --compat_l2_adam --metrics_out F --deterministic --interleaved_rope\n"
+      "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n",
       kProg);
 }
 
@@ -190,6 +191,7 @@ int run(int argc, char** argv) {
   tc.save_every = a.i("save_every", 0);
   tc.use_graph = !a.b("no_graph");
   tc.metrics_out = a.get("metrics_out");
+  tc.state_dir = a.get("state_dir");
   tc.eval_out = a.get("eval_out");
   const std::string sched = a.get("lr_schedule", "linear");
   const float ratio = a.f("warmup_ratio", 0.03f), base = oc.lr;
@@ -197,6 +199,9 @@ int run(int argc, char** argv) {
   else tc.lr_fn = [base, ratio, sched](int64_t it, int64_t total) { return gemma_lr(it + 1, base, ratio, total, sched == "cosine"); };
   std::unique_ptr<PowerMonitor> pm = mft::apps::power_monitor_from(a);
   Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get());
+  if (!tc.state_dir.empty() && trainer.load_state(tc.state_dir))
+    std::printf("  resumed full training state from %s at step %lld / %lld\n", tc.state_dir.c_str(),
+                (long long)trainer.global_step, (long long)trainer.total_steps());
   const std::string out_dir = a.get("output_dir", "runs/gemma_lora");
   const std::string out = out_dir + "/gemma_lora.safetensors";
   if (lead) {

@@ -7,9 +7,13 @@
 #include <fstream>
 #include <thread>
 
+#include <filesystem>
+
 #include "engine/allocator.h"
 #include "engine/autograd.h"
 #include "engine/ops.h"
+#include "runtime/json.h"
+#include "runtime/safetensors.h"
 
 namespace mft {
 namespace eng {
@@ -163,7 +167,7 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
   }
   auto t_last = std::chrono::steady_clock::now();
   int64_t tok_since = 0, steps_since = 0;
-  for (int64_t it = 0; it < total_steps_; ++it) {
+  for (int64_t it = global_step; it < total_steps_; ++it) {  // global_step > 0 after load_state
     const float lr = cfg_.lr_fn ? cfg_.lr_fn(it, total_steps_) : gpt2_cli_lr(it, cfg_.lr, cfg_.warmup, total_steps_);
     opt_.set_lr(lr);
     std::vector<std::pair<const int64_t*, const int64_t*>> micro;
@@ -219,13 +223,75 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
         eo << "{\"step\": " << global_step << ", \"nll\": " << ev.first << ", \"ppl\": " << ev.second << "}\n";
       }
     }
-    if (cfg_.save_every > 0 && global_step % cfg_.save_every == 0 && save_fn && lead()) save_fn(global_step);
+    if (cfg_.save_every > 0 && global_step % cfg_.save_every == 0) {
+      if (!cfg_.state_dir.empty()) save_state(cfg_.state_dir);  // every rank (per-rank data state)
+      if (save_fn && lead()) save_fn(global_step);
+    }
     if (pm_) {
       const int ms = pm_->suggest_sleep_ms(global_step);
       if (ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(ms));
     }
   }
   synchronize();
+  if (!cfg_.state_dir.empty()) save_state(cfg_.state_dir);
+}
+
+// ------------------------------------------------------------------ full-state checkpoint
+void Trainer::save_state(const std::string& dir) {
+  synchronize();
+  const int r = comm_ ? comm_->rank() : 0;
+  std::filesystem::create_directories(dir);
+  if (r == 0) {
+    const Tensor mh = flat_.master.to(Device::cpu()), m1 = opt_.m.to(Device::cpu()), m2 = opt_.v.to(Device::cpu());
+    const size_t nb = (size_t)flat_.numel * sizeof(float);
+    safetensors_save(dir + "/trainable.safetensors", {{"master", "F32", {flat_.numel}, mh.data_ptr(), nb}},
+                     {{"format", "mft-flat"}}, false, true);
+    safetensors_save(dir + "/optimizer.safetensors",
+                     {{"m", "F32", {flat_.numel}, m1.data_ptr(), nb}, {"v", "F32", {flat_.numel}, m2.data_ptr(), nb}},
+                     {{"format", "mft-flat"}}, false, true);
+  }
+  std::ofstream f(dir + "/trainer_state.rank" + std::to_string(r) + ".json");
+  f.precision(17);
+  f << "{\"global_step\": " << global_step << ", \"opt_step\": " << opt_.applied_steps()
+    << ", \"total_tokens\": " << total_tokens << ", \"ema_loss\": " << ema_loss
+    << ", \"ema_init\": " << (ema_init ? 1 : 0) << ", \"total_steps\": " << total_steps_
+    << ", \"numel\": " << flat_.numel << ", \"dropout_ctr\": " << (int64_t)model_.dropout_ctr.item()
+    << ", \"data\": {\"epoch\": " << train_.epoch() << ", \"cursor\": " << train_.cursor() << ", \"rng\": "
+    << json::escape(train_.rng_state()) << "}}\n";
+  MFT_CHECK(f.good(), "save_state: cannot write ", dir);
+  f.close();
+  if (comm_) comm_->barrier(stream_);
+}
+
+bool Trainer::load_state(const std::string& dir) {
+  const int r = comm_ ? comm_->rank() : 0;
+  std::string sp = dir + "/trainer_state.rank" + std::to_string(r) + ".json";
+  if (!std::filesystem::exists(sp)) sp = dir + "/trainer_state.rank0.json";
+  if (!std::filesystem::exists(sp)) return false;
+  std::ifstream f(sp);
+  const std::string txt((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  const json::Value st = json::parse(txt);
+  MFT_CHECK(st["numel"].as_int() == flat_.numel, "load_state: ", dir, " holds ", st["numel"].as_int(),
+            " trainable values, the model has ", flat_.numel);
+  SafeTensorsFile tw(dir + "/trainable.safetensors"), to(dir + "/optimizer.safetensors");
+  auto host_view = [&](SafeTensorsFile& sf, const char* k) {
+    MFT_CHECK(sf.has(k) && sf.info(k).dtype == "F32" && sf.info(k).end - sf.info(k).begin == (uint64_t)flat_.numel * 4,
+              "load_state: bad tensor ", k, " in ", sf.path());
+    return from_blob(const_cast<void*>(sf.data(k)), {flat_.numel}, DType::F32, Device::cpu());
+  };
+  flat_.master.copy_(host_view(tw, "master"));
+  opt_.load_state(host_view(to, "m"), host_view(to, "v"), st["opt_step"].as_int());
+  synchronize();  // the mmaps go away with the files
+  flat_.refresh_shadow();
+  global_step = st["global_step"].as_int();
+  total_tokens = st["total_tokens"].as_int();
+  ema_loss = st["ema_loss"].as_double();
+  ema_init = st["ema_init"].as_int() != 0;
+  model_.dropout_ctr.fill_((double)st["dropout_ctr"].as_int());
+  const json::Value& d = st["data"];
+  train_.restore(d["epoch"].as_int(), (size_t)d["cursor"].as_int(), d["rng"].as_string());
+  synchronize();
+  return true;
 }
 
 }  // namespace eng

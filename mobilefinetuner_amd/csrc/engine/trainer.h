@@ -37,6 +37,7 @@ struct TrainConfig {
   float ema_beta = 0.9f;
   bool use_graph = true;
   std::string eval_out, metrics_out;
+  std::string state_dir;  // full training-state checkpoint written at every save point and at the end
   int pm_interval = 0;
   // learning rate of 0-indexed update `it` of `total`; unset: the GPT-2 CLI schedule (gpt2_cli_lr)
   std::function<float(int64_t it, int64_t total)> lr_fn;
@@ -54,6 +55,14 @@ class Trainer {
   Tensor step(const std::vector<std::pair<const int64_t*, const int64_t*>>& micro);
   void train(const std::function<void(int64_t)>& save_fn);
   std::pair<double, double> evaluate(int max_batches, int batch_size);  // (nll, ppl)
+  // Full training state (same directory layout as the Python CLIs' --state_dir):
+  // trainable.safetensors (fp32 master) + optimizer.safetensors (AdamW m, v) from rank 0 -- data
+  // parallelism keeps them identical on every rank -- and trainer_state.rank<r>.json per rank
+  // {global_step, applied optimizer steps, tokens, EMA, data epoch / cursor / shuffle RNG, LoRA-
+  // dropout counter}.  load_state returns false when `dir` holds no state; train() then continues
+  // from global_step with the same LR schedule position, batches and dropout masks.
+  void save_state(const std::string& dir);
+  bool load_state(const std::string& dir);
   double ema_loss = 0.0;
   bool ema_init = false;
   int64_t global_step = 0, total_tokens = 0;

@@ -234,3 +234,36 @@ def test_native_weight_streaming_matches_resident():
         got, out = losses(["--shard_enable", "--shard_budget_mb", "40", *extra])
         assert "weight streaming ON: 2 device slots" in out, out[-2000:]
         assert len(got) == 6 and got == pytest.approx(ref, abs=2e-3), (extra, got, ref)
+
+
+@pytest.mark.parametrize("prog,model,steps_flag,extra", [
+    ("gpt2_lora_finetune", "gpt2-tiny", "--steps", ["--batch_size", "4", "--warmup_steps", "100", "--lora_dropout", "0.1"]),
+    ("train_lora_gemma", "gemma3-tiny", "--max_steps", ["--batch", "4", "--lr_schedule", "constant",
+                                                        "--lora_dropout", "0.1"]),
+])
+def test_native_full_state_resume(tmp_path, prog, model, steps_flag, extra):
+    """--state_dir: 4 steps, then a fresh process resumes from the saved state (fp32 master, AdamW
+    moments + step, data cursor / shuffle RNG, EMA, LoRA-dropout counter) and runs steps 5-8; its
+    losses equal the uninterrupted 8-step run's (deterministic mode; the schedule is chosen so the
+    learning rate does not depend on the run's total step count)."""
+    common = [_bin(prog), "--random_init", "--model", model, "--synthetic_data", "--synthetic_tokens", "100000",
+              "--seq_len", "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic", *extra]
+
+    def losses(steps, state=None):
+        cmd = common + [steps_flag, str(steps)] + (["--state_dir", state] if state else [])
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        return r.stdout, {int(ln.split("/")[0].split()[1]): ln.split("Loss=")[1].split()[0]
+                          for ln in r.stdout.splitlines() if ln.startswith("[Step")}
+
+    _, ref = losses(8)
+    state = str(tmp_path / "state")
+    _, first = losses(4, state)
+    assert os.path.exists(os.path.join(state, "optimizer.safetensors"))
+    st = json.load(open(os.path.join(state, "trainer_state.rank0.json")))
+    assert st["global_step"] == 4 and st["opt_step"] == 4
+    out, second = losses(8, state)
+    assert "resumed full training state" in out
+    assert sorted(first) == [1, 2, 3, 4] and sorted(second) == [5, 6, 7, 8]
+    assert [first[i] for i in range(1, 5)] == [ref[i] for i in range(1, 5)]
+    assert [second[i] for i in range(5, 9)] == [ref[i] for i in range(5, 9)], (ref, first, second)
