@@ -55,7 +55,7 @@ const std::set<std::string> kBool = {"split_qkv", "random_init", "synthetic_data
                                      "shard_enable", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
                                      "deterministic", "help"};
 const std::set<std::string> kValued = {
-    "data_dir", "pretrained_dir", "lora_out", "resume_from", "state_dir", "eval_out", "output_path", "epochs", "steps",
+    "data_dir", "pretrained_dir", "lora_out", "resume_from", "state_dir", "inject_fault", "eval_out", "output_path", "epochs", "steps",
     "batch_size", "grad_accum_steps", "seq_len", "rank", "alpha", "lr", "weight_decay", "warmup_steps",
     "clip_grad_norm", "lora_dropout", "data_fraction", "log_interval", "eval_interval", "eval_batches",
     "eval_batch_size", "save_every", "ema_beta", "seed", "pm_interval", "pm_batt_thresh", "pm_temp_thresh",
@@ -107,6 +107,7 @@ void usage() {
       "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --pretokenized_path F\n"
       "          --pretokenized_meta F --lora_targets T --split_qkv --no_graph --compat_l2_adam --metrics_out F\n"
       "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"
+      "          --inject_fault STEP:RANK (failure test: that rank throws before that step)\n"
       "          --deterministic\n",
       kProg);
 }
@@ -242,6 +243,12 @@ int run(int argc, char** argv) {
   tc.eval_out = a.get("eval_out");
   tc.metrics_out = a.get("metrics_out");
   tc.state_dir = a.get("state_dir");
+  if (!a.get("inject_fault").empty()) {  // step:rank
+    const std::string f = a.get("inject_fault");
+    const size_t c = f.find(':');
+    tc.fault_step = std::stoll(f.substr(0, c));
+    tc.fault_rank = c == std::string::npos ? 0 : std::stoi(f.substr(c + 1));
+  }
   std::unique_ptr<PowerMonitor> pm = mft::apps::power_monitor_from(a);
   Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get());
   if (!tc.state_dir.empty() && trainer.load_state(tc.state_dir))

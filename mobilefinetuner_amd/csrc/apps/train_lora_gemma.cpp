@@ -48,7 +48,7 @@ const std::set<std::string> kValued = {
     "epochs", "max_steps", "seq_len", "batch", "grad_accum", "lr", "learning_rate", "rank", "lora_r", "alpha",
     "lora_alpha", "lora_dropout", "warmup_ratio", "max_grad_norm", "weight_decay", "loss_reduction", "lr_schedule",
     "data_fraction", "log_interval", "eval_steps", "eval_batches", "save_every", "seed", "model", "synthetic_tokens",
-    "resume_from", "state_dir", "metrics_out", "eval_out", "pm_interval", "pm_batt_thresh", "pm_temp_thresh", "pm_fb_high",
+    "resume_from", "state_dir", "inject_fault", "metrics_out", "eval_out", "pm_interval", "pm_batt_thresh", "pm_temp_thresh", "pm_fb_high",
     "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "device",
     "shard_budget_mb", "shard_dir", "shard_fp16_disk"};
 
@@ -74,7 +74,8 @@ void usage() {
       "  --eval_batches N --save_every N --seed S --pm_* (energy)\n"
       "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --resume_from F --no_graph\n"
       "          --compat_l2_adam --metrics_out F --deterministic --interleaved_rope\n"
-      "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n",
+      "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"
+      "          --inject_fault STEP:RANK (failure test: that rank throws before that step)\n",
       kProg);
 }
 
@@ -192,6 +193,12 @@ int run(int argc, char** argv) {
   tc.use_graph = !a.b("no_graph");
   tc.metrics_out = a.get("metrics_out");
   tc.state_dir = a.get("state_dir");
+  if (!a.get("inject_fault").empty()) {  // step:rank
+    const std::string f = a.get("inject_fault");
+    const size_t c = f.find(':');
+    tc.fault_step = std::stoll(f.substr(0, c));
+    tc.fault_rank = c == std::string::npos ? 0 : std::stoi(f.substr(c + 1));
+  }
   tc.eval_out = a.get("eval_out");
   const std::string sched = a.get("lr_schedule", "linear");
   const float ratio = a.f("warmup_ratio", 0.03f), base = oc.lr;

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <fstream>
+#include <stdexcept>
 #include <thread>
 
 #include <filesystem>
@@ -168,6 +169,9 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
   auto t_last = std::chrono::steady_clock::now();
   int64_t tok_since = 0, steps_since = 0;
   for (int64_t it = global_step; it < total_steps_; ++it) {  // global_step > 0 after load_state
+    if (cfg_.fault_step > 0 && it + 1 == cfg_.fault_step && (comm_ ? comm_->rank() : 0) == cfg_.fault_rank)
+      throw std::runtime_error("injected fault at step " + std::to_string(it + 1) + " on rank " +
+                               std::to_string(cfg_.fault_rank) + " (--inject_fault)");
     const float lr = cfg_.lr_fn ? cfg_.lr_fn(it, total_steps_) : gpt2_cli_lr(it, cfg_.lr, cfg_.warmup, total_steps_);
     opt_.set_lr(lr);
     std::vector<std::pair<const int64_t*, const int64_t*>> micro;

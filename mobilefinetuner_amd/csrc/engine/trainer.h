@@ -38,6 +38,10 @@ struct TrainConfig {
   bool use_graph = true;
   std::string eval_out, metrics_out;
   std::string state_dir;  // full training-state checkpoint written at every save point and at the end
+  // failure injection (--inject_fault step:rank): rank `fault_rank` throws before
+  // running step `fault_step` (1-indexed); the CLI exits non-zero and the launcher stops the job
+  int64_t fault_step = 0;
+  int fault_rank = 0;
   int pm_interval = 0;
   // learning rate of 0-indexed update `it` of `total`; unset: the GPT-2 CLI schedule (gpt2_cli_lr)
   std::function<float(int64_t it, int64_t total)> lr_fn;

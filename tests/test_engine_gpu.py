@@ -267,3 +267,32 @@ def test_native_full_state_resume(tmp_path, prog, model, steps_flag, extra):
     assert sorted(first) == [1, 2, 3, 4] and sorted(second) == [5, 6, 7, 8]
     assert [first[i] for i in range(1, 5)] == [ref[i] for i in range(1, 5)]
     assert [second[i] for i in range(5, 9)] == [ref[i] for i in range(5, 9)], (ref, first, second)
+
+
+def test_native_fault_then_resume(tmp_path):
+    """SURVEY §5.3 failure path: --inject_fault 6:0 kills the run before step 6 (non-zero exit, the
+    state of step 4 from --save_every on disk); relaunching the same command without the fault resumes
+    at step 5 and finishes with the uninterrupted run's losses."""
+    state = str(tmp_path / "state")
+    common = [_bin("gpt2_lora_finetune"), "--random_init", "--model", "gpt2-tiny", "--synthetic_data",
+              "--synthetic_tokens", "100000", "--batch_size", "4", "--seq_len", "64", "--lr", "1e-3",
+              "--warmup_steps", "100", "--log_interval", "1", "--deterministic", "--steps", "8"]
+
+    def run(extra):
+        return subprocess.run(common + extra, capture_output=True, text=True, timeout=180)
+
+    def losses(out):
+        return {int(ln.split("/")[0].split()[1]): ln.split("Loss=")[1].split()[0]
+                for ln in out.splitlines() if ln.startswith("[Step")}
+
+    r = run([])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    ref = losses(r.stdout)
+    r = run(["--save_every", "4", "--state_dir", state, "--inject_fault", "6:0"])
+    assert r.returncode != 0 and "injected fault at step 6" in r.stderr, r.stdout[-1000:] + r.stderr[-1000:]
+    assert sorted(losses(r.stdout)) == [1, 2, 3, 4, 5]
+    assert json.load(open(os.path.join(state, "trainer_state.rank0.json")))["global_step"] == 4
+    r = run(["--save_every", "4", "--state_dir", state])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    got = losses(r.stdout)
+    assert sorted(got) == [5, 6, 7, 8] and all(got[i] == ref[i] for i in got), (ref, got)
