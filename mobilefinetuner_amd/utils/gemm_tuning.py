@@ -37,9 +37,6 @@ def enable_tuned_gemms(path: str | None = None) -> bool:
         return False
     tn.enable(True)
     tn.tuning_enable(tune)
-    # lookups only: never rewrite the shared package file at exit (N ranks of one job, or back-to-back
-    # jobs of a scaling sweep, all read this same file)
-    tn.write_file_on_exit(tune)
     if tune:
         tn.set_max_tuning_duration(30)
     tn.set_filename(path, insert_device_ordinal=False)
