@@ -40,7 +40,7 @@ BASELINE_TOKENS_PER_SEC = 170.0
 # BASELINE.json "configs" -> (model preset, mode, default micro-batch, seq, metric label)
 CONFIGS = {
     # headline: GPT-2 small LoRA r=8 seq 128 (BASELINE.json "metric")
-    "gpt2-lora": dict(model="gpt2", mode="lora", batch=512, seq=128, targets="AttnQKV,AttnProj",
+    "gpt2-lora": dict(model="gpt2", mode="lora", batch=1024, seq=128, targets="AttnQKV,AttnProj",
                       metric="tokens/sec GPT-2-124M LoRA r=8 seq128 (training, whole job)"),
     # Gemma-3 270M LoRA r=8 seq 256 (RMSNorm / QK-norm+RoPE / GQA / sliding-window kernels)
     "gemma3-270m-lora": dict(model="gemma3-270m", mode="lora", batch=256, seq=256, targets="full",
@@ -149,11 +149,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="gpt2-lora", choices=sorted(CONFIGS),
                     help="benchmark configuration (BASELINE.json configs); default = the headline metric")
-    # micro-batch default per config; for the headline 512 x 128 = 64k tokens per GPU per step: the
-    # M dimension every block GEMM sees.  Measured on 1x MI355X (same build, one call): B=256 1.32M
-    # tok/s, B=384 1.37M, B=512 1.44M, B=768 1.40M, B=1024 1.47M -- at M = 64k the N = 768 GEMMs
-    # (qkv / proj / fc data-grads, mlp_proj) tile into whole waves of 256 CUs; 288 GB HBM makes the
-    # activation footprint irrelevant.
+    # micro-batch default per config; for the headline 1024 x 128 = 128k tokens per GPU per step: the
+    # M dimension every block GEMM sees.  Measured on 1x MI355X, round 2 (profiles/r2_batch_ab.txt,
+    # interleaved): B=512 1.537 / 1.544M tok/s, B=768 1.502 / 1.498M, B=1024 1.574 / 1.575M -- the
+    # N = 768 / 2304 GEMMs tile into whole waves of 256 CUs at M = 64k and 128k (not at 96k), and
+    # the per-step fixed costs (optimizer, LM-head finalize, small LoRA kernels) halve per token;
+    # 288 GB HBM makes the activation footprint irrelevant.
     ap.add_argument("--batch", type=int, default=int(os.environ.get("MFT_BENCH_BATCH", 0)),
                     help="micro-batch (sequences) per GPU (0 = the config's default)")
     ap.add_argument("--seq", type=int, default=0)
