@@ -283,7 +283,7 @@ def test_flash_attention(B, S, H, Hkv, D, causal, window):
 
 
 @pytest.mark.parametrize("B,S,H,Hkv,D,window", [
-    (512, 128, 12, 12, 64, 0),   # GPT-2 124M bench step (short path)
+    (512, 128, 12, 12, 64, 0),   # GPT-2 124M heads at seq 128 (short path; the bench step runs 1024 such rows)
     (256, 256, 4, 1, 256, 0),    # Gemma-3 270M bench step, global layer (split path, GQA 4:1)
     (256, 256, 4, 1, 256, 128),  # ... sliding-window layer (window below S so the mask is exercised)
 ])
