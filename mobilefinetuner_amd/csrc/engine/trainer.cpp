@@ -242,19 +242,27 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
 
 // ------------------------------------------------------------------ full-state checkpoint
 void Trainer::save_state(const std::string& dir) {
+  // Written into <dir>.tmp, then swapped in by rank 0 (<dir> -> <dir>.old, <dir>.tmp -> <dir>), so a
+  // crash mid-save never leaves a torn checkpoint: load_state falls back to <dir>.old.
+  namespace fs = std::filesystem;
   synchronize();
   const int r = comm_ ? comm_->rank() : 0;
-  std::filesystem::create_directories(dir);
+  const std::string tmp = dir + ".tmp", old = dir + ".old";
+  if (r == 0) {
+    fs::remove_all(tmp);
+    fs::create_directories(tmp);
+  }
+  if (comm_) comm_->barrier(stream_);
   if (r == 0) {
     const Tensor mh = flat_.master.to(Device::cpu()), m1 = opt_.m.to(Device::cpu()), m2 = opt_.v.to(Device::cpu());
     const size_t nb = (size_t)flat_.numel * sizeof(float);
-    safetensors_save(dir + "/trainable.safetensors", {{"master", "F32", {flat_.numel}, mh.data_ptr(), nb}},
+    safetensors_save(tmp + "/trainable.safetensors", {{"master", "F32", {flat_.numel}, mh.data_ptr(), nb}},
                      {{"format", "mft-flat"}}, false, true);
-    safetensors_save(dir + "/optimizer.safetensors",
+    safetensors_save(tmp + "/optimizer.safetensors",
                      {{"m", "F32", {flat_.numel}, m1.data_ptr(), nb}, {"v", "F32", {flat_.numel}, m2.data_ptr(), nb}},
                      {{"format", "mft-flat"}}, false, true);
   }
-  std::ofstream f(dir + "/trainer_state.rank" + std::to_string(r) + ".json");
+  std::ofstream f(tmp + "/trainer_state.rank" + std::to_string(r) + ".json");
   f.precision(17);
   f << "{\"global_step\": " << global_step << ", \"opt_step\": " << opt_.applied_steps()
     << ", \"total_tokens\": " << total_tokens << ", \"ema_loss\": " << ema_loss
@@ -262,13 +270,22 @@ void Trainer::save_state(const std::string& dir) {
     << ", \"numel\": " << flat_.numel << ", \"dropout_ctr\": " << (int64_t)model_.dropout_ctr.item()
     << ", \"data\": {\"epoch\": " << train_.epoch() << ", \"cursor\": " << train_.cursor() << ", \"rng\": "
     << json::escape(train_.rng_state()) << "}}\n";
-  MFT_CHECK(f.good(), "save_state: cannot write ", dir);
   f.close();
+  MFT_CHECK(!f.fail(), "save_state: cannot write ", tmp);
+  if (comm_) comm_->barrier(stream_);
+  if (r == 0) {
+    fs::remove_all(old);
+    if (fs::exists(dir)) fs::rename(dir, old);
+    fs::rename(tmp, dir);
+    fs::remove_all(old);
+  }
   if (comm_) comm_->barrier(stream_);
 }
 
-bool Trainer::load_state(const std::string& dir) {
+bool Trainer::load_state(const std::string& dir0) {
   const int r = comm_ ? comm_->rank() : 0;
+  // a crash between save_state's two renames leaves only <dir>.old
+  const std::string dir = std::filesystem::exists(dir0) || !std::filesystem::exists(dir0 + ".old") ? dir0 : dir0 + ".old";
   std::string sp = dir + "/trainer_state.rank" + std::to_string(r) + ".json";
   if (!std::filesystem::exists(sp)) sp = dir + "/trainer_state.rank0.json";
   if (!std::filesystem::exists(sp)) return false;
