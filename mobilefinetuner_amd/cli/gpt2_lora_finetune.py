@@ -134,7 +134,7 @@ def main(argv=None):
 
     trainer = Trainer(model, flat, train, valid, tc, dev, save_fn=save, power_monitor=common.build_power_monitor(a),
                       dp=dp)
-    if a.resume_from and os.path.isdir(a.resume_from):
+    if a.resume_from and (os.path.isdir(a.resume_from) or os.path.isdir(a.resume_from + ".old")):
         trainer.load_state(a.resume_from)
     log0("\n[Training plan]")
     log0(f"  epochs         : {a.epochs}\n  steps_per_epoch: {trainer.steps_per_epoch}\n  total_steps    : "

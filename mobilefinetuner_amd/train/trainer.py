@@ -199,9 +199,20 @@ class Trainer:
         return {"m": sd["m"], "v": sd["v"]}
 
     def save_state(self, path: str):
+        """Everything goes into ``<path>.tmp`` first; rank 0 then swaps it in (``path`` ->
+        ``path.old``, ``path.tmp`` -> ``path``) after all ranks wrote, so a crash mid-save never
+        leaves a torn checkpoint (``load_state`` falls back to ``path.old``)."""
+        import shutil
+
         from ..io import safetensors as st
-        os.makedirs(path, exist_ok=True)
+        final, old = path, path + ".old"
+        path = path + ".tmp"
         r = dist.get_rank() if is_dist() else 0
+        if r == 0:
+            shutil.rmtree(path, ignore_errors=True)
+            os.makedirs(path, exist_ok=True)
+        if is_dist():
+            dist.barrier()
         if getattr(self.opt, "sharded", False):
             # ZeRO-3: every rank writes its own partition (master shard + AdamW moments)
             st.save_file(os.path.join(path, f"trainable.rank{r}.safetensors"),
@@ -230,10 +241,20 @@ class Trainer:
             json.dump(state, f)
         if is_dist():
             dist.barrier()
+        if r == 0:
+            shutil.rmtree(old, ignore_errors=True)
+            if os.path.exists(final):
+                os.rename(final, old)
+            os.rename(path, final)
+            shutil.rmtree(old, ignore_errors=True)
+        if is_dist():
+            dist.barrier()
 
     def load_state(self, path: str):
         from ..io import safetensors as st
         r = dist.get_rank() if is_dist() else 0
+        if not os.path.exists(path) and os.path.exists(path + ".old"):  # crash between the swap's renames
+            path = path + ".old"
         def pick(stem):
             per_rank = os.path.join(path, f"{stem}.rank{r}.safetensors")
             return per_rank if os.path.exists(per_rank) else os.path.join(path, f"{stem}.safetensors")

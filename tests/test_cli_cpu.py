@@ -21,6 +21,9 @@ def test_gpt2_lora_cli_and_resume(tmp_path):
     recs = [json.loads(x) for x in open(tmp_path / "eval.jsonl")]
     assert recs[0]["step"] == 6 and recs[0]["valid_ppl"] > 1
     assert len(tr.history) == 6
+    assert not os.path.exists(st + ".tmp") and not os.path.exists(st + ".old")  # swapped in cleanly
+    # a crash between the save's two renames leaves only <state>.old: resume still finds it
+    os.rename(st, st + ".old")
     # full-state resume continues at step 6 and runs to 8
     tr2 = cli.main(["--model", "gpt2-tiny", *CPU, "--steps", "8", "--batch_size", "2", "--seq_len", "32",
                     "--resume_from", st, "--lora_targets", "AttnQKV,AttnProj,MlpFcIn,MlpFcOut", "--lr", "1e-3"])
