@@ -9,6 +9,7 @@ checkpoint (Conv1D [in,out] layout) at ``--save_every`` and at the end.
 from __future__ import annotations
 
 import argparse
+import os
 
 import torch
 
@@ -130,11 +131,15 @@ def main(argv=None):
 
     trainer = Trainer(model, flat, train, valid, tc, dev, save_fn=save, power_monitor=common.build_power_monitor(a),
                       dp=dp, zero_stage=a.zero_stage)
+    if a.state_dir and (os.path.isdir(a.state_dir) or os.path.isdir(a.state_dir + ".old")):
+        trainer.load_state(a.state_dir)  # full-state resume (weights, moments, step, data cursor, RNG)
     log0(f"[Training plan] steps_per_epoch={trainer.steps_per_epoch} total_steps={trainer.total_steps}\n")
     trainer.train()
     if a.output_path:
         save_final(a.output_path)
         log0(f"  ✓ Full model saved to {a.output_path}")
+    if a.state_dir:
+        trainer.save_state(a.state_dir)
     log0(f"✅ Training complete! total_tokens={trainer.total_tokens} final_ema_loss={(trainer.ema_loss or 0):.4f}")
     if dp is not None:
         dp.close()

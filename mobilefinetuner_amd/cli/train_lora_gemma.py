@@ -209,11 +209,15 @@ def main(argv=None):
 
     trainer = Trainer(model, flat, train, valid, tc, dev, save_fn=save, power_monitor=common.build_power_monitor(a),
                       dp=dp)
+    if a.state_dir and (os.path.isdir(a.state_dir) or os.path.isdir(a.state_dir + ".old")):
+        trainer.load_state(a.state_dir)  # full-state resume (weights, moments, step, data cursor, RNG)
     log0(f"[Plan] steps/epoch={trainer.steps_per_epoch} total={trainer.total_steps}")
     trainer.train()
     if rank == 0:
         save_lora(out, model)
         log0(f"  ✓ Saved LoRA to {out}")
+    if a.state_dir:
+        trainer.save_state(a.state_dir)
     ev = trainer.evaluate()
     if ev:
         log0(f"[Eval] valid_loss={ev['nll']:.4f} valid_ppl={ev['ppl']:.2f}")

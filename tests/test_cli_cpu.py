@@ -39,6 +39,11 @@ def test_gpt2_full_cli(tmp_path):
     sd = st.load_file(out)
     assert "h.0.attn.c_attn.weight" in sd and sd["wte.weight"].shape == (1000, 128)
     assert tr.total_tokens == 3 * 2 * 32
+    state = str(tmp_path / "fstate")
+    common = ["--model", "gpt2-tiny", *CPU, "--batch_size", "2", "--seq_len", "32", "--lr", "1e-3", "--state_dir", state]
+    cli.main(common + ["--steps", "3"])
+    tr2 = cli.main(common + ["--steps", "5"])
+    assert [h["step"] for h in tr2.history] == [4, 5] and tr2.total_tokens == 5 * 2 * 32
 
 
 def test_gemma_cli_and_alignment(tmp_path):
@@ -50,6 +55,13 @@ def test_gemma_cli_and_alignment(tmp_path):
     assert meta["targets"] == "attn.q,attn.k,attn.v,attn.proj,mlp.gate,mlp.up,mlp.down"
     assert t["layer.0.attn.q.lora_A"].shape == (8, 128) and t["layer.0.attn.q.lora_B"].shape == (256, 8)
     assert len(tr.history) == 4
+    # --state_dir: written at the end, resumed by the next launch (steps 5-6 only)
+    sd = str(tmp_path / "gstate")
+    common = ["--model", "gemma3-tiny", *CPU, "--batch", "2", "--seq_len", "32", "--output_dir", str(tmp_path / "g2"),
+              "--learning_rate", "1e-3", "--targets", "full", "--state_dir", sd]
+    cli.main(common + ["--max_steps", "4"])
+    tr2 = cli.main(common + ["--max_steps", "6"])
+    assert [h["step"] for h in tr2.history] == [5, 6]
     d = str(tmp_path / "align")
     cli.main(["--model", "gemma3-tiny", *CPU, "--batch", "2", "--seq_len", "16", "--align_dump_dir", d,
               "--align_layers", "0,2", "--align_dump_grads", "--align_do_step", "--align_numeric_attn",
