@@ -138,7 +138,8 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         tmp = OUT_SO + ".tmp"
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp,
                f"-L{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip",
-               "-ltorch_hip", "-lhipblaslt", "-lamdhip64", f"-Wl,-rpath,{libdir}", "-ldl", "-lpthread"]
+               "-ltorch_hip", "-lhipblaslt", "-lamdhip64", f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{libdir}",
+               f"-Wl,-rpath,{ROCM}/lib", "-ldl", "-lpthread"]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -176,7 +177,7 @@ def build_engine(objs_kernels, objs_runtime, abi, hdr, verbose=False, jobs=None)
         path = os.path.join(BIN_DIR, exe)
         if changed or not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(o) for o in libs):
             cmd = [HIPCC, "-fPIC", obj, *libs, "-o", path + ".tmp", f"-L{ROCM}/lib", "-lhipblaslt", "-lrccl", "-lamdhip64",
-                   f"-Wl,-rpath,{ROCM}/lib", "-ldl", "-lpthread"]
+                   "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM}/lib", "-ldl", "-lpthread"]
             if verbose:
                 print(" ".join(cmd), flush=True)
             r = subprocess.run(cmd, capture_output=True, text=True)

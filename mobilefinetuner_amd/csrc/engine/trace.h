@@ -1,0 +1,19 @@
+// libmft engine: roctx ranges around the native trainer's phases -- step, graph
+// capture, evaluation, checkpoint -- so `rocprofv3 --marker-trace` shows them next to the kernel
+// trace of a native CLI run.  Without a profiler tool attached the calls are no-ops.
+#pragma once
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+namespace mft {
+namespace eng {
+
+class TraceRange {
+ public:
+  explicit TraceRange(const char* name) { roctxRangePushA(name); }
+  ~TraceRange() { roctxRangePop(); }
+  TraceRange(const TraceRange&) = delete;
+  TraceRange& operator=(const TraceRange&) = delete;
+};
+
+}  // namespace eng
+}  // namespace mft

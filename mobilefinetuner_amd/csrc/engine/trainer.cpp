@@ -13,6 +13,7 @@
 #include "engine/allocator.h"
 #include "engine/autograd.h"
 #include "engine/ops.h"
+#include "engine/trace.h"
 #include "runtime/json.h"
 #include "runtime/safetensors.h"
 
@@ -73,6 +74,7 @@ void Trainer::fwd_bwd() {
 }
 
 void Trainer::capture() {
+  TraceRange range("mft.capture");
   auto& al = CachingAllocator::get(0);
   pool_ = al.new_pool();
   CachingAllocator::set_current_pool(pool_);
@@ -87,6 +89,7 @@ void Trainer::capture() {
 }
 
 Tensor Trainer::step(const std::vector<std::pair<const int64_t*, const int64_t*>>& micro) {
+  TraceRange range("mft.step");
   MFT_CHECK(micro.size() == ids_.size(), "trainer: expected ", ids_.size(), " micro-batches");
   for (size_t i = 0; i < micro.size(); ++i) {
     Tensor hi = from_blob(const_cast<int64_t*>(micro[i].first), ids_[i].shape(), DType::I64, Device::cpu());
@@ -119,6 +122,7 @@ Tensor Trainer::step(const std::vector<std::pair<const int64_t*, const int64_t*>
 }
 
 std::pair<double, double> Trainer::evaluate(int max_batches, int batch_size) {
+  TraceRange range("mft.eval");
   if (!valid_) return {0.0, 0.0};
   NoGradGuard ng;
   valid_->reset_cursor();
@@ -242,6 +246,7 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
 
 // ------------------------------------------------------------------ full-state checkpoint
 void Trainer::save_state(const std::string& dir) {
+  TraceRange range("mft.save_state");
   // Written into <dir>.tmp, then swapped in by rank 0 (<dir> -> <dir>.old, <dir>.tmp -> <dir>), so a
   // crash mid-save never leaves a torn checkpoint: load_state falls back to <dir>.old.
   namespace fs = std::filesystem;
