@@ -825,6 +825,7 @@ class _LoRALinearAug(Function):
         # several adapters on one input without dropout (q|k|v, gate|up): ONE pass over x for all
         # u_i (the u columns of consecutive slices are adjacent in xa)
         batched = len(slices) > 1 and all(dp == 0 for (_, _, dp, _) in slices)
+        acat = None
         if batched:
             acat = torch.cat([cw(ab[2 * i]) for i in range(len(slices))])
             C.lora_rowdot(x2, acat, xa2[:, K:K + acat.shape[0]], 1.0, 0.0, 0, None)
@@ -841,6 +842,7 @@ class _LoRALinearAug(Function):
         ctx.params = ab
         ctx.slices, ctx.waug, ctx.K, ctx.w = slices, waug, K, w
         ctx.s, ctx.shape = float(s), shape
+        ctx.acat = acat  # [A_1; ..; A_n] of this step's shadows, reused by the backward's LoRA epilogue
         return y.view(*shape[:-1], y.shape[-1])
 
     @staticmethod
@@ -876,7 +878,9 @@ class _LoRALinearAug(Function):
                     db_done.add(i)  # dB_i came out of the same pass over dy_i (lora_dy)
                 vs.append(vall[:, o:o + ranks[i]])
                 o += ranks[i]
-            acat = torch.cat([cw(ab[2 * i]) for i in range(len(ranks))]) if len(ranks) > 1 else cw(ab[0])
+            acat = ctx.acat
+            if acat is None:
+                acat = torch.cat([cw(ab[2 * i]) for i in range(len(ranks))]) if len(ranks) > 1 else cw(ab[0])
             _fused_dx(dy2, ctx.w, GEMM_EPI_LORA, out=dxa[:, :K], lora_u=vall, lora_w=acat)
         grads = []
         ctr = dropout_counter(dy.device)
