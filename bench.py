@@ -17,6 +17,18 @@ set) every process is one rank and ``--gpus`` must equal the world size.
 ``--cpu_smoke``: gpt2-tiny on the CPU over gloo, for the GPU-less multi-rank test of this path.
 
 Prints ONE JSON line on rank 0.
+
+Engines (``--engine``):
+  native  (default for gpt2-lora, gemma3-270m-lora, gpt2-full) -- the torch-free libmft C++ engine:
+          this process starts the native CLI (mobilefinetuner_amd/bin/gpt2_lora_finetune,
+          train_lora_gemma, gpt2_full_finetune) as a fresh child with --random_init --synthetic_data
+          --bench_steps K --bench_warmup W; the child runs the C++ autograd tape + hipGraph-captured
+          step, times exactly K steps between device synchronizes and cross-rank barriers, takes the
+          MAX over ranks (RCCL) and prints one MFT_BENCH line, which this process turns into the
+          driver's JSON record.  Under torch.distributed.run each rank process starts its own child
+          (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* pass through; the native communicator
+          bootstraps on MASTER_PORT + 1).  This process never touches the GPU and never imports torch.
+  torch   the PyTorch-driven Python package path (kept as the test oracle; the ZeRO configs).
 """
 from __future__ import annotations
 
@@ -25,9 +37,6 @@ import json
 import os
 import sys
 import time
-
-import torch
-import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -40,13 +49,13 @@ BASELINE_TOKENS_PER_SEC = 170.0
 # BASELINE.json "configs" -> (model preset, mode, default micro-batch, seq, metric label)
 CONFIGS = {
     # headline: GPT-2 small LoRA r=8 seq 128 (BASELINE.json "metric")
-    "gpt2-lora": dict(model="gpt2", mode="lora", batch=1024, seq=128, targets="AttnQKV,AttnProj",
+    "gpt2-lora": dict(model="gpt2", mode="lora", batch=1024, seq=128, targets="AttnQKV,AttnProj", engine="native",
                       metric="tokens/sec GPT-2-124M LoRA r=8 seq128 (training, whole job)"),
     # Gemma-3 270M LoRA r=8 seq 256 (RMSNorm / QK-norm+RoPE / GQA / sliding-window kernels)
-    "gemma3-270m-lora": dict(model="gemma3-270m", mode="lora", batch=256, seq=256, targets="full",
+    "gemma3-270m-lora": dict(model="gemma3-270m", mode="lora", batch=256, seq=256, targets="full", engine="native",
                              metric="tokens/sec Gemma-3-270M LoRA r=8 seq256 (training, whole job)"),
     # GPT-2 small full fine-tuning, DP over RCCL (bucketed, backward-overlapped all-reduce)
-    "gpt2-full": dict(model="gpt2", mode="full", batch=512, seq=128, zero=0,
+    "gpt2-full": dict(model="gpt2", mode="full", batch=512, seq=128, zero=0, engine="native",
                       metric="tokens/sec GPT-2-124M full fine-tune seq128 (training, whole job)"),
     # GPT-2 XL (1.5B) full fine-tuning with ZeRO-2 partitioned optimizer / reduce-scattered grads
     "gpt2-xl-zero": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=2,
@@ -63,15 +72,123 @@ CONFIGS = {
 }
 
 
+# (layers, attention width) for the model-FLOPs formula (utils/trace.model_flops_per_token_cfg)
+_ATTN_DIMS = {"gpt2": (12, 768), "gpt2-medium": (24, 1024), "gpt2-large": (36, 1280), "gpt2-xl": (48, 1600),
+              "gemma3-270m": (18, 4 * 256), "gemma3-1b": (26, 4 * 256)}
+MI355X_BF16_DENSE_TFLOPS = 2500.0
+
+
+def _flops_per_token(model, seq, n_params, n_train):
+    n_layer, d_attn = _ATTN_DIMS[model]
+    return 4.0 * n_params + 2.0 * n_train + n_layer * 2 * seq * d_attn * 3
+
+
+def _native_cmd(a, cfgd):
+    """argv of the native CLI for this config (random-init weights, synthetic tokens)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    bindir = os.path.join(here, "mobilefinetuner_amd", "bin")
+    total = a.steps + a.warmup
+    # enough distinct synthetic tokens for a few different batches per rank (the stream wraps)
+    ntok = max(2_000_000, 4 * a.batch * (a.seq + 1) * a.grad_accum)
+    common = ["--random_init", "--synthetic_data", "--synthetic_tokens", str(ntok), "--seq_len", str(a.seq),
+              "--bench_steps", str(a.steps), "--bench_warmup", str(a.warmup)]
+    if a.no_graph:
+        common.append("--no_graph")
+    if cfgd["model"].startswith("gemma"):
+        return [os.path.join(bindir, "train_lora_gemma"), "--model", cfgd["model"], "--batch", str(a.batch),
+                "--grad_accum", str(a.grad_accum), "--rank", str(a.rank), "--alpha", str(a.alpha),
+                "--lora_dropout", "0", "--targets", a.targets or cfgd["targets"], "--lr", "2e-4",
+                "--max_steps", str(total), "--log_interval", "0"] + common
+    exe = "gpt2_full_finetune" if cfgd["mode"] == "full" else "gpt2_lora_finetune"
+    cmd = [os.path.join(bindir, exe), "--model", cfgd["model"], "--batch_size", str(a.batch),
+           "--grad_accum_steps", str(a.grad_accum), "--steps", str(total), "--log_interval", "0"]
+    if cfgd["mode"] == "full":
+        cmd += ["--lr", "1e-5", "--weight_decay", "0.01"]
+    else:
+        cmd += ["--rank", str(a.rank), "--alpha", str(a.alpha), "--lr", "2e-4",
+                "--lora_targets", a.targets or cfgd["targets"]]
+    return cmd + common
+
+
+def run_native(a, cfgd) -> int:
+    """Start the native CLI as a child (never exec: this process stays the parent), relay its
+    exit code; rank 0 turns the child's MFT_BENCH line into the driver's JSON record."""
+    import subprocess
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    cmd = _native_cmd(a, cfgd)
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    # the child's log goes to our stderr as it comes (progress), its MFT_BENCH line is kept
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    rec = None
+    for line in p.stdout:
+        if line.startswith("MFT_BENCH "):
+            rec = json.loads(line[len("MFT_BENCH "):])
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = p.wait()
+    if rc != 0:
+        sys.stderr.write(f"bench.py: native engine exited with {rc}: {' '.join(cmd)}\n")
+        return rc
+    if rank != 0:
+        return 0
+    if rec is None:
+        sys.stderr.write("bench.py: the native engine printed no MFT_BENCH line\n")
+        return 1
+    dt = rec["seconds"]
+    tokens = rec["world"] * rec["batch"] * rec["seq"] * rec["accum"] * rec["steps"]
+    value = tokens / dt
+    fpt = _flops_per_token(cfgd["model"], rec["seq"], rec["n_params"], rec["n_trainable"])
+    tflops = value / rec["world"] * fpt / 1e12
+    mode = "LoRA r=%d alpha=%g targets=%s" % (a.rank, a.alpha, a.targets or cfgd["targets"]) \
+        if cfgd["mode"] == "lora" else "full fine-tune"
+    out_rec = {
+        "metric": cfgd["metric"],
+        "value": round(value, 1),
+        "unit": "tokens/s",
+        "n_gpus": rec["world"],
+        "steps": rec["steps"],
+        "warmup": rec["warmup"],
+        "ms_per_step": round(1000 * dt / rec["steps"], 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / BASELINE_TOKENS_PER_SEC, 1) if a.config == "gpt2-lora" else None,
+        "dtype": "bf16",
+        "data": "synthetic (random tokens, random-init weights)",
+        "config": {
+            "model": f"{cfgd['model']} {mode} ({rec['n_params'] / 1e6:.0f}M params)",
+            "global_batch": rec["world"] * rec["batch"] * rec["accum"],
+            "micro_batch_per_gpu": rec["batch"],
+            "seq_len": rec["seq"],
+            "parallelism": f"dp{rec['world']}",
+            "engine": "native libmft (C++ autograd tape, hipGraph-captured step)",
+            "backend": "rccl" if rec["world"] > 1 else "none",
+            "hipgraph": not a.no_graph,
+            "final_loss": round(rec["final_loss"], 4),
+            "model_tflops_per_gpu": round(tflops, 1),
+            "mfu_bf16_dense": round(tflops / MI355X_BF16_DENSE_TFLOPS, 4),
+            "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC if a.config == "gpt2-lora" else None,
+        },
+    }
+    print(json.dumps(out_rec), flush=True)
+    return 0
+
+
 def _odesc(a):
     return " + host-offloaded AdamW (" + ("fp32" if a.offload_fp32 else "bf16 stochastic-rounded") + " moments)"
 
 
 def _force_comm():
+    import torch.distributed as dist
     return dist.is_initialized() and os.environ.get("MFT_DP_FORCE_COMM", "0") == "1"
 
 
 def build(a, cfgd, dev, world):
+    import torch
     from mobilefinetuner_amd.optim.adamw import FusedAdamW
     from mobilefinetuner_amd.parallel.ddp import DataParallel
     from mobilefinetuner_amd.train.engine import TrainStep
@@ -149,6 +266,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="gpt2-lora", choices=sorted(CONFIGS),
                     help="benchmark configuration (BASELINE.json configs); default = the headline metric")
+    ap.add_argument("--engine", default="", choices=["", "native", "torch"],
+                    help="native = the libmft C++ engine (default where the config has one), torch = the Python path")
     # micro-batch default per config; for the headline 1024 x 128 = 128k tokens per GPU per step: the
     # M dimension every block GEMM sees.  Measured on 1x MI355X, round 2 (profiles/r2_batch_ab.txt,
     # interleaved): B=512 1.537 / 1.544M tok/s, B=768 1.502 / 1.498M, B=1024 1.574 / 1.575M -- the
@@ -178,6 +297,13 @@ def main():
         cfgd["model"] = "gpt2-tiny"
     a.batch = a.batch or (4 if a.cpu_smoke else cfgd["batch"])
     a.seq = a.seq or (32 if a.cpu_smoke else cfgd["seq"])
+    engine = a.engine or ("torch" if a.cpu_smoke else cfgd.get("engine", "torch"))
+    if engine == "native":
+        if a.cpu_smoke:
+            raise SystemExit("bench.py: --cpu_smoke runs the torch path (the native engine is GPU-only)")
+        sys.exit(run_native(a, cfgd))
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <functional>
 #include <map>
@@ -17,11 +18,16 @@
 #include <thread>
 #include <vector>
 
+#include "engine/comm.h"
+#include "engine/dist.h"
+#include "engine/optim.h"
 #include "runtime/dataset.h"
 #include "runtime/power_monitor.h"
 
 namespace mft {
 namespace apps {
+
+using eng::DistConfig;
 
 struct Args {
   std::map<std::string, std::string> kv;
@@ -137,6 +143,76 @@ inline bool load_token_splits(const Args& a, DataConfig& dc, int vocab, TokenDat
   if (fva.empty()) return false;
   valid.set_tokens(pack_lines(read_lines(fva, true), enc, dc.eos_id, true, 1.f, seq, threads));
   return true;
+}
+
+// Data-parallel / ZeRO flags shared by the training CLIs:
+//   --zero_stage 0|1|2   optimizer partition (1) + reduce-scattered gradients (2); > 0 also on one
+//                        process (a 1-rank communicator: the partitioned code path runs)
+//   --offload host|none  AdamW moments (bf16, stochastically rounded) in pinned host DRAM
+//   --bucket_mb N        fp32 gradient bytes per reduction bucket (default 25)
+//   --bf16_grads         reduce gradients in bf16      --no_overlap   reduce after the backward
+// MFT_DP_FORCE_COMM=1: a 1-rank communicator even without ZeRO (profiling the reducer on one GPU).
+inline DistConfig dist_config_from(const Args& a) {
+  DistConfig d;
+  d.zero_stage = a.i("zero_stage", 0);
+  d.bucket_bytes = (int64_t)(a.f("bucket_mb", 25.f) * 1048576.0);
+  d.bf16_reduce = a.b("bf16_grads");
+  d.overlap = !a.b("no_overlap");
+  const std::string off = a.get("offload", "none");
+  if (off != "none" && off != "host") throw std::runtime_error("--offload host|none (got '" + off + "')");
+  d.host_moments = off == "host";
+  if (d.zero_stage < 0 || d.zero_stage > 2) throw std::runtime_error("--zero_stage 0|1|2 in the native engine");
+  return d;
+}
+
+inline std::unique_ptr<eng::Communicator> comm_from(const DistConfig& d) {
+  const char* fc = std::getenv("MFT_DP_FORCE_COMM");
+  return eng::Communicator::from_env((fc && fc[0] == '1') || d.zero_stage > 0);
+}
+
+// the flat trainable buffers, bucket-planned when a communicator exists, plus its reducer
+struct DistSetup {
+  std::unique_ptr<eng::FlatParams> flat;
+  eng::FlatPlan plan;
+  std::unique_ptr<eng::DataParallel> dp;
+  void make_flat(std::vector<std::pair<std::string, eng::Param*>> params, eng::Communicator* comm, const DistConfig& d) {
+    if (comm) {
+      plan = eng::plan_flat(params, comm->world(), d.bucket_bytes);
+      flat = std::make_unique<eng::FlatParams>(std::move(params), plan.offsets, plan.numel);
+    } else {
+      flat = std::make_unique<eng::FlatParams>(std::move(params));
+    }
+  }
+  // after the optimizer exists (the reducer shards it)
+  void make_dp(eng::Communicator* comm, eng::AdamW& opt, const DistConfig& d) {
+    if (comm) {
+      dp = std::make_unique<eng::DataParallel>(*flat, plan, *comm, opt, d);
+      std::printf("  data parallel: %s\n", dp->describe().c_str());
+    } else if (d.host_moments) {
+      opt.shard({eng::OptSegment{0, flat->numel, 0}}, nullptr, true);
+      std::printf("  AdamW moments in pinned host DRAM (bf16)\n");
+    }
+  }
+};
+
+// bench.py's native engine (--bench_steps K [--bench_warmup W]): time K full training steps after W
+// untimed ones (Trainer::bench) and print ONE machine-readable line on rank 0:
+//   MFT_BENCH {"seconds": .., "steps": K, "warmup": W, "world": N, "batch": B, "seq": S, "accum": A, ...}
+// bench.py turns it into the driver's JSON record.
+template <class TrainerT, class FlatT>
+inline void bench_report(TrainerT& trainer, const FlatT& flat, const Args& a, int world, bool lead, const std::string& model,
+                         size_t n_params, int batch, int seq, int accum) {
+  const int steps = a.i("bench_steps", 0), warmup = a.i("bench_warmup", 3);
+  float loss = 0.f;
+  const double secs = trainer.bench(warmup, steps, &loss);
+  long long n_train = 0;
+  for (auto& kv : flat.params) n_train += (long long)kv.second->leaf.numel();
+  if (!lead) return;
+  std::printf("MFT_BENCH {\"seconds\": %.9f, \"steps\": %d, \"warmup\": %d, \"world\": %d, \"batch\": %d, "
+              "\"seq\": %d, \"accum\": %d, \"final_loss\": %.6f, \"model\": \"%s\", \"n_params\": %zu, "
+              "\"n_trainable\": %lld}\n",
+              secs, steps, warmup, world, batch, seq, accum, loss, model.c_str(), n_params, n_train);
+  std::fflush(stdout);
 }
 
 // --pm_* flags (reference energy options) -> PowerMonitor, or null when off

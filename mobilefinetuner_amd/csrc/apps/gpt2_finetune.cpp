@@ -53,7 +53,7 @@ namespace {
 
 const std::set<std::string> kBool = {"split_qkv", "random_init", "synthetic_data", "no_graph", "compat_l2_adam",
                                      "shard_enable", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
-                                     "deterministic", "help"};
+                                     "deterministic", "bf16_grads", "no_overlap", "help"};
 const std::set<std::string> kValued = {
     "data_dir", "pretrained_dir", "lora_out", "resume_from", "state_dir", "inject_fault", "eval_out", "output_path", "epochs", "steps",
     "batch_size", "grad_accum_steps", "seq_len", "rank", "alpha", "lr", "weight_decay", "warmup_steps",
@@ -61,7 +61,7 @@ const std::set<std::string> kValued = {
     "eval_batch_size", "save_every", "ema_beta", "seed", "pm_interval", "pm_batt_thresh", "pm_temp_thresh",
     "pm_fb_high", "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule",
     "shard_dir", "shard_budget_mb", "shard_fp16_disk", "model", "synthetic_tokens", "pretokenized_path",
-    "pretokenized_meta", "lora_targets", "metrics_out", "device"};
+    "pretokenized_meta", "lora_targets", "metrics_out", "device", "bench_steps", "bench_warmup", "zero_stage", "offload", "bucket_mb"};
 
 Args parse(int argc, char** argv) { return parse_args(argc, argv, kBool, kValued); }
 
@@ -130,8 +130,8 @@ int run(int argc, char** argv) {
   // data parallelism: one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK, e.g. under
   // `python -m mobilefinetuner_amd.launch --nproc N`), native RCCL communicator; the communicator
   // selects the device LOCAL_RANK.  MFT_DP_FORCE_COMM=1 builds a 1-rank one on a single GPU.
-  const char* fc = std::getenv("MFT_DP_FORCE_COMM");
-  std::unique_ptr<Communicator> comm = Communicator::from_env(fc && fc[0] == '1');
+  const DistConfig dcfg = mft::apps::dist_config_from(a);
+  std::unique_ptr<Communicator> comm = mft::apps::comm_from(dcfg);
   if (!comm) HIP_OK(hipSetDevice(0));
   if (comm && comm->rank() != 0) std::setvbuf(stdout, nullptr, _IOFBF, 1 << 16);  // rank 0 reports
   // one non-blocking stream for everything (graph capture target)
@@ -142,7 +142,9 @@ int run(int argc, char** argv) {
   const int seq_len = a.i("seq_len", 128);
   const uint64_t seed = (uint64_t)a.l("seed", 42);
   std::printf("\n========== %s (MI355X native engine) ==========\n", kProg);
-  if (comm) std::printf("  data parallel: rank %d of %d (RCCL, device %d)\n", comm->rank(), comm->world(), comm->local_rank());
+  if (comm)
+    std::printf("  data parallel: rank %d of %d (%s, device %d)\n", comm->rank(), comm->world(), comm->backend(),
+                comm->device());
 
   std::printf("\n[1/6] Loading model...\n");
   const std::string pdir = a.get("pretrained_dir");
@@ -195,7 +197,9 @@ int run(int argc, char** argv) {
     if (!a.get("shard_dir").empty() || a.kv.count("shard_fp16_disk"))
       std::printf("  (--shard_dir / --shard_fp16_disk: no disk tier in the native engine, host DRAM holds the weights)\n");
   }
-  FlatParams flat(model->trainable());
+  mft::apps::DistSetup ds;
+  ds.make_flat(model->trainable(), comm.get(), dcfg);
+  FlatParams& flat = *ds.flat;
   std::printf("  trainable params: %lld (padded)  |  total: %zu\n", (long long)flat.numel, model->num_parameters());
 
   std::printf("\n[3/6] Loading dataset...\n");
@@ -225,6 +229,7 @@ int run(int argc, char** argv) {
   oc.max_grad_norm = a.f("clip_grad_norm", 1.f);
   oc.l2_coupled = a.b("compat_l2_adam");
   AdamW opt(flat, oc);
+  ds.make_dp(comm.get(), opt, dcfg);
   TrainConfig tc;
   tc.epochs = a.i("epochs", 0);
   tc.steps = a.l("steps", 0);
@@ -250,10 +255,15 @@ int run(int argc, char** argv) {
     tc.fault_rank = c == std::string::npos ? 0 : std::stoi(f.substr(c + 1));
   }
   std::unique_ptr<PowerMonitor> pm = mft::apps::power_monitor_from(a);
-  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get());
+  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get(), ds.dp.get());
   if (!tc.state_dir.empty() && trainer.load_state(tc.state_dir))
     std::printf("  resumed full training state from %s at step %lld / %lld\n", tc.state_dir.c_str(),
                 (long long)trainer.global_step, (long long)trainer.total_steps());
+  if (a.i("bench_steps", 0) > 0) {
+    mft::apps::bench_report(trainer, flat, a, comm ? comm->world() : 1, !comm || comm->rank() == 0, a.get("model", "gpt2"),
+                            model->num_parameters(), tc.batch, tc.seq, tc.accum);
+    return 0;
+  }
   const std::string lora_out = a.get("lora_out"), out_path = a.get("output_path");
   auto save = [&](int64_t step) {
     if (!full && !lora_out.empty()) {

@@ -42,7 +42,7 @@ const char* kProg = "train_lora_gemma";
 
 const std::set<std::string> kBool = {"random_init", "synthetic_data", "no_graph", "compat_l2_adam", "deterministic",
                                      "interleaved_rope", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
-                                     "shard_enable", "help"};
+                                     "shard_enable", "bf16_grads", "no_overlap", "help"};
 const std::set<std::string> kValued = {
     "model_dir", "data_dir", "pretokenized_path", "pretokenized_meta", "output_dir", "targets", "lora_targets",
     "epochs", "max_steps", "seq_len", "batch", "grad_accum", "lr", "learning_rate", "rank", "lora_r", "alpha",
@@ -50,7 +50,7 @@ const std::set<std::string> kValued = {
     "data_fraction", "log_interval", "eval_steps", "eval_batches", "save_every", "seed", "model", "synthetic_tokens",
     "resume_from", "state_dir", "inject_fault", "metrics_out", "eval_out", "pm_interval", "pm_batt_thresh", "pm_temp_thresh", "pm_fb_high",
     "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "device",
-    "shard_budget_mb", "shard_dir", "shard_fp16_disk"};
+    "shard_budget_mb", "shard_dir", "shard_fp16_disk", "bench_steps", "bench_warmup", "zero_stage", "offload", "bucket_mb"};
 
 // first present of several alias flags
 std::string pick(const Args& a, std::initializer_list<const char*> keys, const std::string& d) {
@@ -74,8 +74,10 @@ void usage() {
       "  --eval_batches N --save_every N --seed S --pm_* (energy)\n"
       "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --resume_from F --no_graph\n"
       "          --compat_l2_adam --metrics_out F --deterministic --interleaved_rope\n"
+      "          --zero_stage 0|1|2 --offload host|none --bucket_mb N --bf16_grads --no_overlap\n"
       "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"
-      "          --inject_fault STEP:RANK (failure test: that rank throws before that step)\n",
+      "          --inject_fault STEP:RANK (failure test: that rank throws before that step)\n"
+      "          --bench_steps K [--bench_warmup W] (bench.py: time K steps after W, print one MFT_BENCH line)\n",
       kProg);
 }
 
@@ -93,8 +95,8 @@ int run(int argc, char** argv) {
   if (a.get("loss_reduction", "mean") != "mean")
     throw std::runtime_error("--loss_reduction sum: the native engine trains on the mean token loss");
   if (a.b("deterministic")) set_deterministic(true);
-  const char* fc = std::getenv("MFT_DP_FORCE_COMM");
-  std::unique_ptr<Communicator> comm = Communicator::from_env(fc && fc[0] == '1');
+  const DistConfig dcfg = mft::apps::dist_config_from(a);
+  std::unique_ptr<Communicator> comm = mft::apps::comm_from(dcfg);
   if (!comm) HIP_OK(hipSetDevice(0));
   if (comm && comm->rank() != 0) std::setvbuf(stdout, nullptr, _IOFBF, 1 << 16);
   hipStream_t stream;
@@ -104,7 +106,9 @@ int run(int argc, char** argv) {
   const uint64_t seed = (uint64_t)a.l("seed", 42);
 
   std::printf("\n========== Gemma-3 LoRA Finetune (MI355X native engine) ==========\n");
-  if (comm) std::printf("  data parallel: rank %d of %d (RCCL, device %d)\n", comm->rank(), comm->world(), comm->local_rank());
+  if (comm)
+    std::printf("  data parallel: rank %d of %d (%s, device %d)\n", comm->rank(), comm->world(), comm->backend(),
+                comm->device());
   const std::string mdir = a.get("model_dir");
   const bool random_init = a.b("random_init") || mdir.empty();
   Gemma3Config cfg = (!mdir.empty() && file_exists(mdir + "/config.json")) ? Gemma3Config::from_json(mdir + "/config.json")
@@ -147,7 +151,9 @@ int run(int argc, char** argv) {
     std::printf("  weight streaming ON: %d device slots (%.1f MB) for %.1f MB of frozen layer weights in pinned host memory\n",
                 ws->slots(), ws->device_bytes() / 1048576.0, ws->host_bytes() / 1048576.0);
   }
-  FlatParams flat(model->trainable());
+  mft::apps::DistSetup ds;
+  ds.make_flat(model->trainable(), comm.get(), dcfg);
+  FlatParams& flat = *ds.flat;
   std::printf("  trainable params: %lld (padded)  |  total: %zu\n", (long long)flat.numel, model->num_parameters());
 
   DataConfig dc;
@@ -177,6 +183,7 @@ int run(int argc, char** argv) {
   oc.max_grad_norm = a.f("max_grad_norm", 1.f);
   oc.l2_coupled = a.b("compat_l2_adam");
   AdamW opt(flat, oc);
+  ds.make_dp(comm.get(), opt, dcfg);
   TrainConfig tc;
   tc.epochs = a.i("epochs", 1);
   tc.steps = a.l("max_steps", -1);
@@ -200,15 +207,21 @@ int run(int argc, char** argv) {
     tc.fault_rank = c == std::string::npos ? 0 : std::stoi(f.substr(c + 1));
   }
   tc.eval_out = a.get("eval_out");
+  tc.log_style = "gemma";
   const std::string sched = a.get("lr_schedule", "linear");
   const float ratio = a.f("warmup_ratio", 0.03f), base = oc.lr;
   if (sched == "constant") tc.lr_fn = [base](int64_t, int64_t) { return base; };
   else tc.lr_fn = [base, ratio, sched](int64_t it, int64_t total) { return gemma_lr(it + 1, base, ratio, total, sched == "cosine"); };
   std::unique_ptr<PowerMonitor> pm = mft::apps::power_monitor_from(a);
-  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get());
+  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get(), ds.dp.get());
   if (!tc.state_dir.empty() && trainer.load_state(tc.state_dir))
     std::printf("  resumed full training state from %s at step %lld / %lld\n", tc.state_dir.c_str(),
                 (long long)trainer.global_step, (long long)trainer.total_steps());
+  if (a.i("bench_steps", 0) > 0) {
+    mft::apps::bench_report(trainer, flat, a, comm ? comm->world() : 1, lead, a.get("model", "gemma3-270m"),
+                            model->num_parameters(), tc.batch, tc.seq, tc.accum);
+    return 0;
+  }
   const std::string out_dir = a.get("output_dir", "runs/gemma_lora");
   const std::string out = out_dir + "/gemma_lora.safetensors";
   if (lead) {

@@ -323,7 +323,7 @@ void nonfinite_check(Tensor x, Tensor flag) {
 }
 void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor step, c10::optional<Tensor> sumsq_t,
                 double beta1, double beta2, double eps, double wd, double max_norm, bool l2_coupled,
-                c10::optional<Tensor> shadow, c10::optional<Tensor> nonfinite) {
+                c10::optional<Tensor> shadow, c10::optional<Tensor> nonfinite, int64_t sr_offset) {
   CHECK_F32(p); CHECK_F32(g);
   CHECK_CONTIG(p); CHECK_CONTIG(g); CHECK_CONTIG(m); CHECK_CONTIG(v);
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adamw: size mismatch");
@@ -339,6 +339,7 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor step, 
   a.shadow = optp<bf16_t>(shadow);
   if (a.shadow) TORCH_CHECK(shadow->numel() == p.numel() && shadow->is_contiguous(), "shadow must match params");
   a.nonfinite = optp<int>(nonfinite);
+  a.sr_offset = sr_offset;
   mft::adamw_step(a, stream());
 }
 void adamw_commit(Tensor step, c10::optional<Tensor> nonfinite, c10::optional<Tensor> sumsq_t) {
@@ -657,7 +658,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("logsoftmax_gather", &logsoftmax_gather);
   m.def("sumsq", &sumsq);
   m.def("nonfinite_check", &nonfinite_check);
-  m.def("adamw_step", &adamw_step);
+  m.def("adamw_step", &adamw_step, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr"),
+        py::arg("step"), py::arg("sumsq"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("wd"),
+        py::arg("max_norm"), py::arg("l2_coupled"), py::arg("shadow"), py::arg("nonfinite"),
+        py::arg("sr_offset") = 0);
   m.def("adamw_commit", &adamw_commit);
   m.def("lora_rowdot", &lora_rowdot);
   m.def("lora_update", &lora_update);

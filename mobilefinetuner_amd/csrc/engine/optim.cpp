@@ -16,14 +16,24 @@ constexpr int64_t kAlign = 64;  // every param starts 16-B aligned in fp32 and b
 int64_t round_up(int64_t n, int64_t a) { return (n + a - 1) / a * a; }
 }  // namespace
 
-FlatParams::FlatParams(std::vector<std::pair<std::string, Param*>> ps) : params(std::move(ps)) {
+FlatParams::FlatParams(std::vector<std::pair<std::string, Param*>> ps, std::vector<int64_t> offs, int64_t total)
+    : params(std::move(ps)) {
   NoGradGuard ng;
-  int64_t off = 0;
-  for (auto& kv : params) {
-    offsets.push_back(off);
-    off += round_up(kv.second->leaf.numel(), kAlign);
+  if (!offs.empty()) {
+    MFT_CHECK(offs.size() == params.size(), "FlatParams: one offset per parameter");
+    offsets = std::move(offs);
+    numel = total;
+    for (size_t i = 0; i < params.size(); ++i)
+      MFT_CHECK(offsets[i] % kAlign == 0 && offsets[i] + params[i].second->leaf.numel() <= numel,
+                "FlatParams: bad planned offset for ", params[i].first);
+  } else {
+    int64_t off = 0;
+    for (auto& kv : params) {
+      offsets.push_back(off);
+      off += round_up(kv.second->leaf.numel(), kAlign);
+    }
+    numel = round_up(std::max<int64_t>(off, kAlign), kAlign);
   }
-  numel = round_up(std::max<int64_t>(off, kAlign), kAlign);
   master = zeros({numel}, DType::F32);
   grad = zeros({numel}, DType::F32);
   shadow = zeros({numel}, DType::BF16);
@@ -56,6 +66,28 @@ AdamW::AdamW(FlatParams& flat, const AdamWConfig& cfg) : flat_(flat), cfg_(cfg) 
   sumsq_dev = zeros({1}, DType::F32);
   nonfinite_dev = zeros({1}, DType::I32);
   skipped_dev = zeros({1}, DType::I32);
+  segs_ = {OptSegment{0, flat.numel, 0}};
+  state_numel_ = flat.numel;
+}
+
+void AdamW::shard(const std::vector<OptSegment>& segs, Communicator* comm, bool host_moments) {
+  NoGradGuard ng;
+  segs_ = segs;
+  comm_ = comm;
+  host_moments_ = host_moments;
+  state_numel_ = 0;
+  for (auto& s : segs_) {
+    MFT_CHECK(s.off % 4 == 0 && s.len % 4 == 0 && s.off + s.len <= flat_.numel, "AdamW::shard: bad segment");
+    state_numel_ = std::max(state_numel_, s.state_off + s.len);
+  }
+  const int64_t n = std::max<int64_t>(state_numel_, 4);
+  if (host_moments) {  // pinned host DRAM, read / written in place by the kernel (bf16, SR-rounded)
+    m = zeros({n}, DType::BF16, Device::cpu(true));
+    v = zeros({n}, DType::BF16, Device::cpu(true));
+  } else {
+    m = zeros({n}, DType::F32);
+    v = zeros({n}, DType::F32);
+  }
 }
 
 void AdamW::set_lr(float lr) {
@@ -66,20 +98,21 @@ void AdamW::set_lr(float lr) {
 void AdamW::step() {
   hipStream_t s = current_stream();
   const bool clip = cfg_.max_grad_norm > 0.f;
+  float* g0 = flat_.grad.data<float>();
   if (clip) {
-    Tensor part = empty({(int64_t)::mft::sumsq_blocks(flat_.numel)}, DType::F32);
-    ::mft::sumsq(flat_.grad.data<float>(), flat_.numel, part.data<float>(), sumsq_dev.data<float>(), 0, s);
+    int64_t mx = 0;
+    for (auto& sg : segs_) mx = std::max<int64_t>(mx, ::mft::sumsq_blocks(sg.len));
+    if (!part_.defined() || part_.numel() < mx) part_ = empty({std::max<int64_t>(mx, 1)}, DType::F32);
+    for (size_t i = 0; i < segs_.size(); ++i)
+      ::mft::sumsq(g0 + segs_[i].off, segs_[i].len, part_.data<float>(), sumsq_dev.data<float>(), i > 0, s);
+    if (comm_) comm_->all_reduce(sumsq_dev.data_ptr(), 1, CommType::F32, CommOp::Sum, s);  // global norm^2
   }
   if (cfg_.skip_nonfinite) {
     nonfinite_dev.zero_();
-    ::mft::nonfinite_check(flat_.grad.data<float>(), flat_.numel, nonfinite_dev.data<int>(), s);
+    for (auto& sg : segs_) ::mft::nonfinite_check(g0 + sg.off, sg.len, nonfinite_dev.data<int>(), s);
+    if (comm_) comm_->all_reduce(nonfinite_dev.data_ptr(), 1, CommType::I32, CommOp::Max, s);  // skip together
   }
   ::mft::AdamWArgs a{};
-  a.p = flat_.master.data<float>();
-  a.g = flat_.grad.data<float>();
-  a.m = m.data<float>();
-  a.v = v.data<float>();
-  a.n = flat_.numel;
   a.lr_ptr = lr_dev.data<float>();
   a.beta1 = cfg_.beta1;
   a.beta2 = cfg_.beta2;
@@ -89,9 +122,19 @@ void AdamW::step() {
   a.sumsq = clip ? sumsq_dev.data<float>() : nullptr;
   a.max_norm = cfg_.max_grad_norm;
   a.l2_coupled = cfg_.l2_coupled;
-  a.shadow = (::mft::bf16_t*)flat_.shadow.data_ptr();
   a.nonfinite = cfg_.skip_nonfinite ? nonfinite_dev.data<int>() : nullptr;
-  ::mft::adamw_step(a, s);
+  a.moments_bf16 = m.dtype() == DType::BF16;
+  const size_t ms = m.dtype() == DType::BF16 ? 2 : 4;
+  for (auto& sg : segs_) {
+    a.p = flat_.master.data<float>() + sg.off;
+    a.g = g0 + sg.off;
+    a.m = reinterpret_cast<float*>(static_cast<char*>(m.data_ptr()) + sg.state_off * ms);
+    a.v = reinterpret_cast<float*>(static_cast<char*>(v.data_ptr()) + sg.state_off * ms);
+    a.n = sg.len;
+    a.shadow = (::mft::bf16_t*)flat_.shadow.data_ptr() + sg.off;
+    a.sr_offset = sg.off;
+    ::mft::adamw_step(a, s);
+  }
   ::mft::adamw_commit(step_dev.data<float>(), a.nonfinite, a.sumsq, s);
   if (cfg_.skip_nonfinite) {
     // skipped += nonfinite (int32 counters)
@@ -105,8 +148,10 @@ bool AdamW::skipped_last() const { return nonfinite_dev.to_vector_f32()[0] != 0.
 int64_t AdamW::applied_steps() const { return (int64_t)step_dev.item(); }
 
 void AdamW::load_state(const Tensor& m_h, const Tensor& v_h, int64_t steps) {
-  m.copy_(m_h);
-  v.copy_(v_h);
+  MFT_CHECK(m_h.numel() == m.numel() && v_h.numel() == v.numel(), "AdamW::load_state: state has ", m_h.numel(),
+            " elements, the optimizer ", m.numel());
+  m.copy_(m_h.to(m.dtype()));
+  v.copy_(v_h.to(v.dtype()));
   step_dev.fill_((double)steps);
 }
 

@@ -12,6 +12,7 @@
 #include <utility>
 #include <vector>
 
+#include "engine/comm.h"
 #include "engine/nn.h"
 
 namespace mft {
@@ -20,14 +21,22 @@ namespace eng {
 class FlatParams {
  public:
   // re-homes every param: leaf -> view of `master` (requires grad, .grad = view of `grad`),
-  // compute view -> view of `shadow` (bf16) unless the param computes in fp32
-  explicit FlatParams(std::vector<std::pair<std::string, Param*>> params);
+  // compute view -> view of `shadow` (bf16) unless the param computes in fp32.  `offsets` / `numel`
+  // (optional): a layout planned by the data-parallel reducer (bucket padding, engine/dist.h);
+  // default: params packed in order, each 64-element aligned.
+  explicit FlatParams(std::vector<std::pair<std::string, Param*>> params, std::vector<int64_t> offsets = {},
+                      int64_t numel = 0);
   Tensor master, grad, shadow;
   int64_t numel = 0;
   std::vector<std::pair<std::string, Param*>> params;
   std::vector<int64_t> offsets;
   void zero_grad();
   void refresh_shadow();
+};
+
+// one contiguous range of the flat buffers this rank updates; its moments live at state_off
+struct OptSegment {
+  int64_t off = 0, len = 0, state_off = 0;
 };
 
 struct AdamWConfig {
@@ -48,10 +57,25 @@ class AdamW {
   Tensor m, v, lr_dev, step_dev, sumsq_dev, nonfinite_dev, skipped_dev;
   const AdamWConfig& config() const { return cfg_; }
   void load_state(const Tensor& m_h, const Tensor& v_h, int64_t steps);
+  // ZeRO-1/2 (engine/dist.h): update only `segs` -- this rank's partition of the flat buffers --
+  // with moments of sum(len) elements; host_moments: bf16 moments in pinned host DRAM that the
+  // kernel reads and writes in place over PCIe (the host-offload tier of the optimizer state).
+  // The grad-norm^2 and the non-finite flag are all-reduced over `comm`, so every rank clips and
+  // skips identically.
+  void shard(const std::vector<OptSegment>& segs, Communicator* comm, bool host_moments);
+  const std::vector<OptSegment>& segments() const { return segs_; }
+  bool sharded() const { return comm_ != nullptr; }
+  bool moments_on_host() const { return host_moments_; }
+  int64_t state_numel() const { return state_numel_; }
 
  private:
   FlatParams& flat_;
   AdamWConfig cfg_;
+  std::vector<OptSegment> segs_;  // default: one segment = the whole flat buffer
+  Communicator* comm_ = nullptr;
+  bool host_moments_ = false;
+  int64_t state_numel_ = 0;
+  Tensor part_;  // sumsq partials
 };
 
 // (a) GPT-2 CLIs: linear warmup (step+1)/W, then cosine to min_ratio of lr (0-indexed step)

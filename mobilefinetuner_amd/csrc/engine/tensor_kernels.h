@@ -65,6 +65,8 @@ void nll_rows_bwd(void* dlp, int dt, const int64_t* target, long rows, int n, lo
                   hipStream_t st);
 // gather along the last dim: out[r] = x[r, idx[r]]
 void count_valid(const int64_t* target, long n, int ignore, float* out, hipStream_t st);
+// training-loss EMA on device: ema = {value, initialised}; non-finite losses are skipped
+void ema_update(float* ema, const float* loss, float beta, hipStream_t st);
 
 }  // namespace k
 }  // namespace eng

@@ -375,6 +375,16 @@ __global__ void count_valid_kernel(const int64_t* t, long n, int ignore, float* 
   if (threadIdx.x == 0) out[0] = c;
 }
 
+// ema[0] = beta * ema[0] + (1 - beta) * loss (ema[0] = loss on the first finite loss, ema[1] = 1
+// once initialised); a non-finite loss leaves both unchanged
+__global__ void ema_update_kernel(float* ema, const float* loss, float beta) {
+  if (threadIdx.x != 0) return;
+  const float l = loss[0];
+  if (!isfinite(l)) return;
+  ema[0] = ema[1] > 0.f ? beta * ema[0] + (1.f - beta) * l : l;
+  ema[1] = 1.f;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- launchers
@@ -484,6 +494,10 @@ void nll_rows_bwd(void* d, int dt, const int64_t* t, long rows, int n, long ldl,
 
 void count_valid(const int64_t* t, long n, int ignore, float* out, hipStream_t stm) {
   count_valid_kernel<<<1, 1024, 0, stm>>>(t, n, ignore, out);
+}
+
+void ema_update(float* ema, const float* loss, float beta, hipStream_t stm) {
+  ema_update_kernel<<<1, 64, 0, stm>>>(ema, loss, beta);
 }
 
 }  // namespace k

@@ -4,6 +4,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <stdexcept>
 #include <thread>
@@ -13,6 +14,7 @@
 #include "engine/allocator.h"
 #include "engine/autograd.h"
 #include "engine/ops.h"
+#include "engine/tensor_kernels.h"
 #include "engine/trace.h"
 #include "runtime/json.h"
 #include "runtime/safetensors.h"
@@ -21,9 +23,12 @@ namespace mft {
 namespace eng {
 
 Trainer::Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid,
-                 const TrainConfig& cfg, PowerMonitor* pm, Communicator* comm)
-    : model_(model), flat_(flat), opt_(opt), train_(train), valid_(valid), cfg_(cfg), pm_(pm), comm_(comm) {
+                 const TrainConfig& cfg, PowerMonitor* pm, Communicator* comm, DataParallel* dp)
+    : model_(model), flat_(flat), opt_(opt), train_(train), valid_(valid), cfg_(cfg), pm_(pm), comm_(comm), dp_(dp) {
   stream_ = current_stream();
+  MFT_CHECK(!comm_ || dp_, "Trainer: a communicator needs its DataParallel reducer");
+  const char* gc = std::getenv("MFT_GRAPH_COMM");
+  graph_comm_ = !(gc && gc[0] == '0');
   if (comm_) {  // every rank starts from rank 0's trainable weights
     comm_->broadcast(flat_.master.data_ptr(), (size_t)flat_.numel * sizeof(float), 0, stream_);
     flat_.refresh_shadow();
@@ -39,6 +44,7 @@ Trainer::Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDatase
   }
   loss_acc_ = zeros({1}, DType::F32);
   one_ = ones({1}, DType::I64);
+  ema_dev_ = zeros({2}, DType::F32);
 }
 
 Trainer::~Trainer() {
@@ -49,11 +55,16 @@ Trainer::~Trainer() {
 void Trainer::eager_step() {
   fwd_bwd();
   reduce_grads();
-  opt_.step();
+  optimizer();
 }
 
 void Trainer::reduce_grads() {
-  if (comm_) comm_->all_reduce_avg(static_cast<float*>(flat_.grad.data_ptr()), (size_t)flat_.numel, stream_);
+  if (dp_) dp_->finish();
+}
+
+void Trainer::optimizer() {
+  opt_.step();
+  if (dp_) dp_->after_optimizer();
 }
 
 void Trainer::fwd_bwd() {
@@ -66,6 +77,7 @@ void Trainer::fwd_bwd() {
     k::binary(c, c, desc(one_), k::B_ADD, 1.f, current_stream());
   }
   for (size_t i = 0; i < ids_.size(); ++i) {
+    if (dp_) dp_->begin_micro((int)i, (int)ids_.size());  // the last micro-batch's hooks launch buckets
     Tensor loss = model_.loss(ids_[i], labels_[i], inv);
     Tensor scaled = mul_scalar(loss, inv);
     backward({scaled});
@@ -79,10 +91,11 @@ void Trainer::capture() {
   pool_ = al.new_pool();
   CachingAllocator::set_current_pool(pool_);
   HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
-  // with a communicator the collective and the optimizer run eagerly after each replay (one
-  // latency-bound all-reduce; no RCCL call is recorded into the graph)
-  if (comm_) fwd_bwd();
-  else eager_step();
+  // the whole step, collectives included (the reducer's comm stream forks from and joins back
+  // into the capture stream through events); MFT_GRAPH_COMM=0 leaves the collectives and the
+  // optimizer out of the graph (then run eagerly after each replay, buckets not overlapped)
+  if (graph_comm_) eager_step();
+  else fwd_bwd();
   HIP_OK(hipStreamEndCapture(stream_, &graph_));
   CachingAllocator::set_current_pool(0);
   HIP_OK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
@@ -106,18 +119,19 @@ Tensor Trainer::step(const std::vector<std::pair<const int64_t*, const int64_t*>
     } else {
       capture();
       HIP_OK(hipGraphLaunch(exec_, stream_));
-      if (comm_) {
+      if (!graph_comm_) {
         reduce_grads();
-        opt_.step();
+        optimizer();
       }
     }
   } else {
     HIP_OK(hipGraphLaunch(exec_, stream_));
-    if (comm_) {
+    if (!graph_comm_) {
       reduce_grads();
-      opt_.step();
+      optimizer();
     }
   }
+  if (comm_) comm_->heartbeat();
   return loss_acc_;
 }
 
@@ -156,6 +170,63 @@ std::pair<double, double> Trainer::evaluate(int max_batches, int batch_size) {
   return {m, std::exp(std::min(m, 50.0))};
 }
 
+double Trainer::bench(int warmup, int steps, float* final_loss) {
+  const int B = cfg_.batch, S = cfg_.seq, A = (int)ids_.size();
+  std::vector<std::vector<int64_t>> hid(A, std::vector<int64_t>((size_t)B * S)),
+      htg(A, std::vector<int64_t>((size_t)B * S));
+  std::vector<float> mk((size_t)B * S);
+  Tensor loss;
+  auto one = [&](int64_t it) {
+    opt_.set_lr(cfg_.lr_fn ? cfg_.lr_fn(it, warmup + steps) : cfg_.lr);
+    std::vector<std::pair<const int64_t*, const int64_t*>> micro;
+    for (int a = 0; a < A; ++a) {
+      train_.next_batch(B, true, hid[a].data(), htg[a].data(), mk.data(), nullptr);
+      micro.push_back({hid[a].data(), htg[a].data()});
+    }
+    loss = step(micro);
+    ++global_step;
+    total_tokens += (int64_t)A * B * S;
+  };
+  for (int i = 0; i < warmup; ++i) one(i);
+  auto fence = [&]() {
+    synchronize();
+    if (comm_) comm_->barrier(stream_);
+    synchronize();
+  };
+  fence();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < steps; ++i) one(warmup + i);
+  fence();
+  double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  float l = (float)loss.item();
+  if (comm_) {  // slowest rank's clock; rank-mean loss
+    float h2[2] = {(float)dt, l};
+    Tensor d = from_host(h2, {2}, DType::F32);
+    comm_->all_reduce_max(static_cast<float*>(d.data_ptr()), 1, stream_);
+    comm_->all_reduce_avg(static_cast<float*>(d.data_ptr()) + 1, 1, stream_);
+    const std::vector<float> back = d.to_vector_f32();
+    dt = back[0];
+    l = back[1];
+  }
+  if (final_loss) *final_loss = l;
+  return dt;
+}
+
+void Trainer::sync_ema() {
+  const std::vector<float> h = ema_dev_.to_vector_f32();  // {ema, initialised}
+  float e[2] = {h[0] * h[1], h[1]};
+  if (comm_) {  // every rank joins (rank-invariant): the mean over the initialised ranks
+    Tensor d = from_host(e, {2}, DType::F32);
+    comm_->all_reduce_sum(static_cast<float*>(d.data_ptr()), 2, current_stream());
+    const std::vector<float> b = d.to_vector_f32();
+    e[0] = b[0], e[1] = b[1];
+  }
+  if (e[1] > 0.f) {
+    ema_loss = e[0] / e[1];
+    ema_init = true;
+  }
+}
+
 void Trainer::train(const std::function<void(int64_t)>& save_fn) {
   if (total_steps_ <= 0) {
     std::printf("[Train] nothing to do (steps=0)\n");
@@ -190,6 +261,8 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
     total_tokens += tokens;
     tok_since += tokens;
     ++steps_since;
+    // training-loss EMA every step, on device (a non-finite loss is skipped); read at log / save
+    k::ema_update(ema_dev_.data<float>(), loss.data<float>(), std::max(0.f, std::min(0.9999f, cfg_.ema_beta)), stream_);
     const bool log_now = cfg_.log_interval > 0 && (global_step % cfg_.log_interval == 0 || it + 1 == total_steps_);
     if (log_now) {
       if (comm_) {  // mean over ranks (a copy: the graph keeps accumulating into loss_acc_)
@@ -198,6 +271,7 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
         loss = lc;
       }
       const float l = (float)loss.item();  // syncs the stream
+      sync_ema();
       const auto now = std::chrono::steady_clock::now();
       const double dt = std::chrono::duration<double>(now - t_last).count();
       t_last = now;
@@ -206,29 +280,45 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
       tok_since = 0;
       steps_since = 0;
       losses.push_back(l);
-      ema_loss = ema_init ? cfg_.ema_beta * ema_loss + (1.0 - cfg_.ema_beta) * l : l;
-      ema_init = true;
       const float gn = opt_.grad_norm();
       const int nr = comm_ ? comm_->world() : 1;
-      if (lead())
-        std::printf("[Step %lld/%lld] Loss=%.4f PPL=%.2f LR=%.6g GradNorm=%.4f EMA=%.4f tok/s=%.0f step_ms=%.2f\n",
-                    (long long)global_step, (long long)total_steps_, l, std::exp(std::min<double>(l, 50.0)), lr, gn,
-                    ema_loss, tps * nr, step_ms);
+      const double ppl = std::exp(std::min<double>(l, 50.0));
+      if (lead()) {
+        if (cfg_.log_style == "gemma") {
+          // reference optim/gemma_trainer.cpp:193-197
+          std::printf("[Step %lld] Loss=%.4f PPL=%.2f LR=%.6g GradNorm=%.4f EMA=%.4f tok/s=%.0f step_ms=%.2f\n",
+                      (long long)global_step, l, ppl, lr, gn, ema_loss, tps * nr, step_ms);
+        } else {
+          // reference gpt2_lora_finetune/main.cpp:627-635 (+ throughput fields at the end)
+          std::printf("[Train] epoch %lld/%d | step %lld/%lld (global %lld/%lld) | lr %.6f | loss %.4f | ppl %.2f | "
+                      "grad_norm %.3f | tokens %lld | tok/s %.0f | step_ms %.2f\n",
+                      (long long)(it / steps_per_epoch_ + 1), cfg_.epochs, (long long)(it % steps_per_epoch_ + 1),
+                      (long long)steps_per_epoch_, (long long)global_step, (long long)total_steps_, lr, l, ppl, gn,
+                      (long long)(tokens * nr), tps * nr, step_ms);
+        }
+      }
       std::fflush(stdout);
       if (metrics.is_open() && lead()) {
         metrics << "{\"step\": " << global_step << ", \"loss\": " << l << ", \"lr\": " << lr << ", \"grad_norm\": " << gn
-                << ", \"tokens_per_s\": " << tps << ", \"step_ms\": " << step_ms << "}\n";
+                << ", \"ema_loss\": " << ema_loss << ", \"tokens_per_s\": " << tps * nr << ", \"step_ms\": " << step_ms
+                << "}\n";
         metrics.flush();
       }
     }
     if (cfg_.eval_interval > 0 && global_step % cfg_.eval_interval == 0 && valid_) {
       auto ev = evaluate(cfg_.eval_batches, cfg_.eval_batch_size);
-      if (lead())
-        std::printf("\n[Eval] step %lld | valid_nll %.4f | valid_ppl %.2f\n\n", (long long)global_step, ev.first,
-                    ev.second);
+      sync_ema();
+      const long long epoch = it / steps_per_epoch_ + 1;
+      if (lead())  // reference gpt2_lora_finetune/main.cpp:645-664
+        std::printf("\n[Eval] epoch %lld | step %lld | valid_ppl %.2f | ema_loss %.4f | total_tokens %lld | valid_nll %.4f\n\n",
+                    epoch, (long long)global_step, ev.second, ema_loss, (long long)(total_tokens * (comm_ ? comm_->world() : 1)),
+                    ev.first);
       if (!cfg_.eval_out.empty() && lead()) {
         std::ofstream eo(cfg_.eval_out, std::ios::app);
-        eo << "{\"step\": " << global_step << ", \"nll\": " << ev.first << ", \"ppl\": " << ev.second << "}\n";
+        eo.precision(9);
+        eo << "{\"step\":" << global_step << ",\"epoch\":" << epoch << ",\"valid_ppl\":" << ev.second
+           << ",\"ema_loss\":" << ema_loss << ",\"total_tokens\":" << total_tokens * (comm_ ? comm_->world() : 1)
+           << ",\"valid_nll\":" << ev.first << "}\n";
       }
     }
     if (cfg_.save_every > 0 && global_step % cfg_.save_every == 0) {
@@ -252,6 +342,9 @@ void Trainer::save_state(const std::string& dir) {
   namespace fs = std::filesystem;
   synchronize();
   const int r = comm_ ? comm_->rank() : 0;
+  if (dp_) dp_->gather_master();  // ZeRO: every rank's master chunks (collective)
+  sync_ema();
+  synchronize();
   const std::string tmp = dir + ".tmp", old = dir + ".old";
   if (r == 0) {
     fs::remove_all(tmp);
@@ -259,13 +352,20 @@ void Trainer::save_state(const std::string& dir) {
   }
   if (comm_) comm_->barrier(stream_);
   if (r == 0) {
-    const Tensor mh = flat_.master.to(Device::cpu()), m1 = opt_.m.to(Device::cpu()), m2 = opt_.v.to(Device::cpu());
+    const Tensor mh = flat_.master.to(Device::cpu());
     const size_t nb = (size_t)flat_.numel * sizeof(float);
     safetensors_save(tmp + "/trainable.safetensors", {{"master", "F32", {flat_.numel}, mh.data_ptr(), nb}},
                      {{"format", "mft-flat"}}, false, true);
-    safetensors_save(tmp + "/optimizer.safetensors",
-                     {{"m", "F32", {flat_.numel}, m1.data_ptr(), nb}, {"v", "F32", {flat_.numel}, m2.data_ptr(), nb}},
-                     {{"format", "mft-flat"}}, false, true);
+  }
+  // AdamW moments: the whole flat (replicated, rank 0 writes it) or each rank's ZeRO partition
+  if (r == 0 || opt_.sharded()) {
+    Tensor m1 = empty({opt_.m.numel()}, DType::F32, Device::cpu()), m2 = empty({opt_.v.numel()}, DType::F32, Device::cpu());
+    m1.copy_(opt_.m.is_hip() ? opt_.m.to(Device::cpu()) : opt_.m);
+    m2.copy_(opt_.v.is_hip() ? opt_.v.to(Device::cpu()) : opt_.v);
+    const std::string fn = opt_.sharded() ? "/optimizer.rank" + std::to_string(r) + ".safetensors" : "/optimizer.safetensors";
+    const size_t sb = (size_t)m1.numel() * sizeof(float);
+    safetensors_save(tmp + fn, {{"m", "F32", {m1.numel()}, m1.data_ptr(), sb}, {"v", "F32", {m2.numel()}, m2.data_ptr(), sb}},
+                     {{"format", opt_.sharded() ? "mft-zero-partition" : "mft-flat"}}, false, true);
   }
   std::ofstream f(tmp + "/trainer_state.rank" + std::to_string(r) + ".json");
   f.precision(17);
@@ -299,20 +399,25 @@ bool Trainer::load_state(const std::string& dir0) {
   const json::Value st = json::parse(txt);
   MFT_CHECK(st["numel"].as_int() == flat_.numel, "load_state: ", dir, " holds ", st["numel"].as_int(),
             " trainable values, the model has ", flat_.numel);
-  SafeTensorsFile tw(dir + "/trainable.safetensors"), to(dir + "/optimizer.safetensors");
-  auto host_view = [&](SafeTensorsFile& sf, const char* k) {
-    MFT_CHECK(sf.has(k) && sf.info(k).dtype == "F32" && sf.info(k).end - sf.info(k).begin == (uint64_t)flat_.numel * 4,
-              "load_state: bad tensor ", k, " in ", sf.path());
-    return from_blob(const_cast<void*>(sf.data(k)), {flat_.numel}, DType::F32, Device::cpu());
+  SafeTensorsFile tw(dir + "/trainable.safetensors");
+  SafeTensorsFile to(dir + (opt_.sharded() ? "/optimizer.rank" + std::to_string(r) + ".safetensors" : "/optimizer.safetensors"));
+  auto host_view = [&](SafeTensorsFile& sf, const char* k, int64_t n) {
+    MFT_CHECK(sf.has(k) && sf.info(k).dtype == "F32" && sf.info(k).end - sf.info(k).begin == (uint64_t)n * 4,
+              "load_state: bad tensor ", k, " in ", sf.path(), " (a different ZeRO stage / world size?)");
+    return from_blob(const_cast<void*>(sf.data(k)), {n}, DType::F32, Device::cpu());
   };
-  flat_.master.copy_(host_view(tw, "master"));
-  opt_.load_state(host_view(to, "m"), host_view(to, "v"), st["opt_step"].as_int());
+  flat_.master.copy_(host_view(tw, "master", flat_.numel));
+  opt_.load_state(host_view(to, "m", opt_.m.numel()), host_view(to, "v", opt_.v.numel()), st["opt_step"].as_int());
   synchronize();  // the mmaps go away with the files
   flat_.refresh_shadow();
   global_step = st["global_step"].as_int();
   total_tokens = st["total_tokens"].as_int();
   ema_loss = st["ema_loss"].as_double();
   ema_init = st["ema_init"].as_int() != 0;
+  {
+    const float e[2] = {(float)ema_loss, ema_init ? 1.f : 0.f};
+    ema_dev_.copy_(from_blob(const_cast<float*>(e), {2}, DType::F32, Device::cpu()));
+  }
   model_.dropout_ctr.fill_((double)st["dropout_ctr"].as_int());
   const json::Value& d = st["data"];
   train_.restore(d["epoch"].as_int(), (size_t)d["cursor"].as_int(), d["rng"].as_string());

@@ -7,11 +7,13 @@
 // micro-batch forward+backward, clip, AdamW) is captured ONCE into a hipGraph after two eager
 // warm-up steps (relaxed capture mode, private allocator pool) and replayed with the next batch
 // copied into the graph's static input buffers; the loss stays on the device and is read only when
-// a log line is due.  Data parallelism (native RCCL communicator, engine/comm.h): every rank
-// starts from rank 0's weights (broadcast), reads its own data shard, and the flat gradient is
-// averaged by ONE all-reduce on the compute stream between the replayed forward/backward graph
-// and the optimizer step (LoRA: 1.8 MB, latency-bound); logged losses and eval sums are reduced
-// over the ranks and only rank 0 prints and saves.
+// a log line is due.  Data parallelism (engine/comm.h communicator + engine/dist.h reducer): every
+// rank starts from rank 0's weights (broadcast), reads its own data shard, and the gradient buckets
+// are reduced on a communication stream as the backward completes them (grad-ready hooks), ZeRO-1/2
+// partitioning the optimizer; the bucket collectives, the optimizer and the shadow all-gather are
+// recorded into the same hipGraph as the forward / backward (MFT_GRAPH_COMM=0: run them eagerly
+// after each replay instead).  Logged losses and eval sums are reduced over the ranks and only
+// rank 0 prints and saves.
 #pragma once
 #include <functional>
 #include <memory>
@@ -19,6 +21,7 @@
 #include <vector>
 
 #include "engine/comm.h"
+#include "engine/dist.h"
 #include "engine/lm.h"
 #include "engine/optim.h"
 #include "runtime/dataset.h"
@@ -35,6 +38,9 @@ struct TrainConfig {
   float lr = 1e-4f;  // base learning rate of the schedule
   int log_interval = 1, eval_interval = 0, eval_batches = 50, eval_batch_size = 2, save_every = 0;
   float ema_beta = 0.9f;
+  // console line format: "gpt2" = the reference GPT-2 CLI's "[Train] epoch .. | step s/S (global g/G)
+  // | lr | loss | ppl | grad_norm | tokens", "gemma" = the reference Gemma trainer's "[Step n] Loss=.."
+  std::string log_style = "gpt2";
   bool use_graph = true;
   std::string eval_out, metrics_out;
   std::string state_dir;  // full training-state checkpoint written at every save point and at the end
@@ -49,8 +55,9 @@ struct TrainConfig {
 
 class Trainer {
  public:
+  // comm != null requires dp (the reducer of that communicator)
   Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid, const TrainConfig& cfg,
-          PowerMonitor* pm = nullptr, Communicator* comm = nullptr);
+          PowerMonitor* pm = nullptr, Communicator* comm = nullptr, DataParallel* dp = nullptr);
   ~Trainer();
   int64_t total_steps() const { return total_steps_; }
   int64_t steps_per_epoch() const { return steps_per_epoch_; }
@@ -58,6 +65,11 @@ class Trainer {
   // device loss (mean over micro-batches)
   Tensor step(const std::vector<std::pair<const int64_t*, const int64_t*>>& micro);
   void train(const std::function<void(int64_t)>& save_fn);
+  // Benchmark (bench.py's native engine): `warmup` untimed optimizer steps (the first two eager,
+  // then the hipGraph capture), then `steps` timed steps bracketed on both sides by a device
+  // synchronize and, with a communicator, a cross-rank barrier.  Returns the MAX over ranks of the
+  // timed wall seconds; *final_loss = the last step's (rank-mean) loss.
+  double bench(int warmup, int steps, float* final_loss);
   std::pair<double, double> evaluate(int max_batches, int batch_size);  // (nll, ppl)
   // Full training state (same directory layout as the Python CLIs' --state_dir):
   // trainable.safetensors (fp32 master) + optimizer.safetensors (AdamW m, v) from rank 0 -- data
@@ -76,8 +88,10 @@ class Trainer {
  private:
   void eager_step();
   void fwd_bwd();
-  void reduce_grads();
+  void reduce_grads();   // dp: the buckets no hook launched + join the comm stream
+  void optimizer();      // AdamW (+ ZeRO shadow all-gather)
   void capture();
+  void sync_ema();       // host mirror (ema_loss / ema_init) of the device EMA, rank-mean
   bool lead() const { return !comm_ || comm_->rank() == 0; }
   LanguageModel& model_;
   FlatParams& flat_;
@@ -87,10 +101,12 @@ class Trainer {
   TrainConfig cfg_;
   PowerMonitor* pm_;
   Communicator* comm_;
+  DataParallel* dp_;
+  bool graph_comm_ = true;  // collectives + optimizer inside the captured step
   int64_t total_steps_ = 0, steps_per_epoch_ = 1;
   // static device inputs (the graph reads these) + loss accumulator
   std::vector<Tensor> ids_, labels_;
-  Tensor loss_acc_, one_;
+  Tensor loss_acc_, one_, ema_dev_;
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;
   hipStream_t stream_ = nullptr;

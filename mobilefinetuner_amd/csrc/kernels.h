@@ -189,6 +189,7 @@ struct AdamWArgs {
   bf16_t* shadow;         // optional bf16 copy
   const int* nonfinite;   // optional device flag: skip the step when set
   int moments_bf16;       // m / v are bf16 (stochastically rounded; host-offloaded optimizer state)
+  long sr_offset;         // global element index of p[0] (chunked / sharded launches): keys the SR hash
 };
 void adamw_step(const AdamWArgs& a, hipStream_t st);
 // after every adamw_step launch of one update: *step += 1 unless the update was skipped

@@ -63,7 +63,8 @@ __device__ __forceinline__ bool adamw_skip(const int* nonfinite, const float* su
   return (nonfinite && *nonfinite) || (sumsq && !isfinite(*sumsq));
 }
 
-// bf16 moments (MB): stochastic rounding with a counter hash of (step, element) -- round-to-nearest
+// bf16 moments (MB): stochastic rounding with a counter hash of (step, GLOBAL element index: the
+// launch's sr_offset + local index, so chunked / sharded launches draw independent noise) -- round-to-nearest
 // would freeze v under beta2 = 0.999 (a 0.1% change is below half a bf16 ulp) and bias m; SR keeps
 // both unbiased.  The fp32 master weights and the update itself stay fp32.
 __device__ __forceinline__ uint32_t sr_hash(uint32_t x) {
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
     }
     reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
     if constexpr (MB) {
-      const uint32_t r = sr_hash(seed ^ (uint32_t)i), r2 = sr_hash(r);
+      const uint32_t r = sr_hash(seed ^ (uint32_t)(a.sr_offset / 4 + i)), r2 = sr_hash(r);
       uint2 mb, vb;
       mb.x = (uint32_t)f2bf_sr(mm[0], r) | ((uint32_t)f2bf_sr(mm[1], r >> 16) << 16);
       mb.y = (uint32_t)f2bf_sr(mm[2], r2) | ((uint32_t)f2bf_sr(mm[3], r2 >> 16) << 16);
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
       const float vj = a.beta2 * ld_mom<MB>(a.v, i) + (1.f - a.beta2) * gj * gj;
       pj = pj * decay - step_size * mj / (sqrtf(vj) * rbc2 + a.eps);
       a.p[i] = pj;
-      const uint32_t r = sr_hash(seed ^ 0x5bd1e995U ^ (uint32_t)i);
+      const uint32_t r = sr_hash(seed ^ 0x5bd1e995U ^ (uint32_t)(a.sr_offset + i));
       st_mom<MB>(a.m, i, mj, r);
       st_mom<MB>(a.v, i, vj, r >> 16);
       if (a.shadow) a.shadow[i] = f2bf(pj);

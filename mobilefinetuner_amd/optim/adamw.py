@@ -148,13 +148,13 @@ class FusedAdamW:
                              self.sumsq_dev if self.max_grad_norm is not None else None,
                              self.beta1, self.beta2, self.eps, self.weight_decay,
                              float(self.max_grad_norm or 0.0), self.l2_coupled, sh,
-                             self.nonfinite_dev if self.skip_nonfinite else None)
+                             self.nonfinite_dev if self.skip_nonfinite else None, self.lo)
             elif self.offload:
                 self._step_offloaded(C, p, g, sh)
             else:
                 C.adamw_step(p, g, self.m, self.v, self.lr_dev, self.step_dev, sumsq,
                              self.beta1, self.beta2, self.eps, self.weight_decay,
-                             float(self.max_grad_norm or 0.0), self.l2_coupled, sh, nonfinite)
+                             float(self.max_grad_norm or 0.0), self.l2_coupled, sh, nonfinite, self.lo)
             C.adamw_commit(self.step_dev, nonfinite, sumsq)
         else:
             self._step_reference(p, g)
@@ -203,7 +203,7 @@ class FusedAdamW:
                          self.beta1, self.beta2, self.eps, self.weight_decay,
                          float(self.max_grad_norm or 0.0), self.l2_coupled,
                          sh[c0:c1] if sh is not None else None,
-                         self.nonfinite_dev if self.skip_nonfinite else None)
+                         self.nonfinite_dev if self.skip_nonfinite else None, self.lo + c0)
             self._d2h.wait_stream(cur)
             with torch.cuda.stream(self._d2h):
                 self._host[i][0].copy_(mb[:c1 - c0], non_blocking=True)

@@ -321,11 +321,16 @@ class Zero3:
 
     # ------------------------------------------------------------------ DataParallel-style reducer
     def begin_step(self):
-        u = self.units[0]
-        if not u.g_live:
-            if not self.direct:
-                u.gwork.zero_()
-            u.g_live = True
+        """Host bookkeeping before a step (runs eagerly, also before each graph replay)."""
+        self.units[0].g_live = True
+
+    def zero_grad_buffers(self):
+        """Device side of the step start, issued by TrainStep inside the (captured) step: the outer
+        unit's gradient buffer starts every step at zero.  (Zeroing it from begin_step instead ran
+        outside the graph and, keyed on g_live, was skipped from the second replay on -- the outer
+        unit's gradients then kept adding up across steps on the copy path.)"""
+        if not self.direct:
+            self.units[0].gwork.zero_()
 
     def finish(self):
         """After the last micro-batch's backward: outer-unit grads, replicated grads."""

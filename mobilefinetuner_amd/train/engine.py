@@ -48,6 +48,8 @@ class TrainStep:
             self.loss_dev = torch.zeros(1, device=self.flat.grad.device, dtype=torch.float32)
         self.loss_dev.zero_()
         self.flat.grad.zero_()
+        if self.dp is not None and hasattr(self.dp, "zero_grad_buffers"):
+            self.dp.zero_grad_buffers()  # reducer-owned gradient buffers (ZeRO-3 slots): in the graph
         from ..ops.functional import dropout_counter
         dropout_counter(self.flat.grad.device).add_(1)  # fresh LoRA-dropout masks every step
         for i, (ids, lab) in enumerate(batches):

@@ -302,12 +302,16 @@ class Trainer:
 
     def _sync_metrics(self):
         """Host copies of the device-side EMA and skipped-step counter (one sync, log time)."""
-        if self.cfg.ema_beta > 0 and float(self._ema_init.item()) > 0:
-            e = self._ema_dev.clone()
+        if self.cfg.ema_beta > 0:
+            # rank-invariant: every rank joins the all-reduce whether or not its own EMA has seen a
+            # finite loss yet (branching on the local init flag first could leave some ranks out of
+            # the collective and hang the job); the EMA is the mean over the initialised ranks
+            e = torch.cat([(self._ema_dev * self._ema_init).reshape(1), self._ema_init.reshape(1)]).float()
             if is_dist():
                 allreduce_sum_(e)
-                e /= self.world
-            self.ema_loss = float(e.item())
+            n = float(e[1].item())
+            if n > 0:
+                self.ema_loss = float(e[0].item()) / n
         sk = getattr(self.opt, "skipped_dev", None)
         if sk is not None:
             self.skipped = self._skipped_base + int(sk.item())

@@ -56,7 +56,7 @@ def _worker_ddp(rank, world, port, q):
     loss = m(mine[:, :-1], mine[:, 1:])
     loss.backward()
     dp.finish()
-    q.put((rank, flat.grad.clone(), len(dp.buckets)))
+    q.put((rank, flat.grad.clone().numpy(), len(dp.buckets)))
     dist.destroy_process_group()
 
 
@@ -69,7 +69,7 @@ def test_ddp_grads_equal_single_process_large_batch():
     ps = [ctx.Process(target=_worker_ddp, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict((r, (g, nb)) for r, g, nb in [q.get(timeout=300) for _ in ps])
+    res = dict((r, (torch.as_tensor(g), nb)) for r, g, nb in [q.get(timeout=300) for _ in ps])
     for p in ps:
         p.join(60)
     sys.path.insert(0, ROOT)
@@ -197,7 +197,7 @@ def _worker_zero_shadow(rank, world, port, q):
         opt.reduce_gradients()
         opt.step()
     ln = torch.cat([m.blocks[0].ln_1.weight.detach().flatten(), m.ln_f.bias.detach().flatten()])
-    q.put((rank, ln.clone()))
+    q.put((rank, ln.clone().numpy()))
     dist.destroy_process_group()
 
 
@@ -208,7 +208,7 @@ def test_zero_syncs_fp32_compute_params():
     ps = [ctx.Process(target=_worker_zero_shadow, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    out = dict(q.get(timeout=600) for _ in ps)
+    out = dict((r, torch.as_tensor(v)) for r, v in [q.get(timeout=600) for _ in ps])
     for p in ps:
         p.join(60)
     assert not torch.equal(out[0], torch.ones_like(out[0]))  # updated
@@ -262,7 +262,7 @@ def _worker_ddp_accum_hooks(rank, world, port, q):
             if micro == 1:
                 Fx.grad_ready(p)  # a second announcement (tied weights) must not double count
     dp.finish()
-    q.put((rank, flat.grad.clone(), total.clone()))
+    q.put((rank, flat.grad.clone().numpy(), total.clone().numpy()))
     dist.destroy_process_group()
 
 
@@ -273,7 +273,7 @@ def test_ddp_overlap_with_grad_accumulation():
     ps = [ctx.Process(target=_worker_ddp_accum_hooks, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    out = dict((r, (g, t)) for r, g, t in [q.get(timeout=300) for _ in ps])
+    out = dict((r, (torch.as_tensor(g), torch.as_tensor(t))) for r, g, t in [q.get(timeout=300) for _ in ps])
     for p in ps:
         p.join(60)
     want = (out[0][1] + out[1][1]) / 2  # mean over ranks of the summed micro-batch grads
@@ -306,7 +306,7 @@ def _worker_bucketed_reduce(rank, world, port, q, stage, bf16):
         Fx._sink(sl.param, g)
     dp.finish()
     lo, hi = dp.owned()
-    q.put((rank, lo, hi, flat.grad.clone(), local))
+    q.put((rank, lo, hi, flat.grad.clone().numpy(), local.numpy() if torch.is_tensor(local) else local))
     dp.close()
     dist.destroy_process_group()
 
@@ -319,7 +319,7 @@ def test_bucketed_reduce_owner_and_bf16(stage, bf16):
     ps = [ctx.Process(target=_worker_bucketed_reduce, args=(r, 2, port, q, stage, bf16)) for r in range(2)]
     for p in ps:
         p.start()
-    out = {r: (lo, hi, g, l) for r, lo, hi, g, l in [q.get(timeout=300) for _ in ps]}
+    out = {r: (lo, hi, torch.as_tensor(g), torch.as_tensor(l)) for r, lo, hi, g, l in [q.get(timeout=300) for _ in ps]}
     for p in ps:
         p.join(60)
     want = (out[0][3] + out[1][3]) / 2

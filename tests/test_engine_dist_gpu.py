@@ -1,0 +1,195 @@
+"""Native data parallelism (libmft engine/comm.h + engine/dist.h) with several ranks on ONE GPU.
+
+The loopback backend (MFT_COMM_BACKEND=loopback: host TCP star, collectives as D2H copy -> host
+reduce -> H2D copy, recorded into the hipGraph as host nodes) lets N native rank processes share a
+single MI355X -- RCCL refuses two ranks on one device -- so the multi-rank code paths run here:
+rank-0 weight broadcast, per-rank data shards, bucketed gradient reduction from the grad-ready hooks,
+ZeRO-1 / ZeRO-2 partitioned AdamW (+ pinned-host moments), the bf16 shadow all-gather, reduced losses
+and eval sums.  Each is checked against ONE process at the same GLOBAL batch (--deterministic).
+RCCL itself is exercised on a 1-rank group with the whole ZeRO-2 step (reduce-scatter, all-gather)
+recorded into the hipGraph.  Failure detection: a rank that dies makes its peer exit non-zero.
+"""
+import os
+import re
+import socket
+import subprocess
+import time
+
+import pytest
+import torch
+from native_logs import PLOT_PATTERN1, PLOT_PATTERN2, loss_list
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "mobilefinetuner_amd", "bin")
+
+
+def _bin(name):
+    p = os.path.join(BIN, name)
+    if not os.path.exists(p):
+        pytest.fail(f"{p} missing: run python -m mobilefinetuner_amd._build")
+    return p
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env(rank=0, world=1, port=None, backend="loopback", **extra):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MFT_DP_FORCE_COMM"):
+        env.pop(k, None)
+    if world > 1 or extra.get("MFT_DP_FORCE_COMM") == "1":
+        env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port or _port()), MFT_COMM_BACKEND=backend)
+    env.update({k: str(v) for k, v in extra.items()})
+    return env
+
+
+def _run_ranks(cmd, world, timeout=240, backend="loopback", extra_env=None, per_rank=None):
+    """Start `world` native rank processes (one shared GPU); returns [(rc, stdout, stderr)]."""
+    port = _port()
+    procs = []
+    for r in range(world):
+        c = cmd + (per_rank(r) if per_rank else [])
+        procs.append(subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                      env=_env(r, world, port, backend, **(extra_env or {}))))
+    out = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        out.append((p.returncode, o, e))
+    return out
+
+
+FULL = ["--random_init", "--model", "gpt2-tiny", "--synthetic_data", "--synthetic_tokens", "100000", "--seq_len", "64",
+        "--lr", "1e-3", "--log_interval", "1", "--deterministic", "--steps", "6", "--bucket_mb", "0.25"]
+
+
+def _single(prog, args, batch_flag, batch):
+    r = subprocess.run([_bin(prog), *args, batch_flag, str(batch)], capture_output=True, text=True, timeout=240,
+                       env=_env())
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    return r
+
+
+@pytest.mark.parametrize("extra,tol", [
+    ([], 2e-4),
+    (["--zero_stage", "1"], 2e-4),
+    (["--zero_stage", "2"], 2e-4),
+    (["--zero_stage", "2", "--offload", "host"], 3e-3),   # bf16 stochastically-rounded moments
+    (["--bf16_grads"], 1e-2),
+    (["--zero_stage", "2", "--no_overlap", "--no_graph"], 2e-4),
+])
+def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
+    """2 loopback ranks x batch 4 == 1 process x batch 8 (GPT-2-tiny full fine-tune, ~8 buckets):
+    the same per-step losses and the same final weights."""
+    ref_out = str(tmp_path / "ref.safetensors")
+    ref = _single("gpt2_full_finetune", FULL + ["--output_path", ref_out], "--batch_size", 8)
+    want = loss_list(ref.stdout, True)
+    dp_out = str(tmp_path / "dp.safetensors")
+    res = _run_ranks([_bin("gpt2_full_finetune"), *FULL, "--batch_size", "4", "--output_path", dp_out, *extra], 2)
+    for rc, o, e in res:
+        assert rc == 0, o[-2000:] + e[-2000:]
+    out0 = res[0][1]
+    assert "data parallel: rank 0 of 2 (loopback" in out0 and "bucket(s)" in out0, out0[:3000]
+    got = loss_list(out0, True)
+    assert len(got) == 6 and got == pytest.approx(want, rel=tol, abs=tol), (extra, got, want)
+    from mobilefinetuner_amd.io import safetensors as st
+    a, b = st.load_file(ref_out), st.load_file(dp_out)
+    wtol = 50 * tol
+    for k in a:
+        assert torch.allclose(a[k], b[k], atol=wtol, rtol=wtol), (extra, k, (a[k] - b[k]).abs().max())
+
+
+def test_native_dp_lora_and_gemma_two_ranks():
+    """LoRA (one fused bucket) on GPT-2-tiny and Gemma-3-tiny: 2 loopback ranks == 1 process."""
+    lora = ["--random_init", "--model", "gpt2-tiny", "--synthetic_data", "--synthetic_tokens", "100000", "--seq_len",
+            "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic", "--steps", "5"]
+    want = loss_list(_single("gpt2_lora_finetune", lora, "--batch_size", 8).stdout, True)
+    res = _run_ranks([_bin("gpt2_lora_finetune"), *lora, "--batch_size", "4"], 2)
+    assert all(rc == 0 for rc, _, _ in res), res[0][1][-2000:] + res[0][2][-2000:]
+    assert loss_list(res[0][1], True) == pytest.approx(want, rel=2e-4, abs=2e-4)
+    gem = ["--random_init", "--model", "gemma3-tiny", "--synthetic_data", "--synthetic_tokens", "100000", "--seq_len",
+           "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic", "--max_steps", "5", "--lora_dropout", "0",
+           "--lr_schedule", "constant", "--zero_stage", "1"]
+    want = loss_list(_single("train_lora_gemma", gem[:-2], "--batch", 8).stdout, True)
+    res = _run_ranks([_bin("train_lora_gemma"), *gem, "--batch", "4"], 2)
+    assert all(rc == 0 for rc, _, _ in res), res[0][1][-2000:] + res[0][2][-2000:]
+    assert loss_list(res[0][1], True) == pytest.approx(want, rel=2e-4, abs=2e-4)
+
+
+def test_native_rccl_zero2_step_in_graph():
+    """A 1-rank RCCL group running ZeRO-2 with the whole step (bucket reduce-scatters on the comm
+    stream, partitioned AdamW with the all-reduced norm, shadow all-gather) recorded into ONE
+    hipGraph: the capture succeeds and the losses match the plain single-process step."""
+    want = loss_list(_single("gpt2_full_finetune", FULL, "--batch_size", 4).stdout, True)
+    r = subprocess.run([_bin("gpt2_full_finetune"), *FULL, "--batch_size", "4", "--zero_stage", "2"],
+                       capture_output=True, text=True, timeout=240, env=_env(backend="rccl", MFT_DP_FORCE_COMM="1"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "data parallel: rank 0 of 1 (rccl" in r.stdout and "ZeRO-2" in r.stdout, r.stdout[:3000]
+    assert loss_list(r.stdout, True) == pytest.approx(want, rel=2e-4, abs=2e-4)
+
+
+def test_native_dp_state_resume_two_ranks(tmp_path):
+    """ZeRO-2 full-state checkpoint (gathered fp32 master + one optimizer partition per rank):
+    4 steps, then both ranks resume from the saved state and finish steps 5-8 with the
+    uninterrupted run's losses."""
+    base = FULL[:-4] + ["--bucket_mb", "0.25", "--batch_size", "4", "--zero_stage", "2", "--warmup_steps", "100"]
+    ref = _run_ranks([_bin("gpt2_full_finetune"), *base, "--steps", "8"], 2)
+    assert all(rc == 0 for rc, _, _ in ref)
+    want = loss_list(ref[0][1])
+    state = str(tmp_path / "state")
+    a = _run_ranks([_bin("gpt2_full_finetune"), *base, "--steps", "4", "--state_dir", state], 2)
+    assert all(rc == 0 for rc, _, _ in a), a[0][2][-2000:]
+    assert os.path.exists(os.path.join(state, "optimizer.rank1.safetensors"))
+    b = _run_ranks([_bin("gpt2_full_finetune"), *base, "--steps", "8", "--state_dir", state], 2)
+    assert all(rc == 0 for rc, _, _ in b), b[0][2][-2000:]
+    assert "resumed full training state" in b[0][1]
+    assert loss_list(a[0][1]) + loss_list(b[0][1]) == want, (want, a[0][1][-1500:], b[0][1][-1500:])
+
+
+def test_native_peer_failure_makes_the_other_rank_exit():
+    """rank 1 dies before step 3 (--inject_fault 3:1); rank 0, blocked in that step's
+    collective, sees the lost peer and exits with code 3 well within MFT_COMM_TIMEOUT (no hang)."""
+    t0 = time.time()
+    res = _run_ranks([_bin("gpt2_full_finetune"), *FULL, "--batch_size", "4", "--inject_fault", "3:1"], 2,
+                     timeout=120, extra_env={"MFT_COMM_TIMEOUT": "60"})
+    dt = time.time() - t0
+    (rc0, o0, e0), (rc1, o1, e1) = res
+    assert rc1 != 0 and "injected fault at step 3" in e1, e1[-1500:]
+    assert rc0 == 3 and "[mft comm] rank 0/2" in e0, (rc0, e0[-2000:])
+    assert dt < 100, dt
+
+
+def test_native_logs_parse_with_the_reference_plotter_regexes():
+    """The reference's loss plotter (scripts/Finetune/plot_loss_curve.py:18-19) parses the native
+    GPT-2 ([Train] ... step s/S ... loss X) and Gemma ([Step n] Loss=X) console lines."""
+    r = _single("gpt2_lora_finetune", FULL[:-4] + ["--steps", "3"], "--batch_size", 4)
+    m = [re.search(PLOT_PATTERN2, ln, re.IGNORECASE) for ln in r.stdout.splitlines() if ln.startswith("[Train]")]
+    assert len(m) == 3 and all(m), r.stdout[-1500:]
+    g = _single("train_lora_gemma", ["--random_init", "--model", "gemma3-tiny", "--synthetic_data", "--synthetic_tokens",
+                                     "100000", "--seq_len", "64", "--max_steps", "3", "--log_interval", "1"], "--batch", 4)
+    m = [re.search(PLOT_PATTERN1, ln) for ln in g.stdout.splitlines() if ln.startswith("[Step")]
+    assert len(m) == 3 and all(m) and [int(x.group(1)) for x in m] == [1, 2, 3], g.stdout[-1500:]
+
+
+def test_native_bench_json_line(tmp_path):
+    """bench.py's default (native engine) path prints the driver's JSON record from the native
+    CLI's MFT_BENCH line (a short GPT-2 LoRA run)."""
+    import json
+    r = subprocess.run(["python", os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "3", "--batch", "64"],
+                       capture_output=True, text=True, timeout=300, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["value"] > 0 and "native" in rec["config"]["engine"]
+    assert abs(rec["value"] - 64 * 128 * 3 / (rec["ms_per_step"] * 3 / 1000)) < 0.01 * rec["value"]

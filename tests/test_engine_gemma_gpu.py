@@ -14,6 +14,7 @@ import os
 import subprocess
 
 import pytest
+from native_logs import loss_list
 import torch
 
 pytestmark = pytest.mark.gpu
@@ -138,7 +139,7 @@ def test_native_gemma270m_trains():
                         "--eval_batches", "2"], capture_output=True, text=True, timeout=300)
     print(r.stdout[-3000:], r.stderr[-2000:])
     assert r.returncode == 0
-    losses = [float(line.split("Loss=")[1].split()[0]) for line in r.stdout.splitlines() if "Loss=" in line]
+    losses = loss_list(r.stdout, True)
     assert len(losses) == 6 and all(math.isfinite(x) for x in losses)
     assert abs(losses[0] - math.log(V)) < 1.0, losses
 
@@ -179,7 +180,7 @@ def test_native_gemma_weight_streaming_matches_resident():
     def losses(extra):
         r = subprocess.run([_bin("train_lora_gemma"), *common, *extra], capture_output=True, text=True, timeout=180)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        return [float(line.split("Loss=")[1].split()[0]) for line in r.stdout.splitlines() if "Loss=" in line], r.stdout
+        return loss_list(r.stdout, True), r.stdout
 
     ref, _ = losses([])
     for extra in ([], ["--no_graph"]):

@@ -13,6 +13,7 @@ import subprocess
 
 import pytest
 import torch
+from native_logs import loss_list, native_losses
 
 pytestmark = pytest.mark.gpu
 
@@ -150,7 +151,7 @@ def test_native_eager_and_graph_agree():
     for extra in ([], ["--no_graph"]):
         r = subprocess.run([_bin("gpt2_lora_finetune"), *common, *extra], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        outs.append([ln.split("Loss=")[1].split()[0] for ln in r.stdout.splitlines() if ln.startswith("[Step")])
+        outs.append(loss_list(r.stdout))
     assert outs[0] == outs[1] and len(outs[0]) == 5
 
 
@@ -164,7 +165,7 @@ def test_native_full_finetune_runs(tmp_path):
                             "64", "--lr", "1e-3", "--log_interval", "1", "--output_path", out], capture_output=True,
                            text=True, timeout=120)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        losses = [float(ln.split("Loss=")[1].split()[0]) for ln in r.stdout.splitlines() if ln.startswith("[Step")]
+        losses = loss_list(r.stdout, True)
         assert len(losses) == steps and all(l == l and abs(l) < 20 for l in losses)
         outs[steps] = st.load_file(out)
     sd0, sd6 = outs[0], outs[6]
@@ -191,7 +192,7 @@ def test_native_cli_with_rccl_communicator():
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
         if force == "1":
             assert "data parallel: rank 0 of 1" in r.stdout
-        steps = [ln.split("Loss=")[1].split()[0] for ln in r.stdout.splitlines() if ln.startswith("[Step")]
+        steps = loss_list(r.stdout)
         evals = [ln for ln in r.stdout.splitlines() if ln.startswith("[Eval]")]
         outs.append((steps, evals))
     assert outs[0] == outs[1] and len(outs[0][0]) == 6 and len(outs[0][1]) == 2, outs
@@ -227,7 +228,7 @@ def test_native_weight_streaming_matches_resident():
     def losses(extra):
         r = subprocess.run([_bin("gpt2_lora_finetune"), *common, *extra], capture_output=True, text=True, timeout=180)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        return [float(line.split("Loss=")[1].split()[0]) for line in r.stdout.splitlines() if "Loss=" in line], r.stdout
+        return loss_list(r.stdout, True), r.stdout
 
     ref, _ = losses([])
     for extra in ([], ["--no_graph"]):
@@ -253,8 +254,7 @@ def test_native_full_state_resume(tmp_path, prog, model, steps_flag, extra):
         cmd = common + [steps_flag, str(steps)] + (["--state_dir", state] if state else [])
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        return r.stdout, {int(ln.split("/")[0].split()[1]): ln.split("Loss=")[1].split()[0]
-                          for ln in r.stdout.splitlines() if ln.startswith("[Step")}
+        return r.stdout, native_losses(r.stdout)
 
     _, ref = losses(8)
     state = str(tmp_path / "state")
@@ -282,8 +282,7 @@ def test_native_fault_then_resume(tmp_path):
         return subprocess.run(common + extra, capture_output=True, text=True, timeout=180)
 
     def losses(out):
-        return {int(ln.split("/")[0].split()[1]): ln.split("Loss=")[1].split()[0]
-                for ln in out.splitlines() if ln.startswith("[Step")}
+        return native_losses(out)
 
     r = run([])
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

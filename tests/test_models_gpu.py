@@ -102,22 +102,36 @@ def test_zero3_single_gpu_matches_flat(model_name, copy_path, monkeypatch):
             return gemma3.Gemma3Model(gemma3.Gemma3Config.preset(model_name), device=DEV, seed=3)
         return gpt2.GPT2Model(gpt2.GPT2Config.preset(model_name), device=DEV, seed=3)
 
-    ids = torch.randint(0, 1000, (4, 33), device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
-    b = [(ids[:, :-1].contiguous(), ids[:, 1:].contiguous())]
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    # a DIFFERENT batch every step, and every step's pre-clip gradient norm compared: a gradient
+    # buffer that is not re-zeroed inside a replayed graph keeps adding up across steps, which a
+    # fixed batch (Adam + clipping cancel a scaled gradient) would hide in the losses
+    batches = []
+    for _ in range(6):
+        ids = torch.randint(0, 1000, (4, 33), device=DEV, generator=gen)
+        batches.append([(ids[:, :-1].contiguous(), ids[:, 1:].contiguous())])
     m0 = make()
     m0.set_full_finetune()
     flat = FlatParams(m0.named_parameters(), DEV)
-    st0 = TrainStep(m0, flat, FusedAdamW(flat, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0), use_graph=False)
-    ref_losses = [float(st0(b).item()) for _ in range(5)]
+    opt0 = FusedAdamW(flat, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0)
+    st0 = TrainStep(m0, flat, opt0, use_graph=False)
+    ref_losses, ref_gn = [], []
+    for b in batches:
+        ref_losses.append(float(st0(b).item()))
+        ref_gn.append(float(opt0.grad_norm()))
     for graph in (False, True):
         m1 = make()
         m1.set_full_finetune()
         z3 = attach_zero3(m1, DEV, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0)
         st1 = TrainStep(m1, z3.flat, z3, dp=z3, use_graph=graph)
         assert st1.graph_comm and z3.direct == (not copy_path)
-        losses = [float(st1(b).item()) for _ in range(5)]
+        losses, gns = [], []
+        for b in batches:
+            losses.append(float(st1(b).item()))
+            gns.append(float(z3.grad_norm()))
         assert (st1.graph is not None) == graph
         assert losses == pytest.approx(ref_losses, rel=2e-3, abs=2e-3), (graph, losses, ref_losses)
+        assert gns == pytest.approx(ref_gn, rel=1e-2), (graph, gns, ref_gn)
         full = z3.full_state()
         for n, p in m0.named_parameters():
             assert torch.allclose(full[n], p.detach().float().cpu(), atol=2e-3, rtol=1e-2), (graph, n)
