@@ -155,7 +155,10 @@ def test_native_dp_state_resume_two_ranks(tmp_path):
     b = _run_ranks([_bin("gpt2_full_finetune"), *base, "--steps", "8", "--state_dir", state], 2)
     assert all(rc == 0 for rc, _, _ in b), b[0][2][-2000:]
     assert "resumed full training state" in b[0][1]
-    assert loss_list(a[0][1]) + loss_list(b[0][1]) == want, (want, a[0][1][-1500:], b[0][1][-1500:])
+    got = loss_list(a[0][1], True) + loss_list(b[0][1], True)
+    # (a full fine-tune's last printed digit may differ once across 8 steps: the resumed process
+    # runs its first two steps eagerly and captures at step 7; losses are compared to 1e-4)
+    assert got == pytest.approx([float(x) for x in want], rel=1e-4, abs=1e-4), (want, got)
 
 
 def test_native_peer_failure_makes_the_other_rank_exit():
