@@ -552,7 +552,7 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
 // reduce when the output has few 256x256 tiles.
 std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, c10::optional<Tensor> bias,
                            c10::optional<Tensor> aux, double alpha, c10::optional<Tensor> out,
-                           c10::optional<Tensor> lora_u, c10::optional<Tensor> lora_w) {
+                           c10::optional<Tensor> lora_u, c10::optional<Tensor> lora_w, int64_t impl) {
   CHECK_CUDA(A); CHECK_BF16(A); CHECK_BF16(B);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "gemm_t: row-contiguous 2-D operands");
   const int M = a_t ? A.size(1) : A.size(0), K = a_t ? A.size(0) : A.size(1);
@@ -605,7 +605,12 @@ std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, 
     a.lora_w = bp(*lora_w); a.ld_lw = lora_w->stride(0);
     a.lora_r = lora_u->size(1);
   }
-  mft::gemm8x(a, (int)epi, a_t, b_t, stream());
+  if (impl == 1) {  // gemmw (NT only)
+    TORCH_CHECK(!a_t && !b_t && mft::gemmw_supported(M, N, K), "gemm_t impl 1 (gemmw): NT, K % 32 == 0");
+    mft::gemmw(a, (int)epi, stream());
+  } else {
+    mft::gemm8x(a, (int)epi, a_t, b_t, stream());
+  }
   return {C, X};
 }
 
@@ -671,7 +676,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_dy", &lora_dy);
   m.def("gemm_t", &gemm_t, py::arg("A"), py::arg("B"), py::arg("a_t"), py::arg("b_t"), py::arg("epi"),
         py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("alpha") = 1.0, py::arg("out") = py::none(),
-        py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none());
+        py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none(), py::arg("impl") = 0);
+  m.def("gemm8_set_stream", [](int64_t on) { mft::gemm8_set_stream((int)on); });
   m.def("gemm", &gemm_op, py::arg("A"), py::arg("B"), py::arg("b_nn"), py::arg("epi"), py::arg("bias"), py::arg("aux"),
         py::arg("alpha"), py::arg("cfg"), py::arg("out"), py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none());
   m.def("zero_cols", &zero_cols);

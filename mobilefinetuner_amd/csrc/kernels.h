@@ -113,6 +113,13 @@ void gemm8(const GemmArgs& g, int epi, hipStream_t st);  // NT
 void gemm8x(const GemmArgs& g, int epi, bool a_t, bool b_t, hipStream_t st);
 bool gemm8_supported(int M, int N, int K, bool a_t, bool b_t);
 int gemm8_pick_ksplit(int M, int N, int K);
+// NT NONE / BIAS / BIAS_GELU_D: the persistent streaming form with the deferred epilogue (opt-in,
+// MFT_GEMM8_STREAM=1); A/B switch for benchmarks
+void gemm8_set_stream(int on);
+// 256x128x32 NT GEMM with 4-wave workgroups, two per CU (gemmw.hip): the short-K training shapes
+// (epilogues as gemm8's, minus the CE / split-K ones)
+void gemmw(const GemmArgs& g, int epi, hipStream_t st);
+bool gemmw_supported(int M, int N, int K);
 void gemm_splitk_reduce(const float* ws, int ksplit, int M, int N, float* C, long ldc, float alpha, int accumulate,
                         hipStream_t st);
 

@@ -85,6 +85,30 @@ __device__ __forceinline__ void stage_half(bf16_t* lds, const bf16_t* src, long 
   }
 }
 
+// per-lane byte offsets of stage_half's two loads for an interior half-tile (no row clamping): they
+// depend only on the lane and the row stride, so a kernel that moves between tiles computes them
+// once and each staging is one scalar base + these offsets
+__device__ __forceinline__ void stage_offsets(long ld, uint32_t (&off)[2]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int c = t * 512 + tid;
+    const int r = c >> 3, s = c & 7;
+    off[t] = (uint32_t)((r * (int)ld + ((s ^ (r & 7)) << 3)) * 2);
+  }
+}
+__device__ __forceinline__ void stage_half_fast(bf16_t* lds, const bf16_t* src, long ld, int r0, int rmax, int k0,
+                                                const uint32_t (&off)[2]) {
+  if (r0 + 128 <= rmax) {
+    const int w = threadIdx.x >> 6;
+    const bf16_t* base = src + (long)r0 * ld + k0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) glds16_off(base, off[t], lds + (t * 512 + w * 64) * 8);
+  } else {
+    stage_half(lds, src, ld, r0, rmax, k0);
+  }
+}
+
 // stage one [64 k][128 cols] half-tile of a k-major operand: rows k0..k0+63 of src, columns
 // c0..c0+127 (clamped to cmax-8; cmax % 8 == 0).  256-B rows; the 16-B chunk index is XOR-swizzled
 // with tsw(k) (even, so 32-B pairs stay together) on the SOURCE address: the 8 rows one 32-lane half
@@ -718,15 +742,64 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   G8_STAMP(3);
 }
 
-// Persistent form (ksplit == 1): one workgroup per CU walks its tiles (logical ids b, b + grid, ...,
-// XCD-remapped) as ONE continuous stream of K-tiles.  The 8-phase pipeline never restarts: the
-// prefetches issued near the end of a tile already fetch the next tile's first K-tiles, and the
-// finished tile's epilogue (registers only) runs between two phases while those loads are in
-// flight.  Removes the per-tile prologue fill + workgroup relaunch that cost ~9 us per 256 x 256
-// tile at K = 768 (measured: 28.4 us per tile vs 10.3 us of MFMA work at peak).
+// ------------------------------------------------------------------ persistent streaming form
+// One quadrant of the deferred epilogue (NONE / BIAS / BIAS_GELU_D): acc[q] of the finished tile
+// (rows m0 + qa*128 + wm*64 + 16 i, columns n0 + qb*128 + wn*32 ..) -> 4 (GELU_D: 8) 16-B stores per
+// lane, then acc[q] = 0 for the next tile.  bias_q: the lane's 8 bias values of that column half,
+// loaded when the tile started (no load -- hence no vmcnt wait -- inside the pipeline).
+template <int EPI>
+__device__ __forceinline__ void epi_quad8(const GemmArgs& g, f32x4_t (&aq)[4][2], int q, int m0, int n0, int wm,
+                                          int wn, int lane, const u16x8_t& bias_q) {
+  const int g4 = lane >> 4;
+  const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
+  const int qa = (q == 2 || q == 3) ? 1 : 0, qb = (q == 1 || q == 2) ? 1 : 0;
+  const int col = n0 + qb * 128 + wn * 32 + cofs;
+  const bool col_ok = col < g.N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(aq[i][0][r]), __float_as_uint(aq[i][1][r]),
+                                                       false, false);
+      v[r] = __uint_as_float(sw[0]);
+      v[4 + r] = __uint_as_float(sw[1]);
+    }
+    const int row = m0 + qa * 128 + wm * 64 + i * 16 + (lane & 15);
+    const bool ok = col_ok && row < g.M;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] *= g.alpha;
+      if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU_D) v[e] += bf2f(bias_q[e]);
+    }
+    if constexpr (EPI == GEMM_EPI_BIAS_GELU_D) {
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gelu_tanh_and_grad(v[e], v[e], d[e]);
+      if (ok) store8(g.aux + (long)row * g.ldaux + col, d);
+    }
+    if (ok) store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, v);
+    aq[i][0] = zero4();
+    aq[i][1] = zero4();
+  }
+}
+
+// Persistent streaming form (ksplit == 1; epilogues NONE / BIAS / BIAS_GELU_D): one workgroup per
+// CU walks its tiles (logical ids b, b + grid, ..., XCD-remapped) as ONE continuous stream of
+// K-tiles, so the 8-phase pipeline never restarts -- the prefetches issued near the end of a tile
+// already fetch the next tile's first K-tiles (no prologue fill, no workgroup relaunch).
+// The finished tile's epilogue is DEFERRED by one quadrant-phase each: during the 4 phases after a
+// tile's last K-tile, the phase that is about to accumulate quadrant q of the NEW tile first
+// converts and stores quadrant q of the OLD one (and zeroes it), after that phase's staging loads.
+// So the 128 KB of stores leave in four 32 KB pieces interleaved with MFMA work instead of one
+// issue-bound burst, and -- vmcnt being in order -- the stores are always YOUNGER than the loads
+// the next counted wait needs except for the first quadrant's: that wait allows the 3 later
+// quadrants' stores in flight (vm_wait<4 + 3 S>, S stores per lane per quadrant).
 template <int EPI, bool AT, bool BT>
-__global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs g) {
+__global__ __launch_bounds__(512, 1) void gemm8s_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  constexpr int S = EPI == GEMM_EPI_BIAS_GELU_D ? 8 : 4;  // stores per lane per quadrant
+  constexpr bool kBias = EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU_D;
   const int tiles_n = (g.N + 255) / 256;
   const int ntiles = ((g.M + 255) / 256) * tiles_n;
   const int b = blockIdx.x, grid = gridDim.x;
@@ -735,37 +808,48 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs g) {
   const int NG = n_my * nk;  // K-tiles this workgroup streams
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = w >> 2, wn = w & 3;
+  const int g4 = lane >> 4;
+  const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
 
-  // K-tile Gk of the stream -> (m0, n0, k0); past the end: the last K-tile (uniform re-reads)
-  auto kinfo = [&](int Gk, int& m0, int& n0, int& k0) {
-    const int Gc = min(Gk, NG - 1);
-    const int i = Gc / nk;
-    const int tile = xcd_remap(b + i * grid, ntiles);
-    m0 = (tile / tiles_n) * 256;
-    n0 = (tile % tiles_n) * 256;
-    k0 = (Gc - i * nk) * 64;
+  // position in the stream: K-tile Gk = (tile number i of this workgroup, k-tile kk of it); the
+  // iterator advances with scalar adds, dividing only when it crosses into the next tile; past the
+  // end it stays on the last K-tile (uniform re-reads keep the counted waits exact)
+  struct It {
+    int Gk, i, kk, m0, n0;
   };
-  auto half_ptr = [&](int buf, int h) { return smem + (buf * 4 + h) * kHalf; };
-  auto stage_at = [&](int buf, int h, int m0, int n0, int k0) {
-    if (h < 2) {
-      if constexpr (AT) stage_half_t(half_ptr(buf, h), g.A, g.lda, m0 + h * 128, g.M, k0);
-      else stage_half(half_ptr(buf, h), g.A, g.lda, m0 + h * 128, g.M, k0);
-    } else {
-      if constexpr (BT) stage_half_t(half_ptr(buf, h), g.B, g.ldb, n0 + (h - 2) * 128, g.N, k0);
-      else stage_half(half_ptr(buf, h), g.B, g.ldb, n0 + (h - 2) * 128, g.N, k0);
+  auto tile_origin = [&](It& t) {
+    const int tile = xcd_remap(b + t.i * grid, ntiles);
+    t.m0 = (tile / tiles_n) * 256;
+    t.n0 = (tile % tiles_n) * 256;
+  };
+  auto adv = [&](It t) {
+    if (t.Gk + 1 < NG) {
+      ++t.Gk;
+      if (++t.kk == nk) {
+        t.kk = 0;
+        ++t.i;
+        tile_origin(t);
+      }
     }
+    return t;
+  };
+  uint32_t offA[2], offB[2];
+  stage_offsets(g.lda, offA);
+  stage_offsets(g.ldb, offB);
+  auto half_ptr = [&](int buf, int h) { return smem + (buf * 4 + h) * kHalf; };
+  auto stage_at = [&](int buf, int h, const It& t) {
+    const int k0 = t.kk * 64;
+    if (h < 2) stage_half_fast(half_ptr(buf, h), g.A, g.lda, t.m0 + h * 128, g.M, k0, offA);
+    else stage_half_fast(half_ptr(buf, h), g.B, g.ldb, t.n0 + (h - 2) * 128, g.N, k0, offB);
   };
 
   f32x4_t acc[4][4][2];
-  auto zero_acc = [&]() {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[q][i][j] = zero4();
-  };
-  zero_acc();
+      for (int j = 0; j < 2; ++j) acc[q][i][j] = zero4();
 
   bf16x8_t af[4][2], bfr[2][2];
   auto read_a = [&](int buf, int ah) {
@@ -802,26 +886,41 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs g) {
     lgkm_wait0();
     if constexpr (AT || BT) __builtin_amdgcn_sched_barrier(0);
   };
-  // after the last quadrant of K-tile Gk: if it closes a tile, write that tile and restart acc
-  auto finish = [&](int Gk) {
-    if ((Gk + 1) % nk == 0) {
-      int m0, n0, k0;
-      kinfo(Gk, m0, n0, k0);
-      epilogue8<EPI>(g, acc, m0, n0, wm, wn, lane, 0);
-      zero_acc();
+
+  // the deferred tile: its origin, its bias (the lane's 8 columns of each column half)
+  int pm0 = 0, pn0 = 0;
+  bool pend = false;
+  u16x8_t bias_c[2] = {}, bias_p[2] = {};  // current tile's, pending tile's
+  auto load_bias = [&](int n0) {
+    if constexpr (kBias) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        bias_c[h] = *reinterpret_cast<const u16x8_t*>(g.bias + min(n0 + h * 128 + wn * 32 + cofs, g.N - 8));
     }
   };
+  // after the last quadrant of K-tile t: a finished tile becomes the pending one
+  auto finish = [&](const It& t) {
+    if (t.kk == nk - 1) {
+      pm0 = t.m0, pn0 = t.n0, pend = true;
+      bias_p[0] = bias_c[0], bias_p[1] = bias_c[1];
+      if (t.Gk + 1 < NG) load_bias(adv(t).n0);
+    }
+  };
+  auto epi = [&](int q) {
+    if (pend) epi_quad8<EPI>(g, acc[q], q, pm0, pn0, wm, wn, lane, bias_p[(q == 1 || q == 2) ? 1 : 0]);
+  };
 
+  It t0{0, 0, 0, 0, 0};
+  tile_origin(t0);
+  It t1 = adv(t0);  // stream position of the odd buffer's K-tile
   {  // prologue: E <- K-tile 0 (all halves), O <- K-tile 1 (A0, B1); retire E
-    int m0, n0, k0;
-    kinfo(0, m0, n0, k0);
-    stage_at(0, 0, m0, n0, k0);
-    stage_at(0, 3, m0, n0, k0);
-    stage_at(0, 1, m0, n0, k0);
-    stage_at(0, 2, m0, n0, k0);
-    kinfo(1, m0, n0, k0);
-    stage_at(1, 0, m0, n0, k0);
-    stage_at(1, 3, m0, n0, k0);
+    load_bias(t0.n0);
+    stage_at(0, 0, t0);
+    stage_at(0, 3, t0);
+    stage_at(0, 1, t0);
+    stage_at(0, 2, t0);
+    stage_at(1, 0, t1);
+    stage_at(1, 3, t1);
   }
   vm_wait<4>();
   raw_barrier();
@@ -829,71 +928,89 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs g) {
 
   for (int G = 0; G < NG; G += 2) {
     const bool odd_ok = G + 1 < NG;
-    int m1, n1, k1, m2, n2, k2, m3, n3, k3;  // staging targets: K-tiles G+1, G+2, G+3
-    kinfo(G + 1, m1, n1, k1);
-    kinfo(G + 2, m2, n2, k2);
-    kinfo(G + 3, m3, n3, k3);
-    // ---- phases 1-4: even buffer, K-tile G
+    // staging targets: K-tiles G+1 (= t1), G+2, G+3; t0 = K-tile G
+    const It t2 = adv(t1), t3 = adv(t2);
+    // ---- phases 1-4: even buffer, K-tile G (the pending tile's quadrants leave in order)
+    const bool ep0 = pend;
     read_a(0, 0);
     read_b(0, 0);
-    stage_at(1, 1, m1, n1, k1);
+    stage_at(1, 1, t1);
+    epi(0);
     lds_sync();
     raw_barrier();
     mma(0);
     raw_barrier();
     read_b(0, 1);
-    stage_at(1, 2, m1, n1, k1);
+    stage_at(1, 2, t1);
+    epi(1);
     lds_sync();
     raw_barrier();
     mma(1);
     raw_barrier();
     read_a(0, 1);
-    stage_at(0, 0, m2, n2, k2);
+    stage_at(0, 0, t2);
+    epi(2);
     lds_sync();
     raw_barrier();
     mma(2);
     raw_barrier();
     read_b(0, 0);
-    stage_at(0, 3, m2, n2, k2);
+    stage_at(0, 3, t2);
+    epi(3);
+    pend = false;
     lds_sync();
-    vm_wait<4>();
+    if (ep0) vm_wait<4 + 3 * S>();  // the 3 later quadrants' stores may stay in flight
+    else vm_wait<4>();
     raw_barrier();
     mma(3);
-    finish(G);
+    finish(t0);
     raw_barrier();
     // ---- phases 5-8: odd buffer, K-tile G+1
+    const bool ep1 = pend;
     read_a(1, 0);
     read_b(1, 0);
-    stage_at(0, 1, m2, n2, k2);
+    stage_at(0, 1, t2);
+    epi(0);
     lds_sync();
     raw_barrier();
     if (odd_ok) mma(0);
     raw_barrier();
     read_b(1, 1);
-    stage_at(0, 2, m2, n2, k2);
+    stage_at(0, 2, t2);
+    epi(1);
     lds_sync();
     raw_barrier();
     if (odd_ok) mma(1);
     raw_barrier();
     read_a(1, 1);
-    stage_at(1, 0, m3, n3, k3);
+    stage_at(1, 0, t3);
+    epi(2);
     lds_sync();
     raw_barrier();
     if (odd_ok) mma(2);
     raw_barrier();
     read_b(1, 0);
-    stage_at(1, 3, m3, n3, k3);
+    stage_at(1, 3, t3);
+    epi(3);
+    pend = false;
     lds_sync();
-    vm_wait<4>();
+    if (ep1) vm_wait<4 + 3 * S>();
+    else vm_wait<4>();
     raw_barrier();
     if (odd_ok) {
       mma(3);
-      finish(G + 1);
+      finish(t1);
     }
     raw_barrier();
+    t0 = t2;
+    t1 = t3;
   }
   if (wm == 0) raw_barrier();
   vm_wait<0>();
+  if (pend) {  // the last tile
+#pragma unroll
+    for (int q = 0; q < 4; ++q) epi_quad8<EPI>(g, acc[q], q, pm0, pn0, wm, wn, lane, bias_p[(q == 1 || q == 2) ? 1 : 0]);
+  }
 }
 
 static int num_cus() {
@@ -907,18 +1024,20 @@ static int num_cus() {
   return n;
 }
 
-// MFT_GEMM8_PERSISTENT=1 selects the persistent streaming kernel.  Off by default: measured slower
-// than one tile per workgroup on every training shape (A/B in one call, scripts/bench_gemm_t.py:
-// qkv fwd 327 vs 297 us, LM-head fwd 5.69 vs 5.27 ms, fc dx 325 vs 276 us) -- the inline epilogue
-// stalls both wave groups between barriers and costs more than the prologue fill it hides.
-static bool gemm8_persistent() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("MFT_GEMM8_PERSISTENT");
-    v = (e && e[0] == '1') ? 1 : 0;
+// MFT_GEMM8_STREAM=1: the persistent streaming kernel with the deferred epilogue for NT NONE / BIAS /
+// BIAS_GELU_D whenever every CU gets >= 2 tiles.  Off by default: measured within +-5 % of one tile
+// per workgroup at K = 704-832 and 9-18 % slower at K = 2112-3072 and with the GELU epilogue
+// (profiles/r3_gemm_stream_ab.txt) -- the per-tile cost at short K is not the prologue fill, the
+// relaunch or the store burst, which this form removes.
+static int g_stream = -1;
+static bool gemm8_stream() {
+  if (g_stream < 0) {
+    const char* e = getenv("MFT_GEMM8_STREAM");
+    g_stream = (e && e[0] == '1') ? 1 : 0;
   }
-  return v == 1;
+  return g_stream == 1;
 }
+void gemm8_set_stream(int on) { g_stream = on ? 1 : 0; }
 
 template <int EPI, bool AT, bool BT>
 static void launch8(const GemmArgs& g, hipStream_t st) {
@@ -932,18 +1051,16 @@ static void launch8(const GemmArgs& g, hipStream_t st) {
   }
   const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
   const int ks = g.ksplit > 1 ? g.ksplit : 1;
-  // (the LoRA epilogue's extra operand loads spill in the persistent form: one tile per workgroup)
-  if constexpr (EPI != GEMM_EPI_F32PART && EPI != GEMM_EPI_LORA && EPI != GEMM_EPI_CE_FWD &&
-                EPI != GEMM_EPI_CE_DGRAD) {
-    if (ks == 1 && gemm8_persistent()) {
-      static bool attr_p = false;
-      if (!attr_p) {
-        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, AT, BT>,
+  // streaming form: epilogues without per-element operand loads (NONE / BIAS / BIAS_GELU_D)
+  if constexpr (!AT && !BT && (EPI == GEMM_EPI_NONE || EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU_D)) {
+    if (ks == 1 && gemm8_stream() && tiles >= 2 * num_cus()) {
+      static bool attr_s = false;
+      if (!attr_s) {
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8s_kernel<EPI, AT, BT>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-        attr_p = true;
+        attr_s = true;
       }
-      const int grid = tiles < num_cus() ? tiles : num_cus();
-      gemm8p_kernel<EPI, AT, BT><<<grid, 512, shm, st>>>(g);
+      gemm8s_kernel<EPI, AT, BT><<<num_cus(), 512, shm, st>>>(g);
       return;
     }
   }
