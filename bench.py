@@ -58,15 +58,15 @@ CONFIGS = {
     "gpt2-full": dict(model="gpt2", mode="full", batch=512, seq=128, zero=0, engine="native",
                       metric="tokens/sec GPT-2-124M full fine-tune seq128 (training, whole job)"),
     # GPT-2 XL (1.5B) full fine-tuning with ZeRO-2 partitioned optimizer / reduce-scattered grads
-    "gpt2-xl-zero": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=2,
+    "gpt2-xl-zero": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=2, engine="native",
                          metric="tokens/sec GPT-2-XL full fine-tune ZeRO-2 seq128 (training, whole job)"),
     # same with ZeRO-3: parameters partitioned too, all-gathered per block (prefetched one block
     # ahead on a communication stream), gradients reduce-scattered per block during backward
-    "gpt2-xl-zero3": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=3,
+    "gpt2-xl-zero3": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=3, engine="native",
                           metric="tokens/sec GPT-2-XL full fine-tune ZeRO-3 seq128 (training, whole job)"),
     # BASELINE config 5: ZeRO partition + host-DRAM tier (AdamW moments in pinned host memory,
     # streamed through the GPU per chunk on the native HostTier's copy stream)
-    "gpt2-xl-zero3-offload": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=3, offload=True,
+    "gpt2-xl-zero3-offload": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=3, offload=True, engine="native",
                                   metric="tokens/sec GPT-2-XL full fine-tune ZeRO-3 + host-offloaded AdamW "
                                          "seq128 (training, whole job)"),
 }
@@ -104,6 +104,13 @@ def _native_cmd(a, cfgd):
            "--grad_accum_steps", str(a.grad_accum), "--steps", str(total), "--log_interval", "0"]
     if cfgd["mode"] == "full":
         cmd += ["--lr", "1e-5", "--weight_decay", "0.01"]
+        zero = cfgd.get("zero", 0) if a.zero < 0 else a.zero
+        if zero:  # on one GPU too: the partitioned path (1-rank communicator) is what runs
+            cmd += ["--zero_stage", str(zero)]
+        if cfgd.get("offload", False) or a.offload_optimizer:
+            cmd += ["--offload", "host"]
+        if a.bf16_grads:
+            cmd += ["--bf16_grads"]
     else:
         cmd += ["--rank", str(a.rank), "--alpha", str(a.alpha), "--lr", "2e-4",
                 "--lora_targets", a.targets or cfgd["targets"]]
@@ -144,8 +151,10 @@ def run_native(a, cfgd) -> int:
     value = tokens / dt
     fpt = _flops_per_token(cfgd["model"], rec["seq"], rec["n_params"], rec["n_trainable"])
     tflops = value / rec["world"] * fpt / 1e12
+    zero = (cfgd.get("zero", 0) if a.zero < 0 else a.zero) if cfgd["mode"] == "full" else 0
     mode = "LoRA r=%d alpha=%g targets=%s" % (a.rank, a.alpha, a.targets or cfgd["targets"]) \
-        if cfgd["mode"] == "lora" else "full fine-tune"
+        if cfgd["mode"] == "lora" else "full fine-tune" + (f" ZeRO-{zero}" if zero else "") + \
+        (" + host-offloaded AdamW (bf16 moments)" if (cfgd.get("offload", False) or a.offload_optimizer) else "")
     out_rec = {
         "metric": cfgd["metric"],
         "value": round(value, 1),
@@ -166,7 +175,7 @@ def run_native(a, cfgd) -> int:
             "seq_len": rec["seq"],
             "parallelism": f"dp{rec['world']}",
             "engine": "native libmft (C++ autograd tape, hipGraph-captured step)",
-            "backend": "rccl" if rec["world"] > 1 else "none",
+            "backend": "rccl" if (rec["world"] > 1 or zero) else "none",
             "hipgraph": not a.no_graph,
             "final_loss": round(rec["final_loss"], 4),
             "model_tflops_per_gpu": round(tflops, 1),

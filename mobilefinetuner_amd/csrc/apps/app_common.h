@@ -21,6 +21,7 @@
 #include "engine/comm.h"
 #include "engine/dist.h"
 #include "engine/optim.h"
+#include "engine/zero3.h"
 #include "runtime/dataset.h"
 #include "runtime/power_monitor.h"
 
@@ -146,8 +147,9 @@ inline bool load_token_splits(const Args& a, DataConfig& dc, int vocab, TokenDat
 }
 
 // Data-parallel / ZeRO flags shared by the training CLIs:
-//   --zero_stage 0|1|2   optimizer partition (1) + reduce-scattered gradients (2); > 0 also on one
-//                        process (a 1-rank communicator: the partitioned code path runs)
+//   --zero_stage 0|1|2|3 optimizer partition (1) + reduce-scattered gradients (2) + partitioned
+//                        parameters (3, full fine-tuning: engine/zero3.h); > 0 also on one process
+//                        (a 1-rank communicator: the partitioned code path runs)
 //   --offload host|none  AdamW moments (bf16, stochastically rounded) in pinned host DRAM
 //   --bucket_mb N        fp32 gradient bytes per reduction bucket (default 25)
 //   --bf16_grads         reduce gradients in bf16      --no_overlap   reduce after the backward
@@ -161,7 +163,7 @@ inline DistConfig dist_config_from(const Args& a) {
   const std::string off = a.get("offload", "none");
   if (off != "none" && off != "host") throw std::runtime_error("--offload host|none (got '" + off + "')");
   d.host_moments = off == "host";
-  if (d.zero_stage < 0 || d.zero_stage > 2) throw std::runtime_error("--zero_stage 0|1|2 in the native engine");
+  if (d.zero_stage < 0 || d.zero_stage > 3) throw std::runtime_error("--zero_stage 0|1|2|3 in the native engine");
   return d;
 }
 
@@ -170,22 +172,33 @@ inline std::unique_ptr<eng::Communicator> comm_from(const DistConfig& d) {
   return eng::Communicator::from_env((fc && fc[0] == '1') || d.zero_stage > 0);
 }
 
-// the flat trainable buffers, bucket-planned when a communicator exists, plus its reducer
+// the flat trainable buffers, bucket-planned when a communicator exists, plus its reducer; or,
+// with --zero_stage 3, the parameter partitioner whose flat holds only this rank's partitions
 struct DistSetup {
-  std::unique_ptr<eng::FlatParams> flat;
+  std::unique_ptr<eng::FlatParams> own;
+  eng::FlatParams* flat = nullptr;
   eng::FlatPlan plan;
   std::unique_ptr<eng::DataParallel> dp;
+  std::unique_ptr<eng::Zero3> z3;
   void make_flat(std::vector<std::pair<std::string, eng::Param*>> params, eng::Communicator* comm, const DistConfig& d) {
     if (comm) {
       plan = eng::plan_flat(params, comm->world(), d.bucket_bytes);
-      flat = std::make_unique<eng::FlatParams>(std::move(params), plan.offsets, plan.numel);
+      own = std::make_unique<eng::FlatParams>(std::move(params), plan.offsets, plan.numel);
     } else {
-      flat = std::make_unique<eng::FlatParams>(std::move(params));
+      own = std::make_unique<eng::FlatParams>(std::move(params));
     }
+    flat = own.get();
+  }
+  void make_zero3(const std::vector<eng::NamedParams>& units, const eng::NamedParams& rep, eng::Communicator& comm) {
+    z3 = std::make_unique<eng::Zero3>(units, rep, comm);
+    flat = &z3->flat();
   }
   // after the optimizer exists (the reducer shards it)
   void make_dp(eng::Communicator* comm, eng::AdamW& opt, const DistConfig& d) {
-    if (comm) {
+    if (z3) {
+      z3->shard_optimizer(opt, d.host_moments);
+      std::printf("  %s%s\n", z3->describe().c_str(), d.host_moments ? "; AdamW moments in pinned host DRAM (bf16)" : "");
+    } else if (comm) {
       dp = std::make_unique<eng::DataParallel>(*flat, plan, *comm, opt, d);
       std::printf("  data parallel: %s\n", dp->describe().c_str());
     } else if (d.host_moments) {
@@ -193,6 +206,7 @@ struct DistSetup {
       std::printf("  AdamW moments in pinned host DRAM (bf16)\n");
     }
   }
+  eng::GradReducer* reducer() { return z3 ? static_cast<eng::GradReducer*>(z3.get()) : dp.get(); }
 };
 
 // bench.py's native engine (--bench_steps K [--bench_warmup W]): time K full training steps after W
@@ -205,8 +219,9 @@ inline void bench_report(TrainerT& trainer, const FlatT& flat, const Args& a, in
   const int steps = a.i("bench_steps", 0), warmup = a.i("bench_warmup", 3);
   float loss = 0.f;
   const double secs = trainer.bench(warmup, steps, &loss);
-  long long n_train = 0;
+  long long n_train = 0;  // (ZeRO-3: this rank's partitions)
   for (auto& kv : flat.params) n_train += (long long)kv.second->leaf.numel();
+  if (flat.params.empty()) n_train = (long long)flat.numel;
   if (!lead) return;
   std::printf("MFT_BENCH {\"seconds\": %.9f, \"steps\": %d, \"warmup\": %d, \"world\": %d, \"batch\": %d, "
               "\"seq\": %d, \"accum\": %d, \"final_loss\": %.6f, \"model\": \"%s\", \"n_params\": %zu, "

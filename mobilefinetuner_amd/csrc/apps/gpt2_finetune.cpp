@@ -125,7 +125,7 @@ int run(int argc, char** argv) {
 #endif
   if (a.b("shard_enable") && full)
     throw std::runtime_error("--shard_enable streams FROZEN weights; in full fine-tuning every weight trains "
-                             "(use the Python CLI's ZeRO-3 / host-offloaded optimizer for that)");
+                             "(use --zero_stage 3 [--offload host]: weights partitioned over the ranks, moments in host DRAM)");
   if (a.b("deterministic")) set_deterministic(true);
   // data parallelism: one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK, e.g. under
   // `python -m mobilefinetuner_amd.launch --nproc N`), native RCCL communicator; the communicator
@@ -198,7 +198,16 @@ int run(int argc, char** argv) {
       std::printf("  (--shard_dir / --shard_fp16_disk: no disk tier in the native engine, host DRAM holds the weights)\n");
   }
   mft::apps::DistSetup ds;
-  ds.make_flat(model->trainable(), comm.get(), dcfg);
+  if (dcfg.zero_stage == 3) {  // parameters partitioned over the ranks, gathered per block
+    if (!full) throw std::runtime_error("--zero_stage 3 partitions full fine-tuning weights (gpt2_full_finetune)");
+    std::vector<eng::NamedParams> units;
+    eng::NamedParams rep;
+    model->zero3_layout(units, rep);
+    ds.make_zero3(units, rep, *comm);
+    model->set_block_provider(ds.z3.get());
+  } else {
+    ds.make_flat(model->trainable(), comm.get(), dcfg);
+  }
   FlatParams& flat = *ds.flat;
   std::printf("  trainable params: %lld (padded)  |  total: %zu\n", (long long)flat.numel, model->num_parameters());
 
@@ -255,7 +264,7 @@ int run(int argc, char** argv) {
     tc.fault_rank = c == std::string::npos ? 0 : std::stoi(f.substr(c + 1));
   }
   std::unique_ptr<PowerMonitor> pm = mft::apps::power_monitor_from(a);
-  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get(), ds.dp.get());
+  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get(), ds.reducer());
   if (!tc.state_dir.empty() && trainer.load_state(tc.state_dir))
     std::printf("  resumed full training state from %s at step %lld / %lld\n", tc.state_dir.c_str(),
                 (long long)trainer.global_step, (long long)trainer.total_steps());
@@ -288,6 +297,7 @@ int run(int argc, char** argv) {
     model->save_lora(lora_out);
     std::printf("  LoRA saved to: %s\n", lora_out.c_str());
   }
+  if (full && !out_path.empty() && ds.z3) ds.z3->materialize();  // collective: whole tensors again
   if (full && !out_path.empty() && lead) {
     model->save_hf(out_path);
     std::printf("  model saved to: %s\n", out_path.c_str());

@@ -96,6 +96,8 @@ int run(int argc, char** argv) {
     throw std::runtime_error("--loss_reduction sum: the native engine trains on the mean token loss");
   if (a.b("deterministic")) set_deterministic(true);
   const DistConfig dcfg = mft::apps::dist_config_from(a);
+  if (dcfg.zero_stage == 3)  // the adapters are the only trainable tensors: nothing for ZeRO-3 to partition
+    throw std::runtime_error("--zero_stage 3 partitions full fine-tuning weights; LoRA uses stages 0-2");
   std::unique_ptr<Communicator> comm = mft::apps::comm_from(dcfg);
   if (!comm) HIP_OK(hipSetDevice(0));
   if (comm && comm->rank() != 0) std::setvbuf(stdout, nullptr, _IOFBF, 1 << 16);
@@ -213,7 +215,7 @@ int run(int argc, char** argv) {
   if (sched == "constant") tc.lr_fn = [base](int64_t, int64_t) { return base; };
   else tc.lr_fn = [base, ratio, sched](int64_t it, int64_t total) { return gemma_lr(it + 1, base, ratio, total, sched == "cosine"); };
   std::unique_ptr<PowerMonitor> pm = mft::apps::power_monitor_from(a);
-  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get(), ds.dp.get());
+  Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get(), ds.reducer());
   if (!tc.state_dir.empty() && trainer.load_state(tc.state_dir))
     std::printf("  resumed full training state from %s at step %lld / %lld\n", tc.state_dir.c_str(),
                 (long long)trainer.global_step, (long long)trainer.total_steps());

@@ -35,6 +35,24 @@
 namespace mft {
 namespace eng {
 
+// What the Trainer drives around each step: the data-parallel reducer (DataParallel, ZeRO-0/1/2)
+// or the ZeRO-3 partitioner (engine/zero3.h).
+class GradReducer {
+ public:
+  virtual ~GradReducer() = default;
+  // host bookkeeping of a step (also inside a graph capture): micro-batch i of n starts
+  virtual void begin_micro(int i, int n) = 0;
+  // after the last backward: the reductions no hook launched, comm stream joined back
+  virtual void finish() = 0;
+  // after the optimizer step (ZeRO-1/2: all-gather the updated bf16 shadows)
+  virtual void after_optimizer() {}
+  // full fp32 masters on every rank before a checkpoint (ZeRO-1/2)
+  virtual void gather_master() {}
+  // ZeRO-3: each rank's flat holds only its partitions (no initial broadcast, per-rank masters)
+  virtual bool params_sharded() const { return false; }
+  virtual std::string describe() const = 0;
+};
+
 struct DistConfig {
   int zero_stage = 0;                // 0 DDP, 1 partitioned optimizer, 2 + reduce-scattered grads
   int64_t bucket_bytes = 25 << 20;   // fp32 gradient bytes per bucket (MFT_BUCKET_MB)
@@ -53,24 +71,23 @@ struct FlatPlan {
 // Bucketed, padded flat layout for `world` ranks (world 1: still bucketed, chunking trivial).
 FlatPlan plan_flat(const std::vector<std::pair<std::string, Param*>>& params, int world, int64_t bucket_bytes);
 
-class DataParallel {
+class DataParallel : public GradReducer {
  public:
   DataParallel(FlatParams& flat, const FlatPlan& plan, Communicator& comm, AdamW& opt, const DistConfig& cfg);
   ~DataParallel();
   DataParallel(const DataParallel&) = delete;
   DataParallel& operator=(const DataParallel&) = delete;
 
-  // host bookkeeping of a step (also inside a graph capture): micro-batch i of n starts
-  void begin_micro(int i, int n);
+  void begin_micro(int i, int n) override;
   // after the last backward: launch the buckets no hook completed, join the comm stream
-  void finish();
+  void finish() override;
   // stage >= 1 after the optimizer step: all-gather the updated bf16 shadow chunks
-  void after_optimizer();
+  void after_optimizer() override;
   // stage >= 1: the full fp32 master on every rank (checkpoints / exports), then every shadow
-  void gather_master();
+  void gather_master() override;
   int stage() const { return cfg_.zero_stage; }
   const FlatPlan& plan() const { return plan_; }
-  std::string describe() const;
+  std::string describe() const override;
   int64_t launched = 0;  // bucket collectives issued (host count; graph replays repeat theirs)
 
  private:

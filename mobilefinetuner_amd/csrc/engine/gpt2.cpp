@@ -226,6 +226,23 @@ void GPT2::set_full_finetune() {
   for (auto& kv : all_params()) make_trainable(*kv.second);
 }
 
+void GPT2::zero3_layout(std::vector<std::vector<std::pair<std::string, Param*>>>& units,
+                        std::vector<std::pair<std::string, Param*>>& rep) {
+  MFT_CHECK(full_, "zero3_layout: ZeRO-3 partitions full fine-tuning weights");
+  units.assign(1 + cfg_.n_layer, {});
+  rep.clear();
+  for (auto& kv : all_params()) {
+    const std::string& k = kv.first;
+    if (kv.second->c.dtype() == DType::F32) {
+      rep.push_back(kv);
+      continue;
+    }
+    int u = 0;
+    if (k.compare(0, 2, "h.") == 0) u = 1 + std::stoi(k.substr(2, k.find('.', 2) - 2));
+    units[u].push_back(kv);
+  }
+}
+
 std::vector<std::pair<std::string, Param*>> GPT2::trainable() {
   std::vector<std::pair<std::string, Param*>> v;
   if (full_) {
@@ -441,14 +458,17 @@ Tensor GPT2::hidden(const Tensor& ids) {
   const float scale = spec_.scale();
   // streamed weights: no resident augmented-K copy [W | s B^T], the adapters run beside the GEMM
   const bool st = streamer_ != nullptr;
+  // block weights that are not resident: the host-streaming tier or the ZeRO-3 partitioner
+  BlockProvider* bp = st ? streamer_.get() : provider_;
   auto aug = [&](std::vector<LoraAdapter>& ads) { return (ads.empty() || st) ? 0 : lora_aug_cols(C, ads); };
+  if (bp) bp->begin_forward();
   Tensor x = embed(ids, wte_, &wpe_, 1.f);
   auto n0 = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, aug(active(blocks_[0].lqkv)));
   Tensor h = n0.second;
   for (int i = 0; i < cfg_.n_layer; ++i) {
     auto& b = blocks_[i];
     // attention
-    if (st) streamer_->ensure(i, i + 1);
+    if (bp) bp->ensure(i, i + 1);
     Tensor qkv = active(b.lqkv).empty() ? linear_p(h, b.attn_w, &b.attn_b)
                  : st ? lora_linear(h, b.attn_w, &b.attn_b, active(b.lqkv), scale, training, dropout_ctr)
                       : lora_linear_aug(h, C, b.attn_w, &b.attn_b, active(b.lqkv), scale, b.waug_qkv, training, dropout_ctr);
@@ -476,7 +496,7 @@ Tensor GPT2::hidden(const Tensor& ids) {
     auto r1 = add_norm(x, f, *nw, nb, cfg_.eps, false, 0.f, oc);
     x = r1.first;
     h = r1.second;
-    if (st) std::tie(x, h) = streamer_->gate(x, h, i);
+    if (bp) std::tie(x, h) = bp->gate(x, h, i);
   }
   return h;
 }

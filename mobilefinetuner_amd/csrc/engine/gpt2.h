@@ -76,6 +76,12 @@ class GPT2 : public LanguageModel {
   // within budget_bytes (weight_stream.h); LoRA projections then take the plain (non-augmented) path
   void enable_weight_streaming(size_t budget_bytes);
   const WeightStreamer* streamer() const { return streamer_.get(); }
+  // ZeRO-3 (engine/zero3.h): units[0] = {wte, wpe}, units[1 + i] = block i's bf16-compute
+  // weights and biases; rep = the fp32-compute LayerNorm parameters (replicated)
+  void zero3_layout(std::vector<std::vector<std::pair<std::string, Param*>>>& units,
+                    std::vector<std::pair<std::string, Param*>>& rep);
+  // the partitioner that gathers each block's weights before hidden() uses them (not owned)
+  void set_block_provider(BlockProvider* p) { provider_ = p; }
 
  private:
   void alloc();
@@ -85,6 +91,7 @@ class GPT2 : public LanguageModel {
   Param wte_, wpe_, lnf_w_, lnf_b_;
   std::vector<GPT2Block> blocks_;
   std::unique_ptr<WeightStreamer> streamer_;
+  BlockProvider* provider_ = nullptr;
   void make_trainable(Param& p);
 };
 

@@ -53,6 +53,15 @@ FlatParams::FlatParams(std::vector<std::pair<std::string, Param*>> ps, std::vect
   refresh_shadow();
 }
 
+FlatParams FlatParams::buffers(int64_t n) {
+  FlatParams f({});
+  f.numel = round_up(std::max<int64_t>(n, kAlign), kAlign);
+  f.master = zeros({f.numel}, DType::F32);
+  f.grad = zeros({f.numel}, DType::F32);
+  f.shadow = zeros({f.numel}, DType::BF16);
+  return f;
+}
+
 void FlatParams::zero_grad() { grad.zero_(); }
 
 void FlatParams::refresh_shadow() { ::mft::cast_f32_bf16(master.data<float>(), (::mft::bf16_t*)shadow.data_ptr(), numel, current_stream()); }
@@ -103,9 +112,13 @@ void AdamW::step() {
     int64_t mx = 0;
     for (auto& sg : segs_) mx = std::max<int64_t>(mx, ::mft::sumsq_blocks(sg.len));
     if (!part_.defined() || part_.numel() < mx) part_ = empty({std::max<int64_t>(mx, 1)}, DType::F32);
-    for (size_t i = 0; i < segs_.size(); ++i)
-      ::mft::sumsq(g0 + segs_[i].off, segs_[i].len, part_.data<float>(), sumsq_dev.data<float>(), i > 0, s);
+    int n = 0;  // partitioned segments: summed over the ranks; replicated ones: added once, after
+    for (const auto& sg : segs_)
+      if (!sg.replicated) ::mft::sumsq(g0 + sg.off, sg.len, part_.data<float>(), sumsq_dev.data<float>(), n++ > 0, s);
+    if (n == 0) sumsq_dev.zero_();
     if (comm_) comm_->all_reduce(sumsq_dev.data_ptr(), 1, CommType::F32, CommOp::Sum, s);  // global norm^2
+    for (const auto& sg : segs_)
+      if (sg.replicated) ::mft::sumsq(g0 + sg.off, sg.len, part_.data<float>(), sumsq_dev.data<float>(), 1, s);
   }
   if (cfg_.skip_nonfinite) {
     nonfinite_dev.zero_();

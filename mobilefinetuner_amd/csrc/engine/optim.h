@@ -26,6 +26,8 @@ class FlatParams {
   // default: params packed in order, each 64-element aligned.
   explicit FlatParams(std::vector<std::pair<std::string, Param*>> params, std::vector<int64_t> offsets = {},
                       int64_t numel = 0);
+  // bare buffers of `numel` elements that their owner lays out itself (ZeRO-3 partitions)
+  static FlatParams buffers(int64_t numel);
   Tensor master, grad, shadow;
   int64_t numel = 0;
   std::vector<std::pair<std::string, Param*>> params;
@@ -37,6 +39,7 @@ class FlatParams {
 // one contiguous range of the flat buffers this rank updates; its moments live at state_off
 struct OptSegment {
   int64_t off = 0, len = 0, state_off = 0;
+  bool replicated = false;  // identical on every rank: its norm^2 counts once, outside the all-reduce
 };
 
 struct AdamWConfig {

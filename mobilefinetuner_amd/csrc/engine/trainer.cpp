@@ -23,13 +23,13 @@ namespace mft {
 namespace eng {
 
 Trainer::Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid,
-                 const TrainConfig& cfg, PowerMonitor* pm, Communicator* comm, DataParallel* dp)
+                 const TrainConfig& cfg, PowerMonitor* pm, Communicator* comm, GradReducer* dp)
     : model_(model), flat_(flat), opt_(opt), train_(train), valid_(valid), cfg_(cfg), pm_(pm), comm_(comm), dp_(dp) {
   stream_ = current_stream();
   MFT_CHECK(!comm_ || dp_, "Trainer: a communicator needs its DataParallel reducer");
   const char* gc = std::getenv("MFT_GRAPH_COMM");
   graph_comm_ = !(gc && gc[0] == '0');
-  if (comm_) {  // every rank starts from rank 0's trainable weights
+  if (comm_ && !(dp_ && dp_->params_sharded())) {  // every rank starts from rank 0's trainable weights
     comm_->broadcast(flat_.master.data_ptr(), (size_t)flat_.numel * sizeof(float), 0, stream_);
     flat_.refresh_shadow();
   }
@@ -351,11 +351,13 @@ void Trainer::save_state(const std::string& dir) {
     fs::create_directories(tmp);
   }
   if (comm_) comm_->barrier(stream_);
-  if (r == 0) {
+  const bool per_rank = dp_ && dp_->params_sharded();  // ZeRO-3: every rank's own partitions
+  if (r == 0 || per_rank) {
     const Tensor mh = flat_.master.to(Device::cpu());
     const size_t nb = (size_t)flat_.numel * sizeof(float);
-    safetensors_save(tmp + "/trainable.safetensors", {{"master", "F32", {flat_.numel}, mh.data_ptr(), nb}},
-                     {{"format", "mft-flat"}}, false, true);
+    safetensors_save(tmp + (per_rank ? "/trainable.rank" + std::to_string(r) + ".safetensors" : "/trainable.safetensors"),
+                     {{"master", "F32", {flat_.numel}, mh.data_ptr(), nb}},
+                     {{"format", per_rank ? "mft-zero3-partition" : "mft-flat"}}, false, true);
   }
   // AdamW moments: the whole flat (replicated, rank 0 writes it) or each rank's ZeRO partition
   if (r == 0 || opt_.sharded()) {
@@ -399,7 +401,8 @@ bool Trainer::load_state(const std::string& dir0) {
   const json::Value st = json::parse(txt);
   MFT_CHECK(st["numel"].as_int() == flat_.numel, "load_state: ", dir, " holds ", st["numel"].as_int(),
             " trainable values, the model has ", flat_.numel);
-  SafeTensorsFile tw(dir + "/trainable.safetensors");
+  const bool per_rank = dp_ && dp_->params_sharded();
+  SafeTensorsFile tw(dir + (per_rank ? "/trainable.rank" + std::to_string(r) + ".safetensors" : "/trainable.safetensors"));
   SafeTensorsFile to(dir + (opt_.sharded() ? "/optimizer.rank" + std::to_string(r) + ".safetensors" : "/optimizer.safetensors"));
   auto host_view = [&](SafeTensorsFile& sf, const char* k, int64_t n) {
     MFT_CHECK(sf.has(k) && sf.info(k).dtype == "F32" && sf.info(k).end - sf.info(k).begin == (uint64_t)n * 4,

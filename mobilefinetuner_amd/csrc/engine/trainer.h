@@ -57,7 +57,7 @@ class Trainer {
  public:
   // comm != null requires dp (the reducer of that communicator)
   Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDataset& train, TokenDataset* valid, const TrainConfig& cfg,
-          PowerMonitor* pm = nullptr, Communicator* comm = nullptr, DataParallel* dp = nullptr);
+          PowerMonitor* pm = nullptr, Communicator* comm = nullptr, GradReducer* dp = nullptr);
   ~Trainer();
   int64_t total_steps() const { return total_steps_; }
   int64_t steps_per_epoch() const { return steps_per_epoch_; }
@@ -101,7 +101,7 @@ class Trainer {
   TrainConfig cfg_;
   PowerMonitor* pm_;
   Communicator* comm_;
-  DataParallel* dp_;
+  GradReducer* dp_;
   bool graph_comm_ = true;  // collectives + optimizer inside the captured step
   int64_t total_steps_ = 0, steps_per_epoch_ = 1;
   // static device inputs (the graph reads these) + loss accumulator

@@ -23,7 +23,21 @@
 namespace mft {
 namespace eng {
 
-class WeightStreamer {
+// Per-block residency of a model's weights, driven by the model forward (GPT2::hidden): the
+// host-DRAM weight stream below (--shard_enable, frozen weights) and the ZeRO-3 partitioner
+// (engine/zero3.h, trainable weights gathered from their rank partitions).
+class BlockProvider {
+ public:
+  virtual ~BlockProvider() = default;
+  // start of a forward: the non-block weights (embeddings) resident
+  virtual void begin_forward() {}
+  // block g resident before the current stream's next kernel; prefetch block `next` (-1: none)
+  virtual void ensure(int g, int next) = 0;
+  // identity on (x, h), the block's outputs; its backward runs before block g's backward does
+  virtual std::pair<Tensor, Tensor> gate(const Tensor& x, const Tensor& h, int g) = 0;
+};
+
+class WeightStreamer : public BlockProvider {
  public:
   // groups[i]: the frozen bf16 Params of block i (re-bound to slot views; their device copies freed)
   WeightStreamer(const std::vector<std::vector<Param*>>& groups, size_t budget_bytes);
@@ -31,9 +45,9 @@ class WeightStreamer {
   WeightStreamer(const WeightStreamer&) = delete;
   WeightStreamer& operator=(const WeightStreamer&) = delete;
   // block g resident before the current stream's next kernel; prefetch block `next` (-1: none)
-  void ensure(int g, int next);
+  void ensure(int g, int next) override;
   // identity on (x, h) whose backward calls ensure(g, g - 1) before block g's backward runs
-  std::pair<Tensor, Tensor> gate(const Tensor& x, const Tensor& h, int g);
+  std::pair<Tensor, Tensor> gate(const Tensor& x, const Tensor& h, int g) override;
   int slots() const { return (int)slot_.size(); }
   size_t device_bytes() const { return slot_bytes_ * slot_.size(); }
   size_t host_bytes() const { return host_bytes_; }

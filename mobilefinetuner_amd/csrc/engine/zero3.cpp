@@ -1,0 +1,259 @@
+// libmft engine: ZeRO-3 parameter partitioning (see zero3.h).
+#include "engine/zero3.h"
+
+#include <algorithm>
+#include <sstream>
+
+#include "engine/autograd.h"
+#include "engine/ops.h"
+#include "engine/tensor_kernels.h"
+#include "kernels.h"
+
+namespace mft {
+namespace eng {
+
+namespace {
+constexpr int64_t kAlign = 64;
+int64_t round_up(int64_t n, int64_t a) { return (n + a - 1) / a * a; }
+Tensor value_of(Param& p) { return p.trainable() ? p.leaf.detach() : p.c; }
+}  // namespace
+
+Zero3::Zero3(const std::vector<NamedParams>& units, const NamedParams& rep, Communicator& comm)
+    : comm_(comm), rep_(rep), flat_(FlatParams::buffers(kAlign)) {
+  NoGradGuard ng;
+  MFT_CHECK(units.size() >= 2, "Zero3: an outer unit and at least one block");
+  const int W = comm_.world(), r = comm_.rank();
+  hipStream_t cs = current_stream();
+  // layout: each unit's partition, then the replicated parameters
+  int64_t local = 0, max_block = 0;
+  for (size_t u = 0; u < units.size(); ++u) {
+    Unit un;
+    un.params = units[u];
+    int64_t off = 0;
+    for (auto& kv : un.params) {
+      MFT_CHECK(kv.second->c.dtype() == DType::BF16, "Zero3: unit parameter ", kv.first, " must compute in bf16");
+      un.off.push_back(off);
+      off += round_up(kv.second->c.numel(), kAlign);
+    }
+    un.n = round_up(std::max<int64_t>(off, kAlign), kAlign * W);
+    un.s = un.n / W;
+    un.local = local;
+    local += un.s;
+    un.slot = u == 0 ? 0 : 1 + (int)((u - 1) % 2);
+    un.total = (int)un.params.size();
+    if (u > 0) max_block = std::max(max_block, un.n);
+    units_.push_back(std::move(un));
+  }
+  rep_off_ = local;
+  std::vector<int64_t> rep_at;
+  for (auto& kv : rep_) {
+    MFT_CHECK(kv.second->c.dtype() == DType::F32, "Zero3: replicated parameter ", kv.first, " must compute in fp32");
+    rep_at.push_back(local);
+    local += round_up(kv.second->c.numel(), kAlign);
+  }
+  rep_n_ = local - rep_off_;
+  flat_ = FlatParams::buffers(std::max<int64_t>(local, kAlign));
+  slot_ = {zeros({units_[0].n}, DType::BF16), zeros({max_block}, DType::BF16), zeros({max_block}, DType::BF16)};
+  gwork_ = {zeros({units_[0].n}, DType::F32), zeros({max_block}, DType::F32), zeros({max_block}, DType::F32)};
+  holder_.assign(3, -1);
+  int64_t max_param = kAlign, max_s = kAlign;
+  for (auto& un : units_) {
+    max_s = std::max(max_s, un.s);
+    for (auto& kv : un.params) max_param = std::max(max_param, kv.second->c.numel());
+  }
+  dummy_ = zeros({max_param}, DType::F32);
+  tmp_ = zeros({max_s}, DType::F32);
+  // partitions: every unit's full fp32 value from rank 0, this rank keeps its slice
+  for (auto& un : units_) {
+    Tensor full = zeros({un.n}, DType::F32);
+    for (size_t j = 0; j < un.params.size(); ++j) {
+      Param& p = *un.params[j].second;
+      const int64_t m = p.c.numel();
+      full.slice(0, un.off[j], un.off[j] + m).copy_(value_of(p).contiguous().view({m}));
+    }
+    comm_.broadcast(full.data_ptr(), (size_t)un.n * 4, 0, cs);
+    flat_.master.slice(0, un.local, un.local + un.s).copy_(full.slice(0, (int64_t)r * un.s, (int64_t)(r + 1) * un.s));
+    for (size_t j = 0; j < un.params.size(); ++j) {
+      Param& p = *un.params[j].second;
+      const Shape shp = p.c.shape();
+      const int64_t m = p.c.numel(), o = un.off[j];
+      p.c = slot_[un.slot].slice(0, o, o + m).view(shp);
+      Tensor leaf = dummy_.slice(0, 0, m).view(shp).alias();  // placeholder: never read
+      leaf.requires_grad_(true);
+      leaf.set_grad(gwork_[un.slot].slice(0, o, o + m).view(shp));
+      p.leaf = leaf;
+      p.wt = Tensor();
+      p.streamed = true;
+    }
+  }
+  for (size_t j = 0; j < rep_.size(); ++j) {
+    Param& p = *rep_[j].second;
+    const Shape shp = p.c.shape();
+    const int64_t m = p.c.numel(), o = rep_at[j];
+    Tensor mv = flat_.master.slice(0, o, o + m).view(shp);
+    mv.copy_(value_of(p));
+    Tensor leaf = mv.alias();
+    leaf.requires_grad_(true);
+    leaf.set_grad(flat_.grad.slice(0, o, o + m).view(shp));
+    p.leaf = leaf;
+    p.c = leaf.alias();
+    p.wt = Tensor();
+  }
+  if (rep_n_ > 0) comm_.broadcast(flat_.master.data<float>() + rep_off_, (size_t)rep_n_ * 4, 0, cs);
+  flat_.refresh_shadow();
+  HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  ready_.resize(units_.size());
+  for (auto& e : ready_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  rs_done_.resize(3);
+  rs_live_.assign(3, 0);
+  for (auto& e : rs_done_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&order_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&join_, hipEventDisableTiming));
+  for (size_t u = 0; u < units_.size(); ++u)
+    for (auto& kv : units_[u].params) {
+      const int uu = (int)u;
+      add_ready_hook(kv.second->leaf, [this, uu](TensorImpl*) { on_ready(uu); });
+    }
+  synchronize();
+}
+
+Zero3::~Zero3() {
+  if (stream_) (void)hipStreamSynchronize(stream_);
+  for (auto& e : ready_) (void)hipEventDestroy(e);
+  for (auto& e : rs_done_) (void)hipEventDestroy(e);
+  if (order_) (void)hipEventDestroy(order_);
+  if (join_) (void)hipEventDestroy(join_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+std::string Zero3::describe() const {
+  std::ostringstream os;
+  int64_t n = 0;
+  for (auto& u : units_) n += u.n;
+  os << "ZeRO-3 over " << comm_.world() << " rank(s) [" << comm_.backend() << "]: " << units_.size()
+     << " units (" << n / 1000000 << "M params partitioned, " << rep_n_ / 1000 << "K replicated), blocks gathered into "
+     << "2 slots with one-block prefetch, per-block gradient reduce-scatter";
+  return os.str();
+}
+
+void Zero3::shard_optimizer(AdamW& opt, bool host_moments) {
+  std::vector<OptSegment> segs{OptSegment{0, rep_off_, 0, false}};
+  if (rep_n_ > 0) segs.push_back(OptSegment{rep_off_, rep_n_, rep_off_, true});
+  opt.shard(segs, &comm_, host_moments);
+}
+
+void Zero3::gather(int u) {
+  Unit& un = units_[u];
+  HIP_OK(hipEventRecord(order_, current_stream()));  // the slot's previous user has been enqueued
+  HIP_OK(hipStreamWaitEvent(stream_, order_, 0));
+  const ::mft::bf16_t* src = (const ::mft::bf16_t*)flat_.shadow.data_ptr() + un.local;
+  comm_.all_gather(src, slot_[un.slot].data_ptr(), (size_t)un.s, CommType::BF16, stream_);
+  HIP_OK(hipEventRecord(ready_[u], stream_));
+  holder_[un.slot] = u;
+  ++gathers;
+}
+
+void Zero3::reduce_scatter(int u) {
+  Unit& un = units_[u];
+  if (un.reduced) return;
+  un.reduced = true;
+  HIP_OK(hipEventRecord(order_, current_stream()));  // every gradient kernel of the unit enqueued
+  HIP_OK(hipStreamWaitEvent(stream_, order_, 0));
+  comm_.reduce_scatter(gwork_[un.slot].data_ptr(), tmp_.data_ptr(), (size_t)un.s, CommType::F32, CommOp::Avg, stream_);
+  Tensor dst = flat_.grad.slice(0, un.local, un.local + un.s), src = tmp_.slice(0, 0, un.s);
+  k::axpy(desc(dst), desc(src), 1.f, 1, stream_);  // += : micro-batches accumulate
+  HIP_OK(hipEventRecord(rs_done_[un.slot], stream_));
+  rs_live_[un.slot] = 1;
+  ++reduce_scatters;
+}
+
+void Zero3::zero_work(int s) {
+  // after the slot's last reduce-scatter (this step's) has read it; events of earlier steps are
+  // never waited on, so a hipGraph capture only depends on work it recorded itself
+  if (rs_live_[s]) HIP_OK(hipStreamWaitEvent(current_stream(), rs_done_[s], 0));
+  gwork_[s].zero_();
+}
+
+void Zero3::after_optimizer() { holder_.assign(holder_.size(), -1); }  // every partition changed
+
+void Zero3::on_ready(int u) {
+  if (--units_[u].pending == 0) reduce_scatter(u);
+}
+
+void Zero3::begin_micro(int i, int n) {
+  (void)n;
+  if (i == 0) {  // nothing carries over from the previous step (its finish() joined every collective)
+    holder_.assign(holder_.size(), -1);
+    rs_live_.assign(rs_live_.size(), 0);
+  }
+  for (auto& un : units_) {
+    un.pending = un.total;
+    un.reduced = false;
+  }
+}
+
+void Zero3::begin_forward() {
+  if (holder_[0] != 0) gather(0);
+  HIP_OK(hipStreamWaitEvent(current_stream(), ready_[0], 0));
+  if (grad_enabled()) {  // the tied embedding's gradient starts in the LM-head CE of this forward
+    zero_work(0);
+  }
+}
+
+void Zero3::ensure(int block, int next) {
+  const int u = 1 + block;
+  if (holder_[units_[u].slot] != u) gather(u);
+  HIP_OK(hipStreamWaitEvent(current_stream(), ready_[u], 0));
+  const int nu = 1 + next;
+  if (next >= 0 && nu < (int)units_.size() && units_[nu].slot != units_[u].slot && holder_[units_[nu].slot] != nu)
+    gather(nu);
+}
+
+std::pair<Tensor, Tensor> Zero3::gate(const Tensor& x, const Tensor& h, int block) {
+  Tensor xo = x.alias(), ho = h.alias();
+  if (any_needs_grad({x, h})) {
+    Zero3* self = this;
+    auto n = lambda_node("Zero3GateBackward", [self, block](std::vector<Tensor>& grads) {
+      self->ensure(block, block - 1);  // the block's weights back before its backward reads them
+      self->zero_work(self->units_[1 + block].slot);
+      return std::vector<Tensor>{grads[0], grads[1]};
+    });
+    connect(n, {x, h}, {xo, ho});
+  }
+  return {xo, ho};
+}
+
+void Zero3::finish() {
+  for (size_t u = 0; u < units_.size(); ++u) reduce_scatter((int)u);  // units no hook completed
+  if (rep_n_ > 0) {
+    HIP_OK(hipEventRecord(order_, current_stream()));
+    HIP_OK(hipStreamWaitEvent(stream_, order_, 0));
+    comm_.all_reduce(flat_.grad.data<float>() + rep_off_, (size_t)rep_n_, CommType::F32, CommOp::Avg, stream_);
+  }
+  HIP_OK(hipEventRecord(join_, stream_));
+  HIP_OK(hipStreamWaitEvent(current_stream(), join_, 0));
+}
+
+void Zero3::materialize() {
+  NoGradGuard ng;
+  synchronize();
+  for (auto& un : units_) {
+    Tensor full = zeros({un.n}, DType::F32);
+    comm_.all_gather(flat_.master.data<float>() + un.local, full.data_ptr(), (size_t)un.s, CommType::F32,
+                     current_stream());
+    for (size_t j = 0; j < un.params.size(); ++j) {
+      Param& p = *un.params[j].second;
+      const Shape shp = p.c.shape();
+      const int64_t m = p.c.numel(), o = un.off[j];
+      Tensor v = full.slice(0, o, o + m).view(shp).clone();
+      p.c = v.to(DType::BF16);
+      v.requires_grad_(true);  // trainable(): writers read the fp32 value
+      p.leaf = v;
+      p.streamed = false;
+    }
+  }
+  synchronize();
+}
+
+}  // namespace eng
+}  // namespace mft

@@ -89,6 +89,9 @@ def _single(prog, args, batch_flag, batch):
     (["--zero_stage", "2", "--offload", "host"], 3e-3),   # bf16 stochastically-rounded moments
     (["--bf16_grads"], 1e-2),
     (["--zero_stage", "2", "--no_overlap", "--no_graph"], 2e-4),
+    (["--zero_stage", "3"], 2e-4),
+    (["--zero_stage", "3", "--no_graph", "--grad_accum_steps", "1"], 2e-4),
+    (["--zero_stage", "3", "--offload", "host"], 3e-3),
 ])
 def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
     """2 loopback ranks x batch 4 == 1 process x batch 8 (GPT-2-tiny full fine-tune, ~8 buckets):
@@ -101,7 +104,9 @@ def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
     for rc, o, e in res:
         assert rc == 0, o[-2000:] + e[-2000:]
     out0 = res[0][1]
-    assert "data parallel: rank 0 of 2 (loopback" in out0 and "bucket(s)" in out0, out0[:3000]
+    assert "data parallel: rank 0 of 2 (loopback" in out0, out0[:3000]
+    z3 = "3" in extra[1:2]
+    assert ("ZeRO-3 over 2 rank(s)" if z3 else "bucket(s)") in out0, out0[:3000]
     got = loss_list(out0, True)
     assert len(got) == 6 and got == pytest.approx(want, rel=tol, abs=tol), (extra, got, want)
     from mobilefinetuner_amd.io import safetensors as st
@@ -140,11 +145,25 @@ def test_native_rccl_zero2_step_in_graph():
     assert loss_list(r.stdout, True) == pytest.approx(want, rel=2e-4, abs=2e-4)
 
 
-def test_native_dp_state_resume_two_ranks(tmp_path):
-    """ZeRO-2 full-state checkpoint (gathered fp32 master + one optimizer partition per rank):
-    4 steps, then both ranks resume from the saved state and finish steps 5-8 with the
-    uninterrupted run's losses."""
-    base = FULL[:-4] + ["--bucket_mb", "0.25", "--batch_size", "4", "--zero_stage", "2", "--warmup_steps", "100"]
+def test_native_rccl_zero3_step_in_graph():
+    """ZeRO-3 on a 1-rank RCCL group: per-block all-gathers into the two device slots, per-block
+    gradient reduce-scatters and the partitioned AdamW, all recorded into ONE hipGraph, with the
+    plain single-process losses (2 micro-batches: the reduce-scatters accumulate)."""
+    args = FULL + ["--batch_size", "2", "--grad_accum_steps", "2"]
+    want = loss_list(_single("gpt2_full_finetune", args[:-2], "--grad_accum_steps", 2).stdout, True)
+    r = subprocess.run([_bin("gpt2_full_finetune"), *args, "--zero_stage", "3"],
+                       capture_output=True, text=True, timeout=240, env=_env(backend="rccl", MFT_DP_FORCE_COMM="1"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "ZeRO-3 over 1 rank(s) [rccl]" in r.stdout and "hipGraph" in r.stdout, r.stdout[:3000]
+    assert loss_list(r.stdout, True) == pytest.approx(want, rel=2e-4, abs=2e-4)
+
+
+@pytest.mark.parametrize("stage", ["2", "3"])
+def test_native_dp_state_resume_two_ranks(tmp_path, stage):
+    """ZeRO-2 / ZeRO-3 full-state checkpoint (gathered fp32 master, or each rank's own parameter
+    partitions, + one optimizer partition per rank): 4 steps, then both ranks resume from the saved
+    state and finish steps 5-8 with the uninterrupted run's losses."""
+    base = FULL[:-4] + ["--bucket_mb", "0.25", "--batch_size", "4", "--zero_stage", stage, "--warmup_steps", "100"]
     ref = _run_ranks([_bin("gpt2_full_finetune"), *base, "--steps", "8"], 2)
     assert all(rc == 0 for rc, _, _ in ref)
     want = loss_list(ref[0][1])
