@@ -25,14 +25,54 @@ bool CachingAllocator::BySize::operator()(const Block* a, const Block* b) const 
   return (uintptr_t)a->ptr < (uintptr_t)b->ptr;
 }
 
-CachingAllocator::CachingAllocator(int device) : device_(device) {}
+namespace {
+// device memory + HIP events of one GPU
+class HipBackend : public AllocatorBackend {
+ public:
+  explicit HipBackend(int device) : device_(device) {}
+  bool map(void** ptr, size_t nbytes) override {
+    HIP_OK(hipSetDevice(device_));
+    if (hipMalloc(ptr, nbytes) == hipSuccess) return true;
+    (void)hipGetLastError();
+    return false;
+  }
+  void unmap(void* ptr) override { HIP_OK(hipFree(ptr)); }
+  void synchronize() override { HIP_OK(hipDeviceSynchronize()); }
+  void* record(hipStream_t stream) override {
+    hipEvent_t e;
+    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(e, stream));
+    return (void*)e;
+  }
+  bool passed(void* event) override { return hipEventQuery((hipEvent_t)event) == hipSuccess; }
+  void destroy(void* event) override { (void)hipEventDestroy((hipEvent_t)event); }
+
+ private:
+  int device_;
+};
+}  // namespace
+
+CachingAllocator::CachingAllocator(std::unique_ptr<AllocatorBackend> backend) : be_(std::move(backend)) {}
+
+CachingAllocator::~CachingAllocator() {
+  // (the engine's allocators live for the process; private ones release everything they hold)
+  std::lock_guard<std::mutex> g(mu_);
+  for (Block* b : with_events_)
+    for (void* e : b->pending) be_->destroy(e);
+  std::vector<Block*> all;
+  for (auto& kv : free_) all.insert(all.end(), kv.second.begin(), kv.second.end());
+  for (Block* b : with_events_) all.push_back(b);
+  for (auto& kv : live_) all.push_back(kv.second);
+  for (Block* b : all) delete b;
+  for (void* p : segments_) be_->unmap(p);
+}
 
 CachingAllocator& CachingAllocator::get(int device) {
   static std::mutex mu;
   static std::vector<CachingAllocator*> all;
   std::lock_guard<std::mutex> g(mu);
   if ((int)all.size() <= device) all.resize(device + 1, nullptr);
-  if (!all[device]) all[device] = new CachingAllocator(device);  // process lifetime
+  if (!all[device]) all[device] = new CachingAllocator(std::make_unique<HipBackend>(device));  // process lifetime
   return *all[device];
 }
 
@@ -53,18 +93,18 @@ void CachingAllocator::process_events() {
   for (size_t i = 0; i < with_events_.size();) {
     Block* b = with_events_[i];
     bool done = true;
-    for (hipEvent_t e : b->pending) {
-      if (hipEventQuery(e) != hipSuccess) {
+    for (void* e : b->pending) {
+      if (!be_->passed(e)) {
         done = false;
         break;
       }
     }
     if (done) {
-      for (hipEvent_t e : b->pending) (void)hipEventDestroy(e);
+      for (void* e : b->pending) be_->destroy(e);
       b->pending.clear();
-      insert_free(b);
       with_events_[i] = with_events_.back();
       with_events_.pop_back();
+      free_block(b);  // (coalesces, so the segment can become whole and idle again)
     } else {
       ++i;
     }
@@ -94,7 +134,7 @@ bool CachingAllocator::free_idle_segments() {
       Block* b = *it;
       if (!b->prev && !b->next) {  // whole segment idle
         it = fs.erase(it);
-        HIP_OK(hipFree(b->ptr));
+        be_->unmap(b->ptr);
         st_.reserved -= b->size;
         st_.n_segments--;
         segments_.erase(std::remove(segments_.begin(), segments_.end(), b->ptr), segments_.end());
@@ -123,15 +163,11 @@ void* CachingAllocator::allocate(size_t nbytes, hipStream_t stream) {
     // graph's private pool: it stays owned by that pool, so replays never alias eager tensors
     const size_t seg = small ? kSmallSeg : round_up(size, kLargeRound);
     void* p = nullptr;
-    HIP_OK(hipSetDevice(device_));
-    hipError_t e = hipMalloc(&p, seg);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      HIP_OK(hipDeviceSynchronize());
+    if (!be_->map(&p, seg)) {
+      be_->synchronize();
       process_events();
       free_idle_segments();
-      e = hipMalloc(&p, seg);
-      MFT_CHECK(e == hipSuccess, "allocator: out of device memory allocating ", seg, " bytes (allocated ",
+      MFT_CHECK(be_->map(&p, seg), "allocator: out of device memory allocating ", seg, " bytes (allocated ",
                 st_.allocated, ", reserved ", st_.reserved, ")");
     }
     st_.n_hip_malloc++;
@@ -190,16 +226,15 @@ void CachingAllocator::release(void* ptr) {
   st_.allocated -= b->size;
   st_.n_free++;
   if (!b->uses.empty()) {
-    for (hipStream_t s : b->uses) {
-      hipEvent_t e;
-      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      HIP_OK(hipEventRecord(e, s));
-      b->pending.push_back(e);
-    }
+    for (hipStream_t s : b->uses) b->pending.push_back(be_->record(s));
     b->uses.clear();
     with_events_.push_back(b);
     return;
   }
+  free_block(b);
+}
+
+void CachingAllocator::free_block(Block* b) {
   // coalesce with free neighbours of the same segment (same pool / stream by construction)
   auto mergeable = [&](Block* n) {
     return n && !n->allocated && n->pending.empty() &&
@@ -227,7 +262,7 @@ void CachingAllocator::release(void* ptr) {
 
 void CachingAllocator::empty_cache() {
   std::lock_guard<std::mutex> g(mu_);
-  HIP_OK(hipDeviceSynchronize());
+  be_->synchronize();
   process_events();
   free_idle_segments();
 }

@@ -14,7 +14,10 @@
 //   * stats: allocated / reserved / peak bytes, segment count; empty_cache() returns whole idle
 //     segments to HIP (the reference's clear_unused, memory_manager.cpp:99-145);
 //   * a capture runs in hipStreamCaptureModeRelaxed, so a cache miss may hipMalloc a new segment
-//     for the graph's private pool (never for pool 0).
+//     for the graph's private pool (never for pool 0);
+//   * segments and cross-stream events come from an AllocatorBackend: HIP in the engine, a host
+//     test double in tests/engine_host_selftest.cpp, so the split / coalesce / event bookkeeping
+//     runs under ASan / UBSan on a machine without a GPU (CMakePresets.json).
 // Sized for 288 GB of HBM3E per GPU: nothing here caps the cache below the device.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -22,6 +25,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <unordered_map>
@@ -30,6 +34,18 @@
 namespace mft {
 namespace eng {
 
+// Where the caching allocator's memory and stream-ordering events come from.
+class AllocatorBackend {
+ public:
+  virtual ~AllocatorBackend() = default;
+  virtual bool map(void** ptr, size_t nbytes) = 0;  // false: out of memory (the cache is trimmed, then retried)
+  virtual void unmap(void* ptr) = 0;
+  virtual void synchronize() = 0;             // all queued work on the device has completed
+  virtual void* record(hipStream_t stream) = 0;  // an event after the work queued on `stream` so far
+  virtual bool passed(void* event) = 0;       // that work has completed
+  virtual void destroy(void* event) = 0;
+};
+
 struct AllocStats {
   size_t allocated = 0, reserved = 0, peak_allocated = 0, peak_reserved = 0;
   uint64_t n_alloc = 0, n_free = 0, n_segments = 0, n_hip_malloc = 0, n_cache_hits = 0;
@@ -37,7 +53,12 @@ struct AllocStats {
 
 class CachingAllocator {
  public:
-  static CachingAllocator& get(int device);
+  static CachingAllocator& get(int device);  // the engine's HIP-backed allocator of `device`
+  // a private allocator over any backend (tests; the engine uses get())
+  explicit CachingAllocator(std::unique_ptr<AllocatorBackend> backend);
+  ~CachingAllocator();
+  CachingAllocator(const CachingAllocator&) = delete;
+  CachingAllocator& operator=(const CachingAllocator&) = delete;
   void* allocate(size_t nbytes, hipStream_t stream);
   void release(void* ptr);
   // ptr will be used by `stream` too: on release it is reused only after that work completed
@@ -52,7 +73,6 @@ class CachingAllocator {
   size_t block_size(void* ptr) const;
 
  private:
-  explicit CachingAllocator(int device);
   struct Block;
   struct BySize {
     bool operator()(const Block* a, const Block* b) const;
@@ -66,16 +86,17 @@ class CachingAllocator {
     hipStream_t stream = nullptr;
     Block *prev = nullptr, *next = nullptr;  // neighbours inside the same hipMalloc segment
     std::vector<hipStream_t> uses;          // record_stream
-    std::vector<hipEvent_t> pending;        // events to pass before reuse
+    std::vector<void*> pending;             // backend events to pass before reuse
   };
   using FreeSet = std::set<Block*, BySize>;
   FreeSet& free_set(int pool, bool small);
   Block* find_free(int pool, bool small, size_t size, hipStream_t stream);
   void insert_free(Block* b);
   void erase_free(Block* b);
+  void free_block(Block* b);  // coalesce with idle neighbours, then into the free set
   void process_events();
   bool free_idle_segments();
-  int device_;
+  std::unique_ptr<AllocatorBackend> be_;
   mutable std::mutex mu_;
   std::map<std::pair<int, bool>, FreeSet> free_;
   std::unordered_map<void*, Block*> live_;

@@ -92,6 +92,17 @@ Tensor grad_buffer(const Tensor& t) {
 // it carries extra leading dims or size-1 broadcast dims
 static void add_into(Tensor& buf, const Tensor& g, float alpha) {
   NoGradGuard ng;
+  if (!buf.is_hip()) {  // host tensors (engine_host_selftest: the tape under ASan / UBSan), via fp32
+    MFT_CHECK(!g.is_hip() && g.dim() <= buf.dim(), "add_into: host gradient ", g.str(), " into ", buf.str());
+    Tensor a = empty(buf.shape(), DType::F32, Device::cpu()), b = empty(buf.shape(), DType::F32, Device::cpu());
+    a.copy_(buf);
+    b.copy_(g);  // (broadcast over leading / size-1 dims)
+    float* pa = a.data<float>();
+    const float* pb = b.data<float>();
+    for (int64_t i = 0; i < a.numel(); ++i) pa[i] += alpha * pb[i];
+    buf.copy_(a);
+    return;
+  }
   Tensor gg = g;
   if (gg.shape() != buf.shape()) gg = sum_to(gg, buf.shape());
   k::axpy(desc(buf), desc_bcast(gg, buf.shape()), alpha, 1, current_stream());

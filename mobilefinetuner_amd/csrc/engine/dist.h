@@ -50,6 +50,12 @@ class GradReducer {
   virtual void gather_master() {}
   // ZeRO-3: each rank's flat holds only its partitions (no initial broadcast, per-rank masters)
   virtual bool params_sharded() const { return false; }
+  // factor folded into the loss seed (and the fused LM-head weight grad): a reducer that SUMS
+  // returns 1 / world so the reduced gradient is the average
+  virtual float grad_prescale() const { return 1.f; }
+  // clear the gradients a step accumulates into (a reducer whose first reduction overwrites its
+  // destination clears less)
+  virtual void zero_grad(FlatParams& flat) { flat.zero_grad(); }
   virtual std::string describe() const = 0;
 };
 

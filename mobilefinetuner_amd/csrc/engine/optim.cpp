@@ -120,7 +120,10 @@ void AdamW::step() {
     for (const auto& sg : segs_)
       if (sg.replicated) ::mft::sumsq(g0 + sg.off, sg.len, part_.data<float>(), sumsq_dev.data<float>(), 1, s);
   }
-  if (cfg_.skip_nonfinite) {
+  // non-finite grads: with clipping the (all-reduced) norm^2 is non-finite exactly then, so no
+  // separate pass over the grads is needed (adamw_commit records the flag); without, one scan
+  const bool scan = cfg_.skip_nonfinite && !clip;
+  if (scan) {
     nonfinite_dev.zero_();
     for (auto& sg : segs_) ::mft::nonfinite_check(g0 + sg.off, sg.len, nonfinite_dev.data<int>(), s);
     if (comm_) comm_->all_reduce(nonfinite_dev.data_ptr(), 1, CommType::I32, CommOp::Max, s);  // skip together
@@ -135,7 +138,7 @@ void AdamW::step() {
   a.sumsq = clip ? sumsq_dev.data<float>() : nullptr;
   a.max_norm = cfg_.max_grad_norm;
   a.l2_coupled = cfg_.l2_coupled;
-  a.nonfinite = cfg_.skip_nonfinite ? nonfinite_dev.data<int>() : nullptr;
+  a.nonfinite = scan ? nonfinite_dev.data<int>() : nullptr;
   a.moments_bf16 = m.dtype() == DType::BF16;
   const size_t ms = m.dtype() == DType::BF16 ? 2 : 4;
   for (auto& sg : segs_) {
@@ -148,7 +151,8 @@ void AdamW::step() {
     a.sr_offset = sg.off;
     ::mft::adamw_step(a, s);
   }
-  ::mft::adamw_commit(step_dev.data<float>(), a.nonfinite, a.sumsq, s);
+  ::mft::adamw_commit(step_dev.data<float>(), a.nonfinite, a.sumsq, s,
+                      cfg_.skip_nonfinite ? nonfinite_dev.data<int>() : nullptr);
   if (cfg_.skip_nonfinite) {
     // skipped += nonfinite (int32 counters)
     k::Desc d = desc(skipped_dev), x = desc(nonfinite_dev);

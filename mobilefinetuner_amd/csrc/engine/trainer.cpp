@@ -69,7 +69,9 @@ void Trainer::optimizer() {
 
 void Trainer::fwd_bwd() {
   const float inv = 1.f / (float)ids_.size();
-  flat_.zero_grad();
+  const float gs = inv * (dp_ ? dp_->grad_prescale() : 1.f);  // backward seed
+  if (dp_) dp_->zero_grad(flat_);
+  else flat_.zero_grad();
   loss_acc_.zero_();
   {
     // fresh LoRA-dropout masks every step (device counter, advanced inside the graph too)
@@ -78,8 +80,8 @@ void Trainer::fwd_bwd() {
   }
   for (size_t i = 0; i < ids_.size(); ++i) {
     if (dp_) dp_->begin_micro((int)i, (int)ids_.size());  // the last micro-batch's hooks launch buckets
-    Tensor loss = model_.loss(ids_[i], labels_[i], inv);
-    Tensor scaled = mul_scalar(loss, inv);
+    Tensor loss = model_.loss(ids_[i], labels_[i], gs);
+    Tensor scaled = mul_scalar(loss, gs);
     backward({scaled});
     add_(loss_acc_, loss.detach(), inv);
   }

@@ -159,9 +159,14 @@ void Zero3::reduce_scatter(int u) {
   un.reduced = true;
   HIP_OK(hipEventRecord(order_, current_stream()));  // every gradient kernel of the unit enqueued
   HIP_OK(hipStreamWaitEvent(stream_, order_, 0));
-  comm_.reduce_scatter(gwork_[un.slot].data_ptr(), tmp_.data_ptr(), (size_t)un.s, CommType::F32, CommOp::Avg, stream_);
-  Tensor dst = flat_.grad.slice(0, un.local, un.local + un.s), src = tmp_.slice(0, 0, un.s);
-  k::axpy(desc(dst), desc(src), 1.f, 1, stream_);  // += : micro-batches accumulate
+  Tensor dst = flat_.grad.slice(0, un.local, un.local + un.s);
+  if (first_micro_) {  // the partition's first contribution of the step: written in place
+    comm_.reduce_scatter(gwork_[un.slot].data_ptr(), dst.data_ptr(), (size_t)un.s, CommType::F32, CommOp::Sum, stream_);
+  } else {  // later micro-batches accumulate
+    comm_.reduce_scatter(gwork_[un.slot].data_ptr(), tmp_.data_ptr(), (size_t)un.s, CommType::F32, CommOp::Sum, stream_);
+    Tensor src = tmp_.slice(0, 0, un.s);
+    k::axpy(desc(dst), desc(src), 1.f, 1, stream_);
+  }
   HIP_OK(hipEventRecord(rs_done_[un.slot], stream_));
   rs_live_[un.slot] = 1;
   ++reduce_scatters;
@@ -180,8 +185,19 @@ void Zero3::on_ready(int u) {
   if (--units_[u].pending == 0) reduce_scatter(u);
 }
 
+float Zero3::grad_prescale() const { return 1.f / (float)comm_.world(); }
+
+void Zero3::zero_grad(FlatParams& flat) {
+  // the partitions are overwritten by the first micro-batch's reduce-scatters; only the replicated
+  // gradients accumulate from zero
+  if (rep_n_ > 0) flat.grad.slice(0, rep_off_, rep_off_ + rep_n_).zero_();
+}
+
 void Zero3::begin_micro(int i, int n) {
   (void)n;
+  if (i > 0)  // (a unit no hook completed in the previous micro-batch: reduce it before its slot is reused)
+    for (size_t u = 0; u < units_.size(); ++u) reduce_scatter((int)u);
+  first_micro_ = i == 0;
   if (i == 0) {  // nothing carries over from the previous step (its finish() joined every collective)
     holder_.assign(holder_.size(), -1);
     rs_live_.assign(rs_live_.size(), 0);
@@ -228,7 +244,7 @@ void Zero3::finish() {
   if (rep_n_ > 0) {
     HIP_OK(hipEventRecord(order_, current_stream()));
     HIP_OK(hipStreamWaitEvent(stream_, order_, 0));
-    comm_.all_reduce(flat_.grad.data<float>() + rep_off_, (size_t)rep_n_, CommType::F32, CommOp::Avg, stream_);
+    comm_.all_reduce(flat_.grad.data<float>() + rep_off_, (size_t)rep_n_, CommType::F32, CommOp::Sum, stream_);
   }
   HIP_OK(hipEventRecord(join_, stream_));
   HIP_OK(hipStreamWaitEvent(current_stream(), join_, 0));

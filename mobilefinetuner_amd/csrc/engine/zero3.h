@@ -20,8 +20,9 @@
 //     re-gathers it (prefetching i - 1).  The Params' compute views point into the slots.
 //   * gradients: block i's kernels accumulate into an fp32 work slot (i % 2) that is zeroed at the
 //     gate; when the last of the unit's parameters is final (the tape's grad-ready hooks) the slot
-//     is REDUCE-SCATTERED (average) into this rank's partition of the gradient (+=, so micro-
-//     batches accumulate).  Replicated gradients are all-reduced in finish().
+//     is REDUCE-SCATTERED (sum; the loss seed carries 1 / world) straight into this rank's
+//     partition of the gradient in the first micro-batch, through a landing buffer + add in later
+//     ones -- so the partitions are never zeroed.  Replicated gradients are all-reduced in finish().
 // Every cross-stream dependency is an event, so the whole step (gathers, reduce-scatters, the
 // partitioned optimizer) records into the trainer's hipGraph like any other work.
 #pragma once
@@ -59,6 +60,8 @@ class Zero3 : public GradReducer, public BlockProvider {
   void finish() override;
   void after_optimizer() override;
   bool params_sharded() const override { return true; }
+  float grad_prescale() const override;
+  void zero_grad(FlatParams& flat) override;
   std::string describe() const override;
   // BlockProvider
   void begin_forward() override;
@@ -80,6 +83,7 @@ class Zero3 : public GradReducer, public BlockProvider {
     int pending = 0, total = 0;
     bool reduced = false;
   };
+  bool first_micro_ = true;
   void gather(int u);
   void reduce_scatter(int u);
   void on_ready(int u);

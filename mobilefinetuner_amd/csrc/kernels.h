@@ -200,7 +200,7 @@ struct AdamWArgs {
 };
 void adamw_step(const AdamWArgs& a, hipStream_t st);
 // after every adamw_step launch of one update: *step += 1 unless the update was skipped
-void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStream_t st);
+void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStream_t st, int* flag_out = nullptr);
 // flag[0] = any(!isfinite(x))  (accumulates with OR)
 void nonfinite_check(const float* x, long n, int* flag, hipStream_t st);
 

@@ -172,13 +172,19 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
   }
 }
 
-// step += 1 only when the update was applied (a skipped step must not advance bias correction)
-__global__ void adamw_commit_kernel(float* step, const int* nonfinite, const float* sumsq) {
-  if (threadIdx.x == 0 && !adamw_skip(nonfinite, sumsq)) step[0] += 1.f;
+// step += 1 only when the update was applied (a skipped step must not advance bias correction);
+// flag_out (optional) records whether the step was skipped -- with clipping on, a non-finite grad
+// makes the global norm^2 non-finite, so that one reduction replaces the separate scan of the grads
+__global__ void adamw_commit_kernel(float* step, const int* nonfinite, const float* sumsq, int* flag_out) {
+  if (threadIdx.x == 0) {
+    const bool skip = adamw_skip(nonfinite, sumsq);
+    if (!skip) step[0] += 1.f;
+    if (flag_out) flag_out[0] = skip ? 1 : 0;
+  }
 }
 
-void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStream_t st) {
-  adamw_commit_kernel<<<1, 64, 0, st>>>(step, nonfinite, sumsq);
+void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStream_t st, int* flag_out) {
+  adamw_commit_kernel<<<1, 64, 0, st>>>(step, nonfinite, sumsq, flag_out);
 }
 
 void adamw_step(const AdamWArgs& a, hipStream_t st) {
