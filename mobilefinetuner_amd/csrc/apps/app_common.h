@@ -9,6 +9,9 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstdio>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
 #include <functional>
 #include <map>
 #include <memory>
@@ -18,6 +21,7 @@
 #include <thread>
 #include <vector>
 
+#include "engine/autograd.h"
 #include "engine/comm.h"
 #include "engine/dist.h"
 #include "engine/optim.h"
@@ -62,6 +66,14 @@ inline Args parse_args(int argc, char** argv, const std::set<std::string>& kBool
       has_val = true;
     }
     if (kBool.count(key)) {
+      if (!has_val && i + 1 < argc) {  // "--flag 0" / "--flag true" (the reference's get_val form)
+        const std::string nx = argv[i + 1];
+        if (nx == "0" || nx == "1" || nx == "true" || nx == "false" || nx == "True" || nx == "False") {
+          val = nx;
+          has_val = true;
+          ++i;
+        }
+      }
       if (has_val) a.kv[key] = val;
       else a.flags.insert(key);
       continue;
@@ -228,6 +240,61 @@ inline void bench_report(TrainerT& trainer, const FlatT& flat, const Args& a, in
               "\"n_trainable\": %lld}\n",
               secs, steps, warmup, world, batch, seq, accum, loss, model.c_str(), n_params, n_train);
   std::fflush(stdout);
+}
+
+// --dump_grads PATH (parity tests): ONE forward + backward of the first B chunks of the train split
+// (chunk order 0..B-1, no shuffle, no optimizer step); the gradients then REPLACE the trainable
+// fp32 masters so the model's own checkpoint writer (LoRA or HF layout) stores them under the
+// usual keys.  Returns the (mean) loss.
+template <class ModelT>
+inline float grads_into_masters(ModelT& model, eng::FlatParams& flat, TokenDataset& train, int B, int S) {
+  std::vector<size_t> idx((size_t)B);
+  for (int i = 0; i < B; ++i) idx[i] = (size_t)i % std::max<size_t>(1, train.num_sequences());
+  std::vector<int64_t> hid((size_t)B * S), htg((size_t)B * S);
+  std::vector<float> mk((size_t)B * S);
+  train.get_batch(idx.data(), B, hid.data(), htg.data(), mk.data(), nullptr);
+  eng::Tensor ids = eng::from_host(hid.data(), {B, S}, eng::DType::I64);
+  eng::Tensor tg = eng::from_host(htg.data(), {B, S}, eng::DType::I64);
+  flat.zero_grad();
+  eng::Tensor loss = model.loss(ids, tg, 1.f);
+  eng::backward({loss});
+  const float lv = (float)loss.item();
+  flat.master.copy_(flat.grad);
+  eng::synchronize();
+  return lv;
+}
+
+// NumPy .npy v1.0 writer for the alignment dumps (the reference's save_npy, train_lora_gemma.cpp:
+// 137-178): descr "<f4" / "<i4", C order, header padded to a 64-byte boundary.  Parent directories
+// are created.
+inline void save_npy(const std::string& path, const void* data, const std::vector<int64_t>& shape, const char* descr,
+                     size_t elem_bytes) {
+  std::filesystem::path fp(path);
+  if (fp.has_parent_path()) std::filesystem::create_directories(fp.parent_path());
+  std::string sh = "(";
+  size_t n = 1;
+  for (size_t i = 0; i < shape.size(); ++i) {
+    sh += std::to_string(shape[i]) + (shape.size() == 1 ? "," : (i + 1 < shape.size() ? ", " : ""));
+    n *= (size_t)shape[i];
+  }
+  sh += ")";
+  std::string hdr = std::string("{'descr': '") + descr + "', 'fortran_order': False, 'shape': " + sh + ", }";
+  const size_t base = 10;  // magic (6) + version (2) + header length (2)
+  hdr.append((64 - (base + hdr.size() + 1) % 64) % 64, ' ');
+  hdr += '\n';
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot write " + path);
+  const unsigned char magic[8] = {0x93, 'N', 'U', 'M', 'P', 'Y', 1, 0};
+  f.write((const char*)magic, 8);
+  const uint16_t hl = (uint16_t)hdr.size();
+  const unsigned char hlb[2] = {(unsigned char)(hl & 0xff), (unsigned char)(hl >> 8)};
+  f.write((const char*)hlb, 2);
+  f.write(hdr.data(), (std::streamsize)hdr.size());
+  f.write((const char*)data, (std::streamsize)(n * elem_bytes));
+  if (!f) throw std::runtime_error("short write " + path);
+}
+inline void save_npy_f32(const std::string& path, const std::vector<float>& v, const std::vector<int64_t>& shape) {
+  save_npy(path, v.data(), shape, "<f4", 4);
 }
 
 // --pm_* flags (reference energy options) -> PowerMonitor, or null when off

@@ -52,7 +52,7 @@ static const char* kProg = "gpt2_lora_finetune";
 namespace {
 
 const std::set<std::string> kBool = {"split_qkv", "random_init", "synthetic_data", "no_graph", "compat_l2_adam",
-                                     "shard_enable", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
+                                     "activation_checkpointing", "shard_enable", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
                                      "deterministic", "bf16_grads", "no_overlap", "help"};
 const std::set<std::string> kValued = {
     "data_dir", "pretrained_dir", "lora_out", "resume_from", "state_dir", "inject_fault", "eval_out", "output_path", "epochs", "steps",
@@ -61,7 +61,7 @@ const std::set<std::string> kValued = {
     "eval_batch_size", "save_every", "ema_beta", "seed", "pm_interval", "pm_batt_thresh", "pm_temp_thresh",
     "pm_fb_high", "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule",
     "shard_dir", "shard_budget_mb", "shard_fp16_disk", "model", "synthetic_tokens", "pretokenized_path",
-    "pretokenized_meta", "lora_targets", "metrics_out", "device", "bench_steps", "bench_warmup", "zero_stage", "offload", "bucket_mb"};
+    "pretokenized_meta", "lora_targets", "metrics_out", "device", "bench_steps", "bench_warmup", "zero_stage", "offload", "bucket_mb", "dump_grads"};
 
 Args parse(int argc, char** argv) { return parse_args(argc, argv, kBool, kValued); }
 
@@ -153,6 +153,7 @@ int run(int argc, char** argv) {
   if (!random_init && file_exists(pdir + "/config.json")) cfg = GPT2Config::from_json(pdir + "/config.json");
   else cfg = GPT2Config::preset(a.get("model", "gpt2"));
   auto model = std::make_unique<GPT2>(cfg);
+  model->grad_checkpoint = a.b("activation_checkpointing");  // recompute blocks in the backward
   if (random_init) {
     model->init_random(1234);
     std::printf("  random-init %s (%d layers, C=%d, H=%d)\n", a.get("model", "gpt2").c_str(), cfg.n_layer,
@@ -232,6 +233,14 @@ int run(int argc, char** argv) {
   std::printf("  train: %zu sequences | valid: %zu sequences\n", train.num_sequences(),
               have_valid ? valid.num_sequences() : (size_t)0);
 
+  if (!a.get("dump_grads").empty()) {  // parity tests: one fwd+bwd, gradients in the checkpoint layout
+    MFT_CHECK(!comm && !ds.z3, "--dump_grads runs on one process without ZeRO-3");
+    const float lv = mft::apps::grads_into_masters(*model, flat, train, a.i("batch_size", 1), seq);
+    if (full) model->save_hf(a.get("dump_grads"));
+    else model->save_lora(a.get("dump_grads"));
+    std::printf("MFT_DUMP loss=%.8f path=%s\n", lv, a.get("dump_grads").c_str());
+    return 0;
+  }
   AdamWConfig oc;
   oc.lr = a.f("lr", full ? 5e-5f : 1e-4f);
   oc.weight_decay = a.f("weight_decay", full ? 0.01f : 0.f);

@@ -10,19 +10,37 @@
 //   --model P --random_init --synthetic_data [--synthetic_tokens N] --resume_from F (initial
 //   adapter) --no_graph --compat_l2_adam --metrics_out F --deterministic --interleaved_rope
 //   --shard_enable --shard_budget_mb N: frozen layer weights streamed from pinned host memory
-// The alignment-dump harness (--align_*) and the embedding dump stay in the Python CLI.
+// Alignment harness (--align_dump_dir D, reference train_lora_gemma.cpp:609-922): one fixed batch,
+// LoRA dropout off; dumps input_ids / labels / per-token NLL / loss_scalar, the MLP output of each
+// --align_layers layer, the LoRA gradients of those layers (--align_dump_grads, default on) and,
+// with --align_do_step (default on), the adapters after one AdamW step (wd 0); --align_numeric_attn
+// adds central finite-difference checks of the largest attention-LoRA gradients
+// (--align_numeric_targets q,k,v,o; --align_numeric_eps; --align_numeric_count) and
+// --align_pt_weights_dir overrides the initial adapters from a PyTorch dump.  File names follow the
+// reference: grads/base_model_model_model_layers_<i>_self_attn_q_proj_lora_A_default_weight.npy
+// (A as [in, r], B as [r, out]).  --loss_reduction sum|sum_debug: summed token NLL, unnormalised
+// gradient (core/lm_loss.cpp:184-192).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <map>
 #include <memory>
+#include <sstream>
 #include <set>
 #include <string>
 #include <vector>
 
 #include "apps/app_common.h"
 #include "engine/allocator.h"
+#include "engine/autograd.h"
+#include "engine/nn.h"
 #include "engine/comm.h"
 #include "engine/gemm.h"
 #include "engine/gemma3.h"
@@ -42,7 +60,8 @@ const char* kProg = "train_lora_gemma";
 
 const std::set<std::string> kBool = {"random_init", "synthetic_data", "no_graph", "compat_l2_adam", "deterministic",
                                      "interleaved_rope", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
-                                     "shard_enable", "bf16_grads", "no_overlap", "help"};
+                                     "activation_checkpointing", "shard_enable", "bf16_grads", "no_overlap", "help", "align_dump_grads",
+                                     "align_do_step", "align_disable_debug", "align_no_retain_grad", "align_numeric_attn"};
 const std::set<std::string> kValued = {
     "model_dir", "data_dir", "pretokenized_path", "pretokenized_meta", "output_dir", "targets", "lora_targets",
     "epochs", "max_steps", "seq_len", "batch", "grad_accum", "lr", "learning_rate", "rank", "lora_r", "alpha",
@@ -50,7 +69,9 @@ const std::set<std::string> kValued = {
     "data_fraction", "log_interval", "eval_steps", "eval_batches", "save_every", "seed", "model", "synthetic_tokens",
     "resume_from", "state_dir", "inject_fault", "metrics_out", "eval_out", "pm_interval", "pm_batt_thresh", "pm_temp_thresh", "pm_fb_high",
     "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "device",
-    "shard_budget_mb", "shard_dir", "shard_fp16_disk", "bench_steps", "bench_warmup", "zero_stage", "offload", "bucket_mb"};
+    "shard_budget_mb", "shard_dir", "shard_fp16_disk", "bench_steps", "bench_warmup", "zero_stage", "offload", "bucket_mb",
+    "align_dump_dir", "align_layers", "align_pt_weights_dir", "align_numeric_eps", "align_numeric_count",
+    "align_numeric_targets", "dump_grads"};
 
 // first present of several alias flags
 std::string pick(const Args& a, std::initializer_list<const char*> keys, const std::string& d) {
@@ -81,6 +102,225 @@ void usage() {
       kProg);
 }
 
+// ---------------------------------------------------------------- alignment harness
+bool flag_on(const Args& a, const char* k, bool d) {
+  if (!a.kv.count(k)) return a.flags.count(k) ? true : d;
+  const std::string v = a.kv.at(k);
+  return !(v == "0" || v == "false" || v == "False");
+}
+
+// "layer.3.attn.q" -> "layers_3_self_attn_q_proj" (the PEFT module path, '.' -> '_')
+std::string peft_stem(const std::string& name) {
+  const size_t d1 = name.find('.', 6);
+  const std::string li = name.substr(6, d1 - 6), part = name.substr(d1 + 1);
+  static const std::map<std::string, std::string> m = {
+      {"attn.q", "self_attn_q_proj"}, {"attn.k", "self_attn_k_proj"}, {"attn.v", "self_attn_v_proj"},
+      {"attn.proj", "self_attn_o_proj"}, {"mlp.gate", "mlp_gate_proj"}, {"mlp.up", "mlp_up_proj"},
+      {"mlp.down", "mlp_down_proj"}};
+  auto it = m.find(part);
+  return "layers_" + li + "_" + (it == m.end() ? part : it->second);
+}
+
+// "<stem>_lora_A_default_weight" for a trainable "layer.i.<part>.lora_A"
+std::string ref_key(const std::string& name) {
+  const bool isA = name.substr(name.size() - 7) == ".lora_A";
+  return "base_model_model_model_" + peft_stem(name.substr(0, name.size() - 7)) + (isA ? "_lora_A" : "_lora_B") +
+         "_default_weight";
+}
+
+int layer_of(const std::string& name) { return std::stoi(name.substr(6, name.find('.', 6) - 6)); }
+
+// a LoRA tensor in the reference's layout: A [r, in] -> [in, r], B [r, out] as is
+void dump_lora_tensor(const std::string& path, const std::string& name, const Tensor& t) {
+  const bool isA = name.substr(name.size() - 7) == ".lora_A";
+  Tensor src = isA ? t.t() : t;
+  Tensor h = empty(src.shape(), DType::F32, Device::cpu());
+  h.copy_(src);
+  mft::apps::save_npy(path, h.data_ptr(), h.shape(), "<f4", 4);
+}
+
+// minimal float32 .npy reader (C order, v1/v2 header)
+bool load_npy_f32(const std::string& path, std::vector<int64_t>& shape, std::vector<float>& data) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  char magic[8];
+  f.read(magic, 8);
+  if (!f || std::memcmp(magic, "\x93NUMPY", 6) != 0) return false;
+  uint32_t hl = 0;
+  if (magic[6] == 1) {
+    unsigned char b[2];
+    f.read((char*)b, 2);
+    hl = b[0] | (b[1] << 8);
+  } else {
+    unsigned char b[4];
+    f.read((char*)b, 4);
+    hl = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+  }
+  std::string hdr(hl, ' ');
+  f.read(&hdr[0], hl);
+  if (hdr.find("'<f4'") == std::string::npos || hdr.find("'fortran_order': True") != std::string::npos) return false;
+  const size_t l = hdr.find('(', hdr.find("'shape'")), r = hdr.find(')', l);
+  shape.clear();
+  std::stringstream ss(hdr.substr(l + 1, r - l - 1));
+  std::string tok;
+  size_t n = 1;
+  while (std::getline(ss, tok, ','))
+    if (tok.find_first_of("0123456789") != std::string::npos) {
+      shape.push_back(std::stoll(tok));
+      n *= (size_t)shape.back();
+    }
+  data.resize(n);
+  f.read((char*)data.data(), (std::streamsize)(n * 4));
+  return (bool)f;
+}
+
+int alignment_mode(const Args& a, Gemma3& model, FlatParams& flat, TokenDataset& train, AdamWConfig oc, int S) {
+  const std::string d = a.get("align_dump_dir");
+  std::filesystem::create_directories(d);
+  std::vector<int> layers;
+  {
+    std::stringstream ss(a.get("align_layers", "0,1,17"));
+    std::string t;
+    while (std::getline(ss, t, ','))
+      if (!t.empty() && std::stoi(t) < model.cfg().n_layer) layers.push_back(std::stoi(t));
+  }
+  std::string ls;
+  for (int l : layers) ls += (ls.empty() ? "" : ",") + std::to_string(l);
+  std::printf("[Align] align_layers=%s\n", ls.c_str());
+  auto in_layers = [&](const std::string& name) {
+    return std::find(layers.begin(), layers.end(), layer_of(name)) != layers.end();
+  };
+  // optional: initial adapters from a PyTorch dump (either orientation)
+  const std::string ptw = a.get("align_pt_weights_dir");
+  if (!ptw.empty()) {
+    NoGradGuard ng;
+    int loaded = 0;
+    for (auto& kv : flat.params) {
+      const std::string fn = ptw + "/weights_after_step/" + ref_key(kv.first) + ".npy";
+      std::vector<int64_t> shp;
+      std::vector<float> v;
+      if (!std::filesystem::exists(fn) || !load_npy_f32(fn, shp, v)) continue;
+      Tensor leaf = kv.second->leaf;
+      Tensor h = from_blob(v.data(), shp, DType::F32, Device::cpu());
+      if (shp.size() == 2 && shp[0] == leaf.size(1) && shp[1] == leaf.size(0) && shp[0] != shp[1]) h = h.t();
+      MFT_CHECK(h.numel() == leaf.numel() && h.size(0) == leaf.size(0), "align_pt_weights_dir: ", fn, " has shape ",
+                shape_str(shp), ", the adapter is ", leaf.str());
+      Tensor c = empty(leaf.shape(), DType::F32, Device::cpu());
+      c.copy_(h);
+      leaf.copy_(c);
+      ++loaded;
+    }
+    flat.refresh_shadow();
+    synchronize();
+    std::printf("[Align] %d adapter tensors loaded from %s\n", loaded, ptw.c_str());
+  }
+  // the fixed batch: the first chunks of the train split
+  const int B = std::max(1, std::min<int>(a.i("batch", 4), (int)train.num_sequences()));
+  std::vector<size_t> idx(B);
+  for (int i = 0; i < B; ++i) idx[i] = (size_t)i;
+  std::vector<int64_t> hid((size_t)B * S), htg((size_t)B * S);
+  std::vector<float> mk((size_t)B * S);
+  train.get_batch(idx.data(), B, hid.data(), htg.data(), mk.data(), nullptr);
+  {
+    std::vector<int32_t> i32(hid.begin(), hid.end()), t32(htg.begin(), htg.end());
+    mft::apps::save_npy(d + "/input_ids.npy", i32.data(), {B, S}, "<i4", 4);
+    mft::apps::save_npy(d + "/labels.npy", t32.data(), {B, S}, "<i4", 4);  // next-token targets, -100 ignored
+    mft::apps::save_npy(d + "/attention_mask.npy", mk.data(), {B, S}, "<f4", 4);
+  }
+  Tensor ids = from_host(hid.data(), {B, S}, DType::I64), tg = from_host(htg.data(), {B, S}, DType::I64);
+  model.training = true;
+  model.capture_layers = layers;
+  Tensor loss = model.loss(ids, tg, 1.f);
+  model.capture_layers.clear();
+  const float lv = (float)loss.item();
+  mft::apps::save_npy_f32(d + "/loss_scalar.npy", {lv}, {1});
+  for (auto& kv : model.captured)
+    mft::apps::save_npy_f32(d + "/layer" + std::to_string(kv.first) + "_mlp_out.npy", kv.second.to_vector_f32(),
+                            {B, S, model.cfg().hidden});
+  {
+    NoGradGuard ng;
+    Tensor h = model.hidden(ids);
+    Tensor rows = lm_head_token_nll(h, model.output_embedding(), tg, model.vocab(), model.ce_chunk);
+    mft::apps::save_npy_f32(d + "/per_token_nll.npy", rows.to_vector_f32(), {B, S});
+  }
+  std::printf("[Align] loss=%.6f (%s)\n", lv, model.loss_sum ? "sum" : "mean");
+  const bool dump_grads = flag_on(a, "align_dump_grads", true), do_step = flag_on(a, "align_do_step", true);
+  if (dump_grads || do_step || flag_on(a, "align_numeric_attn", false)) {
+    flat.zero_grad();
+    backward({loss});
+    synchronize();
+  }
+  if (dump_grads) {
+    int n = 0;
+    for (auto& kv : flat.params)
+      if (in_layers(kv.first)) {
+        dump_lora_tensor(d + "/grads/" + ref_key(kv.first) + ".npy", kv.first, kv.second->leaf.grad());
+        ++n;
+      }
+    std::printf("[Align] %d LoRA gradients dumped\n", n);
+  }
+  if (flag_on(a, "align_numeric_attn", false)) {
+    // central differences on the largest-|grad| element of each attention adapter in the layers
+    const float eps = a.f("align_numeric_eps", 1e-3f);
+    const int count = a.i("align_numeric_count", 4);
+    std::vector<std::string> tgs;
+    {
+      std::stringstream ss(a.get("align_numeric_targets", "q,v"));
+      std::string t;
+      while (std::getline(ss, t, ','))
+        if (!t.empty()) tgs.push_back(".attn." + std::string(t == "o" ? "proj" : t) + ".lora_");
+    }
+    model.training = false;  // (dropout is off anyway; deterministic forward)
+    std::vector<float> ana, num;
+    int checked = 0;
+    for (auto& kv : flat.params) {
+      if (checked >= count || !in_layers(kv.first)) continue;
+      bool hit = false;
+      for (auto& t : tgs) hit = hit || kv.first.find(t) != std::string::npos;
+      if (!hit) continue;
+      Tensor leaf = kv.second->leaf;
+      const std::vector<float> g = leaf.grad().to_vector_f32(), w = leaf.to_vector_f32();
+      size_t i = 0;
+      for (size_t j = 1; j < g.size(); ++j)
+        if (std::fabs(g[j]) > std::fabs(g[i])) i = j;
+      auto loss_at = [&](float val) {
+        NoGradGuard ng;
+        float hv = val;
+        leaf.view({-1}).slice(0, (int64_t)i, (int64_t)i + 1).copy_(from_blob(&hv, {1}, DType::F32, Device::cpu()));
+        flat.refresh_shadow();
+        return model.loss(ids, tg, 1.f).item();
+      };
+      const double lp = loss_at(w[i] + eps), lm = loss_at(w[i] - eps);
+      loss_at(w[i]);
+      const double nd = (lp - lm) / (2.0 * eps);
+      std::printf("[Align] %s[%zu] analytic=%.6e numeric=%.6e rel=%.3e\n", kv.first.c_str(), i, g[i], nd,
+                  std::fabs(g[i] - nd) / std::max(std::fabs(nd), 1e-12));
+      ana.push_back(g[i]);
+      num.push_back((float)nd);
+      ++checked;
+    }
+    mft::apps::save_npy_f32(d + "/numeric/lora_numeric_grad.npy", num, {(int64_t)num.size()});
+    mft::apps::save_npy_f32(d + "/numeric/lora_analytic_grad.npy", ana, {(int64_t)ana.size()});
+    model.training = true;
+  }
+  if (do_step) {
+    oc.weight_decay = 0.f;  // reference: single AdamW step, wd 0
+    AdamW opt(flat, oc);
+    opt.set_lr(oc.lr);
+    opt.step();
+    synchronize();
+    int n = 0;
+    for (auto& kv : flat.params)
+      if (in_layers(kv.first)) {
+        dump_lora_tensor(d + "/weights_after_step/" + ref_key(kv.first) + ".npy", kv.first, kv.second->leaf.detach());
+        ++n;
+      }
+    std::printf("[Align] one AdamW step (grad_norm=%.6f), %d adapter tensors dumped\n", opt.grad_norm(), n);
+  }
+  std::printf("[AlignDump] wrote activations and loss to %s\n", d.c_str());
+  return 0;
+}
+
 int run(int argc, char** argv) {
   Args a = mft::apps::parse_args(argc, argv, kBool, kValued, /*lenient=*/true);
   if (a.b("help")) {
@@ -92,8 +332,9 @@ int run(int argc, char** argv) {
     for (auto& u : a.unknown) std::printf(" %s", u.c_str());
     std::printf("\n");
   }
-  if (a.get("loss_reduction", "mean") != "mean")
-    throw std::runtime_error("--loss_reduction sum: the native engine trains on the mean token loss");
+  const std::string red = a.get("loss_reduction", "mean");
+  if (red != "mean" && red != "sum" && red != "sum_debug")
+    throw std::runtime_error("--loss_reduction mean|sum|sum_debug (got '" + red + "')");
   if (a.b("deterministic")) set_deterministic(true);
   const DistConfig dcfg = mft::apps::dist_config_from(a);
   if (dcfg.zero_stage == 3)  // the adapters are the only trainable tensors: nothing for ZeRO-3 to partition
@@ -119,6 +360,8 @@ int run(int argc, char** argv) {
               cfg.n_head, cfg.n_kv, cfg.head_dim, cfg.vocab_size);
   auto model = std::make_unique<Gemma3>(cfg);
   model->interleaved_rope = a.b("interleaved_rope");
+  model->grad_checkpoint = a.b("activation_checkpointing");  // recompute blocks in the backward
+  model->loss_sum = red != "mean";
   if (random_init) {
     model->init_random(1234);
     std::printf("  random-initialised weights\n");
@@ -135,7 +378,7 @@ int run(int argc, char** argv) {
     GemmaLoraSpec spec;
     spec.rank = std::stoi(pick(a, {"rank", "lora_r"}, "8"));
     spec.alpha = std::stof(pick(a, {"alpha", "lora_alpha"}, "32"));
-    spec.dropout = a.f("lora_dropout", 0.1f);
+    spec.dropout = a.get("align_dump_dir").empty() ? a.f("lora_dropout", 0.1f) : 0.f;  // alignment: no dropout
     spec.targets = GemmaLoraSpec::parse_targets(a.kv.count("lora_targets") ? a.get("lora_targets") : a.get("targets", "full"));
     spec.seed = 42;
     model->inject_lora(spec);
@@ -184,6 +427,17 @@ int run(int argc, char** argv) {
   oc.weight_decay = a.f("weight_decay", 0.f);
   oc.max_grad_norm = a.f("max_grad_norm", 1.f);
   oc.l2_coupled = a.b("compat_l2_adam");
+  if (!a.get("dump_grads").empty()) {  // parity tests: one fwd+bwd, gradients in the adapter layout
+    MFT_CHECK(!comm, "--dump_grads runs on one process");
+    const float lv = mft::apps::grads_into_masters(*model, flat, train, a.i("batch", 4), dc.seq_len);
+    model->save_lora(a.get("dump_grads"));
+    std::printf("MFT_DUMP loss=%.8f path=%s\n", lv, a.get("dump_grads").c_str());
+    return 0;
+  }
+  if (!a.get("align_dump_dir").empty()) {
+    if (comm) throw std::runtime_error("--align_dump_dir runs on one process");
+    return alignment_mode(a, *model, flat, train, oc, dc.seq_len);
+  }
   AdamW opt(flat, oc);
   ds.make_dp(comm.get(), opt, dcfg);
   TrainConfig tc;

@@ -33,8 +33,9 @@ bool any_needs_grad(const std::vector<Tensor>& ts) {
   return false;
 }
 
-bool connect(const std::shared_ptr<Node>& node, const std::vector<Tensor>& inputs, const std::vector<Tensor>& outputs) {
-  if (!any_needs_grad(inputs)) return false;
+bool connect(const std::shared_ptr<Node>& node, const std::vector<Tensor>& inputs, const std::vector<Tensor>& outputs,
+             bool force) {
+  if (!(force ? t_grad : any_needs_grad(inputs))) return false;
   node->seq = ++g_seq;
   node->next.clear();
   for (auto& in : inputs) {
@@ -121,6 +122,54 @@ void accumulate_grad(TensorImpl* t, const Tensor& g, float alpha) {
 }
 
 void accumulate_grad(const Tensor& t, const Tensor& g, float alpha) { accumulate_grad(t.impl(), g, alpha); }
+
+// ------------------------------------------------------------------ activation checkpointing
+std::vector<Tensor> checkpoint(CheckpointFn fn, const std::vector<Tensor>& inputs) {
+  if (!t_grad) return fn(inputs);
+  std::vector<Tensor> saved;
+  std::vector<char> need;
+  for (auto& t : inputs) {
+    saved.push_back(t.defined() ? t.detach() : Tensor());
+    need.push_back(t.defined() && t.requires_grad());
+  }
+  std::vector<Tensor> outs;
+  {
+    NoGradGuard ng;
+    outs = fn(saved);
+  }
+  auto n = lambda_node("CheckpointBackward", [fn, saved, need](std::vector<Tensor>& g) {
+    std::vector<Tensor> xin;
+    for (size_t i = 0; i < saved.size(); ++i) {
+      Tensor t = saved[i].defined() ? saved[i].alias() : Tensor();
+      if (need[i]) {
+        t.requires_grad_(true);
+        t.set_grad(zeros(t.shape(), t.dtype(), t.device()));  // same dtype as the forward's tensor
+      }
+      xin.push_back(t);
+    }
+    std::vector<Tensor> re;
+    {
+      const bool prev = grad_enabled();
+      set_grad_enabled(true);
+      re = fn(xin);
+      set_grad_enabled(prev);
+    }
+    std::vector<Tensor> roots, seeds;
+    for (size_t k = 0; k < re.size() && k < g.size(); ++k)
+      if (g[k].defined() && re[k].defined() && re[k].requires_grad()) {
+        roots.push_back(re[k]);
+        seeds.push_back(g[k]);
+      }
+    if (!roots.empty()) backward(roots, seeds);
+    std::vector<Tensor> res;
+    for (size_t i = 0; i < xin.size(); ++i) res.push_back(need[i] ? xin[i].grad() : Tensor());
+    return res;
+  });
+  std::vector<Tensor> alias_outs;
+  for (auto& o : outs) alias_outs.push_back(o.defined() ? o.alias() : Tensor());
+  connect(n, inputs, alias_outs, /*force=*/true);
+  return alias_outs;
+}
 
 // ------------------------------------------------------------------ views
 namespace {

@@ -70,7 +70,8 @@ bool any_needs_grad(const std::vector<Tensor>& ts);
 // Wire `node` to the differentiable `inputs` (one edge slot per input, in order) and make every
 // output require grad with this node as grad_fn.  Returns false (node dropped) when no input needs
 // a gradient or grad mode is off.
-bool connect(const std::shared_ptr<Node>& node, const std::vector<Tensor>& inputs, const std::vector<Tensor>& outputs);
+bool connect(const std::shared_ptr<Node>& node, const std::vector<Tensor>& inputs, const std::vector<Tensor>& outputs,
+             bool force = false);  // force: record the node even when no input needs a gradient
 
 // g accumulated (+=, with dtype cast) into leaf t's gradient, allocated zero-filled on first use
 // unless a gradient buffer was installed (set_grad with a view into a flat buffer).
@@ -89,6 +90,15 @@ void backward(const std::vector<Tensor>& roots, const std::vector<Tensor>& grads
 // in's shape; `full` = the view covers every element of `in`, so no zero fill is needed)
 void record_view(const Tensor& in, const Tensor& out, std::function<Tensor(const Tensor&)> reapply,
                  std::function<Tensor(const Tensor&)> inverse, bool full);
+
+// Activation checkpointing (the Python models use torch.utils.checkpoint): fn(inputs)
+// runs WITHOUT recording and only the inputs are kept; the backward re-runs fn from them with
+// recording on and back-propagates the incoming gradients through that recomputed graph (a nested
+// backward: the parameters' gradients accumulate and their grad-ready hooks fire there), returning
+// the inputs' gradients.  fn must be a pure function of its inputs and state that does not change
+// before the backward (weights; the LoRA-dropout counter) -- it is called twice.
+using CheckpointFn = std::function<std::vector<Tensor>(const std::vector<Tensor>&)>;
+std::vector<Tensor> checkpoint(CheckpointFn fn, const std::vector<Tensor>& inputs);
 
 // Node built from lambdas (for simple ops)
 struct LambdaNode : Node {

@@ -275,9 +275,12 @@ void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
   MFT_CHECK(buf.dtype() == DType::F32 && buf.is_contiguous(), "gemm_wgrad: fp32 contiguous grad buffer");
   const long M = dy2.size(0), N = dy2.size(1), K = x2.size(1);
   MFT_CHECK(x2.size(0) == M && buf.numel() == N * K, "gemm_wgrad: shapes");
-  // (gemm8 split-K wins small outputs in isolation but loses inside the full-FT step: opt-in only)
-  const bool small = N * K <= 2304L * 768L && std::getenv("MFT_G8_SMALL_WGRAD") && std::getenv("MFT_G8_SMALL_WGRAD")[0] == '1';
-  if ((deterministic() || gemm8_all() || small) && M % 64 == 0 && N % 8 == 0 && K % 8 == 0 && dy2.stride(0) % 8 == 0 &&
+  // gemm8 (F32ACC epilogue straight into the flat grad, split-K over the tokens when the output
+  // alone does not fill the CUs) by default: 0.9-1.1 PF/s on the GPT-2 shapes, 0.65-0.77 on XL's,
+  // vs hipBLASLt's fp32-out kernels at 0.42-0.95 (profiles/r3_wgrad_shapes.txt);
+  // MFT_WGRAD=lt routes to hipBLASLt (A/B)
+  static const bool lt_wgrad = std::getenv("MFT_WGRAD") && std::string(std::getenv("MFT_WGRAD")) == "lt";
+  if ((deterministic() || gemm8_all() || !lt_wgrad) && M % 64 == 0 && N % 8 == 0 && K % 8 == 0 && dy2.stride(0) % 8 == 0 &&
       x2.stride(0) % 8 == 0 && ::mft::gemm8_supported((int)N, (int)K, (int)M, true, true)) {
     ::mft::GemmArgs g{};
     g.A = (const ::mft::bf16_t*)dy2.data_ptr();

@@ -458,8 +458,7 @@ std::pair<Tensor, Tensor> Gemma3::rope(bool local, int S) {
   return t;
 }
 
-Tensor Gemma3::hidden(const Tensor& ids) {
-  const int64_t B = ids.size(0), S = ids.size(1);
+std::pair<Tensor, Tensor> Gemma3::layer(int i, const Tensor& x0, const Tensor& h, int64_t B, int64_t S) {
   const int H = cfg_.hidden, D = cfg_.head_dim, nq = cfg_.n_head, nkv = cfg_.n_kv, I = cfg_.intermediate;
   const float s = spec_.scale(), eps = cfg_.eps;
   const float attn_scale = 1.f / std::sqrt(cfg_.query_pre_attn_scalar);
@@ -471,33 +470,54 @@ Tensor Gemma3::hidden(const Tensor& ids) {
     if (st) return lora_linear(x, w, nullptr, ads, s, training, dropout_ctr);
     return lora_linear_aug(x, K, w, nullptr, ads, s, waug, training, dropout_ctr);
   };
-  auto gl = rope(false, (int)S), lc = rope(true, (int)S);
+  auto& L = layers_[i];
+  const auto cs = rope(L.sliding, (int)S);
+  Tensor x = x0;
+  // attention
+  Tensor qkv = proj(h, H, L.qkv_w, active(L.lqkv), L.waug_qkv).view({B, S, nq + 2 * nkv, D});
+  Tensor o = qknorm_rope_attention(qkv, nq, nkv, L.q_norm, L.k_norm, cs.first, cs.second, eps, 1.f,
+                                   interleaved_rope, attn_scale, L.sliding ? cfg_.sliding_window : 0,
+                                   aug(active(L.lo), nq * D));
+  o = o.view({B * S, o.size(-1)});
+  Tensor a = proj(o, nq * D, L.o_w, active(L.lo), L.waug_o);
+  a = add_norm(a, Tensor(), L.post_attn_norm, nullptr, eps, true, 1.f, 0).second;
+  auto r = add_norm(x, a, L.pre_ff_norm, nullptr, eps, true, 1.f, aug(active(L.lgu), H));
+  x = r.first;
+  // GeGLU MLP
+  Tensor gu = proj(r.second, H, L.gu_w, active(L.lgu), L.waug_gu);
+  Tensor g = gated_act(gu, cfg_.act, aug(active(L.ldown), I));
+  Tensor f = proj(g, I, L.down_w, active(L.ldown), L.waug_down);
+  f = add_norm(f, Tensor(), L.post_ff_norm, nullptr, eps, true, 1.f, 0).second;
+  if (!capture_layers.empty() && std::find(capture_layers.begin(), capture_layers.end(), i) != capture_layers.end()) {
+    NoGradGuard ng;
+    captured[i] = f.detach().clone();
+  }
+  Param& nw = i + 1 < cfg_.n_layer ? layers_[i + 1].in_norm : final_norm_;
+  const int oc = i + 1 < cfg_.n_layer ? aug(active(layers_[i + 1].lqkv), H) : 0;
+  return add_norm(x, f, nw, nullptr, eps, true, 1.f, oc);
+}
+
+Tensor Gemma3::hidden(const Tensor& ids) {
+  const int64_t B = ids.size(0), S = ids.size(1);
+  const int H = cfg_.hidden;
+  const bool st = streamer_ != nullptr;
+  rope(false, (int)S), rope(true, (int)S);  // tables before any capture / checkpoint
   Tensor x = embed(ids, embed_, nullptr, embed_scale_);
-  Tensor h = add_norm(x, Tensor(), layers_[0].in_norm, nullptr, eps, true, 1.f, aug(active(layers_[0].lqkv), H)).second;
+  const int oc0 = (active(layers_[0].lqkv).empty() || st) ? 0 : lora_aug_cols(H, active(layers_[0].lqkv));
+  Tensor h = add_norm(x, Tensor(), layers_[0].in_norm, nullptr, cfg_.eps, true, 1.f, oc0).second;
+  const bool ckpt = grad_checkpoint && training && grad_enabled();
   for (int i = 0; i < cfg_.n_layer; ++i) {
-    auto& L = layers_[i];
-    const auto& cs = L.sliding ? lc : gl;
     if (st) streamer_->ensure(i, i + 1);
-    // attention
-    Tensor qkv = proj(h, H, L.qkv_w, active(L.lqkv), L.waug_qkv).view({B, S, nq + 2 * nkv, D});
-    Tensor o = qknorm_rope_attention(qkv, nq, nkv, L.q_norm, L.k_norm, cs.first, cs.second, eps, 1.f,
-                                     interleaved_rope, attn_scale, L.sliding ? cfg_.sliding_window : 0,
-                                     aug(active(L.lo), nq * D));
-    o = o.view({B * S, o.size(-1)});
-    Tensor a = proj(o, nq * D, L.o_w, active(L.lo), L.waug_o);
-    a = add_norm(a, Tensor(), L.post_attn_norm, nullptr, eps, true, 1.f, 0).second;
-    auto r = add_norm(x, a, L.pre_ff_norm, nullptr, eps, true, 1.f, aug(active(L.lgu), H));
-    x = r.first;
-    // GeGLU MLP
-    Tensor gu = proj(r.second, H, L.gu_w, active(L.lgu), L.waug_gu);
-    Tensor g = gated_act(gu, cfg_.act, aug(active(L.ldown), I));
-    Tensor f = proj(g, I, L.down_w, active(L.ldown), L.waug_down);
-    f = add_norm(f, Tensor(), L.post_ff_norm, nullptr, eps, true, 1.f, 0).second;
-    Param& nw = i + 1 < cfg_.n_layer ? layers_[i + 1].in_norm : final_norm_;
-    const int oc = i + 1 < cfg_.n_layer ? aug(active(layers_[i + 1].lqkv), H) : 0;
-    auto r1 = add_norm(x, f, nw, nullptr, eps, true, 1.f, oc);
-    x = r1.first;
-    h = r1.second;
+    if (ckpt) {
+      auto o = checkpoint([this, i, B, S](const std::vector<Tensor>& in) {
+        auto r = layer(i, in[0], in[1], B, S);
+        return std::vector<Tensor>{r.first, r.second};
+      }, {x, h});
+      x = o[0];
+      h = o[1];
+    } else {
+      std::tie(x, h) = layer(i, x, h, B, S);
+    }
     if (st) std::tie(x, h) = streamer_->gate(x, h, i);
   }
   return h;
@@ -505,7 +525,7 @@ Tensor Gemma3::hidden(const Tensor& ids) {
 
 Tensor Gemma3::loss(const Tensor& ids, const Tensor& labels, float w_grad_scale) {
   Tensor h = hidden(ids);
-  return lm_head_ce(h, embed_, labels, cfg_.vocab_size, ce_chunk, w_grad_scale);
+  return lm_head_ce(h, embed_, labels, cfg_.vocab_size, ce_chunk, w_grad_scale, loss_sum);
 }
 
 std::pair<Tensor, Tensor> Gemma3::nll(const Tensor& ids, const Tensor& labels) {

@@ -84,6 +84,8 @@ class Gemma3 : public LanguageModel {
  private:
   void alloc();
   std::pair<Tensor, Tensor> rope(bool local, int S);
+  // decoder layer i: (residual x, normed h) -> (x, h normed for the next layer)
+  std::pair<Tensor, Tensor> layer(int i, const Tensor& x, const Tensor& h, int64_t B, int64_t S);
   Gemma3Config cfg_;
   GemmaLoraSpec spec_;
   Param embed_, final_norm_;

@@ -451,51 +451,66 @@ void GPT2::enable_weight_streaming(size_t budget_bytes) {
 }
 
 // ------------------------------------------------------------------ forward
-Tensor GPT2::hidden(const Tensor& ids) {
-  const int64_t B = ids.size(0), S = ids.size(1);
-  MFT_CHECK(S <= cfg_.n_positions, "sequence ", S, " exceeds n_positions ", cfg_.n_positions);
+std::pair<Tensor, Tensor> GPT2::block(int i, const Tensor& x0, const Tensor& h, int64_t B, int64_t S) {
   const int C = cfg_.n_embd, H = cfg_.n_head, D = cfg_.head_dim();
   const float scale = spec_.scale();
   // streamed weights: no resident augmented-K copy [W | s B^T], the adapters run beside the GEMM
   const bool st = streamer_ != nullptr;
+  auto aug = [&](std::vector<LoraAdapter>& ads) { return (ads.empty() || st) ? 0 : lora_aug_cols(C, ads); };
+  auto& b = blocks_[i];
+  Tensor x = x0;
+  // attention
+  Tensor qkv = active(b.lqkv).empty() ? linear_p(h, b.attn_w, &b.attn_b)
+               : st ? lora_linear(h, b.attn_w, &b.attn_b, active(b.lqkv), scale, training, dropout_ctr)
+                    : lora_linear_aug(h, C, b.attn_w, &b.attn_b, active(b.lqkv), scale, b.waug_qkv, training, dropout_ctr);
+  Tensor o = attention_packed(qkv.view({B, S, 3, H, D}), 1.f / std::sqrt((float)D), true, 0, aug(active(b.lproj)));
+  o = o.view({B * S, o.size(-1)});
+  Tensor a = active(b.lproj).empty() ? linear_p(o, b.proj_w, &b.proj_b)
+             : st ? lora_linear(o, b.proj_w, &b.proj_b, active(b.lproj), scale, training, dropout_ctr)
+                  : lora_linear_aug(o, C, b.proj_w, &b.proj_b, active(b.lproj), scale, b.waug_proj, training, dropout_ctr);
+  auto r2 = add_norm(x, a, b.ln2_w, &b.ln2_b, cfg_.eps, false, 0.f, 0);
+  x = r2.first;
+  // MLP
+  Tensor f;
+  if (active(b.lfc).empty() && active(b.lfcout).empty()) {
+    f = mlp_gelu(r2.second, b.fc_w, b.fc_b, b.mproj_w, b.mproj_b);
+  } else {
+    Tensor u = active(b.lfc).empty() ? linear_p(r2.second, b.fc_w, &b.fc_b)
+                             : lora_linear(r2.second, b.fc_w, &b.fc_b, active(b.lfc), scale, training, dropout_ctr);
+    u = gelu(u, true);
+    f = active(b.lfcout).empty() ? linear_p(u, b.mproj_w, &b.mproj_b)
+                         : lora_linear(u, b.mproj_w, &b.mproj_b, active(b.lfcout), scale, training, dropout_ctr);
+  }
+  Param* nw = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_w : &lnf_w_;
+  Param* nb = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_b : &lnf_b_;
+  const int oc = i + 1 < cfg_.n_layer ? aug(active(blocks_[i + 1].lqkv)) : 0;
+  return add_norm(x, f, *nw, nb, cfg_.eps, false, 0.f, oc);
+}
+
+Tensor GPT2::hidden(const Tensor& ids) {
+  const int64_t B = ids.size(0), S = ids.size(1);
+  MFT_CHECK(S <= cfg_.n_positions, "sequence ", S, " exceeds n_positions ", cfg_.n_positions);
+  const int C = cfg_.n_embd;
+  const bool st = streamer_ != nullptr;
   // block weights that are not resident: the host-streaming tier or the ZeRO-3 partitioner
   BlockProvider* bp = st ? streamer_.get() : provider_;
-  auto aug = [&](std::vector<LoraAdapter>& ads) { return (ads.empty() || st) ? 0 : lora_aug_cols(C, ads); };
   if (bp) bp->begin_forward();
   Tensor x = embed(ids, wte_, &wpe_, 1.f);
-  auto n0 = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, aug(active(blocks_[0].lqkv)));
-  Tensor h = n0.second;
+  const int oc0 = (active(blocks_[0].lqkv).empty() || st) ? 0 : lora_aug_cols(C, active(blocks_[0].lqkv));
+  Tensor h = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, oc0).second;
+  const bool ckpt = grad_checkpoint && training && grad_enabled();
   for (int i = 0; i < cfg_.n_layer; ++i) {
-    auto& b = blocks_[i];
-    // attention
     if (bp) bp->ensure(i, i + 1);
-    Tensor qkv = active(b.lqkv).empty() ? linear_p(h, b.attn_w, &b.attn_b)
-                 : st ? lora_linear(h, b.attn_w, &b.attn_b, active(b.lqkv), scale, training, dropout_ctr)
-                      : lora_linear_aug(h, C, b.attn_w, &b.attn_b, active(b.lqkv), scale, b.waug_qkv, training, dropout_ctr);
-    Tensor o = attention_packed(qkv.view({B, S, 3, H, D}), 1.f / std::sqrt((float)D), true, 0, aug(active(b.lproj)));
-    o = o.view({B * S, o.size(-1)});
-    Tensor a = active(b.lproj).empty() ? linear_p(o, b.proj_w, &b.proj_b)
-               : st ? lora_linear(o, b.proj_w, &b.proj_b, active(b.lproj), scale, training, dropout_ctr)
-                    : lora_linear_aug(o, C, b.proj_w, &b.proj_b, active(b.lproj), scale, b.waug_proj, training, dropout_ctr);
-    auto r2 = add_norm(x, a, b.ln2_w, &b.ln2_b, cfg_.eps, false, 0.f, 0);
-    x = r2.first;
-    // MLP
-    Tensor f;
-    if (active(b.lfc).empty() && active(b.lfcout).empty()) {
-      f = mlp_gelu(r2.second, b.fc_w, b.fc_b, b.mproj_w, b.mproj_b);
+    if (ckpt) {
+      auto o = checkpoint([this, i, B, S](const std::vector<Tensor>& in) {
+        auto r = block(i, in[0], in[1], B, S);
+        return std::vector<Tensor>{r.first, r.second};
+      }, {x, h});
+      x = o[0];
+      h = o[1];
     } else {
-      Tensor u = active(b.lfc).empty() ? linear_p(r2.second, b.fc_w, &b.fc_b)
-                               : lora_linear(r2.second, b.fc_w, &b.fc_b, active(b.lfc), scale, training, dropout_ctr);
-      u = gelu(u, true);
-      f = active(b.lfcout).empty() ? linear_p(u, b.mproj_w, &b.mproj_b)
-                           : lora_linear(u, b.mproj_w, &b.mproj_b, active(b.lfcout), scale, training, dropout_ctr);
+      std::tie(x, h) = block(i, x, h, B, S);
     }
-    Param* nw = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_w : &lnf_w_;
-    Param* nb = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_b : &lnf_b_;
-    const int oc = i + 1 < cfg_.n_layer ? aug(active(blocks_[i + 1].lqkv)) : 0;
-    auto r1 = add_norm(x, f, *nw, nb, cfg_.eps, false, 0.f, oc);
-    x = r1.first;
-    h = r1.second;
     if (bp) std::tie(x, h) = bp->gate(x, h, i);
   }
   return h;
@@ -503,7 +518,7 @@ Tensor GPT2::hidden(const Tensor& ids) {
 
 Tensor GPT2::loss(const Tensor& ids, const Tensor& labels, float w_grad_scale) {
   Tensor h = hidden(ids);
-  return lm_head_ce(h, wte_, labels, cfg_.vocab_size, ce_chunk, w_grad_scale);
+  return lm_head_ce(h, wte_, labels, cfg_.vocab_size, ce_chunk, w_grad_scale, loss_sum);
 }
 
 std::pair<Tensor, Tensor> GPT2::nll(const Tensor& ids, const Tensor& labels) {

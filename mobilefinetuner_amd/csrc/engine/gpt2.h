@@ -85,6 +85,8 @@ class GPT2 : public LanguageModel {
 
  private:
   void alloc();
+  // transformer block i: (residual x, normed h) -> (x, h normed for the next block)
+  std::pair<Tensor, Tensor> block(int i, const Tensor& x, const Tensor& h, int64_t B, int64_t S);
   GPT2Config cfg_;
   LoraSpec spec_;
   bool lora_ = false, full_ = false;

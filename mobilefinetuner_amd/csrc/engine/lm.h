@@ -5,6 +5,7 @@
 // runs either model through this interface: a mean-token-NLL loss with autograd, an eval NLL sum
 // without it, the trainable parameters in checkpoint order, the LoRA-dropout step counter.
 #pragma once
+#include <map>
 #include <string>
 #include <utility>
 #include <vector>
@@ -33,6 +34,15 @@ class LanguageModel {
   bool lora_enabled = true;
   Tensor dropout_ctr;    // device int64 step counter (fresh LoRA-dropout masks per step)
   int64_t ce_chunk = 0;  // LM-head CE rows per fused call (default_ce_chunk)
+  // --loss_reduction sum|sum_debug (reference core/lm_loss.cpp:184-192): loss() returns the SUM of
+  // the token NLL and its gradient is not divided by the valid-token count
+  bool loss_sum = false;
+  // --activation_checkpointing: each block's activations are recomputed in the backward
+  // (autograd.h checkpoint()) instead of kept -- one more forward for O(blocks) less memory
+  bool grad_checkpoint = false;
+  // alignment harness: hidden() copies the listed layers' MLP outputs (after the post-FF norm)
+  std::vector<int> capture_layers;
+  std::map<int, Tensor> captured;
 
  protected:
   // the adapters of one projection as the forward sees them (none while merged)

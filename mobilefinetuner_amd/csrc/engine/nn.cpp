@@ -752,11 +752,13 @@ Tensor inv_valid(const Tensor& labels) {
 }
 }  // namespace
 
-Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk, float w_grad_scale) {
+Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk, float w_grad_scale,
+                  bool sum_reduction) {
   const int64_t M = h.size(0), C = h.size(1), Vp = w.c.size(0);
   Tensor hc = h.detach().contiguous();
   Tensor lab = labels.reshape({-1}).contiguous();
-  Tensor scale = inv_valid(lab);
+  // mean: the loss and every gradient scaled by 1 / valid tokens; sum: unscaled
+  Tensor scale = sum_reduction ? ones({1}, DType::F32, h.device()) : inv_valid(lab);
   Tensor loss_rows = empty({M}, DType::F32, h.device());
   const bool need_h = needs_grad(h);
   const bool need_w = w.trainable() && grad_enabled();
@@ -799,7 +801,7 @@ Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_
   return loss;
 }
 
-std::pair<Tensor, Tensor> lm_head_nll(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk) {
+Tensor lm_head_token_nll(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk) {
   NoGradGuard ng;
   const int64_t M = h.size(0), Vp = w.c.size(0);
   Tensor hc = h.detach().contiguous();
@@ -819,6 +821,13 @@ std::pair<Tensor, Tensor> lm_head_nll(const Tensor& h, Param& w, const Tensor& l
     a.ws = fp(ws);
     ::mft::lm_head_ce(a, S());
   }
+  return loss_rows;
+}
+
+std::pair<Tensor, Tensor> lm_head_nll(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk) {
+  NoGradGuard ng;
+  Tensor loss_rows = lm_head_token_nll(h, w, labels, V, chunk);
+  Tensor lab = labels.reshape({-1}).contiguous();
   Tensor cnt = empty({1}, DType::F32, h.device());
   k::count_valid(lab.data<int64_t>(), lab.numel(), -100, fp(cnt), S());
   return {sum(loss_rows), cnt};

@@ -72,7 +72,10 @@ Tensor lora_linear(const Tensor& x, Param& w, Param* b, std::vector<LoraAdapter>
                    const Tensor& drop_ctr);
 // mean token NLL of logits = h W^T over the first V columns (labels -100 ignored); the W gradient
 // (tied embedding in full fine-tuning) is produced during forward scaled by w_grad_scale
-Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk, float w_grad_scale);
+Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk, float w_grad_scale,
+                  bool sum_reduction = false);
+// per-token NLL [M] fp32 (0 at ignored labels), no gradients (alignment dumps)
+Tensor lm_head_token_nll(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk);
 // (sum of NLL over valid rows, number of valid rows) without gradients -- evaluation
 std::pair<Tensor, Tensor> lm_head_nll(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk);
 

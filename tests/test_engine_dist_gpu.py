@@ -215,3 +215,24 @@ def test_native_bench_json_line(tmp_path):
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["value"] > 0 and "native" in rec["config"]["engine"]
     assert abs(rec["value"] - 64 * 128 * 3 / (rec["ms_per_step"] * 3 / 1000)) < 0.01 * rec["value"]
+
+
+@pytest.mark.parametrize("prog,args,bflag", [
+    ("gpt2_full_finetune", FULL, "--batch_size"),
+    ("gpt2_full_finetune", FULL + ["--zero_stage", "3"], "--batch_size"),
+    ("gpt2_lora_finetune", FULL + ["--lora_targets", "AttnQKV,AttnProj,MlpFcIn,MlpFcOut"], "--batch_size"),
+    ("train_lora_gemma", ["--random_init", "--model", "gemma3-tiny", "--synthetic_data", "--synthetic_tokens", "100000",
+                          "--seq_len", "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic", "--max_steps", "5",
+                          "--lora_dropout", "0.1", "--lr_schedule", "constant"], "--batch"),
+], ids=["gpt2-full", "gpt2-full-zero3", "gpt2-lora", "gemma-lora-dropout"])
+def test_native_activation_checkpointing_same_losses(prog, args, bflag):
+    """--activation_checkpointing (autograd.h checkpoint(): each block recomputed in the backward,
+    a nested backward through it) trains to the same per-step losses as keeping the activations --
+    LoRA dropout masks included (counter-based, identical in the recompute), ZeRO-3 gathers too."""
+    want = loss_list(_single(prog, args, bflag, 4).stdout, True)
+    extra_env = {"MFT_DP_FORCE_COMM": "1"} if "--zero_stage" in args else {}
+    r = subprocess.run([_bin(prog), *args, bflag, "4", "--activation_checkpointing"], capture_output=True, text=True,
+                       timeout=240, env=_env(backend="rccl", **extra_env) if extra_env else _env())
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    got = loss_list(r.stdout, True)
+    assert len(got) == len(want) and got == pytest.approx(want, rel=1e-5, abs=1e-5), (got, want)

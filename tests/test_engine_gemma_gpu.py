@@ -187,3 +187,52 @@ def test_native_gemma_weight_streaming_matches_resident():
         got, out = losses(["--shard_enable", "--shard_budget_mb", "1", *extra])
         assert "weight streaming ON: 2 device slots" in out, out[-2000:]
         assert len(got) == 5 and got == pytest.approx(ref, abs=2e-3), (extra, got, ref)
+
+
+def test_native_gemma_alignment_harness(tmp_path):
+    """--align_dump_dir (reference train_lora_gemma.cpp:609-922) on the native CLI: one fixed batch,
+    the reference's dump layout, --loss_reduction sum_debug (summed loss, unnormalised gradients =
+    the mean run's x valid tokens), central finite differences agreeing with the analytic LoRA
+    gradients, and the loss matching the PyTorch-driven model on the same batch."""
+    import re
+
+    import numpy as np
+    tmp, S, B = str(tmp_path), 64, 4
+    model, lora = _fixture(tmp, S, n_tokens=20_000)
+    base = [_bin("train_lora_gemma"), "--model_dir", tmp, "--resume_from", lora, "--pretokenized_path",
+            os.path.join(tmp, "tokens.bin"), "--seq_len", str(S), "--batch", str(B), "--align_layers", "0,1",
+            "--lr", "1e-3"]
+    dm, dsum = os.path.join(tmp, "align_mean"), os.path.join(tmp, "align_sum")
+    r = subprocess.run(base + ["--align_dump_dir", dm, "--align_numeric_attn", "--align_numeric_count", "3",
+                               "--align_numeric_eps", "1e-2"], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    r2 = subprocess.run(base + ["--align_dump_dir", dsum, "--loss_reduction", "sum_debug", "--align_do_step", "0"],
+                        capture_output=True, text=True, timeout=180)
+    assert r2.returncode == 0, r2.stdout[-2000:] + r2.stderr[-2000:]
+    ld = lambda d, f: np.load(os.path.join(d, f))  # noqa: E731
+    ids, lab = ld(dm, "input_ids.npy"), ld(dm, "labels.npy")
+    assert ids.shape == (B, S) and lab.shape == (B, S) and ids.dtype == np.int32
+    assert ld(dm, "layer0_mlp_out.npy").shape == (B, S, 128) and os.path.exists(os.path.join(dm, "layer1_mlp_out.npy"))
+    tok, valid = ld(dm, "per_token_nll.npy"), lab != -100
+    mean_loss, sum_loss = float(ld(dm, "loss_scalar.npy")[0]), float(ld(dsum, "loss_scalar.npy")[0])
+    assert abs(tok[valid].mean() - mean_loss) < 1e-3 * mean_loss
+    assert abs(sum_loss - tok[valid].sum()) < 1e-3 * sum_loss
+    grads = sorted(os.listdir(os.path.join(dm, "grads")))
+    assert len(grads) == 2 * 7 * 2 and all(g.startswith("base_model_model_model_layers_") for g in grads), grads
+    n = int(valid.sum())
+    for g in grads:
+        gm, gs = np.load(os.path.join(dm, "grads", g)), np.load(os.path.join(dsum, "grads", g))
+        assert np.abs(gs - gm * n).max() <= 2e-2 * np.abs(gm * n).max() + 1e-6, g
+    assert len(os.listdir(os.path.join(dm, "weights_after_step"))) == len(grads)
+    assert not os.path.exists(os.path.join(dsum, "weights_after_step"))
+    # central differences of a bf16-computed loss: ~1e-4 loss noise against 1e-4..1e-3 loss changes,
+    # so this catches sign / factor errors (a wrong gradient), not the last digit
+    pairs = re.findall(r"analytic=([0-9.e+-]+) numeric=([0-9.e+-]+)", r.stdout)
+    assert len(pairs) == 3, r.stdout[-2000:]
+    for an, nu in pairs:
+        an, nu = float(an), float(nu)
+        assert an * nu > 0 and 0.5 < an / nu < 2.0, (an, nu)
+    # the PyTorch-driven model on the same batch
+    with torch.no_grad():
+        py = float(model(torch.from_numpy(ids).long().cuda(), torch.from_numpy(lab).long().cuda()))
+    assert abs(py - mean_loss) < 1e-2 * py, (py, mean_loss)
