@@ -155,11 +155,14 @@ def run_native(a, cfgd) -> int:
     mode = "LoRA r=%d alpha=%g targets=%s" % (a.rank, a.alpha, a.targets or cfgd["targets"]) \
         if cfgd["mode"] == "lora" else "full fine-tune" + (f" ZeRO-{zero}" if zero else "") + \
         (" + host-offloaded AdamW (bf16 moments)" if (cfgd.get("offload", False) or a.offload_optimizer) else "")
+    # physical devices, not ranks: the loopback backend runs every rank on one GPU (tests)
+    cbe = os.environ.get("MFT_COMM_BACKEND", "rccl")
+    phys = 1 if cbe == "loopback" else rec["world"]
     out_rec = {
         "metric": cfgd["metric"],
         "value": round(value, 1),
         "unit": "tokens/s",
-        "n_gpus": rec["world"],
+        "n_gpus": phys,
         "steps": rec["steps"],
         "warmup": rec["warmup"],
         "ms_per_step": round(1000 * dt / rec["steps"], 3),
@@ -175,7 +178,8 @@ def run_native(a, cfgd) -> int:
             "seq_len": rec["seq"],
             "parallelism": f"dp{rec['world']}",
             "engine": "native libmft (C++ autograd tape, hipGraph-captured step)",
-            "backend": "rccl" if (rec["world"] > 1 or zero) else "none",
+            "ranks": rec["world"],
+            "backend": cbe if (rec["world"] > 1 or zero) else "none",
             "hipgraph": not a.no_graph,
             "final_loss": round(rec["final_loss"], 4),
             "model_tflops_per_gpu": round(tflops, 1),
@@ -390,12 +394,15 @@ def main():
     tokens = world * a.batch * a.seq * a.grad_accum * a.steps
     value = tokens / dt
     tflops, mfu = trace.mfu(value / world, fpt)
+    # physical devices, not ranks: gloo ranks share GPU 0 (tests), the CPU smoke uses none
+    tbe = ("gloo" if a.cpu_smoke else os.environ.get("MFT_DIST_BACKEND", "nccl")) if world > 1 else "none"
+    phys = 0 if a.cpu_smoke else (1 if tbe not in ("nccl", "none") else world)
     if rank == 0:
         out = {
             "metric": cfgd["metric"],
             "value": round(value, 1),
             "unit": "tokens/s",
-            "n_gpus": world,
+            "n_gpus": phys,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(1000 * dt / a.steps, 3),
@@ -411,6 +418,8 @@ def main():
                 "micro_batch_per_gpu": a.batch,
                 "seq_len": a.seq,
                 "parallelism": f"dp{world}",
+                "ranks": world,
+                "backend": "rccl" if tbe == "nccl" else tbe,
                 "hipgraph": bool(getattr(step, "use_graph", False)),
                 "final_loss": round(final_loss, 4),
                 "model_tflops_per_gpu": round(tflops, 1),

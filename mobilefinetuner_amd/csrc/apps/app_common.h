@@ -25,6 +25,7 @@
 #include "engine/comm.h"
 #include "engine/dist.h"
 #include "engine/optim.h"
+#include "engine/weight_stream.h"
 #include "engine/zero3.h"
 #include "runtime/dataset.h"
 #include "runtime/power_monitor.h"
@@ -262,6 +263,24 @@ inline float grads_into_masters(ModelT& model, eng::FlatParams& flat, TokenDatas
   flat.master.copy_(flat.grad);
   eng::synchronize();
   return lv;
+}
+
+// --shard_dir D [--shard_fp16_disk 0|1]: the streamed weights' disk tier (weight_stream.h)
+inline eng::DiskTier disk_tier_from(const Args& a) {
+  eng::DiskTier d;
+  d.dir = a.get("shard_dir");
+  d.fp16 = !a.kv.count("shard_fp16_disk") || (a.kv.at("shard_fp16_disk") != "0" && a.kv.at("shard_fp16_disk") != "false");
+  return d;
+}
+
+inline void print_streaming(const eng::WeightStreamer* ws, const char* what) {
+  if (ws->on_disk())
+    std::printf("  weight streaming ON: %d device slots (%.1f MB) for %.1f MB of frozen %s weights on disk (%s), "
+                "%.1f MB pinned staging\n", ws->slots(), ws->device_bytes() / 1048576.0, ws->disk_bytes() / 1048576.0, what,
+                "block files", ws->host_bytes() / 1048576.0);
+  else
+    std::printf("  weight streaming ON: %d device slots (%.1f MB) for %.1f MB of frozen %s weights in pinned host memory\n",
+                ws->slots(), ws->device_bytes() / 1048576.0, ws->host_bytes() / 1048576.0, what);
 }
 
 // NumPy .npy v1.0 writer for the alignment dumps (the reference's save_npy, train_lora_gemma.cpp:

@@ -189,14 +189,11 @@ int run(int argc, char** argv) {
   }
   if (a.b("shard_enable")) {
     // reference ParameterSharder flags: --shard_budget_mb (device bytes for streamed weights);
-    // --shard_dir / --shard_fp16_disk name its disk tier, which pinned host memory replaces here
+    // --shard_dir D [--shard_fp16_disk 0|1]: block files on disk (fp16 by default) instead of
+    // resident pinned host copies
     const size_t budget = (size_t)a.l("shard_budget_mb", 512) << 20;
-    model->enable_weight_streaming(budget);
-    const WeightStreamer* ws = model->streamer();
-    std::printf("  weight streaming ON: %d device slots (%.1f MB) for %.1f MB of frozen block weights in pinned host memory\n",
-                ws->slots(), ws->device_bytes() / 1048576.0, ws->host_bytes() / 1048576.0);
-    if (!a.get("shard_dir").empty() || a.kv.count("shard_fp16_disk"))
-      std::printf("  (--shard_dir / --shard_fp16_disk: no disk tier in the native engine, host DRAM holds the weights)\n");
+    model->enable_weight_streaming(budget, mft::apps::disk_tier_from(a));
+    mft::apps::print_streaming(model->streamer(), "block");
   }
   mft::apps::DistSetup ds;
   if (dcfg.zero_stage == 3) {  // parameters partitioned over the ranks, gathered per block

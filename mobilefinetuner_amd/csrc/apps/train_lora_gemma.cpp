@@ -391,10 +391,8 @@ int run(int argc, char** argv) {
     // budget to the largest parameter, train_lora_gemma.cpp:431-441; here the tied embedding stays
     // resident and every slot holds one whole layer)
     const size_t budget = (size_t)a.l("shard_budget_mb", 512) << 20;
-    model->enable_weight_streaming(budget);
-    const WeightStreamer* ws = model->streamer();
-    std::printf("  weight streaming ON: %d device slots (%.1f MB) for %.1f MB of frozen layer weights in pinned host memory\n",
-                ws->slots(), ws->device_bytes() / 1048576.0, ws->host_bytes() / 1048576.0);
+    model->enable_weight_streaming(budget, mft::apps::disk_tier_from(a));
+    mft::apps::print_streaming(model->streamer(), "layer");
   }
   mft::apps::DistSetup ds;
   ds.make_flat(model->trainable(), comm.get(), dcfg);

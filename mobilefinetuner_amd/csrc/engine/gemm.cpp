@@ -276,11 +276,15 @@ void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
   const long M = dy2.size(0), N = dy2.size(1), K = x2.size(1);
   MFT_CHECK(x2.size(0) == M && buf.numel() == N * K, "gemm_wgrad: shapes");
   // gemm8 (F32ACC epilogue straight into the flat grad, split-K over the tokens when the output
-  // alone does not fill the CUs) by default: 0.9-1.1 PF/s on the GPT-2 shapes, 0.65-0.77 on XL's,
-  // vs hipBLASLt's fp32-out kernels at 0.42-0.95 (profiles/r3_wgrad_shapes.txt);
-  // MFT_WGRAD=lt routes to hipBLASLt (A/B)
-  static const bool lt_wgrad = std::getenv("MFT_WGRAD") && std::string(std::getenv("MFT_WGRAD")) == "lt";
-  if ((deterministic() || gemm8_all() || !lt_wgrad) && M % 64 == 0 && N % 8 == 0 && K % 8 == 0 && dy2.stride(0) % 8 == 0 &&
+  // alone does not fill the CUs) for long token reductions: 0.9-1.1 PF/s on the GPT-2 shapes at
+  // 65536 tokens, and the gpt2-full step 63.1 vs 66.5 ms with hipBLASLt's fp32-out kernels.  At
+  // GPT-2 XL's 8192 tokens the 1600-6400-wide outputs need 7-way splits whose fp32 slabs cost more
+  // than they save: hipBLASLt there (XL ZeRO-3 step 115.4 vs 121.9 ms; profiles/r3_wgrad_ab.jsonl).
+  // MFT_WGRAD=gemm8|lt forces one (A/B).
+  static const char* wg_env = std::getenv("MFT_WGRAD");
+  static const int wg_mode = !wg_env ? 0 : std::string(wg_env) == "lt" ? 1 : std::string(wg_env) == "gemm8" ? 2 : 0;
+  const bool want_g8 = wg_mode == 2 || (wg_mode == 0 && M >= 32768);
+  if ((deterministic() || gemm8_all() || want_g8) && M % 64 == 0 && N % 8 == 0 && K % 8 == 0 && dy2.stride(0) % 8 == 0 &&
       x2.stride(0) % 8 == 0 && ::mft::gemm8_supported((int)N, (int)K, (int)M, true, true)) {
     ::mft::GemmArgs g{};
     g.A = (const ::mft::bf16_t*)dy2.data_ptr();

@@ -427,13 +427,13 @@ void Gemma3::merge_lora(float sign) {
   }
 }
 
-void Gemma3::enable_weight_streaming(size_t budget_bytes) {
+void Gemma3::enable_weight_streaming(size_t budget_bytes, const DiskTier& disk) {
   std::vector<std::vector<Param*>> groups;
   for (auto& L : layers_) {
     groups.push_back({&L.qkv_w, &L.o_w, &L.gu_w, &L.down_w});
     L.waug_qkv = L.waug_o = L.waug_gu = L.waug_down = Tensor();
   }
-  streamer_ = std::make_unique<WeightStreamer>(groups, budget_bytes);
+  streamer_ = std::make_unique<WeightStreamer>(groups, budget_bytes, disk);
 }
 
 // ------------------------------------------------------------------ forward

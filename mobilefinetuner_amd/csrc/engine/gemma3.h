@@ -77,7 +77,7 @@ class Gemma3 : public LanguageModel {
   const GemmaLoraSpec& lora_spec() const { return spec_; }
   // --shard_enable: the layers' frozen projection weights streamed from pinned host memory through
   // device slots within budget_bytes (weight_stream.h); LoRA projections take the plain path
-  void enable_weight_streaming(size_t budget_bytes);
+  void enable_weight_streaming(size_t budget_bytes, const DiskTier& disk = {});
   const WeightStreamer* streamer() const { return streamer_.get(); }
   bool interleaved_rope = false;  // reference RoPE pairing
 

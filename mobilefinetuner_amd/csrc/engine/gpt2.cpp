@@ -438,7 +438,7 @@ void GPT2::merge_lora(float sign) {
   }
 }
 
-void GPT2::enable_weight_streaming(size_t budget_bytes) {
+void GPT2::enable_weight_streaming(size_t budget_bytes, const DiskTier& disk) {
   std::vector<std::vector<Param*>> groups;
   for (auto& b : blocks_) {
     std::vector<Param*> g;
@@ -447,7 +447,7 @@ void GPT2::enable_weight_streaming(size_t budget_bytes) {
     groups.push_back(g);
     b.waug_qkv = Tensor(), b.waug_proj = Tensor();
   }
-  streamer_ = std::make_unique<WeightStreamer>(groups, budget_bytes);
+  streamer_ = std::make_unique<WeightStreamer>(groups, budget_bytes, disk);
 }
 
 // ------------------------------------------------------------------ forward

@@ -74,7 +74,7 @@ class GPT2 : public LanguageModel {
   size_t num_parameters() const override;
   // --shard_enable: every block's frozen weights into the host tier, streamed through device slots
   // within budget_bytes (weight_stream.h); LoRA projections then take the plain (non-augmented) path
-  void enable_weight_streaming(size_t budget_bytes);
+  void enable_weight_streaming(size_t budget_bytes, const DiskTier& disk = {});
   const WeightStreamer* streamer() const { return streamer_.get(); }
   // ZeRO-3 (engine/zero3.h): units[0] = {wte, wpe}, units[1 + i] = block i's bf16-compute
   // weights and biases; rep = the fp32-compute LayerNorm parameters (replicated)

@@ -13,9 +13,17 @@
 // and prefetches `next` into its own slot while block i computes.  The forward walks the blocks up,
 // a gate node at each block boundary re-loads the block on the way back down in the backward.
 // Embeddings, norms and trainable (LoRA) parameters stay resident.
+//
+// Disk tier (--shard_dir D [--shard_fp16_disk 0|1]; the reference's offload files,
+// parameter_sharder.cpp:21-76,205-276): every block's bytes go to D/block_<i>.bin -- as fp16 when
+// asked (half the bytes of fp32, lossless for bf16 weights in fp16's range) -- and no host copy
+// stays resident.  A load is then a HOST NODE on the copy stream (pread of the file into one of two
+// pinned staging buffers) followed by the H2D copy (+ an fp16 -> bf16 cast kernel on the device),
+// so the disk -> DRAM -> HBM pipeline is still one static schedule that a hipGraph records.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <string>
 #include <vector>
 
 #include "engine/nn.h"
@@ -37,10 +45,15 @@ class BlockProvider {
   virtual std::pair<Tensor, Tensor> gate(const Tensor& x, const Tensor& h, int g) = 0;
 };
 
+struct DiskTier {
+  std::string dir;    // empty: host-DRAM tier only
+  bool fp16 = true;   // store fp16 on disk (reference --shard_fp16_disk, default 1)
+};
+
 class WeightStreamer : public BlockProvider {
  public:
   // groups[i]: the frozen bf16 Params of block i (re-bound to slot views; their device copies freed)
-  WeightStreamer(const std::vector<std::vector<Param*>>& groups, size_t budget_bytes);
+  WeightStreamer(const std::vector<std::vector<Param*>>& groups, size_t budget_bytes, const DiskTier& disk = {});
   ~WeightStreamer();
   WeightStreamer(const WeightStreamer&) = delete;
   WeightStreamer& operator=(const WeightStreamer&) = delete;
@@ -50,7 +63,9 @@ class WeightStreamer : public BlockProvider {
   std::pair<Tensor, Tensor> gate(const Tensor& x, const Tensor& h, int g) override;
   int slots() const { return (int)slot_.size(); }
   size_t device_bytes() const { return slot_bytes_ * slot_.size(); }
-  size_t host_bytes() const { return host_bytes_; }
+  size_t host_bytes() const { return host_bytes_; }    // resident pinned bytes (staging only with a disk tier)
+  size_t disk_bytes() const { return disk_bytes_; }
+  bool on_disk() const { return !disk_.dir.empty(); }
   int64_t copies = 0;  // H2D group copies issued (a graph replay repeats its recorded ones)
 
  private:
@@ -58,17 +73,26 @@ class WeightStreamer : public BlockProvider {
   struct Group {
     std::vector<Param*> ps;
     std::vector<int64_t> off;  // element offsets inside the slot
-    Tensor host;               // pinned bf16 [elems]
+    Tensor host;               // pinned bf16 [elems] (host tier)
     int64_t elems = 0;
+    // disk tier: the host node's arguments (stable addresses for hipLaunchHostFunc)
+    int fd = -1;
+    void* stage = nullptr;
+    size_t bytes = 0;
+    std::string path;
   };
+  static void read_group(void* group);  // host node: pread the block's file into its staging buffer
   std::vector<Group> groups_;
   std::vector<Tensor> slot_;
   std::vector<int> holder_;  // group whose copy was last issued into each slot (-1: none)
   std::vector<hipEvent_t> ready_;
   hipEvent_t order_ = nullptr;
   hipStream_t copy_ = nullptr;
-  size_t slot_bytes_ = 0, host_bytes_ = 0;
+  size_t slot_bytes_ = 0, host_bytes_ = 0, disk_bytes_ = 0;
   bool capturing_ = false;
+  DiskTier disk_;
+  std::vector<Tensor> stage_host_;  // two pinned staging buffers (disk tier)
+  Tensor stage_dev_;                // fp16 landing buffer before the cast (fp16 on disk)
 };
 
 }  // namespace eng

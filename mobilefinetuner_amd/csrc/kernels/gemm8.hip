@@ -499,7 +499,12 @@ __device__ unsigned long long* g8_stamps;
 #define G8_STAMP(k)
 #endif
 
-template <int EPI, bool AT, bool BT>
+// LATE: each phase arrives at its first barrier with its fragment reads still in flight and waits
+// for them after it (the guide §5 template order: s_barrier; lgkmcnt(0); MFMAs), the B fragments
+// read before the A fragments -- the read latency then overlaps the barrier skew instead of adding
+// to it.  (Reads complete before the phase's MFMAs; the half-tile they read is restaged only after
+// the phase's second barrier, so the order is safe.)
+template <int EPI, bool AT, bool BT, bool LATE = false>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   G8_STAMP(0);
@@ -662,73 +667,95 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   // L2, and a faster third tile breaks that sharing (measured 21.9 -> 23.2 ms at Gemma-3's shape).
   const bool b1_ok = EPI == GEMM_EPI_CE_DGRAD || g.ntail_full || n0 + 128 < g.N;
 
+  // a phase's first barrier: fragment-read wait before (default) or after (LATE) it
+  auto pre_sync = [&]() {
+    if constexpr (LATE) {
+      raw_barrier();
+      lds_sync();
+    } else {
+      lds_sync();
+      raw_barrier();
+    }
+  };
+  auto pre_sync_vm = [&]() {  // phases 4 / 8: + retire the other buffer's half-tiles
+    if constexpr (LATE) {
+      vm_wait<4>();
+      raw_barrier();
+      lds_sync();
+    } else {
+      lds_sync();
+      vm_wait<4>();
+      raw_barrier();
+    }
+  };
+
   for (int kt = 0; kt < nk; kt += 2) {
     const bool odd_ok = kt + 1 < nk;  // the odd K-tile of this iteration exists
     // ---- phases 1-4: even buffer, K-tile kt
     // phase 1: quadrant (A0, B0); stage O.A1 (kt+1)
-    read_a(0, 0);
-    read_b(0, 0);
+    if constexpr (LATE) {
+      read_b(0, 0);
+      read_a(0, 0);
+    } else {
+      read_a(0, 0);
+      read_b(0, 0);
+    }
     const f32x4_t rq0 = ce_read(0, kt);
     stage(1, 1, kt + 1);
-    lds_sync();
-    raw_barrier();
+    pre_sync();
     mma_ce(0, rq0);
     raw_barrier();
     // phase 2: (A0, B1); stage O.B0 (kt+1)
     if (b1_ok) read_b(0, 1);
     const f32x4_t rq1 = ce_read(1, kt);
     stage(1, 2, kt + 1);
-    lds_sync();
-    raw_barrier();
+    pre_sync();
     if (b1_ok) mma_ce(1, rq1);
     raw_barrier();
     // phase 3: (A1, B1); stage E.A0 (kt+2)
     read_a(0, 1);
     const f32x4_t rq2 = ce_read(2, kt);
     stage(0, 0, kt + 2);
-    lds_sync();
-    raw_barrier();
+    pre_sync();
     if (b1_ok) mma_ce(2, rq2);
     raw_barrier();
     // phase 4: (A1, B0); stage E.B1 (kt+2); retire the odd buffer
     read_b(0, 0);
     const f32x4_t rq3 = ce_read(3, kt);
     stage(0, 3, kt + 2);
-    lds_sync();
-    vm_wait<4>();
-    raw_barrier();
+    pre_sync_vm();
     mma_ce(3, rq3);
     raw_barrier();
     // ---- phases 5-8: odd buffer, K-tile kt+1 (MFMAs skipped past the end; loads/waits stay uniform)
     // phase 5: (A0, B0); stage E.A1 (kt+2)
-    read_a(1, 0);
-    read_b(1, 0);
+    if constexpr (LATE) {
+      read_b(1, 0);
+      read_a(1, 0);
+    } else {
+      read_a(1, 0);
+      read_b(1, 0);
+    }
     ce_dma(kt);
     stage(0, 1, kt + 2);
-    lds_sync();
-    raw_barrier();
+    pre_sync();
     if (odd_ok) mma(0);
     raw_barrier();
     // phase 6: (A0, B1); stage E.B0 (kt+2)
     if (b1_ok) read_b(1, 1);
     stage(0, 2, kt + 2);
-    lds_sync();
-    raw_barrier();
+    pre_sync();
     if (odd_ok && b1_ok) mma(1);
     raw_barrier();
     // phase 7: (A1, B1); stage O.A0 (kt+3)
     read_a(1, 1);
     stage(1, 0, kt + 3);
-    lds_sync();
-    raw_barrier();
+    pre_sync();
     if (odd_ok && b1_ok) mma(2);
     raw_barrier();
     // phase 8: (A1, B0); stage O.B1 (kt+3); retire the even buffer
     read_b(1, 0);
     stage(1, 3, kt + 3);
-    lds_sync();
-    vm_wait<4>();
-    raw_barrier();
+    pre_sync_vm();
     if (odd_ok) mma(3);
     raw_barrier();
   }
@@ -1033,11 +1060,15 @@ static int g_stream = -1;
 static bool gemm8_stream() {
   if (g_stream < 0) {
     const char* e = getenv("MFT_GEMM8_STREAM");
-    g_stream = (e && e[0] == '1') ? 1 : 0;
+    g_stream = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
   }
   return g_stream == 1;
 }
-void gemm8_set_stream(int on) { g_stream = on ? 1 : 0; }
+void gemm8_set_stream(int on) { g_stream = on; }  // 0 plain, 1 streaming form, 2 LATE phase order (NT)
+static bool gemm8_late() {
+  gemm8_stream();
+  return g_stream == 2;
+}
 
 template <int EPI, bool AT, bool BT>
 static void launch8(const GemmArgs& g, hipStream_t st) {
@@ -1061,6 +1092,18 @@ static void launch8(const GemmArgs& g, hipStream_t st) {
         attr_s = true;
       }
       gemm8s_kernel<EPI, AT, BT><<<num_cus(), 512, shm, st>>>(g);
+      return;
+    }
+  }
+  if constexpr (!AT && !BT && EPI == GEMM_EPI_NONE) {
+    if (gemm8_late()) {
+      static bool attr_l = false;
+      if (!attr_l) {
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI, AT, BT, true>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        attr_l = true;
+      }
+      gemm8_kernel<EPI, AT, BT, true><<<tiles * ks, 512, shm, st>>>(g);
       return;
     }
   }

@@ -410,7 +410,7 @@ def test_zero2_checkpoint_has_every_shard(tmp_path):
 
 def test_bench_spawns_ranks_cpu_smoke():
     """bench.py --gpus 2 without a launcher spawns 2 rank processes itself (no re-exec) and reports
-    the launched world size."""
+    the launched world size: 2 ranks (gloo) on no GPU -- n_gpus counts physical devices."""
     import json
     import subprocess
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
@@ -420,5 +420,6 @@ def test_bench_spawns_ranks_cpu_smoke():
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["n_gpus"] == 0 and out["config"]["ranks"] == 2 and out["config"]["backend"] == "gloo"
+    assert out["config"]["parallelism"] == "dp2"
     assert out["config"]["global_batch"] == 2 * out["config"]["micro_batch_per_gpu"]

@@ -170,7 +170,7 @@ def test_native_gemma_eval_ppl_matches_python_cli(tmp_path):
     assert abs(ppl["1"] - ppl["0"]) < 5e-3 * ppl["0"], ppl
 
 
-def test_native_gemma_weight_streaming_matches_resident():
+def test_native_gemma_weight_streaming_matches_resident(tmp_path):
     """train_lora_gemma --shard_enable: the layers' frozen projections stream from pinned host memory
     through 2 device slots (3 layers), graph-captured and eager, with the resident run's losses."""
     common = ["--random_init", "--model", "gemma3-tiny", "--synthetic_data", "--synthetic_tokens", "50000",
@@ -183,7 +183,7 @@ def test_native_gemma_weight_streaming_matches_resident():
         return loss_list(r.stdout, True), r.stdout
 
     ref, _ = losses([])
-    for extra in ([], ["--no_graph"]):
+    for extra in ([], ["--no_graph"], ["--shard_dir", str(tmp_path / "d")]):
         got, out = losses(["--shard_enable", "--shard_budget_mb", "1", *extra])
         assert "weight streaming ON: 2 device slots" in out, out[-2000:]
         assert len(got) == 5 and got == pytest.approx(ref, abs=2e-3), (extra, got, ref)
@@ -232,7 +232,10 @@ def test_native_gemma_alignment_harness(tmp_path):
     for an, nu in pairs:
         an, nu = float(an), float(nu)
         assert an * nu > 0 and 0.5 < an / nu < 2.0, (an, nu)
-    # the PyTorch-driven model on the same batch
+    # the PyTorch-driven model on the same batch (its adapters on the flat fp32 master + bf16 shadow)
+    from mobilefinetuner_amd.peft.lora import lora_parameters
+    from mobilefinetuner_amd.utils.params import FlatParams
+    FlatParams(lora_parameters(model), "cuda")
     with torch.no_grad():
         py = float(model(torch.from_numpy(ids).long().cuda(), torch.from_numpy(lab).long().cuda()))
     assert abs(py - mean_loss) < 1e-2 * py, (py, mean_loss)

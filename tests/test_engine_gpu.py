@@ -218,10 +218,12 @@ def test_native_eval_ppl_matches_python_cli(tmp_path):
     assert abs(nat["ppl"] - py["ppl"]) < 2e-3 * py["ppl"], (nat, py)
 
 
-def test_native_weight_streaming_matches_resident():
+def test_native_weight_streaming_matches_resident(tmp_path):
     """--shard_enable in the native CLI: GPT-2's frozen block weights in pinned host memory, streamed
     through 2 device slots (40 MB budget, 14 MB per block) with prefetch and backward re-loads, in the
-    hipGraph-captured step and eagerly -- the same per-step losses as the resident run."""
+    hipGraph-captured step and eagerly -- the same per-step losses as the resident run.  With
+    --shard_dir the blocks live in files (fp16 by default, --shard_fp16_disk 0: bf16) read by host
+    nodes of the copy stream: same losses (bf16 -> fp16 -> bf16 is exact for these weights)."""
     common = ["--random_init", "--model", "gpt2", "--synthetic_data", "--synthetic_tokens", "200000", "--steps", "6",
               "--batch_size", "4", "--seq_len", "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic"]
 
@@ -231,9 +233,15 @@ def test_native_weight_streaming_matches_resident():
         return loss_list(r.stdout, True), r.stdout
 
     ref, _ = losses([])
-    for extra in ([], ["--no_graph"]):
+    d16, d = str(tmp_path / "fp16"), str(tmp_path / "bf16")
+    for extra in ([], ["--no_graph"], ["--shard_dir", d16], ["--shard_dir", d, "--shard_fp16_disk", "0", "--no_graph"]):
         got, out = losses(["--shard_enable", "--shard_budget_mb", "40", *extra])
         assert "weight streaming ON: 2 device slots" in out, out[-2000:]
+        if extra and extra[0] == "--shard_dir":
+            assert "on disk" in out, out[-2000:]
+            files = sorted(os.listdir(extra[1]))
+            assert len(files) == 12 and all(f.startswith("block_") for f in files), files
+            assert os.path.getsize(os.path.join(extra[1], "block_0.bin")) >= 7_000_000 * 2
         assert len(got) == 6 and got == pytest.approx(ref, abs=2e-3), (extra, got, ref)
 
 
