@@ -499,12 +499,13 @@ __device__ unsigned long long* g8_stamps;
 #define G8_STAMP(k)
 #endif
 
-// LATE: each phase arrives at its first barrier with its fragment reads still in flight and waits
-// for them after it (the guide §5 template order: s_barrier; lgkmcnt(0); MFMAs), the B fragments
-// read before the A fragments -- the read latency then overlaps the barrier skew instead of adding
-// to it.  (Reads complete before the phase's MFMAs; the half-tile they read is restaged only after
-// the phase's second barrier, so the order is safe.)
-template <int EPI, bool AT, bool BT, bool LATE = false>
+// LATE (default): each phase arrives at its first barrier with its fragment reads still in flight
+// and waits for them after it (the guide §5 template order: s_barrier; lgkmcnt(0); MFMAs), the B
+// fragments read before the A fragments -- the read latency then overlaps the barrier skew instead
+// of adding to it: +1-4 % on every NT shape measured (profiles/r3_g8late.txt).  (Reads complete
+// before the phase's MFMAs; the half-tile they read is restaged only after the phase's second
+// barrier, so the order is safe.)  LATE = false keeps the earlier order for A/B runs.
+template <int EPI, bool AT, bool BT, bool LATE = true>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   G8_STAMP(0);
@@ -1064,8 +1065,8 @@ static bool gemm8_stream() {
   }
   return g_stream == 1;
 }
-void gemm8_set_stream(int on) { g_stream = on; }  // 0 plain, 1 streaming form, 2 LATE phase order (NT)
-static bool gemm8_late() {
+void gemm8_set_stream(int on) { g_stream = on; }  // 0 default, 1 streaming form, 2 early-wait phase order (NT A/B)
+static bool gemm8_early() {
   gemm8_stream();
   return g_stream == 2;
 }
@@ -1096,14 +1097,14 @@ static void launch8(const GemmArgs& g, hipStream_t st) {
     }
   }
   if constexpr (!AT && !BT && EPI == GEMM_EPI_NONE) {
-    if (gemm8_late()) {
+    if (gemm8_early()) {
       static bool attr_l = false;
       if (!attr_l) {
-        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI, AT, BT, true>,
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI, AT, BT, false>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
         attr_l = true;
       }
-      gemm8_kernel<EPI, AT, BT, true><<<tiles * ks, 512, shm, st>>>(g);
+      gemm8_kernel<EPI, AT, BT, false><<<tiles * ks, 512, shm, st>>>(g);
       return;
     }
   }

@@ -70,11 +70,15 @@ def allreduce_sum_(t: torch.Tensor, group=None):
 
 
 class DataParallel:
-    """Bucketed, overlapped gradient averaging for a FlatParams grad buffer (all-reduce, or reduce
-    to the owning rank of a ZeRO-2 shard of ``shard`` elements per rank)."""
+    """Bucketed, overlapped gradient averaging for a FlatParams grad buffer: all-reduce, or (ZeRO-2,
+    ``chunked=True``) one ``reduce_scatter_tensor`` per bucket into this rank's chunk of it --
+    bucket b = [lo, hi) splits into ``world`` equal chunks, rank r owns [lo + r c, lo + (r+1) c),
+    and the chunks land back to back in ``own_grad`` (the rank's contiguous optimizer view).
+    ``shard`` (legacy contiguous ZeRO-2 shards) reduces each bucket to its owner(s) instead."""
 
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 64.0, overlap: bool = True,
-                 broadcast_from: int | None = 0, reduce_dtype=None, shard: int | None = None):
+                 broadcast_from: int | None = 0, reduce_dtype=None, shard: int | None = None,
+                 chunked: bool = False):
         self.flat, self.group = flat, group
         self.world = dist.get_world_size(group) if is_dist() else 1
         self.rank = dist.get_rank(group) if is_dist() else 0
@@ -112,6 +116,20 @@ class DataParallel:
         for bi, b in enumerate(self.buckets):
             for s in b["slots"]:
                 self.param_bucket[id(s.param)] = bi
+        # ZeRO-2 chunk layout: every bucket length divides by world (slot offsets are 64-aligned and
+        # the buffer is padded to ALIGN * world), chunk b of this rank at own_off[b] in own_grad
+        self.chunked = bool(chunked)
+        self.own_off, self.own_numel = [], 0
+        if self.chunked:
+            for b in self.buckets:
+                assert (b["hi"] - b["lo"]) % self.world == 0, "ZeRO-2 chunks need bucket lengths divisible by world"
+                b["c"] = (b["hi"] - b["lo"]) // self.world
+                self.own_off.append(self.own_numel)
+                self.own_numel += b["c"]
+            self.own_grad = torch.zeros(self.own_numel, dtype=flat.grad.dtype, device=flat.grad.device)
+            self.own_buf = None  # bf16 landing buffer of the reduced chunks
+            if reduce_dtype is not None and reduce_dtype != flat.grad.dtype:
+                self.own_buf = torch.empty(self.own_numel, dtype=reduce_dtype, device=flat.grad.device)
         self.comm_buf = None
         if reduce_dtype is not None and reduce_dtype != flat.grad.dtype and self.active:
             self.comm_buf = torch.empty(flat.numel, dtype=reduce_dtype, device=flat.grad.device)
@@ -168,7 +186,11 @@ class DataParallel:
             c.copy_(t)
             t = c
         op = dist.ReduceOp.AVG if self.nccl else dist.ReduceOp.SUM
-        if self.shard is None:
+        if self.chunked:
+            c, o = b["c"], self.own_off[bi]
+            out = (self.own_buf if self.comm_buf is not None else self.own_grad)[o:o + c]
+            self._works.append(dist.reduce_scatter_tensor(out, t, op=op, group=self.group, async_op=True))
+        elif self.shard is None:
             self._works.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
         else:
             for r, a, z in self._owner_segments(lo, hi):
@@ -197,7 +219,7 @@ class DataParallel:
         return self.capturable and self._hook is not None
 
     def owned(self):
-        """(lo, hi) of the reduced gradient this rank's optimizer reads."""
+        """(lo, hi) of the reduced gradient this rank's optimizer reads (contiguous layouts)."""
         if self.shard is None:
             return 0, self.flat.numel
         lo = self.rank * self.shard
@@ -214,6 +236,12 @@ class DataParallel:
             if w is not None:
                 w.wait()
         self._works = []
+        if self.chunked:
+            if self.own_buf is not None:
+                self.own_grad.copy_(self.own_buf)
+            if not self.nccl:
+                self.own_grad.div_(self.world)
+            return
         lo, hi = self.owned()
         if self.comm_buf is not None:
             self.flat.grad[lo:hi].copy_(self.comm_buf[lo:hi])

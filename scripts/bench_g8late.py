@@ -1,5 +1,5 @@
-"""gemm8 phase-order A/B on the NT shapes: variant 0 (lgkmcnt(0) then s_barrier) vs variant 2 (LATE:
-s_barrier then lgkmcnt(0), B fragments first) vs hipBLASLt (torch.mm).  Each variant is checked
+"""gemm8 phase-order A/B on the NT shapes: variant 2 (early: lgkmcnt(0) then s_barrier) vs variant 0 (the
+default LATE order: s_barrier then lgkmcnt(0), B fragments first) vs hipBLASLt (torch.mm).  Each variant is checked
 against an fp32 reference first; interleaved rounds, min over rounds.
 
 usage: PYTHONPATH=. python scripts/bench_g8late.py [--iters 10] [--rounds 4]
@@ -54,7 +54,7 @@ def main():
                 res[v].append(timeit(lambda: C.gemm_t(x, w, False, False, 0), a.iters))
             res["lt"].append(timeit(lambda: torch.mm(x, w.t()), a.iters))
         line = f"{name:14s} M={M:6d} K={K:5d} N={N:6d} |"
-        for k, lab in ((0, "gemm8"), (2, "gemm8-late"), ("lt", "hipBLASLt")):
+        for k, lab in ((2, "gemm8-early"), (0, "gemm8-late"), ("lt", "hipBLASLt")):
             t = min(res[k])
             line += f" {lab} {t:8.1f} us {fl / t / 1e6:6.0f} TF |"
         print(line, flush=True)
