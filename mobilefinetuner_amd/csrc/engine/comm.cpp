@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "engine/tensor.h"
+#include "engine/tensor_kernels.h"
 
 namespace mft {
 namespace eng {
@@ -188,7 +189,20 @@ void nccl_ok(ncclResult_t r, const char* what) {
 ncclDataType_t nccl_type(CommType t) {
   return t == CommType::F32 ? ncclFloat32 : t == CommType::BF16 ? ncclBfloat16 : ncclInt32;
 }
-ncclRedOp_t nccl_op(CommOp op) { return op == CommOp::Sum ? ncclSum : op == CommOp::Avg ? ncclAvg : ncclMax; }
+// CommOp::Avg is issued as ncclSum + an in-place scale: RCCL 2.26's ncclAvg (PreMulSum kernels)
+// returns wrong values in the last 4-8 elements of some lengths (fp32, 1-rank group, 66304 / 66240
+// elements; ncclSum exact at every length -- scripts/diag/rs_tail.py, profiles/r3_rccl_avg_tail.txt)
+ncclRedOp_t nccl_op(CommOp op) { return op == CommOp::Max ? ncclMax : ncclSum; }
+void scale_inplace(void* buf, size_t n, CommType t, float s, hipStream_t st) {
+  if (n == 0 || t == CommType::I32) return;
+  k::Desc d{};
+  d.ptr = buf;
+  d.dtype = (int)(t == CommType::F32 ? DType::F32 : DType::BF16);
+  d.ndim = 1;
+  d.shape[0] = (int64_t)n;
+  d.stride[0] = 1;
+  k::axpy(d, d, s, 0, st);  // buf = s * buf
+}
 
 class RcclComm final : public Communicator {
  public:
@@ -224,10 +238,12 @@ class RcclComm final : public Communicator {
   void all_reduce(void* buf, size_t n, CommType t, CommOp op, hipStream_t st) override {
     ++issued;
     nccl_ok(ncclAllReduce(buf, buf, n, nccl_type(t), nccl_op(op), comm_, st), "ncclAllReduce");
+    if (op == CommOp::Avg && world_ > 1) scale_inplace(buf, n, t, 1.f / (float)world_, st);
   }
   void reduce_scatter(const void* send, void* recv, size_t n, CommType t, CommOp op, hipStream_t st) override {
     ++issued;
     nccl_ok(ncclReduceScatter(send, recv, n, nccl_type(t), nccl_op(op), comm_, st), "ncclReduceScatter");
+    if (op == CommOp::Avg && world_ > 1) scale_inplace(recv, n, t, 1.f / (float)world_, st);
   }
   void all_gather(const void* send, void* recv, size_t n, CommType t, hipStream_t st) override {
     ++issued;

@@ -135,17 +135,17 @@ void DataParallel::launch(int b) {
   const int r = comm_.rank();
   float* g = flat_.grad.data<float>() + lo;
   if (!cfg_.bf16_reduce) {
-    if (cfg_.zero_stage == 2) comm_.reduce_scatter(g, g + r * c, c, CommType::F32, CommOp::Avg, stream_);
-    else comm_.all_reduce(g, n, CommType::F32, CommOp::Avg, stream_);
+    if (cfg_.zero_stage == 2) comm_.reduce_scatter(g, g + r * c, c, CommType::F32, CommOp::Sum, stream_);
+    else comm_.all_reduce(g, n, CommType::F32, CommOp::Sum, stream_);
     return;
   }
   ::mft::bf16_t* h = (::mft::bf16_t*)comm_buf_.data_ptr() + lo;
   ::mft::cast_f32_bf16(g, h, n, stream_);
   if (cfg_.zero_stage == 2) {
-    comm_.reduce_scatter(h, h + r * c, c, CommType::BF16, CommOp::Avg, stream_);
+    comm_.reduce_scatter(h, h + r * c, c, CommType::BF16, CommOp::Sum, stream_);
     ::mft::cast_bf16_f32(h + r * c, g + r * c, c, stream_);
   } else {
-    comm_.all_reduce(h, n, CommType::BF16, CommOp::Avg, stream_);
+    comm_.all_reduce(h, n, CommType::BF16, CommOp::Sum, stream_);
     ::mft::cast_bf16_f32(h, g, n, stream_);
   }
 }

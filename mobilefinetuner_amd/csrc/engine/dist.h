@@ -15,8 +15,8 @@
 // Step.  The autograd tape's grad-ready hooks (engine/autograd.h) count the parameters of each
 // bucket during the LAST micro-batch's backward; when a bucket is complete, an event on the compute
 // stream orders a collective on a dedicated communication stream:
-//   stage 0 / 1  all-reduce (average) of the bucket       (fp32, or bf16 with --bf16 reduce)
-//   stage 2      reduce-scatter (average) into the owned chunk (half the bytes of an all-reduce)
+//   stage 0 / 1  all-reduce (sum; the loss seed carries 1 / world) of the bucket (fp32, or bf16)
+//   stage 2      reduce-scatter (sum) into the owned chunk (half the bytes of an all-reduce)
 // so the reduction of early buckets overlaps the backward of the remaining layers.  finish() joins
 // the communication stream back.  The optimizer then updates either everything (stage 0) or only
 // the owned chunks (stages 1 / 2: AdamW::shard, moments for 1/world of the parameters, optionally
@@ -91,6 +91,9 @@ class DataParallel : public GradReducer {
   void after_optimizer() override;
   // stage >= 1: the full fp32 master on every rank (checkpoints / exports), then every shadow
   void gather_master() override;
+  // the loss seed carries 1 / world, the buckets are SUMMED (RCCL's Avg is inexact at some lengths:
+  // comm.h)
+  float grad_prescale() const override { return 1.f / (float)comm_.world(); }
   int stage() const { return cfg_.zero_stage; }
   const FlatPlan& plan() const { return plan_; }
   std::string describe() const override;

@@ -53,11 +53,12 @@ def _supports_avg(group=None):
         return False
 
 
+# Averages are SUM + divide, never ReduceOp.AVG: RCCL 2.26's AVG (its PreMulSum kernels) returns
+# wrong values in the last 4-8 elements of some lengths (66304, 66240 of fp32 on a 1-rank group;
+# SUM exact at every length and offset -- scripts/diag/rs_tail.py, profiles/r3_rccl_avg_tail.txt)
 def allreduce_mean_(t: torch.Tensor, group=None, async_op=False):
     if not is_dist() or dist.get_world_size(group) == 1:
         return None
-    if _supports_avg(group):
-        return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group, async_op=async_op)
     w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=False)
     t.div_(dist.get_world_size(group))
     return None if not async_op else w
@@ -185,7 +186,7 @@ class DataParallel:
             c = self.comm_buf[lo:hi]
             c.copy_(t)
             t = c
-        op = dist.ReduceOp.AVG if self.nccl else dist.ReduceOp.SUM
+        op = dist.ReduceOp.SUM  # (averaged in finish(): RCCL's AVG is inexact, allreduce_mean_ above)
         if self.chunked:
             c, o = b["c"], self.own_off[bi]
             out = (self.own_buf if self.comm_buf is not None else self.own_grad)[o:o + c]
@@ -239,13 +240,13 @@ class DataParallel:
         if self.chunked:
             if self.own_buf is not None:
                 self.own_grad.copy_(self.own_buf)
-            if not self.nccl:
+            if self.world > 1:
                 self.own_grad.div_(self.world)
             return
         lo, hi = self.owned()
         if self.comm_buf is not None:
             self.flat.grad[lo:hi].copy_(self.comm_buf[lo:hi])
-        if not self.nccl:
+        if self.world > 1:
             self.flat.grad[lo:hi].div_(self.world)
 
     def close(self):
