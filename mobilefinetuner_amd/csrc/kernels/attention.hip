@@ -885,12 +885,17 @@ __device__ __forceinline__ bf16x8_t frag_tr_perm_sw(const bf16_t* t, int r0, int
 }
 
 
-template <int D, int NW>
+// RPW = query rows per wave (16 or 32).  At RPW = 32 every K fragment (ds_read_b128) and V^T
+// fragment (ds_read_b64_tr_b16) read from LDS feeds TWO MFMAs -- one per 16-query half -- so the
+// workgroup's LDS read bytes per FLOP halve (at D = 256 the 16-row form reads the whole 32 KB
+// K+V stage per wave per 32-key tile: LDS-bandwidth bound), at ~2x the accumulator registers.
+template <int D, int NW, int RPW = 16>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
     float* __restrict__ lse, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides os, int H, int Hkv, int Sq,
     int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
-  constexpr int BQ = 16 * NW, BK = kSplitBK, TILE = BK * D, LDO = D + kSplitPad;
+  constexpr int R = RPW / 16;  // 16-query halves per wave
+  constexpr int BQ = RPW * NW, BK = kSplitBK, TILE = BK * D, LDO = D + kSplitPad;
   constexpr int OPW = 2 * (BK * D / 8 / 64) / NW;  // DMA ops per wave per ring stage (K + V)
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // ring stage s: K at smem + 2 s TILE, V after
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
@@ -900,28 +905,35 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
   const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
   const int coff = Sk - Sq;
   const float c2 = scale * kLog2e;
-  const int wq_lo = q0 + 16 * w, wq_hi = wq_lo + 15;
-  const int qi = wq_lo + c16;
+  const int wq_lo = q0 + RPW * w, wq_hi = wq_lo + RPW - 1;
   int kend = kv_len;
   if (causal) kend = min(kend, q0 + BQ + coff);
   int kstart = 0;
   if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
   const int nt = kend > kstart ? (kend - kstart + BK - 1) / BK : 0;  // WG-uniform
-  bf16x8_t qf[D / 32];
+  bf16x8_t qf[R][D / 32];
 #pragma unroll
-  for (int s = 0; s < D / 32; ++s)
-    qf[s] = qi < Sq ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qi * qs.ss + h * qs.sh + s * 32 + 8 * g)
-                    : bf16x8_t{};
+  for (int r = 0; r < R; ++r) {
+    const int qi = wq_lo + 16 * r + c16;
+#pragma unroll
+    for (int s2 = 0; s2 < D / 32; ++s2)
+      qf[r][s2] = qi < Sq ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qi * qs.ss + h * qs.sh + s2 * 32 + 8 * g)
+                          : bf16x8_t{};
+  }
   auto issue = [&](int j) {  // ring stage j % 3 <- tile min(j, nt - 1) (tail re-reads keep counts uniform)
     const int kb = kstart + min(j, nt - 1) * BK;
     bf16_t* st = smem + (j % kRing) * 2 * TILE;
     dma_tile32<D, NW>(st, k, ks, b, hk, kb, kv_len);
     dma_tile32<D, NW>(st + TILE, v, vs, b, hk, kb, kv_len);
   };
-  f32x4_t acc[D / 16];
+  f32x4_t acc[R][D / 16];
 #pragma unroll
-  for (int n = 0; n < D / 16; ++n) acc[n] = zero4();
-  float m = -INFINITY, l = 0.f;
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int n = 0; n < D / 16; ++n) acc[r][n] = zero4();
+  float m[R], l[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) m[r] = -INFINITY, l[r] = 0.f;
   if (nt > 0) {
     issue(0);
     issue(1);
@@ -936,66 +948,84 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
     const bool live = wq_lo < Sq && (!causal || kb <= wq_hi + coff) &&
                       (window <= 0 || wq_lo + coff - (kb + BK - 1) < window);
     if (live) {
-      f32x4_t st[2];
+      f32x4_t st[R][2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        st[t] = zero4();
 #pragma unroll
-        for (int s = 0; s < D / 32; ++s) st[t] = mfma16(frag_row_sw<D>(Ks, 16 * t, s * 32), qf[s], st[t]);
-      }
-      const bool need_mask = kb + BK > kv_len || (causal && kb + BK - 1 > wq_lo + coff) ||
-                             (window > 0 && wq_hi + coff - kb >= window) || wq_hi >= Sq;
-      float mx = -INFINITY;
+        for (int r = 0; r < R; ++r) st[r][t] = zero4();
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+        for (int s2 = 0; s2 < D / 32; ++s2) {
+          const bf16x8_t kf = frag_row_sw<D>(Ks, 16 * t, s2 * 32);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float sv = st[t][i] * c2;
-          if (need_mask && !(qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window)))
-            sv = -INFINITY;
-          st[t][i] = sv;
-          mx = fmaxf(mx, sv);
+          for (int r = 0; r < R; ++r) st[r][t] = mfma16(kf, qf[r][s2], st[r][t]);
         }
-      mx = fmaxf(mx, xor16_pl(mx));
-      mx = fmaxf(mx, xor32_pl(mx));
-      const float mnew = fmaxf(m, mx);
-      const float msafe = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = fast_exp2(m - msafe);
-      float rs = 0.f;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = fast_exp2(st[t][i] - msafe);
-          st[t][i] = p;
-          rs += p;
-        }
-      rs += xor16_pl(rs);
-      rs += xor32_pl(rs);
-      l = l * alpha + rs;
-      m = mnew;
-      if (__any(alpha != 1.f)) {  // wave-uniform: skip the rescale when no running max moved
-        float ar[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ar[i] = __shfl(alpha, 4 * g + i, 64);
-#pragma unroll
-        for (int n = 0; n < D / 16; ++n)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[n][i] *= ar[i];
       }
-      const bf16x8_t pa = pack_c2a(st[0], st[1]);
+      bf16x8_t pa[R];
 #pragma unroll
-      for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr_perm_sw<D>(Vs, 0, n * 16), acc[n]);
+      for (int r = 0; r < R; ++r) {
+        const int rlo = wq_lo + 16 * r, rhi = rlo + 15, qi = rlo + c16;
+        const bool need_mask = kb + BK > kv_len || (causal && kb + BK - 1 > rlo + coff) ||
+                               (window > 0 && rhi + coff - kb >= window) || rhi >= Sq;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float sv = st[r][t][i] * c2;
+            if (need_mask && !(qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window)))
+              sv = -INFINITY;
+            st[r][t][i] = sv;
+            mx = fmaxf(mx, sv);
+          }
+        mx = fmaxf(mx, xor16_pl(mx));
+        mx = fmaxf(mx, xor32_pl(mx));
+        const float mnew = fmaxf(m[r], mx);
+        const float msafe = mnew == -INFINITY ? 0.f : mnew;
+        const float alpha = fast_exp2(m[r] - msafe);
+        float rs = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = fast_exp2(st[r][t][i] - msafe);
+            st[r][t][i] = p;
+            rs += p;
+          }
+        rs += xor16_pl(rs);
+        rs += xor32_pl(rs);
+        l[r] = l[r] * alpha + rs;
+        m[r] = mnew;
+        if (__any(alpha != 1.f)) {  // wave-uniform: skip the rescale when no running max moved
+          float ar[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ar[i] = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+          for (int n = 0; n < D / 16; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[r][n][i] *= ar[i];
+        }
+        pa[r] = pack_c2a(st[r][0], st[r][1]);
+      }
+#pragma unroll
+      for (int n = 0; n < D / 16; ++n) {
+        const bf16x8_t vf = frag_tr_perm_sw<D>(Vs, 0, n * 16);
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r][n] = mfma16(pa[r], vf, acc[r][n]);
+      }
     }
   }
   vmcnt_wait<0>();  // the tail's re-read DMA must land before the LDS is reused / the WG exits
   __syncthreads();
-  const float inv_own = l > 0.f ? 1.f / l : 0.f;
-  if (g == 0 && qi < Sq) lse[((long)b * H + h) * Sq + qi] = l > 0.f ? (m + log2f(l)) / kLog2e : 1e30f;
-  float inv[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) inv[i] = __shfl(inv_own, 4 * g + i, 64);
-  if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * LDO, LDO, acc, inv, o, os, b, h, wq_lo, min(16, Sq - wq_lo));
+  for (int r = 0; r < R; ++r) {
+    const int rlo = wq_lo + 16 * r, qi = rlo + c16;
+    const float inv_own = l[r] > 0.f ? 1.f / l[r] : 0.f;
+    if (g == 0 && qi < Sq) lse[((long)b * H + h) * Sq + qi] = l[r] > 0.f ? (m[r] + log2f(l[r])) / kLog2e : 1e30f;
+    float inv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) inv[i] = __shfl(inv_own, 4 * g + i, 64);
+    if (rlo < Sq) store_tile16<D>(smem + w * 16 * LDO, LDO, acc[r], inv, o, os, b, h, rlo, min(16, Sq - rlo));
+  }
 }
 
 // two 32-row tiles (rows >= nvalid zero-filled) -> lds0/lds1 [32][D + kSplitPad]; all loads issue first
@@ -1230,19 +1260,27 @@ static void fwd_split_launch(const AttnArgs& a, hipStream_t stream) {
       a.causal, a.window, a.kv_lens);
 }
 
-template <int D>
-static void fwd_dma_launch(const AttnArgs& a, hipStream_t stream) {
-  constexpr int NW = 8;
+template <int D, int NW, int RPW>
+static void fwd_dma_launch_rpw(const AttnArgs& a, hipStream_t stream) {
   const size_t shm = std::max(sizeof(bf16_t) * kRing * 2 * kSplitBK * D, sizeof(bf16_t) * NW * 16 * (D + kSplitPad));
   static bool attr = false;
   if (!attr) {
-    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_dma_kernel<D, NW>,
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_dma_kernel<D, NW, RPW>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  attn_fwd_dma_kernel<D, NW><<<dim3(cdiv(a.Sq, 16 * NW), a.H, a.B), 64 * NW, shm, stream>>>(
+  attn_fwd_dma_kernel<D, NW, RPW><<<dim3(cdiv(a.Sq, RPW * NW), a.H, a.B), 64 * NW, shm, stream>>>(
       a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale,
       a.causal, a.window, a.kv_lens);
+}
+
+// MFT_ATTN_RPW=16|32: query rows per wave of the DMA forward (A/B).  32 rows need the 512-register
+// budget of one wave per SIMD (4 waves: 128 queries per workgroup, as 8 x 16).
+template <int D>
+static void fwd_dma_launch(const AttnArgs& a, hipStream_t stream) {
+  static const int rpw = env_int("MFT_ATTN_RPW", 16);
+  if (rpw == 32) fwd_dma_launch_rpw<D, 4, 32>(a, stream);
+  else fwd_dma_launch_rpw<D, 8, 16>(a, stream);
 }
 
 template <int D, int NW>

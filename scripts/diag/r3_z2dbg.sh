@@ -1,5 +1,4 @@
 #!/bin/bash
 set -o pipefail
-mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONPATH=$PWD
-timeout -k 10 200 python3 scripts/diag/z2_debug.py 2>&1 | grep -v amdgpu.ids | tail -12
+timeout -k 10 200 python3 scripts/diag/z2_debug.py 2>&1 | grep -v amdgpu.ids | grep -E "mismatch|rel diff|sync" | tail -8

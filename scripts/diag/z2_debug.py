@@ -58,7 +58,9 @@ def run(kind, graph, overlap, steps=5):
         st(b)
         torch.cuda.synchronize()
         ws.append(flat.master.clone())
-        gs.append((opt.reducer.own_grad.clone() if kind == "zero2" else None, flat.grad.clone()))
+        gs.append((opt.reducer.own_grad.clone() if kind == "zero2" else None, flat.grad.clone(), flat.shadow.clone()))
+    global flat_slots
+    flat_slots = flat.slots
     return ws, gs, opt
 
 
@@ -73,7 +75,8 @@ for op in (dist.ReduceOp.AVG, dist.ReduceOp.SUM):
     dist.reduce_scatter_tensor(out2, y, op=op)
     torch.cuda.synchronize()
     print("  offset slice: max |out - x| =", (out2 - y).abs().max().item(), flush=True)
-for sync in (False, True):
+flat_slots = []
+for sync in (False,):
   SYNC[0] = sync
   print("sync before finish:", sync, flush=True)
   for graph in (False,):
@@ -84,10 +87,20 @@ for sync in (False, True):
         diffs = [((a - b).norm() / a.norm()).item() for a, b in zip(w0, w1)]
         # the reduced chunk vs the plain grad, per step
         gd = []
-        for (own, fg), (_, fg0) in zip(g1, g0):
+        for (own, fg, _), (_, fg0, _) in zip(g1, g0):
             full = torch.cat([fg0[b_["lo"]:b_["hi"]] for b_ in R.buckets])
             gd.append(((own - full).norm() / full.norm()).item())
-        fgd = [((fg0 - fg).norm() / fg0.norm()).item() for (_, fg), (_, fg0) in zip(g1, g0)]
+        fgd = [((fg0 - fg).norm() / fg0.norm()).item() for (_, fg, _), (_, fg0, _) in zip(g1, g0)]
+        shd = []
+        for (_, _, s1), (_, _, s0) in zip(g1, g0):
+            d = (s1.float() - s0.float()).abs()
+            nz = torch.nonzero(d > 0).flatten()
+            who = []
+            if nz.numel():
+                j = int(nz[0])
+                who = [(sl.name, j - sl.offset) for sl in flat_slots if sl.offset <= j < sl.offset + sl.numel]
+            shd.append((int((d > 0).sum()), who))
+        print("shadow mismatches per step (count, first):", shd, flush=True)
         own, fgz = SNAP[0]
         bad = []
         for i, b_ in enumerate(R.buckets):

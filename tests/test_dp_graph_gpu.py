@@ -65,10 +65,19 @@ MODES = [False] + ([True] if os.environ.get("MFT_TEST_GRAPH_COMM") == "1" else [
 @pytest.mark.parametrize("graph_comm", MODES)
 @pytest.mark.parametrize("kind", ["ddp", "bf16", "zero2"])
 def test_reducer_with_graph_step_matches_no_dp(rccl1, kind, graph_comm, monkeypatch):
+    """(deterministic reductions: the embedding's scatter-add otherwise differs in the last bits
+    between two runs, and AdamW's per-element normalisation turns such noise on near-zero gradients
+    into +-lr updates within a few steps.  ZeRO-2 also sums the grad-norm^2 over its bucket-ordered
+    chunks -- a different fp32 order than the flat buffer's -- hence its looser weight bound.)"""
+    from mobilefinetuner_amd.ops import functional as Fx
     monkeypatch.setenv("MFT_GRAPH_COMM", "1" if graph_comm else "0")
-    ref_l, ref_w = _run("none")
-    l, w = _run(kind, graph_comm=graph_comm)
+    Fx.set_deterministic(True)
+    try:
+        ref_l, ref_w = _run("none")
+        l, w = _run(kind, graph_comm=graph_comm)
+    finally:
+        Fx.set_deterministic(False)
     tol = 3e-2 if kind == "bf16" else 2e-3
     assert l == pytest.approx(ref_l, rel=tol, abs=tol), (kind, l, ref_l)
     err = ((w - ref_w).norm() / ref_w.norm()).item()
-    assert err < (5e-3 if kind == "bf16" else 1e-4), (kind, err)
+    assert err < {"bf16": 5e-3, "zero2": 2e-3}.get(kind, 1e-4), (kind, err)
