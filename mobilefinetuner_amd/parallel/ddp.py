@@ -7,12 +7,12 @@ The reference has no parallelism at all.  Design for MI355X:
   slice — no packing/unpacking copies;
 * buckets are laid out in reverse-forward order and launched asynchronously from the
   ``grad_ready`` hook that the fused backward kernels call, so the reduction of late layers
-  overlaps the backward of early layers (eager steps); with ``MFT_GRAPH_COMM=1`` also inside the
+  overlaps the backward of early layers (eager steps) and, on RCCL (``MFT_GRAPH_COMM``, default 1), inside the
   step's hipGraph: the hooks enqueue their RCCL collectives while the step is being captured, so
   the replay runs each bucket's collective on RCCL's stream as soon as the kernels producing it are
-  done (``capturable``; opt-in, see __init__);
-* two reductions: ``all_reduce`` (DDP, ZeRO-1) or, with ``shard`` (ZeRO-2), ``reduce`` of every
-  bucket segment to the rank whose optimizer shard owns it -- the reduce-scatter traffic, bucketed
+  done (``capturable``, see __init__);
+* reductions: ``all_reduce`` (DDP, ZeRO-1), ``reduce_scatter_tensor`` per bucket into this rank's
+  chunk (ZeRO-2, ``chunked``), or (legacy contiguous shards) ``reduce`` to the owning rank -- bucketed
   and overlapped, while the owned shard stays one contiguous range for the fused AdamW;
 * optional bf16 reduction (``reduce_dtype=torch.bfloat16``): the bucket is cast into a bf16 comm
   buffer, reduced at half the xGMI bytes and cast back (full fine-tuning: 498 MB -> 249 MB per
@@ -87,10 +87,14 @@ class DataParallel:
         self.active = self.world > 1 or self.force
         self.nccl = _supports_avg(group)
         self.overlap = overlap and self.active
-        # collectives recorded into the step's hipGraph: opt-in (MFT_GRAPH_COMM=1).  On ROCm 7 /
-        # RCCL 2.26 capturing them aborted intermittently at capture end on a 1-rank group, so the
-        # default replays the captured fwd/bwd and reduces the buckets right after the replay
-        self.capturable = self.nccl and os.environ.get("MFT_GRAPH_COMM", "0") == "1"
+        # collectives recorded into the step's hipGraph from the backward's grad-ready hooks: the
+        # default on RCCL (MFT_GRAPH_COMM=0 reduces the buckets eagerly after the replay instead).
+        # Round 2 kept it opt-in after captures aborted intermittently at capture end on a 1-rank
+        # group; round 3 re-ran the recorded-collective tests (DDP, bf16, ZeRO-2) without an abort
+        # (profiles/r3_graph_comm_tests.log) and found RCCL's AVG inexact at some lengths, which is
+        # no longer used (sum + divide).  The capture runs in thread_local mode so RCCL's watchdog
+        # thread polling earlier events cannot invalidate it (train/engine.py).
+        self.capturable = self.nccl and os.environ.get("MFT_GRAPH_COMM", "1") == "1"
         self.shard = shard
         cap = int(bucket_mb * (1 << 20) / 4)
         # buckets over slots in REVERSE order (last layer's grads are ready first)

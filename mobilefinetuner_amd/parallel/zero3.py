@@ -123,10 +123,10 @@ class Zero3:
 
     def graph_ok(self):
         """A captured ZeRO-3 step records its all-gathers / reduce-scatters into the graph: on one
-        rank there are none; across ranks only with MFT_GRAPH_COMM=1 (the opt-in of recorded RCCL
-        collectives, parallel/ddp.py) -- otherwise the step runs eagerly."""
+        rank there are none; across ranks unless MFT_GRAPH_COMM=0 (recorded RCCL collectives,
+        parallel/ddp.py) -- then the step runs eagerly."""
         import os
-        return self.world == 1 or os.environ.get("MFT_GRAPH_COMM", "0") == "1"
+        return self.world == 1 or os.environ.get("MFT_GRAPH_COMM", "1") == "1"
 
     def __init__(self, units, device, group=None, prefetch: bool = True, **adamw_kwargs):
         self.group = group

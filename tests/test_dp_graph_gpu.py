@@ -1,9 +1,9 @@
 """Data-parallel reducers with the hipGraph step, on one GPU with a 1-rank RCCL group
 (MFT_DP_FORCE_COMM=1 keeps the collectives even though there is nothing to average): the bucketed
-all-reduce (DDP), its bf16 variant and the ZeRO-2 reduce-to-owner buckets run after each replay
-(the default) while RCCL's watchdog polls during the capture, and the replayed steps equal the no-DP
-step.  MFT_TEST_GRAPH_COMM=1 additionally runs them with the collectives recorded into the graph
-from the backward's grad-ready hooks (MFT_GRAPH_COMM=1, opt-in)."""
+all-reduce (DDP), its bf16 variant and the ZeRO-2 per-bucket reduce-scatter, both recorded into the
+graph from the backward's grad-ready hooks (MFT_GRAPH_COMM=1, the default) and run after each
+replay (MFT_GRAPH_COMM=0), while RCCL's watchdog polls during the capture; the replayed steps equal
+the no-DP step."""
 import os
 
 import pytest
@@ -59,7 +59,7 @@ def _run(kind, steps=6, graph_comm=False):
     return losses, w
 
 
-MODES = [False] + ([True] if os.environ.get("MFT_TEST_GRAPH_COMM") == "1" else [])
+MODES = [False, True]  # eager reduction after the replay / collectives recorded into the graph (default)
 
 
 @pytest.mark.parametrize("graph_comm", MODES)
