@@ -505,7 +505,10 @@ __device__ unsigned long long* g8_stamps;
 // of adding to it: +1-4 % on every NT shape measured (profiles/r3_g8late.txt).  (Reads complete
 // before the phase's MFMAs; the half-tile they read is restaged only after the phase's second
 // barrier, so the order is safe.)  LATE = false keeps the earlier order for A/B runs.
-template <int EPI, bool AT, bool BT, bool LATE = true>
+// KEEPB defaults on where the 16 extra VGPRs fit without spilling (not the TT wgrad form, the LoRA
+// epilogue or the CE dgrad, which spill 2-7 VGPRs with it)
+template <int EPI, bool AT, bool BT, bool LATE = true,
+          bool KEEPB = !(AT && BT) && EPI != GEMM_EPI_LORA && EPI != GEMM_EPI_CE_DGRAD>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   G8_STAMP(0);
@@ -548,7 +551,9 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[q][i][j] = zero4();
 
-  bf16x8_t af[4][2], bfr[2][2];
+  // B fragments per 128-column half: with KEEPB the (A1, B0) phase reuses the B0 fragments its
+  // (A0, B0) phase read (+16 VGPRs, 4 of the 28 ds_read_b128 per wave and K-tile saved)
+  bf16x8_t af[4][2], bfr2[2][2][2];
   auto read_a = [&](int buf, int ah) {
     const bf16_t* t = half_ptr(buf, ah);
 #pragma unroll
@@ -565,8 +570,8 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        if constexpr (BT) bfr[j][ks] = frag8_t(t, wn * 32 + j * 16, ks * 4);
-        else bfr[j][ks] = frag8(t, wn * 32 + j * 16, ks * 4);
+        if constexpr (BT) bfr2[KEEPB ? bh : 0][j][ks] = frag8_t(t, wn * 32 + j * 16, ks * 4);
+        else bfr2[KEEPB ? bh : 0][j][ks] = frag8(t, wn * 32 + j * 16, ks * 4);
       }
   };
   auto mma = [&](int q) {
@@ -576,7 +581,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[q][i][j] = mfma16(bfr[j][ks], af[i][ks], acc[q][i][j]);
+        for (int j = 0; j < 2; ++j) acc[q][i][j] = mfma16(bfr2[KEEPB && (q == 1 || q == 2)][j][ks], af[i][ks], acc[q][i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -636,7 +641,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
                 acc[q][i][j][e] = x;
               }
             }
-            acc[q][i][j] = mfma16(bfr[j][ks], af[i][ks], acc[q][i][j]);
+            acc[q][i][j] = mfma16(bfr2[KEEPB && (q == 1 || q == 2)][j][ks], af[i][ks], acc[q][i][j]);
           }
       __builtin_amdgcn_s_setprio(0);
     } else {
@@ -721,7 +726,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     if (b1_ok) mma_ce(2, rq2);
     raw_barrier();
     // phase 4: (A1, B0); stage E.B1 (kt+2); retire the odd buffer
-    read_b(0, 0);
+    if constexpr (!KEEPB) read_b(0, 0);
     const f32x4_t rq3 = ce_read(3, kt);
     stage(0, 3, kt + 2);
     pre_sync_vm();
@@ -754,7 +759,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     if (odd_ok && b1_ok) mma(2);
     raw_barrier();
     // phase 8: (A1, B0); stage O.B1 (kt+3); retire the even buffer
-    read_b(1, 0);
+    if constexpr (!KEEPB) read_b(1, 0);
     stage(1, 3, kt + 3);
     pre_sync_vm();
     if (odd_ok) mma(3);
@@ -1061,14 +1066,19 @@ static int g_stream = -1;
 static bool gemm8_stream() {
   if (g_stream < 0) {
     const char* e = getenv("MFT_GEMM8_STREAM");
-    g_stream = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+    g_stream = (e && e[0] >= '1' && e[0] <= '3') ? e[0] - '0' : 0;
   }
   return g_stream == 1;
 }
-void gemm8_set_stream(int on) { g_stream = on; }  // 0 default, 1 streaming form, 2 early-wait phase order (NT A/B)
+// 0 default, 1 streaming form, 2 early-wait phase order, 3 LATE without B0 reuse (NT A/Bs)
+void gemm8_set_stream(int on) { g_stream = on; }
 static bool gemm8_early() {
   gemm8_stream();
   return g_stream == 2;
+}
+static bool gemm8_nokeepb() {
+  gemm8_stream();
+  return g_stream == 3;
 }
 
 template <int EPI, bool AT, bool BT>
@@ -1100,11 +1110,21 @@ static void launch8(const GemmArgs& g, hipStream_t st) {
     if (gemm8_early()) {
       static bool attr_l = false;
       if (!attr_l) {
-        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI, AT, BT, false>,
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI, AT, BT, false, false>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
         attr_l = true;
       }
-      gemm8_kernel<EPI, AT, BT, false><<<tiles * ks, 512, shm, st>>>(g);
+      gemm8_kernel<EPI, AT, BT, false, false><<<tiles * ks, 512, shm, st>>>(g);
+      return;
+    }
+    if (gemm8_nokeepb()) {
+      static bool attr_k = false;
+      if (!attr_k) {
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI, AT, BT, true, false>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        attr_k = true;
+      }
+      gemm8_kernel<EPI, AT, BT, true, false><<<tiles * ks, 512, shm, st>>>(g);
       return;
     }
   }

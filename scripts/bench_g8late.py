@@ -1,8 +1,9 @@
-"""gemm8 phase-order A/B on the NT shapes: variant 2 (early: lgkmcnt(0) then s_barrier) vs variant 0 (the
-default LATE order: s_barrier then lgkmcnt(0), B fragments first) vs hipBLASLt (torch.mm).  Each variant is checked
-against an fp32 reference first; interleaved rounds, min over rounds.
+"""gemm8 variant A/B on the NT shapes: variant 0 (the default: LATE order -- s_barrier then lgkmcnt(0), B
+fragments first -- with B0 fragment reuse), 2 (early: lgkmcnt(0) then s_barrier, no reuse), 3 (LATE without the B0
+reuse) vs hipBLASLt (torch.mm).  Each variant is checked against an fp32 reference first; interleaved rounds, min
+over rounds.
 
-usage: PYTHONPATH=. python scripts/bench_g8late.py [--iters 10] [--rounds 4]
+usage: PYTHONPATH=. python scripts/bench_g8late.py [--iters 10] [--rounds 4] [--variants 2,3,0]
 """
 import argparse
 
@@ -27,8 +28,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--variants", default="2,0")
     a = ap.parse_args()
     C = native()
+    vs = [int(v) for v in a.variants.split(",")]
+    labels = {0: "gemm8", 2: "g8-early", 3: "g8-nokeepb"}
     shapes = [("gpt2 qkv fwd", 131072, 768, 2304), ("gpt2 proj fwd", 131072, 768, 768),
               ("gpt2 fc fwd", 131072, 768, 3072), ("gpt2 mproj fwd", 131072, 3072, 768),
               ("gpt2 lm_head", 32768, 768, 50304), ("xl qkv fwd", 8192, 1600, 4800), ("xl fc fwd", 8192, 1600, 6400),
@@ -39,7 +43,7 @@ def main():
         ref = None
         if M * N <= 8192 * 8192:
             ref = x.float() @ w.float().t()
-        for v in (0, 2):
+        for v in vs:
             C.gemm8_set_stream(v)
             y = C.gemm_t(x, w, False, False, 0)[0]
             if ref is not None:
@@ -47,14 +51,15 @@ def main():
                 assert err < 1e-2, (name, v, err)
         del ref
         fl = 2.0 * M * N * K
-        res = {0: [], 2: [], "lt": []}
+        res = {v: [] for v in vs}
+        res["lt"] = []
         for _ in range(a.rounds):
-            for v in (0, 2):
+            for v in vs:
                 C.gemm8_set_stream(v)
                 res[v].append(timeit(lambda: C.gemm_t(x, w, False, False, 0), a.iters))
             res["lt"].append(timeit(lambda: torch.mm(x, w.t()), a.iters))
         line = f"{name:14s} M={M:6d} K={K:5d} N={N:6d} |"
-        for k, lab in ((2, "gemm8-early"), (0, "gemm8-late"), ("lt", "hipBLASLt")):
+        for k, lab in [(v, labels[v]) for v in vs] + [("lt", "hipBLASLt")]:
             t = min(res[k])
             line += f" {lab} {t:8.1f} us {fl / t / 1e6:6.0f} TF |"
         print(line, flush=True)
