@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
   bf16_t* Ks = smem;                // [BK][D]
   bf16_t* Vs = Ks + BK * D;         // [BK][D]
   bf16_t* Ps = Vs + BK * D;         // [4][16][LDP]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * BQ;
   const int hk = h / (H / Hkv);
   const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
   bf16_t* DST = PT + BK * LDT;   // [BK][LDT]  dS^T * scale
   float* lse_s = reinterpret_cast<float*>(DST + BK * LDT);  // [BQ]
   float* del_s = lse_s + BQ;                                 // [BQ]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.z, h = blockIdx.y, kb = blockIdx.x * BK;
   const int hk = h / (H / Hkv);
   const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __re
   bf16_t* Ks = smem;                                      // [SM][D]
   bf16_t* Vs = Ks + SM * D;                               // [SM][D]
   bf16_t* Ow = Vs + SM * D + (threadIdx.x >> 6) * 16 * LDO;  // per-wave [16][LDO] output staging
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const int h = blockIdx.x, b = blockIdx.y, hk = h / (H / Hkv);
   const int kv_len = kv_lens ? min(kv_lens[b], S) : S;
   const float c2 = scale * kLog2e;
@@ -527,7 +527,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
   bf16_t* DS = Vs;
   float* lse_s = reinterpret_cast<float*>(Qs + SM * D);  // [SM]
   float* del_s = lse_s + SM;                             // [SM]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, c16 = lane & 15;
   const int h = blockIdx.x, b = blockIdx.y, hk = h / (H / Hkv);
   const int kv_len = kv_lens ? min(kv_lens[b], S) : S;
   const float c2 = scale * kLog2e;
@@ -667,6 +667,14 @@ constexpr int kSplitBK = 32;  // rows per staged tile
 // their cycles in SQ_WAIT_ANY (tile staging latency), not in LDS.
 constexpr int kSplitPad = 16;
 
+// LDS writes / reads retired, then a raw s_barrier: unlike __syncthreads (whose fence implies
+// vmcnt(0)) it lets global prefetches issued before it stay in flight
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Two 32-row tiles (rows >= nvalid zero-filled) held in registers between the global load and the
 // LDS store, so the NEXT tile's loads are in flight while the current one is multiplied
 // (double-buffered LDS, one barrier per step).  LDS rows are padded to D + kSplitPad elements.
@@ -725,7 +733,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
     int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
   constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + kSplitPad;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // buffer j: K at smem + 2 j BK LD, V after it
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, c16 = lane & 15;
   int tx, h, b;
   split_task(tx, h, b);
   const int q0 = tx * BQ, hk = h / (H / Hkv);
@@ -753,7 +761,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_split_kernel(
   for (int kb = kstart, j = 0; kb < kend; kb += BK, ++j) {
     const bool more = kb + BK < kend;
     if (more) tl.load(k, v, ks, vs, b, hk, kb + BK, min(BK, kv_len - kb - BK));
-    __syncthreads();
+    lds_barrier();  // raw: the prefetch above stays in flight (no implied vmcnt(0))
     const bf16_t* Ks = smem + (j & 1) * 2 * BK * LD;
     const bf16_t* Vs = Ks + BK * LD;
     const bool live = wq_lo < Sq && (!causal || kb <= wq_hi + coff) &&
@@ -837,14 +845,13 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
+__device__ __forceinline__ void dma4(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 4, 0, 0);
+}
 template <int N>
 __device__ __forceinline__ void vmcnt_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row & 7) << 1); }
 
@@ -854,7 +861,7 @@ __device__ __forceinline__ void dma_tile32(bf16_t* lds, const bf16_t* src, AttnS
                                            int rmax) {
   constexpr int CPR = D / 8, OPS = kSplitBK * CPR / 64;  // 1-KB DMA ops per tile
   static_assert(OPS % NW == 0, "every wave issues the same number of DMA ops");
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
   for (int k = 0; k < OPS / NW; ++k) {
     const int o = w + k * NW;
@@ -884,6 +891,45 @@ __device__ __forceinline__ bf16x8_t frag_tr_perm_sw(const bf16_t* t, int r0, int
   return __builtin_bit_cast(bf16x8_t, rr);
 }
 
+// ---- row-pair LDS image of a [32][256] bf16 tile (LDS-DMA target, D = 256) ----------------------
+// One 1-KB LDS-DMA piece (a wave-instruction: 64 lanes x 16 B, lane-linear) holds two 512-B rows;
+// pieces sit at a pitch of 1088 B (64 B pad).  Unlike the XOR swizzle this keeps every fragment
+// read at ONE lane base + immediate offsets (the swizzled form needs a per-K-slice address
+// register: at D = 256 those spilled and serialised the dK/dV loop, scratch reload -> ds_read ->
+// MFMA).  Bank cost: 2-way on the ds_read_b128 row fragments and the ds_read_b64_tr_b16 pairs (the
+// two rows of a piece share banks), which the kernels' LDS budget absorbs.
+constexpr int kPairPitch = 544;  // elements per 2-row piece (1024 B data + 64 B pad)
+constexpr int kPairTile = 16 * kPairPitch;
+__device__ __forceinline__ int pr_row(int r) { return (r >> 1) * kPairPitch + (r & 1) * 256; }
+// rows [row0, row0 + 32) of a [rows][256] operand (rows clamped into [0, rmax)) -> pair image
+template <int NW>
+__device__ __forceinline__ void dma_tile32_pr(bf16_t* lds, const bf16_t* src, AttnStrides st, int b, int h, int row0,
+                                              int rmax) {
+  static_assert(16 % NW == 0, "every wave issues the same number of DMA pieces");
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int k = 0; k < 16 / NW; ++k) {
+    const int o = w + k * NW;
+    const int gr = min(row0 + 2 * o + (lane >> 5), rmax - 1);
+    dma16(src + b * st.sb + (long)gr * st.ss + h * st.sh + (lane & 31) * 8, lds + o * kPairPitch);
+  }
+}
+// frag_row on the pair image (r0 even): lane holds T[r0 + (l&15)][c0 + 8 (l>>4) + j]
+__device__ __forceinline__ bf16x8_t frag_row_pr(const bf16_t* t, int r0, int c0) {
+  const int l = threadIdx.x & 63;
+  return *reinterpret_cast<const bf16x8_t*>(t + (r0 >> 1) * kPairPitch + pr_row(l & 15) + c0 + 8 * (l >> 4));
+}
+// frag_tr_perm (mfma.h) on the pair image, rows 0..31
+__device__ __forceinline__ bf16x8_t frag_tr_pr(const bf16_t* t, int c0) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const bf16_t* a0 = t + pr_row(4 * g + q) + c0 + 4 * p;
+  s16x4_t lo = ds_tr16(a0);
+  s16x4_t hi = ds_tr16(a0 + 8 * kPairPitch);  // row + 16
+  s16x8_t rr = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, rr);
+}
+
 
 // RPW = query rows per wave (16 or 32).  At RPW = 32 every K fragment (ds_read_b128) and V^T
 // fragment (ds_read_b64_tr_b16) read from LDS feeds TWO MFMAs -- one per 16-query half -- so the
@@ -895,10 +941,12 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
     float* __restrict__ lse, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides os, int H, int Hkv, int Sq,
     int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
   constexpr int R = RPW / 16;  // 16-query halves per wave
-  constexpr int BQ = RPW * NW, BK = kSplitBK, TILE = BK * D, LDO = D + kSplitPad;
+  constexpr bool kPair = D == 256;  // row-pair images (one address base per lane), else XOR swizzle
+  constexpr int BQ = RPW * NW, BK = kSplitBK, TILE = kPair ? kPairTile : BK * D, LDO = D + kSplitPad;
   constexpr int OPW = 2 * (BK * D / 8 / 64) / NW;  // DMA ops per wave per ring stage (K + V)
+  constexpr int RG = kPair ? 4 : kRing;  // ring depth: RG - 1 tiles in flight (4 x 34 KB at D = 256)
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // ring stage s: K at smem + 2 s TILE, V after
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, c16 = lane & 15;
   int tx, h, b;
   split_task(tx, h, b);
   const int q0 = tx * BQ, hk = h / (H / Hkv);
@@ -920,11 +968,16 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
       qf[r][s2] = qi < Sq ? *reinterpret_cast<const bf16x8_t*>(q + b * qs.sb + (long)qi * qs.ss + h * qs.sh + s2 * 32 + 8 * g)
                           : bf16x8_t{};
   }
-  auto issue = [&](int j) {  // ring stage j % 3 <- tile min(j, nt - 1) (tail re-reads keep counts uniform)
+  auto issue = [&](int j) {  // ring stage j % RG <- tile min(j, nt - 1) (tail re-reads keep counts uniform)
     const int kb = kstart + min(j, nt - 1) * BK;
-    bf16_t* st = smem + (j % kRing) * 2 * TILE;
-    dma_tile32<D, NW>(st, k, ks, b, hk, kb, kv_len);
-    dma_tile32<D, NW>(st + TILE, v, vs, b, hk, kb, kv_len);
+    bf16_t* st = smem + (j % RG) * 2 * TILE;
+    if constexpr (kPair) {
+      dma_tile32_pr<NW>(st, k, ks, b, hk, kb, kv_len);
+      dma_tile32_pr<NW>(st + TILE, v, vs, b, hk, kb, kv_len);
+    } else {
+      dma_tile32<D, NW>(st, k, ks, b, hk, kb, kv_len);
+      dma_tile32<D, NW>(st + TILE, v, vs, b, hk, kb, kv_len);
+    }
   };
   f32x4_t acc[R][D / 16];
 #pragma unroll
@@ -935,15 +988,15 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
 #pragma unroll
   for (int r = 0; r < R; ++r) m[r] = -INFINITY, l[r] = 0.f;
   if (nt > 0) {
-    issue(0);
-    issue(1);
+#pragma unroll
+    for (int j = 0; j < RG - 1; ++j) issue(j);
   }
   for (int j = 0; j < nt; ++j) {
-    vmcnt_wait<OPW>();  // this wave's ops for stage j are done (stage j + 1 may still fly)
-    lds_barrier();      // ... and every other wave's; stage (j + 2) % 3 was last read in step j - 1
-    issue(j + 2);
+    vmcnt_wait<OPW * (RG - 2)>();  // this wave's ops for stage j are done (later stages may still fly)
+    lds_barrier();      // ... and every other wave's; stage (j + RG - 1) % RG was last read in step j - 1
+    issue(j + RG - 1);
     const int kb = kstart + j * BK;
-    const bf16_t* Ks = smem + (j % kRing) * 2 * TILE;
+    const bf16_t* Ks = smem + (j % RG) * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
     const bool live = wq_lo < Sq && (!causal || kb <= wq_hi + coff) &&
                       (window <= 0 || wq_lo + coff - (kb + BK - 1) < window);
@@ -955,7 +1008,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
         for (int r = 0; r < R; ++r) st[r][t] = zero4();
 #pragma unroll
         for (int s2 = 0; s2 < D / 32; ++s2) {
-          const bf16x8_t kf = frag_row_sw<D>(Ks, 16 * t, s2 * 32);
+          const bf16x8_t kf = kPair ? frag_row_pr(Ks, 16 * t, s2 * 32) : frag_row_sw<D>(Ks, 16 * t, s2 * 32);
 #pragma unroll
           for (int r = 0; r < R; ++r) st[r][t] = mfma16(kf, qf[r][s2], st[r][t]);
         }
@@ -1008,7 +1061,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
       }
 #pragma unroll
       for (int n = 0; n < D / 16; ++n) {
-        const bf16x8_t vf = frag_tr_perm_sw<D>(Vs, 0, n * 16);
+        const bf16x8_t vf = kPair ? frag_tr_pr(Vs, n * 16) : frag_tr_perm_sw<D>(Vs, 0, n * 16);
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r][n] = mfma16(pa[r], vf, acc[r][n]);
       }
@@ -1028,31 +1081,15 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
   }
 }
 
-// two 32-row tiles (rows >= nvalid zero-filled) -> lds0/lds1 [32][D + kSplitPad]; all loads issue first
-template <int D, int NT>
-__device__ __forceinline__ void stage32x2(bf16_t* lds0, bf16_t* lds1, const bf16_t* src0, const bf16_t* src1,
-                                          AttnStrides s0, AttnStrides s1, int b, int h, int row0, int nvalid) {
-  constexpr int CPR = D / 8, LD = D + kSplitPad, PER = (kSplitBK * CPR + NT - 1) / NT;
-  u16x8_t r0[PER], r1[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int c = threadIdx.x + j * NT, r = c / CPR, ch = c % CPR;
-    const bool ok = c < kSplitBK * CPR && r < nvalid;
-    r0[j] = ok ? *reinterpret_cast<const u16x8_t*>(src0 + b * s0.sb + (long)(row0 + r) * s0.ss + h * s0.sh + ch * 8)
-               : u16x8_t{};
-    r1[j] = ok ? *reinterpret_cast<const u16x8_t*>(src1 + b * s1.sb + (long)(row0 + r) * s1.ss + h * s1.sh + ch * 8)
-               : u16x8_t{};
-  }
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int c = threadIdx.x + j * NT, r = c / CPR, ch = c % CPR;
-    if (c < kSplitBK * CPR) {
-      *reinterpret_cast<u16x8_t*>(lds0 + r * LD + ch * 8) = r0[j];
-      *reinterpret_cast<u16x8_t*>(lds1 + r * LD + ch * 8) = r1[j];
-    }
-  }
-}
-
+// The (q-head, query tile) sweep is software-pipelined: the NEXT tile's Q / dO rows and row
+// statistics are fetched while the current tile is multiplied, into the other half of a double-
+// buffered LDS image -- one raw barrier per tile (the previous form staged every tile synchronously
+// between two __syncthreads, whose implied vmcnt(0) exposed the whole global-load latency).
+// D = 256: the tiles go global -> LDS by LDS-DMA (no VGPRs: the 16-key-per-wave dK/dV accumulators
+// plus register staging spill at D = 256) into row-pair images (frag_row_pr / frag_tr_pr, one
+// address base per lane); smaller D: register staging (Tile2) into rows padded to D + kSplitPad.
+// The causal / window / padding mask is a select in front of the exp (exp2(-inf) = 0), not a
+// branch around it: the branch split every step into divergent blocks the MFMAs could not cross.
 template <int D, int NW>
 __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
@@ -1060,13 +1097,15 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
     bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides dos,
     AttnStrides dks, AttnStrides dvs, int H, int Hkv, int Sq, int Sk, float scale, int causal, int window,
     const int* __restrict__ kv_lens) {
+  constexpr bool kDma = D == 256;
   constexpr int NT = 64 * NW, BKEY = 16 * NW, BQ = kSplitBK, LD = D + kSplitPad;
+  constexpr int TILE = kDma ? kPairTile : BQ * LD;  // elements of one staged [BQ] x D tile
+  // DMA: a 3-slot ring, two tiles in flight; register staging: 2 buffers
+  constexpr int RG = kDma ? 3 : 2, OPT = 2 * (16 / NW) + 1;  // slots; DMA ops per wave per tile (+ row stats)
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  bf16_t* Qs = smem;            // [BQ][LD]
-  bf16_t* dOs = Qs + BQ * LD;   // [BQ][LD]
-  float* ls = reinterpret_cast<float*>(dOs + BQ * LD);  // [BQ] lse * log2 e
-  float* dl = ls + BQ;                                  // [BQ] delta
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  // slot j: Q at smem + 2 j TILE, dO after it; row floats [j][lse | delta][BQ] after every slot
+  float* const rowf = reinterpret_cast<float*>(smem + 2 * RG * TILE);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, c16 = lane & 15;
   int tx, hk, b;
   split_task(tx, hk, b);
   const int kb = tx * BKEY, G = H / Hkv;
@@ -1075,6 +1114,52 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
   const float c2 = scale * kLog2e;
   const int wk_lo = kb + 16 * w, wk_hi = wk_lo + 15;
   const int key = wk_lo + c16;  // this lane's key (C column of S = Q K^T)
+  int qstart = 0, qend = Sq;
+  if (causal) qstart = max(0, kb - coff) / BQ * BQ;
+  if (window > 0) qend = min(Sq, kb + BKEY - 1 - coff + window);
+  if (kb >= kv_len) qend = qstart;  // fully padded key block: grads are zero
+  const int nq = qend > qstart ? (qend - qstart + BQ - 1) / BQ : 0;
+  const int total = G * nq;  // (q-head, query tile) steps, WG-uniform
+  Tile2<D, NT> tl;
+  float ls_r = 0.f, dl_r = 0.f;  // register staging: the prefetched tile's row statistics (threads < BQ)
+  auto load = [&](int it, int j) {  // start fetching step it's tile into slot j
+    const int h = hk * G + it / nq, q0 = qstart + (it % nq) * BQ;
+    const long rs = ((long)b * H + h) * Sq;
+    if constexpr (kDma) {
+      dma_tile32_pr<NW>(smem + 2 * j * TILE, q, qs, b, h, q0, Sq);  // rows past Sq: clamped, masked below
+      dma_tile32_pr<NW>(smem + (2 * j + 1) * TILE, dout, dos, b, h, q0, Sq);
+      // row statistics by one 4-byte DMA per wave (every wave the same bytes: uniform vmcnt counts):
+      // lanes 0-31 the tile's lse, lanes 32-63 its delta
+      const int r = min(q0 + (lane & 31), Sq - 1);
+      dma4((lane < 32 ? lse : delta) + rs + r, rowf + j * 2 * BQ);
+    } else {
+      tl.load(q, dout, qs, dos, b, h, q0, min(BQ, Sq - q0));
+      if (threadIdx.x < BQ) {
+        const int qi = q0 + threadIdx.x;
+        ls_r = qi < Sq ? lse[rs + qi] : 1e30f;
+        dl_r = qi < Sq ? delta[rs + qi] : 0.f;
+      }
+    }
+  };
+  auto land = [&](int j) {  // register staging: buffer j complete for every wave after the next barrier
+    tl.store(smem + 2 * j * TILE, smem + (2 * j + 1) * TILE);
+    if (threadIdx.x < BQ) {
+      rowf[j * 2 * BQ + threadIdx.x] = ls_r;
+      rowf[j * 2 * BQ + BQ + threadIdx.x] = dl_r;
+    }
+  };
+  auto frow = [&](const bf16_t* t, int r0, int c0) {
+    if constexpr (kDma) return frag_row_pr(t, r0, c0);
+    else return frag_row(t, LD, r0, c0);
+  };
+  auto ftr = [&](const bf16_t* t, int c0) {
+    if constexpr (kDma) return frag_tr_pr(t, c0);
+    else return frag_tr_perm(t, LD, 0, c0);
+  };
+  if (total > 0) {
+    load(0, 0);
+    if constexpr (kDma) load(min(1, total - 1), 1);  // past the end: the last tile again (uniform counts)
+  }
   bf16x8_t kf[D / 32], vf[D / 32];  // B operands: K[key][32 s + 8 g + j], V[key][...]
 #pragma unroll
   for (int s = 0; s < D / 32; ++s) {
@@ -1084,28 +1169,33 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
     vf[s] = ok ? *reinterpret_cast<const bf16x8_t*>(v + b * vs.sb + (long)key * vs.ss + hk * vs.sh + s * 32 + 8 * g)
                : bf16x8_t{};
   }
+  if constexpr (!kDma) {
+    if (total > 0) land(0);
+  }
   f32x4_t dKa[D / 16], dVa[D / 16];
 #pragma unroll
   for (int n = 0; n < D / 16; ++n) { dKa[n] = zero4(); dVa[n] = zero4(); }
-  int qstart = 0, qend = Sq;
-  if (causal) qstart = max(0, kb - coff) / BQ * BQ;
-  if (window > 0) qend = min(Sq, kb + BKEY - 1 - coff + window);
-  if (kb >= kv_len) qend = qstart;  // fully padded key block: grads are zero
   const bool wave_keys = wk_lo < kv_len;
-  for (int gi = 0; gi < G; ++gi) {
-    const int h = hk * G + gi;
-    for (int q0 = qstart; q0 < qend; q0 += BQ) {
-      __syncthreads();
-      stage32x2<D, NT>(Qs, dOs, q, dout, qs, dos, b, h, q0, min(BQ, Sq - q0));
-      if (threadIdx.x < BQ) {
-        const int qi = q0 + threadIdx.x;
-        ls[threadIdx.x] = qi < Sq ? lse[((long)b * H + h) * Sq + qi] * kLog2e : 1e30f;
-        dl[threadIdx.x] = qi < Sq ? delta[((long)b * H + h) * Sq + qi] : 0.f;
-      }
-      __syncthreads();
-      const bool live = wave_keys && (!causal || q0 + BQ - 1 + coff >= wk_lo) &&
-                        (window <= 0 || q0 + coff - wk_hi < window);
-      if (!live) continue;
+  for (int it = 0; it < total; ++it) {
+    const bool more = it + 1 < total;
+    if constexpr (kDma) {
+      vmcnt_wait<OPT>();  // this wave's pieces of step it's tile landed (step it + 1's may still fly)
+      lds_barrier();      // ... and every wave's; slot (it + 2) % 3, read in step it - 1, is free
+      load(min(it + 2, total - 1), (it + 2) % RG);
+    } else {
+      // step it's buffer stored by every wave; the other buffer, read in step it - 1, is free.  Raw
+      // barrier: the register prefetch below stays in flight across the next one.
+      lds_barrier();
+      if (more) load(it + 1, (it + 1) & 1);
+    }
+    const int j = it % RG, q0 = qstart + (it % nq) * BQ;
+    const bf16_t* Qs = smem + 2 * j * TILE;
+    const bf16_t* dOs = Qs + TILE;
+    const float* ls = rowf + j * 2 * BQ;
+    const float* dl = ls + BQ;
+    const bool live = wave_keys && (!causal || q0 + BQ - 1 + coff >= wk_lo) &&
+                      (window <= 0 || q0 + coff - wk_hi < window);
+    if (live) {
       f32x4_t sc[2], dp[2];  // [t][i] = S / dP [query q0 + 16 t + 4 g + i][key]
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -1113,27 +1203,36 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
         dp[t] = zero4();
 #pragma unroll
         for (int s = 0; s < D / 32; ++s) {
-          sc[t] = mfma16(frag_row(Qs, LD, 16 * t, s * 32), kf[s], sc[t]);
-          dp[t] = mfma16(frag_row(dOs, LD, 16 * t, s * 32), vf[s], dp[t]);
+          sc[t] = mfma16(frow(Qs, 16 * t, s * 32), kf[s], sc[t]);
+          dp[t] = mfma16(frow(dOs, 16 * t, s * 32), vf[s], dp[t]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int qr = 16 * t + 4 * g + i, qi = q0 + qr;
           const bool ok = qi < Sq && attn_allowed(qi, key, kv_len, coff, causal, window);
-          const float p = ok ? fast_exp2(sc[t][i] * c2 - ls[qr]) : 0.f;
+          // unconditional reads, pinned (asm) so the compiler cannot sink them into a branch
+          float lsq = ls[qr], dlq = dl[qr];
+          asm volatile("" : "+v"(lsq), "+v"(dlq));
+          float x = sc[t][i] * c2 - lsq * kLog2e;
+          asm volatile("" : "+v"(x));
+          const float p = fast_exp2(ok ? x : -INFINITY);
           sc[t][i] = p;
-          dp[t][i] = p * (dp[t][i] - dl[qr]) * scale;
+          dp[t][i] = p * (dp[t][i] - dlq) * scale;
         }
       }
       const bf16x8_t pa = pack_c2a(sc[0], sc[1]);  // A: m = key, k = query (permuted)
       const bf16x8_t da = pack_c2a(dp[0], dp[1]);
 #pragma unroll
       for (int n = 0; n < D / 16; ++n) {
-        dVa[n] = mfma16(pa, frag_tr_perm(dOs, LD, 0, n * 16), dVa[n]);
-        dKa[n] = mfma16(da, frag_tr_perm(Qs, LD, 0, n * 16), dKa[n]);
+        dVa[n] = mfma16(pa, ftr(dOs, n * 16), dVa[n]);
+        dKa[n] = mfma16(da, ftr(Qs, n * 16), dKa[n]);
       }
     }
+    if constexpr (!kDma) {
+      if (more) land((it + 1) & 1);
+    }
   }
+  vmcnt_wait<0>();  // the tail's re-read DMA must land before the LDS is reused
   __syncthreads();  // Q/dO tiles dead: reuse LDS as per-wave output staging
   const float one[4] = {1.f, 1.f, 1.f, 1.f};
   if (wk_lo < Sk) {
@@ -1143,15 +1242,29 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
   }
 }
 
-template <int D, int NW>
+// D = 256: K / V tiles by LDS-DMA into row-pair images (no staging VGPRs, no per-element load
+// predicates -- those became 8 divergent branches per step) prefetched one tile ahead; smaller D:
+// register staging (Tile2) into padded rows.  The mask is a select in front of the exp.
+// delta = rowsum(dO * O) of the wave's queries is computed here from the dO fragments the kernel
+// holds anyway (+ one pass over the O row) and written out for the dK/dV kernel, which runs after
+// this one -- no separate delta pass over O and dO.
+// RGD: DMA ring slots (2: one tile of prefetch, 3: two); FOLD: compute delta here (else read it)
+template <int D, int NW, int RGD = 2, bool FOLD = true>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
-    bf16_t* __restrict__ dq, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides dos, AttnStrides dqs, int H,
-    int Hkv, int Sq, int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
+    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ o, const float* __restrict__ lse,
+    float* __restrict__ delta, bf16_t* __restrict__ dq, AttnStrides qs, AttnStrides ks, AttnStrides vs,
+    AttnStrides dos, AttnStrides oss, AttnStrides dqs, int H, int Hkv, int Sq, int Sk, float scale, int causal,
+    int window, const int* __restrict__ kv_lens) {
+  constexpr bool kDma = D == 256;
   constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + kSplitPad;
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // buffer j: K, V tiles at smem + 2 j BK LD
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  constexpr int TILE = kDma ? kPairTile : BK * LD;
+  // DMA: a 3-slot ring, two tiles in flight (a step is only 48 MFMAs per wave: one tile of prefetch
+  // leaves the load latency exposed); register staging: 2 buffers
+  constexpr int RG = kDma ? RGD : 2, OPT = 2 * (16 / NW);  // ring slots; DMA ops per wave per tile
+  constexpr int PF = RG - 1;                                // tiles of prefetch
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // slot j: K at smem + 2 j TILE, V after it
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, c16 = lane & 15;
   int tx, h, b;
   split_task(tx, h, b);
   const int q0 = tx * BQ, hk = h / (H / Hkv);
@@ -1164,8 +1277,36 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
   if (causal) kend = min(kend, q0 + BQ + coff);
   int kstart = 0;
   if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
+  const int nt = kend > kstart ? (kend - kstart + BK - 1) / BK : 0;  // key tiles, WG-uniform
   Tile2<D, NT> tl;
-  if (kstart < kend) tl.load(k, v, ks, vs, b, hk, kstart, min(BK, kv_len - kstart));
+  auto load = [&](int kb, int j) {  // start fetching key tile kb into slot j
+    if constexpr (kDma) {
+      dma_tile32_pr<NW>(smem + 2 * j * TILE, k, ks, b, hk, kb, kv_len);  // rows past kv_len: clamped, masked
+      dma_tile32_pr<NW>(smem + (2 * j + 1) * TILE, v, vs, b, hk, kb, kv_len);
+    } else {
+      tl.load(k, v, ks, vs, b, hk, kb, min(BK, kv_len - kb));
+    }
+  };
+  auto land = [&](int j) {
+    if constexpr (kDma) vmcnt_wait<0>();
+    else tl.store(smem + 2 * j * TILE, smem + (2 * j + 1) * TILE);
+  };
+  auto frow = [&](const bf16_t* t, int r0, int c0) {
+    if constexpr (kDma) return frag_row_pr(t, r0, c0);
+    else return frag_row(t, LD, r0, c0);
+  };
+  auto ftr = [&](const bf16_t* t, int c0) {
+    if constexpr (kDma) return frag_tr_pr(t, c0);
+    else return frag_tr_perm(t, LD, 0, c0);
+  };
+  if constexpr (kDma) {  // tiles 0 .. PF - 1 (past the end: the last tile again, keeping the counts uniform)
+    if (nt > 0) {
+#pragma unroll
+      for (int t = 0; t < PF; ++t) load(kstart + min(t, nt - 1) * BK, t);
+    }
+  } else {
+    if (nt > 0) load(kstart, 0);
+  }
   bf16x8_t qf[D / 32], df[D / 32];  // B operands: Q[qi][32 s + 8 g + j], dO[qi][...]
 #pragma unroll
   for (int s = 0; s < D / 32; ++s) {
@@ -1176,17 +1317,41 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
                : bf16x8_t{};
   }
   const float lq = qi < Sq ? lse[((long)b * H + h) * Sq + qi] * kLog2e : 1e30f;
-  const float dlq = qi < Sq ? delta[((long)b * H + h) * Sq + qi] : 0.f;
-  if (kstart < kend) tl.store(smem, smem + BK * LD);
+  float dlq = 0.f;  // delta of query qi: this lane's 64 of the D products, summed over the 4 lane groups
+  if constexpr (!FOLD) {
+    dlq = qi < Sq ? delta[((long)b * H + h) * Sq + qi] : 0.f;
+  } else {
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    const bf16x8_t ov = qi < Sq ? *reinterpret_cast<const bf16x8_t*>(o + b * oss.sb + (long)qi * oss.ss + h * oss.sh +
+                                                                     s * 32 + 8 * g)
+                                : bf16x8_t{};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dlq += static_cast<float>(ov[e]) * static_cast<float>(df[s][e]);
+  }
+  dlq += xor16_pl(dlq);
+  dlq += xor32_pl(dlq);
+  if (g == 0 && qi < Sq) delta[((long)b * H + h) * Sq + qi] = dlq;
+  }
+  if constexpr (!kDma) {
+    if (nt > 0) land(0);
+  }
   f32x4_t dQa[D / 16];
 #pragma unroll
   for (int n = 0; n < D / 16; ++n) dQa[n] = zero4();
-  for (int kb = kstart, j = 0; kb < kend; kb += BK, ++j) {
-    const bool more = kb + BK < kend;
-    if (more) tl.load(k, v, ks, vs, b, hk, kb + BK, min(BK, kv_len - kb - BK));
-    __syncthreads();
-    const bf16_t* Ks = smem + (j & 1) * 2 * BK * LD;
-    const bf16_t* Vs = Ks + BK * LD;
+  for (int j = 0; j < nt; ++j) {
+    const int kb = kstart + j * BK;
+    const bool more = j + 1 < nt;
+    if constexpr (kDma) {
+      vmcnt_wait<OPT * (PF - 1)>();  // this wave's pieces of tile j landed (later tiles may still fly)
+      lds_barrier();                 // ... and every wave's; slot (j + PF) % RG, read in step j - 1, is free
+      load(kstart + min(j + PF, nt - 1) * BK, (j + PF) % RG);
+    } else {
+      if (more) load(kb + BK, (j + 1) & 1);  // registers: in flight across the raw barrier
+      lds_barrier();  // tile j stored by every wave; buffer (j + 1) & 1, read in step j - 1, is free
+    }
+    const bf16_t* Ks = smem + 2 * (j % RG) * TILE;
+    const bf16_t* Vs = Ks + TILE;
     const bool live = wq_lo < Sq && (!causal || kb <= wq_hi + coff) &&
                       (window <= 0 || wq_lo + coff - (kb + BK - 1) < window);
     if (live) {
@@ -1197,25 +1362,27 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
         dpt[t] = zero4();
 #pragma unroll
         for (int s = 0; s < D / 32; ++s) {
-          st[t] = mfma16(frag_row(Ks, LD, 16 * t, s * 32), qf[s], st[t]);
-          dpt[t] = mfma16(frag_row(Vs, LD, 16 * t, s * 32), df[s], dpt[t]);
+          st[t] = mfma16(frow(Ks, 16 * t, s * 32), qf[s], st[t]);
+          dpt[t] = mfma16(frow(Vs, 16 * t, s * 32), df[s], dpt[t]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const bool ok = qi < Sq && attn_allowed(qi, kb + 16 * t + 4 * g + i, kv_len, coff, causal, window);
-          const float p = ok ? fast_exp2(st[t][i] * c2 - lq) : 0.f;
+          float x = st[t][i] * c2 - lq;
+          asm volatile("" : "+v"(x));  // a select, not a branch around the exp
+          const float p = fast_exp2(ok ? x : -INFINITY);
           dpt[t][i] = p * (dpt[t][i] - dlq) * scale;
         }
       }
       const bf16x8_t da = pack_c2a(dpt[0], dpt[1]);  // A: m = query, k = key (permuted)
 #pragma unroll
-      for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(da, frag_tr_perm(Ks, LD, 0, n * 16), dQa[n]);
+      for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(da, ftr(Ks, n * 16), dQa[n]);
     }
-    if (more) {
-      bf16_t* nb = smem + ((j + 1) & 1) * 2 * BK * LD;
-      tl.store(nb, nb + BK * LD);
+    if constexpr (!kDma) {
+      if (more) land((j + 1) & 1);
     }
   }
+  vmcnt_wait<0>();  // the tail's re-read DMA must land before the LDS is reused
   __syncthreads();
   const float one[4] = {1.f, 1.f, 1.f, 1.f};
   if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * LD, LD, dQa, one, dq, dqs, b, h, wq_lo, min(16, Sq - wq_lo));
@@ -1262,7 +1429,8 @@ static void fwd_split_launch(const AttnArgs& a, hipStream_t stream) {
 
 template <int D, int NW, int RPW>
 static void fwd_dma_launch_rpw(const AttnArgs& a, hipStream_t stream) {
-  const size_t shm = std::max(sizeof(bf16_t) * kRing * 2 * kSplitBK * D, sizeof(bf16_t) * NW * 16 * (D + kSplitPad));
+  const size_t shm = std::max(D == 256 ? sizeof(bf16_t) * 4 * 2 * kPairTile : sizeof(bf16_t) * kRing * 2 * kSplitBK * D,
+                              sizeof(bf16_t) * NW * 16 * (D + kSplitPad));
   static bool attr = false;
   if (!attr) {
     MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_dma_kernel<D, NW, RPW>,
@@ -1286,7 +1454,10 @@ static void fwd_dma_launch(const AttnArgs& a, hipStream_t stream) {
 template <int D, int NW>
 static void dkdv_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
   constexpr int LD = D + kSplitPad;
-  const size_t shm = std::max(sizeof(bf16_t) * 2 * kSplitBK * LD + sizeof(float) * 2 * kSplitBK,
+  // two {Q, dO} tile buffers (row-pair images for the D = 256 LDS-DMA form) + their row statistics, or the
+  // epilogue's per-wave output staging
+  const size_t shm = std::max(D == 256 ? sizeof(bf16_t) * 6 * kPairTile + sizeof(float) * 6 * kSplitBK
+                                        : sizeof(bf16_t) * 4 * kSplitBK * LD + sizeof(float) * 4 * kSplitBK,
                               sizeof(bf16_t) * NW * 16 * LD);
   static bool attr = false;
   if (!attr) {
@@ -1299,18 +1470,42 @@ static void dkdv_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
       mk(a.dk_st), mk(a.dv_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale, a.causal, a.window, a.kv_lens);
 }
 
-template <int D, int NW>
-static void dq_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
-  const size_t shm = split_shm<D, NW>(0);
+template <int D, int NW, int RGD, bool FOLD>
+static void dq_split_launch_v(const AttnBwdArgs& a, hipStream_t stream) {
+  const size_t shm = D == 256 ? std::max(sizeof(bf16_t) * RGD * 2 * kPairTile, sizeof(bf16_t) * NW * 16 * (D + kSplitPad))
+                              : split_shm<D, NW>(0);
   static bool attr = false;
   if (!attr) {
-    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, NW>,
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, NW, RGD, FOLD>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  attn_bwd_dq_kernel<D, NW><<<dim3(cdiv(a.Sq, 16 * NW), a.H, a.B), 64 * NW, shm, stream>>>(
-      a.q, a.k, a.v, a.dout, a.lse, a.delta, a.dq, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.do_st), mk(a.dq_st), a.H,
-      a.Hkv, a.Sq, a.Sk, a.scale, a.causal, a.window, a.kv_lens);
+  attn_bwd_dq_kernel<D, NW, RGD, FOLD><<<dim3(cdiv(a.Sq, 16 * NW), a.H, a.B), 64 * NW, shm, stream>>>(
+      a.q, a.k, a.v, a.dout, a.o, a.lse, a.delta, a.dq, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.do_st), mk(a.o_st),
+      mk(a.dq_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale, a.causal, a.window, a.kv_lens);
+}
+// D = 256 A/B knobs: MFT_ATTN_DQ_RING=2|3 (DMA ring slots), MFT_ATTN_DELTA_FOLD=1|0 (delta in the dQ
+// kernel, or by the separate pass).  Measured at B 256 S 256 H 4 Hkv 1 (profiles/r3_attn256_bwd_ab.txt):
+// dQ 240 us with 2 slots + fold vs 252 (3 slots), and 207 + 45 (delta pass) unfolded
+static bool delta_fold(int D) {
+  static const int f = env_int("MFT_ATTN_DELTA_FOLD", 1);
+  return D != 256 || f != 0;
+}
+template <int D, int NW>
+static void dq_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
+  if constexpr (D == 256) {
+    static const int ring = env_int("MFT_ATTN_DQ_RING", 2);
+    const bool fold = delta_fold(D);
+    if (ring == 2) {
+      if (fold) dq_split_launch_v<D, NW, 2, true>(a, stream);
+      else dq_split_launch_v<D, NW, 2, false>(a, stream);
+    } else {
+      if (fold) dq_split_launch_v<D, NW, 3, true>(a, stream);
+      else dq_split_launch_v<D, NW, 3, false>(a, stream);
+    }
+  } else {
+    dq_split_launch_v<D, NW, 2, true>(a, stream);
+  }
 }
 
 
@@ -1377,17 +1572,24 @@ static void bwd_launch(const AttnBwdArgs& a, hipStream_t stream) {
     }
   }
   constexpr int BQ = 64, BK = 64, LDT = BQ + 8;
+  if (attn_bwd_path(D, a.Sq, a.Sk, a.window) == 2) {
+    if (!delta_fold(D)) {
+      const long rows = (long)a.B * a.H * a.Sq;
+      attn_bwd_delta_kernel<D><<<cdiv(rows * (D / 8), 256), 256, 0, stream>>>(a.o, a.dout, a.delta, mk(a.o_st),
+                                                                              mk(a.do_st), a.B, a.H, a.Sq);
+    }
+    // dQ first: it writes delta (rowsum dO * O), which the dK/dV kernel reads
+    if (split_nw("MFT_ATTN_NW_DQ", 8) == 8) dq_split_launch<D, 8>(a, stream);
+    else dq_split_launch<D, 4>(a, stream);
+    // D = 256: 8 waves (its 3-slot DMA ring holds one workgroup per CU; 4 waves would leave one per SIMD)
+    if (split_nw("MFT_ATTN_NW_DKDV", D == 256 ? 8 : 4) == 8) dkdv_split_launch<D, 8>(a, stream);
+    else dkdv_split_launch<D, 4>(a, stream);
+    return;
+  }
   {
     const long rows = (long)a.B * a.H * a.Sq;
     attn_bwd_delta_kernel<D><<<cdiv(rows * (D / 8), 256), 256, 0, stream>>>(a.o, a.dout, a.delta, mk(a.o_st),
                                                                             mk(a.do_st), a.B, a.H, a.Sq);
-  }
-  if (attn_bwd_path(D, a.Sq, a.Sk, a.window) == 2) {
-    if (split_nw("MFT_ATTN_NW_DKDV", 4) == 8) dkdv_split_launch<D, 8>(a, stream);
-    else dkdv_split_launch<D, 4>(a, stream);
-    if (split_nw("MFT_ATTN_NW_DQ", 8) == 8) dq_split_launch<D, 8>(a, stream);
-    else dq_split_launch<D, 4>(a, stream);
-    return;
   }
   MFT_HIP_CHECK(hipMemsetAsync(a.dq_acc, 0, sizeof(float) * (size_t)a.B * a.Sq * a.H * D, stream));
   const size_t shm = sizeof(bf16_t) * (2 * BK * D + 2 * BQ * D + 2 * BK * LDT) + sizeof(float) * 2 * BQ;
