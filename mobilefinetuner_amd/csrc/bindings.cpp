@@ -608,6 +608,9 @@ std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, 
   if (impl == 1) {  // gemmw (NT only)
     TORCH_CHECK(!a_t && !b_t && mft::gemmw_supported(M, N, K), "gemm_t impl 1 (gemmw): NT, K % 32 == 0");
     mft::gemmw(a, (int)epi, stream());
+  } else if (impl == 2) {  // gemm4 (NT only)
+    TORCH_CHECK(!a_t && !b_t && mft::gemm4_supported(M, N, K), "gemm_t impl 2 (gemm4): NT, K % 64 == 0");
+    mft::gemm4(a, (int)epi, stream());
   } else {
     mft::gemm8x(a, (int)epi, a_t, b_t, stream());
   }

@@ -120,6 +120,9 @@ void gemm8_set_stream(int on);
 // (epilogues as gemm8's, minus the CE / split-K ones)
 void gemmw(const GemmArgs& g, int epi, hipStream_t st);
 bool gemmw_supported(int M, int N, int K);
+// 256x256x64 NT GEMM with 4 waves (one per SIMD, 128x128 per wave, AGPR accumulators; gemmw.hip)
+void gemm4(const GemmArgs& g, int epi, hipStream_t st);
+bool gemm4_supported(int M, int N, int K);
 void gemm_splitk_reduce(const float* ws, int ksplit, int M, int N, float* C, long ldc, float alpha, int accumulate,
                         hipStream_t st);
 

@@ -266,6 +266,232 @@ __global__ __launch_bounds__(256, 2) void gemmw_kernel(GemmArgs g) {
   epilogue_w<EPI>(g, acc, m0, n0, wm, wn, lane);
 }
 
+// ================================================================== gemm4: 256 x 256 x 64, 4 waves
+// One workgroup per CU, ONE wave per SIMD, each wave a 128 x 128 quadrant of the tile: 8 x 8
+// accumulator blocks = 256 fp32 registers per lane, which the 512-entry unified register file of a
+// lone wave holds in AGPRs beside the VGPR fragments.  Against gemm8 (8 waves of 64 x 32 pieces,
+// 16 barriers per K-tile) a wave re-reads each LDS fragment for 8 MFMAs instead of 2-4: 32
+// ds_read_b128 per 128 MFMAs and only 2 barriers per 64-deep K-tile.  Latency is hidden inside the
+// wave by register double-buffering of the two 32-deep k-steps:
+//
+//   top of K-tile t (buffer c = t & 1 holds it; k-step-0 fragments of t already requested):
+//     seg 1: request the k-step-1 fragments of t (16 ds_read_b128) | 64 MFMAs of k-step 0
+//     lgkmcnt(0); barrier M   -- every wave is done reading buffer c
+//     issue the LDS-DMA of K-tile t + 2 into buffer c (16 global_load_lds_dwordx4 per lane)
+//     seg 2: 32 MFMAs of k-step 1
+//     vmcnt(16) (K-tile t + 1 landed: only t + 2 still in flight); barrier E
+//     seg 3: request the k-step-0 fragments of t + 1 from buffer c ^ 1 | 32 MFMAs of k-step 1
+//
+// so a K-tile's loads are in flight for ~1.5 K-tiles of MFMA work, never drained inside the loop
+// (raw s_barrier, counted waits; guide §5 "Pipelining across barriers").  LDS images as gemm8: 128-B
+// rows, the 16-B chunk index XOR-swizzled with (row & 7) on the SOURCE address (rule 21).
+namespace {
+constexpr int G4_HALF = 256 * 64;  // elements of one operand's K-tile image (32 KB)
+
+__device__ __forceinline__ void g4_raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// One operand's K-tile (256 rows x 64 k) is 8 LDS-DMA pieces per lane: piece t of wave w moves
+// chunk c = t * 256 + tid -> row 32 t + (tid >> 3), 16-B chunk (tid & 7) ^ (row & 7) (the swizzle
+// term (tid >> 3) & 7 does not depend on t).  Through a buffer descriptor whose base is the tile's
+// row r0 at column k0 and whose size ends at the last valid row: rows past the matrix are dropped
+// by the range check (their LDS rows only feed output rows / columns that are never stored), and
+// each piece is one 32-bit VGPR offset (voff + t * 64 ld bytes) -- no 64-bit address math.
+struct G4Src {
+  __amdgpu_buffer_rsrc_t rsrc;
+};
+__device__ __forceinline__ G4Src g4_src(const bf16_t* src, long ld, int r0, int rmax, int k0, bool none = false) {
+  const long rows = (long)rmax - r0;  // >= 1
+  const long bytes = none ? 0 : ((rows - 1) * ld + 64) * 2;
+  return G4Src{__builtin_amdgcn_make_buffer_rsrc((void*)(src + (long)r0 * ld + k0), (short)0,
+                                                 (int)min(bytes, 0x7FFFFFFFL), 0x00020000)};
+}
+__device__ __forceinline__ uint32_t g4_voff(long ld) {
+  const int tid = threadIdx.x, r = tid >> 3, s = tid & 7;
+  return (uint32_t)((r * (int)ld + ((s ^ (r & 7)) << 3)) * 2);
+}
+__device__ __forceinline__ void g4_piece(const G4Src& s, uint32_t voff, long ld, int t, bf16_t* lds_img, int w) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(s.rsrc, (__attribute__((address_space(3))) void*)(lds_img + (t * 256 + w * 64) * 8),
+                                           16, voff + (uint32_t)(t * 64 * ld), 0, 0, 0);
+}
+
+// lane holds T[r0 + (l & 15)][8 * kc + 8 * (l >> 4) + j] of a swizzled [256][64] image
+__device__ __forceinline__ bf16x8_t g4_frag(const bf16_t* t, int r0, int kc) {
+  const int l = threadIdx.x & 63;
+  const int r = r0 + (l & 15), q = kc + (l >> 4);
+  return *reinterpret_cast<const bf16x8_t*>(t + r * 64 + ((q ^ (r & 7)) << 3));
+}
+
+// acc += b^T-swapped product: inline asm with the accumulator tied "+a" so it stays in place in the
+// AGPR file (hipcc's own MFMA selection rotates accumulators between iterations: ~370 v_accvgpr
+// copies per K-tile).  Hazards: an accumulator is next read by an MFMA 63 MFMAs later (none), the
+// fragments come from ds_read waited by hipcc's own lgkmcnt, and g4_mfma_drain pads the last MFMA
+// before any compiler code reads the AGPRs.
+__device__ __forceinline__ void g4_mfma(f32x4_t& c, const bf16x8_t& b, const bf16x8_t& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+}
+}  // namespace
+
+// DBG (timing diagnostics only, results invalid): 1 = every LDS-DMA dropped by a zero-size
+// descriptor (same instruction stream, no memory traffic), 2 = no barriers in the loop, 4 = no
+// LDS-DMA instructions in the loop
+template <int EPI, int DBG = 0>
+__global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem4[];
+  const int tiles_n = (g.N + 255) / 256;
+  const int ntiles = ((g.M + 255) / 256) * tiles_n;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  if (tile >= ntiles) return;
+  const int m0 = (tile / tiles_n) * 256, n0 = (tile % tiles_n) * 256;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int nk = g.K / 64;
+  auto sa = [&](int b) { return smem4 + b * 2 * G4_HALF; };
+  auto sb = [&](int b) { return smem4 + b * 2 * G4_HALF + G4_HALF; };
+  const uint32_t voa = g4_voff(g.lda), vob = g4_voff(g.ldb);
+  // piece p (0..15) of K-tile kt into buffer b: p < 8 -> A piece p, else B piece p - 8
+  G4Src srcA, srcB;
+  auto set_src = [&](int kt) {
+    const int k0 = min(kt, nk - 1) * 64;  // past the end: re-read the last K-tile (uniform counts)
+    srcA = g4_src(g.A, g.lda, m0, g.M, k0, DBG == 1 && kt >= 2);
+    srcB = g4_src(g.B, g.ldb, n0, g.N, k0, DBG == 1 && kt >= 2);
+  };
+  auto piece = [&](int b, int p) {
+    if (p < 8) g4_piece(srcA, voa, g.lda, p, sa(b), w);
+    else g4_piece(srcB, vob, g.ldb, p - 8, sb(b), w);
+  };
+
+  f32x4_t acc[2][8][4];  // [column half][i: 16-row block][j: 16-column block]
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[h][i][j] = zero4();
+  bf16x8_t a0[8], b0[8], a1[8], b1[8];
+  // fragment r (0..15) of k-step ks: r < 8 -> B fragment r, else A fragment r - 8
+  auto frag = [&](bf16x8_t (&af)[8], bf16x8_t (&bf)[8], int b, int ks, int r) {
+    if (r < 8) bf[r] = g4_frag(sb(b), wc * 128 + r * 16, ks * 4);
+    else af[r - 8] = g4_frag(sa(b), wr * 128 + (r - 8) * 16, ks * 4);
+  };
+  // MFMA number m (0..63) of a k-step: i = m / 8, j = m % 8
+  auto mma = [&](const bf16x8_t (&af)[8], const bf16x8_t (&bf)[8], int m) {
+    const int i = m >> 3, j = m & 7;
+    g4_mfma(acc[j >> 2][i][j & 3], bf[j], af[i]);
+  };
+
+  set_src(0);
+#pragma unroll
+  for (int p = 0; p < 16; ++p) piece(0, p);
+  set_src(1);
+#pragma unroll
+  for (int p = 0; p < 16; ++p) piece(1, p);
+  vm_wait_w<16>();  // K-tile 0 landed (this wave's share); the barrier makes it everyone's
+  g4_raw_barrier();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) frag(a0, b0, 0, 0, r);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int c = kt & 1;
+    // seg 1: k-step-1 fragments of K-tile kt | 64 MFMAs of k-step 0
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      frag(a1, b1, c, 1, r);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mma(a0, b0, 4 * r + q);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (DBG != 2) g4_raw_barrier();  // M: every wave is done reading buffer c
+    // seg 2: LDS-DMA of K-tile kt + 2 into buffer c | 32 MFMAs of k-step 1
+    set_src(kt + 2);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if constexpr (DBG != 4) piece(c, r);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) mma(a1, b1, 2 * r + q);
+    }
+    if constexpr (DBG == 4) vm_wait_w<0>();
+    else vm_wait_w<16>();  // K-tile kt + 1 landed (only kt + 2 still in flight)
+    if constexpr (DBG != 2) g4_raw_barrier();  // E: ... for every wave
+    // seg 3: k-step-0 fragments of K-tile kt + 1 | the other 32 MFMAs of k-step 1
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      frag(a0, b0, c ^ 1, 0, r);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) mma(a1, b1, 32 + 2 * r + q);
+    }
+  }
+  vm_wait_w<0>();  // drain the clamped tail prefetches (LDS-DMA must not outlive the workgroup)
+  // MFMA result -> first compiler read of the AGPR: 8-pass XDL needs >= 12 wait states, which hipcc
+  // does not insert after an asm MFMA.  The pad "redefines" the accumulators of the last 8 MFMAs
+  // (i = 7), so no read or copy of them (hipcc emits AGPR copies right after the loop) can be
+  // scheduled above it; every earlier MFMA is >= 8 MFMA issues old.
+  asm volatile("s_nop 15\n\ts_nop 7"
+               : "+a"(acc[0][7][0]), "+a"(acc[0][7][1]), "+a"(acc[0][7][2]), "+a"(acc[0][7][3]), "+a"(acc[1][7][0]),
+                 "+a"(acc[1][7][1]), "+a"(acc[1][7][2]), "+a"(acc[1][7][3])
+               :
+               : "memory");
+  epilogue_w<EPI>(g, acc[0], m0, n0 + wc * 128, wr, 0, lane);
+  epilogue_w<EPI>(g, acc[1], m0, n0 + wc * 128, wr, 1, lane);
+}
+
+template <int EPI>
+static void launch4(const GemmArgs& g, hipStream_t st) {
+  constexpr size_t shm = sizeof(bf16_t) * 4 * G4_HALF;  // 128 KB: 2 K-tile buffers of A and B
+  static bool attr = false;
+  if (!attr) {
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)shm));
+    attr = true;
+  }
+  const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+  if constexpr (EPI == GEMM_EPI_NONE) {
+    static const int dbg = getenv("MFT_G4_DBG") ? atoi(getenv("MFT_G4_DBG")) : 0;
+    if (dbg) {
+      static bool attr_d = false;
+      if (!attr_d) {
+        for (const void* f : {(const void*)gemm4_kernel<EPI, 1>, (const void*)gemm4_kernel<EPI, 2>,
+                              (const void*)gemm4_kernel<EPI, 4>})
+          MFT_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        attr_d = true;
+      }
+      const int v = getenv("MFT_G4_DBG_V") ? atoi(getenv("MFT_G4_DBG_V")) : 0;  // re-read per call
+      if (v == 1) { gemm4_kernel<EPI, 1><<<tiles, 256, shm, st>>>(g); return; }
+      if (v == 2) { gemm4_kernel<EPI, 2><<<tiles, 256, shm, st>>>(g); return; }
+      if (v == 4) { gemm4_kernel<EPI, 4><<<tiles, 256, shm, st>>>(g); return; }
+    }
+  }
+  gemm4_kernel<EPI><<<tiles, 256, shm, st>>>(g);
+}
+
+bool gemm4_supported(int M, int N, int K) { return M > 0 && K > 0 && K % 64 == 0 && N >= 8 && N % 8 == 0; }
+
+void gemm4(const GemmArgs& g, int epi, hipStream_t st) {
+  if (!gemm4_supported(g.M, g.N, g.K) || g.lda > (1L << 23) || g.ldb > (1L << 23) || g.lda % 8 || g.ldb % 8) {
+    fprintf(stderr, "mft::gemm4: unsupported shape M=%d N=%d K=%d lda=%ld ldb=%ld\n", g.M, g.N, g.K, g.lda, g.ldb);
+    abort();
+  }
+  switch (epi) {
+    case GEMM_EPI_NONE: launch4<GEMM_EPI_NONE>(g, st); break;
+    case GEMM_EPI_BIAS: launch4<GEMM_EPI_BIAS>(g, st); break;
+    case GEMM_EPI_BIAS_GELU: launch4<GEMM_EPI_BIAS_GELU>(g, st); break;
+    case GEMM_EPI_DGELU: launch4<GEMM_EPI_DGELU>(g, st); break;
+    case GEMM_EPI_BIAS_GELU_D: launch4<GEMM_EPI_BIAS_GELU_D>(g, st); break;
+    case GEMM_EPI_MUL_AUX: launch4<GEMM_EPI_MUL_AUX>(g, st); break;
+    case GEMM_EPI_F32ACC: launch4<GEMM_EPI_F32ACC>(g, st); break;
+    case GEMM_EPI_LORA:
+      if (g.lora_r <= 0 || g.lora_r > 32 || g.lora_r % 8 || g.ld_lu % 8) {
+        fprintf(stderr, "mft::gemm4: LoRA epilogue needs rank %% 8 == 0, <= 32 (got %d)\n", g.lora_r);
+        abort();
+      }
+      launch4<GEMM_EPI_LORA>(g, st);
+      break;
+    default: fprintf(stderr, "mft::gemm4: unsupported epilogue %d\n", epi); abort();
+  }
+}
+
 template <int EPI>
 static void launchw(const GemmArgs& g, hipStream_t st) {
   constexpr size_t shm = sizeof(bf16_t) * WNS * W_STAGE;  // 72 KB: two workgroups per CU

@@ -112,6 +112,7 @@ def test_zero3_single_gpu_matches_flat(model_name, copy_path, monkeypatch):
         batches.append([(ids[:, :-1].contiguous(), ids[:, 1:].contiguous())])
     m0 = make()
     m0.set_full_finetune()
+    init = {n: p.detach().float().cpu().clone() for n, p in m0.named_parameters()}
     flat = FlatParams(m0.named_parameters(), DEV)
     opt0 = FusedAdamW(flat, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0)
     st0 = TrainStep(m0, flat, opt0, use_graph=False)
@@ -132,9 +133,19 @@ def test_zero3_single_gpu_matches_flat(model_name, copy_path, monkeypatch):
         assert (st1.graph is not None) == graph
         assert losses == pytest.approx(ref_losses, rel=2e-3, abs=2e-3), (graph, losses, ref_losses)
         assert gns == pytest.approx(ref_gn, rel=1e-2), (graph, gns, ref_gn)
+        # parameters: compare the UPDATES against the reference run's.  Adam normalises every element's
+        # step to ~lr whatever its gradient magnitude, so an element whose gradient is ~0 takes a
+        # bf16-noise-signed step in either run (up to 2 lr per step apart): an elementwise allclose is
+        # a coin toss on such elements; the relative L2 of the update difference is not
         full = z3.full_state()
+        num = den = 0.0
         for n, p in m0.named_parameters():
-            assert torch.allclose(full[n], p.detach().float().cpu(), atol=2e-3, rtol=1e-2), (graph, n)
+            d0 = p.detach().float().cpu() - init[n]
+            d1 = full[n] - init[n]
+            e, r = float((d1 - d0).norm()), float(d0.norm())
+            assert e <= 0.25 * r + 1e-6, (graph, n, e, r)
+            num, den = num + e * e, den + r * r
+        assert num ** 0.5 <= 0.05 * den ** 0.5, (graph, num ** 0.5, den ** 0.5)
         assert z3.stats["all_gather"] > 0 and z3.stats["reduce_scatter"] > 0
 
 
