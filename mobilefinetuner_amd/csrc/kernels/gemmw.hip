@@ -345,7 +345,15 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs g) {
   const int ntiles = ((g.M + 255) / 256) * tiles_n;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   if (tile >= ntiles) return;
-  const int m0 = (tile / tiles_n) * 256, n0 = (tile % tiles_n) * 256;
+  // grouped order: GM row panels sweep the column tiles together, so the 32 workgroups an XCD holds
+  // at once (consecutive ids after the remap) form a compact block sharing A and B panels in its L2
+  // (8192^3: 980 -> 1432 TF/s; fc forward 895 -> 943)
+  constexpr int GM = 8;
+  const int tiles_m = (g.M + 255) / 256;
+  const int group = tile / (GM * tiles_n), first_m = group * GM;
+  const int gsz = min(tiles_m - first_m, GM);
+  const int in_g = tile - group * GM * tiles_n;
+  const int m0 = (first_m + in_g % gsz) * 256, n0 = (in_g / gsz) * 256;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 1, wc = w & 1;
   const int nk = g.K / 64;
