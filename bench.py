@@ -185,6 +185,7 @@ def run_native(a, cfgd) -> int:
             "model_tflops_per_gpu": round(tflops, 1),
             "mfu_bf16_dense": round(tflops / MI355X_BF16_DENSE_TFLOPS, 4),
             "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC if a.config == "gpt2-lora" else None,
+            "peak_hbm_gb_rank0": rec.get("peak_reserved_gb"),
         },
     }
     print(json.dumps(out_rec), flush=True)

@@ -21,6 +21,7 @@
 #include <thread>
 #include <vector>
 
+#include "engine/allocator.h"
 #include "engine/autograd.h"
 #include "engine/comm.h"
 #include "engine/dist.h"
@@ -236,10 +237,14 @@ inline void bench_report(TrainerT& trainer, const FlatT& flat, const Args& a, in
   for (auto& kv : flat.params) n_train += (long long)kv.second->leaf.numel();
   if (flat.params.empty()) n_train = (long long)flat.numel;
   if (!lead) return;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const eng::AllocStats ms = eng::CachingAllocator::get(dev).stats();  // HBM high-water mark of this rank
   std::printf("MFT_BENCH {\"seconds\": %.9f, \"steps\": %d, \"warmup\": %d, \"world\": %d, \"batch\": %d, "
               "\"seq\": %d, \"accum\": %d, \"final_loss\": %.6f, \"model\": \"%s\", \"n_params\": %zu, "
-              "\"n_trainable\": %lld}\n",
-              secs, steps, warmup, world, batch, seq, accum, loss, model.c_str(), n_params, n_train);
+              "\"n_trainable\": %lld, \"peak_allocated_gb\": %.3f, \"peak_reserved_gb\": %.3f}\n",
+              secs, steps, warmup, world, batch, seq, accum, loss, model.c_str(), n_params, n_train,
+              ms.peak_allocated / 1e9, ms.peak_reserved / 1e9);
   std::fflush(stdout);
 }
 

@@ -7,8 +7,8 @@ MFT_G4_DBG=1 timeout -k 10 240 python3 -u scripts/bench_gemm4.py --rounds 3 --it
 MFT_G4_DBG=1 timeout -k 10 240 python3 -u scripts/bench_gemm4.py --rounds 3 --iters 10 --only "square" --M 8192 2>&1 | grep square >> gpurun_out/r3_gemm4_diag.txt || exit 1
 grep -v amdgpu.ids gpurun_out/r3_gemm4_diag.txt
 cd /tmp && cd $GRAFT_REPO_ROOT
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS -d gpurun_out/pmc/g1 -o run -- python3 scripts/diag/gemm4_pmc_probe.py > gpurun_out/pmc/g1.log 2>&1 && \
-timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/pmc/g2 -o run -- python3 scripts/diag/gemm4_pmc_probe.py > gpurun_out/pmc/g2.log 2>&1
+true && \
+true
 rc=$?
 for p in g1 g2; do DB=$(find gpurun_out/pmc/$p -name "*.db" | head -1); [ -n "$DB" ] && python3 scripts/pmc_db.py $DB gemm8 gemm4 Cijk; done > gpurun_out/r3_gemm4_pmc.txt
 rm -rf gpurun_out/pmc/g1 gpurun_out/pmc/g2

@@ -142,6 +142,9 @@ def test_zero3_single_gpu_matches_flat(model_name, copy_path, monkeypatch):
         for n, p in m0.named_parameters():
             d0 = p.detach().float().cpu() - init[n]
             d1 = full[n] - init[n]
+            if n.endswith("c_attn.bias"):  # the key bias gets an exactly-zero gradient (softmax shift
+                c = d0.numel() // 3          # invariance): pure Adam sign noise, left out
+                d0, d1 = torch.cat([d0[:c], d0[2 * c:]]), torch.cat([d1[:c], d1[2 * c:]])
             e, r = float((d1 - d0).norm()), float(d0.norm())
             assert e <= 0.25 * r + 1e-6, (graph, n, e, r)
             num, den = num + e * e, den + r * r
