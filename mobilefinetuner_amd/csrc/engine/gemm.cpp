@@ -3,6 +3,8 @@
 
 #include <hipblaslt/hipblaslt.h>
 
+#include <functional>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstdio>
@@ -227,6 +229,52 @@ void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c,
   ::mft::gemm8x(g, epi, false, b_kn, current_stream());
 }
 
+namespace {
+// Per-shape choice between the hand-written gemm8 and hipBLASLt, timed ONCE on the real operands at
+// the first call outside a graph capture (the trainer's eager warm-up steps; inside a capture the
+// library runs and the choice waits for the next eager call).  Returns true for gemm8.  `tag`
+// names the call site in the MFT_NT_VERBOSE report.
+bool timed_gemm8_choice(const char* tag, const char* key, const std::function<void()>& run_lt,
+                        const std::function<void()>& run_g8) {
+  static std::mutex mu;
+  static std::unordered_map<std::string, int> choice;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = choice.find(key);
+    if (it != choice.end()) return it->second == 1;
+  }
+  hipStream_t s = current_stream();
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (s) (void)hipStreamIsCapturing(s, &cap);
+  if (cap != hipStreamCaptureStatusNone) return false;
+  run_lt();  // hipBLASLt's own candidate tuning happens on this first call
+  run_g8();
+  hipEvent_t e0, e1, e2;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  HIP_OK(hipEventCreate(&e2));
+  HIP_OK(hipEventRecord(e0, s));
+  for (int r = 0; r < 3; ++r) run_lt();
+  HIP_OK(hipEventRecord(e1, s));
+  for (int r = 0; r < 3; ++r) run_g8();
+  HIP_OK(hipEventRecord(e2, s));
+  HIP_OK(hipEventSynchronize(e2));
+  float t_lt = 0.f, t_g8 = 0.f;
+  HIP_OK(hipEventElapsedTime(&t_lt, e0, e1));
+  HIP_OK(hipEventElapsedTime(&t_g8, e1, e2));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipEventDestroy(e2);
+  const int c = t_g8 < t_lt ? 1 : 0;
+  if (std::getenv("MFT_NT_VERBOSE"))
+    std::fprintf(stderr, "[mft %s] %s: gemm8 %.1f us, hipBLASLt %.1f us -> %s\n", tag, key, 1e3f * t_g8 / 3,
+                 1e3f * t_lt / 3, c ? "gemm8" : "hipBLASLt");
+  std::lock_guard<std::mutex> g(mu);
+  choice[key] = c;
+  return c == 1;
+}
+}  // namespace
+
 void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y) {
   MFT_CHECK(rowmajor2(x2) && rowmajor2(w) && rowmajor2(y) && x2.dtype() == DType::BF16 && w.dtype() == DType::BF16,
             "gemm_nt: bf16 row-major");
@@ -267,65 +315,39 @@ void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y) {
   static const int forced = !env ? -1 : std::string(env) == "gemm8" ? 1 : std::string(env) == "lt" ? 0 : -1;
   if (forced >= 0) return forced ? run_g8() : run_lt();
   if (deterministic()) return run_lt();
-  static std::mutex mu;
-  static std::unordered_map<std::string, int> choice;
   char kb[160];
-  snprintf(kb, sizeof(kb), "%d|%ld|%ld|%ld|%ld|%ld|%ld|%d", cur_dev(), M, N, K, (long)x2.stride(0), (long)w.stride(0),
-           (long)y.stride(0), bias.defined() ? 1 : 0);
-  int c = -1;
-  {
-    std::lock_guard<std::mutex> g(mu);
-    auto it = choice.find(kb);
-    if (it != choice.end()) c = it->second;
-  }
-  if (c < 0) {
-    hipStream_t s = current_stream();
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (s) (void)hipStreamIsCapturing(s, &cap);
-    if (cap != hipStreamCaptureStatusNone) return run_lt();  // (decided at the next eager call)
-    run_lt();  // hipBLASLt's own candidate tuning happens on this first call
-    run_g8();
-    hipEvent_t e0, e1, e2;
-    HIP_OK(hipEventCreate(&e0));
-    HIP_OK(hipEventCreate(&e1));
-    HIP_OK(hipEventCreate(&e2));
-    HIP_OK(hipEventRecord(e0, s));
-    for (int r = 0; r < 3; ++r) run_lt();
-    HIP_OK(hipEventRecord(e1, s));
-    for (int r = 0; r < 3; ++r) run_g8();
-    HIP_OK(hipEventRecord(e2, s));
-    HIP_OK(hipEventSynchronize(e2));
-    float t_lt = 0.f, t_g8 = 0.f;
-    HIP_OK(hipEventElapsedTime(&t_lt, e0, e1));
-    HIP_OK(hipEventElapsedTime(&t_g8, e1, e2));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipEventDestroy(e2);
-    c = t_g8 < t_lt ? 1 : 0;
-    if (std::getenv("MFT_NT_VERBOSE"))
-      std::fprintf(stderr, "[mft gemm_nt] M=%ld N=%ld K=%ld%s: gemm8 %.1f us, hipBLASLt %.1f us -> %s\n", M, N, K,
-                   bias.defined() ? " +bias" : "", 1e3f * t_g8 / 3, 1e3f * t_lt / 3, c ? "gemm8" : "hipBLASLt");
-    std::lock_guard<std::mutex> g(mu);
-    choice[kb] = c;
-  }
-  return c ? run_g8() : run_lt();
+  snprintf(kb, sizeof(kb), "dev %d M=%ld N=%ld K=%ld ld %ld/%ld/%ld%s", cur_dev(), M, N, K, (long)x2.stride(0),
+           (long)w.stride(0), (long)y.stride(0), bias.defined() ? " +bias" : "");
+  return timed_gemm8_choice("gemm_nt", kb, run_lt, run_g8) ? run_g8() : run_lt();
 }
 
 void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out) {
-  const long N = w.size(0);
-  if (N % 64 == 0 && w.size(1) % 8 == 0 && dy2.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 8 == 0) {
-    gemm8_call(dy2, w, true, ::mft::GEMM_EPI_NONE, out);
-    return;
-  }
-  Problem p;  // out^T [K, M] = W^T [K, N] . dy^T [N, M]
-  p.dev = cur_dev();
-  p.m = w.size(1);
-  p.n = dy2.size(0);
-  p.k = N;
-  p.lda = w.stride(0);
-  p.ldb = dy2.stride(0);
-  p.ldd = out.stride(0);
-  lt_run(p, w.data_ptr(), dy2.data_ptr(), out.data_ptr(), nullptr, 1.f, 0.f);
+  const long N = w.size(0), M = dy2.size(0), K = w.size(1);
+  auto run_g8 = [&]() { gemm8_call(dy2, w, true, ::mft::GEMM_EPI_NONE, out); };
+  auto run_lt = [&]() {
+    Problem p;  // out^T [K, M] = W^T [K, N] . dy^T [N, M]
+    p.dev = cur_dev();
+    p.m = K;
+    p.n = M;
+    p.k = N;
+    p.lda = w.stride(0);
+    p.ldb = dy2.stride(0);
+    p.ldd = out.stride(0);
+    lt_run(p, w.data_ptr(), dy2.data_ptr(), out.data_ptr(), nullptr, 1.f, 0.f);
+  };
+  const bool g8_ok =
+      N % 64 == 0 && K % 8 == 0 && dy2.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 8 == 0;
+  if (!g8_ok) return run_lt();
+  // plain data-gradient GEMMs: the same timed per-shape choice as the NT forwards (MFT_NN=gemm8|lt
+  // forces one; deterministic mode and MFT_GEMM8_ALL=1 keep gemm8)
+  static const char* env = std::getenv("MFT_NN");
+  static const int forced = !env ? -1 : std::string(env) == "gemm8" ? 1 : std::string(env) == "lt" ? 0 : -1;
+  if (forced >= 0) return forced ? run_g8() : run_lt();
+  if (deterministic() || gemm8_all()) return run_g8();
+  char kb[160];
+  snprintf(kb, sizeof(kb), "NN dev %d M=%ld N=%ld K=%ld ld %ld/%ld/%ld", cur_dev(), M, K, N, (long)dy2.stride(0),
+           (long)w.stride(0), (long)out.stride(0));
+  return timed_gemm8_choice("gemm_nn", kb, run_lt, run_g8) ? run_g8() : run_lt();
 }
 
 void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
