@@ -54,19 +54,23 @@ CONFIGS = {
     # Gemma-3 270M LoRA r=8 seq 256 (RMSNorm / QK-norm+RoPE / GQA / sliding-window kernels)
     "gemma3-270m-lora": dict(model="gemma3-270m", mode="lora", batch=256, seq=256, targets="full", engine="native",
                              metric="tokens/sec Gemma-3-270M LoRA r=8 seq256 (training, whole job)"),
-    # GPT-2 small full fine-tuning, DP over RCCL (bucketed, backward-overlapped all-reduce)
-    "gpt2-full": dict(model="gpt2", mode="full", batch=512, seq=128, zero=0, engine="native",
+    # GPT-2 small full fine-tuning, DP over RCCL (bucketed, backward-overlapped all-reduce).  Micro-
+    # batches (profiles/r3_fullbatch_ab.txt, one MI355X): gpt2-full 512 x 128 1.046M tok/s, 1024 x 128
+    # 1.075M (97 GB peak); GPT-2 XL ZeRO-3 64 x 128 70.6K, 128 x 128 84.8K, 256 x 128 87.1K (210 GB
+    # peak on ONE GPU -- 1/N of the 25 GB optimizer state at N ranks); + host AdamW 64 x 128 34.2K,
+    # 256 x 128 65.0K (the PCIe-bound optimizer step amortised over 4x the tokens)
+    "gpt2-full": dict(model="gpt2", mode="full", batch=1024, seq=128, zero=0, engine="native",
                       metric="tokens/sec GPT-2-124M full fine-tune seq128 (training, whole job)"),
     # GPT-2 XL (1.5B) full fine-tuning with ZeRO-2 partitioned optimizer / reduce-scattered grads
-    "gpt2-xl-zero": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=2, engine="native",
+    "gpt2-xl-zero": dict(model="gpt2-xl", mode="full", batch=256, seq=128, zero=2, engine="native",
                          metric="tokens/sec GPT-2-XL full fine-tune ZeRO-2 seq128 (training, whole job)"),
     # same with ZeRO-3: parameters partitioned too, all-gathered per block (prefetched one block
     # ahead on a communication stream), gradients reduce-scattered per block during backward
-    "gpt2-xl-zero3": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=3, engine="native",
+    "gpt2-xl-zero3": dict(model="gpt2-xl", mode="full", batch=256, seq=128, zero=3, engine="native",
                           metric="tokens/sec GPT-2-XL full fine-tune ZeRO-3 seq128 (training, whole job)"),
     # BASELINE config 5: ZeRO partition + host-DRAM tier (AdamW moments in pinned host memory,
     # streamed through the GPU per chunk on the native HostTier's copy stream)
-    "gpt2-xl-zero3-offload": dict(model="gpt2-xl", mode="full", batch=64, seq=128, zero=3, offload=True, engine="native",
+    "gpt2-xl-zero3-offload": dict(model="gpt2-xl", mode="full", batch=256, seq=128, zero=3, offload=True, engine="native",
                                   metric="tokens/sec GPT-2-XL full fine-tune ZeRO-3 + host-offloaded AdamW "
                                          "seq128 (training, whole job)"),
 }
