@@ -338,7 +338,10 @@ __device__ __forceinline__ void g4_mfma(f32x4_t& c, const bf16x8_t& b, const bf1
 // DBG (timing diagnostics only, results invalid): 1 = every LDS-DMA dropped by a zero-size
 // descriptor (same instruction stream, no memory traffic), 2 = no barriers in the loop, 4 = no
 // LDS-DMA instructions in the loop
-template <int EPI, int DBG = 0>
+// A3: asymmetric LDS ring -- THREE 32 KB slots for the A (activation) K-tiles, two for B (weights,
+// L2-resident): the A loads are issued three K-tiles ahead (in flight ~2 K-tiles of MFMA work instead
+// of ~1), B two ahead; 5 x 32 KB = the whole 160 KB LDS.
+template <int EPI, int DBG = 0, bool A3 = false>
 __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem4[];
   const int tiles_n = (g.N + 255) / 256;
@@ -357,8 +360,9 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs g) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 1, wc = w & 1;
   const int nk = g.K / 64;
-  auto sa = [&](int b) { return smem4 + b * 2 * G4_HALF; };
-  auto sb = [&](int b) { return smem4 + b * 2 * G4_HALF + G4_HALF; };
+  // A3: A slot s at smem + s HALF (s < 3), B slot s at smem + (3 + s) HALF; else buffer b = {A, B}
+  auto sa = [&](int b) { return A3 ? smem4 + b * G4_HALF : smem4 + b * 2 * G4_HALF; };
+  auto sb = [&](int b) { return A3 ? smem4 + (3 + b) * G4_HALF : smem4 + b * 2 * G4_HALF + G4_HALF; };
   const uint32_t voa = g4_voff(g.lda), vob = g4_voff(g.ldb);
   // piece p (0..15) of K-tile kt into buffer b: p < 8 -> A piece p, else B piece p - 8
   G4Src srcA, srcB;
@@ -391,6 +395,66 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs g) {
     g4_mfma(acc[j >> 2][i][j & 3], bf[j], af[i]);
   };
 
+  if constexpr (A3) {
+    auto src_a = [&](int kt) { srcA = g4_src(g.A, g.lda, m0, g.M, min(kt, nk - 1) * 64); };
+    auto src_b = [&](int kt) { srcB = g4_src(g.B, g.ldb, n0, g.N, min(kt, nk - 1) * 64); };
+    // issue order B(0) A(0) B(1) A(1) A(2), then per K-tile kt: B(kt + 2) A(kt + 3) -- so "B(kt + 1)
+    // and A(kt + 1) landed" is always vmcnt(24): A(kt + 2), B(kt + 2), A(kt + 3) may still fly
+    src_b(0);
+    src_a(0);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) g4_piece(srcB, vob, g.ldb, p, sb(0), w);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) g4_piece(srcA, voa, g.lda, p, sa(0), w);
+    src_b(1);
+    src_a(1);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) g4_piece(srcB, vob, g.ldb, p, sb(1), w);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) g4_piece(srcA, voa, g.lda, p, sa(1), w);
+    src_a(2);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) g4_piece(srcA, voa, g.lda, p, sa(2), w);
+    vm_wait_w<24>();
+    g4_raw_barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (r < 8) b0[r] = g4_frag(sb(0), wc * 128 + r * 16, 0);
+      else a0[r - 8] = g4_frag(sa(0), wr * 128 + (r - 8) * 16, 0);
+    }
+    int ca = 0;  // kt % 3
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cb = kt & 1, ca1 = ca == 2 ? 0 : ca + 1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r < 8) b1[r] = g4_frag(sb(cb), wc * 128 + r * 16, 4);
+        else a1[r - 8] = g4_frag(sa(ca), wr * 128 + (r - 8) * 16, 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mma(a0, b0, 4 * r + q);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      g4_raw_barrier();  // M: A slot ca and B slot cb fully read by every wave
+      src_b(kt + 2);
+      src_a(kt + 3);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r < 8) g4_piece(srcB, vob, g.ldb, r, sb(cb), w);
+        else g4_piece(srcA, voa, g.lda, r - 8, sa(ca), w);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) mma(a1, b1, 2 * r + q);
+      }
+      vm_wait_w<24>();   // B(kt + 1), A(kt + 1) landed
+      g4_raw_barrier();  // E
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r < 8) b0[r] = g4_frag(sb(cb ^ 1), wc * 128 + r * 16, 0);
+        else a0[r - 8] = g4_frag(sa(ca1), wr * 128 + (r - 8) * 16, 0);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) mma(a1, b1, 32 + 2 * r + q);
+      }
+      ca = ca1;
+    }
+  } else {
   set_src(0);
 #pragma unroll
   for (int p = 0; p < 16; ++p) piece(0, p);
@@ -431,6 +495,7 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(GemmArgs g) {
       for (int q = 0; q < 2; ++q) mma(a1, b1, 32 + 2 * r + q);
     }
   }
+  }
   vm_wait_w<0>();  // drain the clamped tail prefetches (LDS-DMA must not outlive the workgroup)
   // MFMA result -> first compiler read of the AGPR: 8-pass XDL needs >= 12 wait states, which hipcc
   // does not insert after an asm MFMA.  The pad "redefines" the accumulators of the last 8 MFMAs
@@ -455,6 +520,19 @@ static void launch4(const GemmArgs& g, hipStream_t st) {
     attr = true;
   }
   const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+  {
+    const char* a3 = getenv("MFT_G4_A3");  // re-read per call (bench A/B)
+    if (a3 && a3[0] == '1') {
+      static bool attr3 = false;
+      if (!attr3) {
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm4_kernel<EPI, 0, true>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 5 * G4_HALF * (int)sizeof(bf16_t)));
+        attr3 = true;
+      }
+      gemm4_kernel<EPI, 0, true><<<tiles, 256, 5 * G4_HALF * sizeof(bf16_t), st>>>(g);
+      return;
+    }
+  }
   if constexpr (EPI == GEMM_EPI_NONE) {
     static const int dbg = getenv("MFT_G4_DBG") ? atoi(getenv("MFT_G4_DBG")) : 0;
     if (dbg) {

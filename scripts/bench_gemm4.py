@@ -33,8 +33,9 @@ def check(C):
     def err(got, want):
         return ((got.float() - want).abs().max() / want.abs().max().clamp_min(1e-6)).item()
 
-    for impl, stream in ((0, 0), (2, 0)):
-        C.gemm8_set_stream(stream)
+    for impl, stream in ((0, 0), (2, 0), (2, 1)):
+        os.environ["MFT_G4_A3"] = str(stream)  # (impl 2, 1) = gemm4 with the A3 ring
+        C.gemm8_set_stream(0)
         y = C.gemm_t(x, w, False, False, NONE, impl=impl)[0]
         e = err(y, ref)
         y, pre = C.gemm_t(x, w, False, False, BIAS_GELU, bias=b, impl=impl)
@@ -48,13 +49,14 @@ def check(C):
         want = out + 2.0 * ref
         C.gemm_t(x, w, False, False, F32ACC, alpha=2.0, out=out, impl=impl)
         e = max(e, err(out, want))
-        print(f"impl {impl} stream {stream}: max relative error over the epilogues {e:.2e}", flush=True)
+        print(f"impl {impl} A3 {stream}: max relative error over the epilogues {e:.2e}", flush=True)
         worst = max(worst, e)
     # many K-tiles, row and column tails: gemm4 vs gemm8 vs fp32
     M, K, N = 65536 + 200, 768, 2048 - 8
     x, w, b = rnd(M, K), rnd(N, K, s=0.05), rnd(N, s=0.1)
     ref = x.float() @ w.float().t()
-    for impl in (0, 2):
+    for impl, a3 in ((0, "0"), (2, "0"), (2, "1")):
+        os.environ["MFT_G4_A3"] = a3
         y = C.gemm_t(x, w, False, False, NONE, impl=impl)[0]
         e1 = err(y, ref)
         y = C.gemm_t(x, w, False, False, BIAS, bias=b, impl=impl)[0]
@@ -62,9 +64,10 @@ def check(C):
         aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         y = C.gemm_t(x, w, False, False, BIAS_GELU_D, bias=b, aux=aux, impl=impl)[0]
         e3 = err(y, gelu(ref + b.float()))
-        print(f"large NT, impl {impl}: errors none {e1:.2e} bias {e2:.2e} gelu {e3:.2e}", flush=True)
+        print(f"large NT, impl {impl} A3 {a3}: errors none {e1:.2e} bias {e2:.2e} gelu {e3:.2e}", flush=True)
         worst = max(worst, e1, e2, e3)
     del ref
+    os.environ["MFT_G4_A3"] = "0"
     assert worst < 2e-2, worst
 
 
@@ -116,6 +119,9 @@ def main():
                 os.environ["MFT_G4_DBG_V"] = "0"
             res["gemm8"].append(timeit(lambda: C.gemm_t(x, w, False, False, epi, impl=0, **kw), a.iters))
             res["gemm4"].append(timeit(lambda: C.gemm_t(x, w, False, False, epi, impl=2, **kw), a.iters))
+            os.environ["MFT_G4_A3"] = "1"
+            res.setdefault("gemm4-A3", []).append(timeit(lambda: C.gemm_t(x, w, False, False, epi, impl=2, **kw), a.iters))
+            os.environ["MFT_G4_A3"] = "0"
             if epi == NONE:
                 res["hipBLASLt"].append(timeit(lambda: torch.mm(x, w.t()), a.iters))
         line = f"{name:20s} M={M:6d} K={K:5d} N={N:6d} |"
