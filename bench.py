@@ -132,12 +132,23 @@ def run_native(a, cfgd) -> int:
     cmd = _native_cmd(a, cfgd)
     env = dict(os.environ)
     env.setdefault("MASTER_ADDR", "127.0.0.1")
-    # the child's log goes to our stderr as it comes (progress), its MFT_BENCH line is kept
+    env["MFT_BENCH_MARKS"] = "1"
+    # the child's log goes to our stderr as it comes (progress), its MFT_BENCH line is kept; rank 0
+    # integrates its GPU's socket power over the timed steps (MFT_BENCH_T0 .. T1) -- sysfs hwmon reads
+    # in this process, which never touches the GPU runtime
+    from mobilefinetuner_amd.energy import EnergyMeter
+    meter = EnergyMeter(gpu=int(os.environ.get("LOCAL_RANK", "0")), interval=0.02) if rank == 0 else None
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
     rec = None
     for line in p.stdout:
         if line.startswith("MFT_BENCH "):
             rec = json.loads(line[len("MFT_BENCH "):])
+        elif line.startswith("MFT_BENCH_T0"):
+            if meter:
+                meter.__enter__()
+        elif line.startswith("MFT_BENCH_T1"):
+            if meter and meter._thr is not None:
+                meter.__exit__(None, None, None)
         else:
             sys.stderr.write(line)
             sys.stderr.flush()
@@ -190,10 +201,23 @@ def run_native(a, cfgd) -> int:
             "mfu_bf16_dense": round(tflops / MI355X_BF16_DENSE_TFLOPS, 4),
             "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC if a.config == "gpt2-lora" else None,
             "peak_hbm_gb_rank0": rec.get("peak_reserved_gb"),
+            "gpu_energy_rank0": _energy(meter, rec["batch"] * rec["seq"] * rec["accum"] * rec["steps"]),
         },
     }
     print(json.dumps(out_rec), flush=True)
     return 0
+
+
+def _energy(meter, tokens_rank0):
+    """rank 0's GPU over the timed steps: mean / peak socket power and joules per token of that GPU's
+    own tokens (None when the sensors are not readable)"""
+    if meter is None or meter._thr is None:
+        return None
+    r = meter.report(tokens_rank0)
+    if not r.get("ok"):
+        return None
+    return {"mean_w": round(r["mean_w"], 1), "peak_w": round(r["peak_w"], 1),
+            "joules_per_token": round(r["joules_per_token"], 6), "samples": r["samples"]}
 
 
 def _odesc(a):

@@ -195,11 +195,23 @@ double Trainer::bench(int warmup, int steps, float* final_loss) {
     if (comm_) comm_->barrier(stream_);
     synchronize();
   };
+  // MFT_BENCH_MARKS=1 (bench.py): rank 0 brackets the timed region on stdout, so the parent can
+  // integrate the GPU's power over exactly these steps (energy per token)
+  static const bool marks = std::getenv("MFT_BENCH_MARKS") && std::getenv("MFT_BENCH_MARKS")[0] == '1';
+  const bool lead = !comm_ || comm_->rank() == 0;
   fence();
+  if (marks && lead) {
+    std::printf("MFT_BENCH_T0\n");
+    std::fflush(stdout);
+  }
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < steps; ++i) one(warmup + i);
   fence();
   double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (marks && lead) {
+    std::printf("MFT_BENCH_T1\n");
+    std::fflush(stdout);
+  }
   float l = (float)loss.item();
   if (comm_) {  // slowest rank's clock; rank-mean loss
     float h2[2] = {(float)dt, l};

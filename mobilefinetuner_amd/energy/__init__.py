@@ -9,8 +9,14 @@ The policy and the telemetry reader are native C++ (`csrc/runtime/power_monitor.
   and junction temperature instead of mocked battery values.
 * `read_gpu_telemetry(index)` — one sample of the GPU's power / temperature sensors.
 * `from_args(ns)` — build a monitor from the CLIs' `--pm_*` flags (None when throttling is off).
+* `EnergyMeter` — integrates the GPU's socket power over a run on a sampling thread (trapezoid rule over
+  the timestamped samples) and reports joules, mean / peak power and joules per token: the energy side of
+  the reference's energy-aware training, measured on the accelerator rather than a phone battery.
 """
 from __future__ import annotations
+
+import threading
+import time
 
 
 def _rt():
@@ -35,4 +41,63 @@ def from_args(ns):
     return build_power_monitor(ns)
 
 
-__all__ = ["PowerConfig", "PowerMonitor", "read_gpu_telemetry", "from_args"]
+class EnergyMeter:
+    """`with EnergyMeter(gpu=0) as m: ...train...; m.report(tokens)` -> joules, mean/peak watts, J/token.
+
+    Power is sampled every `interval` seconds on a daemon thread; the energy is the trapezoid integral
+    of the (time, watts) samples, the first one taken at `__enter__` and the last at `__exit__`.
+    `reader` (index -> dict with "ok" and "power_w") defaults to the native hwmon reader; tests pass a
+    synthetic one.  When the sensors are unavailable (`ok` false) `report()` says so instead of
+    returning a number."""
+
+    def __init__(self, gpu: int = 0, interval: float = 0.05, reader=None):
+        self.gpu, self.interval = gpu, interval
+        self._read = reader or read_gpu_telemetry
+        self.samples: list[tuple[float, float]] = []
+        self.ok = True
+        self._stop = threading.Event()
+        self._thr = None
+
+    def _sample(self):
+        t = self._read(self.gpu)
+        if not t.get("ok", False):
+            self.ok = False
+            return
+        self.samples.append((time.monotonic(), float(t["power_w"])))
+
+    def _loop(self):
+        while not self._stop.wait(self.interval):
+            self._sample()
+
+    def __enter__(self):
+        self.samples.clear()
+        self.ok = True
+        self._stop.clear()
+        self._sample()
+        self._thr = threading.Thread(target=self._loop, daemon=True)
+        self._thr.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._thr.join()
+        self._sample()
+        return False
+
+    def joules(self) -> float:
+        s = self.samples
+        return sum(0.5 * (s[i][1] + s[i - 1][1]) * (s[i][0] - s[i - 1][0]) for i in range(1, len(s)))
+
+    def report(self, tokens: int = 0) -> dict:
+        if not self.ok or len(self.samples) < 2:
+            return {"ok": False, "reason": "no GPU power telemetry"}
+        secs = self.samples[-1][0] - self.samples[0][0]
+        j = self.joules()
+        r = {"ok": True, "seconds": secs, "joules": j, "mean_w": j / secs if secs > 0 else 0.0,
+             "peak_w": max(w for _, w in self.samples), "samples": len(self.samples)}
+        if tokens:
+            r["joules_per_token"] = j / tokens
+        return r
+
+
+__all__ = ["PowerConfig", "PowerMonitor", "read_gpu_telemetry", "from_args", "EnergyMeter"]
