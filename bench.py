@@ -136,15 +136,17 @@ def run_native(a, cfgd) -> int:
     # the child's log goes to our stderr as it comes (progress), its MFT_BENCH line is kept; rank 0
     # integrates its GPU's socket power over the timed steps (MFT_BENCH_T0 .. T1) -- sysfs hwmon reads
     # in this process, which never touches the GPU runtime
-    from mobilefinetuner_amd.energy import EnergyMeter
-    meter = EnergyMeter(gpu=int(os.environ.get("LOCAL_RANK", "0")), interval=0.02) if rank == 0 else None
+    from mobilefinetuner_amd.energy import EnergyMeter, pci_power_reader
+    meter = None
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
     rec = None
     for line in p.stdout:
         if line.startswith("MFT_BENCH "):
             rec = json.loads(line[len("MFT_BENCH "):])
         elif line.startswith("MFT_BENCH_T0"):
-            if meter:
+            reader = pci_power_reader(line[len("MFT_BENCH_T0"):]) if rank == 0 else None
+            if reader:  # the GPU this rank's engine runs on, by PCI address
+                meter = EnergyMeter(interval=0.02, reader=reader)
                 meter.__enter__()
         elif line.startswith("MFT_BENCH_T1"):
             if meter and meter._thr is not None:

@@ -200,8 +200,11 @@ double Trainer::bench(int warmup, int steps, float* final_loss) {
   static const bool marks = std::getenv("MFT_BENCH_MARKS") && std::getenv("MFT_BENCH_MARKS")[0] == '1';
   const bool lead = !comm_ || comm_->rank() == 0;
   fence();
-  if (marks && lead) {
-    std::printf("MFT_BENCH_T0\n");
+  if (marks && lead) {  // + this GPU's PCI address: the parent maps it to its sysfs hwmon node
+    char bus[64] = "";
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) bus[0] = 0;
+    std::printf("MFT_BENCH_T0 %s\n", bus);
     std::fflush(stdout);
   }
   const auto t0 = std::chrono::steady_clock::now();

@@ -41,6 +41,39 @@ def from_args(ns):
     return build_power_monitor(ns)
 
 
+def pci_power_reader(pci_bus_id: str):
+    """A telemetry reader (index ignored) for the amdgpu card at `pci_bus_id` ("0000:05:00.0"), or None
+    when sysfs has no such card: the card numbering of /sys/class/drm need not follow the devices a
+    process sees, so the engine reports the PCI address of the GPU it runs on."""
+    import glob
+    import os
+    want = pci_bus_id.strip().lower()
+    if not want:
+        return None
+    for card in sorted(glob.glob("/sys/class/drm/card*/device")):
+        try:
+            if not os.path.realpath(card).lower().endswith(want):
+                continue
+        except OSError:
+            continue
+        hw = sorted(glob.glob(os.path.join(card, "hwmon", "hwmon*")))
+        if not hw:
+            return None
+        files = [os.path.join(hw[0], f) for f in ("power1_average", "power1_input")]
+
+        def read(_index=0, files=files):
+            for f in files:
+                try:
+                    with open(f) as fh:
+                        return {"ok": True, "power_w": int(fh.read().strip()) / 1e6}
+                except (OSError, ValueError):
+                    continue
+            return {"ok": False, "power_w": 0.0}
+
+        return read
+    return None
+
+
 class EnergyMeter:
     """`with EnergyMeter(gpu=0) as m: ...train...; m.report(tokens)` -> joules, mean/peak watts, J/token.
 
@@ -100,4 +133,4 @@ class EnergyMeter:
         return r
 
 
-__all__ = ["PowerConfig", "PowerMonitor", "read_gpu_telemetry", "from_args", "EnergyMeter"]
+__all__ = ["PowerConfig", "PowerMonitor", "read_gpu_telemetry", "from_args", "EnergyMeter", "pci_power_reader"]

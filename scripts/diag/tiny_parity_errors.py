@@ -1,7 +1,9 @@
 """Measured bf16-GPU vs fp32-CPU errors of the tiny-model checks in tests/test_models_gpu.py (to size
 their tolerances from data): GPT-2 tiny LoRA loss / grad rel-L2, Gemma-3 tiny logits rel-L2 / max and loss."""
+import os
 import sys
-import torch
+os.environ.setdefault("MFT_HOST_ORACLE", os.path.abspath("tests/oracle"))  # the fp32 host reference (as conftest)
+import torch  # noqa: E402
 sys.path.insert(0, ".")
 sys.path.insert(0, "tests")
 from test_models_gpu import _copy_weights, DEV  # noqa: E402

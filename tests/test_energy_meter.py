@@ -39,3 +39,9 @@ def test_energy_meter_without_telemetry():
     with m:
         time.sleep(0.03)
     assert m.report(10) == {"ok": False, "reason": "no GPU power telemetry"}
+
+
+def test_pci_power_reader_unknown_bus():
+    from mobilefinetuner_amd.energy import pci_power_reader
+    assert pci_power_reader("") is None
+    assert pci_power_reader("ffff:ff:ff.7") is None

@@ -37,10 +37,12 @@ def test_gpt2_gpu_matches_cpu_reference():
     lg = gpu(ids[:, :-1].to(DEV), ids[:, 1:].to(DEV))
     lc.backward()
     lg.backward()
-    assert abs(lc.item() - lg.item()) < 2e-2
+    # tolerances sized from measurements (scripts/diag/tiny_parity_errors.py, 4 seeds on MI355X:
+    # loss |d| 6-9e-5, LoRA grad rel-L2 1.02-1.21e-2) with ~2x margin
+    assert abs(lc.item() - lg.item()) < 1e-3
     gc, gg = fc.grad, fg.grad.cpu()
     rel = (gc - gg).norm() / gc.norm()
-    assert rel < 0.05, rel
+    assert rel < 2.5e-2, rel
 
 
 def test_gemma_gpu_matches_cpu_reference():
@@ -57,11 +59,14 @@ def test_gemma_gpu_matches_cpu_reference():
     with torch.no_grad():
         a = cpu.logits(ids)
         b = gpu.logits(ids.to(DEV)).float().cpu()
+    # measured (4 seeds): logits rel-L2 1.34-1.46e-2, max |d| / max |logit| 1.44-1.80e-2, loss |d| <= 6e-4
+    rel = ((a - b).norm() / a.norm()).item()
+    assert rel < 3e-2, rel
     err = (a - b).abs().max().item()
-    assert err < 0.1 * a.abs().max().item(), err
+    assert err < 4e-2 * a.abs().max().item(), err
     lc = cpu(ids[:, :-1], ids[:, 1:]).item()
     lg = gpu(ids[:, :-1].to(DEV), ids[:, 1:].to(DEV)).item()
-    assert abs(lc - lg) < 3e-2
+    assert abs(lc - lg) < 3e-3
 
 
 def test_full_finetune_gpu_decreases_loss():
