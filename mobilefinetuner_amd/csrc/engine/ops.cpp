@@ -234,9 +234,10 @@ Tensor sum(const Tensor& x) {
     NoGradGuard ng;
     Tensor xc = x.contiguous();
     o = empty({1}, DType::F32, x.device());
-    // two-stage: rows of up to 4096, then the row sums
+    // two-stage: rows of 4096 (one wave each), then the row sums -- a single wave only for n <= 4096
+    // (one wave over Gemma's 65,536 per-token losses was a 0.5 ms dependent-load chain per step)
     const int64_t n = x.numel();
-    if (n <= 65536) {
+    if (n <= 4096) {
       k::sum_rows(xc.data_ptr(), (int)xc.dtype(), o.data_ptr(), (int)DType::F32, 1, (int)n, 1.f, S());
     } else {
       const int64_t w = 4096, rows = n / w, rem = n - rows * w;

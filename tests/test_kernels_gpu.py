@@ -161,6 +161,34 @@ def test_gemm8_lora_epilogue(M, N, K, R):
     assert (wide[:, N:].float() == 7.0).all()
 
 
+@pytest.mark.parametrize("a3", ["0", "1"])
+@pytest.mark.parametrize("M,K,N", [(1000, 832, 776), (4096 + 40, 768, 2040)])
+def test_gemm4_nt_epilogues(M, K, N, a3, monkeypatch):
+    """gemm4 (4-wave 256x256, AGPR accumulators via tied asm MFMAs, range-checked buffer LDS-DMA;
+    gemm_t impl=2, opt-in) and its asymmetric-ring form (MFT_G4_A3=1): every NT epilogue vs fp32
+    torch on row / column tails, many K-tiles."""
+    from mobilefinetuner_amd._ext import native
+    monkeypatch.setenv("MFT_G4_A3", a3)  # read on every launch
+    C = native()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    ref_ = x.float() @ w.float().t()
+    _close(C.gemm_t(x, w, False, False, 0, impl=2)[0], ref_, 0.02, 0.01, msg="gemm4 none")
+    _close(C.gemm_t(x, w, False, False, 1, bias=b, impl=2)[0], ref_ + b.float(), 0.02, 0.01, msg="gemm4 bias")
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    y = C.gemm_t(x, w, False, False, 9, bias=b, aux=aux, impl=2)[0]  # BIAS_GELU_D
+    _close(y, torch.nn.functional.gelu(ref_ + b.float(), approximate="tanh"), 0.02, 0.01, msg="gemm4 gelu")
+    u = torch.randn(M, 8, device=DEV).bfloat16()
+    lw = (torch.randn(8, N, device=DEV) * 0.1).bfloat16()
+    y = C.gemm_t(x, w, False, False, 5, alpha=0.5, lora_u=u, lora_w=lw, impl=2)[0]
+    _close(y, 0.5 * ref_ + u.float() @ lw.float(), 0.03, 0.01, msg="gemm4 lora")
+    acc = torch.randn(M, N, device=DEV)
+    want = acc + 2.0 * ref_
+    C.gemm_t(x, w, False, False, 4, alpha=2.0, out=acc, impl=2)
+    _close(acc, want, 0.03, 0.01, msg="gemm4 f32 acc")
+
+
 @pytest.mark.parametrize("dropout", [0.0, 0.2])
 def test_lora_augmented_k_matches_plain(dropout):
     """_LoRALinearAug ([x | u] . [W | sB^T] single GEMM) == _LoRALinear (GEMM + rank-r update)."""
