@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONPATH=$PWD
-timeout -k 10 600 python3 -u -m pytest tests/test_kernels_gpu.py tests/test_engine_gemma_gpu.py tests/test_engine_gpu.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r3_check3.log 2>&1; rc=$?
+timeout -k 10 600 python3 -u -m pytest tests/test_kernels_gpu.py tests/test_lm_head_ce_gpu.py tests/test_engine_gemma_gpu.py tests/test_engine_gpu.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r3_check3.log 2>&1; rc=$?
 echo "tests rc=$rc"; grep -E "passed|failed" gpurun_out/r3_check3.log | tail -2; grep -E "^FAILED" gpurun_out/r3_check3.log | head; [ $rc -eq 0 ] || exit 1
 for cfg in gemma3-270m-lora gpt2-lora; do
   timeout -k 10 300 python3 bench.py --config $cfg --steps 20 --warmup 5 > gpurun_out/r3_c3.json 2> gpurun_out/r3_c3.err || { tail -20 gpurun_out/r3_c3.err; exit 1; }
