@@ -370,7 +370,17 @@ __global__ void nll_rows_bwd_kernel(void* d, int dt, const int64_t* t, long rows
 __global__ void count_valid_kernel(const int64_t* t, long n, int ignore, float* out) {
   __shared__ float sm[16];
   float c = 0.f;
-  for (long i = threadIdx.x; i < n; i += blockDim.x) c += (t[i] != ignore && t[i] >= 0) ? 1.f : 0.f;
+  // 8 independent loads in flight per thread (one block: the step's 131,072 labels were a 60 us chain
+  // of dependent-latency iterations); integer counts, so the sum is exact in any order
+  long i = threadIdx.x;
+  for (; i + 7 * (long)blockDim.x < n; i += 8 * (long)blockDim.x) {
+    int64_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = t[i + u * (long)blockDim.x];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) c += (v[u] != ignore && v[u] >= 0) ? 1.f : 0.f;
+  }
+  for (; i < n; i += blockDim.x) c += (t[i] != ignore && t[i] >= 0) ? 1.f : 0.f;
   c = block_sum(c, sm);
   if (threadIdx.x == 0) out[0] = c;
 }
