@@ -531,10 +531,10 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
   bool nodrop = true;
   for (auto& a : ads) nodrop = nodrop && (a.dropout <= 0.f || !training);
   int off = K;
+  Tensor acat;  // [sum r_i, K]: built once per step, reused by the backward's fused dx epilogue
   if (nodrop && ads.size() > 1) {  // one pass over x for every u_i (adjacent appended columns)
     std::vector<Tensor> as;
     for (auto& a : ads) as.push_back(a.A.c);
-    Tensor acat;
     {
       NoGradGuard ng;
       acat = cat(as, 0);
@@ -569,7 +569,7 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
     std::vector<LoraAdapter>* pads = &ads;
     Tensor wa = waug;
     Shape xshape = xa.shape();
-    auto n = lambda_node("LoRALinearBackward", [xa2, xshape, K, Ka, M, N, pw, pads, s, wa, training, drop_ctr,
+    auto n = lambda_node("LoRALinearBackward", [xa2, xshape, K, Ka, M, N, pw, pads, s, wa, training, drop_ctr, acat_f = acat,
                                                  nin = ins.size()](std::vector<Tensor>& g) {
       std::vector<Tensor> out(nin);
       if (!g[0].defined()) return out;
@@ -606,8 +606,8 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         }
         o += a.rank;
       }
-      Tensor acat;
-      {
+      Tensor acat = acat_f;
+      if (!acat.defined()) {
         std::vector<Tensor> as;
         for (auto& a : ads) as.push_back(a.A.c);
         acat = as.size() == 1 ? as[0] : cat(as, 0);
