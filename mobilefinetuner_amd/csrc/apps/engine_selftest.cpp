@@ -392,7 +392,7 @@ int main() {
   }
   // ---------------------------------------------------------------- allocator
   {
-    auto& al = CachingAllocator::get(0);
+    auto& al = CachingAllocator::get(Device::current_hip_device());
     synchronize();
     const auto s0 = al.stats();
     { Tensor big = empty({64 << 20}, DType::F32); }

@@ -308,7 +308,7 @@ int run(int argc, char** argv) {
     model->save_hf(out_path);
     std::printf("  model saved to: %s\n", out_path.c_str());
   }
-  const AllocStats st = CachingAllocator::get(0).stats();
+  const AllocStats st = CachingAllocator::get(Device::current_hip_device()).stats();
   std::printf("\n========================================\nTraining complete!\n  Total steps: %lld\n"
               "  Total tokens: %lld\n  Wall time: %.2f s (%.0f tokens/s)\n  Final EMA loss: %.4f\n"
               "  HBM: peak allocated %.2f GB, reserved %.2f GB\n========================================\n",

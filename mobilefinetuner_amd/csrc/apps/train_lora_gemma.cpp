@@ -500,7 +500,7 @@ int run(int argc, char** argv) {
     auto ev = trainer.evaluate(tc.eval_batches, tc.eval_batch_size);
     if (lead) std::printf("[Eval] valid_loss=%.4f valid_ppl=%.2f\n", ev.first, ev.second);
   }
-  const AllocStats st = CachingAllocator::get(0).stats();
+  const AllocStats st = CachingAllocator::get(Device::current_hip_device()).stats();
   std::printf("\nTraining complete: %lld steps, %lld tokens, %.2f s (%.0f tokens/s), final EMA loss %.4f, "
               "HBM peak allocated %.2f GB\n",
               (long long)trainer.global_step, (long long)trainer.total_tokens, secs, trainer.total_tokens / secs,

@@ -49,6 +49,11 @@ namespace {
 thread_local hipStream_t t_stream = nullptr;
 }
 hipStream_t current_stream() { return t_stream; }
+int Device::current_hip_device() {
+  int d = 0;
+  HIP_OK(hipGetDevice(&d));
+  return d;
+}
 void set_current_stream(hipStream_t s) { t_stream = s; }
 void synchronize() { HIP_OK(hipStreamSynchronize(t_stream)); }
 

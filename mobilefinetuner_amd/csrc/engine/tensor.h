@@ -57,7 +57,10 @@ struct Device {
   int index = 0;
   bool pinned = false;  // CPU only: page-locked (hipHostMalloc) staging memory
   static Device cpu(bool pinned = false) { return Device{CPU, -1, pinned}; }
-  static Device hip(int i = 0) { return Device{HIP, i, false}; }
+  // i < 0: the calling thread's current HIP device (LOCAL_RANK's GPU once the communicator has
+  // selected it), so one-process-per-GPU ranks allocate on their own card, never on GPU 0
+  static Device hip(int i = -1) { return Device{HIP, i < 0 ? current_hip_device() : i, false}; }
+  static int current_hip_device();
   bool is_hip() const { return kind == HIP; }
   bool operator==(const Device& o) const { return kind == o.kind && index == o.index; }
 };

@@ -89,7 +89,7 @@ void Trainer::fwd_bwd() {
 
 void Trainer::capture() {
   TraceRange range("mft.capture");
-  auto& al = CachingAllocator::get(0);
+  auto& al = CachingAllocator::get(Device::current_hip_device());
   pool_ = al.new_pool();
   CachingAllocator::set_current_pool(pool_);
   HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
