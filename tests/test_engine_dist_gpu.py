@@ -217,6 +217,27 @@ def test_native_bench_json_line(tmp_path):
     assert abs(rec["value"] - 64 * 128 * 3 / (rec["ms_per_step"] * 3 / 1000)) < 0.01 * rec["value"]
 
 
+def test_native_bench_under_torchrun_two_ranks():
+    """The driver's N>1 launch exactly (python -m torch.distributed.run ... bench.py --gpus 2): each
+    rank's bench.py starts its native child, the children bootstrap their communicator on
+    MASTER_PORT + 1 and rank 0 prints one record for the whole job.  Loopback backend: both ranks
+    share the box's one GPU, so the record counts one physical device."""
+    import json
+    env = _env()
+    env["MFT_COMM_BACKEND"] = "loopback"
+    r = subprocess.run(["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2", "--batch", "64"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 1 and rec["config"]["ranks"] == 2 and rec["config"]["global_batch"] == 128
+    assert rec["config"]["parallelism"] == "dp2" and rec["steps"] == 3 and rec["value"] > 0
+    assert abs(rec["value"] - 2 * 64 * 128 * 3 / (rec["ms_per_step"] * 3 / 1000)) < 0.01 * rec["value"]
+
+
 @pytest.mark.parametrize("prog,args,bflag", [
     ("gpt2_full_finetune", FULL, "--batch_size"),
     ("gpt2_full_finetune", FULL + ["--zero_stage", "3"], "--batch_size"),
