@@ -13,6 +13,12 @@ static inline int ew_grid(long n8) {
   return (int)(g < 8192 ? (g > 0 ? g : 1) : 8192);
 }
 
+// one block per row pair, capped at 16,384 blocks (64 per CU)
+static inline int gated_grid(long M) {
+  const long g = (M + 1) / 2;
+  return (int)(g < 16384 ? (g > 0 ? g : 1) : 16384);
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 __device__ __forceinline__ float silu_grad(float x) {
   float s = 1.f / (1.f + __expf(-x));
@@ -47,43 +53,61 @@ __global__ void gelu_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __re
     for (long i = n8 * 8 + threadIdx.x; i < n; i += blockDim.x) dx[i] = f2bf(bf2f(dy[i]) * gelu_tanh_grad(bf2f(x[i])));
 }
 
+// Gated kernels: a block walks whole rows (blockIdx.x, stride gridDim.x) and its threads stride the row's
+// 8-column groups, so no 64-bit division per element; two rows' loads are issued before either is used
+// (3 x 16 B per lane in flight in the forward, 6 in the backward).
 template <int ACT>
 __global__ void gated_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ y, long M, int I, long ldy) {
-  const int c8 = I / 8;
-  const long n8 = M * c8;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += (long)gridDim.x * blockDim.x) {
-    const long m = t / c8;
-    const int c = (int)(t % c8) * 8;
-    float g[8], u[8];
-    load8(gu + m * 2 * I + c, g);
-    load8(gu + m * 2 * I + I + c, u);
+  for (long m0 = 2L * blockIdx.x; m0 < M; m0 += 2L * gridDim.x) {
+    const bool two = m0 + 1 < M;
+    for (int c = threadIdx.x * 8; c < I; c += blockDim.x * 8) {
+      float g[2][8], u[2][8];
+      load8(gu + m0 * 2 * I + c, g[0]);
+      load8(gu + m0 * 2 * I + I + c, u[0]);
+      if (two) {
+        load8(gu + (m0 + 1) * 2 * I + c, g[1]);
+        load8(gu + (m0 + 1) * 2 * I + I + c, u[1]);
+      }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) g[j] = (ACT == 0 ? gelu_tanh(g[j]) : silu(g[j])) * u[j];
-    store8(y + m * ldy + c, g);
+      for (int r = 0; r < 2; ++r) {
+        if (r == 1 && !two) break;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[r][j] = (ACT == 0 ? gelu_tanh(g[r][j]) : silu(g[r][j])) * u[r][j];
+        store8(y + (m0 + r) * ldy + c, g[r]);
+      }
+    }
   }
 }
 
 template <int ACT>
 __global__ void gated_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dy, bf16_t* __restrict__ dgu,
                                  long M, int I, long ldd) {
-  const int c8 = I / 8;
-  const long n8 = M * c8;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += (long)gridDim.x * blockDim.x) {
-    const long m = t / c8;
-    const int c = (int)(t % c8) * 8;
-    float g[8], u[8], d[8], dg[8], du[8];
-    load8(gu + m * 2 * I + c, g);
-    load8(gu + m * 2 * I + I + c, u);
-    load8(dy + m * ldd + c, d);
+  for (long m0 = 2L * blockIdx.x; m0 < M; m0 += 2L * gridDim.x) {
+    const bool two = m0 + 1 < M;
+    for (int c = threadIdx.x * 8; c < I; c += blockDim.x * 8) {
+      float g[2][8], u[2][8], d[2][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float a = ACT == 0 ? gelu_tanh(g[j]) : silu(g[j]);
-      const float ag = ACT == 0 ? gelu_tanh_grad(g[j]) : silu_grad(g[j]);
-      du[j] = d[j] * a;
-      dg[j] = d[j] * u[j] * ag;
+      for (int r = 0; r < 2; ++r) {
+        if (r == 1 && !two) break;
+        load8(gu + (m0 + r) * 2 * I + c, g[r]);
+        load8(gu + (m0 + r) * 2 * I + I + c, u[r]);
+        load8(dy + (m0 + r) * ldd + c, d[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        if (r == 1 && !two) break;
+        float dg[8], du[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = ACT == 0 ? gelu_tanh(g[r][j]) : silu(g[r][j]);
+          const float ag = ACT == 0 ? gelu_tanh_grad(g[r][j]) : silu_grad(g[r][j]);
+          du[j] = d[r][j] * a;
+          dg[j] = d[r][j] * u[r][j] * ag;
+        }
+        store8(dgu + (m0 + r) * 2 * I + c, dg);
+        store8(dgu + (m0 + r) * 2 * I + I + c, du);
+      }
     }
-    store8(dgu + m * 2 * I + c, dg);
-    store8(dgu + m * 2 * I + I + c, du);
   }
 }
 
@@ -96,12 +120,12 @@ void gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, long n, hipStream_t
 // ldy / ldd: row strides of y / dy (> I when y is the widened augmented-K input of a LoRA
 // consumer, see bindings.cpp alloc_wide)
 void gated_fwd(const bf16_t* gu, bf16_t* y, long M, int I, long ldy, int act, hipStream_t st) {
-  const int g = ew_grid(M * (I / 8));
+  const int g = gated_grid(M);
   if (act == 0) gated_fwd_kernel<0><<<g, 256, 0, st>>>(gu, y, M, I, ldy);
   else gated_fwd_kernel<1><<<g, 256, 0, st>>>(gu, y, M, I, ldy);
 }
 void gated_bwd(const bf16_t* gu, const bf16_t* dy, long ldd, bf16_t* dgu, long M, int I, int act, hipStream_t st) {
-  const int g = ew_grid(M * (I / 8));
+  const int g = gated_grid(M);
   if (act == 0) gated_bwd_kernel<0><<<g, 256, 0, st>>>(gu, dy, dgu, M, I, ldd);
   else gated_bwd_kernel<1><<<g, 256, 0, st>>>(gu, dy, dgu, M, I, ldd);
 }
