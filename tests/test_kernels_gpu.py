@@ -669,3 +669,23 @@ def test_colsum_and_wgrad_accumulate():
     w = torch.ones(N, K, device=DEV)
     C.lt_wgrad_acc(x, dy, w, 0.5)
     _close(w, 1.0 + 0.5 * dy.float().t() @ x.float(), 0.05, 1e-3, msg="wgrad acc")
+
+
+def test_gated_row_pair_grid_stride():
+    """gated kernels' row-pair mapping: an odd row count past the 16,384-block cap (grid-strided pairs, a
+    lone last row) and I = 2056 > 256 lanes x 8 columns (a partial second column pass)."""
+    from mobilefinetuner_amd.ops import functional as Fx
+    M, I = 32771, 2056
+    for act in ("gelu", "silu"):
+        gu = torch.randn(M, 2 * I, device=DEV).bfloat16().requires_grad_()
+        y = Fx.gated_act(gu, act)
+        g = torch.randn_like(y)
+        (y.float() * g.float()).sum().backward()
+        r = gu.detach().float().requires_grad_()
+        a, u = r.chunk(2, -1)
+        yr = (torch.nn.functional.gelu(a, approximate="tanh") if act == "gelu" else torch.nn.functional.silu(a)) * u
+        (yr * g.float()).sum().backward()
+        # |y| reaches ~25 over 67M outputs: half a bf16 ulp there is ~0.06, so the bound scales with max |y|
+        _close(y, yr, 0.02, 0.01, msg=f"gated {act} long")
+        _close(gu.grad, r.grad, 0.1, 0.01, msg=f"gated {act} long grad")
+        del gu, y, g, r, yr
