@@ -281,8 +281,9 @@ inline eng::DiskTier disk_tier_from(const Args& a) {
 inline void print_streaming(const eng::WeightStreamer* ws, const char* what) {
   if (ws->on_disk())
     std::printf("  weight streaming ON: %d device slots (%.1f MB) for %.1f MB of frozen %s weights on disk (%s), "
-                "%.1f MB pinned staging\n", ws->slots(), ws->device_bytes() / 1048576.0, ws->disk_bytes() / 1048576.0, what,
-                "block files", ws->host_bytes() / 1048576.0);
+                "%.1f MB pinned staging; %lld block(s) kept bf16 (not exactly representable in fp16)\n", ws->slots(),
+                ws->device_bytes() / 1048576.0, ws->disk_bytes() / 1048576.0, what, "block files",
+                ws->host_bytes() / 1048576.0, (long long)ws->bf16_fallbacks);
   else
     std::printf("  weight streaming ON: %d device slots (%.1f MB) for %.1f MB of frozen %s weights in pinned host memory\n",
                 ws->slots(), ws->device_bytes() / 1048576.0, ws->host_bytes() / 1048576.0, what);
@@ -321,9 +322,13 @@ inline void save_npy_f32(const std::string& path, const std::vector<float>& v, c
   save_npy(path, v.data(), shape, "<f4", 4);
 }
 
-// --pm_* flags (reference energy options) -> PowerMonitor, or null when off
+// --pm_* flags (reference energy options) -> PowerMonitor, or null when off.  The telemetry is this
+// rank's own GPU (the HIP device's PCI address -> its DRM card's hwmon), never "card 0".
+// --pm_power_cap W: software power cap (sleep per step so the socket power averages <= W; implies
+// GPU telemetry and, without --pm_interval, a check every step).
 inline std::unique_ptr<PowerMonitor> power_monitor_from(const Args& a) {
-  if (a.i("pm_interval", 0) <= 0 && a.get("pm_schedule").empty()) return nullptr;
+  const float cap = a.f("pm_power_cap", 0.f);
+  if (a.i("pm_interval", 0) <= 0 && a.get("pm_schedule").empty() && cap <= 0.f) return nullptr;
   PowerConfig pc;
   pc.check_interval_steps = a.i("pm_interval", 0);
   pc.battery_threshold = a.f("pm_batt_thresh", 20.f);
@@ -334,7 +339,14 @@ inline std::unique_ptr<PowerMonitor> power_monitor_from(const Args& a) {
   pc.freq_t_low = a.f("pm_ft_low", 0.5f);
   pc.enable_battery = !a.b("pm_disable_batt");
   pc.enable_temp = !a.b("pm_disable_temp");
-  pc.use_gpu_telemetry = a.b("pm_gpu_telemetry");
+  pc.use_gpu_telemetry = a.b("pm_gpu_telemetry") || cap > 0.f;
+  pc.power_cap_w = cap;
+  if (cap > 0.f && pc.check_interval_steps <= 0) pc.check_interval_steps = 1;
+  {
+    int dev = 0;
+    char bus[64] = {0};
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) pc.pci_bus = bus;
+  }
   auto pm = std::make_unique<PowerMonitor>(pc);
   pm->set_manual_readings(a.f("pm_manual_batt", 100.f), a.f("pm_manual_temp", 30.f));
   if (!a.get("pm_schedule").empty()) pm->set_step_schedule(PowerMonitor::parse_schedule(a.get("pm_schedule")));

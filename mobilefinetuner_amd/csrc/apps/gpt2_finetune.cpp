@@ -59,7 +59,7 @@ const std::set<std::string> kValued = {
     "batch_size", "grad_accum_steps", "seq_len", "rank", "alpha", "lr", "weight_decay", "warmup_steps",
     "clip_grad_norm", "lora_dropout", "data_fraction", "log_interval", "eval_interval", "eval_batches",
     "eval_batch_size", "save_every", "ema_beta", "seed", "pm_interval", "pm_batt_thresh", "pm_temp_thresh",
-    "pm_fb_high", "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule",
+    "pm_fb_high", "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "pm_power_cap",
     "shard_dir", "shard_budget_mb", "shard_fp16_disk", "model", "synthetic_tokens", "pretokenized_path",
     "pretokenized_meta", "lora_targets", "metrics_out", "device", "bench_steps", "bench_warmup", "zero_stage", "offload", "bucket_mb", "dump_grads"};
 
@@ -103,7 +103,7 @@ void usage() {
       "  --weight_decay W --warmup_steps W --clip_grad_norm C --lora_dropout P --data_fraction F --log_interval N\n"
       "  --eval_interval N --eval_batches N --eval_batch_size B --save_every N --ema_beta B --seed S\n"
       "  --pm_interval --pm_batt_thresh --pm_temp_thresh --pm_fb_high --pm_fb_low --pm_ft_high --pm_ft_low\n"
-      "  --pm_manual_batt --pm_manual_temp --pm_disable_batt --pm_disable_temp --pm_schedule --pm_gpu_telemetry\n"
+      "  --pm_manual_batt --pm_manual_temp --pm_disable_batt --pm_disable_temp --pm_schedule --pm_gpu_telemetry --pm_power_cap W\n"
       "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --pretokenized_path F\n"
       "          --pretokenized_meta F --lora_targets T --split_qkv --no_graph --compat_l2_adam --metrics_out F\n"
       "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"

@@ -288,26 +288,39 @@ class LoopbackComm final : public Communicator {
     std::atomic<bool> done{false};
   };
 
-  LoopbackComm(int rank, int world, int local) {
+  // host_only: no HIP call at all (GPU-less CI): collectives take HOST buffers and run
+  // synchronously on the calling thread (the stream argument is ignored) -- the same bootstrap, wire
+  // protocol, rank-0 reduction and watchdog as the device path, which stages through pinned buffers
+  // and runs them on a HIP host-callback thread instead
+  LoopbackComm(int rank, int world, int local, bool host_only = false) : host_(host_only) {
     rank_ = rank, world_ = world, local_ = local;
-    int ndev = 1;
-    HIP_OK(hipGetDeviceCount(&ndev));
-    device_ = ndev > 0 ? local % ndev : 0;
-    HIP_OK(hipSetDevice(device_));
+    if (!host_) {
+      int ndev = 1;
+      HIP_OK(hipGetDeviceCount(&ndev));
+      device_ = ndev > 0 ? local % ndev : 0;
+      HIP_OK(hipSetDevice(device_));
+    } else {
+      device_ = -1;
+    }
     if (world_ > 1) fds_ = star_connect(rank_, world_);
-    HIP_OK(hipMalloc(&barrier_buf_, sizeof(float)));
+    if (!host_) HIP_OK(hipMalloc(&barrier_buf_, sizeof(float)));
+    else barrier_buf_ = &host_barrier_;
     start_watchdog();
   }
   ~LoopbackComm() override {
-    (void)hipDeviceSynchronize();
+    if (!host_) (void)hipDeviceSynchronize();
     stop_watchdog();
     for (int fd : fds_)
       if (fd >= 0) ::close(fd);
     for (Op* o : ops_) release(o);
     for (auto& kv : pool_)
-      for (void* p : kv.second) (void)hipHostFree(p);
-    if (barrier_buf_) (void)hipFree(barrier_buf_);
+      for (void* p : kv.second) {
+        if (host_) std::free(p);
+        else (void)hipHostFree(p);
+      }
+    if (barrier_buf_ && !host_) (void)hipFree(barrier_buf_);
   }
+  bool host_only() const override { return host_; }
   const char* backend() const override { return "loopback"; }
 
   void all_reduce(void* buf, size_t n, CommType t, CommOp op, hipStream_t st) override {
@@ -336,7 +349,9 @@ class LoopbackComm final : public Communicator {
       return p;
     }
     void* p = nullptr;
-    HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    if (host_) p = std::malloc(bytes);
+    else HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    if (!p) throw std::runtime_error("loopback: out of host memory");
     return p;
   }
   void release(Op* o) {
@@ -362,6 +377,21 @@ class LoopbackComm final : public Communicator {
     ++issued;
     std::lock_guard<std::mutex> g(host_mu_);
     reclaim();
+    if (host_) {  // synchronous host collective
+      Op o;
+      o.self = this;
+      o.kind = kind, o.t = t, o.op = op, o.root = root, o.n = n;
+      o.tag = next_tag_++;
+      o.in_bytes = in_bytes, o.out_bytes = out_bytes;
+      o.in = static_cast<char*>(pinned(in_bytes));
+      o.out = static_cast<char*>(pinned(out_bytes));
+      if (in_bytes) std::memcpy(o.in, dsend, in_bytes);
+      exchange(o);
+      if (out_bytes) std::memcpy(drecv, o.out, out_bytes);
+      if (o.in) pool_[in_bytes].push_back(o.in);
+      if (o.out) pool_[out_bytes].push_back(o.out);
+      return;
+    }
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIP_OK(hipStreamIsCapturing(st, &cs));
     Op* o = new Op();
@@ -462,6 +492,8 @@ class LoopbackComm final : public Communicator {
   std::set<Op*> persistent_;
   std::map<size_t, std::vector<void*>> pool_;
   uint32_t next_tag_ = 1;
+  bool host_ = false;
+  float host_barrier_ = 0.f;
 };
 
 int64_t now_ns() {
@@ -491,12 +523,12 @@ struct Communicator::Watchdog {
   std::mutex mu;
   std::condition_variable cv;
   bool stop = false;
-  std::atomic<int64_t> last_ns{0};
+  std::atomic<int64_t> last_ns{0};  // 0: no heartbeat yet (setup is not timed)
+  std::atomic<int> quiet{0};
 };
 
 void Communicator::start_watchdog() {
   wd_ = std::make_unique<Watchdog>();
-  wd_->last_ns = now_ns();
   const double timeout = comm_timeout_s();
   Watchdog* wd = wd_.get();
   wd->th = std::thread([this, wd, timeout]() {
@@ -506,7 +538,9 @@ void Communicator::start_watchdog() {
       if (wd->stop) break;
       std::string what;
       if (async_error(&what)) fail(what);
-      const double idle = (double)(now_ns() - wd->last_ns.load()) * 1e-9;
+      if (wd->quiet.load() > 0) wd->last_ns = now_ns();
+      const int64_t last = wd->last_ns.load();
+      const double idle = last > 0 ? (double)(now_ns() - last) * 1e-9 : 0.0;
       if (timeout > 0 && idle > timeout)
         fail("no progress for " + std::to_string((int)idle) + " s (MFT_COMM_TIMEOUT=" + std::to_string((int)timeout) +
              "): a peer rank is gone or hung");
@@ -527,6 +561,10 @@ void Communicator::stop_watchdog() {
 
 void Communicator::heartbeat() {
   if (wd_) wd_->last_ns = now_ns();
+}
+
+void Communicator::quiet(int delta) {
+  if (wd_) wd_->quiet += delta;
 }
 
 void Communicator::fail(const std::string& why) {
@@ -554,7 +592,12 @@ std::unique_ptr<Communicator> Communicator::from_env(bool force) {
 
 void Communicator::barrier(hipStream_t st) {
   all_reduce(barrier_buf_, 1, CommType::F32, CommOp::Sum, st);
-  HIP_OK(hipStreamSynchronize(st));
+  if (!host_only()) HIP_OK(hipStreamSynchronize(st));
+}
+
+std::unique_ptr<Communicator> Communicator::host_loopback(int rank, int world) {
+  if (rank < 0 || rank >= world) throw std::runtime_error("comm: RANK out of range");
+  return std::unique_ptr<Communicator>(new LoopbackComm(rank, world, rank, true));
 }
 
 }  // namespace eng

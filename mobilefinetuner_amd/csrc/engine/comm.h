@@ -59,6 +59,10 @@ class Communicator {
   // send == recv + rank * n_per_rank
   virtual void all_gather(const void* send, void* recv, size_t n_per_rank, CommType t, hipStream_t st) = 0;
   virtual void broadcast(void* buf, size_t bytes, int root, hipStream_t st) = 0;
+  // a host-only loopback communicator (no HIP calls; collectives on HOST buffers, synchronous):
+  // the GPU-less CI of the bootstrap, wire protocol, reductions and watchdog (tests/, ctest)
+  static std::unique_ptr<Communicator> host_loopback(int rank, int world);
+  virtual bool host_only() const { return false; }
   void barrier(hipStream_t st);  // a 1-element all-reduce, then a stream sync
 
   void all_reduce_sum(float* buf, size_t n, hipStream_t st) { all_reduce(buf, n, CommType::F32, CommOp::Sum, st); }
@@ -66,7 +70,25 @@ class Communicator {
   void all_reduce_max(float* buf, size_t n, hipStream_t st) { all_reduce(buf, n, CommType::F32, CommOp::Max, st); }
 
   // ---- failure detection
+  // The idle timer starts at the first heartbeat (setup -- model / checkpoint loading, ZeRO-3
+  // layout, the first capture -- is not timed) and is suspended while a QuietScope is open (long
+  // rank-local phases: evaluation, checkpoint writes / reads).
   void heartbeat();                                 // progress mark (once per trainer step)
+  void quiet(int delta);                            // QuietScope's counter
+  struct QuietScope {
+    Communicator* c;
+    explicit QuietScope(Communicator* cm) : c(cm) {
+      if (c) c->quiet(+1);
+    }
+    ~QuietScope() {
+      if (c) {
+        c->quiet(-1);
+        c->heartbeat();
+      }
+    }
+    QuietScope(const QuietScope&) = delete;
+    QuietScope& operator=(const QuietScope&) = delete;
+  };
   [[noreturn]] void fail(const std::string& why);  // abort the backend, print, _exit(3)
   int64_t issued = 0;                               // collectives this rank enqueued
 

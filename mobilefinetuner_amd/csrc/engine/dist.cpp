@@ -21,26 +21,41 @@ FlatPlan plan_flat(const std::vector<std::pair<std::string, Param*>>& params, in
   FlatPlan p;
   p.offsets.assign(n, 0);
   p.bucket_of.assign(n, 0);
-  // buckets of consecutive parameters, formed in backward order (last parameter first)
-  std::vector<std::pair<int, int>> ranges;  // [first, last] parameter index, backward order
-  int hi = n - 1;
-  int64_t bytes = 0;
-  for (int i = n - 1; i >= 0; --i) {
-    bytes += params[i].second->leaf.numel() * 4;
-    if (bytes >= bucket_bytes || i == 0) {
-      ranges.push_back({i, hi});
-      hi = i - 1;
-      bytes = 0;
+  // Parameters that COMPUTE in fp32 (the norm weights) read the fp32 master itself (FlatParams), so
+  // under ZeRO-1/2 a rank that does not own their chunk would never see their update: they go into
+  // one trailing REPLICATED bucket (all-reduced, updated in full on every rank; it is small).
+  std::vector<int> part, rep;
+  for (int i = 0; i < n; ++i) (params[i].second->c.dtype() == DType::F32 ? rep : part).push_back(i);
+  // buckets of consecutive partitioned parameters, formed in backward order (last parameter first);
+  // each is a list of parameter indices in forward order
+  std::vector<std::vector<int>> groups;
+  {
+    std::vector<int> cur;
+    int64_t bytes = 0;
+    for (int j = (int)part.size() - 1; j >= 0; --j) {
+      cur.insert(cur.begin(), part[j]);
+      bytes += params[part[j]].second->leaf.numel() * 4;
+      if (bytes >= bucket_bytes || j == 0) {
+        groups.push_back(cur);
+        cur.clear();
+        bytes = 0;
+      }
     }
+    if (groups.empty() && rep.empty()) groups.push_back({});
   }
-  if (n == 0) ranges.push_back({0, -1});
-  // offsets in forward order; each bucket padded to world x 64 elements
+  const int np = (int)groups.size();
+  if (!rep.empty()) groups.push_back(rep);  // launched last: its grads are final only at the end
+  // offsets in forward order (partitioned buckets: the launch order reversed, then the replicated
+  // one); every bucket padded to world x 64 elements
   const int64_t quantum = kAlign * world;
   int64_t off = 0;
-  std::vector<std::pair<int64_t, int64_t>> fwd(ranges.size());
-  for (int k = (int)ranges.size() - 1; k >= 0; --k) {
+  std::vector<std::pair<int64_t, int64_t>> fwd(groups.size());
+  std::vector<int> layout;
+  for (int k = np - 1; k >= 0; --k) layout.push_back(k);
+  if ((int)groups.size() > np) layout.push_back(np);
+  for (int k : layout) {
     const int64_t lo = off;
-    for (int i = ranges[k].first; i <= ranges[k].second; ++i) {
+    for (int i : groups[k]) {
       p.offsets[i] = off;
       p.bucket_of[i] = k;
       off += round_up(params[i].second->leaf.numel(), kAlign);
@@ -50,6 +65,8 @@ FlatPlan plan_flat(const std::vector<std::pair<std::string, Param*>>& params, in
   }
   p.numel = off;
   p.buckets = fwd;  // index k = launch order (k = 0 holds the last parameters of the forward)
+  p.replicated.assign(groups.size(), 0);
+  if ((int)groups.size() > np) p.replicated[np] = 1;
   return p;
 }
 
@@ -84,6 +101,12 @@ DataParallel::DataParallel(FlatParams& flat, const FlatPlan& plan, Communicator&
     for (int b = 0; b < nb; ++b) order[b] = b;
     std::sort(order.begin(), order.end(), [&](int a, int b) { return plan_.buckets[a].first < plan_.buckets[b].first; });
     for (int b : order) {
+      if (plan_.replicated[b]) {  // every rank updates (and keeps moments for) the whole bucket
+        const int64_t len = plan_.buckets[b].second - plan_.buckets[b].first;
+        segs.push_back({plan_.buckets[b].first, len, st, true});
+        st += len;
+        continue;
+      }
       const int64_t cs = chunk(b);
       segs.push_back({plan_.buckets[b].first + r * cs, cs, st});
       st += cs;
@@ -134,14 +157,15 @@ void DataParallel::launch(int b) {
   const int64_t lo = plan_.buckets[b].first, n = plan_.buckets[b].second - lo, c = chunk(b);
   const int r = comm_.rank();
   float* g = flat_.grad.data<float>() + lo;
+  const bool scatter = cfg_.zero_stage == 2 && !plan_.replicated[b];
   if (!cfg_.bf16_reduce) {
-    if (cfg_.zero_stage == 2) comm_.reduce_scatter(g, g + r * c, c, CommType::F32, CommOp::Sum, stream_);
+    if (scatter) comm_.reduce_scatter(g, g + r * c, c, CommType::F32, CommOp::Sum, stream_);
     else comm_.all_reduce(g, n, CommType::F32, CommOp::Sum, stream_);
     return;
   }
   ::mft::bf16_t* h = (::mft::bf16_t*)comm_buf_.data_ptr() + lo;
   ::mft::cast_f32_bf16(g, h, n, stream_);
-  if (cfg_.zero_stage == 2) {
+  if (scatter) {
     comm_.reduce_scatter(h, h + r * c, c, CommType::BF16, CommOp::Sum, stream_);
     ::mft::cast_bf16_f32(h + r * c, g + r * c, c, stream_);
   } else {
@@ -161,6 +185,7 @@ void DataParallel::after_optimizer() {
   const int r = comm_.rank();
   ::mft::bf16_t* sh = (::mft::bf16_t*)flat_.shadow.data_ptr();
   for (int b = 0; b < (int)plan_.buckets.size(); ++b) {
+    if (plan_.replicated[b]) continue;  // updated in full on every rank
     const int64_t lo = plan_.buckets[b].first, c = chunk(b);
     comm_.all_gather(sh + lo + r * c, sh + lo, c, CommType::BF16, current_stream());
   }
@@ -171,6 +196,7 @@ void DataParallel::gather_master() {
   const int r = comm_.rank();
   float* m = flat_.master.data<float>();
   for (int b = 0; b < (int)plan_.buckets.size(); ++b) {
+    if (plan_.replicated[b]) continue;
     const int64_t lo = plan_.buckets[b].first, c = chunk(b);
     comm_.all_gather(m + lo + r * c, m + lo, c, CommType::F32, current_stream());
   }

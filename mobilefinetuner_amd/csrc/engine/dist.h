@@ -11,6 +11,9 @@
 // parameters of the forward are ready first) of about `bucket_bytes` of fp32 gradient each, and
 // pads every bucket to a multiple of world x 64 elements, so bucket b = [lo, hi) splits into
 // `world` equal, 256-B aligned chunks.  Rank r owns chunk r of every bucket: its ZeRO partition.
+// Parameters that compute in fp32 (norm weights: their compute tensor IS the fp32 master) form one
+// extra REPLICATED bucket, launched last: always all-reduced and updated in full on every rank, so
+// no rank computes with a stale copy of a chunk it does not own.
 //
 // Step.  The autograd tape's grad-ready hooks (engine/autograd.h) count the parameters of each
 // bucket during the LAST micro-batch's backward; when a bucket is complete, an event on the compute
@@ -72,6 +75,7 @@ struct FlatPlan {
   int64_t numel = 0;
   std::vector<std::pair<int64_t, int64_t>> buckets;  // [lo, hi) in backward (launch) order
   std::vector<int> bucket_of;                        // per parameter
+  std::vector<char> replicated;                      // per bucket: the fp32-compute parameters' bucket
 };
 
 // Bucketed, padded flat layout for `world` ranks (world 1: still bucketed, chunking trivial).

@@ -140,6 +140,7 @@ Tensor Trainer::step(const std::vector<std::pair<const int64_t*, const int64_t*>
 std::pair<double, double> Trainer::evaluate(int max_batches, int batch_size) {
   TraceRange range("mft.eval");
   if (!valid_) return {0.0, 0.0};
+  Communicator::QuietScope quiet(comm_);  // rank-local work between collectives: not a hang
   NoGradGuard ng;
   valid_->reset_cursor();
   const int S = cfg_.seq;
@@ -259,6 +260,7 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
     metrics.precision(9);
   }
   auto t_last = std::chrono::steady_clock::now();
+  pm_t0_ = t_last;
   int64_t tok_since = 0, steps_since = 0;
   for (int64_t it = global_step; it < total_steps_; ++it) {  // global_step > 0 after load_state
     if (cfg_.fault_step > 0 && it + 1 == cfg_.fault_step && (comm_ ? comm_->rank() : 0) == cfg_.fault_rank)
@@ -339,21 +341,40 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
       }
     }
     if (cfg_.save_every > 0 && global_step % cfg_.save_every == 0) {
-      if (!cfg_.state_dir.empty()) save_state(cfg_.state_dir);  // every rank (per-rank data state)
+      if (!cfg_.state_dir.empty()) save_state(cfg_.state_dir);  // every rank (per-rank data state; gathers)
+      else if (save_fn) gather_for_export();                    // collective: whole masters on every rank
       if (save_fn && lead()) save_fn(global_step);
+      if (comm_) comm_->heartbeat();
     }
     if (pm_) {
+      // the energy scheduler sleeps between whole steps: drain the GPU queue first (an async host
+      // would otherwise sleep while the GPU keeps running), so the busy time it sees is the step's
+      synchronize();
+      const auto t_busy = std::chrono::steady_clock::now();
+      pm_->note_step_ms((float)std::chrono::duration<double, std::milli>(t_busy - pm_t0_).count());
       const int ms = pm_->suggest_sleep_ms(global_step);
       if (ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+      pm_t0_ = std::chrono::steady_clock::now();
     }
   }
   synchronize();
+  // the final exports (LoRA / HF writers read the fp32 masters) need every rank's ZeRO-1/2 chunks
   if (!cfg_.state_dir.empty()) save_state(cfg_.state_dir);
+  else gather_for_export();
+}
+
+void Trainer::gather_for_export() {
+  if (!dp_) return;
+  synchronize();
+  dp_->gather_master();  // ZeRO-1/2: all-gather the master chunks (a no-op otherwise); collective
+  synchronize();
+  if (comm_) comm_->heartbeat();
 }
 
 // ------------------------------------------------------------------ full-state checkpoint
 void Trainer::save_state(const std::string& dir) {
   TraceRange range("mft.save_state");
+  Communicator::QuietScope quiet(comm_);
   // Written into <dir>.tmp, then swapped in by rank 0 (<dir> -> <dir>.old, <dir>.tmp -> <dir>), so a
   // crash mid-save never leaves a torn checkpoint: load_state falls back to <dir>.old.
   namespace fs = std::filesystem;
@@ -407,6 +428,7 @@ void Trainer::save_state(const std::string& dir) {
 }
 
 bool Trainer::load_state(const std::string& dir0) {
+  Communicator::QuietScope quiet(comm_);
   const int r = comm_ ? comm_->rank() : 0;
   // a crash between save_state's two renames leaves only <dir>.old
   const std::string dir = std::filesystem::exists(dir0) || !std::filesystem::exists(dir0 + ".old") ? dir0 : dir0 + ".old";

@@ -15,6 +15,7 @@
 // after each replay instead).  Logged losses and eval sums are reduced over the ranks and only
 // rank 0 prints and saves.
 #pragma once
+#include <chrono>
 #include <functional>
 #include <memory>
 #include <string>
@@ -64,6 +65,9 @@ class Trainer {
   // one optimizer step on `accum` micro-batches (host int64 [B, S] ids / targets); returns the
   // device loss (mean over micro-batches)
   Tensor step(const std::vector<std::pair<const int64_t*, const int64_t*>>& micro);
+  // ZeRO-1/2: the full fp32 masters on every rank before a checkpoint writer reads them
+  // (collective; train() calls it before periodic save_fn exports and once at the end)
+  void gather_for_export();
   void train(const std::function<void(int64_t)>& save_fn);
   // Benchmark (bench.py's native engine): `warmup` untimed optimizer steps (the first two eager,
   // then the hipGraph capture), then `steps` timed steps bracketed on both sides by a device
@@ -99,6 +103,7 @@ class Trainer {
   TokenDataset& train_;
   TokenDataset* valid_;
   TrainConfig cfg_;
+  std::chrono::steady_clock::time_point pm_t0_;  // end of the last energy-scheduler sleep
   PowerMonitor* pm_;
   Communicator* comm_;
   GradReducer* dp_;

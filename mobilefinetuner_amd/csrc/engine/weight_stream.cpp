@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <filesystem>
 
 #include "engine/autograd.h"
@@ -58,8 +59,16 @@ WeightStreamer::WeightStreamer(const std::vector<std::vector<Param*>>& groups, s
     if (on_disk) {
       Tensor out = hostv;
       if (disk_.fp16) {
-        out = empty({gr.elems}, DType::F16, Device::cpu());
-        out.copy_(hostv);  // host bf16 -> fp16 (exact for weights within fp16's range)
+        // bf16 -> fp16 is exact only inside fp16's NORMAL range (|x| in [6.1e-5, 65504] or 0):
+        // a block stays fp16 on disk only if every value survives the round trip, else bf16 (the
+        // same 2 bytes per value, lossless)
+        Tensor h = empty({gr.elems}, DType::F16, Device::cpu());
+        h.copy_(hostv);
+        Tensor back = empty({gr.elems}, DType::BF16, Device::cpu());
+        back.copy_(h);
+        gr.fp16 = std::memcmp(back.data_ptr(), hostv.data_ptr(), hostv.nbytes()) == 0;
+        if (gr.fp16) out = h;
+        else ++bf16_fallbacks;
       }
       gr.path = disk_.dir + "/block_" + std::to_string(g) + ".bin";
       std::FILE* f = std::fopen(gr.path.c_str(), "wb");
@@ -115,7 +124,7 @@ void WeightStreamer::issue(int g) {
     // disk -> pinned staging (host node, ordered after the staging buffer's previous H2D on this
     // stream) -> HBM (+ fp16 -> bf16 on the device)
     HIP_OK(hipLaunchHostFunc(copy_, &WeightStreamer::read_group, &gr));
-    if (!disk_.fp16) {
+    if (!gr.fp16) {
       HIP_OK(hipMemcpyAsync(slot_[s].data_ptr(), gr.stage, gr.bytes, hipMemcpyHostToDevice, copy_));
     } else {
       HIP_OK(hipMemcpyAsync(stage_dev_.data_ptr(), gr.stage, gr.bytes, hipMemcpyHostToDevice, copy_));

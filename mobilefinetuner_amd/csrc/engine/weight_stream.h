@@ -16,7 +16,8 @@
 //
 // Disk tier (--shard_dir D [--shard_fp16_disk 0|1]; the reference's offload files,
 // parameter_sharder.cpp:21-76,205-276): every block's bytes go to D/block_<i>.bin -- as fp16 when
-// asked (half the bytes of fp32, lossless for bf16 weights in fp16's range) -- and no host copy
+// asked AND every value of the block survives bf16 -> fp16 -> bf16 exactly (fp16's normal range);
+// otherwise that block is written as bf16 (the same 2 bytes, lossless) -- and no host copy
 // stays resident.  A load is then a HOST NODE on the copy stream (pread of the file into one of two
 // pinned staging buffers) followed by the H2D copy (+ an fp16 -> bf16 cast kernel on the device),
 // so the disk -> DRAM -> HBM pipeline is still one static schedule that a hipGraph records.
@@ -67,6 +68,7 @@ class WeightStreamer : public BlockProvider {
   size_t disk_bytes() const { return disk_bytes_; }
   bool on_disk() const { return !disk_.dir.empty(); }
   int64_t copies = 0;  // H2D group copies issued (a graph replay repeats its recorded ones)
+  int64_t bf16_fallbacks = 0;  // --shard_fp16_disk blocks kept bf16 (values outside fp16's exact range)
 
  private:
   void issue(int g);
@@ -80,6 +82,7 @@ class WeightStreamer : public BlockProvider {
     void* stage = nullptr;
     size_t bytes = 0;
     std::string path;
+    bool fp16 = false;  // this block's file holds fp16 (exact round trip), else bf16
   };
   static void read_group(void* group);  // host node: pread the block's file into its staging buffer
   std::vector<Group> groups_;

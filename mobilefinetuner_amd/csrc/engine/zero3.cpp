@@ -18,6 +18,37 @@ int64_t round_up(int64_t n, int64_t a) { return (n + a - 1) / a * a; }
 Tensor value_of(Param& p) { return p.trainable() ? p.leaf.detach() : p.c; }
 }  // namespace
 
+Zero3Layout plan_zero3(const std::vector<NamedParams>& units, const NamedParams& rep, int world) {
+  MFT_CHECK(world >= 1, "plan_zero3: world ", world);
+  Zero3Layout L;
+  int64_t local = 0;
+  for (size_t u = 0; u < units.size(); ++u) {
+    Zero3Layout::UnitLayout un;
+    int64_t off = 0;
+    for (auto& kv : units[u]) {
+      MFT_CHECK(kv.second->c.dtype() == DType::BF16, "Zero3: unit parameter ", kv.first, " must compute in bf16");
+      un.off.push_back(off);
+      off += round_up(kv.second->c.numel(), kAlign);
+    }
+    un.n = round_up(std::max<int64_t>(off, kAlign), kAlign * world);
+    un.s = un.n / world;
+    un.local = local;
+    local += un.s;
+    un.slot = u == 0 ? 0 : 1 + (int)((u - 1) % 2);
+    if (u > 0) L.max_block = std::max(L.max_block, un.n);
+    L.units.push_back(std::move(un));
+  }
+  L.rep_off = local;
+  for (auto& kv : rep) {
+    MFT_CHECK(kv.second->c.dtype() == DType::F32, "Zero3: replicated parameter ", kv.first, " must compute in fp32");
+    L.rep_at.push_back(local);
+    local += round_up(kv.second->c.numel(), kAlign);
+  }
+  L.rep_n = local - L.rep_off;
+  L.numel = local;
+  return L;
+}
+
 Zero3::Zero3(const std::vector<NamedParams>& units, const NamedParams& rep, Communicator& comm)
     : comm_(comm), rep_(rep), flat_(FlatParams::buffers(kAlign)) {
   NoGradGuard ng;
@@ -25,33 +56,22 @@ Zero3::Zero3(const std::vector<NamedParams>& units, const NamedParams& rep, Comm
   const int W = comm_.world(), r = comm_.rank();
   hipStream_t cs = current_stream();
   // layout: each unit's partition, then the replicated parameters
-  int64_t local = 0, max_block = 0;
+  const Zero3Layout lay = plan_zero3(units, rep_, W);
   for (size_t u = 0; u < units.size(); ++u) {
     Unit un;
     un.params = units[u];
-    int64_t off = 0;
-    for (auto& kv : un.params) {
-      MFT_CHECK(kv.second->c.dtype() == DType::BF16, "Zero3: unit parameter ", kv.first, " must compute in bf16");
-      un.off.push_back(off);
-      off += round_up(kv.second->c.numel(), kAlign);
-    }
-    un.n = round_up(std::max<int64_t>(off, kAlign), kAlign * W);
-    un.s = un.n / W;
-    un.local = local;
-    local += un.s;
-    un.slot = u == 0 ? 0 : 1 + (int)((u - 1) % 2);
+    un.off = lay.units[u].off;
+    un.n = lay.units[u].n;
+    un.s = lay.units[u].s;
+    un.local = lay.units[u].local;
+    un.slot = lay.units[u].slot;
     un.total = (int)un.params.size();
-    if (u > 0) max_block = std::max(max_block, un.n);
     units_.push_back(std::move(un));
   }
-  rep_off_ = local;
-  std::vector<int64_t> rep_at;
-  for (auto& kv : rep_) {
-    MFT_CHECK(kv.second->c.dtype() == DType::F32, "Zero3: replicated parameter ", kv.first, " must compute in fp32");
-    rep_at.push_back(local);
-    local += round_up(kv.second->c.numel(), kAlign);
-  }
-  rep_n_ = local - rep_off_;
+  const int64_t local = lay.numel, max_block = lay.max_block;
+  const std::vector<int64_t>& rep_at = lay.rep_at;
+  rep_off_ = lay.rep_off;
+  rep_n_ = lay.rep_n;
   flat_ = FlatParams::buffers(std::max<int64_t>(local, kAlign));
   slot_ = {zeros({units_[0].n}, DType::BF16), zeros({max_block}, DType::BF16), zeros({max_block}, DType::BF16)};
   gwork_ = {zeros({units_[0].n}, DType::F32), zeros({max_block}, DType::F32), zeros({max_block}, DType::F32)};

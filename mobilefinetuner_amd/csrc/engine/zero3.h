@@ -42,6 +42,22 @@ namespace eng {
 
 using NamedParams = std::vector<std::pair<std::string, Param*>>;
 
+// The local flat layout of a rank (pure function of the parameter sizes and the world size; the
+// host self-test checks it without a GPU): unit u is padded to n = world x s elements (s a
+// multiple of 64), each parameter at off[j] inside it; this rank's partition of unit u sits at
+// `local` in the flat, then the replicated parameters at rep_at[j] in [rep_off, rep_off + rep_n).
+struct Zero3Layout {
+  struct UnitLayout {
+    std::vector<int64_t> off;
+    int64_t n = 0, s = 0, local = 0;
+    int slot = 0;  // 0: the outer unit's slot; blocks alternate 1, 2
+  };
+  std::vector<UnitLayout> units;
+  std::vector<int64_t> rep_at;
+  int64_t rep_off = 0, rep_n = 0, numel = 0, max_block = 0;
+};
+Zero3Layout plan_zero3(const std::vector<NamedParams>& units, const NamedParams& rep, int world);
+
 class Zero3 : public GradReducer, public BlockProvider {
  public:
   // units[0]: the outer unit; units[1 + i]: block i; rep: replicated fp32-compute parameters.

@@ -775,6 +775,155 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   G8_STAMP(3);
 }
 
+// ------------------------------------------------------------------ 4-phase form (32-MFMA segments)
+// The same tile, waves, LDS image and epilogues as gemm8_kernel, with HALF the barriers: a K-tile is
+// TWO compute segments of 32 MFMAs -- quadrants (A0,B0)+(A0,B1) sharing the A0 fragments, then
+// (A1,B1)+(A1,B0) reusing both B halves' fragments -- so an iteration (2 K-tiles) is 4 phases and 8
+// barriers instead of 8 phases and 16.  Each barrier interval costs ~100 cycles beyond its MFMAs
+// (profiles/r4_*): fewer, longer intervals.  Per phase 2 half-tiles are restaged, one phase after
+// their last read (reads retire with lgkmcnt(0) BEFORE the phase's first barrier, so the 1-phase WAR
+// distance is strict):
+//   P1 (E, kt):   read E.B0 E.B1 E.A0   stage O.B1 O.A1 (kt+1)
+//   P2 (E, kt):   read E.A1             stage E.A0 E.B0 (kt+2)   vmcnt(4): O (kt+1) retired
+//   P3 (O, kt+1): read O.B0 O.B1 O.A0   stage E.B1 E.A1 (kt+2)
+//   P4 (O, kt+1): read O.A1             stage O.A0 O.B0 (kt+3)   vmcnt(4): E (kt+2) retired
+// A half-tile is read >= 1 phase after the (per-wave) wait + barrier that retires it, for both
+// ping-pong groups (group 1 one barrier behind).
+template <int EPI, bool AT, bool BT>
+__global__ __launch_bounds__(512, 1) void gemm8p2_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int tiles_n = (g.N + 255) / 256;
+  const int ntiles = ((g.M + 255) / 256) * tiles_n;
+  const int ksplit = g.ksplit > 1 ? g.ksplit : 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int m0 = (tile / tiles_n) * 256, n0 = (tile % tiles_n) * 256;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int nk_all = g.K / 64;
+  const int kps = (nk_all + ksplit - 1) / ksplit;
+  const int kbase = split * kps;
+  const int nk = max(0, min(nk_all - kbase, kps));
+  const int last = max(nk - 1, 0);
+
+  auto half_ptr = [&](int buf, int h) { return smem + (buf * 4 + h) * kHalf; };
+  auto stage = [&](int buf, int h, int kt) {
+    const int k0 = min(kbase + min(kt, last), nk_all - 1) * 64;
+    if (h < 2) {
+      if constexpr (AT) stage_half_t(half_ptr(buf, h), g.A, g.lda, m0 + h * 128, g.M, k0);
+      else stage_half(half_ptr(buf, h), g.A, g.lda, m0 + h * 128, g.M, k0);
+    } else {
+      if constexpr (BT) stage_half_t(half_ptr(buf, h), g.B, g.ldb, n0 + (h - 2) * 128, g.N, k0);
+      else stage_half(half_ptr(buf, h), g.B, g.ldb, n0 + (h - 2) * 128, g.N, k0);
+    }
+  };
+
+  f32x4_t acc[4][4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[q][i][j] = zero4();
+
+  bf16x8_t af[4][2], bfr[2][2][2];  // A fragments of one A half; B fragments of both B halves
+  auto read_a = [&](int buf, int ah) {
+    const bf16_t* t = half_ptr(buf, ah);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (AT) af[i][ks] = frag8_t(t, wm * 64 + i * 16, ks * 4);
+        else af[i][ks] = frag8(t, wm * 64 + i * 16, ks * 4);
+      }
+  };
+  auto read_b = [&](int buf, int bh) {
+    const bf16_t* t = half_ptr(buf, 2 + bh);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (BT) bfr[bh][j][ks] = frag8_t(t, wn * 32 + j * 16, ks * 4);
+        else bfr[bh][j][ks] = frag8(t, wn * 32 + j * 16, ks * 4);
+      }
+  };
+  // two quadrants sharing the A fragments: qa (with B half ba) and qb (with B half bb)
+  auto mma2 = [&](int qa, int ba, int qb, int bb, bool do_b) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[qa][i][j] = mfma16(bfr[ba][j][ks], af[i][ks], acc[qa][i][j]);
+          if (do_b) acc[qb][i][j] = mfma16(bfr[bb][j][ks], af[i][ks], acc[qb][i][j]);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_reads = [&]() {
+    lgkm_wait0();
+    if constexpr (AT || BT) __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: E <- K-tile 0 (all halves), O.A0 O.B0 <- K-tile 1; retire E
+  stage(0, 0, 0);
+  stage(0, 2, 0);
+  stage(0, 3, 0);
+  stage(0, 1, 0);
+  stage(1, 0, 1);
+  stage(1, 2, 1);
+  vm_wait<4>();
+  raw_barrier();
+  if (wm == 1) raw_barrier();  // ping-pong: group 1 one barrier behind
+  const bool b1_ok = g.ntail_full || n0 + 128 < g.N;
+
+  for (int kt = 0; kt < nk; kt += 2) {
+    const bool odd_ok = kt + 1 < nk;
+    // P1: (A0,B0) + (A0,B1) of K-tile kt
+    read_b(0, 0);
+    if (b1_ok) read_b(0, 1);
+    read_a(0, 0);
+    stage(1, 3, kt + 1);
+    stage(1, 1, kt + 1);
+    sync_reads();
+    raw_barrier();
+    mma2(0, 0, 1, 1, b1_ok);
+    raw_barrier();
+    // P2: (A1,B1) + (A1,B0)
+    read_a(0, 1);
+    stage(0, 0, kt + 2);
+    stage(0, 2, kt + 2);
+    sync_reads();
+    vm_wait<4>();
+    raw_barrier();
+    mma2(3, 0, 2, 1, b1_ok);
+    raw_barrier();
+    // P3: odd buffer, K-tile kt+1 (MFMAs skipped past the end; loads / waits stay uniform)
+    read_b(1, 0);
+    if (b1_ok) read_b(1, 1);
+    read_a(1, 0);
+    stage(0, 3, kt + 2);
+    stage(0, 1, kt + 2);
+    sync_reads();
+    raw_barrier();
+    if (odd_ok) mma2(0, 0, 1, 1, b1_ok);
+    raw_barrier();
+    // P4
+    read_a(1, 1);
+    stage(1, 0, kt + 3);
+    stage(1, 2, kt + 3);
+    sync_reads();
+    vm_wait<4>();
+    raw_barrier();
+    if (odd_ok) mma2(3, 0, 2, 1, b1_ok);
+    raw_barrier();
+  }
+  if (wm == 0) raw_barrier();
+  vm_wait<0>();
+  epilogue8<EPI>(g, acc, m0, n0, wm, wn, lane, split);
+}
+
 // ------------------------------------------------------------------ persistent streaming form
 // One quadrant of the deferred epilogue (NONE / BIAS / BIAS_GELU_D): acc[q] of the finished tile
 // (rows m0 + qa*128 + wm*64 + 16 i, columns n0 + qb*128 + wn*32 ..) -> 4 (GELU_D: 8) 16-B stores per
@@ -1066,7 +1215,7 @@ static int g_stream = -1;
 static bool gemm8_stream() {
   if (g_stream < 0) {
     const char* e = getenv("MFT_GEMM8_STREAM");
-    g_stream = (e && e[0] >= '1' && e[0] <= '3') ? e[0] - '0' : 0;
+    g_stream = (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 0;
   }
   return g_stream == 1;
 }
@@ -1079,6 +1228,13 @@ static bool gemm8_early() {
 static bool gemm8_nokeepb() {
   gemm8_stream();
   return g_stream == 3;
+}
+static bool gemm8_p2() {  // 4 (MFT_GEMM8_STREAM=4): the 4-phase form (32-MFMA segments)
+  if (g_stream < 0) {
+    const char* e = getenv("MFT_GEMM8_STREAM");
+    g_stream = (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 0;
+  }
+  return g_stream == 4;
 }
 
 template <int EPI, bool AT, bool BT>
@@ -1103,6 +1259,18 @@ static void launch8(const GemmArgs& g, hipStream_t st) {
         attr_s = true;
       }
       gemm8s_kernel<EPI, AT, BT><<<num_cus(), 512, shm, st>>>(g);
+      return;
+    }
+  }
+  if constexpr (EPI != GEMM_EPI_CE_FWD && EPI != GEMM_EPI_CE_DGRAD) {
+    if (gemm8_p2()) {
+      static bool attr_p = false;
+      if (!attr_p) {
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8p2_kernel<EPI, AT, BT>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        attr_p = true;
+      }
+      gemm8p2_kernel<EPI, AT, BT><<<tiles * ks, 512, shm, st>>>(g);
       return;
     }
   }

@@ -22,7 +22,9 @@ struct PowerConfig {
   float freq_t_high = 2.0f, freq_t_low = 0.5f;
   bool enable_temp = true;
   bool use_gpu_telemetry = false;
-  int gpu_index = 0;
+  int gpu_index = 0;       // n-th amdgpu card in DRM minor order (when pci_bus is empty)
+  std::string pci_bus;     // this rank's GPU ("0000:05:00.0", hipDeviceGetPCIBusId): its own sensors
+  float power_cap_w = 0.f;  // > 0: software power cap -- sleep so the average socket power stays <= cap
 };
 
 struct StepSleep {
@@ -38,6 +40,14 @@ struct GpuTelemetry {
 };
 
 GpuTelemetry read_gpu_telemetry(int gpu_index);
+// the amdgpu card whose PCI device is `pci_bus` (case-insensitive, e.g. "0000:05:00.0")
+GpuTelemetry read_gpu_telemetry_bus(const std::string& pci_bus);
+
+// Software power cap (no root needed, the board cap is untouched): with the step's busy time t and
+// the measured average power P, a sleep s per step keeps P * t / (t + s) <= cap, i.e.
+// s >= t (P / cap - 1).  P is a running average (hwmon power1_average), so the sleep is adjusted
+// multiplicatively toward that target each check instead of jumping to it.
+int power_cap_sleep_ms(float power_w, float cap_w, float step_ms, int prev_sleep_ms);
 
 class PowerMonitor {
  public:
@@ -49,12 +59,18 @@ class PowerMonitor {
   void set_step_schedule(const std::vector<StepSleep>& s) { schedule_ = s; }
   static std::vector<StepSleep> parse_schedule(const std::string& spec);
   int suggest_sleep_ms(int64_t global_step);
+  // the last step's busy time (the trainer's host-side step period minus the previous sleep); the
+  // power-cap mode sizes its sleep from it
+  void note_step_ms(float ms) { step_ms_ = ms; }
   std::string debug_state() const;
   float battery() const { return battery_; }
   float temperature() const { return temp_; }
 
  private:
   int recompute();
+  float step_ms_ = 0.f, power_w_ = 0.f;
+  bool have_power_ = false;
+  int cap_sleep_ = 0;
   void refresh_telemetry();
   static int freq_to_sleep_ms(float f);
   PowerConfig cfg_;

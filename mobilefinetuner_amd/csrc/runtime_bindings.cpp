@@ -322,7 +322,9 @@ void register_runtime(py::module_& m) {
       .def_readwrite("freq_t_low", &mft::PowerConfig::freq_t_low)
       .def_readwrite("enable_temp", &mft::PowerConfig::enable_temp)
       .def_readwrite("use_gpu_telemetry", &mft::PowerConfig::use_gpu_telemetry)
-      .def_readwrite("gpu_index", &mft::PowerConfig::gpu_index);
+      .def_readwrite("gpu_index", &mft::PowerConfig::gpu_index)
+      .def_readwrite("pci_bus", &mft::PowerConfig::pci_bus)
+      .def_readwrite("power_cap_w", &mft::PowerConfig::power_cap_w);
   py::class_<mft::PowerMonitor>(rt, "PowerMonitor")
       .def(py::init<const mft::PowerConfig&>())
       .def("set_manual_readings", &mft::PowerMonitor::set_manual_readings)
@@ -335,9 +337,20 @@ void register_runtime(py::module_& m) {
                     return out;
                   })
       .def("suggest_sleep_ms", &mft::PowerMonitor::suggest_sleep_ms)
+      .def("note_step_ms", &mft::PowerMonitor::note_step_ms)
       .def("debug_state", &mft::PowerMonitor::debug_state)
       .def_property_readonly("battery", &mft::PowerMonitor::battery)
       .def_property_readonly("temperature", &mft::PowerMonitor::temperature);
+  rt.def("power_cap_sleep_ms", &mft::power_cap_sleep_ms);
+  rt.def("read_gpu_telemetry_bus", [](const std::string& bus) {
+    auto t = mft::read_gpu_telemetry_bus(bus);
+    py::dict d;
+    d["ok"] = t.ok;
+    d["temp_c"] = t.temp_c;
+    d["power_w"] = t.power_w;
+    d["power_cap_w"] = t.power_cap_w;
+    return d;
+  });
   rt.def("read_gpu_telemetry", [](int i) {
     auto t = mft::read_gpu_telemetry(i);
     py::dict d;

@@ -324,6 +324,21 @@ static void test_power() {
   CHECK(p2.suggest_sleep_ms(1) == 500);
   p2.set_manual_readings(10.f, 30.f);   // low battery: 0.5 Hz -> 2000 ms
   CHECK(p2.suggest_sleep_ms(2) == 2000);
+  // software power cap: above the cap the sleep grows toward t (P_busy / cap - 1); below it decays
+  {
+    int sl = 0;
+    for (int it = 0; it < 12; ++it) {
+      // a GPU drawing 1400 W busy, 100 ms steps: the measured average includes the previous sleep
+      const float measured = 1400.f * 100.f / (100.f + (float)sl);
+      sl = power_cap_sleep_ms(measured, 1000.f, 100.f, sl);
+    }
+    CHECK(sl >= 35 && sl <= 45);  // fixed point: 100 (1400 / 1000 - 1) = 40 ms
+    int d = 40;
+    for (int it = 0; it < 12; ++it) d = power_cap_sleep_ms(500.f, 1000.f, 100.f, d);
+    CHECK(d <= 2);
+    CHECK(power_cap_sleep_ms(0.f, 1000.f, 100.f, 7) == 7);  // no reading: unchanged
+    CHECK(read_gpu_telemetry_bus("0000:ff:1f.7").ok == false);  // no such card
+  }
 }
 
 int main() {

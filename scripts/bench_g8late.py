@@ -32,7 +32,7 @@ def main():
     a = ap.parse_args()
     C = native()
     vs = [int(v) for v in a.variants.split(",")]
-    labels = {0: "gemm8", 2: "g8-early", 3: "g8-nokeepb"}
+    labels = {0: "gemm8", 2: "g8-early", 3: "g8-nokeepb", 4: "g8-4ph"}
     shapes = [("gpt2 qkv fwd", 131072, 768, 2304), ("gpt2 proj fwd", 131072, 768, 768),
               ("gpt2 fc fwd", 131072, 768, 3072), ("gpt2 mproj fwd", 131072, 3072, 768),
               ("gpt2 lm_head", 32768, 768, 50304), ("xl qkv fwd", 8192, 1600, 4800), ("xl fc fwd", 8192, 1600, 6400),

@@ -108,6 +108,8 @@ int main() {
   run_tn(65536, 2304, 768, 9);
   run_tn(65536, 3072, 768, 8);
   run_tn(65536, 3072, 768, 7);
+  run(131072, 3072, 768, GEMM_EPI_NONE);
+  run(131072, 2304, 832, GEMM_EPI_NONE);
   run(65536, 768, 3072, GEMM_EPI_NONE);
   run(65536, 3072, 768, GEMM_EPI_NONE);
   run(65536, 3072, 768, GEMM_EPI_BIAS_GELU);

@@ -110,10 +110,20 @@ def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
     got = loss_list(out0, True)
     assert len(got) == 6 and got == pytest.approx(want, rel=tol, abs=tol), (extra, got, want)
     from mobilefinetuner_amd.io import safetensors as st
-    a, b = st.load_file(ref_out), st.load_file(dp_out)
-    wtol = 50 * tol
+    # compare the UPDATES (final - initial weights), per tensor, relative to the reference update:
+    # a chunk a rank never updated (or exported stale) moves by 0 and fails; so do LayerNorm values a
+    # non-owning rank kept stale (fp32-compute parameters under ZeRO-1/2)
+    init_out = str(tmp_path / "init.safetensors")
+    _single("gpt2_full_finetune", [x for x in FULL if x not in ("--steps", "6")] + ["--steps", "0", "--output_path",
+                                                                                       init_out], "--batch_size", 8)
+    a, b, w0 = st.load_file(ref_out), st.load_file(dp_out), st.load_file(init_out)
+    rel = 0.05 if tol <= 2e-4 else 0.3
     for k in a:
-        assert torch.allclose(a[k], b[k], atol=wtol, rtol=wtol), (extra, k, (a[k] - b[k]).abs().max())
+        da, db = (a[k] - w0[k]).float(), (b[k] - w0[k]).float()
+        scale = da.abs().max().item()
+        assert scale > 0, (extra, k, "the reference did not update this tensor")
+        err = (da - db).abs().max().item()
+        assert err <= rel * scale, (extra, k, err, scale)
 
 
 def test_native_dp_lora_and_gemma_two_ranks():
