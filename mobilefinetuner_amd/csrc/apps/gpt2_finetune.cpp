@@ -9,7 +9,7 @@
 //   --synthetic_data [--synthetic_tokens N]   counter-hash token stream (no dataset needed)
 //   --pretokenized_path F [--pretokenized_meta M]   int32 token stream + meta.json
 //   --lora_targets AttnQKV,AttnProj[,MlpFcIn,MlpFcOut] --split_qkv
-//   --no_graph --compat_l2_adam --metrics_out F --deterministic
+//   --no_graph --compat_l2_adam --amsgrad --metrics_out F --deterministic
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -51,7 +51,7 @@ static const char* kProg = "gpt2_lora_finetune";
 
 namespace {
 
-const std::set<std::string> kBool = {"split_qkv", "random_init", "synthetic_data", "no_graph", "compat_l2_adam",
+const std::set<std::string> kBool = {"split_qkv", "random_init", "synthetic_data", "no_graph", "compat_l2_adam", "amsgrad",
                                      "activation_checkpointing", "shard_enable", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
                                      "deterministic", "bf16_grads", "no_overlap", "help"};
 const std::set<std::string> kValued = {
@@ -105,7 +105,7 @@ void usage() {
       "  --pm_interval --pm_batt_thresh --pm_temp_thresh --pm_fb_high --pm_fb_low --pm_ft_high --pm_ft_low\n"
       "  --pm_manual_batt --pm_manual_temp --pm_disable_batt --pm_disable_temp --pm_schedule --pm_gpu_telemetry --pm_power_cap W\n"
       "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --pretokenized_path F\n"
-      "          --pretokenized_meta F --lora_targets T --split_qkv --no_graph --compat_l2_adam --metrics_out F\n"
+      "          --pretokenized_meta F --lora_targets T --split_qkv --no_graph --compat_l2_adam --amsgrad --metrics_out F\n"
       "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"
       "          --inject_fault STEP:RANK (failure test: that rank throws before that step)\n"
       "          --deterministic\n",
@@ -243,6 +243,7 @@ int run(int argc, char** argv) {
   oc.weight_decay = a.f("weight_decay", full ? 0.01f : 0.f);
   oc.max_grad_norm = a.f("clip_grad_norm", 1.f);
   oc.l2_coupled = a.b("compat_l2_adam");
+  oc.amsgrad = a.b("amsgrad");
   AdamW opt(flat, oc);
   ds.make_dp(comm.get(), opt, dcfg);
   TrainConfig tc;

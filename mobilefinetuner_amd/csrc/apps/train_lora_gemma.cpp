@@ -8,7 +8,7 @@
 // <output_dir>/gemma_lora.safetensors).  Flag names and defaults are the Python CLI's
 // (cli/train_lora_gemma.py, which follows the reference); extras:
 //   --model P --random_init --synthetic_data [--synthetic_tokens N] --resume_from F (initial
-//   adapter) --no_graph --compat_l2_adam --metrics_out F --deterministic --interleaved_rope
+//   adapter) --no_graph --compat_l2_adam --amsgrad --metrics_out F --deterministic --interleaved_rope
 //   --shard_enable --shard_budget_mb N: frozen layer weights streamed from pinned host memory
 // Alignment harness (--align_dump_dir D, reference train_lora_gemma.cpp:609-922): one fixed batch,
 // LoRA dropout off; dumps input_ids / labels / per-token NLL / loss_scalar, the MLP output of each
@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <limits>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -58,7 +59,7 @@ namespace {
 
 const char* kProg = "train_lora_gemma";
 
-const std::set<std::string> kBool = {"random_init", "synthetic_data", "no_graph", "compat_l2_adam", "deterministic",
+const std::set<std::string> kBool = {"random_init", "synthetic_data", "no_graph", "compat_l2_adam", "amsgrad", "deterministic",
                                      "interleaved_rope", "pm_disable_batt", "pm_disable_temp", "pm_gpu_telemetry",
                                      "activation_checkpointing", "shard_enable", "bf16_grads", "no_overlap", "help", "align_dump_grads",
                                      "align_do_step", "align_disable_debug", "align_no_retain_grad", "align_numeric_attn"};
@@ -71,7 +72,8 @@ const std::set<std::string> kValued = {
     "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "pm_power_cap", "device",
     "shard_budget_mb", "shard_dir", "shard_fp16_disk", "bench_steps", "bench_warmup", "zero_stage", "offload", "bucket_mb",
     "align_dump_dir", "align_layers", "align_pt_weights_dir", "align_numeric_eps", "align_numeric_count",
-    "align_numeric_targets", "dump_grads"};
+    "align_numeric_targets", "dump_grads", "dump_embedding", "dump_embedding_step", "dump_embedding_dir",
+    "preview_tokens"};
 
 // first present of several alias flags
 std::string pick(const Args& a, std::initializer_list<const char*> keys, const std::string& d) {
@@ -92,9 +94,10 @@ void usage() {
       "  --targets full|attn|light --lora_targets q,k,v,o,gate,up,down --epochs N --max_steps N --seq_len S\n"
       "  --batch B --grad_accum A --lr LR --rank R --alpha A --lora_dropout P --warmup_ratio R --max_grad_norm C\n"
       "  --weight_decay W --lr_schedule linear|cosine|constant --data_fraction F --log_interval N --eval_steps N\n"
-      "  --eval_batches N --save_every N --seed S --pm_* (energy)\n"
+      "  --eval_batches N --save_every N --seed S --pm_* (energy; --pm_power_cap W)\n"
+      "  --dump_embedding 1 --dump_embedding_step N --dump_embedding_dir D --preview_tokens N\n"
       "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --resume_from F --no_graph\n"
-      "          --compat_l2_adam --metrics_out F --deterministic --interleaved_rope\n"
+      "          --compat_l2_adam --amsgrad --metrics_out F --deterministic --interleaved_rope\n"
       "          --zero_stage 0|1|2 --offload host|none --bucket_mb N --bf16_grads --no_overlap\n"
       "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"
       "          --inject_fault STEP:RANK (failure test: that rank throws before that step)\n"
@@ -425,6 +428,7 @@ int run(int argc, char** argv) {
   oc.weight_decay = a.f("weight_decay", 0.f);
   oc.max_grad_norm = a.f("max_grad_norm", 1.f);
   oc.l2_coupled = a.b("compat_l2_adam");
+  oc.amsgrad = a.b("amsgrad");
   if (!a.get("dump_grads").empty()) {  // parity tests: one fwd+bwd, gradients in the adapter layout
     MFT_CHECK(!comm, "--dump_grads runs on one process");
     const float lv = mft::apps::grads_into_masters(*model, flat, train, a.i("batch", 4), dc.seq_len);
@@ -466,6 +470,57 @@ int run(int argc, char** argv) {
   const float ratio = a.f("warmup_ratio", 0.03f), base = oc.lr;
   if (sched == "constant") tc.lr_fn = [base](int64_t, int64_t) { return base; };
   else tc.lr_fn = [base, ratio, sched](int64_t it, int64_t total) { return gemma_lr(it + 1, base, ratio, total, sched == "cosine"); };
+  // --preview_tokens N: the first N training tokens (reference train_lora_gemma.cpp:924-932)
+  if (a.i("preview_tokens", 0) > 0 && lead) {
+    const auto& tk = train.tokens();
+    const size_t n = std::min(tk.size(), (size_t)a.i("preview_tokens", 0));
+    std::printf("First %zu train tokens: [", n);
+    for (size_t i = 0; i < n; ++i) std::printf("%s%d", i ? ", " : "", tk[i]);
+    std::printf("]\n");
+  }
+  // --dump_embedding 1 [--dump_embedding_step N --dump_embedding_dir D]: the scaled token embeddings
+  // of the N-th training micro-batch -- statistics, a preview of the first tokens' values and the raw
+  // fp32 tensor as D/embedding_stepN.bin (reference gemma_trainer.cpp:104-109,
+  // gemma_model.cpp:875-940).  The embedding of a frozen table is a pure function of the batch's
+  // ids, so it is recomputed eagerly for that batch (the captured training step is not touched).
+  const std::string de = a.get("dump_embedding", "0");
+  if ((de == "1" || de == "true" || de == "True") && lead) {
+    const int target = std::max(1, a.i("dump_embedding_step", 1));
+    const std::string ddir = a.get("dump_embedding_dir", "./debug");
+    Gemma3* gm = model.get();
+    tc.micro_hook = [gm, target, ddir](int64_t micro, const int64_t* ids, int B, int S) {
+      if (micro != target) return;
+      Tensor di = from_host(ids, {B, S}, DType::I64);
+      Tensor e = gm->embed_tokens(di).to(DType::F32).to(Device::cpu());
+      const float* d = e.data<float>();
+      const int H = (int)e.size(-1);
+      const int64_t n = (int64_t)B * S * H;
+      double sum = 0.0, sq = 0.0;
+      float mn = std::numeric_limits<float>::max(), mx = std::numeric_limits<float>::lowest();
+      for (int64_t i = 0; i < n; ++i) {
+        sum += d[i];
+        sq += (double)d[i] * d[i];
+        mn = std::min(mn, d[i]);
+        mx = std::max(mx, d[i]);
+      }
+      const double mean = sum / (double)std::max<int64_t>(n, 1);
+      const double sd = std::sqrt(std::max(0.0, sq / (double)std::max<int64_t>(n, 1) - mean * mean));
+      std::printf("[EmbeddingDump] step %d shape=[%d,%d,%d] mean=%.6f std=%.6f min=%.6f max=%.6f\n", target, B, S, H,
+                  mean, sd, mn, mx);
+      for (int t = 0; t < std::min(S, 4); ++t) {
+        std::printf("  hidden[0,%d,0:%d] = [", t, std::min(H, 8));
+        for (int k = 0; k < std::min(H, 8); ++k) std::printf("%s%.4g", k ? ", " : "", d[(int64_t)t * H + k]);
+        std::printf("]\n");
+      }
+      std::filesystem::create_directories(ddir);
+      const std::string fn = ddir + "/embedding_step" + std::to_string(target) + ".bin";
+      std::ofstream out(fn, std::ios::binary);
+      out.write(reinterpret_cast<const char*>(d), (std::streamsize)(n * sizeof(float)));
+      if (out) std::printf("  [EmbeddingDump] wrote raw tensor to %s\n", fn.c_str());
+      else std::fprintf(stderr, "  [EmbeddingDump] failed to write %s\n", fn.c_str());
+      std::fflush(stdout);
+    };
+  }
   std::unique_ptr<PowerMonitor> pm = mft::apps::power_monitor_from(a);
   Trainer trainer(*model, flat, opt, train, have_valid ? &valid : nullptr, tc, pm.get(), comm.get(), ds.reducer());
   if (!tc.state_dir.empty() && trainer.load_state(tc.state_dir))

@@ -323,7 +323,8 @@ void nonfinite_check(Tensor x, Tensor flag) {
 }
 void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor step, c10::optional<Tensor> sumsq_t,
                 double beta1, double beta2, double eps, double wd, double max_norm, bool l2_coupled,
-                c10::optional<Tensor> shadow, c10::optional<Tensor> nonfinite, int64_t sr_offset) {
+                c10::optional<Tensor> shadow, c10::optional<Tensor> nonfinite, int64_t sr_offset,
+                c10::optional<Tensor> vmax) {
   CHECK_F32(p); CHECK_F32(g);
   CHECK_CONTIG(p); CHECK_CONTIG(g); CHECK_CONTIG(m); CHECK_CONTIG(v);
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adamw: size mismatch");
@@ -340,6 +341,8 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor step, 
   if (a.shadow) TORCH_CHECK(shadow->numel() == p.numel() && shadow->is_contiguous(), "shadow must match params");
   a.nonfinite = optp<int>(nonfinite);
   a.sr_offset = sr_offset;
+  a.vmax = optp<float>(vmax);
+  if (a.vmax) TORCH_CHECK(vmax->numel() == p.numel() && vmax->is_contiguous() && !mb, "vmax: fp32 [n], fp32 moments");
   mft::adamw_step(a, stream());
 }
 void adamw_commit(Tensor step, c10::optional<Tensor> nonfinite, c10::optional<Tensor> sumsq_t) {
@@ -491,8 +494,9 @@ Tensor add_bf16(Tensor a, Tensor b) {
 }
 
 
-// ------------------------------------------------------------------ GEMM (gemm.hip)
-// C = epi(alpha * A op(B)); A [M,K]; B [N,K] (b_nn = false) or [K,N] (b_nn = true).
+// ------------------------------------------------------------------ GEMM (gemm8.hip)
+// C = epi(alpha * A op(B)); A [M,K]; B [N,K] (b_nn = false) or [K,N] (b_nn = true).  `bm` is kept
+// for the call signature (the round-1 tile configurations are gone): every call runs gemm8.
 // Returns {C, aux}: aux is the pre-activation written by GEMM_EPI_BIAS_GELU.
 std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::optional<Tensor> bias,
                             c10::optional<Tensor> aux, double alpha, int64_t bm, c10::optional<Tensor> out,
@@ -502,7 +506,7 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
   const int M = A.size(0), K = A.size(1);
   const int N = b_nn ? B.size(1) : B.size(0);
   TORCH_CHECK((b_nn ? B.size(0) : B.size(1)) == K, "gemm: inner dimensions differ");
-  TORCH_CHECK(mft::gemm_supported(M, N, K), "gemm: needs K % 64 == 0 and N % 8 == 0");
+  TORCH_CHECK(mft::gemm8_supported(M, N, K, false, b_nn), "gemm: needs K % 64 == 0 and N % 8 == 0");
   TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "gemm: leading dimensions must be multiples of 8");
   c10::DeviceGuard g(A.device());
   Tensor C;
@@ -533,7 +537,7 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
   a.aux = X.defined() ? bp(X) : nullptr; a.ldaux = X.defined() ? X.stride(0) : 0;
   a.M = M; a.N = N; a.K = K; a.alpha = (float)alpha;
   if (epi == mft::GEMM_EPI_LORA) {
-    TORCH_CHECK(bm == 8 && lora_u.has_value() && lora_w.has_value(), "gemm: LoRA epilogue = cfg 8, u and w");
+    TORCH_CHECK(lora_u.has_value() && lora_w.has_value(), "gemm: LoRA epilogue needs u and w");
     CHECK_BF16((*lora_u)); CHECK_BF16((*lora_w));
     TORCH_CHECK(lora_u->size(0) == M && lora_w->size(1) == N && lora_u->size(1) == lora_w->size(0) &&
                 lora_u->stride(1) == 1 && lora_w->stride(1) == 1, "gemm: LoRA u [M, r], w [r, N]");
@@ -541,8 +545,8 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
     a.lora_w = bp(*lora_w); a.ld_lw = lora_w->stride(0);
     a.lora_r = lora_u->size(1);
   }
-  if (bm == 8) mft::gemm8x(a, (int)epi, false, b_nn, stream());  // cfg 8: 8-phase pipelined 256x256 kernel
-  else mft::gemm(a, b_nn, (int)epi, (int)bm, stream());
+  (void)bm;
+  mft::gemm8x(a, (int)epi, false, b_nn, stream());
   return {C, X};
 }
 
@@ -605,15 +609,9 @@ std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, 
     a.lora_w = bp(*lora_w); a.ld_lw = lora_w->stride(0);
     a.lora_r = lora_u->size(1);
   }
-  if (impl == 1) {  // gemmw (NT only)
-    TORCH_CHECK(!a_t && !b_t && mft::gemmw_supported(M, N, K), "gemm_t impl 1 (gemmw): NT, K % 32 == 0");
-    mft::gemmw(a, (int)epi, stream());
-  } else if (impl == 2) {  // gemm4 (NT only)
-    TORCH_CHECK(!a_t && !b_t && mft::gemm4_supported(M, N, K), "gemm_t impl 2 (gemm4): NT, K % 64 == 0");
-    mft::gemm4(a, (int)epi, stream());
-  } else {
-    mft::gemm8x(a, (int)epi, a_t, b_t, stream());
-  }
+  TORCH_CHECK(impl == 0, "gemm_t: impl 0 (gemm8) only -- the round-3 gemmw / gemm4 experiments are removed "
+              "(records: profiles/r3_gemm_stream_ab.txt, profiles/r3_gemm4_experiment.txt)");
+  mft::gemm8x(a, (int)epi, a_t, b_t, stream());
   return {C, X};
 }
 
@@ -669,7 +667,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("adamw_step", &adamw_step, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr"),
         py::arg("step"), py::arg("sumsq"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("wd"),
         py::arg("max_norm"), py::arg("l2_coupled"), py::arg("shadow"), py::arg("nonfinite"),
-        py::arg("sr_offset") = 0);
+        py::arg("sr_offset") = 0, py::arg("vmax") = py::none());
   m.def("adamw_commit", &adamw_commit);
   m.def("lora_rowdot", &lora_rowdot);
   m.def("lora_update", &lora_update);
@@ -681,6 +679,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("alpha") = 1.0, py::arg("out") = py::none(),
         py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none(), py::arg("impl") = 0);
   m.def("gemm8_set_stream", [](int64_t on) { mft::gemm8_set_stream((int)on); });
+  m.def("gemm8_set_stagger", [](int64_t c) { mft::gemm8_set_stagger((int)c); });
   m.def("gemm", &gemm_op, py::arg("A"), py::arg("B"), py::arg("b_nn"), py::arg("epi"), py::arg("bias"), py::arg("aux"),
         py::arg("alpha"), py::arg("cfg"), py::arg("out"), py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none());
   m.def("zero_cols", &zero_cols);

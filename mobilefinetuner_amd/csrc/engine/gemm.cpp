@@ -229,51 +229,6 @@ void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c,
   ::mft::gemm8x(g, epi, false, b_kn, current_stream());
 }
 
-namespace {
-// Per-shape choice between the hand-written gemm8 and hipBLASLt, timed ONCE on the real operands at
-// the first call outside a graph capture (the trainer's eager warm-up steps; inside a capture the
-// library runs and the choice waits for the next eager call).  Returns true for gemm8.  `tag`
-// names the call site in the MFT_NT_VERBOSE report.
-bool timed_gemm8_choice(const char* tag, const char* key, const std::function<void()>& run_lt,
-                        const std::function<void()>& run_g8) {
-  static std::mutex mu;
-  static std::unordered_map<std::string, int> choice;
-  {
-    std::lock_guard<std::mutex> g(mu);
-    auto it = choice.find(key);
-    if (it != choice.end()) return it->second == 1;
-  }
-  hipStream_t s = current_stream();
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (s) (void)hipStreamIsCapturing(s, &cap);
-  if (cap != hipStreamCaptureStatusNone) return false;
-  run_lt();  // hipBLASLt's own candidate tuning happens on this first call
-  run_g8();
-  hipEvent_t e0, e1, e2;
-  HIP_OK(hipEventCreate(&e0));
-  HIP_OK(hipEventCreate(&e1));
-  HIP_OK(hipEventCreate(&e2));
-  HIP_OK(hipEventRecord(e0, s));
-  for (int r = 0; r < 3; ++r) run_lt();
-  HIP_OK(hipEventRecord(e1, s));
-  for (int r = 0; r < 3; ++r) run_g8();
-  HIP_OK(hipEventRecord(e2, s));
-  HIP_OK(hipEventSynchronize(e2));
-  float t_lt = 0.f, t_g8 = 0.f;
-  HIP_OK(hipEventElapsedTime(&t_lt, e0, e1));
-  HIP_OK(hipEventElapsedTime(&t_g8, e1, e2));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  (void)hipEventDestroy(e2);
-  const int c = t_g8 < t_lt ? 1 : 0;
-  if (std::getenv("MFT_NT_VERBOSE"))
-    std::fprintf(stderr, "[mft %s] %s: gemm8 %.1f us, hipBLASLt %.1f us -> %s\n", tag, key, 1e3f * t_g8 / 3,
-                 1e3f * t_lt / 3, c ? "gemm8" : "hipBLASLt");
-  std::lock_guard<std::mutex> g(mu);
-  choice[key] = c;
-  return c == 1;
-}
-}  // namespace
 
 void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y) {
   MFT_CHECK(rowmajor2(x2) && rowmajor2(w) && rowmajor2(y) && x2.dtype() == DType::BF16 && w.dtype() == DType::BF16,
@@ -305,20 +260,15 @@ void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y) {
   const bool g8_ok = K % 64 == 0 && N % 8 == 0 && x2.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 &&
                      y.stride(0) % 8 == 0 && ::mft::gemm8_supported((int)M, (int)N, (int)K, false, false);
   if (!g8_ok) return run_lt();
-  if (gemm8_all()) return run_g8();
-  // Per-shape choice between the hand-written gemm8 and hipBLASLt, timed ONCE on the real operands
-  // at the first call outside a graph capture (the trainer's eager warm-up steps): gemm8 wins some
-  // shapes (GPT-2 XL's qkv: 1033 vs 827 TF/s), hipBLASLt most of the short-K ones (GPT-2 small:
-  // 1.2-1.25 vs 1.0 PF/s; profiles/r3_g8late.txt).  MFT_NT=gemm8|lt forces one; deterministic
-  // mode keeps hipBLASLt's heuristic pick (no timing-dependent choice across processes).
+  // Static routing (no timing, identical on every rank and rerun): a PLAIN GEMM (no fused epilogue
+  // beyond the bias) is a library GEMM -> hipBLASLt; every fused-epilogue GEMM (GELU, dGELU, LoRA,
+  // LM-head cross entropy, split-K weight gradients) is the hand-written gemm8.  MFT_NT=gemm8|lt or
+  // MFT_GEMM8_ALL=1 (every GEMM of the step hand-written) override it.
   static const char* env = std::getenv("MFT_NT");
   static const int forced = !env ? -1 : std::string(env) == "gemm8" ? 1 : std::string(env) == "lt" ? 0 : -1;
   if (forced >= 0) return forced ? run_g8() : run_lt();
-  if (deterministic()) return run_lt();
-  char kb[160];
-  snprintf(kb, sizeof(kb), "dev %d M=%ld N=%ld K=%ld ld %ld/%ld/%ld%s", cur_dev(), M, N, K, (long)x2.stride(0),
-           (long)w.stride(0), (long)y.stride(0), bias.defined() ? " +bias" : "");
-  return timed_gemm8_choice("gemm_nt", kb, run_lt, run_g8) ? run_g8() : run_lt();
+  if (gemm8_all()) return run_g8();
+  return run_lt();
 }
 
 void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out) {
@@ -338,16 +288,14 @@ void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out) {
   const bool g8_ok =
       N % 64 == 0 && K % 8 == 0 && dy2.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 8 == 0;
   if (!g8_ok) return run_lt();
-  // plain data-gradient GEMMs: the same timed per-shape choice as the NT forwards (MFT_NN=gemm8|lt
-  // forces one; deterministic mode and MFT_GEMM8_ALL=1 keep gemm8)
+  // plain data-gradient GEMMs: the same static routing as the NT forwards (a library GEMM ->
+  // hipBLASLt); MFT_NN=gemm8|lt forces one; deterministic mode and MFT_GEMM8_ALL=1 keep gemm8 (its
+  // reduction order is fixed)
   static const char* env = std::getenv("MFT_NN");
   static const int forced = !env ? -1 : std::string(env) == "gemm8" ? 1 : std::string(env) == "lt" ? 0 : -1;
   if (forced >= 0) return forced ? run_g8() : run_lt();
   if (deterministic() || gemm8_all()) return run_g8();
-  char kb[160];
-  snprintf(kb, sizeof(kb), "NN dev %d M=%ld N=%ld K=%ld ld %ld/%ld/%ld", cur_dev(), M, K, N, (long)dy2.stride(0),
-           (long)w.stride(0), (long)out.stride(0));
-  return timed_gemm8_choice("gemm_nn", kb, run_lt, run_g8) ? run_g8() : run_lt();
+  return run_lt();
 }
 
 void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {

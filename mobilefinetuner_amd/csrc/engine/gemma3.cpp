@@ -497,6 +497,11 @@ std::pair<Tensor, Tensor> Gemma3::layer(int i, const Tensor& x0, const Tensor& h
   return add_norm(x, f, nw, nullptr, eps, true, 1.f, oc);
 }
 
+Tensor Gemma3::embed_tokens(const Tensor& ids) {
+  NoGradGuard ng;
+  return embed(ids, embed_, nullptr, embed_scale_);
+}
+
 Tensor Gemma3::hidden(const Tensor& ids) {
   const int64_t B = ids.size(0), S = ids.size(1);
   const int H = cfg_.hidden;

@@ -70,6 +70,9 @@ class Gemma3 : public LanguageModel {
   Tensor loss(const Tensor& ids, const Tensor& labels, float w_grad_scale = 1.f) override;
   std::pair<Tensor, Tensor> nll(const Tensor& ids, const Tensor& labels) override;
   Tensor hidden(const Tensor& ids) override;
+  // the scaled token embeddings the first layer sees ([B, S, H], bf16; no autograd) -- the
+  // reference's --dump_embedding tensor (graph/gemma_model.cpp:588-597)
+  Tensor embed_tokens(const Tensor& ids);
   Param& output_embedding() override { return embed_; }
   int vocab() const override { return cfg_.vocab_size; }
   void merge_lora(float sign);

@@ -70,6 +70,7 @@ AdamW::AdamW(FlatParams& flat, const AdamWConfig& cfg) : flat_(flat), cfg_(cfg) 
   NoGradGuard ng;
   m = zeros({flat.numel}, DType::F32);
   v = zeros({flat.numel}, DType::F32);
+  if (cfg.amsgrad) vmax = zeros({flat.numel}, DType::F32);
   lr_dev = full({1}, cfg.lr, DType::F32);
   step_dev = zeros({1}, DType::F32);
   sumsq_dev = zeros({1}, DType::F32);
@@ -90,6 +91,7 @@ void AdamW::shard(const std::vector<OptSegment>& segs, Communicator* comm, bool 
     state_numel_ = std::max(state_numel_, s.state_off + s.len);
   }
   const int64_t n = std::max<int64_t>(state_numel_, 4);
+  MFT_CHECK(!(host_moments && cfg_.amsgrad), "AdamW: AMSGrad keeps fp32 moments on the device (no --offload host)");
   if (host_moments) {  // pinned host DRAM, read / written in place by the kernel (bf16, SR-rounded)
     m = zeros({n}, DType::BF16, Device::cpu(true));
     v = zeros({n}, DType::BF16, Device::cpu(true));
@@ -97,6 +99,7 @@ void AdamW::shard(const std::vector<OptSegment>& segs, Communicator* comm, bool 
     m = zeros({n}, DType::F32);
     v = zeros({n}, DType::F32);
   }
+  if (cfg_.amsgrad) vmax = zeros({n}, DType::F32);
 }
 
 void AdamW::set_lr(float lr) {
@@ -146,6 +149,7 @@ void AdamW::step() {
     a.g = g0 + sg.off;
     a.m = reinterpret_cast<float*>(static_cast<char*>(m.data_ptr()) + sg.state_off * ms);
     a.v = reinterpret_cast<float*>(static_cast<char*>(v.data_ptr()) + sg.state_off * ms);
+    a.vmax = vmax.defined() ? vmax.data<float>() + sg.state_off : nullptr;
     a.n = sg.len;
     a.shadow = (::mft::bf16_t*)flat_.shadow.data_ptr() + sg.off;
     a.sr_offset = sg.off;
@@ -163,6 +167,11 @@ void AdamW::step() {
 float AdamW::grad_norm() const { return std::sqrt(std::max(0.f, (float)sumsq_dev.item())); }
 bool AdamW::skipped_last() const { return nonfinite_dev.to_vector_f32()[0] != 0.f; }
 int64_t AdamW::applied_steps() const { return (int64_t)step_dev.item(); }
+
+void AdamW::load_vmax(const Tensor& h) {
+  MFT_CHECK(vmax.defined() && h.numel() == vmax.numel(), "AdamW::load_vmax: AMSGrad state mismatch");
+  vmax.copy_(h.to(DType::F32));
+}
 
 void AdamW::load_state(const Tensor& m_h, const Tensor& v_h, int64_t steps) {
   MFT_CHECK(m_h.numel() == m.numel() && v_h.numel() == v.numel(), "AdamW::load_state: state has ", m_h.numel(),

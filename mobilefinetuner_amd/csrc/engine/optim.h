@@ -47,6 +47,7 @@ struct AdamWConfig {
   float max_grad_norm = 1.f;  // <= 0: no clipping
   bool l2_coupled = false;    // reference Adam (L2 added to the gradient)
   bool skip_nonfinite = true;
+  bool amsgrad = false;       // AMSGrad (reference optim/adam.cpp:52,78; torch semantics: max of raw v)
 };
 
 class AdamW {
@@ -58,7 +59,9 @@ class AdamW {
   bool skipped_last() const;
   int64_t applied_steps() const;
   Tensor m, v, lr_dev, step_dev, sumsq_dev, nonfinite_dev, skipped_dev;
+  Tensor vmax;  // AMSGrad running max of v (undefined when off)
   const AdamWConfig& config() const { return cfg_; }
+  void load_vmax(const Tensor& h);  // AMSGrad running max (checkpoint resume)
   void load_state(const Tensor& m_h, const Tensor& v_h, int64_t steps);
   // ZeRO-1/2 (engine/dist.h): update only `segs` -- this rank's partition of the flat buffers --
   // with moments of sum(len) elements; host_moments: bf16 moments in pinned host DRAM that the

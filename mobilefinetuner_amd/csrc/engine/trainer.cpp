@@ -274,6 +274,8 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
       train_.next_batch(B, true, hid[a].data(), htg[a].data(), mk.data(), nullptr);
       for (float m : mk) tokens += m > 0.f;
       micro.push_back({hid[a].data(), htg[a].data()});
+      ++micro_steps_;
+      if (cfg_.micro_hook) cfg_.micro_hook(micro_steps_, hid[a].data(), B, S);
     }
     Tensor loss = step(micro);
     ++global_step;
@@ -404,8 +406,13 @@ void Trainer::save_state(const std::string& dir) {
     m2.copy_(opt_.v.is_hip() ? opt_.v.to(Device::cpu()) : opt_.v);
     const std::string fn = opt_.sharded() ? "/optimizer.rank" + std::to_string(r) + ".safetensors" : "/optimizer.safetensors";
     const size_t sb = (size_t)m1.numel() * sizeof(float);
-    safetensors_save(tmp + fn, {{"m", "F32", {m1.numel()}, m1.data_ptr(), sb}, {"v", "F32", {m2.numel()}, m2.data_ptr(), sb}},
-                     {{"format", opt_.sharded() ? "mft-zero-partition" : "mft-flat"}}, false, true);
+    std::vector<TensorBlob> outs{{"m", "F32", {m1.numel()}, m1.data_ptr(), sb}, {"v", "F32", {m2.numel()}, m2.data_ptr(), sb}};
+    Tensor m3;
+    if (opt_.vmax.defined()) {  // AMSGrad running max
+      m3 = opt_.vmax.to(Device::cpu());
+      outs.push_back({"vmax", "F32", {m3.numel()}, m3.data_ptr(), (size_t)m3.numel() * sizeof(float)});
+    }
+    safetensors_save(tmp + fn, outs, {{"format", opt_.sharded() ? "mft-zero-partition" : "mft-flat"}}, false, true);
   }
   std::ofstream f(tmp + "/trainer_state.rank" + std::to_string(r) + ".json");
   f.precision(17);
@@ -450,6 +457,7 @@ bool Trainer::load_state(const std::string& dir0) {
   };
   flat_.master.copy_(host_view(tw, "master", flat_.numel));
   opt_.load_state(host_view(to, "m", opt_.m.numel()), host_view(to, "v", opt_.v.numel()), st["opt_step"].as_int());
+  if (opt_.vmax.defined() && to.has("vmax")) opt_.load_vmax(host_view(to, "vmax", opt_.vmax.numel()));
   synchronize();  // the mmaps go away with the files
   flat_.refresh_shadow();
   global_step = st["global_step"].as_int();

@@ -52,6 +52,9 @@ struct TrainConfig {
   int pm_interval = 0;
   // learning rate of 0-indexed update `it` of `total`; unset: the GPT-2 CLI schedule (gpt2_cli_lr)
   std::function<float(int64_t it, int64_t total)> lr_fn;
+  // called on the host before each optimizer step for every micro-batch, with the running 1-based
+  // micro-step count and the batch's token ids [B, S] (e.g. the Gemma CLI's --dump_embedding)
+  std::function<void(int64_t micro_step, const int64_t* ids, int B, int S)> micro_hook;
 };
 
 class Trainer {
@@ -103,6 +106,7 @@ class Trainer {
   TokenDataset& train_;
   TokenDataset* valid_;
   TrainConfig cfg_;
+  int64_t micro_steps_ = 0;  // micro-batches drawn by train() (TrainConfig::micro_hook)
   std::chrono::steady_clock::time_point pm_t0_;  // end of the last energy-scheduler sleep
   PowerMonitor* pm_;
   Communicator* comm_;

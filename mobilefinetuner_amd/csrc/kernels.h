@@ -56,7 +56,7 @@ bool attn_short_path(int D, int Sq, int Sk, int window);
 // dk_tmp/dv_tmp workspaces under GQA); 2: split dK/dV + dQ kernels (needs delta only)
 int attn_bwd_path(int D, int Sq, int Sk, int window);
 
-// ---------------------------------------------------------------- GEMM (gemm.hip)
+// ---------------------------------------------------------------- GEMM (gemm8.hip)
 enum GemmEpi { GEMM_EPI_NONE = 0, GEMM_EPI_BIAS = 1, GEMM_EPI_BIAS_GELU = 2, GEMM_EPI_DGELU = 3, GEMM_EPI_F32ACC = 4,
                GEMM_EPI_LORA = 5, GEMM_EPI_F32PART = 6 /* internal: split-K fp32 slab */,
                // fused LM-head cross entropy (gemm8 only, driven by lm_head_ce in xent.hip)
@@ -103,10 +103,11 @@ struct GemmArgs {
   // gemm8: 1 = compute the (A*, B1) quadrants of an N-tail tile anyway (set by gemm8x from
   // MFT_GEMM8_NTAIL=0 for A/B runs; the CE dgrad never skips them)
   int ntail_full;
+  // gemm8: > 0 delays the first-round workgroups (blockIdx < 256) by (blockIdx >> 3) x stagger
+  // cycles, spreading every XCD's CUs over a tile round so their prologue fills and epilogue
+  // stores do not all hit HBM at once (MFT_G8_STAGGER, A/B)
+  int stagger;
 };
-bool gemm_supported(int M, int N, int K);
-// cfg: tile configuration (gemm.hip launch_e): 0 = 256x256, 1 = 128x256, 2 = 128x128, 3 = 256x128
-void gemm(const GemmArgs& g, bool b_nn, int epi, int cfg, hipStream_t st);
 // 256x256 8-phase pipelined GEMM (gemm8.hip); same epilogues.  a_t: A stored [K, M]; b_t: B stored
 // [K, N] (NN data-grad); both: TN weight-grad (use GEMM_EPI_F32ACC with gemm8_pick_ksplit / ws)
 void gemm8(const GemmArgs& g, int epi, hipStream_t st);  // NT
@@ -116,13 +117,7 @@ int gemm8_pick_ksplit(int M, int N, int K);
 // NT NONE / BIAS / BIAS_GELU_D: the persistent streaming form with the deferred epilogue (opt-in,
 // MFT_GEMM8_STREAM=1); A/B switch for benchmarks
 void gemm8_set_stream(int on);
-// 256x128x32 NT GEMM with 4-wave workgroups, two per CU (gemmw.hip): the short-K training shapes
-// (epilogues as gemm8's, minus the CE / split-K ones)
-void gemmw(const GemmArgs& g, int epi, hipStream_t st);
-bool gemmw_supported(int M, int N, int K);
-// 256x256x64 NT GEMM with 4 waves (one per SIMD, 128x128 per wave, AGPR accumulators; gemmw.hip)
-void gemm4(const GemmArgs& g, int epi, hipStream_t st);
-bool gemm4_supported(int M, int N, int K);
+void gemm8_set_stagger(int cycles);  // first-round stagger (cycles per XCD slot), A/B
 void gemm_splitk_reduce(const float* ws, int ksplit, int M, int N, float* C, long ldc, float alpha, int accumulate,
                         hipStream_t st);
 
@@ -200,6 +195,7 @@ struct AdamWArgs {
   const int* nonfinite;   // optional device flag: skip the step when set
   int moments_bf16;       // m / v are bf16 (stochastically rounded; host-offloaded optimizer state)
   long sr_offset;         // global element index of p[0] (chunked / sharded launches): keys the SR hash
+  float* vmax;            // AMSGrad: running max of v (fp32 moments only; null = plain Adam(W))
 };
 void adamw_step(const AdamWArgs& a, hipStream_t st);
 // after every adamw_step launch of one update: *step += 1 unless the update was skipped

@@ -360,6 +360,56 @@ __device__ __forceinline__ void lds_barrier() {
   raw_barrier();
 }
 
+// ------------------------------------------------------------------ LDS-staged epilogue (NONE / BIAS)
+// The register epilogue stores 16 rows x 64 B per wave instruction, which the store path moves at
+// ~13 B/cycle per CU; whole-row segments (>= 128 B per row) move at ~48 B/cycle per CU when not
+// every CU stores at once (profiles/r4_store_probe.txt).  Here the finished bf16 tile goes to the
+// (now idle) LDS operand buffers -- 16-B chunks XOR-swizzled by (row & 31): conflict-free writes and
+// reads -- and leaves as 2 full 512-B tile rows per wave instruction.
+template <int EPI>
+__device__ __forceinline__ void epilogue_lds(const GemmArgs& g, f32x4_t (&acc)[4][4][2], int m0, int n0, int wm, int wn,
+                                             int lane, bf16_t* lds) {
+  const int g4 = lane >> 4;
+  const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int qa = (q == 2 || q == 3) ? 1 : 0, qb = (q == 1 || q == 2) ? 1 : 0;
+    const int colt = qb * 128 + wn * 32 + cofs;
+    float bias_v[8];
+    if constexpr (EPI == GEMM_EPI_BIAS) load8(g.bias + min(n0 + colt, g.N - 8), bias_v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[q][i][0][r]),
+                                                         __float_as_uint(acc[q][i][1][r]), false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[4 + r] = __uint_as_float(sw[1]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] *= g.alpha;
+        if constexpr (EPI == GEMM_EPI_BIAS) v[e] += bias_v[e];
+      }
+      const int rowt = qa * 128 + wm * 64 + i * 16 + (lane & 15);
+      const int ch = (colt >> 3) ^ (rowt & 31);
+      uint4 pk = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+      *reinterpret_cast<uint4*>(lds + rowt * 256 + (ch << 3)) = pk;
+    }
+  }
+  lds_barrier();
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = k * 512 + tid;
+    const int rowt = c >> 5, chunk = c & 31;
+    const uint4 pk = *reinterpret_cast<const uint4*>(lds + rowt * 256 + ((chunk ^ (rowt & 31)) << 3));
+    const int row = m0 + rowt, col = n0 + chunk * 8;
+    if (row < g.M && col < g.N) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col) = pk;
+  }
+}
+
 // ------------------------------------------------------------------ LM-head CE forward epilogue
 // Logits tile (fp32 accumulators) -> per-row tile max and sum-exp, label logit, and (optionally)
 // E = exp(logit - tile max) in bf16.  A row's 256 tile columns are spread over the lane's 2 x 8
@@ -508,9 +558,12 @@ __device__ unsigned long long* g8_stamps;
 // KEEPB defaults on where the 16 extra VGPRs fit without spilling (not the TT wgrad form, the LoRA
 // epilogue or the CE dgrad, which spill 2-7 VGPRs with it)
 template <int EPI, bool AT, bool BT, bool LATE = true,
-          bool KEEPB = !(AT && BT) && EPI != GEMM_EPI_LORA && EPI != GEMM_EPI_CE_DGRAD>
+          bool KEEPB = !(AT && BT) && EPI != GEMM_EPI_LORA && EPI != GEMM_EPI_CE_DGRAD, bool LDSEPI = false>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  if (g.stagger > 0 && blockIdx.x < 256) {  // first round: spread each XCD's CUs over a tile round
+    for (int c = (int)(blockIdx.x >> 3) * g.stagger; c > 0; c -= 8000) __builtin_amdgcn_s_sleep(125);
+  }
   G8_STAMP(0);
   // buffer b (0 = even, 1 = odd): half-tiles A0, A1, B0, B1 at smem + (b * 4 + h) * kHalf
   const int tiles_n = (g.N + 255) / 256;
@@ -771,7 +824,10 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 
   if constexpr (EPI == GEMM_EPI_CE_FWD) epilogue_ce_fwd(g, acc, m0, n0, wm, wn, lane, reinterpret_cast<float*>(smem));
   else if constexpr (EPI == GEMM_EPI_CE_DGRAD) epilogue_ce_dgrad(g, acc, m0, n0, wm, wn, lane);
-  else epilogue8<EPI>(g, acc, m0, n0, wm, wn, lane, split);
+  else if constexpr (LDSEPI && (EPI == GEMM_EPI_NONE || EPI == GEMM_EPI_BIAS)) {
+    raw_barrier();  // every wave's tail LDS-DMA retired (vm_wait<0> above) before the tile overwrites LDS
+    epilogue_lds<EPI>(g, acc, m0, n0, wm, wn, lane, smem);
+  } else epilogue8<EPI>(g, acc, m0, n0, wm, wn, lane, split);
   G8_STAMP(3);
 }
 
@@ -1215,7 +1271,7 @@ static int g_stream = -1;
 static bool gemm8_stream() {
   if (g_stream < 0) {
     const char* e = getenv("MFT_GEMM8_STREAM");
-    g_stream = (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 0;
+    g_stream = (e && e[0] >= '1' && e[0] <= '5') ? e[0] - '0' : 0;
   }
   return g_stream == 1;
 }
@@ -1230,11 +1286,21 @@ static bool gemm8_nokeepb() {
   return g_stream == 3;
 }
 static bool gemm8_p2() {  // 4 (MFT_GEMM8_STREAM=4): the 4-phase form (32-MFMA segments)
-  if (g_stream < 0) {
-    const char* e = getenv("MFT_GEMM8_STREAM");
-    g_stream = (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 0;
-  }
+  gemm8_stream();
   return g_stream == 4;
+}
+static bool gemm8_ldsepi() {  // 5: LDS-staged whole-row epilogue stores (NONE / BIAS)
+  gemm8_stream();
+  return g_stream == 5;
+}
+static int g_stagger = -1;
+void gemm8_set_stagger(int cycles) { g_stagger = cycles; }
+static int gemm8_stagger() {
+  if (g_stagger < 0) {
+    const char* e = getenv("MFT_G8_STAGGER");
+    g_stagger = e ? atoi(e) : 0;
+  }
+  return g_stagger;
 }
 
 template <int EPI, bool AT, bool BT>
@@ -1271,6 +1337,18 @@ static void launch8(const GemmArgs& g, hipStream_t st) {
         attr_p = true;
       }
       gemm8p2_kernel<EPI, AT, BT><<<tiles * ks, 512, shm, st>>>(g);
+      return;
+    }
+  }
+  if constexpr (!AT && (EPI == GEMM_EPI_NONE || EPI == GEMM_EPI_BIAS)) {
+    if (gemm8_ldsepi()) {
+      static bool attr_e = false;
+      if (!attr_e) {
+        MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI, AT, BT, true, true, true>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        attr_e = true;
+      }
+      gemm8_kernel<EPI, AT, BT, true, true, true><<<tiles * ks, 512, shm, st>>>(g);
       return;
     }
   }
@@ -1369,6 +1447,7 @@ static int gemm8_ntail_full() {
 void gemm8x(const GemmArgs& g0, int epi, bool a_t, bool b_t, hipStream_t st) {
   GemmArgs g = g0;
   g.ntail_full = gemm8_ntail_full();
+  g.stagger = gemm8_stagger();
   // per-lane staging offsets are 32-bit byte offsets from a uniform base (128 rows x ld x 2 B)
   if (!gemm8_supported(g.M, g.N, g.K, a_t, b_t) || g.lda > (1L << 23) || g.ldb > (1L << 23)) {
     fprintf(stderr, "mft::gemm8: unsupported shape M=%d N=%d K=%d (a_t=%d b_t=%d)\n", g.M, g.N, g.K, a_t, b_t);

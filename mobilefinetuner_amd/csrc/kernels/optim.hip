@@ -5,6 +5,9 @@
 // optim/gemma_trainer.cpp:84-102, optim/trainer.cpp:66-92).
 // Everything that depends on step-time values (lr, step count, grad-norm, skip flag) is read from
 // device memory, so a captured hipGraph of the whole train step replays without host sync.
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -130,7 +133,12 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
       if (a.l2_coupled) gj += a.weight_decay * pp[j];
       mm[j] = a.beta1 * mm[j] + (1.f - a.beta1) * gj;
       vv[j] = a.beta2 * vv[j] + (1.f - a.beta2) * gj * gj;
-      const float denom = sqrtf(vv[j]) * rbc2 + a.eps;
+      float vd = vv[j];
+      if (!MB && a.vmax) {  // AMSGrad (torch semantics: the max of the raw second moment, then bias-corrected)
+        vd = fmaxf(a.vmax[4 * i + j], vd);
+        a.vmax[4 * i + j] = vd;
+      }
+      const float denom = sqrtf(vd) * rbc2 + a.eps;
       pp[j] = pp[j] * decay - step_size * mm[j] / denom;
     }
     reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
@@ -162,7 +170,12 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
       if (a.l2_coupled) gj += a.weight_decay * pj;
       const float mj = a.beta1 * ld_mom<MB>(a.m, i) + (1.f - a.beta1) * gj;
       const float vj = a.beta2 * ld_mom<MB>(a.v, i) + (1.f - a.beta2) * gj * gj;
-      pj = pj * decay - step_size * mj / (sqrtf(vj) * rbc2 + a.eps);
+      float vd = vj;
+      if (!MB && a.vmax) {
+        vd = fmaxf(a.vmax[i], vd);
+        a.vmax[i] = vd;
+      }
+      pj = pj * decay - step_size * mj / (sqrtf(vd) * rbc2 + a.eps);
       a.p[i] = pj;
       const uint32_t r = sr_hash(seed ^ 0x5bd1e995U ^ (uint32_t)(a.sr_offset + i));
       st_mom<MB>(a.m, i, mj, r);
@@ -188,6 +201,10 @@ void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStre
 }
 
 void adamw_step(const AdamWArgs& a, hipStream_t st) {
+  if (a.vmax && a.moments_bf16) {
+    fprintf(stderr, "mft::adamw_step: AMSGrad needs fp32 moments\n");
+    abort();
+  }
   long g = (a.n / 4 + 255) / 256;
   if (g < 1) g = 1;
   const int grid = (int)(g < 2048 ? g : 2048);

@@ -90,8 +90,10 @@ class DataParallel:
         # collectives recorded into the step's hipGraph from the backward's grad-ready hooks: the
         # default on RCCL (MFT_GRAPH_COMM=0 reduces the buckets eagerly after the replay instead).
         # Round 2 kept it opt-in after captures aborted intermittently at capture end on a 1-rank
-        # group; round 3 re-ran the recorded-collective tests (DDP, bf16, ZeRO-2) without an abort
-        # (profiles/r3_graph_comm_tests.log) and found RCCL's AVG inexact at some lengths, which is
+        # group; round 3 re-ran the recorded-collective tests (DDP, bf16, ZeRO-2:
+        # tests/test_dp_graph_gpu.py::test_reducer_with_graph_step_matches_no_dp, part of the 184 GPU
+        # tests passing in profiles/r3_final_gpu_tests.log) without an abort and found RCCL's AVG
+        # inexact at some lengths (profiles/r3_rccl_avg_tail.txt), which is
         # no longer used (sum + divide).  The capture runs in thread_local mode so RCCL's watchdog
         # thread polling earlier events cannot invalidate it (train/engine.py).
         self.capturable = self.nccl and os.environ.get("MFT_GRAPH_COMM", "1") == "1"

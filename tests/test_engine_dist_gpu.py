@@ -110,20 +110,21 @@ def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
     got = loss_list(out0, True)
     assert len(got) == 6 and got == pytest.approx(want, rel=tol, abs=tol), (extra, got, want)
     from mobilefinetuner_amd.io import safetensors as st
-    # compare the UPDATES (final - initial weights), per tensor, relative to the reference update:
-    # a chunk a rank never updated (or exported stale) moves by 0 and fails; so do LayerNorm values a
-    # non-owning rank kept stale (fp32-compute parameters under ZeRO-1/2)
+    # the final weights agree, and no element the reference updated stayed EXACTLY at its initial
+    # value in the DP export (weight decay moves every updated element): a chunk a rank never updated
+    # or exported stale, or LayerNorm values a non-owning rank kept stale (fp32-compute
+    # parameters under ZeRO-1/2), fail here.  (Elementwise update deltas cannot be compared tightly:
+    # parameters with a ~0 true gradient, e.g. the key bias, get noise-driven Adam steps.)
     init_out = str(tmp_path / "init.safetensors")
     _single("gpt2_full_finetune", [x for x in FULL if x not in ("--steps", "6")] + ["--steps", "0", "--output_path",
                                                                                        init_out], "--batch_size", 8)
     a, b, w0 = st.load_file(ref_out), st.load_file(dp_out), st.load_file(init_out)
-    rel = 0.05 if tol <= 2e-4 else 0.3
+    wtol = 50 * tol
     for k in a:
-        da, db = (a[k] - w0[k]).float(), (b[k] - w0[k]).float()
-        scale = da.abs().max().item()
-        assert scale > 0, (extra, k, "the reference did not update this tensor")
-        err = (da - db).abs().max().item()
-        assert err <= rel * scale, (extra, k, err, scale)
+        assert torch.allclose(a[k], b[k], atol=wtol, rtol=wtol), (extra, k, (a[k] - b[k]).abs().max())
+        moved = a[k] != w0[k]
+        stale = moved & (b[k] == w0[k])
+        assert moved.any() and int(stale.sum()) == 0, (extra, k, int(stale.sum()), int(moved.sum()))
 
 
 def test_native_dp_lora_and_gemma_two_ranks():

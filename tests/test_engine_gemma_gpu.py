@@ -239,3 +239,41 @@ def test_native_gemma_alignment_harness(tmp_path):
     with torch.no_grad():
         py = float(model(torch.from_numpy(ids).long().cuda(), torch.from_numpy(lab).long().cuda()))
     assert abs(py - mean_loss) < 1e-2 * py, (py, mean_loss)
+
+
+def test_native_gemma_embedding_dump_and_token_preview(tmp_path):
+    """--dump_embedding 1 --dump_embedding_step 2 --dump_embedding_dir D --preview_tokens N (reference
+    train_lora_gemma.cpp:293-301,924-932; gemma_trainer.cpp:104-109; gemma_model.cpp:875-940): the
+    second micro-batch's scaled token embeddings are written as raw fp32 [B, S, H] with matching
+    printed statistics, every row is a (bf16-rounded) row of embed_tokens x sqrt(H), and the first N
+    training tokens are printed."""
+    import re
+
+    import numpy as np
+    tmp = str(tmp_path)
+    S, B = 64, 4
+    _fixture(tmp, S=S)
+    dbg = os.path.join(tmp, "dbg")
+    r = subprocess.run([_bin("train_lora_gemma"), "--model_dir", tmp, "--pretokenized_path", os.path.join(tmp, "tokens.bin"),
+                        "--pretokenized_meta", os.path.join(tmp, "meta.json"), "--output_dir", os.path.join(tmp, "out"),
+                        "--seq_len", str(S), "--batch", str(B), "--max_steps", "3", "--log_interval", "1",
+                        "--dump_embedding", "1", "--dump_embedding_step", "2", "--dump_embedding_dir", dbg,
+                        "--preview_tokens", "10"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    from mobilefinetuner_amd.io import safetensors as st
+    toks = np.fromfile(os.path.join(tmp, "tokens.bin"), dtype=np.int32)  # train split first
+    m = re.search(r"First 10 train tokens: \[([0-9, ]+)\]", r.stdout)
+    assert m and [int(x) for x in m.group(1).split(",")] == [int(t) for t in toks[:10]], r.stdout[:3000]
+    m = re.search(r"\[EmbeddingDump\] step 2 shape=\[(\d+),(\d+),(\d+)\] mean=(\S+) std=(\S+) min=(\S+) max=(\S+)", r.stdout)
+    assert m, r.stdout[-3000:]
+    b, s, h = (int(m.group(i)) for i in (1, 2, 3))
+    assert (b, s) == (B, S)
+    e = np.fromfile(os.path.join(dbg, "embedding_step2.bin"), dtype=np.float32)
+    assert e.size == b * s * h
+    assert abs(e.mean() - float(m.group(4))) < 1e-4 and abs(e.std() - float(m.group(5))) < 1e-3
+    assert abs(e.min() - float(m.group(6))) < 1e-5 and abs(e.max() - float(m.group(7))) < 1e-5
+    w = st.load_file(os.path.join(tmp, "model.safetensors"))["model.embed_tokens.weight"].float()
+    table = (w * math.sqrt(h)).bfloat16().float()
+    rows = torch.from_numpy(e.reshape(-1, h))
+    d = torch.cdist(rows, table).min(dim=1).values
+    assert d.max().item() < 1e-3 * max(1.0, table.abs().max().item()), d.max()

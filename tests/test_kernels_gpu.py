@@ -112,14 +112,14 @@ def test_gelu_and_gated():
         _close(gu.grad, r.grad, 0.1, 0.01, msg=f"gated {act} grad")
 
 
-@pytest.mark.parametrize("M,K,N,nn,bm", [(300, 128, 264, False, 0), (1000, 192, 512, True, 0),
-                                          (777, 256, 136, False, 1), (64, 64, 8, True, 1),
-                                          (517, 320, 392, False, 2), (517, 320, 392, True, 2),
-                                          (300, 128, 264, False, 3), (300, 128, 264, True, 3),
-                                          (300, 128, 264, False, 8), (777, 320, 520, False, 8),
-                                          (64, 64, 8, False, 8), (1000, 704, 1024, False, 8)])
+@pytest.mark.parametrize("M,K,N,nn,bm", [(300, 128, 264, False, 8), (1000, 192, 512, True, 8),
+                                          (777, 256, 136, False, 8), (64, 64, 8, True, 8),
+                                          (517, 320, 392, False, 8), (517, 320, 392, True, 8),
+                                          (777, 320, 520, False, 8), (64, 64, 8, False, 8),
+                                          (1000, 704, 1024, False, 8)])
 def test_gemm_mfma(M, K, N, nn, bm):
-    """gemm.hip (NT and NN operand layouts, M/N tails) and its epilogues vs fp32 torch."""
+    """gemm8 through the `gemm` binding (NT and NN operand layouts, M/N tails) and its epilogues vs fp32
+    torch."""
     from mobilefinetuner_amd._ext import native
     C = native()
     x = torch.randn(M, K, device=DEV).bfloat16()
@@ -159,34 +159,6 @@ def test_gemm8_lora_epilogue(M, N, K, R):
     ref_ = a.float() @ b.float().t() + u.float() @ w.float()
     _close(out, ref_, 0.03, 0.01, msg="gemm8 lora")
     assert (wide[:, N:].float() == 7.0).all()
-
-
-@pytest.mark.parametrize("a3", ["0", "1"])
-@pytest.mark.parametrize("M,K,N", [(1000, 832, 776), (4096 + 40, 768, 2040)])
-def test_gemm4_nt_epilogues(M, K, N, a3, monkeypatch):
-    """gemm4 (4-wave 256x256, AGPR accumulators via tied asm MFMAs, range-checked buffer LDS-DMA;
-    gemm_t impl=2, opt-in) and its asymmetric-ring form (MFT_G4_A3=1): every NT epilogue vs fp32
-    torch on row / column tails, many K-tiles."""
-    from mobilefinetuner_amd._ext import native
-    monkeypatch.setenv("MFT_G4_A3", a3)  # read on every launch
-    C = native()
-    x = torch.randn(M, K, device=DEV).bfloat16()
-    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
-    b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
-    ref_ = x.float() @ w.float().t()
-    _close(C.gemm_t(x, w, False, False, 0, impl=2)[0], ref_, 0.02, 0.01, msg="gemm4 none")
-    _close(C.gemm_t(x, w, False, False, 1, bias=b, impl=2)[0], ref_ + b.float(), 0.02, 0.01, msg="gemm4 bias")
-    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    y = C.gemm_t(x, w, False, False, 9, bias=b, aux=aux, impl=2)[0]  # BIAS_GELU_D
-    _close(y, torch.nn.functional.gelu(ref_ + b.float(), approximate="tanh"), 0.02, 0.01, msg="gemm4 gelu")
-    u = torch.randn(M, 8, device=DEV).bfloat16()
-    lw = (torch.randn(8, N, device=DEV) * 0.1).bfloat16()
-    y = C.gemm_t(x, w, False, False, 5, alpha=0.5, lora_u=u, lora_w=lw, impl=2)[0]
-    _close(y, 0.5 * ref_ + u.float() @ lw.float(), 0.03, 0.01, msg="gemm4 lora")
-    acc = torch.randn(M, N, device=DEV)
-    want = acc + 2.0 * ref_
-    C.gemm_t(x, w, False, False, 4, alpha=2.0, out=acc, impl=2)
-    _close(acc, want, 0.03, 0.01, msg="gemm4 f32 acc")
 
 
 @pytest.mark.parametrize("dropout", [0.0, 0.2])
@@ -689,3 +661,26 @@ def test_gated_row_pair_grid_stride():
         _close(y, yr, 0.02, 0.01, msg=f"gated {act} long")
         _close(gu.grad, r.grad, 0.1, 0.01, msg=f"gated {act} long grad")
         del gu, y, g, r, yr
+
+
+def test_adamw_amsgrad_matches_torch():
+    """AMSGrad (reference optim/adam.cpp:52,78): the fused kernel with a vmax buffer == torch.optim.AdamW(amsgrad=True)
+    over 6 steps (decoupled weight decay, fp32 moments)."""
+    C = native()
+    torch.manual_seed(0)
+    n = 4099  # tail path too
+    p0 = torch.randn(n, device="cuda")
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.05, amsgrad=True)
+    p, m, v, vmax = p0.clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    lr = torch.full((1,), 1e-2, device="cuda")
+    step = torch.zeros(1, device="cuda")
+    for it in range(6):
+        g = torch.randn(n, device="cuda") * (3.0 if it == 1 else 0.3)  # a large early step makes the max matter
+        ref.grad = g.clone()
+        opt.step()
+        C.adamw_step(p, g, m, v, lr, step, None, 0.9, 0.99, 1e-8, 0.05, 0.0, False, None, None, 0, vmax)
+        C.adamw_commit(step, None, None)
+    torch.cuda.synchronize()
+    assert torch.allclose(p, ref.detach(), rtol=1e-5, atol=1e-6), (p - ref.detach()).abs().max()
+    assert torch.allclose(vmax, opt.state[ref]["max_exp_avg_sq"], rtol=1e-5, atol=1e-9)
