@@ -113,6 +113,8 @@ def _native_cmd(a, cfgd):
             cmd += ["--zero_stage", str(zero)]
         if cfgd.get("offload", False) or a.offload_optimizer:
             cmd += ["--offload", "host"]
+            if a.offload_fp32:
+                cmd += ["--offload_moments", "fp32"]
         if a.bf16_grads:
             cmd += ["--bf16_grads"]
     else:

@@ -164,7 +164,10 @@ inline bool load_token_splits(const Args& a, DataConfig& dc, int vocab, TokenDat
 //   --zero_stage 0|1|2|3 optimizer partition (1) + reduce-scattered gradients (2) + partitioned
 //                        parameters (3, full fine-tuning: engine/zero3.h); > 0 also on one process
 //                        (a 1-rank communicator: the partitioned code path runs)
-//   --offload host|none  AdamW moments (bf16, stochastically rounded) in pinned host DRAM
+//   --offload host|none  AdamW moments in pinned host DRAM (--offload_moments bf16 (stochastically
+//                        rounded, default) | fp32); ZeRO-3: --offload_mode stream (default: each
+//                        unit's moments copied through device slots and updated during the next
+//                        forward) | zerocopy (the kernel reads / writes them over PCIe)
 //   --bucket_mb N        fp32 gradient bytes per reduction bucket (default 25)
 //   --bf16_grads         reduce gradients in bf16      --no_overlap   reduce after the backward
 // MFT_DP_FORCE_COMM=1: a 1-rank communicator even without ZeRO (profiling the reducer on one GPU).
@@ -177,6 +180,12 @@ inline DistConfig dist_config_from(const Args& a) {
   const std::string off = a.get("offload", "none");
   if (off != "none" && off != "host") throw std::runtime_error("--offload host|none (got '" + off + "')");
   d.host_moments = off == "host";
+  const std::string om = a.get("offload_moments", "bf16");
+  if (om != "bf16" && om != "fp32") throw std::runtime_error("--offload_moments bf16|fp32 (got '" + om + "')");
+  d.host_fp32 = om == "fp32";
+  const std::string mode = a.get("offload_mode", "stream");
+  if (mode != "stream" && mode != "zerocopy") throw std::runtime_error("--offload_mode stream|zerocopy (got '" + mode + "')");
+  d.host_stream = mode == "stream";
   if (d.zero_stage < 0 || d.zero_stage > 3) throw std::runtime_error("--zero_stage 0|1|2|3 in the native engine");
   return d;
 }
@@ -210,14 +219,18 @@ struct DistSetup {
   // after the optimizer exists (the reducer shards it)
   void make_dp(eng::Communicator* comm, eng::AdamW& opt, const DistConfig& d) {
     if (z3) {
-      z3->shard_optimizer(opt, d.host_moments);
-      std::printf("  %s%s\n", z3->describe().c_str(), d.host_moments ? "; AdamW moments in pinned host DRAM (bf16)" : "");
+      z3->shard_optimizer(opt, d.host_moments, d.host_fp32, d.host_stream);
+      std::printf("  %s%s%s%s\n", z3->describe().c_str(),
+                  !d.host_moments ? "" : d.host_fp32 ? "; AdamW moments in pinned host DRAM (fp32)" : "; AdamW moments in pinned host DRAM (bf16)",
+                  !d.host_moments ? "" : d.host_stream ? ", streamed per unit through 3 device slots on copy streams, "
+                                                          "applied during the next forward" : ", read in place over PCIe",
+                  "");
     } else if (comm) {
       dp = std::make_unique<eng::DataParallel>(*flat, plan, *comm, opt, d);
       std::printf("  data parallel: %s\n", dp->describe().c_str());
     } else if (d.host_moments) {
-      opt.shard({eng::OptSegment{0, flat->numel, 0}}, nullptr, true);
-      std::printf("  AdamW moments in pinned host DRAM (bf16)\n");
+      opt.shard({eng::OptSegment{0, flat->numel, 0}}, nullptr, true, d.host_fp32);
+      std::printf("  AdamW moments in pinned host DRAM (%s)\n", d.host_fp32 ? "fp32" : "bf16");
     }
   }
   eng::GradReducer* reducer() { return z3 ? static_cast<eng::GradReducer*>(z3.get()) : dp.get(); }

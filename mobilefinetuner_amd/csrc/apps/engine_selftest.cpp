@@ -14,6 +14,7 @@
 #include "engine/allocator.h"
 #include "engine/autograd.h"
 #include "engine/gemm.h"
+#include "engine/nn.h"
 #include "engine/ops.h"
 #include "engine/tensor.h"
 
@@ -408,6 +409,31 @@ int main() {
     expect("allocator: small blocks coalesce back", al.stats().allocated == s0.allocated);
   }
   synchronize();
+  {  // fused LoRA input projection in the norm (nn.h add_norm with lora_a): the appended columns hold
+     // u = y A^T of the stored bf16 row, the rest of the tail is zero; LayerNorm and RMSNorm(1 + w)
+    NoGradGuard ng;
+    for (int rms = 0; rms < 2; ++rms)
+      for (int R : {8, 24}) {
+        const int M = 37, N = 96, OC = 128;
+        Tensor x = dev(rnd((size_t)M * N), {M, N}, DType::BF16);
+        Param w, b;
+        w.c = w.leaf = dev(rnd(N, 0.5, 1.5), {N});
+        b.c = b.leaf = dev(rnd(N), {N});
+        Tensor A = dev(rnd((size_t)R * N, -0.2, 0.2), {R, N}, DType::BF16);
+        Tensor y = add_norm(x, Tensor(), w, rms ? nullptr : &b, 1e-5f, rms == 1, rms ? 1.f : 0.f, OC, A).second;
+        const std::vector<double> yv = host(y), av = host(A);
+        std::vector<double> got, ref;
+        for (int m = 0; m < M; ++m)
+          for (int c = N; c < OC; ++c) {
+            double u = 0.0;
+            if (c < N + R)
+              for (int k = 0; k < N; ++k) u += yv[(size_t)m * OC + k] * av[(size_t)(c - N) * N + k];
+            ref.push_back(u);
+            got.push_back(yv[(size_t)m * OC + c]);
+          }
+        check(std::string(rms ? "rms" : "layer") + "_norm + fused LoRA u (R=" + std::to_string(R) + ")", got, ref, 1e-2);
+      }
+  }
   std::printf(g_fail ? "FAILED: %d check(s)\n" : "ALL OK\n", g_fail);
   return g_fail ? 1 : 0;
 }

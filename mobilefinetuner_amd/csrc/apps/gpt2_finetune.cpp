@@ -61,7 +61,7 @@ const std::set<std::string> kValued = {
     "eval_batch_size", "save_every", "ema_beta", "seed", "pm_interval", "pm_batt_thresh", "pm_temp_thresh",
     "pm_fb_high", "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "pm_power_cap",
     "shard_dir", "shard_budget_mb", "shard_fp16_disk", "model", "synthetic_tokens", "pretokenized_path",
-    "pretokenized_meta", "lora_targets", "metrics_out", "device", "bench_steps", "bench_warmup", "zero_stage", "offload", "bucket_mb", "dump_grads"};
+    "pretokenized_meta", "lora_targets", "metrics_out", "device", "bench_steps", "bench_warmup", "zero_stage", "offload", "offload_moments", "offload_mode", "bucket_mb", "dump_grads"};
 
 Args parse(int argc, char** argv) { return parse_args(argc, argv, kBool, kValued); }
 

@@ -70,7 +70,7 @@ const std::set<std::string> kValued = {
     "data_fraction", "log_interval", "eval_steps", "eval_batches", "save_every", "seed", "model", "synthetic_tokens",
     "resume_from", "state_dir", "inject_fault", "metrics_out", "eval_out", "pm_interval", "pm_batt_thresh", "pm_temp_thresh", "pm_fb_high",
     "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "pm_power_cap", "device",
-    "shard_budget_mb", "shard_dir", "shard_fp16_disk", "bench_steps", "bench_warmup", "zero_stage", "offload", "bucket_mb",
+    "shard_budget_mb", "shard_dir", "shard_fp16_disk", "bench_steps", "bench_warmup", "zero_stage", "offload", "offload_moments", "offload_mode", "bucket_mb",
     "align_dump_dir", "align_layers", "align_pt_weights_dir", "align_numeric_eps", "align_numeric_count",
     "align_numeric_targets", "dump_grads", "dump_embedding", "dump_embedding_step", "dump_embedding_dir",
     "preview_tokens"};

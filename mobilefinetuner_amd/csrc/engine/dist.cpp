@@ -111,7 +111,7 @@ DataParallel::DataParallel(FlatParams& flat, const FlatPlan& plan, Communicator&
       segs.push_back({plan_.buckets[b].first + r * cs, cs, st});
       st += cs;
     }
-    opt_.shard(segs, &comm_, cfg_.host_moments);
+    opt_.shard(segs, &comm_, cfg_.host_moments, cfg_.host_fp32);
   }
 }
 
@@ -128,7 +128,7 @@ std::string DataParallel::describe() const {
      << " rank(s) [" << comm_.backend() << "], " << plan_.buckets.size() << " bucket(s) of <= "
      << cfg_.bucket_bytes / 1048576 << " MB fp32, " << (cfg_.bf16_reduce ? "bf16" : "fp32") << " reduction, "
      << (cfg_.overlap ? "overlapped with the backward" : "after the backward");
-  if (cfg_.host_moments) os << ", AdamW moments in pinned host DRAM";
+  if (cfg_.host_moments) os << ", AdamW moments in pinned host DRAM (" << (cfg_.host_fp32 ? "fp32" : "bf16") << ")";
   return os.str();
 }
 

@@ -51,6 +51,13 @@ class GradReducer {
   virtual void after_optimizer() {}
   // full fp32 masters on every rank before a checkpoint (ZeRO-1/2)
   virtual void gather_master() {}
+  // a reducer that runs the optimizer itself (ZeRO-3's host-streamed AdamW, engine/zero3.h): the
+  // trainer calls prepare_optimizer() after the backward instead of AdamW::step(); the update is
+  // applied per unit during the NEXT forward, and flush_optimizer() applies a pending update at once
+  // (before evaluation, checkpoints, exports and at the end of training)
+  virtual bool owns_optimizer() const { return false; }
+  virtual void prepare_optimizer() {}
+  virtual void flush_optimizer() {}
   // ZeRO-3: each rank's flat holds only its partitions (no initial broadcast, per-rank masters)
   virtual bool params_sharded() const { return false; }
   // factor folded into the loss seed (and the fused LM-head weight grad): a reducer that SUMS
@@ -67,7 +74,10 @@ struct DistConfig {
   int64_t bucket_bytes = 25 << 20;   // fp32 gradient bytes per bucket (MFT_BUCKET_MB)
   bool bf16_reduce = false;          // reduce gradients in bf16 (half the bytes on the links)
   bool overlap = true;               // launch buckets from the grad-ready hooks during backward
-  bool host_moments = false;         // stage >= 1: AdamW moments (bf16) in pinned host DRAM
+  bool host_moments = false;         // stage >= 1: AdamW moments in pinned host DRAM
+  bool host_fp32 = false;            // ... as fp32 (default bf16, stochastically rounded)
+  bool host_stream = true;           // ZeRO-3: stream each unit's moments through device slots during
+                                     // the next forward (false: the kernel reads them over PCIe)
 };
 
 struct FlatPlan {

@@ -465,28 +465,31 @@ std::pair<Tensor, Tensor> Gemma3::layer(int i, const Tensor& x0, const Tensor& h
   // streamed weights: no resident augmented-K copy [W | s B^T], the adapters run beside the GEMM
   const bool st = streamer_ != nullptr;
   auto aug = [&](std::vector<LoraAdapter>& ads, int in) { return (ads.empty() || st) ? 0 : lora_aug_cols(in, ads); };
-  auto proj = [&](const Tensor& x, int K, Param& w, std::vector<LoraAdapter>& ads, Tensor& waug) {
+  // the fused A stack when the producing RMSNorm computes u = y A^T itself (no dropout, sum r <= 32)
+  auto fused_a = [&](std::vector<LoraAdapter>& ads) { return (ads.empty() || st) ? Tensor() : lora_fused_a(ads, training); };
+  auto proj = [&](const Tensor& x, int K, Param& w, std::vector<LoraAdapter>& ads, Tensor& waug, bool u_ready) {
     if (ads.empty()) return linear_p(x, w, nullptr);
     if (st) return lora_linear(x, w, nullptr, ads, s, training, dropout_ctr);
-    return lora_linear_aug(x, K, w, nullptr, ads, s, waug, training, dropout_ctr);
+    return lora_linear_aug(x, K, w, nullptr, ads, s, waug, training, dropout_ctr, u_ready);
   };
   auto& L = layers_[i];
   const auto cs = rope(L.sliding, (int)S);
   Tensor x = x0;
   // attention
-  Tensor qkv = proj(h, H, L.qkv_w, active(L.lqkv), L.waug_qkv).view({B, S, nq + 2 * nkv, D});
+  Tensor qkv = proj(h, H, L.qkv_w, active(L.lqkv), L.waug_qkv, fused_a(active(L.lqkv)).defined()).view({B, S, nq + 2 * nkv, D});
   Tensor o = qknorm_rope_attention(qkv, nq, nkv, L.q_norm, L.k_norm, cs.first, cs.second, eps, 1.f,
                                    interleaved_rope, attn_scale, L.sliding ? cfg_.sliding_window : 0,
                                    aug(active(L.lo), nq * D));
   o = o.view({B * S, o.size(-1)});
-  Tensor a = proj(o, nq * D, L.o_w, active(L.lo), L.waug_o);
+  Tensor a = proj(o, nq * D, L.o_w, active(L.lo), L.waug_o, false);
   a = add_norm(a, Tensor(), L.post_attn_norm, nullptr, eps, true, 1.f, 0).second;
-  auto r = add_norm(x, a, L.pre_ff_norm, nullptr, eps, true, 1.f, aug(active(L.lgu), H));
+  const Tensor agu = fused_a(active(L.lgu));
+  auto r = add_norm(x, a, L.pre_ff_norm, nullptr, eps, true, 1.f, aug(active(L.lgu), H), agu);
   x = r.first;
   // GeGLU MLP
-  Tensor gu = proj(r.second, H, L.gu_w, active(L.lgu), L.waug_gu);
+  Tensor gu = proj(r.second, H, L.gu_w, active(L.lgu), L.waug_gu, agu.defined());
   Tensor g = gated_act(gu, cfg_.act, aug(active(L.ldown), I));
-  Tensor f = proj(g, I, L.down_w, active(L.ldown), L.waug_down);
+  Tensor f = proj(g, I, L.down_w, active(L.ldown), L.waug_down, false);
   f = add_norm(f, Tensor(), L.post_ff_norm, nullptr, eps, true, 1.f, 0).second;
   if (!capture_layers.empty() && std::find(capture_layers.begin(), capture_layers.end(), i) != capture_layers.end()) {
     NoGradGuard ng;
@@ -494,7 +497,7 @@ std::pair<Tensor, Tensor> Gemma3::layer(int i, const Tensor& x0, const Tensor& h
   }
   Param& nw = i + 1 < cfg_.n_layer ? layers_[i + 1].in_norm : final_norm_;
   const int oc = i + 1 < cfg_.n_layer ? aug(active(layers_[i + 1].lqkv), H) : 0;
-  return add_norm(x, f, nw, nullptr, eps, true, 1.f, oc);
+  return add_norm(x, f, nw, nullptr, eps, true, 1.f, oc, oc ? fused_a(active(layers_[i + 1].lqkv)) : Tensor());
 }
 
 Tensor Gemma3::embed_tokens(const Tensor& ids) {
@@ -509,7 +512,9 @@ Tensor Gemma3::hidden(const Tensor& ids) {
   rope(false, (int)S), rope(true, (int)S);  // tables before any capture / checkpoint
   Tensor x = embed(ids, embed_, nullptr, embed_scale_);
   const int oc0 = (active(layers_[0].lqkv).empty() || st) ? 0 : lora_aug_cols(H, active(layers_[0].lqkv));
-  Tensor h = add_norm(x, Tensor(), layers_[0].in_norm, nullptr, cfg_.eps, true, 1.f, oc0).second;
+  Tensor h = add_norm(x, Tensor(), layers_[0].in_norm, nullptr, cfg_.eps, true, 1.f, oc0,
+                      oc0 ? lora_fused_a(active(layers_[0].lqkv), training) : Tensor())
+                 .second;
   const bool ckpt = grad_checkpoint && training && grad_enabled();
   for (int i = 0; i < cfg_.n_layer; ++i) {
     if (st) streamer_->ensure(i, i + 1);

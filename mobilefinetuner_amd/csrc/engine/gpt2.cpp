@@ -459,10 +459,12 @@ std::pair<Tensor, Tensor> GPT2::block(int i, const Tensor& x0, const Tensor& h, 
   auto aug = [&](std::vector<LoraAdapter>& ads) { return (ads.empty() || st) ? 0 : lora_aug_cols(C, ads); };
   auto& b = blocks_[i];
   Tensor x = x0;
-  // attention
+  // attention (u = ln_1(x) A^T of the qkv adapter(s) was written by the LayerNorm that produced h)
+  const bool u_ready = !st && !active(b.lqkv).empty() && lora_fused_a(active(b.lqkv), training).defined();
   Tensor qkv = active(b.lqkv).empty() ? linear_p(h, b.attn_w, &b.attn_b)
                : st ? lora_linear(h, b.attn_w, &b.attn_b, active(b.lqkv), scale, training, dropout_ctr)
-                    : lora_linear_aug(h, C, b.attn_w, &b.attn_b, active(b.lqkv), scale, b.waug_qkv, training, dropout_ctr);
+                    : lora_linear_aug(h, C, b.attn_w, &b.attn_b, active(b.lqkv), scale, b.waug_qkv, training, dropout_ctr,
+                                      u_ready);
   Tensor o = attention_packed(qkv.view({B, S, 3, H, D}), 1.f / std::sqrt((float)D), true, 0, aug(active(b.lproj)));
   o = o.view({B * S, o.size(-1)});
   Tensor a = active(b.lproj).empty() ? linear_p(o, b.proj_w, &b.proj_b)
@@ -484,7 +486,8 @@ std::pair<Tensor, Tensor> GPT2::block(int i, const Tensor& x0, const Tensor& h, 
   Param* nw = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_w : &lnf_w_;
   Param* nb = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_b : &lnf_b_;
   const int oc = i + 1 < cfg_.n_layer ? aug(active(blocks_[i + 1].lqkv)) : 0;
-  return add_norm(x, f, *nw, nb, cfg_.eps, false, 0.f, oc);
+  return add_norm(x, f, *nw, nb, cfg_.eps, false, 0.f, oc,
+                  oc ? lora_fused_a(active(blocks_[i + 1].lqkv), training) : Tensor());
 }
 
 Tensor GPT2::hidden(const Tensor& ids) {
@@ -497,7 +500,9 @@ Tensor GPT2::hidden(const Tensor& ids) {
   if (bp) bp->begin_forward();
   Tensor x = embed(ids, wte_, &wpe_, 1.f);
   const int oc0 = (active(blocks_[0].lqkv).empty() || st) ? 0 : lora_aug_cols(C, active(blocks_[0].lqkv));
-  Tensor h = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, oc0).second;
+  Tensor h = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, oc0,
+                      oc0 ? lora_fused_a(active(blocks_[0].lqkv), training) : Tensor())
+                 .second;
   const bool ckpt = grad_checkpoint && training && grad_enabled();
   for (int i = 0; i < cfg_.n_layer; ++i) {
     if (bp) bp->ensure(i, i + 1);

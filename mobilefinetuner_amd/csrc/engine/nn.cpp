@@ -113,7 +113,7 @@ struct NormNode : Node {
 }  // namespace
 
 std::pair<Tensor, Tensor> add_norm(const Tensor& x, const Tensor& delta, Param& w, Param* b, float eps, bool rms,
-                                   float offset, int out_cols) {
+                                   float offset, int out_cols, const Tensor& lora_a) {
   const int N = (int)x.size(-1);
   MFT_CHECK(x.dtype() == DType::BF16 && N % 8 == 0 && N <= 4096, "norm: bf16 rows, width % 8, <= 4096");
   const long M = x.numel() / N;
@@ -127,12 +127,20 @@ std::pair<Tensor, Tensor> add_norm(const Tensor& x, const Tensor& delta, Param& 
   Tensor mean = rms ? Tensor() : empty({M}, DType::F32, x.device());
   Tensor rstd = empty({M}, DType::F32, x.device());
   Tensor s = d2.defined() ? empty({M, (int64_t)N}, DType::BF16, x.device()) : Tensor();
+  const int lr = lora_a.defined() ? (int)lora_a.size(0) : 0;
+  if (lr) {
+    MFT_CHECK(lora_a.dtype() == DType::BF16 && lora_a.dim() == 2 && lora_a.size(1) == N && lora_a.stride(1) == 1 &&
+                  lora_a.stride(0) % 8 == 0 && lr <= 32 && oc >= N + lr,
+              "add_norm: fused LoRA A [R <= 32, N] bf16 with R appended columns");
+  }
+  const ::mft::bf16_t* la = lr ? bp(lora_a) : nullptr;
+  const long lda = lr ? lora_a.stride(0) : 0;
   if (rms) {
     ::mft::rmsnorm_fwd(bp(x2), d2.defined() ? bp(d2) : nullptr, s.defined() ? bp(s) : nullptr, fp(w32), bp(y),
-                       fp(rstd), (int)M, N, eps, offset, oc, S());
+                       fp(rstd), (int)M, N, eps, offset, oc, S(), la, lda, lr);
   } else {
     ::mft::layernorm_fwd(bp(x2), d2.defined() ? bp(d2) : nullptr, s.defined() ? bp(s) : nullptr, fp(w32), fp(b32),
-                         bp(y), fp(mean), fp(rstd), (int)M, N, eps, oc, S());
+                         bp(y), fp(mean), fp(rstd), (int)M, N, eps, oc, S(), la, lda, lr);
   }
   Shape ys = x.shape();
   ys.back() = oc;
@@ -514,8 +522,24 @@ int lora_aug_cols(int in_features, const std::vector<LoraAdapter>& ads) {
   return (in_features + r + 63) / 64 * 64;
 }
 
+Tensor lora_fused_a(const std::vector<LoraAdapter>& ads, bool training) {
+  if (ads.empty()) return Tensor();
+  int rt = 0;
+  for (auto& a : ads) {
+    if (a.dropout > 0.f && training) return Tensor();
+    if (a.A.c.dtype() != DType::BF16 || a.A.c.stride(1) != 1) return Tensor();
+    rt += a.rank;
+  }
+  if (rt > 32) return Tensor();
+  if (ads.size() == 1) return ads[0].A.c;
+  NoGradGuard ng;
+  std::vector<Tensor> as;
+  for (auto& a : ads) as.push_back(a.A.c);
+  return cat(as, 0);
+}
+
 Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<LoraAdapter>& ads, float s,
-                       Tensor& waug, bool training, const Tensor& drop_ctr) {
+                       Tensor& waug, bool training, const Tensor& drop_ctr, bool u_ready) {
   MFT_CHECK(!w.trainable(), "lora_linear_aug: the base weight must be frozen");
   const int64_t Ka = xa.size(-1), N = w.c.size(0);
   Tensor xa2 = xa.detach().reshape({-1, Ka});
@@ -532,7 +556,10 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
   for (auto& a : ads) nodrop = nodrop && (a.dropout <= 0.f || !training);
   int off = K;
   Tensor acat;  // [sum r_i, K]: built once per step, reused by the backward's fused dx epilogue
-  if (nodrop && ads.size() > 1) {  // one pass over x for every u_i (adjacent appended columns)
+  MFT_CHECK(!u_ready || nodrop, "lora_linear_aug: u precomputed by the producer needs dropout off");
+  if (u_ready) {
+    // u_1..u_n already in the appended columns (the norm that produced xa computed them)
+  } else if (nodrop && ads.size() > 1) {  // one pass over x for every u_i (adjacent appended columns)
     std::vector<Tensor> as;
     for (auto& a : ads) as.push_back(a.A.c);
     {
@@ -545,7 +572,7 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
   }
   for (auto& a : ads) {
     const int R = a.rank;
-    if (!(nodrop && ads.size() > 1)) {
+    if (!u_ready && !(nodrop && ads.size() > 1)) {
       ::mft::LoraDrop d{drop_ctr.defined() ? drop_ctr.data<int64_t>() : nullptr, a.salt, training ? a.dropout : 0.f};
       ::mft::lora_rowdot(bp(x2), x2.stride(0), bp(a.A.c), a.A.c.stride(0), bp(xa2) + off, xa2.stride(0), M, K, R, 1.f,
                          d, S());

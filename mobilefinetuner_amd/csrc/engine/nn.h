@@ -35,8 +35,10 @@ struct Param {
 // s = x + delta (if delta defined), y = LayerNorm(s) (or RMSNorm(1+w) when rms); y allocated
 // [M, out_cols] when out_cols > N (appended columns zeroed, for a LoRA consumer's augmented input).
 // Returns {s, y} (s == x when no delta).
+// lora_a [R, N] (bf16, defined only with out_cols >= N + R): the appended columns receive u = y A^T
+// instead of zeros -- the LoRA consumer's input projection fused into the norm (lora_fused_a).
 std::pair<Tensor, Tensor> add_norm(const Tensor& x, const Tensor& delta, Param& w, Param* b, float eps, bool rms,
-                                   float offset, int out_cols);
+                                   float offset, int out_cols, const Tensor& lora_a = Tensor());
 Tensor embed(const Tensor& ids, Param& wte, Param* wpe, float scale);
 // qkv [B, S, 3, H, D] -> o [B, S, H*D] (or [B, S, out_cols] with zeroed tail when out_cols > H*D)
 Tensor attention_packed(const Tensor& qkv, float scale, bool causal, int window, int out_cols);
@@ -65,8 +67,13 @@ struct LoraAdapter {
 int lora_aug_cols(int in_features, const std::vector<LoraAdapter>& ads);
 // xa [M, Ka] holds x in its first K columns (zero tail); waug [N, Ka] = [W | s B^T.. | 0] (owned by
 // the caller, W copied once); W frozen.
+// u_ready: the producer already wrote u_1..u_n into xa's appended columns (add_norm with lora_a =
+// lora_fused_a(ads)); the adapters' A must not change between that producer and this call.
 Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<LoraAdapter>& ads, float scale,
-                       Tensor& waug, bool training, const Tensor& drop_ctr);
+                       Tensor& waug, bool training, const Tensor& drop_ctr, bool u_ready = false);
+// the [sum r_i, in] stack of the adapters' A (bf16 compute copies) when a producer can compute u for
+// lora_linear_aug itself (no dropout in effect, sum r <= 32); undefined otherwise
+Tensor lora_fused_a(const std::vector<LoraAdapter>& ads, bool training);
 // plain (non-augmented) LoRA Linear: y = x W^T + b + s * (drop(x) A_i^T) B_i in column slices
 Tensor lora_linear(const Tensor& x, Param& w, Param* b, std::vector<LoraAdapter>& ads, float scale, bool training,
                    const Tensor& drop_ctr);

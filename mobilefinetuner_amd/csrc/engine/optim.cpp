@@ -80,7 +80,7 @@ AdamW::AdamW(FlatParams& flat, const AdamWConfig& cfg) : flat_(flat), cfg_(cfg) 
   state_numel_ = flat.numel;
 }
 
-void AdamW::shard(const std::vector<OptSegment>& segs, Communicator* comm, bool host_moments) {
+void AdamW::shard(const std::vector<OptSegment>& segs, Communicator* comm, bool host_moments, bool host_fp32) {
   NoGradGuard ng;
   segs_ = segs;
   comm_ = comm;
@@ -92,9 +92,10 @@ void AdamW::shard(const std::vector<OptSegment>& segs, Communicator* comm, bool 
   }
   const int64_t n = std::max<int64_t>(state_numel_, 4);
   MFT_CHECK(!(host_moments && cfg_.amsgrad), "AdamW: AMSGrad keeps fp32 moments on the device (no --offload host)");
-  if (host_moments) {  // pinned host DRAM, read / written in place by the kernel (bf16, SR-rounded)
-    m = zeros({n}, DType::BF16, Device::cpu(true));
-    v = zeros({n}, DType::BF16, Device::cpu(true));
+  if (host_moments) {  // pinned host DRAM, read / written in place by the kernel (bf16 SR-rounded, or fp32)
+    const DType md = host_fp32 ? DType::F32 : DType::BF16;
+    m = zeros({n}, md, Device::cpu(true));
+    v = zeros({n}, md, Device::cpu(true));
   } else {
     m = zeros({n}, DType::F32);
     v = zeros({n}, DType::F32);
@@ -107,7 +108,7 @@ void AdamW::set_lr(float lr) {
   lr_dev.fill_(lr);  // the value travels as a kernel argument: no host-buffer race, no sync
 }
 
-void AdamW::step() {
+void AdamW::prepare() {
   hipStream_t s = current_stream();
   const bool clip = cfg_.max_grad_norm > 0.f;
   float* g0 = flat_.grad.data<float>();
@@ -125,12 +126,15 @@ void AdamW::step() {
   }
   // non-finite grads: with clipping the (all-reduced) norm^2 is non-finite exactly then, so no
   // separate pass over the grads is needed (adamw_commit records the flag); without, one scan
-  const bool scan = cfg_.skip_nonfinite && !clip;
-  if (scan) {
+  if (cfg_.skip_nonfinite && !clip) {
     nonfinite_dev.zero_();
     for (auto& sg : segs_) ::mft::nonfinite_check(g0 + sg.off, sg.len, nonfinite_dev.data<int>(), s);
     if (comm_) comm_->all_reduce(nonfinite_dev.data_ptr(), 1, CommType::I32, CommOp::Max, s);  // skip together
   }
+}
+
+::mft::AdamWArgs AdamW::args() const {
+  const bool clip = cfg_.max_grad_norm > 0.f;
   ::mft::AdamWArgs a{};
   a.lr_ptr = lr_dev.data<float>();
   a.beta1 = cfg_.beta1;
@@ -141,7 +145,15 @@ void AdamW::step() {
   a.sumsq = clip ? sumsq_dev.data<float>() : nullptr;
   a.max_norm = cfg_.max_grad_norm;
   a.l2_coupled = cfg_.l2_coupled;
-  a.nonfinite = scan ? nonfinite_dev.data<int>() : nullptr;
+  a.nonfinite = (cfg_.skip_nonfinite && !clip) ? nonfinite_dev.data<int>() : nullptr;
+  return a;
+}
+
+void AdamW::step() {
+  hipStream_t s = current_stream();
+  prepare();
+  ::mft::AdamWArgs a = args();
+  float* g0 = flat_.grad.data<float>();
   a.moments_bf16 = m.dtype() == DType::BF16;
   const size_t ms = m.dtype() == DType::BF16 ? 2 : 4;
   for (auto& sg : segs_) {
@@ -162,6 +174,39 @@ void AdamW::step() {
     k::Desc d = desc(skipped_dev), x = desc(nonfinite_dev);
     k::binary(d, d, x, k::B_ADD, 1.f, s);
   }
+}
+
+// ---------------------------------------------------------------- delayed (streamed) updates
+void AdamW::prepare_delayed() {
+  if (!pending_dev.defined()) {
+    pending_dev = zeros({1}, DType::I32);
+    lr_step_dev = zeros({1}, DType::F32);
+  }
+  prepare();
+  lr_step_dev.copy_(lr_dev);  // this step's lr travels with its gradients
+  pending_dev.fill_(1.0);
+}
+
+void AdamW::apply_delayed(int64_t off, int64_t len, void* m_dev, void* v_dev, bool moments_bf16, hipStream_t s) {
+  MFT_CHECK(pending_dev.defined() && !vmax.defined(), "AdamW::apply_delayed: prepare_delayed first (no AMSGrad)");
+  ::mft::AdamWArgs a = args();
+  a.lr_ptr = lr_step_dev.data<float>();
+  a.enable = pending_dev.data<int>();
+  a.p = flat_.master.data<float>() + off;
+  a.g = flat_.grad.data<float>() + off;
+  a.m = static_cast<float*>(m_dev);
+  a.v = static_cast<float*>(v_dev);
+  a.moments_bf16 = moments_bf16;
+  a.n = len;
+  a.shadow = (::mft::bf16_t*)flat_.shadow.data_ptr() + off;
+  a.sr_offset = off;
+  ::mft::adamw_step(a, s);
+}
+
+void AdamW::commit_delayed(hipStream_t s) {
+  if (!pending_dev.defined()) return;
+  ::mft::AdamWArgs a = args();
+  ::mft::adamw_commit(step_dev.data<float>(), a.nonfinite, a.sumsq, s, nullptr, pending_dev.data<int>(), 1);
 }
 
 float AdamW::grad_norm() const { return std::sqrt(std::max(0.f, (float)sumsq_dev.item())); }

@@ -14,6 +14,7 @@
 
 #include "engine/comm.h"
 #include "engine/nn.h"
+#include "kernels.h"
 
 namespace mft {
 namespace eng {
@@ -54,7 +55,17 @@ class AdamW {
  public:
   AdamW(FlatParams& flat, const AdamWConfig& cfg);
   void set_lr(float lr);  // host -> device scalar (outside graph capture)
-  void step();            // device-only work: capturable
+  void step();            // device-only work: capturable (prepare + every segment + commit)
+  // the gradient statistics of step(): global norm^2 (all-reduced) / non-finite flag
+  void prepare();
+  // Delayed, streamed updates (ZeRO-3 + host moments, engine/zero3.h): prepare_delayed() after the
+  // backward records the step's statistics and lr and marks the gradients pending;
+  // apply_delayed() then updates one flat range [off, off + len) with moments staged on the device
+  // (gated on the pending flag); commit_delayed() advances the step count and clears the flag.
+  void prepare_delayed();
+  void apply_delayed(int64_t off, int64_t len, void* m_dev, void* v_dev, bool moments_bf16, hipStream_t s);
+  void commit_delayed(hipStream_t s);
+  Tensor pending_dev, lr_step_dev;  // delayed mode: gradients pending (int32), their lr
   float grad_norm() const;  // host sync
   bool skipped_last() const;
   int64_t applied_steps() const;
@@ -68,7 +79,7 @@ class AdamW {
   // kernel reads and writes in place over PCIe (the host-offload tier of the optimizer state).
   // The grad-norm^2 and the non-finite flag are all-reduced over `comm`, so every rank clips and
   // skips identically.
-  void shard(const std::vector<OptSegment>& segs, Communicator* comm, bool host_moments);
+  void shard(const std::vector<OptSegment>& segs, Communicator* comm, bool host_moments, bool host_fp32 = false);
   const std::vector<OptSegment>& segments() const { return segs_; }
   bool sharded() const { return comm_ != nullptr; }
   bool moments_on_host() const { return host_moments_; }
@@ -82,6 +93,7 @@ class AdamW {
   bool host_moments_ = false;
   int64_t state_numel_ = 0;
   Tensor part_;  // sumsq partials
+  ::mft::AdamWArgs args() const;  // hyper-parameters, lr / step / norm / skip pointers
 };
 
 // (a) GPT-2 CLIs: linear warmup (step+1)/W, then cosine to min_ratio of lr (0-indexed step)

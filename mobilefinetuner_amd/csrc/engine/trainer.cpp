@@ -63,8 +63,16 @@ void Trainer::reduce_grads() {
 }
 
 void Trainer::optimizer() {
+  if (dp_ && dp_->owns_optimizer()) {  // ZeRO-3 host-streamed AdamW: applied during the next forward
+    dp_->prepare_optimizer();
+    return;
+  }
   opt_.step();
   if (dp_) dp_->after_optimizer();
+}
+
+void Trainer::flush_optimizer() {
+  if (dp_ && dp_->owns_optimizer()) dp_->flush_optimizer();
 }
 
 void Trainer::fwd_bwd() {
@@ -141,6 +149,7 @@ std::pair<double, double> Trainer::evaluate(int max_batches, int batch_size) {
   TraceRange range("mft.eval");
   if (!valid_) return {0.0, 0.0};
   Communicator::QuietScope quiet(comm_);  // rank-local work between collectives: not a hang
+  flush_optimizer();                      // the weights of every step so far
   NoGradGuard ng;
   valid_->reset_cursor();
   const int S = cfg_.seq;
@@ -367,6 +376,7 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
 
 void Trainer::gather_for_export() {
   if (!dp_) return;
+  flush_optimizer();
   synchronize();
   dp_->gather_master();  // ZeRO-1/2: all-gather the master chunks (a no-op otherwise); collective
   synchronize();
@@ -382,6 +392,7 @@ void Trainer::save_state(const std::string& dir) {
   namespace fs = std::filesystem;
   synchronize();
   const int r = comm_ ? comm_->rank() : 0;
+  flush_optimizer();
   if (dp_) dp_->gather_master();  // ZeRO: every rank's master chunks (collective)
   sync_ema();
   synchronize();

@@ -71,6 +71,8 @@ class Trainer {
   // ZeRO-1/2: the full fp32 masters on every rank before a checkpoint writer reads them
   // (collective; train() calls it before periodic save_fn exports and once at the end)
   void gather_for_export();
+  // a reducer-owned delayed optimizer (ZeRO-3 host-streamed AdamW): apply the pending update now
+  void flush_optimizer();
   void train(const std::function<void(int64_t)>& save_fn);
   // Benchmark (bench.py's native engine): `warmup` untimed optimizer steps (the first two eager,
   // then the hipGraph capture), then `steps` timed steps bracketed on both sides by a device

@@ -68,13 +68,23 @@ class Zero3 : public GradReducer, public BlockProvider {
   Zero3& operator=(const Zero3&) = delete;
 
   FlatParams& flat() { return flat_; }  // this rank's partitions + the replicated parameters
-  // the partitioned AdamW (moments for the local flat; host_moments: bf16 in pinned host DRAM)
-  void shard_optimizer(AdamW& opt, bool host_moments);
+  // the partitioned AdamW (moments for the local flat; host_moments: in pinned host DRAM, bf16 or
+  // fp32).  streamed (with host_moments): the moments never sit in HBM whole and are never read
+  // over PCIe by the kernel -- each unit's partition is updated right before the next forward
+  // gathers it: its moments are copied host -> device into one of `slots` staging slots on an H2D
+  // copy stream (issued slots - 1 units ahead, so the copies run under the forward's compute), the
+  // fused AdamW runs on its own stream, the moments go back device -> host on a D2H stream and the
+  // unit's all-gather waits only for its own update.  The step's gradients, norm and lr wait in
+  // place from the end of one backward to the next forward (AdamW::prepare_delayed).
+  void shard_optimizer(AdamW& opt, bool host_moments, bool host_fp32 = false, bool streamed = false, int slots = 3);
 
   // GradReducer
   void begin_micro(int i, int n) override;
   void finish() override;
   void after_optimizer() override;
+  bool owns_optimizer() const override { return sopt_ != nullptr; }
+  void prepare_optimizer() override;
+  void flush_optimizer() override;
   bool params_sharded() const override { return true; }
   float grad_prescale() const override;
   void zero_grad(FlatParams& flat) override;
@@ -116,6 +126,23 @@ class Zero3 : public GradReducer, public BlockProvider {
   hipEvent_t order_ = nullptr, join_ = nullptr;
   hipStream_t stream_ = nullptr;  // communication stream
   Tensor dummy_, tmp_;            // placeholder leaf storage, reduce-scatter landing buffer
+  // ---- host-streamed optimizer (shard_optimizer(..., streamed = true))
+  // update index i: 0 = the replicated parameters, 1 + u = unit u (forward order)
+  int64_t upd_off(int i) const { return i == 0 ? rep_off_ : units_[i - 1].local; }
+  int64_t upd_len(int i) const { return i == 0 ? rep_n_ : units_[i - 1].s; }
+  void opt_fork();             // the copy / optimizer streams join the current stream's work
+  void opt_prefetch(int i);    // H2D of update i's moments into its slot
+  void opt_update(int i);      // AdamW on update i (after its H2D), then its D2H
+  AdamW* sopt_ = nullptr;
+  bool sfp32_ = false, pending_host_ = false, forked_ = false;
+  int nslot_ = 0;
+  std::vector<Tensor> mslot_, vslot_;           // device staging of one update's moments
+  std::vector<int> sh2d_, supd_;                // per update: prefetch issued / update issued (this step)
+  std::vector<hipEvent_t> h2d_ev_, upd_ev_;     // per update
+  std::vector<hipEvent_t> d2h_ev_;              // per slot: its moments are back on the host
+  std::vector<char> d2h_live_;
+  hipEvent_t fork_ev_ = nullptr, ojoin_ev_ = nullptr;
+  hipStream_t h2d_ = nullptr, d2h_ = nullptr, ostream_ = nullptr;
 };
 
 }  // namespace eng

@@ -14,10 +14,14 @@ int norm_bwd_partial_blocks(int M);
 void reduce_rows(const float* part, float* out, int nb, int N, int accumulate, hipStream_t st);
 // ldy / lddy: row stride of the normalised output / of its gradient (0 = N).  A wider output row
 // leaves room for appended columns (the LoRA augmented-K input [x | u], lora.hip).
+// lora_a [lora_r, N] (row stride lda, bf16; lora_r <= 32 <= ldy - N): the appended columns receive
+// u = y A^T (the LoRA consumer's input projection) instead of zeros.
 void layernorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, const float* b,
-                   bf16_t* y, float* mean, float* rstd, int M, int N, float eps, long ldy, hipStream_t st);
+                   bf16_t* y, float* mean, float* rstd, int M, int N, float eps, long ldy, hipStream_t st,
+                   const bf16_t* lora_a = nullptr, long lda = 0, int lora_r = 0);
 void rmsnorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, bf16_t* y, float* rstd,
-                 int M, int N, float eps, float w_offset, long ldy, hipStream_t st);
+                 int M, int N, float eps, float w_offset, long ldy, hipStream_t st, const bf16_t* lora_a = nullptr,
+                 long lda = 0, int lora_r = 0);
 void layernorm_bwd(const bf16_t* x, const bf16_t* dy, const float* w, const float* mean, const float* rstd,
                    const bf16_t* dresid, bf16_t* dx, float* dw, float* db, float* work, int M, int N, int accumulate,
                    long lddy, hipStream_t st);
@@ -196,10 +200,14 @@ struct AdamWArgs {
   int moments_bf16;       // m / v are bf16 (stochastically rounded; host-offloaded optimizer state)
   long sr_offset;         // global element index of p[0] (chunked / sharded launches): keys the SR hash
   float* vmax;            // AMSGrad: running max of v (fp32 moments only; null = plain Adam(W))
+  const int* enable;      // optional device gate: the update runs only when *enable != 0 (a delayed
+                          // optimizer's "gradients pending" flag)
 };
 void adamw_step(const AdamWArgs& a, hipStream_t st);
-// after every adamw_step launch of one update: *step += 1 unless the update was skipped
-void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStream_t st, int* flag_out = nullptr);
+// after every adamw_step launch of one update: *step += 1 unless the update was skipped (or gated
+// off by *enable == 0); clear_enable: then *enable = 0 (the pending update is consumed)
+void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStream_t st, int* flag_out = nullptr,
+                  int* enable = nullptr, int clear_enable = 0);
 // flag[0] = any(!isfinite(x))  (accumulates with OR)
 void nonfinite_check(const float* x, long n, int* flag, hipStream_t st);
 

@@ -9,17 +9,26 @@
 // and the normalise pass, so the row is read from HBM exactly once.  Optional fused residual
 // add (s = x + d; y = norm(s)) removes a separate elementwise pass per transformer sub-block.
 // Statistics (mean/rstd) are saved in fp32 for the backward.  The affine weight is fp32.
+// LoRA consumer fusion: when the output row is wider (augmented-K input of a LoRA projection,
+// engine/nn.h lora_linear_aug) and an adapter matrix A [R, N] is given, the same pass also writes
+// u = y A^T (the bf16-rounded normalised row, as the consumer reads it) into the appended columns
+// N .. N+R-1 -- the separate pass over y (lora_rowdot) disappears.
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace mft {
 
-template <int CH, bool RMS, bool RESID>
+template <int CH, bool RMS, bool RESID, int LR = 0>
 __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ d,
                                                        bf16_t* __restrict__ s_out, const float* __restrict__ w,
                                                        const float* __restrict__ b, bf16_t* __restrict__ y,
                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                       int M, int N, float eps, float w_offset, long ldy) {
+                                                       int M, int N, float eps, float w_offset, long ldy,
+                                                       const bf16_t* __restrict__ la = nullptr, long lda = 0,
+                                                       int R = 0) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -64,6 +73,9 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
     }
   }
   const float rstd = rsqrtf(wave_sum(sq) / N + eps);
+  float up[LR > 0 ? LR : 1];  // LoRA: this lane's partial sums of y . A[r]
+#pragma unroll
+  for (int r = 0; r < (LR > 0 ? LR : 1); ++r) up[r] = 0.f;
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     const int ch = lane + c * 64;
@@ -83,11 +95,42 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
         for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * wv[j] + bv[j];
       }
       store8(y + (long)row * ldy + ch * 8, o);
+      if constexpr (LR > 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(o[j]));  // the consumer reads the stored bf16 row
+#pragma unroll
+        for (int r = 0; r < LR; ++r) {
+          if (r < R) {
+            float av[8];
+            load8(la + (long)r * lda + ch * 8, av);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) up[r] = fmaf(o[j], av[j], up[r]);
+          }
+        }
+      }
     }
   }
-  // a wider output row (appended LoRA columns, see kernels.h) leaves its extra columns zeroed
-  for (long c = N + lane * 8; c < ldy; c += 64 * 8)
-    *reinterpret_cast<u16x8_t*>(y + (long)row * ldy + c) = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  if constexpr (LR > 0) {
+#pragma unroll
+    for (int r = 0; r < LR; ++r)
+      if (r < R) up[r] = wave_sum(up[r]);
+  }
+  // a wider output row (appended LoRA columns, see kernels.h): u in the first R of them (LoRA
+  // fusion), the rest zeroed
+  for (long c = N + lane * 8; c < ldy; c += 64 * 8) {
+    float z[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      z[j] = 0.f;
+      if constexpr (LR > 0) {
+        const long r = c - N + j;
+#pragma unroll
+        for (int q = 0; q < LR; ++q)
+          if (r == q && q < R) z[j] = up[q];
+      }
+    }
+    store8(y + (long)row * ldy + c, z);
+  }
   if (lane == 0) {
     if (!RMS) mean_out[row] = mean;
     rstd_out[row] = rstd;
@@ -209,9 +252,31 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
 template <bool RMS>
 static void norm_fwd_dispatch(const bf16_t* x, const bf16_t* d, bf16_t* s_out, const float* w, const float* b,
                               bf16_t* y, float* mean, float* rstd, int M, int N, float eps, float w_offset,
-                              long ldy, hipStream_t st) {
+                              long ldy, hipStream_t st, const bf16_t* la = nullptr, long lda = 0, int R = 0) {
   const int nch = N / 8, ch = (nch + 63) / 64;
   dim3 grid(cdiv(M, 4)), block(256);
+  if (la && R > 0) {  // fused LoRA input projection: R <= 32 ranks, appended columns hold them
+    if (R > 32 || ldy < N + R) {
+      fprintf(stderr, "mft::norm_fwd: LoRA fusion needs R <= 32 appended columns (R=%d, ldy=%ld, N=%d)\n", R, ldy, N);
+      abort();
+    }
+#define MFT_NFL(CHV, LRV)                                                                                      \
+  if (d)                                                                                                       \
+    norm_fwd_kernel<CHV, RMS, true, LRV><<<grid, block, 0, st>>>(x, d, s_out, w, b, y, mean, rstd, M, N, eps, w_offset, ldy, la, lda, R); \
+  else                                                                                                         \
+    norm_fwd_kernel<CHV, RMS, false, LRV><<<grid, block, 0, st>>>(x, d, s_out, w, b, y, mean, rstd, M, N, eps, w_offset, ldy, la, lda, R);
+#define MFT_NFR(LRV)                  \
+  if (ch <= 1) { MFT_NFL(1, LRV) }    \
+  else if (ch <= 2) { MFT_NFL(2, LRV) } \
+  else if (ch <= 4) { MFT_NFL(4, LRV) } \
+  else { MFT_NFL(8, LRV) }
+    if (R <= 8) { MFT_NFR(8) }
+    else if (R <= 16) { MFT_NFR(16) }
+    else { MFT_NFR(32) }
+#undef MFT_NFR
+#undef MFT_NFL
+    return;
+  }
 #define MFT_NF(CHV)                                                                                        \
   if (d)                                                                                                   \
     norm_fwd_kernel<CHV, RMS, true><<<grid, block, 0, st>>>(x, d, s_out, w, b, y, mean, rstd, M, N, eps, w_offset, ldy); \
@@ -262,14 +327,17 @@ int norm_bwd_partial_blocks(int M) {
 }
 
 void layernorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, const float* b,
-                   bf16_t* y, float* mean, float* rstd, int M, int N, float eps, long ldy, hipStream_t st) {
-  norm_fwd_dispatch<false>(x, resid_delta, resid_out, w, b, y, mean, rstd, M, N, eps, 0.f, ldy > 0 ? ldy : N, st);
+                   bf16_t* y, float* mean, float* rstd, int M, int N, float eps, long ldy, hipStream_t st,
+                   const bf16_t* lora_a, long lda, int lora_r) {
+  norm_fwd_dispatch<false>(x, resid_delta, resid_out, w, b, y, mean, rstd, M, N, eps, 0.f, ldy > 0 ? ldy : N, st,
+                           lora_a, lda, lora_r);
 }
 
 void rmsnorm_fwd(const bf16_t* x, const bf16_t* resid_delta, bf16_t* resid_out, const float* w, bf16_t* y,
-                 float* rstd, int M, int N, float eps, float w_offset, long ldy, hipStream_t st) {
+                 float* rstd, int M, int N, float eps, float w_offset, long ldy, hipStream_t st,
+                 const bf16_t* lora_a, long lda, int lora_r) {
   norm_fwd_dispatch<true>(x, resid_delta, resid_out, w, nullptr, y, nullptr, rstd, M, N, eps, w_offset,
-                          ldy > 0 ? ldy : N, st);
+                          ldy > 0 ? ldy : N, st, lora_a, lda, lora_r);
 }
 
 void layernorm_bwd(const bf16_t* x, const bf16_t* dy, const float* w, const float* mean, const float* rstd,

@@ -97,6 +97,7 @@ __device__ __forceinline__ void st_mom(void* p, long i, float x, uint32_t r) {
 
 template <bool MB>
 __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
+  if (a.enable && *a.enable == 0) return;         // delayed optimizer: no gradients pending
   if (adamw_skip(a.nonfinite, a.sumsq)) return;  // skip-step on NaN/Inf grads (fault tolerance)
   const float lr = *a.lr_ptr;
   const float t = *a.step_ptr + 1.f;  // *step_ptr counts APPLIED steps; adamw_commit advances it
@@ -188,16 +189,20 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
 // step += 1 only when the update was applied (a skipped step must not advance bias correction);
 // flag_out (optional) records whether the step was skipped -- with clipping on, a non-finite grad
 // makes the global norm^2 non-finite, so that one reduction replaces the separate scan of the grads
-__global__ void adamw_commit_kernel(float* step, const int* nonfinite, const float* sumsq, int* flag_out) {
+__global__ void adamw_commit_kernel(float* step, const int* nonfinite, const float* sumsq, int* flag_out, int* enable,
+                                    int clear_enable) {
   if (threadIdx.x == 0) {
+    if (enable && *enable == 0) return;  // nothing was pending: nothing applied, nothing to record
     const bool skip = adamw_skip(nonfinite, sumsq);
     if (!skip) step[0] += 1.f;
     if (flag_out) flag_out[0] = skip ? 1 : 0;
+    if (enable && clear_enable) *enable = 0;
   }
 }
 
-void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStream_t st, int* flag_out) {
-  adamw_commit_kernel<<<1, 64, 0, st>>>(step, nonfinite, sumsq, flag_out);
+void adamw_commit(float* step, const int* nonfinite, const float* sumsq, hipStream_t st, int* flag_out, int* enable,
+                  int clear_enable) {
+  adamw_commit_kernel<<<1, 64, 0, st>>>(step, nonfinite, sumsq, flag_out, enable, clear_enable);
 }
 
 void adamw_step(const AdamWArgs& a, hipStream_t st) {

@@ -92,6 +92,9 @@ def _single(prog, args, batch_flag, batch):
     (["--zero_stage", "3"], 2e-4),
     (["--zero_stage", "3", "--no_graph", "--grad_accum_steps", "1"], 2e-4),
     (["--zero_stage", "3", "--offload", "host"], 3e-3),
+    (["--zero_stage", "2", "--offload", "host", "--offload_moments", "fp32"], 2e-4),  # fp32 host moments: exact
+    (["--zero_stage", "3", "--offload", "host", "--offload_moments", "fp32"], 2e-4),  # streamed (default)
+    (["--zero_stage", "3", "--offload", "host", "--offload_mode", "zerocopy"], 3e-3),
 ])
 def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
     """2 loopback ranks x batch 4 == 1 process x batch 8 (GPT-2-tiny full fine-tune, ~8 buckets):
@@ -169,12 +172,14 @@ def test_native_rccl_zero3_step_in_graph():
     assert loss_list(r.stdout, True) == pytest.approx(want, rel=2e-4, abs=2e-4)
 
 
-@pytest.mark.parametrize("stage", ["2", "3"])
+@pytest.mark.parametrize("stage", ["2", "3", "3+offload"])
 def test_native_dp_state_resume_two_ranks(tmp_path, stage):
     """ZeRO-2 / ZeRO-3 full-state checkpoint (gathered fp32 master, or each rank's own parameter
     partitions, + one optimizer partition per rank): 4 steps, then both ranks resume from the saved
     state and finish steps 5-8 with the uninterrupted run's losses."""
-    base = FULL[:-4] + ["--bucket_mb", "0.25", "--batch_size", "4", "--zero_stage", stage, "--warmup_steps", "100"]
+    extra = ["--offload", "host", "--offload_moments", "fp32"] if stage.endswith("+offload") else []
+    base = FULL[:-4] + ["--bucket_mb", "0.25", "--batch_size", "4", "--zero_stage", stage[:1], "--warmup_steps", "100",
+                        *extra]
     ref = _run_ranks([_bin("gpt2_full_finetune"), *base, "--steps", "8"], 2)
     assert all(rc == 0 for rc, _, _ in ref)
     want = loss_list(ref[0][1])
