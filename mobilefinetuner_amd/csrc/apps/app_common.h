@@ -3,6 +3,9 @@
 // eval CLI accepts (pretokenized stream, synthetic stream, raw WikiText-2 text) and the
 // power-monitor flags.
 #pragma once
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -33,6 +36,23 @@
 
 namespace mft {
 namespace apps {
+
+// Fatal-signal report (SIGSEGV / SIGBUS / SIGFPE / SIGILL / SIGABRT): the native backtrace of the
+// faulting thread on stderr, then the default action (core / exit status unchanged) -- how a crash
+// inside a runtime call (e.g. a profiler hooking hipGraphLaunch) is located without a debugger.
+inline void crash_report(int sig) {
+  void* frames[64];
+  const int n = ::backtrace(frames, 64);
+  char head[96];
+  const int k = std::snprintf(head, sizeof(head), "\n[mft] fatal signal %d; native backtrace (%d frames):\n", sig, n);
+  if (k > 0) (void)!::write(2, head, (size_t)k);
+  ::backtrace_symbols_fd(frames, n, 2);
+  ::signal(sig, SIG_DFL);
+  ::raise(sig);
+}
+inline void install_crash_report() {
+  for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT}) ::signal(sig, crash_report);
+}
 
 using eng::DistConfig;
 

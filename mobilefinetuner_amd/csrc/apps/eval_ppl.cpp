@@ -196,6 +196,7 @@ int run(int argc, char** argv) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  mft::apps::install_crash_report();
   try {
     return run(argc, argv);
   } catch (const std::exception& e) {

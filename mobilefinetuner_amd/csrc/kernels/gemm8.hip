@@ -360,53 +360,102 @@ __device__ __forceinline__ void lds_barrier() {
   raw_barrier();
 }
 
-// ------------------------------------------------------------------ LDS-staged epilogue (NONE / BIAS)
+// ------------------------------------------------------------------ LDS-staged epilogues
 // The register epilogue stores 16 rows x 64 B per wave instruction, which the store path moves at
 // ~13 B/cycle per CU; whole-row segments (>= 128 B per row) move at ~48 B/cycle per CU when not
-// every CU stores at once (profiles/r4_store_probe.txt).  Here the finished bf16 tile goes to the
-// (now idle) LDS operand buffers -- 16-B chunks XOR-swizzled by (row & 31): conflict-free writes and
-// reads -- and leaves as 2 full 512-B tile rows per wave instruction.
-template <int EPI>
-__device__ __forceinline__ void epilogue_lds(const GemmArgs& g, f32x4_t (&acc)[4][4][2], int m0, int n0, int wm, int wn,
-                                             int lane, bf16_t* lds) {
-  const int g4 = lane >> 4;
-  const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int qa = (q == 2 || q == 3) ? 1 : 0, qb = (q == 1 || q == 2) ? 1 : 0;
-    const int colt = qb * 128 + wn * 32 + cofs;
-    float bias_v[8];
-    if constexpr (EPI == GEMM_EPI_BIAS) load8(g.bias + min(n0 + colt, g.N - 8), bias_v);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float v[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[q][i][0][r]),
-                                                         __float_as_uint(acc[q][i][1][r]), false, false);
-        v[r] = __uint_as_float(sw[0]);
-        v[4 + r] = __uint_as_float(sw[1]);
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        v[e] *= g.alpha;
-        if constexpr (EPI == GEMM_EPI_BIAS) v[e] += bias_v[e];
-      }
-      const int rowt = qa * 128 + wm * 64 + i * 16 + (lane & 15);
-      const int ch = (colt >> 3) ^ (rowt & 31);
-      uint4 pk = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
-      *reinterpret_cast<uint4*>(lds + rowt * 256 + (ch << 3)) = pk;
-    }
-  }
-  lds_barrier();
+// every CU stores at once (profiles/r4_store_probe.txt).  Here the finished bf16 tile goes through
+// the (now idle) LDS operand buffers -- 16-B chunks XOR-swizzled by (row & 31): conflict-free
+// writes and reads -- and leaves as 2 full 512-B tile rows per wave instruction.  Epilogues with an
+// [M, N] operand (dGELU, MUL_AUX) bring it in the same way: one LDS-DMA of whole tile rows into the
+// image, then every lane reads back its own fragment positions and overwrites them in place.
+// BIAS_GELU_D has two outputs: two rounds through the one 128 KB image.
+__device__ __forceinline__ int lds_tile_off(int rowt, int chunk) { return rowt * 256 + ((chunk ^ (rowt & 31)) << 3); }
+
+// the whole [256 x 256] bf16 tile image -> C rows (bounds-checked), 16 x 16 B per lane
+__device__ __forceinline__ void lds_tile_store(const bf16_t* lds, bf16_t* C, long ldc, int m0, int n0, int M, int N) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int c = k * 512 + tid;
     const int rowt = c >> 5, chunk = c & 31;
-    const uint4 pk = *reinterpret_cast<const uint4*>(lds + rowt * 256 + ((chunk ^ (rowt & 31)) << 3));
+    const uint4 pk = *reinterpret_cast<const uint4*>(lds + lds_tile_off(rowt, chunk));
     const int row = m0 + rowt, col = n0 + chunk * 8;
-    if (row < g.M && col < g.N) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col) = pk;
+    if (row < M && col < N) *reinterpret_cast<uint4*>(C + (long)row * ldc + col) = pk;
+  }
+}
+
+// X rows [m0, m0 + 256) x cols [n0, n0 + 256) (clamped at the edges) -> the swizzled tile image by
+// LDS-DMA (lane-linear destination; the swizzle is applied on the source column), then waited
+__device__ __forceinline__ void lds_tile_load(bf16_t* lds, const bf16_t* X, long ldx, int m0, int n0, int M, int N) {
+  const int tid = threadIdx.x, w = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = k * 512 + tid;           // destination chunk of the image (lane-linear)
+    const int rowt = c >> 5, dch = c & 31;  // image row, swizzled chunk slot
+    const int chunk = dch ^ (rowt & 31);    // the logical column chunk stored at that slot
+    const int row = min(m0 + rowt, M - 1), col = min(n0 + chunk * 8, N - 8);
+    glds16_8(X + (long)row * ldx + col, lds + (k * 512 + w * 64) * 8);
+  }
+  vm_wait<0>();
+  lds_barrier();
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue_lds(const GemmArgs& g, f32x4_t (&acc)[4][4][2], int m0, int n0, int wm, int wn,
+                                             int lane, bf16_t* lds) {
+  constexpr bool kAux = EPI == GEMM_EPI_DGELU || EPI == GEMM_EPI_MUL_AUX;
+  constexpr bool kBias = EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU_D;
+  constexpr int kRounds = EPI == GEMM_EPI_BIAS_GELU_D ? 2 : 1;
+  const int g4 = lane >> 4;
+  const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
+  if constexpr (kAux) lds_tile_load(lds, g.aux, g.ldaux, m0, n0, g.M, g.N);
+#pragma unroll
+  for (int rnd = 0; rnd < kRounds; ++rnd) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int qa = (q == 2 || q == 3) ? 1 : 0, qb = (q == 1 || q == 2) ? 1 : 0;
+      const int colt = qb * 128 + wn * 32 + cofs;
+      float bias_v[8];
+      if constexpr (kBias) load8(g.bias + min(n0 + colt, g.N - 8), bias_v);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[q][i][0][r]),
+                                                           __float_as_uint(acc[q][i][1][r]), false, false);
+          v[r] = __uint_as_float(sw[0]);
+          v[4 + r] = __uint_as_float(sw[1]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] *= g.alpha;
+          if constexpr (kBias) v[e] += bias_v[e];
+        }
+        const int rowt = qa * 128 + wm * 64 + i * 16 + (lane & 15);
+        uint4* slot = reinterpret_cast<uint4*>(lds + lds_tile_off(rowt, colt >> 3));
+        if constexpr (kAux) {
+          const u16x8_t av = __builtin_bit_cast(u16x8_t, *slot);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= EPI == GEMM_EPI_DGELU ? gelu_tanh_grad(bf2f(av[e])) : bf2f(av[e]);
+        }
+        if constexpr (EPI == GEMM_EPI_BIAS_GELU_D) {
+          float d[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gelu_tanh_and_grad(v[e], v[e], d[e]);
+          if (rnd == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = d[e];
+          }
+        }
+        *slot = uint4{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+      }
+    }
+    lds_barrier();
+    bf16_t* dst = (EPI == GEMM_EPI_BIAS_GELU_D && rnd == 1) ? g.aux : reinterpret_cast<bf16_t*>(g.C);
+    const long ldd = (EPI == GEMM_EPI_BIAS_GELU_D && rnd == 1) ? g.ldaux : g.ldc;
+    lds_tile_store(lds, dst, ldd, m0, n0, g.M, g.N);
+    if (rnd + 1 < kRounds) lds_barrier();  // every wave's reads of the image done before round 2 writes
   }
 }
 
@@ -417,8 +466,12 @@ __device__ __forceinline__ void epilogue_lds(const GemmArgs& g, f32x4_t (&acc)[4
 // Numerics: the loss comes from fp32 logits; E is relative to its tile max, so every softmax term
 // keeps bf16's relative precision whatever the logit magnitude (raw bf16 logits of a pretrained
 // model, |logit| ~ 100, would be quantised to 0.5).
+// LDSE: the E tile goes through an LDS image (after the 4 KB reduction scratch) and leaves as whole
+// tile rows (lds_tile_store) instead of 16-row x 64-B register stores.
+template <bool LDSE = false>
 __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc)[4][4][2], int m0, int n0, int wm,
                                                 int wn, int lane, float* red) {
+  bf16_t* img = reinterpret_cast<bf16_t*>(red) + 4096;  // 8 KB past the scratch (LDSE)
   const int g4 = lane >> 4, r16 = lane & 15;
   const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
   const int T = (g.N + 255) / 256, tn = n0 >> 8;
@@ -508,7 +561,14 @@ __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc
           o[q][i][e] = x;
           s += x;
         }
-        if (g.C && rok && c < g.N) store8(reinterpret_cast<bf16_t*>(g.C) + (long)R * g.ldc + c, o[q][i]);
+        if constexpr (LDSE) {
+          const int rowt = R - m0, colt = c - n0;
+          const float* ov = o[q][i];
+          *reinterpret_cast<uint4*>(img + lds_tile_off(rowt, colt >> 3)) =
+              uint4{pack_bf2(ov[0], ov[1]), pack_bf2(ov[2], ov[3]), pack_bf2(ov[4], ov[5]), pack_bf2(ov[6], ov[7])};
+        } else {
+          if (g.C && rok && c < g.N) store8(reinterpret_cast<bf16_t*>(g.C) + (long)R * g.ldc + c, o[q][i]);
+        }
       }
       s += xor16_pl(s);
       s += xor32_pl(s);
@@ -533,6 +593,10 @@ __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc
         p[0] = mt[qa][i];
         p[1] = (v[0] + v[1]) + (v[2] + v[3]);
       }
+  }
+  if constexpr (LDSE) {
+    if (g.C) lds_tile_store(img, reinterpret_cast<bf16_t*>(g.C), g.ldc, m0, n0, g.M, g.N);  // (the image was
+    // complete at the lds_barrier above: every wave wrote its E pieces before it)
   }
 }
 
@@ -822,9 +886,13 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   vm_wait<0>();  // drain the clamped tail prefetches (LDS-DMA must not outlive the workgroup)
   G8_STAMP(2);
 
-  if constexpr (EPI == GEMM_EPI_CE_FWD) epilogue_ce_fwd(g, acc, m0, n0, wm, wn, lane, reinterpret_cast<float*>(smem));
+  if constexpr (EPI == GEMM_EPI_CE_FWD) {
+    if constexpr (LDSEPI) raw_barrier();  // every wave's tail LDS-DMA retired before the image overwrites LDS
+    epilogue_ce_fwd<LDSEPI>(g, acc, m0, n0, wm, wn, lane, reinterpret_cast<float*>(smem));
+  }
   else if constexpr (EPI == GEMM_EPI_CE_DGRAD) epilogue_ce_dgrad(g, acc, m0, n0, wm, wn, lane);
-  else if constexpr (LDSEPI && (EPI == GEMM_EPI_NONE || EPI == GEMM_EPI_BIAS)) {
+  else if constexpr (LDSEPI && (EPI == GEMM_EPI_NONE || EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU_D ||
+                                 EPI == GEMM_EPI_DGELU || EPI == GEMM_EPI_MUL_AUX)) {
     raw_barrier();  // every wave's tail LDS-DMA retired (vm_wait<0> above) before the tile overwrites LDS
     epilogue_lds<EPI>(g, acc, m0, n0, wm, wn, lane, smem);
   } else epilogue8<EPI>(g, acc, m0, n0, wm, wn, lane, split);
@@ -1340,15 +1408,17 @@ static void launch8(const GemmArgs& g, hipStream_t st) {
       return;
     }
   }
-  if constexpr (!AT && (EPI == GEMM_EPI_NONE || EPI == GEMM_EPI_BIAS)) {
+  if constexpr (!AT && (EPI == GEMM_EPI_NONE || EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU_D ||
+                        EPI == GEMM_EPI_DGELU || EPI == GEMM_EPI_MUL_AUX || EPI == GEMM_EPI_CE_FWD)) {
     if (gemm8_ldsepi()) {
+      constexpr size_t shm_e = EPI == GEMM_EPI_CE_FWD ? shm + 8192 : shm;  // + the CE reduction scratch
       static bool attr_e = false;
       if (!attr_e) {
         MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm8_kernel<EPI, AT, BT, true, true, true>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_e));
         attr_e = true;
       }
-      gemm8_kernel<EPI, AT, BT, true, true, true><<<tiles * ks, 512, shm, st>>>(g);
+      gemm8_kernel<EPI, AT, BT, true, true, true><<<tiles * ks, 512, shm_e, st>>>(g);
       return;
     }
   }
