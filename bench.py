@@ -115,6 +115,8 @@ def _native_cmd(a, cfgd):
             cmd += ["--offload", "host"]
             if a.offload_fp32:
                 cmd += ["--offload_moments", "fp32"]
+            if a.offload_mode:
+                cmd += ["--offload_mode", a.offload_mode]
         if a.bf16_grads:
             cmd += ["--bf16_grads"]
     else:
@@ -325,6 +327,9 @@ def main():
     ap.add_argument("--seq", type=int, default=0)
     ap.add_argument("--offload_optimizer", action="store_true", help="full fine-tune: AdamW state in pinned host DRAM")
     ap.add_argument("--offload_fp32", action="store_true", help="offloaded AdamW moments in fp32 (default bf16)")
+    ap.add_argument("--offload_mode", choices=["stream", "zerocopy"], default=None,
+                    help="native ZeRO-3 offload: per-unit updates during the next forward (stream, default) or one "
+                         "update after the backward (zerocopy)")
     ap.add_argument("--zero", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
                     help="full fine-tune configs: ZeRO stage override (-1 = the config's, used when N > 1)")
     ap.add_argument("--rank", type=int, default=8)

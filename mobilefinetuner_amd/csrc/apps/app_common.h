@@ -51,7 +51,10 @@ inline void crash_report(int sig) {
   ::raise(sig);
 }
 inline void install_crash_report() {
-  for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT}) ::signal(sig, crash_report);
+  struct sigaction sa {};
+  sa.sa_handler = crash_report;
+  sigemptyset(&sa.sa_mask);
+  for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT}) ::sigaction(sig, &sa, nullptr);
 }
 
 using eng::DistConfig;
@@ -186,8 +189,9 @@ inline bool load_token_splits(const Args& a, DataConfig& dc, int vocab, TokenDat
 //                        (a 1-rank communicator: the partitioned code path runs)
 //   --offload host|none  AdamW moments in pinned host DRAM (--offload_moments bf16 (stochastically
 //                        rounded, default) | fp32); ZeRO-3: --offload_mode stream (default: each
-//                        unit's moments copied through device slots and updated during the next
-//                        forward) | zerocopy (the kernel reads / writes them over PCIe)
+//                        unit updated during the next forward, on its own stream, under the
+//                        compute) | zerocopy (one update after the backward); both read / write the
+//                        moments in place over PCIe
 //   --bucket_mb N        fp32 gradient bytes per reduction bucket (default 25)
 //   --bf16_grads         reduce gradients in bf16      --no_overlap   reduce after the backward
 // MFT_DP_FORCE_COMM=1: a 1-rank communicator even without ZeRO (profiling the reducer on one GPU).
@@ -242,8 +246,8 @@ struct DistSetup {
       z3->shard_optimizer(opt, d.host_moments, d.host_fp32, d.host_stream);
       std::printf("  %s%s%s%s\n", z3->describe().c_str(),
                   !d.host_moments ? "" : d.host_fp32 ? "; AdamW moments in pinned host DRAM (fp32)" : "; AdamW moments in pinned host DRAM (bf16)",
-                  !d.host_moments ? "" : d.host_stream ? ", streamed per unit through 3 device slots on copy streams, "
-                                                          "applied during the next forward" : ", read in place over PCIe",
+                  !d.host_moments ? "" : d.host_stream ? ", read in place over PCIe, each unit updated during the next "
+                                                          "forward on its own stream" : ", read in place over PCIe after the backward",
                   "");
     } else if (comm) {
       dp = std::make_unique<eng::DataParallel>(*flat, plan, *comm, opt, d);

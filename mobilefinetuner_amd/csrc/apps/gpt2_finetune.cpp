@@ -138,6 +138,7 @@ int run(int argc, char** argv) {
   hipStream_t stream;
   HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   set_current_stream(stream);
+  mft::apps::install_crash_report();  // again: the HIP runtime's initialisation may replace handlers
 
   const int seq_len = a.i("seq_len", 128);
   const uint64_t seed = (uint64_t)a.l("seed", 42);

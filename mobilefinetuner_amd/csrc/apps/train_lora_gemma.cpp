@@ -348,6 +348,7 @@ int run(int argc, char** argv) {
   hipStream_t stream;
   HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   set_current_stream(stream);
+  mft::apps::install_crash_report();  // again: the HIP runtime's initialisation may replace handlers
   const bool lead = !comm || comm->rank() == 0;
   const uint64_t seed = (uint64_t)a.l("seed", 42);
 

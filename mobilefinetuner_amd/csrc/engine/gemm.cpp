@@ -263,11 +263,12 @@ void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y) {
   // Static routing (no timing, identical on every rank and rerun): a PLAIN GEMM (no fused epilogue
   // beyond the bias) is a library GEMM -> hipBLASLt; every fused-epilogue GEMM (GELU, dGELU, LoRA,
   // LM-head cross entropy, split-K weight gradients) is the hand-written gemm8.  MFT_NT=gemm8|lt or
-  // MFT_GEMM8_ALL=1 (every GEMM of the step hand-written) override it.
+  // MFT_GEMM8_ALL=1 (every GEMM of the step hand-written) override it; deterministic mode keeps gemm8
+  // (one fixed reduction order whatever the operands' addresses and the library's heuristic pick).
   static const char* env = std::getenv("MFT_NT");
   static const int forced = !env ? -1 : std::string(env) == "gemm8" ? 1 : std::string(env) == "lt" ? 0 : -1;
   if (forced >= 0) return forced ? run_g8() : run_lt();
-  if (gemm8_all()) return run_g8();
+  if (deterministic() || gemm8_all()) return run_g8();
   return run_lt();
 }
 

@@ -187,7 +187,8 @@ void AdamW::prepare_delayed() {
   pending_dev.fill_(1.0);
 }
 
-void AdamW::apply_delayed(int64_t off, int64_t len, void* m_dev, void* v_dev, bool moments_bf16, hipStream_t s) {
+void AdamW::apply_delayed(int64_t off, int64_t len, void* m_dev, void* v_dev, bool moments_bf16, hipStream_t s,
+                          int max_grid) {
   MFT_CHECK(pending_dev.defined() && !vmax.defined(), "AdamW::apply_delayed: prepare_delayed first (no AMSGrad)");
   ::mft::AdamWArgs a = args();
   a.lr_ptr = lr_step_dev.data<float>();
@@ -200,6 +201,7 @@ void AdamW::apply_delayed(int64_t off, int64_t len, void* m_dev, void* v_dev, bo
   a.n = len;
   a.shadow = (::mft::bf16_t*)flat_.shadow.data_ptr() + off;
   a.sr_offset = off;
+  a.max_grid = max_grid;
   ::mft::adamw_step(a, s);
 }
 

@@ -63,7 +63,8 @@ class AdamW {
   // apply_delayed() then updates one flat range [off, off + len) with moments staged on the device
   // (gated on the pending flag); commit_delayed() advances the step count and clears the flag.
   void prepare_delayed();
-  void apply_delayed(int64_t off, int64_t len, void* m_dev, void* v_dev, bool moments_bf16, hipStream_t s);
+  void apply_delayed(int64_t off, int64_t len, void* m_dev, void* v_dev, bool moments_bf16, hipStream_t s,
+                     int max_grid = 0);
   void commit_delayed(hipStream_t s);
   Tensor pending_dev, lr_step_dev;  // delayed mode: gradients pending (int32), their lr
   float grad_norm() const;  // host sync

@@ -106,9 +106,12 @@ void Trainer::capture() {
   // optimizer out of the graph (then run eagerly after each replay, buckets not overlapped)
   if (graph_comm_) eager_step();
   else fwd_bwd();
+  if (std::getenv("MFT_Z3_TRACE")) std::fprintf(stderr, "[trainer] ending capture\n");
   HIP_OK(hipStreamEndCapture(stream_, &graph_));
   CachingAllocator::set_current_pool(0);
+  if (std::getenv("MFT_Z3_TRACE")) std::fprintf(stderr, "[trainer] captured; instantiating\n");
   HIP_OK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+  if (std::getenv("MFT_Z3_TRACE")) std::fprintf(stderr, "[trainer] instantiated\n");
 }
 
 Tensor Trainer::step(const std::vector<std::pair<const int64_t*, const int64_t*>>& micro) {

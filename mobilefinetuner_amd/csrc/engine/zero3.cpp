@@ -2,6 +2,8 @@
 #include "engine/zero3.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <sstream>
 
 #include "engine/autograd.h"
@@ -138,13 +140,11 @@ Zero3::Zero3(const std::vector<NamedParams>& units, const NamedParams& rep, Comm
 }
 
 Zero3::~Zero3() {
-  for (hipStream_t s : {h2d_, d2h_, ostream_})
-    if (s) {
-      (void)hipStreamSynchronize(s);
-      (void)hipStreamDestroy(s);
-    }
-  for (auto* v : {&h2d_ev_, &upd_ev_, &d2h_ev_})
-    for (auto& e : *v) (void)hipEventDestroy(e);
+  if (ostream_) {
+    (void)hipStreamSynchronize(ostream_);
+    (void)hipStreamDestroy(ostream_);
+  }
+  for (auto& e : upd_ev_) (void)hipEventDestroy(e);
   if (fork_ev_) (void)hipEventDestroy(fork_ev_);
   if (ojoin_ev_) (void)hipEventDestroy(ojoin_ev_);
   if (stream_) (void)hipStreamSynchronize(stream_);
@@ -165,7 +165,7 @@ std::string Zero3::describe() const {
   return os.str();
 }
 
-void Zero3::shard_optimizer(AdamW& opt, bool host_moments, bool host_fp32, bool streamed, int slots) {
+void Zero3::shard_optimizer(AdamW& opt, bool host_moments, bool host_fp32, bool streamed) {
   std::vector<OptSegment> segs{OptSegment{0, rep_off_, 0, false}};
   if (rep_n_ > 0) segs.push_back(OptSegment{rep_off_, rep_n_, rep_off_, true});
   opt.shard(segs, &comm_, host_moments, host_fp32);
@@ -173,105 +173,90 @@ void Zero3::shard_optimizer(AdamW& opt, bool host_moments, bool host_fp32, bool 
   MFT_CHECK(!opt.config().amsgrad, "Zero3: the host-streamed optimizer has no AMSGrad state");
   sopt_ = &opt;
   sfp32_ = host_fp32;
-  nslot_ = std::max(2, slots);
-  int64_t mx = std::max<int64_t>(rep_n_, kAlign);
-  for (auto& un : units_) mx = std::max(mx, un.s);
-  const DType md = host_fp32 ? DType::F32 : DType::BF16;
-  for (int k = 0; k < nslot_; ++k) {
-    mslot_.push_back(zeros({mx}, md));
-    vslot_.push_back(zeros({mx}, md));
-  }
   const int nupd = 1 + (int)units_.size();
-  sh2d_.assign(nupd, 0);
   supd_.assign(nupd, 0);
-  h2d_ev_.resize(nupd);
   upd_ev_.resize(nupd);
-  for (auto& e : h2d_ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto& e : upd_ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  d2h_ev_.resize(nslot_);
-  for (auto& e : d2h_ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  d2h_live_.assign(nslot_, 0);
   HIP_OK(hipEventCreateWithFlags(&fork_ev_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ojoin_ev_, hipEventDisableTiming));
-  HIP_OK(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking));
-  HIP_OK(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
-  HIP_OK(hipStreamCreateWithFlags(&ostream_, hipStreamNonBlocking));
+  // the updates run beside the forward's kernels: a low-priority stream and a bounded grid (the
+  // kernel waits on PCIe, not on the CU)
+  const char* pr = std::getenv("MFT_Z3_OPT_PRIO");
+  if (!(pr && pr[0] == '0')) {
+    int least = 0, greatest = 0;
+    HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_OK(hipStreamCreateWithPriority(&ostream_, hipStreamNonBlocking, least));
+  } else {
+    HIP_OK(hipStreamCreateWithFlags(&ostream_, hipStreamNonBlocking));
+  }
+  const char* gr = std::getenv("MFT_Z3_OPT_GRID");
+  opt_grid_ = gr ? std::atoi(gr) : 32;  // profiles/r4_offload_modes.txt: 32 best of 16-2048
 }
 
 // ---------------------------------------------------------------- host-streamed optimizer
+// MFT_Z3_TRACE=1: one stderr line per streamed-optimizer call (locating a failure without a debugger)
+static bool z3_trace() {
+  static const bool on = [] {
+    const char* e = std::getenv("MFT_Z3_TRACE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+#define Z3_TRACE(...)                            \
+  do {                                           \
+    if (z3_trace()) {                            \
+      std::fprintf(stderr, "[z3] " __VA_ARGS__); \
+      std::fflush(stderr);                       \
+    }                                            \
+  } while (0)
+
 void Zero3::opt_fork() {
   if (forked_) return;
   forked_ = true;
   HIP_OK(hipEventRecord(fork_ev_, current_stream()));
-  for (hipStream_t s : {h2d_, d2h_, ostream_}) HIP_OK(hipStreamWaitEvent(s, fork_ev_, 0));
+  HIP_OK(hipStreamWaitEvent(ostream_, fork_ev_, 0));
 }
 
-void Zero3::opt_prefetch(int i) {
-  if (i >= (int)sh2d_.size() || sh2d_[i]) return;
-  sh2d_[i] = 1;
-  opt_fork();
-  const int k = i % nslot_;
-  if (d2h_live_[k]) HIP_OK(hipStreamWaitEvent(h2d_, d2h_ev_[k], 0));  // the slot's previous moments are home
-  const int64_t n = upd_len(i);
-  if (n > 0) {
-    const size_t es = sfp32_ ? 4 : 2, off = (size_t)upd_off(i) * es;
-    HIP_OK(hipMemcpyAsync(mslot_[k].data_ptr(), static_cast<char*>(sopt_->m.data_ptr()) + off, (size_t)n * es,
-                          hipMemcpyHostToDevice, h2d_));
-    HIP_OK(hipMemcpyAsync(vslot_[k].data_ptr(), static_cast<char*>(sopt_->v.data_ptr()) + off, (size_t)n * es,
-                          hipMemcpyHostToDevice, h2d_));
-  }
-  HIP_OK(hipEventRecord(h2d_ev_[i], h2d_));
+void Zero3::join_opt_stream() {
+  HIP_OK(hipEventRecord(ojoin_ev_, ostream_));
+  HIP_OK(hipStreamWaitEvent(current_stream(), ojoin_ev_, 0));
 }
 
 void Zero3::opt_update(int i) {
   if (supd_[i]) return;
   supd_[i] = 1;
-  opt_prefetch(i);
-  const int k = i % nslot_;
+  Z3_TRACE("update %d\n", i);
+  opt_fork();
   const int64_t n = upd_len(i);
-  HIP_OK(hipStreamWaitEvent(ostream_, h2d_ev_[i], 0));
-  if (n > 0) sopt_->apply_delayed(upd_off(i), n, mslot_[k].data_ptr(), vslot_[k].data_ptr(), !sfp32_, ostream_);
-  HIP_OK(hipEventRecord(upd_ev_[i], ostream_));
-  HIP_OK(hipStreamWaitEvent(d2h_, upd_ev_[i], 0));
-  if (n > 0) {
+  if (n > 0) {  // the moments of the partition, in place in pinned host DRAM
     const size_t es = sfp32_ ? 4 : 2, off = (size_t)upd_off(i) * es;
-    HIP_OK(hipMemcpyAsync(static_cast<char*>(sopt_->m.data_ptr()) + off, mslot_[k].data_ptr(), (size_t)n * es,
-                          hipMemcpyDeviceToHost, d2h_));
-    HIP_OK(hipMemcpyAsync(static_cast<char*>(sopt_->v.data_ptr()) + off, vslot_[k].data_ptr(), (size_t)n * es,
-                          hipMemcpyDeviceToHost, d2h_));
+    sopt_->apply_delayed(upd_off(i), n, static_cast<char*>(sopt_->m.data_ptr()) + off,
+                         static_cast<char*>(sopt_->v.data_ptr()) + off, !sfp32_, ostream_, opt_grid_);
   }
-  HIP_OK(hipEventRecord(d2h_ev_[k], d2h_));
-  d2h_live_[k] = 1;
+  HIP_OK(hipEventRecord(upd_ev_[i], ostream_));
   bool all = true;
-  for (char c : supd_) all = all && c;
+  for (int c : supd_) all = all && c;
   if (all) sopt_->commit_delayed(ostream_);  // after every update of the step (same stream)
-  opt_prefetch(i + nslot_ - 1);               // into the slot update i - 1 just released
 }
 
 void Zero3::prepare_optimizer() {
   // end of the step's backward (finish() joined every collective): the gradients, their norm and
   // the lr wait in place; the next forward applies them unit by unit
+  Z3_TRACE("prepare\n");
   sopt_->prepare_delayed();
   pending_host_ = true;
-  std::fill(sh2d_.begin(), sh2d_.end(), 0);
   std::fill(supd_.begin(), supd_.end(), 0);
-  std::fill(d2h_live_.begin(), d2h_live_.end(), 0);
   forked_ = false;
 }
 
 void Zero3::flush_optimizer() {
   if (!sopt_ || !pending_host_) return;
   for (int i = 0; i < (int)supd_.size(); ++i) opt_update(i);
-  for (hipStream_t s : {h2d_, d2h_, ostream_}) {
-    HIP_OK(hipEventRecord(ojoin_ev_, s));
-    HIP_OK(hipStreamWaitEvent(current_stream(), ojoin_ev_, 0));
-  }
+  join_opt_stream();
   synchronize();
   pending_host_ = false;
   forked_ = false;
-  std::fill(sh2d_.begin(), sh2d_.end(), 0);
   std::fill(supd_.begin(), supd_.end(), 0);
-  std::fill(d2h_live_.begin(), d2h_live_.end(), 0);
   holder_.assign(holder_.size(), -1);  // every partition changed
 }
 
@@ -328,7 +313,6 @@ void Zero3::zero_grad(FlatParams& flat) {
   // streamed optimizer: the replicated parameters' pending update reads their gradients -- it runs
   // before they are cleared, with the first units' moment prefetches behind it
   if (sopt_ && pending_host_) {
-    for (int i = 0; i < nslot_ - 1; ++i) opt_prefetch(i);
     opt_update(0);
     HIP_OK(hipStreamWaitEvent(current_stream(), upd_ev_[0], 0));
   }
@@ -384,14 +368,12 @@ std::pair<Tensor, Tensor> Zero3::gate(const Tensor& x, const Tensor& h, int bloc
 }
 
 void Zero3::finish() {
+  Z3_TRACE("finish (pending %d)\n", (int)pending_host_);
   if (sopt_ && pending_host_) {
-    // every pending update issued (a unit the forward did not gather) and the copy / optimizer
-    // streams joined back: a captured step ends with every stream it forked
+    // every pending update issued (a unit the forward did not gather) and the optimizer stream
+    // joined back: a captured step ends with every stream it forked
     for (int i = 0; i < (int)supd_.size(); ++i) opt_update(i);
-    for (hipStream_t s : {h2d_, d2h_, ostream_}) {
-      HIP_OK(hipEventRecord(ojoin_ev_, s));
-      HIP_OK(hipStreamWaitEvent(current_stream(), ojoin_ev_, 0));
-    }
+    join_opt_stream();
     pending_host_ = false;
   }
   for (size_t u = 0; u < units_.size(); ++u) reduce_scatter((int)u);  // units no hook completed
@@ -402,6 +384,7 @@ void Zero3::finish() {
   }
   HIP_OK(hipEventRecord(join_, stream_));
   HIP_OK(hipStreamWaitEvent(current_stream(), join_, 0));
+  Z3_TRACE("finish done\n");
 }
 
 void Zero3::materialize() {

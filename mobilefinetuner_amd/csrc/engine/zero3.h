@@ -69,14 +69,13 @@ class Zero3 : public GradReducer, public BlockProvider {
 
   FlatParams& flat() { return flat_; }  // this rank's partitions + the replicated parameters
   // the partitioned AdamW (moments for the local flat; host_moments: in pinned host DRAM, bf16 or
-  // fp32).  streamed (with host_moments): the moments never sit in HBM whole and are never read
-  // over PCIe by the kernel -- each unit's partition is updated right before the next forward
-  // gathers it: its moments are copied host -> device into one of `slots` staging slots on an H2D
-  // copy stream (issued slots - 1 units ahead, so the copies run under the forward's compute), the
-  // fused AdamW runs on its own stream, the moments go back device -> host on a D2H stream and the
-  // unit's all-gather waits only for its own update.  The step's gradients, norm and lr wait in
-  // place from the end of one backward to the next forward (AdamW::prepare_delayed).
-  void shard_optimizer(AdamW& opt, bool host_moments, bool host_fp32 = false, bool streamed = false, int slots = 3);
+  // fp32).  streamed (with host_moments): the update moves out of the step's critical path -- each
+  // unit's partition is updated right before the next forward gathers it, by the fused AdamW on its
+  // own stream reading and writing that unit's moments in place over PCIe (both directions at once),
+  // under the forward's compute; the unit's all-gather waits only for its own update.  The step's
+  // gradients, norm and lr wait in place from the end of one backward to the next forward
+  // (AdamW::prepare_delayed).
+  void shard_optimizer(AdamW& opt, bool host_moments, bool host_fp32 = false, bool streamed = false);
 
   // GradReducer
   void begin_micro(int i, int n) override;
@@ -130,19 +129,21 @@ class Zero3 : public GradReducer, public BlockProvider {
   // update index i: 0 = the replicated parameters, 1 + u = unit u (forward order)
   int64_t upd_off(int i) const { return i == 0 ? rep_off_ : units_[i - 1].local; }
   int64_t upd_len(int i) const { return i == 0 ? rep_n_ : units_[i - 1].s; }
-  void opt_fork();             // the copy / optimizer streams join the current stream's work
-  void opt_prefetch(int i);    // H2D of update i's moments into its slot
-  void opt_update(int i);      // AdamW on update i (after its H2D), then its D2H
+  void opt_fork();             // the optimizer stream joins the current stream's work
+  void opt_update(int i);      // AdamW on update i, moments in place in host DRAM
+  void join_opt_stream();      // the current stream waits for the optimizer stream
   AdamW* sopt_ = nullptr;
   bool sfp32_ = false, pending_host_ = false, forked_ = false;
-  int nslot_ = 0;
-  std::vector<Tensor> mslot_, vslot_;           // device staging of one update's moments
-  std::vector<int> sh2d_, supd_;                // per update: prefetch issued / update issued (this step)
-  std::vector<hipEvent_t> h2d_ev_, upd_ev_;     // per update
-  std::vector<hipEvent_t> d2h_ev_;              // per slot: its moments are back on the host
-  std::vector<char> d2h_live_;
+  std::vector<int> supd_;             // per update: issued this step
+  std::vector<hipEvent_t> upd_ev_;    // per update: applied
   hipEvent_t fork_ev_ = nullptr, ojoin_ev_ = nullptr;
-  hipStream_t h2d_ = nullptr, d2h_ = nullptr, ostream_ = nullptr;
+  // ONE side stream: a staged variant (H2D copy -> update -> D2H copy on three streams, the slot's
+  // next H2D behind its D2H) forms a dependency ring over three side streams, which crashes
+  // hipStreamEndCapture on this ROCm (scripts/diag/r4_capture_probe.hip, profiles/r4_capture_probe.txt),
+  // and with the copies folded onto one stream its two PCIe directions serialise (slower than in place:
+  // profiles/r4_offload_modes.txt).
+  hipStream_t ostream_ = nullptr;
+  int opt_grid_ = 0;  // workgroups per update (MFT_Z3_OPT_GRID)
 };
 
 }  // namespace eng

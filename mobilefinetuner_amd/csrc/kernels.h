@@ -202,6 +202,8 @@ struct AdamWArgs {
   float* vmax;            // AMSGrad: running max of v (fp32 moments only; null = plain Adam(W))
   const int* enable;      // optional device gate: the update runs only when *enable != 0 (a delayed
                           // optimizer's "gradients pending" flag)
+  int max_grid;           // > 0: at most this many workgroups (an update that runs beside compute
+                          // kernels, latency-bound on PCIe, keeps to a few CUs); 0 = fill the chip
 };
 void adamw_step(const AdamWArgs& a, hipStream_t st);
 // after every adamw_step launch of one update: *step += 1 unless the update was skipped (or gated

@@ -7,6 +7,7 @@
 // device memory, so a captured hipGraph of the whole train step replays without host sync.
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -96,6 +97,12 @@ __device__ __forceinline__ void st_mom(void* p, long i, float x, uint32_t r) {
 }
 
 template <bool MB>
+using Mom4 = typename std::conditional<MB, uint2, float4>::type;
+
+// U > 1: each thread keeps U float4 groups in flight (all loads first, then the updates) -- the
+// host-moment launches that run beside the compute kernels on a few CUs are bound by PCIe latency,
+// so their memory-level parallelism has to come from each wave (engine/zero3.cpp)
+template <bool MB, int U>
 __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
   if (a.enable && *a.enable == 0) return;         // delayed optimizer: no gradients pending
   if (adamw_skip(a.nonfinite, a.sumsq)) return;  // skip-step on NaN/Inf grads (fault tolerance)
@@ -113,55 +120,71 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
   const float decay = a.l2_coupled ? 1.f : 1.f - lr * a.weight_decay;
   const long n4 = a.n / 4;
   const uint32_t seed = sr_hash((uint32_t)t * 0x9E3779B9U);
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    float4 p = reinterpret_cast<float4*>(a.p)[i];
-    float4 g = reinterpret_cast<const float4*>(a.g)[i];
-    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w}, mm[4], vv[4];
-    if constexpr (MB) {
-      const uint2 mb = reinterpret_cast<const uint2*>(a.m)[i], vb = reinterpret_cast<const uint2*>(a.v)[i];
-      mm[0] = __uint_as_float(mb.x << 16); mm[1] = __uint_as_float(mb.x & 0xFFFF0000U);
-      mm[2] = __uint_as_float(mb.y << 16); mm[3] = __uint_as_float(mb.y & 0xFFFF0000U);
-      vv[0] = __uint_as_float(vb.x << 16); vv[1] = __uint_as_float(vb.x & 0xFFFF0000U);
-      vv[2] = __uint_as_float(vb.y << 16); vv[3] = __uint_as_float(vb.y & 0xFFFF0000U);
-    } else {
-      const float4 m = reinterpret_cast<const float4*>(a.m)[i], v = reinterpret_cast<const float4*>(a.v)[i];
-      mm[0] = m.x; mm[1] = m.y; mm[2] = m.z; mm[3] = m.w;
-      vv[0] = v.x; vv[1] = v.y; vv[2] = v.z; vv[3] = v.w;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += stride * U) {
+    float4 P[U], G[U];
+    Mom4<MB> M[U], V[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + u * stride;
+      if (i < n4) {
+        P[u] = reinterpret_cast<const float4*>(a.p)[i];
+        G[u] = reinterpret_cast<const float4*>(a.g)[i];
+        M[u] = reinterpret_cast<const Mom4<MB>*>(a.m)[i];
+        V[u] = reinterpret_cast<const Mom4<MB>*>(a.v)[i];
+      }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float gj = gg[j] * clip;
-      if (a.l2_coupled) gj += a.weight_decay * pp[j];
-      mm[j] = a.beta1 * mm[j] + (1.f - a.beta1) * gj;
-      vv[j] = a.beta2 * vv[j] + (1.f - a.beta2) * gj * gj;
-      float vd = vv[j];
-      if (!MB && a.vmax) {  // AMSGrad (torch semantics: the max of the raw second moment, then bias-corrected)
-        vd = fmaxf(a.vmax[4 * i + j], vd);
-        a.vmax[4 * i + j] = vd;
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= n4) break;
+      float pp[4] = {P[u].x, P[u].y, P[u].z, P[u].w}, gg[4] = {G[u].x, G[u].y, G[u].z, G[u].w}, mm[4], vv[4];
+      if constexpr (MB) {
+        const uint2 mb = M[u], vb = V[u];
+        mm[0] = __uint_as_float(mb.x << 16); mm[1] = __uint_as_float(mb.x & 0xFFFF0000U);
+        mm[2] = __uint_as_float(mb.y << 16); mm[3] = __uint_as_float(mb.y & 0xFFFF0000U);
+        vv[0] = __uint_as_float(vb.x << 16); vv[1] = __uint_as_float(vb.x & 0xFFFF0000U);
+        vv[2] = __uint_as_float(vb.y << 16); vv[3] = __uint_as_float(vb.y & 0xFFFF0000U);
+      } else {
+        const float4 m = M[u], v = V[u];
+        mm[0] = m.x; mm[1] = m.y; mm[2] = m.z; mm[3] = m.w;
+        vv[0] = v.x; vv[1] = v.y; vv[2] = v.z; vv[3] = v.w;
       }
-      const float denom = sqrtf(vd) * rbc2 + a.eps;
-      pp[j] = pp[j] * decay - step_size * mm[j] / denom;
-    }
-    reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-    if constexpr (MB) {
-      const uint32_t r = sr_hash(seed ^ (uint32_t)(a.sr_offset / 4 + i)), r2 = sr_hash(r);
-      uint2 mb, vb;
-      mb.x = (uint32_t)f2bf_sr(mm[0], r) | ((uint32_t)f2bf_sr(mm[1], r >> 16) << 16);
-      mb.y = (uint32_t)f2bf_sr(mm[2], r2) | ((uint32_t)f2bf_sr(mm[3], r2 >> 16) << 16);
-      const uint32_t r3 = sr_hash(r2), r4 = sr_hash(r3);
-      vb.x = (uint32_t)f2bf_sr(vv[0], r3) | ((uint32_t)f2bf_sr(vv[1], r3 >> 16) << 16);
-      vb.y = (uint32_t)f2bf_sr(vv[2], r4) | ((uint32_t)f2bf_sr(vv[3], r4 >> 16) << 16);
-      reinterpret_cast<uint2*>(a.m)[i] = mb;
-      reinterpret_cast<uint2*>(a.v)[i] = vb;
-    } else {
-      reinterpret_cast<float4*>(a.m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
-      reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-    }
-    if (a.shadow) {
-      uint2 sh;
-      sh.x = pack_bf2(pp[0], pp[1]);
-      sh.y = pack_bf2(pp[2], pp[3]);
-      reinterpret_cast<uint2*>(a.shadow)[i] = sh;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float gj = gg[j] * clip;
+        if (a.l2_coupled) gj += a.weight_decay * pp[j];
+        mm[j] = a.beta1 * mm[j] + (1.f - a.beta1) * gj;
+        vv[j] = a.beta2 * vv[j] + (1.f - a.beta2) * gj * gj;
+        float vd = vv[j];
+        if (!MB && a.vmax) {  // AMSGrad (torch semantics: the max of the raw second moment, then bias-corrected)
+          vd = fmaxf(a.vmax[4 * i + j], vd);
+          a.vmax[4 * i + j] = vd;
+        }
+        const float denom = sqrtf(vd) * rbc2 + a.eps;
+        pp[j] = pp[j] * decay - step_size * mm[j] / denom;
+      }
+      reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+      if constexpr (MB) {
+        const uint32_t r = sr_hash(seed ^ (uint32_t)(a.sr_offset / 4 + i)), r2 = sr_hash(r);
+        uint2 mb, vb;
+        mb.x = (uint32_t)f2bf_sr(mm[0], r) | ((uint32_t)f2bf_sr(mm[1], r >> 16) << 16);
+        mb.y = (uint32_t)f2bf_sr(mm[2], r2) | ((uint32_t)f2bf_sr(mm[3], r2 >> 16) << 16);
+        const uint32_t r3 = sr_hash(r2), r4 = sr_hash(r3);
+        vb.x = (uint32_t)f2bf_sr(vv[0], r3) | ((uint32_t)f2bf_sr(vv[1], r3 >> 16) << 16);
+        vb.y = (uint32_t)f2bf_sr(vv[2], r4) | ((uint32_t)f2bf_sr(vv[3], r4 >> 16) << 16);
+        reinterpret_cast<uint2*>(a.m)[i] = mb;
+        reinterpret_cast<uint2*>(a.v)[i] = vb;
+      } else {
+        reinterpret_cast<float4*>(a.m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+        reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      }
+      if (a.shadow) {
+        uint2 sh;
+        sh.x = pack_bf2(pp[0], pp[1]);
+        sh.y = pack_bf2(pp[2], pp[3]);
+        reinterpret_cast<uint2*>(a.shadow)[i] = sh;
+      }
     }
   }
   if (blockIdx.x == 0) {
@@ -212,9 +235,22 @@ void adamw_step(const AdamWArgs& a, hipStream_t st) {
   }
   long g = (a.n / 4 + 255) / 256;
   if (g < 1) g = 1;
-  const int grid = (int)(g < 2048 ? g : 2048);
-  if (a.moments_bf16) adamw_kernel<true><<<grid, 256, 0, st>>>(a);
-  else adamw_kernel<false><<<grid, 256, 0, st>>>(a);
+  const long cap = a.max_grid > 0 ? a.max_grid : 2048;
+  const int grid = (int)(g < cap ? g : cap);
+  static const int unroll = [] {  // MFT_OPT_UNROLL=4|8: float4 groups in flight in a bounded launch
+    const char* e = std::getenv("MFT_OPT_UNROLL");
+    return e && std::atoi(e) == 8 ? 8 : 4;
+  }();
+  if (a.max_grid > 0 && unroll == 8) {
+    if (a.moments_bf16) adamw_kernel<true, 8><<<grid, 256, 0, st>>>(a);
+    else adamw_kernel<false, 8><<<grid, 256, 0, st>>>(a);
+  } else if (a.max_grid > 0) {  // a bounded launch beside other kernels: more loads in flight per thread
+    if (a.moments_bf16) adamw_kernel<true, 4><<<grid, 256, 0, st>>>(a);
+    else adamw_kernel<false, 4><<<grid, 256, 0, st>>>(a);
+  } else {
+    if (a.moments_bf16) adamw_kernel<true, 1><<<grid, 256, 0, st>>>(a);
+    else adamw_kernel<false, 1><<<grid, 256, 0, st>>>(a);
+  }
 }
 
 }  // namespace mft

@@ -275,5 +275,7 @@ def test_native_gemma_embedding_dump_and_token_preview(tmp_path):
     w = st.load_file(os.path.join(tmp, "model.safetensors"))["model.embed_tokens.weight"].float()
     table = (w * math.sqrt(h)).bfloat16().float()
     rows = torch.from_numpy(e.reshape(-1, h))
+    # nearest table row within bf16 rounding (a last-bit difference in a few of the H elements, e.g.
+    # the sqrt(H) normaliser rounded differently); any other row is orders of magnitude further away
     d = torch.cdist(rows, table).min(dim=1).values
-    assert d.max().item() < 1e-3 * max(1.0, table.abs().max().item()), d.max()
+    assert d.max().item() < 5e-3 * table.norm(dim=1).max().item(), d.max()

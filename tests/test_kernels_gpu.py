@@ -666,6 +666,7 @@ def test_gated_row_pair_grid_stride():
 def test_adamw_amsgrad_matches_torch():
     """AMSGrad (reference optim/adam.cpp:52,78): the fused kernel with a vmax buffer == torch.optim.AdamW(amsgrad=True)
     over 6 steps (decoupled weight decay, fp32 moments)."""
+    from mobilefinetuner_amd._ext import native
     C = native()
     torch.manual_seed(0)
     n = 4099  # tail path too
