@@ -289,7 +289,7 @@ void lm_head_ce(Tensor h, Tensor W, Tensor labels, int64_t V, c10::optional<Tens
     TORCH_CHECK(dh->size(0) == M && dh->size(1) == K && dh->stride(1) == 1 && dh->stride(0) % 8 == 0, "lm_head_ce: dh [M, K]");
   }
   c10::DeviceGuard g(h.device());
-  auto ws = torch::empty({mft::lm_head_ce_ws_floats(M, Vpad)}, h.options().dtype(torch::kFloat32));
+  auto ws = torch::empty({mft::lm_head_ce_ws_floats(M, Vpad, dh.has_value() ? K : 0)}, h.options().dtype(torch::kFloat32));
   mft::CeArgs a{};
   a.h = bp(h); a.ldh = h.stride(0);
   a.W = bp(W); a.ldw = W.stride(0);
@@ -661,6 +661,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("xent_fwd_bwd", &xent_fwd_bwd);
   m.def("lm_head_ce", &lm_head_ce);
+  m.def("ce_dgrad_splits", &mft::ce_dgrad_splits, "vocab splits of the LM-head CE dgrad for an M-row chunk");
   m.def("logsoftmax_gather", &logsoftmax_gather);
   m.def("sumsq", &sumsq);
   m.def("nonfinite_check", &nonfinite_check);

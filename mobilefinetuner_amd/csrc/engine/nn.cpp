@@ -799,7 +799,7 @@ Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_
     // fused forward (softmax statistics from the fp32 logits tile, E = exp(logit - tile max)) +
     // per-tile-rescaled NN dgrad; E becomes dlogits in place only when W itself trains
     Tensor E = need ? empty({r, Vp}, DType::BF16, h.device()) : Tensor();
-    Tensor ws = empty({::mft::lm_head_ce_ws_floats((int)r, (int)Vp)}, DType::F32, h.device());
+    Tensor ws = empty({::mft::lm_head_ce_ws_floats((int)r, (int)Vp, (int)C)}, DType::F32, h.device());
     ::mft::CeArgs a{};
     a.h = bp(hi); a.ldh = C;
     a.W = bp(w.c); a.ldw = C;
@@ -837,7 +837,7 @@ Tensor lm_head_token_nll(const Tensor& h, Param& w, const Tensor& labels, int V,
   if (chunk <= 0) chunk = M;
   for (int64_t i = 0; i < M; i += chunk) {
     const int64_t r = std::min(chunk, M - i);
-    Tensor ws = empty({::mft::lm_head_ce_ws_floats((int)r, (int)Vp)}, DType::F32, h.device());
+    Tensor ws = empty({::mft::lm_head_ce_ws_floats((int)r, (int)Vp, 0)}, DType::F32, h.device());
     ::mft::CeArgs a{};  // loss only: no logits are stored
     a.h = bp(hc) + i * hc.size(1); a.ldh = hc.size(1);
     a.W = bp(w.c); a.ldw = w.c.size(1);

@@ -168,9 +168,11 @@ struct CeArgs {
   float extra;
   bf16_t* dh; long lddh;       // [M, K] out (null: no gradient)
   int materialize;             // E := dlogits (for a W gradient by the caller)
-  float* ws;                   // lm_head_ce_ws_floats(M, Vpad) floats
+  float* ws;                   // lm_head_ce_ws_floats(M, Vpad, K) floats
 };
-long lm_head_ce_ws_floats(int M, int Vpad);
+long lm_head_ce_ws_floats(int M, int Vpad, int K);
+// vocab splits of the CE dgrad for an M-row chunk (1 = one pass straight into dh)
+int ce_dgrad_splits(int M, int K, int Vpad);
 void lm_head_ce(const CeArgs& a, hipStream_t st);
 // log-softmax gather: out[m, c] = logits[m, idx[c]] - lse(logits[m])  (MMLU scoring)
 void logsoftmax_gather(const bf16_t* logits, const int64_t* idx, float* out, long M, int V, long ld, int nidx,

@@ -299,10 +299,15 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4
 // dh = fin * acc - wlab * W[label] (B = W stored [Vpad, N]).  Every per-row operand of the lane's
 // 8 rows is loaded before the first store (the stores could alias them, so the compiler would
 // otherwise serialise 16 dependent load chains behind them).
+// Vocab-split form (ksplit > 1, a row chunk too short to fill the CUs with its 256 x 256 output
+// tiles): split s covers whole vocab tiles, applies its own final factor ce_fin[s][row] (the
+// accumulator is relative to its LAST tile's max), only split 0 subtracts the label row, and the
+// result goes to the fp32 slab ws[s][M][N] reduced in split order by ce_split_reduce.
 __device__ __forceinline__ void epilogue_ce_dgrad(const GemmArgs& g, f32x4_t (&acc)[4][4][2], int m0, int n0, int wm,
-                                                  int wn, int lane) {
+                                                  int wn, int lane, int split) {
   const int g4 = lane >> 4;
   const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
+  const bool slab = g.ksplit > 1;
   float fin[2][4], wl[2][4];
   long lab[2][4];
 #pragma unroll
@@ -310,8 +315,8 @@ __device__ __forceinline__ void epilogue_ce_dgrad(const GemmArgs& g, f32x4_t (&a
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rr = min(m0 + qa * 128 + wm * 64 + i * 16 + (lane & 15), g.M - 1);
-      fin[qa][i] = g.ce_fin[rr];
-      wl[qa][i] = g.ce_wlab[rr];
+      fin[qa][i] = g.ce_fin[(long)split * g.M + rr];
+      wl[qa][i] = split == 0 ? g.ce_wlab[rr] : 0.f;
       lab[qa][i] = g.ce_labels[rr];
     }
 #pragma unroll
@@ -345,7 +350,15 @@ __device__ __forceinline__ void epilogue_ce_dgrad(const GemmArgs& g, f32x4_t (&a
         const int row = m0 + qa * 128 + wm * 64 + i * 16 + (lane & 15);
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[i][e] = o[i][e] * fin[qa][i] - wl[qa][i] * bf2f(wv[h][i][e]);
-        if (col < g.N && row < g.M) store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, o[i]);
+        if (col < g.N && row < g.M) {
+          if (slab) {
+            float* P = g.ws + ((long)split * g.M + row) * g.N + col;
+            *reinterpret_cast<f32x4_t*>(P) = f32x4_t{o[i][0], o[i][1], o[i][2], o[i][3]};
+            *reinterpret_cast<f32x4_t*>(P + 4) = f32x4_t{o[i][4], o[i][5], o[i][6], o[i][7]};
+          } else {
+            store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, o[i]);
+          }
+        }
       }
     }
   }
@@ -719,10 +732,10 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   float* const rslot = reinterpret_cast<float*>(smem + 8 * kHalf);
   auto ce_dma = [&](int kt) {
     if constexpr (EPI == GEMM_EPI_CE_DGRAD) {
-      const int tt = kt / 4 + 1;
+      const int tt = kt / 4 + 1;  // local vocab tile of this split (kbase is a whole number of tiles)
       if ((kt & 3) == 0 && tt * 4 < nk && w == 0) {
         const long mpad = (long)((g.M + 255) / 256) * 256;
-        glds16_8(g.ce_ratio + (long)tt * mpad + m0 + lane * 4, rslot + (tt & 1) * 256);
+        glds16_8(g.ce_ratio + (long)(kbase / 4 + tt) * mpad + m0 + lane * 4, rslot + (tt & 1) * 256);
       }
     }
   };
@@ -890,7 +903,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     if constexpr (LDSEPI) raw_barrier();  // every wave's tail LDS-DMA retired before the image overwrites LDS
     epilogue_ce_fwd<LDSEPI>(g, acc, m0, n0, wm, wn, lane, reinterpret_cast<float*>(smem));
   }
-  else if constexpr (EPI == GEMM_EPI_CE_DGRAD) epilogue_ce_dgrad(g, acc, m0, n0, wm, wn, lane);
+  else if constexpr (EPI == GEMM_EPI_CE_DGRAD) epilogue_ce_dgrad(g, acc, m0, n0, wm, wn, lane, split);
   else if constexpr (LDSEPI && (EPI == GEMM_EPI_NONE || EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU_D ||
                                  EPI == GEMM_EPI_DGELU || EPI == GEMM_EPI_MUL_AUX)) {
     raw_barrier();  // every wave's tail LDS-DMA retired (vm_wait<0> above) before the tile overwrites LDS
@@ -1559,8 +1572,10 @@ void gemm8x(const GemmArgs& g0, int epi, bool a_t, bool b_t, hipStream_t st) {
       launch8<GEMM_EPI_CE_FWD, false, false>(g, st);
       break;
     case GEMM_EPI_CE_DGRAD:  // NN only (dh = dlogits W, W stored [V, N])
-      if (a_t || !b_t || g.ksplit > 1 || !g.ce_labels || !g.ce_ratio || !g.ce_fin || !g.ce_wlab) {
-        fprintf(stderr, "mft::gemm8: CE dgrad needs the NN layout and ratio/fin/wlab/labels\n");
+      if (a_t || !b_t || !g.ce_labels || !g.ce_ratio || !g.ce_fin || !g.ce_wlab ||
+          (g.ksplit > 1 && (!g.ws || ((g.K / 64 + g.ksplit - 1) / g.ksplit) % 4 != 0))) {
+        fprintf(stderr, "mft::gemm8: CE dgrad needs the NN layout, ratio/fin/wlab/labels, and for a vocab split a "
+                        "slab workspace and whole vocab tiles per split\n");
         abort();
       }
       launch8<GEMM_EPI_CE_DGRAD, false, true>(g, st);

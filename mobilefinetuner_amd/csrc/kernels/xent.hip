@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void ce_finalize_kernel(const float2* __restri
                                                           long mpad, const float* __restrict__ scale, float extra,
                                                           float* __restrict__ loss, float* __restrict__ lse_out,
                                                           float* __restrict__ ratio, float* __restrict__ fin,
-                                                          float* __restrict__ wlab) {
+                                                          float* __restrict__ wlab, int nsplit, int tps) {
   __shared__ float s_mx[64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r0 = blockIdx.x * 64;
@@ -196,18 +196,23 @@ __global__ __launch_bounds__(256) void ce_finalize_kernel(const float2* __restri
       if (v.y > 0.f) s += v.y * __expf(v.x - m);
     }
     s = wave_sum(s);
+    // (every lane holds the butterfly-reduced m and s)
+    const float l = m + __logf(s);
+    const int64_t lab = labels[R];
+    const bool valid = lab >= 0 && lab < V;
+    const float wv = valid ? (scale ? *scale : 1.f) * extra : 0.f;
     if (lane == 0) {
-      const float l = m + __logf(s);
-      const int64_t lab = labels[R];
-      const bool valid = lab >= 0 && lab < V;
       loss[R] = valid ? l - lbl[R] : 0.f;
       if (lse_out) lse_out[R] = l;
-      if (fin) {
-        const float wv = valid ? (scale ? *scale : 1.f) * extra : 0.f;
-        wlab[R] = wv;
-        fin[R] = wv * __expf(fmaxf(st[T - 1].x, m - 60.f) - l);
-      }
       s_mx[rr] = m;
+      if (fin) wlab[R] = wv;
+    }
+    // the dgrad's final factor per vocab split: relative to the split's last tile's (clamped) max
+    if (fin) {
+      for (int sp = lane; sp < nsplit; sp += 64) {
+        const int te = min((sp + 1) * tps, T) - 1;
+        fin[(long)sp * M + R] = wv * __expf(fmaxf(st[te].x, m - 60.f) - l);
+      }
     }
   }
   if (!ratio) return;
@@ -257,23 +262,106 @@ __global__ __launch_bounds__(256) void ce_materialize_kernel(bf16_t* __restrict_
   }
 }
 
-long lm_head_ce_ws_floats(int M, int Vpad) {
+// dh[row, col] = sum_s slab[s][row][col] in split order (deterministic), bf16 out; 8 columns per thread
+__global__ __launch_bounds__(256) void ce_split_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
+                                                              bf16_t* __restrict__ dh, long lddh) {
+  const long i8 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  const long MN = (long)M * N;
+  if (i8 >= MN) return;
+  f32x4_t a = *reinterpret_cast<const f32x4_t*>(ws + i8), b = *reinterpret_cast<const f32x4_t*>(ws + i8 + 4);
+  for (int sp = 1; sp < S; ++sp) {
+    a += *reinterpret_cast<const f32x4_t*>(ws + (long)sp * MN + i8);
+    b += *reinterpret_cast<const f32x4_t*>(ws + (long)sp * MN + i8 + 4);
+  }
+  const long row = i8 / N, col = i8 % N;
+  const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  store8(dh + row * lddh + col, v);
+}
+
+static int ce_num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    MFT_HIP_CHECK(hipGetDevice(&dev));
+    MFT_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+// Vocab splits of the CE dgrad.  Its output dh [M, d_model] has only ceil(M / 256) x ceil(d / 256)
+// tiles (Gemma-3 at 8,192 rows: 96 for 256 CUs), so a row chunk alone leaves most CUs idle and
+// bounding the E buffer by small chunks used to cost 17 % (profiles/r3_ce_budget_and_attn_nw_ab.txt).
+// Split the vocab (the dgrad's K) so tiles x splits fills the CUs in as few, as full rounds as
+// possible: time ~ rounds / splits, a split only for a > 5 % gain, >= 16 vocab tiles per split, whole
+// vocab tiles per split (the per-tile rescale chain restarts at a split's first tile with acc = 0).
+// MFT_CE_SPLIT forces a count (1 = off).
+int ce_dgrad_splits(int M, int K, int Vpad) {
+  const int nk = (Vpad + 63) / 64, T = (Vpad + 255) / 256;
+  const int tiles = ((M + 255) / 256) * ((K + 255) / 256);
+  auto ok = [&](int sp) {
+    const int kps = (nk + sp - 1) / sp;
+    return kps % 4 == 0 && (long)(sp - 1) * kps < nk;
+  };
+  if (const char* e = getenv("MFT_CE_SPLIT")) {
+    const int f = atoi(e);
+    if (f >= 1 && f <= 32 && ok(f)) return f;
+  }
+  const int cus = ce_num_cus();
+  int best = 1;
+  double best_t = 1.0 * ((tiles + cus - 1) / cus);
+  for (int sp = 2; sp <= 32 && T / sp >= 16; ++sp) {
+    if (!ok(sp)) continue;
+    const double t = (double)((tiles * sp + cus - 1) / cus) / sp;
+    if (t < best_t * 0.95) {
+      best_t = t;
+      best = sp;
+    }
+  }
+  return best;
+}
+
+namespace {
+struct CeLayout {
+  float *stats, *lbl, *lse, *fin, *wlab, *ratio, *slab;
+  long total;
+};
+// stats [M][T] float2 | lbl [M] | lse [M] | wlab [M] | fin [S][M] | ratio [T][mpad] (256-B aligned:
+// read by 16-B LDS-DMA) | split slabs [S][M][K] fp32 (S > 1)
+CeLayout ce_layout(float* base, int M, int Vpad, int K, int S) {
   const long T = (Vpad + 255) / 256, mpad = (long)((M + 255) / 256) * 256;
-  return 2 * (long)M * T + 4L * M + T * mpad + 64;
+  CeLayout L{};
+  long o = 0;
+  auto take = [&](long n, bool align) {
+    if (align) o = (o + 63) / 64 * 64;
+    float* p = base ? base + o : nullptr;
+    o += n;
+    return p;
+  };
+  L.stats = take(2 * (long)M * T, false);
+  L.lbl = take(M, false);
+  L.lse = take(M, false);
+  L.wlab = take(M, false);
+  L.fin = take((long)S * M, false);
+  L.ratio = take(T * mpad, true);
+  L.slab = S > 1 ? take((long)S * M * K, true) : nullptr;
+  L.total = o + 64;
+  return L;
+}
+}  // namespace
+
+long lm_head_ce_ws_floats(int M, int Vpad, int K) {
+  return ce_layout(nullptr, M, Vpad, K, K > 0 ? ce_dgrad_splits(M, K, Vpad) : 1).total;
 }
 
 void lm_head_ce(const CeArgs& a, hipStream_t st) {
   if (a.M <= 0) return;
   const int T = (a.Vpad + 255) / 256;
   const long mpad = (long)((a.M + 255) / 256) * 256;
-  float* p = a.ws;
-  float* stats = p; p += 2 * (long)a.M * T;
-  float* lbl = p; p += a.M;
-  float* lse = a.lse ? a.lse : p; p += a.M;
-  float* fin = p; p += a.M;
-  float* wlab = p; p += a.M;
-  float* ratio = a.ws + ((p - a.ws + 63) / 64) * 64;  // 256-B aligned: read by 16-B LDS-DMA
   const bool grad = a.dh != nullptr;
+  const int S = grad && !a.materialize ? ce_dgrad_splits(a.M, a.K, a.Vpad) : 1;
+  const CeLayout L = ce_layout(a.ws, a.M, a.Vpad, a.K, S);
+  float* lse = a.lse ? a.lse : L.lse;
   if (grad && !a.E) {
     fprintf(stderr, "mft::lm_head_ce: the gradient needs the E workspace\n");
     abort();
@@ -283,12 +371,14 @@ void lm_head_ce(const CeArgs& a, hipStream_t st) {
   f.B = a.W; f.ldb = a.ldw;
   f.C = a.E; f.ldc = a.lde;
   f.M = a.M; f.N = a.Vpad; f.K = a.K; f.alpha = 1.f;
-  f.ce_labels = a.labels; f.ce_stats = stats; f.ce_lbl = lbl; f.ce_V = a.V;
+  f.ce_labels = a.labels; f.ce_stats = L.stats; f.ce_lbl = L.lbl; f.ce_V = a.V;
   gemm8x(f, GEMM_EPI_CE_FWD, false, false, st);
   const bool fused = grad && !a.materialize;
-  ce_finalize_kernel<<<(a.M + 63) / 64, 256, 0, st>>>(reinterpret_cast<const float2*>(stats), lbl, a.labels, a.M, T,
-                                                       a.V, mpad, a.scale, a.extra, a.loss, lse,
-                                                       fused ? ratio : nullptr, fused ? fin : nullptr, wlab);
+  const int nk = (a.Vpad + 63) / 64, tps = ((nk + S - 1) / S) / 4;
+  ce_finalize_kernel<<<(a.M + 63) / 64, 256, 0, st>>>(reinterpret_cast<const float2*>(L.stats), L.lbl, a.labels, a.M,
+                                                       T, a.V, mpad, a.scale, a.extra, a.loss, lse,
+                                                       fused ? L.ratio : nullptr, fused ? L.fin : nullptr, L.wlab, S,
+                                                       S > 1 ? tps : T);
   if (!grad) return;
   GemmArgs d{};
   d.A = a.E; d.lda = a.lde;
@@ -296,12 +386,20 @@ void lm_head_ce(const CeArgs& a, hipStream_t st) {
   d.C = a.dh; d.ldc = a.lddh;
   d.M = a.M; d.N = a.K; d.K = a.Vpad; d.alpha = 1.f;
   if (a.materialize) {
-    ce_materialize_kernel<<<a.M, 256, 0, st>>>(a.E, a.lde, a.Vpad, reinterpret_cast<const float2*>(stats), T, lse,
+    ce_materialize_kernel<<<a.M, 256, 0, st>>>(a.E, a.lde, a.Vpad, reinterpret_cast<const float2*>(L.stats), T, lse,
                                                a.labels, a.V, a.scale, a.extra);
     gemm8x(d, GEMM_EPI_NONE, false, true, st);
   } else {
-    d.ce_labels = a.labels; d.ce_ratio = ratio; d.ce_fin = fin; d.ce_wlab = wlab;
+    d.ce_labels = a.labels; d.ce_ratio = L.ratio; d.ce_fin = L.fin; d.ce_wlab = L.wlab;
+    if (S > 1) {
+      d.ksplit = S;
+      d.ws = L.slab;
+    }
     gemm8x(d, GEMM_EPI_CE_DGRAD, false, true, st);
+    if (S > 1) {
+      const long n8 = (long)a.M * a.K / 8;
+      ce_split_reduce_kernel<<<(int)((n8 + 255) / 256), 256, 0, st>>>(L.slab, S, a.M, a.K, a.dh, a.lddh);
+    }
   }
 }
 

@@ -91,3 +91,26 @@ def test_lm_head_token_nll_matches_fp32():
     torch.cuda.synchronize()
     assert n.item() == (labels >= 0).sum().item()
     assert abs(nll.item() - ref.item()) < 1e-4 * abs(ref.item()), (nll.item(), ref.item())
+
+
+@pytest.mark.parametrize("M,K,V,Vpad,forced", [(8192, 640, 262144, 262144, "4"), (6000, 768, 50257, 50304, "9")])
+def test_lm_head_ce_vocab_split_dgrad_matches_unsplit(M, K, V, Vpad, forced, monkeypatch):
+    """The vocab-split CE dgrad (fp32 slabs per split, reduced in split order; chosen automatically when a
+    row chunk's dh tiles cannot fill the CUs) against the single-pass dgrad (MFT_CE_SPLIT=1) and fp32."""
+    from mobilefinetuner_amd._ext import native
+    h, W, labels = _case(M, K, V, Vpad, 3.0, seed=7)
+    auto = native().ce_dgrad_splits(M, K, Vpad)
+    assert auto > 1, auto
+    monkeypatch.setenv("MFT_CE_SPLIT", "1")
+    l1, dh1, _ = _fused(h, W, labels, V, materialize=False)
+    monkeypatch.setenv("MFT_CE_SPLIT", forced)
+    l2, dh2, _ = _fused(h, W, labels, V, materialize=False)
+    monkeypatch.delenv("MFT_CE_SPLIT")
+    l3, dh3, _ = _fused(h, W, labels, V, materialize=False)
+    _, ref_dh, _ = _ref(h, W, labels, V)
+    torch.cuda.synchronize()
+    assert l1.item() == l2.item() == l3.item()
+    for dh in (dh1, dh2, dh3):
+        assert ((dh.float() - ref_dh).norm() / ref_dh.norm()).item() < 1e-2
+    assert ((dh2.float() - dh1.float()).norm() / dh1.float().norm()).item() < 1e-2
+    assert dh2[labels < 0].abs().max().item() == 0.0
