@@ -523,7 +523,12 @@ int lora_aug_cols(int in_features, const std::vector<LoraAdapter>& ads) {
 }
 
 Tensor lora_fused_a(const std::vector<LoraAdapter>& ads, bool training) {
-  if (ads.empty()) return Tensor();
+  // The norm-fused u = y A^T (norm_fwd_kernel LR > 0: one wave per row, every rank reduced across the
+  // wave and A re-read per row) measured 2-8x the plain norm's time -- Gemma-3 +5.4 ms, GPT-2 +0.9 ms
+  // per step against norm + lora_rowdot (profiles/r4b_norm_lora_regression.txt): opt-in only
+  // (MFT_NORM_LORA=1), the MFMA rowdot pass is the default.
+  static const bool on = std::getenv("MFT_NORM_LORA") && std::getenv("MFT_NORM_LORA")[0] == '1';
+  if (!on || ads.empty()) return Tensor();
   int rt = 0;
   for (auto& a : ads) {
     if (a.dropout > 0.f && training) return Tensor();

@@ -504,6 +504,13 @@ __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc
   auto qcol = [&](int q) { return n0 + ((q == 1 || q == 2) ? 128 : 0) + wn * 32 + cofs; };
   // only the last vocab tile has padding columns: the mask is a uniform branch elsewhere
   const bool full = n0 + 256 <= g.ce_V;
+  const int rl0 = wm * 64 + r16;  // tile row = qa * 128 + rl0 + 16 i
+  // the rows' labels are fetched first: their global-load latency hides under the max reduction
+  long labs[2][4];
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) labs[qa][i] = g.ce_labels[min(m0 + qa * 128 + rl0 + i * 16, g.M - 1)];
   float mt[2][4];
 #pragma unroll
   for (int qa = 0; qa < 2; ++qa)
@@ -526,7 +533,6 @@ __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc
       m = fmaxf(m, xor32_pl(m));
       mt[qa][i] = m;
     }
-  const int rl0 = wm * 64 + r16;  // tile row = qa * 128 + rl0 + 16 i
   if (g4 == 0) {
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa)
@@ -542,11 +548,6 @@ __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc
       mt[qa][i] = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));  // -inf only for an all-padding tile
     }
   lds_barrier();  // red is reused for the sums
-  long labs[2][4];
-#pragma unroll
-  for (int qa = 0; qa < 2; ++qa)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) labs[qa][i] = g.ce_labels[min(m0 + qa * 128 + rl0 + i * 16, g.M - 1)];
   float st[2][4];
 #pragma unroll
   for (int qa = 0; qa < 2; ++qa)

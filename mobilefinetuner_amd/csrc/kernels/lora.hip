@@ -338,9 +338,13 @@ __global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restric
   for (int cb = 0; cb < 16; ++cb) db[cb] = zero4();
   const long mbeg = (long)blockIdx.y * chunk;
   const long mend = min(M, mbeg + chunk);
-  for (long t0 = mbeg + 32 * w; t0 < mend; t0 += 128) {
-    // ---- loads: dy A fragments (2 row blocks x 8 column groups) and this tile's u rows
-    bf16x8_t a[2][8];
+  // The tile's dy fragments are dead once the v MFMAs and the LDS image have consumed them, so the
+  // NEXT tile's loads are issued into the same registers right there: they stream in under this
+  // tile's dB MFMAs / transposed reads / v stores (no extra VGPRs; the loads used to start only after
+  // the whole tile was done).
+  bf16x8_t a[2][8];
+  u16x8_t ur;
+  auto load_tile = [&](long t0) {
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
       const long m = t0 + 16 * rb + c16;
@@ -352,8 +356,11 @@ __global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restric
         a[rb][cg] = (rok && n < N) ? *reinterpret_cast<const bf16x8_t*>(rowp + n) : bf16x8_t{};
       }
     }
-    u16x8_t ur{0, 0, 0, 0, 0, 0, 0, 0};
+    ur = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
     if (lane < 32 && t0 + lane < mend) ur = *reinterpret_cast<const u16x8_t*>(u + (t0 + lane) * ldu);
+  };
+  if (mbeg + 32 * w < mend) load_tile(mbeg + 32 * w);
+  for (long t0 = mbeg + 32 * w; t0 < mend; t0 += 128) {
     // ---- v partials: D[row][rank] += dy[row][32 cols] . B^T[32 cols][rank]
     f32x4_t vacc[2] = {zero4(), zero4()};
 #pragma unroll
@@ -370,6 +377,7 @@ __global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restric
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (t0 + 128 < mend) load_tile(t0 + 128);
     // ---- dB^T tiles: D[rank][16 cols] += u^T[rank][32 rows] . dy[32 rows][16 cols]
     const bf16x8_t ua = frag_tr(uimg, 16, 0, 0);  // lane: u[row 8g + j][rank l&15]
 #pragma unroll
@@ -540,8 +548,10 @@ __global__ __launch_bounds__(256, 2) void lora_xty_kernel(const bf16_t* __restri
     for (int cb = 0; cb < 16; ++cb) acc[nr][cb] = zero4();
   const long mbeg = (long)blockIdx.y * chunk;
   const long mend = min(M, mbeg + chunk);
-  for (long t0 = mbeg + 32 * w; t0 < mend; t0 += 128) {
-    bf16x8_t a[2][8];
+  // as lora_dy: the next tile's X / Y loads go out as soon as this tile sits in LDS
+  bf16x8_t a[2][8];
+  u16x8_t yr[2 * NR];
+  auto load_tile = [&](long t0) {
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
       const long m = t0 + 16 * rb + c16;
@@ -554,12 +564,18 @@ __global__ __launch_bounds__(256, 2) void lora_xty_kernel(const bf16_t* __restri
       }
     }
     // Y rows of the tile: lane < 32 -> row t0 + lane, 8 ranks per 16-B load (zero past R / mend)
-    u16x8_t yr[2 * NR];
 #pragma unroll
     for (int j = 0; j < 2 * NR; ++j) {
       yr[j] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
       if (lane < 32 && t0 + lane < mend && 8 * j < R) yr[j] = *reinterpret_cast<const u16x8_t*>(Y + (t0 + lane) * ldy + 8 * j);
     }
+  };
+  // (the early load needs the 64 fragment VGPRs live across the MFMAs: with NR = 2's 128 accumulators
+  // it spills, so NR = 2 keeps the load at the top of each tile)
+  constexpr bool kEarly = NR == 1;
+  if (kEarly && mbeg + 32 * w < mend) load_tile(mbeg + 32 * w);
+  for (long t0 = mbeg + 32 * w; t0 < mend; t0 += 128) {
+    if (!kEarly) load_tile(t0);
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -572,6 +588,7 @@ __global__ __launch_bounds__(256, 2) void lora_xty_kernel(const bf16_t* __restri
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (kEarly && t0 + 128 < mend) load_tile(t0 + 128);
 #pragma unroll
     for (int nr = 0; nr < NR; ++nr) {
       const bf16x8_t ya = frag_tr(yimg, YL, 0, 16 * nr);  // lane: Y[row 8g + j][rank 16 nr + (l & 15)]

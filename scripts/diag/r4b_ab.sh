@@ -22,4 +22,6 @@ for r in 1 2; do
   run gpt2-lora MFT_CE_BUDGET_GB=32
   run gpt2-lora MFT_CE_BUDGET_GB=4
   run gpt2-lora MFT_CE_BUDGET_GB=32 MFT_GEMM8_STREAM=5
+  run gpt2-lora MFT_CE_BUDGET_GB=32 MFT_GEMM8_ALL=1
+  run gemma3-270m-lora MFT_CE_BUDGET_GB=4 MFT_GEMM8_ALL=1
 done
