@@ -50,7 +50,7 @@ class LanguageModel {
   std::vector<LoraAdapter> no_adapters_;
 };
 
-// rows of the fused LM-head CE per call: one [rows, Vpad] bf16 E workspace within a 32 GiB budget
+// rows of the fused LM-head CE per call: one [rows, Vpad] bf16 E workspace within a 4 GiB budget
 // (MFT_CE_BUDGET_GB; MFT_CE_CHUNK overrides), at most 65536 rows (ops/functional.default_ce_chunk)
 int64_t default_ce_chunk(int vocab_padded);
 

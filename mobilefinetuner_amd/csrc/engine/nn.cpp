@@ -47,8 +47,11 @@ const Tensor& Param::transposed() {
 // ------------------------------------------------------------------ model helpers (lm.h)
 int64_t default_ce_chunk(int vocab_padded) {
   if (const char* env = std::getenv("MFT_CE_CHUNK")) return std::atoll(env);
+  // 4 GiB: with the vocab-split dgrad a short row chunk still fills the CUs, so bounding the E buffer
+  // costs ~1.6 % on Gemma-3 at 256 x 256 (542 vs 551 K tok/s) for 81.5 instead of 139 GB peak HBM
+  // (profiles/r4b_ce_budget_ab.txt; round 3 paid 17 % for the same bound)
   const char* gbs = std::getenv("MFT_CE_BUDGET_GB");
-  const double gb = gbs ? std::atof(gbs) : 32.0;
+  const double gb = gbs ? std::atof(gbs) : 4.0;
   const int64_t rows = (int64_t)(gb * (1ull << 30) / (2.0 * vocab_padded));
   return std::max<int64_t>(64, std::min<int64_t>(65536, rows / 64 * 64));
 }

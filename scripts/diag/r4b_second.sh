@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONPATH=$PWD
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_lm_head_ce_gpu.py \
-  tests/test_lora_dy_gpu.py tests/test_lora_wgrad_gpu.py tests/test_engine_gpu.py tests/test_engine_gemma_gpu.py \
+  tests/test_lora_dy_gpu.py tests/test_lora_wgrad_gpu.py tests/test_kernels_gpu.py tests/test_engine_gpu.py tests/test_engine_gemma_gpu.py \
   > gpurun_out/r4b2_tests.log 2>&1; rc=$?
 tail -3 gpurun_out/r4b2_tests.log
 [ $rc -eq 0 ] || exit 1
