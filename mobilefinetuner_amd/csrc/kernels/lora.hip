@@ -112,67 +112,6 @@ __global__ __launch_bounds__(256) void lora_rowdot_kernel(const bf16_t* __restri
   }
 }
 
-// Row-per-wave form (default): a wave owns 16 whole rows (every k-step of K), so nothing is reduced
-// across waves (no LDS fold, no barrier) and the u tile leaves straight from the accumulator; the
-// X loads of UNR k-steps (one 16-row x 256-column slab: 16 x 512 B) are all issued before the first
-// MFMA consumes one.  The form above splits one 16-row block's K over 4 waves (~5 k-steps each at
-// K = 640), whose short lifetimes left few bytes in flight (Gemma-3: 42-50 us for an 84 MB pass).
-template <int RT>
-__global__ __launch_bounds__(256) void lora_rowdot_w_kernel(const bf16_t* __restrict__ X, long ldx,
-                                                            const bf16_t* __restrict__ Wt, long ldw,
-                                                            bf16_t* __restrict__ U, long ldu, long M, int K, int R,
-                                                            float s, LoraDrop drop) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t dseed = drop.p > 0.f ? drop_seed(drop) : 0u;
-  const long m0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-  if (m0 >= M) return;
-  const long mr = m0 + (lane & 15);
-  const bool row_ok = mr < M;
-  const bf16_t* xr = X + (row_ok ? mr : m0) * ldx + 8 * (lane >> 4);
-  const int nks = K / 32;
-  f32x4_t acc[RT];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) acc[t] = zero4();
-  // two register batches of UNR k-steps: batch j + 1's loads are in flight while batch j is multiplied
-  constexpr int UNR = 8;
-  bf16x8_t a0[UNR], a1[UNR];
-  auto load = [&](bf16x8_t (&a)[UNR], int kb) {
-#pragma unroll
-    for (int u = 0; u < UNR; ++u)
-      a[u] = (kb + u < nks && row_ok) ? *reinterpret_cast<const bf16x8_t*>(xr + (kb + u) * 32) : bf16x8_t{};
-  };
-  auto mult = [&](bf16x8_t (&a)[UNR], int kb) {
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      if (kb + u >= nks) break;
-      const int k = (kb + u) * 32 + 8 * (lane >> 4);
-      if (drop.p > 0.f) a[u] = apply_drop8(a[u], drop, dseed, mr, k, K);
-#pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        const int r = t * 16 + (lane & 15);
-        const bf16x8_t b = r < R ? *reinterpret_cast<const bf16x8_t*>(Wt + (long)r * ldw + k) : bf16x8_t{};
-        acc[t] = mfma16(a[u], b, acc[t]);
-      }
-    }
-  };
-  load(a0, 0);
-  for (int kb = 0; kb < nks; kb += 2 * UNR) {
-    if (kb + UNR < nks) load(a1, kb + UNR);
-    mult(a0, kb);
-    if (kb + UNR >= nks) break;
-    if (kb + 2 * UNR < nks) load(a0, kb + 2 * UNR);
-    mult(a1, kb + UNR);
-  }
-#pragma unroll
-  for (int t = 0; t < RT; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const long m = m0 + 4 * (lane >> 4) + i;
-      const int r = t * 16 + (lane & 15);
-      if (m < M && r < R) U[m * ldu + r] = f2bf(acc[t][i] * s);
-    }
-}
-
 // ------------------------------------------------------------------------------------ update
 // grid (ceil(N/8/blockDim), ceil(M/ROWS)); thread owns 8 columns, W[0..R)[n..n+8) in registers.
 // With dropout (dx += mask * (v A) in backward) the mask of element (m, n) is re-derived.
@@ -549,25 +488,8 @@ __global__ void lora_merge_kernel(T* W, long wsk, long wsn, const float* __restr
   }
 }
 
-// MFT_ROWDOT_V1=1: the split-K-over-waves form (A/B)
-static bool rowdot_v1() {
-  static const int v = [] {
-    const char* e = getenv("MFT_ROWDOT_V1");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  return v == 1;
-}
-
 void lora_rowdot(const bf16_t* X, long ldx, const bf16_t* Wt, long ldw, bf16_t* U, long ldu, long M, int K, int R, float s,
                  LoraDrop drop, hipStream_t st) {
-  if (!rowdot_v1() && K % 32 == 0 && ldx % 8 == 0 && ldw % 8 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0 &&
-      reinterpret_cast<uintptr_t>(Wt) % 16 == 0) {
-    const int gw = (int)cdiv(cdiv(M, 16), 4);
-    if (R <= 16) lora_rowdot_w_kernel<1><<<gw, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);
-    else if (R <= 32) lora_rowdot_w_kernel<2><<<gw, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);
-    else lora_rowdot_w_kernel<4><<<gw, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);
-    return;
-  }
   const int grid = cdiv(M, 16);
   if (R <= 16) lora_rowdot_kernel<1><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);
   else if (R <= 32) lora_rowdot_kernel<2><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);

@@ -58,6 +58,15 @@ def main():
             del os.environ["MFT_CE_SPLIT"]
         if S > 1:
             cases["CE fwd+E+dgrad (split 1)"] = one_split
+
+        def lds_epi(fn):  # gemm8 LDS-staged epilogues (E leaves as whole tile rows): MFT_GEMM8_STREAM=5
+            def run():
+                C.gemm8_set_stream(5)
+                fn()
+                C.gemm8_set_stream(0)
+            return run
+        cases["CE fwd, no E, LDS epi"] = lds_epi(cases["CE fwd, no E (loss only)"])
+        cases[f"CE fwd+E+dgrad, LDS epi"] = lds_epi(cases[f"CE fwd+E+dgrad (auto split {S})"])
         res = {k: [] for k in cases}
         for _ in range(a.rounds):
             for k, fn in cases.items():
@@ -65,7 +74,7 @@ def main():
         print(f"{name}: M={M} K={K} Vpad={Vp}  ({fl / 1e12:.2f} TFLOP per GEMM)", flush=True)
         for k in cases:
             t = min(res[k])
-            nf = 2 if "dgrad (" in k else 1
+            nf = 2 if "+dgrad" in k else 1
             print(f"  {k:34s} {t:9.1f} us  {nf * fl / t / 1e6:6.0f} TF/s", flush=True)
         del h, W, E, dh
         torch.cuda.empty_cache()

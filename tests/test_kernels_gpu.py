@@ -685,3 +685,19 @@ def test_adamw_amsgrad_matches_torch():
     torch.cuda.synchronize()
     assert torch.allclose(p, ref.detach(), rtol=1e-5, atol=1e-6), (p - ref.detach()).abs().max()
     assert torch.allclose(vmax, opt.state[ref]["max_exp_avg_sq"], rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("M,K,R,ldx", [(1000, 640, 8, 704), (77, 768, 32, 768), (4099, 2048, 16, 2112)])
+def test_lora_rowdot_matches_fp32(M, K, R, ldx, monkeypatch):
+    """u = s x A^T on the row-per-wave MFMA kernel (default) against fp32, with X a strided column slice
+    of a wider row (the augmented-K buffer) and ragged row counts."""
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    xbuf = (torch.randn(M, ldx, device=DEV, generator=g) * 0.5).bfloat16()
+    x = xbuf[:, :K]
+    A = (torch.randn(R, K, device=DEV, generator=g) * 0.05).bfloat16()
+    u = torch.empty(M, R, device=DEV, dtype=torch.bfloat16)
+    C.lora_rowdot(x, A, u, 1.5, 0.0, 0, None)
+    ref = 1.5 * x.float() @ A.float().t()
+    _close(u, ref, 0.02, 0.01, msg="rowdot")
