@@ -28,6 +28,7 @@
 #include "engine/autograd.h"
 #include "engine/comm.h"
 #include "engine/dist.h"
+#include "engine/gemm.h"
 #include "engine/optim.h"
 #include "engine/weight_stream.h"
 #include "engine/zero3.h"
@@ -216,7 +217,11 @@ inline DistConfig dist_config_from(const Args& a) {
 
 inline std::unique_ptr<eng::Communicator> comm_from(const DistConfig& d) {
   const char* fc = std::getenv("MFT_DP_FORCE_COMM");
-  return eng::Communicator::from_env((fc && fc[0] == '1') || d.zero_stage > 0);
+  auto c = eng::Communicator::from_env((fc && fc[0] == '1') || d.zero_stage > 0);
+  // ranks must not pick kernels by timing on their own: hipBLASLt takes its heuristic's first algorithm
+  // (the gemm8 / hipBLASLt routing itself is a fixed table)
+  if (c && c->world() > 1) eng::set_lt_autotune(false);
+  return c;
 }
 
 // the flat trainable buffers, bucket-planned when a communicator exists, plus its reducer; or,

@@ -29,6 +29,29 @@ namespace {
 
 constexpr size_t kWorkspace = 32u << 20;
 bool g_det = std::getenv("MFT_DETERMINISTIC") && std::getenv("MFT_DETERMINISTIC")[0] == '1';
+// hipBLASLt algorithm choice: time the heuristic's candidates on the real operands (one process), or
+// take its first pick (MFT_LT_TUNE=0; and by default under a multi-rank communicator, so every rank
+// -- and every rerun -- runs the same algorithm: set_lt_autotune(false) from the app's comm setup)
+int g_lt_tune = [] {
+  const char* e = std::getenv("MFT_LT_TUNE");
+  return e ? (e[0] == '0' ? 0 : 1) : -1;  // -1: not forced
+}();
+bool g_lt_tune_on = g_lt_tune != 0;
+// MFT_GEMM_MAP=1: one line per GEMM shape the first time it is routed (backend, hipBLASLt algorithm
+// index) -- two ranks' maps must be identical
+bool gemm_map() {
+  static const bool v = std::getenv("MFT_GEMM_MAP") && std::getenv("MFT_GEMM_MAP")[0] == '1';
+  return v;
+}
+void map_line(const char* op, long M, long N, long K, const char* backend) {
+  if (!gemm_map()) return;
+  static std::mutex mu;
+  static std::unordered_map<std::string, bool> seen;
+  char b[160];
+  snprintf(b, sizeof(b), "[gemm-map] %s M=%ld N=%ld K=%ld -> %s", op, M, N, K, backend);
+  std::lock_guard<std::mutex> g(mu);
+  if (seen.emplace(b, true).second) std::fprintf(stderr, "%s\n", b);
+}
 
 hipblasLtHandle_t lt_handle() {
   static std::mutex mu;
@@ -112,10 +135,9 @@ Plan& plan_for(const Problem& p, const void* A, const void* B) {
   hipStream_t s = current_stream();
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (s) (void)hipStreamIsCapturing(s, &cap);
-  const char* tune = std::getenv("MFT_LT_TUNE");
-  // (deterministic mode keeps the heuristic's first pick: a timing-based choice can differ between
-  // processes, and different algorithms sum in different orders)
-  if (got > 1 && A && B && cap == hipStreamCaptureStatusNone && !(tune && tune[0] == '0') && !g_det) {
+  // (deterministic mode and multi-rank runs keep the heuristic's first pick: a timing-based choice
+  // can differ between processes, and different algorithms sum in different orders)
+  if (got > 1 && A && B && cap == hipStreamCaptureStatusNone && g_lt_tune_on && !g_det) {
     auto& al = CachingAllocator::get(p.dev);
     size_t wmax = 1;
     for (int i = 0; i < got; ++i) wmax = std::max(wmax, (size_t)res[i].workspaceSize);
@@ -152,6 +174,9 @@ Plan& plan_for(const Problem& p, const void* A, const void* B) {
   }
   pl.algo = res[best].algo;
   pl.ws = res[best].workspaceSize;
+  if (gemm_map())
+    std::fprintf(stderr, "[gemm-map] hipBLASLt m=%ld n=%ld k=%ld ta=%d tb=%d epi=%d -> algorithm %d of %d (%s)\n", p.m, p.n,
+                 p.k, p.ta, p.tb, p.epi, best, got, (g_lt_tune_on && !g_det) ? "timed" : "heuristic first");
   return plans.emplace(key, pl).first->second;
 }
 
@@ -194,6 +219,9 @@ bool gemm8_all() {
   return v == 1;
 }
 bool deterministic() { return g_det; }
+void set_lt_autotune(bool on) {
+  if (g_lt_tune < 0) g_lt_tune_on = on;  // an explicit MFT_LT_TUNE wins
+}
 void set_deterministic(bool on) { g_det = on; }
 
 void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c, const Gemm8Extra& ex) {
@@ -267,9 +295,9 @@ void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y) {
   // (one fixed reduction order whatever the operands' addresses and the library's heuristic pick).
   static const char* env = std::getenv("MFT_NT");
   static const int forced = !env ? -1 : std::string(env) == "gemm8" ? 1 : std::string(env) == "lt" ? 0 : -1;
-  if (forced >= 0) return forced ? run_g8() : run_lt();
-  if (deterministic() || gemm8_all()) return run_g8();
-  return run_lt();
+  const bool g8 = forced >= 0 ? forced == 1 : (deterministic() || gemm8_all());
+  map_line("nt", M, N, K, g8 ? "gemm8" : "hipBLASLt");
+  return g8 ? run_g8() : run_lt();
 }
 
 void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out) {
@@ -294,9 +322,9 @@ void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out) {
   // reduction order is fixed)
   static const char* env = std::getenv("MFT_NN");
   static const int forced = !env ? -1 : std::string(env) == "gemm8" ? 1 : std::string(env) == "lt" ? 0 : -1;
-  if (forced >= 0) return forced ? run_g8() : run_lt();
-  if (deterministic() || gemm8_all()) return run_g8();
-  return run_lt();
+  const bool g8 = forced >= 0 ? forced == 1 : (deterministic() || gemm8_all());
+  map_line("nn", M, K, N, g8 ? "gemm8" : "hipBLASLt");
+  return g8 ? run_g8() : run_lt();
 }
 
 void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
@@ -326,6 +354,7 @@ void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
     g.K = (int)M;
     g.alpha = alpha;
     g.ksplit = ::mft::gemm8_pick_ksplit((int)N, (int)K, (int)M);
+    map_line("wgrad", N, K, M, g.ksplit > 1 ? "gemm8 split-K" : "gemm8");
     void* ws = nullptr;
     auto& al = CachingAllocator::get(cur_dev());
     if (g.ksplit > 1) {
@@ -336,6 +365,7 @@ void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
     if (ws) al.release(ws);
     return;
   }
+  map_line("wgrad", N, K, M, "hipBLASLt");
   // col-major: buf^T [K, N] += x^T [K, M] . dy [M, N]  (beta = 1)
   Problem p;
   p.dev = cur_dev();

@@ -33,6 +33,9 @@ void blas_gemm(const Tensor& a, bool ta, const Tensor& b, bool tb, Tensor& c, fl
 bool gemm8_all();
 bool deterministic();
 void set_deterministic(bool on);
+// hipBLASLt per-shape algorithm autotuning (timing the heuristic's candidates) on / off; multi-rank
+// apps turn it off so every rank runs the same algorithms (an explicit MFT_LT_TUNE overrides)
+void set_lt_autotune(bool on);
 
 }  // namespace eng
 }  // namespace mft

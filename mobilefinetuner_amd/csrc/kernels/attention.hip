@@ -919,6 +919,46 @@ __device__ __forceinline__ bf16x8_t frag_row_pr(const bf16_t* t, int r0, int c0)
   const int l = threadIdx.x & 63;
   return *reinterpret_cast<const bf16x8_t*>(t + (r0 >> 1) * kPairPitch + pr_row(l & 15) + c0 + 8 * (l >> 4));
 }
+// Swizzled pair image (the forward's K and V tiles): the odd row of each piece
+// stores 16-B chunk c at slot c ^ 2 (the DMA writes lane-linear, so the swizzle is on the SOURCE
+// column).  The two rows of a piece then no longer share banks: every 16-lane group of a
+// ds_read_b128 row fragment hits 16 distinct 16-B slots (the plain pair image is 2-way: rows 2k and
+// 2k + 1 sit 512 B apart, SQ_LDS_BANK_CONFLICT 11.5 M cycles on 5.1 M LDS instructions,
+// profiles/r3_attn256_pmc.txt), and the read keeps one lane base + immediates: the XOR only touches
+// bit 1 of the lane-group chunk index (chunk = 4 s2 + g).
+template <int NW>
+__device__ __forceinline__ void dma_tile32_prs(bf16_t* lds, const bf16_t* src, AttnStrides st, int b, int h, int row0,
+                                               int rmax) {
+  static_assert(16 % NW == 0, "every wave issues the same number of DMA pieces");
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = ((lane & 31) ^ ((lane >> 5) << 1)) * 8;
+#pragma unroll
+  for (int k = 0; k < 16 / NW; ++k) {
+    const int o = w + k * NW;
+    const int gr = min(row0 + 2 * o + (lane >> 5), rmax - 1);
+    dma16(src + b * st.sb + (long)gr * st.ss + h * st.sh + col, lds + o * kPairPitch);
+  }
+}
+// frag_row_pr on the swizzled pair image (r0 even: the lane's row parity is l & 1)
+__device__ __forceinline__ bf16x8_t frag_row_prs(const bf16_t* t, int r0, int c0) {
+  const int l = threadIdx.x & 63;
+  return *reinterpret_cast<const bf16x8_t*>(t + (r0 >> 1) * kPairPitch + pr_row(l & 15) + c0 +
+                                            8 * ((l >> 4) ^ ((l & 1) << 1)));
+}
+// frag_tr_pr on the swizzled pair image.  The transposed read's 16-B chunk is 2 n + (p >> 1) for c0 =
+// 16 n, so the odd rows' XOR flips n's low bit: +16 elements for even n, -16 for odd n (n is an
+// immediate of the unrolled loops -- two lane bases, no per-read address math).  Per 32-lane group
+// the 8 rows then hit 8 distinct 32-B units (the plain image puts rows 2k, 2k + 1 on the same one).
+__device__ __forceinline__ bf16x8_t frag_tr_prs(const bf16_t* t, int c0) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const int sw = (q & 1) ? ((c0 & 16) ? -16 : 16) : 0;
+  const bf16_t* a0 = t + pr_row(4 * g + q) + c0 + 4 * p + sw;
+  s16x4_t lo = ds_tr16(a0);
+  s16x4_t hi = ds_tr16(a0 + 8 * kPairPitch);  // row + 16 (same parity)
+  s16x8_t rr = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, rr);
+}
 // frag_tr_perm (mfma.h) on the pair image, rows 0..31
 __device__ __forceinline__ bf16x8_t frag_tr_pr(const bf16_t* t, int c0) {
   const int l = threadIdx.x & 63;
@@ -935,7 +975,7 @@ __device__ __forceinline__ bf16x8_t frag_tr_pr(const bf16_t* t, int c0) {
 // fragment (ds_read_b64_tr_b16) read from LDS feeds TWO MFMAs -- one per 16-query half -- so the
 // workgroup's LDS read bytes per FLOP halve (at D = 256 the 16-row form reads the whole 32 KB
 // K+V stage per wave per 32-key tile: LDS-bandwidth bound), at ~2x the accumulator registers.
-template <int D, int NW, int RPW = 16>
+template <int D, int NW, int RPW = 16, bool SWZ = true>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
     float* __restrict__ lse, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides os, int H, int Hkv, int Sq,
@@ -972,8 +1012,13 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
     const int kb = kstart + min(j, nt - 1) * BK;
     bf16_t* st = smem + (j % RG) * 2 * TILE;
     if constexpr (kPair) {
-      dma_tile32_pr<NW>(st, k, ks, b, hk, kb, kv_len);
-      dma_tile32_pr<NW>(st + TILE, v, vs, b, hk, kb, kv_len);
+      if constexpr (SWZ) {  // swizzled pair images (conflict-free reads)
+        dma_tile32_prs<NW>(st, k, ks, b, hk, kb, kv_len);
+        dma_tile32_prs<NW>(st + TILE, v, vs, b, hk, kb, kv_len);
+      } else {
+        dma_tile32_pr<NW>(st, k, ks, b, hk, kb, kv_len);
+        dma_tile32_pr<NW>(st + TILE, v, vs, b, hk, kb, kv_len);
+      }
     } else {
       dma_tile32<D, NW>(st, k, ks, b, hk, kb, kv_len);
       dma_tile32<D, NW>(st + TILE, v, vs, b, hk, kb, kv_len);
@@ -1008,7 +1053,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
         for (int r = 0; r < R; ++r) st[r][t] = zero4();
 #pragma unroll
         for (int s2 = 0; s2 < D / 32; ++s2) {
-          const bf16x8_t kf = kPair ? frag_row_pr(Ks, 16 * t, s2 * 32) : frag_row_sw<D>(Ks, 16 * t, s2 * 32);
+          const bf16x8_t kf = kPair ? (SWZ ? frag_row_prs(Ks, 16 * t, s2 * 32) : frag_row_pr(Ks, 16 * t, s2 * 32))
+                                   : frag_row_sw<D>(Ks, 16 * t, s2 * 32);
 #pragma unroll
           for (int r = 0; r < R; ++r) st[r][t] = mfma16(kf, qf[r][s2], st[r][t]);
         }
@@ -1061,7 +1107,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
       }
 #pragma unroll
       for (int n = 0; n < D / 16; ++n) {
-        const bf16x8_t vf = kPair ? frag_tr_pr(Vs, n * 16) : frag_tr_perm_sw<D>(Vs, 0, n * 16);
+        const bf16x8_t vf = kPair ? (SWZ ? frag_tr_prs(Vs, n * 16) : frag_tr_pr(Vs, n * 16)) : frag_tr_perm_sw<D>(Vs, 0, n * 16);
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r][n] = mfma16(pa[r], vf, acc[r][n]);
       }
@@ -1427,17 +1473,17 @@ static void fwd_split_launch(const AttnArgs& a, hipStream_t stream) {
       a.causal, a.window, a.kv_lens);
 }
 
-template <int D, int NW, int RPW>
+template <int D, int NW, int RPW, bool SWZ>
 static void fwd_dma_launch_rpw(const AttnArgs& a, hipStream_t stream) {
   const size_t shm = std::max(D == 256 ? sizeof(bf16_t) * 4 * 2 * kPairTile : sizeof(bf16_t) * kRing * 2 * kSplitBK * D,
                               sizeof(bf16_t) * NW * 16 * (D + kSplitPad));
   static bool attr = false;
   if (!attr) {
-    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_dma_kernel<D, NW, RPW>,
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_dma_kernel<D, NW, RPW, SWZ>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  attn_fwd_dma_kernel<D, NW, RPW><<<dim3(cdiv(a.Sq, RPW * NW), a.H, a.B), 64 * NW, shm, stream>>>(
+  attn_fwd_dma_kernel<D, NW, RPW, SWZ><<<dim3(cdiv(a.Sq, RPW * NW), a.H, a.B), 64 * NW, shm, stream>>>(
       a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale,
       a.causal, a.window, a.kv_lens);
 }
@@ -1447,8 +1493,11 @@ static void fwd_dma_launch_rpw(const AttnArgs& a, hipStream_t stream) {
 template <int D>
 static void fwd_dma_launch(const AttnArgs& a, hipStream_t stream) {
   static const int rpw = env_int("MFT_ATTN_RPW", 16);
-  if (rpw == 32) fwd_dma_launch_rpw<D, 4, 32>(a, stream);
-  else fwd_dma_launch_rpw<D, 8, 16>(a, stream);
+  // MFT_ATTN_SWZ=0: the plain (2-way bank-conflicted) K / V pair images, for A/B
+  static const int swz = env_int("MFT_ATTN_SWZ", 1);
+  if (rpw == 32) fwd_dma_launch_rpw<D, 4, 32, true>(a, stream);
+  else if (swz) fwd_dma_launch_rpw<D, 8, 16, true>(a, stream);
+  else fwd_dma_launch_rpw<D, 8, 16, false>(a, stream);
 }
 
 template <int D, int NW>
