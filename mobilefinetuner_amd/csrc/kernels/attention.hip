@@ -1172,6 +1172,7 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
     const int h = hk * G + it / nq, q0 = qstart + (it % nq) * BQ;
     const long rs = ((long)b * H + h) * Sq;
     if constexpr (kDma) {
+      // (plain pair images here: the swizzled transposed reads' second lane base spills this 256-VGPR kernel)
       dma_tile32_pr<NW>(smem + 2 * j * TILE, q, qs, b, h, q0, Sq);  // rows past Sq: clamped, masked below
       dma_tile32_pr<NW>(smem + (2 * j + 1) * TILE, dout, dos, b, h, q0, Sq);
       // row statistics by one 4-byte DMA per wave (every wave the same bytes: uniform vmcnt counts):
@@ -1327,8 +1328,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
   Tile2<D, NT> tl;
   auto load = [&](int kb, int j) {  // start fetching key tile kb into slot j
     if constexpr (kDma) {
-      dma_tile32_pr<NW>(smem + 2 * j * TILE, k, ks, b, hk, kb, kv_len);  // rows past kv_len: clamped, masked
-      dma_tile32_pr<NW>(smem + (2 * j + 1) * TILE, v, vs, b, hk, kb, kv_len);
+      dma_tile32_prs<NW>(smem + 2 * j * TILE, k, ks, b, hk, kb, kv_len);  // rows past kv_len: clamped, masked
+      dma_tile32_prs<NW>(smem + (2 * j + 1) * TILE, v, vs, b, hk, kb, kv_len);
     } else {
       tl.load(k, v, ks, vs, b, hk, kb, min(BK, kv_len - kb));
     }
@@ -1338,11 +1339,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
     else tl.store(smem + 2 * j * TILE, smem + (2 * j + 1) * TILE);
   };
   auto frow = [&](const bf16_t* t, int r0, int c0) {
-    if constexpr (kDma) return frag_row_pr(t, r0, c0);
+    if constexpr (kDma) return frag_row_prs(t, r0, c0);  // swizzled pair images (conflict-free)
     else return frag_row(t, LD, r0, c0);
   };
   auto ftr = [&](const bf16_t* t, int c0) {
-    if constexpr (kDma) return frag_tr_pr(t, c0);
+    if constexpr (kDma) return frag_tr_prs(t, c0);
     else return frag_tr_perm(t, LD, 0, c0);
   };
   if constexpr (kDma) {  // tiles 0 .. PF - 1 (past the end: the last tile again, keeping the counts uniform)
