@@ -662,6 +662,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("xent_fwd_bwd", &xent_fwd_bwd);
   m.def("lm_head_ce", &lm_head_ce);
   m.def("ce_dgrad_splits", &mft::ce_dgrad_splits, "vocab splits of the LM-head CE dgrad for an M-row chunk");
+  m.def("lora_dy_grid_blocks", &mft::lora_dy_grid_blocks, "workgroups of the lora_dy / lora_xty grids");
   m.def("logsoftmax_gather", &logsoftmax_gather);
   m.def("sumsq", &sumsq);
   m.def("nonfinite_check", &nonfinite_check);

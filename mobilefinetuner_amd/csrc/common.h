@@ -82,6 +82,14 @@ __device__ __forceinline__ void store8(bf16_t* p, const float* f) {
   *reinterpret_cast<u16x8_t*>(p) = v;
 }
 
+// store8 with the non-temporal hint (a streaming output nothing re-reads soon: keep it out of the caches)
+__device__ __forceinline__ void store8_nt(bf16_t* p, const float* f) {
+  u16x8_t v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = f2bf(f[j]);
+  __builtin_nontemporal_store(v, reinterpret_cast<u16x8_t*>(p));
+}
+
 // XCD-aware bijective remap of a 1-D block id (CDNA HIP guide §5 "XCD swizzle must be bijective"):
 // consecutive logical tiles land on the same XCD (same L2) instead of being dealt round-robin.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

@@ -246,6 +246,8 @@ long lora_wgrad_ws_floats(long M, int K, int R);
 void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,
              float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st, float* det_ws = nullptr);
 long lora_dy_ws_floats(long M, int N);  // deterministic-mode workspace of lora_dy (det_ws)
+// workgroups of the lora_dy / lora_xty (MFMA) grids for an [M, N] operand: <= 512, one resident round
+long lora_dy_grid_blocks(long M, int N);
 // W[k*wsk + n*wsn] += s * sum_r A[r, k] * B[r, n]   (A [R,K], B [R,N] fp32)
 void lora_merge(void* W, int w_is_bf16, long wsk, long wsn, const float* A, const float* B, int K, int N, int R, float s,
                 hipStream_t st);

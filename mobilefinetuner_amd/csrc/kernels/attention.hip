@@ -959,6 +959,49 @@ __device__ __forceinline__ bf16x8_t frag_tr_prs(const bf16_t* t, int c0) {
   s16x8_t rr = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8_t, rr);
 }
+// Offset pair image (the dK/dV kernel's Q and dO tiles, read by rows AND transposed): the odd row of
+// each piece starts 544 B (not 512 B) into it, i.e. 32 B further round the banks, so both read forms
+// are conflict-free with ONE lane base (a row base + immediates): every 16-lane group of a
+// ds_read_b128 row fragment covers 16 distinct 16-B slots (rows at 4 (r >> 1) + 2 (r & 1) slots), and
+// each 32-lane group of a ds_read_b64_tr_b16 pair covers 8 distinct 32-B units (rows at 2 (r >> 1) +
+// (r & 1)).  The price is two half-wave LDS-DMA instructions per piece (the even row's 32 lanes at the
+// piece, the odd row's at piece + 32 B): the XOR-swizzled image needs a second lane base for the
+// transposed reads, which spills this 256-VGPR kernel.
+__device__ __forceinline__ int pr2_row(int r) { return (r >> 1) * kPairPitch + (r & 1) * 272; }
+template <int NW>
+__device__ __forceinline__ void dma_tile32_pr2(bf16_t* lds, const bf16_t* src, AttnStrides st, int b, int h, int row0,
+                                               int rmax) {
+  static_assert(16 % NW == 0, "every wave issues the same number of DMA pieces");
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int k = 0; k < 16 / NW; ++k) {
+    const int o = w + k * NW;
+    const int gr = min(row0 + 2 * o + (lane >> 5), rmax - 1);
+    const bf16_t* sp = src + b * st.sb + (long)gr * st.ss + h * st.sh + (lane & 31) * 8;
+    // Two half-wave instructions.  The empty asm after the second keeps the branches' tails different:
+    // otherwise hipcc sinks both calls into ONE instruction with a per-lane select of the LDS base and
+    // then takes lane 0's value for M0 -- the odd rows land at +512 B (measured: NaN dK).
+    if (lane < 32) {
+      dma16(sp, lds + o * kPairPitch);
+    } else {
+      dma16(sp, lds + o * kPairPitch + 16);  // lane 32 lands at 512 + 32 B
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+__device__ __forceinline__ bf16x8_t frag_row_pr2(const bf16_t* t, int r0, int c0) {
+  const int l = threadIdx.x & 63;
+  return *reinterpret_cast<const bf16x8_t*>(t + (r0 >> 1) * kPairPitch + pr2_row(l & 15) + c0 + 8 * (l >> 4));
+}
+__device__ __forceinline__ bf16x8_t frag_tr_pr2(const bf16_t* t, int c0) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const bf16_t* a0 = t + pr2_row(4 * g + q) + c0 + 4 * p;
+  s16x4_t lo = ds_tr16(a0);
+  s16x4_t hi = ds_tr16(a0 + 8 * kPairPitch);  // row + 16
+  s16x8_t rr = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, rr);
+}
 // frag_tr_perm (mfma.h) on the pair image, rows 0..31
 __device__ __forceinline__ bf16x8_t frag_tr_pr(const bf16_t* t, int c0) {
   const int l = threadIdx.x & 63;
@@ -1147,7 +1190,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
   constexpr int NT = 64 * NW, BKEY = 16 * NW, BQ = kSplitBK, LD = D + kSplitPad;
   constexpr int TILE = kDma ? kPairTile : BQ * LD;  // elements of one staged [BQ] x D tile
   // DMA: a 3-slot ring, two tiles in flight; register staging: 2 buffers
-  constexpr int RG = kDma ? 3 : 2, OPT = 2 * (16 / NW) + 1;  // slots; DMA ops per wave per tile (+ row stats)
+  // slots; DMA ops per wave per tile (two half-wave ops per offset-pair piece, + the row stats)
+  constexpr int RG = kDma ? 3 : 2, OPT = 2 * 2 * (16 / NW) + 1;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   // slot j: Q at smem + 2 j TILE, dO after it; row floats [j][lse | delta][BQ] after every slot
   float* const rowf = reinterpret_cast<float*>(smem + 2 * RG * TILE);
@@ -1172,9 +1216,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
     const int h = hk * G + it / nq, q0 = qstart + (it % nq) * BQ;
     const long rs = ((long)b * H + h) * Sq;
     if constexpr (kDma) {
-      // (plain pair images here: the swizzled transposed reads' second lane base spills this 256-VGPR kernel)
-      dma_tile32_pr<NW>(smem + 2 * j * TILE, q, qs, b, h, q0, Sq);  // rows past Sq: clamped, masked below
-      dma_tile32_pr<NW>(smem + (2 * j + 1) * TILE, dout, dos, b, h, q0, Sq);
+      dma_tile32_pr2<NW>(smem + 2 * j * TILE, q, qs, b, h, q0, Sq);  // rows past Sq: clamped, masked below
+      dma_tile32_pr2<NW>(smem + (2 * j + 1) * TILE, dout, dos, b, h, q0, Sq);
       // row statistics by one 4-byte DMA per wave (every wave the same bytes: uniform vmcnt counts):
       // lanes 0-31 the tile's lse, lanes 32-63 its delta
       const int r = min(q0 + (lane & 31), Sq - 1);
@@ -1196,11 +1239,11 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
     }
   };
   auto frow = [&](const bf16_t* t, int r0, int c0) {
-    if constexpr (kDma) return frag_row_pr(t, r0, c0);
+    if constexpr (kDma) return frag_row_pr2(t, r0, c0);  // offset pair images (conflict-free)
     else return frag_row(t, LD, r0, c0);
   };
   auto ftr = [&](const bf16_t* t, int c0) {
-    if constexpr (kDma) return frag_tr_pr(t, c0);
+    if constexpr (kDma) return frag_tr_pr2(t, c0);
     else return frag_tr_perm(t, LD, 0, c0);
   };
   if (total > 0) {

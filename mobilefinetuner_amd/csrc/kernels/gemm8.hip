@@ -581,7 +581,9 @@ __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc
           *reinterpret_cast<uint4*>(img + lds_tile_off(rowt, colt >> 3)) =
               uint4{pack_bf2(ov[0], ov[1]), pack_bf2(ov[2], ov[3]), pack_bf2(ov[4], ov[5]), pack_bf2(ov[6], ov[7])};
         } else {
-          if (g.C && rok && c < g.N) store8(reinterpret_cast<bf16_t*>(g.C) + (long)R * g.ldc + c, o[q][i]);
+          // non-temporal: E is re-read only by the dgrad after the whole chunk (GBs later), far beyond
+          // L2 / MALL reach -- streaming stores keep it from evicting the operand tiles
+          if (g.C && rok && c < g.N) store8_nt(reinterpret_cast<bf16_t*>(g.C) + (long)R * g.ldc + c, o[q][i]);
         }
       }
       s += xor16_pl(s);

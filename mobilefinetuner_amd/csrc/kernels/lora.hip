@@ -440,19 +440,21 @@ __global__ void lora_dy_reduce_kernel(const float* __restrict__ ws, int ny, int 
 
 static long dy_chunks(long M, int N, long* chunk_out) {
   const int gx = cdiv(N, 256);
-  // 2 resident blocks per CU (68 KB LDS each): ~512 blocks in total, >= 2 tiles per wave (a 256-column
-  // slice such as Gemma's k / v projections then still fills every CU: 256 row chunks at M = 64k)
-  long ny = cdiv(512, gx);
-  const long max_ny = cdiv(M, 256);
-  if (ny > max_ny) ny = max_ny;
+  // 2 resident blocks per CU (68 KB LDS each): at most 512 blocks, so the whole grid is ONE round.  (The
+  // round-3 sizing, ny = ceil(512 / gx), gave 513 blocks for gx = 3 and 9 -- GPT-2's 768 / 2304 and
+  // Gemma-3's 640-wide strips -- and the 513th block ran alone after the first round.)  Row chunks are
+  // whole 128-row quads (4 waves x 32 rows) split as evenly as the quads allow.
+  long ny = 512 / gx;
+  const long quads = cdiv(M, 128);
+  if (ny > quads) ny = quads;
   if (ny < 1) ny = 1;
-  long chunk = cdiv(M, ny);
-  chunk = cdiv(chunk, 128) * 128;
+  const long chunk = cdiv(quads, ny) * 128;
   if (chunk_out) *chunk_out = chunk;
   return cdiv(M, chunk);
 }
 
 long lora_dy_ws_floats(long M, int N) { return dy_chunks(M, N, nullptr) * 8L * cdiv(N, 256) * 256; }
+long lora_dy_grid_blocks(long M, int N) { return dy_chunks(M, N, nullptr) * cdiv(N, 256); }
 
 void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,
              float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st, float* det_ws) {

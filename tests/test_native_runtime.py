@@ -40,3 +40,17 @@ def test_mfu_counters():
     assert abs(fpt - (4 * 124_439_808 + 2 * 442_368 + 12 * 2 * 128 * 768 * 3)) < 1
     tf, frac = trace.mfu(1e6, fpt)
     assert abs(tf - fpt * 1e6 / 1e12) < 1e-9 and abs(frac - tf / 2500.0) < 1e-12
+
+
+def test_lora_dy_grids_fit_one_round():
+    """lora_dy / lora_xty grids (2 resident 68-KB workgroups per CU on 256 CUs) never exceed one round:
+    round 3 sized GPT-2's 768 / 2304 and Gemma-3's 640-wide operands to 513 workgroups, the last of which
+    ran alone after the first round.  Host-side sizing only (no GPU needed)."""
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    for M, N in [(131072, 2304), (131072, 768), (65536, 640), (65536, 1024), (65536, 2048), (65536, 256),
+                 (512, 2304), (7, 768)]:
+        blocks = C.lora_dy_grid_blocks(M, N)
+        assert 1 <= blocks <= 512, (M, N, blocks)
+        if M >= 65536:
+            assert blocks >= 384, (M, N, blocks)  # still fills most of the 512 slots
