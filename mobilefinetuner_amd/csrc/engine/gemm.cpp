@@ -180,14 +180,16 @@ Plan& plan_for(const Problem& p, const void* A, const void* B) {
   return plans.emplace(key, pl).first->second;
 }
 
-void lt_run(const Problem& p, const void* A, const void* B, void* D, const void* bias, float alpha, float beta) {
+// D = alpha op(A) op(B) (+ bias) + beta C, C = D unless given (same layout)
+void lt_run(const Problem& p, const void* A, const void* B, void* D, const void* bias, float alpha, float beta,
+            const void* C = nullptr) {
   Plan& pl = plan_for(p, A, B);
   if (bias) LT_OK(hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
   void* ws = nullptr;
   auto& al = CachingAllocator::get(p.dev);
   if (pl.ws) ws = al.allocate(pl.ws, current_stream());
-  LT_OK(hipblasLtMatmul(lt_handle(), pl.op, &alpha, A, pl.a, B, pl.b, &beta, D, pl.d, D, pl.d, &pl.algo, ws, pl.ws,
-                        current_stream()));
+  LT_OK(hipblasLtMatmul(lt_handle(), pl.op, &alpha, A, pl.a, B, pl.b, &beta, C ? C : D, pl.d, D, pl.d, &pl.algo, ws,
+                        pl.ws, current_stream()));
   if (ws) al.release(ws);  // stream-ordered reuse
 }
 
@@ -258,16 +260,26 @@ void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c,
 }
 
 
-void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y) {
+void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y, const Tensor& resid) {
   MFT_CHECK(rowmajor2(x2) && rowmajor2(w) && rowmajor2(y) && x2.dtype() == DType::BF16 && w.dtype() == DType::BF16,
             "gemm_nt: bf16 row-major");
   const long M = x2.size(0), K = x2.size(1), N = w.size(0);
   MFT_CHECK(w.size(1) == K && y.size(0) == M && y.size(1) == N, "gemm_nt: shapes ", x2.str(), " ", w.str(), " ",
             y.str());
+  // resid: the residual stream [M, N] added in the epilogue (y = x W^T + b + resid): hipBLASLt's beta = 1
+  // with C = resid, gemm8's BIAS_ADD epilogue -- the residual add never makes its own pass
+  MFT_CHECK(!resid.defined() || (rowmajor2(resid) && resid.dtype() == DType::BF16 && resid.size(0) == M &&
+                                 resid.size(1) == N && resid.stride(0) == y.stride(0) && bias.defined()),
+            "gemm_nt: the fused residual must match y (bf16 [M, N], same row stride) and come with a bias");
   auto run_g8 = [&]() {
     Gemm8Extra ex;
     ex.bias = bias.defined() ? &bias : nullptr;
-    gemm8_call(x2, w, false, bias.defined() ? ::mft::GEMM_EPI_BIAS : ::mft::GEMM_EPI_NONE, y, ex);
+    Tensor r = resid;
+    if (resid.defined()) ex.aux = &r;
+    gemm8_call(x2, w, false,
+               resid.defined() ? ::mft::GEMM_EPI_BIAS_ADD
+                               : bias.defined() ? ::mft::GEMM_EPI_BIAS : ::mft::GEMM_EPI_NONE,
+               y, ex);
   };
   auto run_lt = [&]() {
     // col-major view: y^T [N, M] = W [N, K] . x^T  -> op(A) = T on W (stored K x N col-major)
@@ -283,7 +295,8 @@ void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y) {
     p.lda = w.stride(0);
     p.ldb = x2.stride(0);
     p.ldd = y.stride(0);
-    lt_run(p, w.data_ptr(), x2.data_ptr(), y.data_ptr(), bias.defined() ? bias.data_ptr() : nullptr, 1.f, 0.f);
+    lt_run(p, w.data_ptr(), x2.data_ptr(), y.data_ptr(), bias.defined() ? bias.data_ptr() : nullptr, 1.f,
+           resid.defined() ? 1.f : 0.f, resid.defined() ? resid.data_ptr() : nullptr);
   };
   const bool g8_ok = K % 64 == 0 && N % 8 == 0 && x2.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 &&
                      y.stride(0) % 8 == 0 && ::mft::gemm8_supported((int)M, (int)N, (int)K, false, false);

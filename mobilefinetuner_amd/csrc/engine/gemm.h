@@ -13,7 +13,7 @@ namespace mft {
 namespace eng {
 
 // y[M, N] = x[M, K] . W[N, K]^T (+ bias[N]); bf16; y row-major (may be a row-strided view)
-void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y);
+void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y, const Tensor& resid = Tensor());
 // out[M, K] = dy[M, N] . W[N, K]   (data gradient; out may be a row-strided view)
 void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out);
 // buf[N, K] (fp32) += alpha * dy[M, N]^T . x[M, K]

@@ -467,15 +467,23 @@ std::pair<Tensor, Tensor> GPT2::block(int i, const Tensor& x0, const Tensor& h, 
                                       u_ready);
   Tensor o = attention_packed(qkv.view({B, S, 3, H, D}), 1.f / std::sqrt((float)D), true, 0, aug(active(b.lproj)));
   o = o.view({B * S, o.size(-1)});
+  // The residual adds ride in the producing GEMMs' epilogues where the producer supports it (augmented-K
+  // LoRA projection, the fused GELU MLP): s = x + proj(o) comes out of the projection, and the norm that
+  // follows reads s alone -- one [M, C] read and one write fewer per add than norm(x + delta)
+  const bool fuse_proj = !active(b.lproj).empty() && !st;
   Tensor a = active(b.lproj).empty() ? linear_p(o, b.proj_w, &b.proj_b)
              : st ? lora_linear(o, b.proj_w, &b.proj_b, active(b.lproj), scale, training, dropout_ctr)
-                  : lora_linear_aug(o, C, b.proj_w, &b.proj_b, active(b.lproj), scale, b.waug_proj, training, dropout_ctr);
-  auto r2 = add_norm(x, a, b.ln2_w, &b.ln2_b, cfg_.eps, false, 0.f, 0);
+                  : lora_linear_aug(o, C, b.proj_w, &b.proj_b, active(b.lproj), scale, b.waug_proj, training, dropout_ctr,
+                                    false, x);
+  auto r2 = fuse_proj ? add_norm(a, Tensor(), b.ln2_w, &b.ln2_b, cfg_.eps, false, 0.f, 0, Tensor(), true)
+                      : add_norm(x, a, b.ln2_w, &b.ln2_b, cfg_.eps, false, 0.f, 0);
   x = r2.first;
   // MLP
   Tensor f;
+  bool fuse_mlp = false;
   if (active(b.lfc).empty() && active(b.lfcout).empty()) {
-    f = mlp_gelu(r2.second, b.fc_w, b.fc_b, b.mproj_w, b.mproj_b);
+    f = mlp_gelu(r2.second, b.fc_w, b.fc_b, b.mproj_w, b.mproj_b, x);
+    fuse_mlp = true;
   } else {
     Tensor u = active(b.lfc).empty() ? linear_p(r2.second, b.fc_w, &b.fc_b)
                              : lora_linear(r2.second, b.fc_w, &b.fc_b, active(b.lfc), scale, training, dropout_ctr);
@@ -486,8 +494,9 @@ std::pair<Tensor, Tensor> GPT2::block(int i, const Tensor& x0, const Tensor& h, 
   Param* nw = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_w : &lnf_w_;
   Param* nb = i + 1 < cfg_.n_layer ? &blocks_[i + 1].ln1_b : &lnf_b_;
   const int oc = i + 1 < cfg_.n_layer ? aug(active(blocks_[i + 1].lqkv)) : 0;
-  return add_norm(x, f, *nw, nb, cfg_.eps, false, 0.f, oc,
-                  oc ? lora_fused_a(active(blocks_[i + 1].lqkv), training) : Tensor());
+  const Tensor la = oc ? lora_fused_a(active(blocks_[i + 1].lqkv), training) : Tensor();
+  if (fuse_mlp) return add_norm(f, Tensor(), *nw, nb, cfg_.eps, false, 0.f, oc, la, true);
+  return add_norm(x, f, *nw, nb, cfg_.eps, false, 0.f, oc, la);
 }
 
 Tensor GPT2::hidden(const Tensor& ids) {
@@ -500,9 +509,10 @@ Tensor GPT2::hidden(const Tensor& ids) {
   if (bp) bp->begin_forward();
   Tensor x = embed(ids, wte_, &wpe_, 1.f);
   const int oc0 = (active(blocks_[0].lqkv).empty() || st) ? 0 : lora_aug_cols(C, active(blocks_[0].lqkv));
-  Tensor h = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, oc0,
-                      oc0 ? lora_fused_a(active(blocks_[0].lqkv), training) : Tensor())
-                 .second;
+  // (resid_out: block 0's residual consumers send their gradient through this norm's backward kernel)
+  Tensor h;
+  std::tie(x, h) = add_norm(x, Tensor(), blocks_[0].ln1_w, &blocks_[0].ln1_b, cfg_.eps, false, 0.f, oc0,
+                            oc0 ? lora_fused_a(active(blocks_[0].lqkv), training) : Tensor(), true);
   const bool ckpt = grad_checkpoint && training && grad_enabled();
   for (int i = 0; i < cfg_.n_layer; ++i) {
     if (bp) bp->ensure(i, i + 1);

@@ -87,12 +87,12 @@ struct NormNode : Node {
   Tensor xs, w32, mean, rstd;
   Param* w = nullptr;
   Param* b = nullptr;
-  bool rms = false, has_delta = false;
+  bool rms = false, has_delta = false, has_sout = false;  // has_sout: s is an output (delta or resid_out)
   float offset = 0.f;
   int N = 0;
   std::vector<Tensor> apply(std::vector<Tensor>& g) override {
     // outputs: {s, y}; inputs: {x, delta, w.leaf, b.leaf}
-    Tensor ds = has_delta ? g[0] : Tensor();
+    Tensor ds = has_sout ? g[0] : Tensor();
     Tensor dy = g[1];
     const long M = xs.numel() / N;
     if (!dy.defined()) dy = zeros({M, (int64_t)N}, DType::BF16, xs.device());
@@ -116,7 +116,7 @@ struct NormNode : Node {
 }  // namespace
 
 std::pair<Tensor, Tensor> add_norm(const Tensor& x, const Tensor& delta, Param& w, Param* b, float eps, bool rms,
-                                   float offset, int out_cols, const Tensor& lora_a) {
+                                   float offset, int out_cols, const Tensor& lora_a, bool resid_out) {
   const int N = (int)x.size(-1);
   MFT_CHECK(x.dtype() == DType::BF16 && N % 8 == 0 && N <= 4096, "norm: bf16 rows, width % 8, <= 4096");
   const long M = x.numel() / N;
@@ -148,7 +148,8 @@ std::pair<Tensor, Tensor> add_norm(const Tensor& x, const Tensor& delta, Param& 
   Shape ys = x.shape();
   ys.back() = oc;
   y = y.detach().view(ys);
-  Tensor sv = s.defined() ? s.view(x.shape()) : x;
+  const bool pass = resid_out && !d2.defined();  // s = x, but as this node's output
+  Tensor sv = s.defined() ? s.view(x.shape()) : pass ? x2.view(x.shape()) : x;
   auto n = std::make_shared<NormNode>();
   n->name = rms ? "RMSNormBackward" : "LayerNormBackward";
   n->xs = s.defined() ? s : x2;
@@ -159,12 +160,13 @@ std::pair<Tensor, Tensor> add_norm(const Tensor& x, const Tensor& delta, Param& 
   n->b = b;
   n->rms = rms;
   n->has_delta = d2.defined();
+  n->has_sout = d2.defined() || pass;
   n->offset = offset;
   n->N = N;
-  Tensor s_out = d2.defined() ? sv : Tensor();
+  Tensor s_out = n->has_sout ? sv : Tensor();
   // (grads of trainable w / b land in their flat buffers inside apply())
   connect(n, {x, delta, w.leaf, b ? b->leaf : Tensor()}, {s_out, y});
-  return {d2.defined() ? s_out : x, y};
+  return {n->has_sout ? s_out : x, y};
 }
 
 // ------------------------------------------------------------------ embedding
@@ -475,7 +477,7 @@ Tensor linear_p(const Tensor& x, Param& w, Param* b) {
   return y.view(ys);
 }
 
-Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2) {
+Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2, const Tensor& resid) {
   const int64_t K = x.size(-1), I = w1.c.size(0), N = w2.c.size(0);
   Tensor x2 = x.detach().reshape({-1, K}).contiguous();
   const int64_t M = x2.size(0);
@@ -485,10 +487,12 @@ Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2) {
   ex.aux = &pre;
   gemm8_call(x2, w1.c, false, ::mft::GEMM_EPI_BIAS_GELU_D, h, ex);  // aux = GELU'(pre)
   Tensor y = empty({M, N}, DType::BF16, x.device());
-  gemm_nt(h, w2.c, b2.c, y);
+  // resid: y = resid + MLP(x) straight from the projection's epilogue (the block's residual add)
+  const Tensor r2 = resid.defined() ? resid.detach().reshape({M, N}).contiguous() : Tensor();
+  gemm_nt(h, w2.c, b2.c, y, r2);
   Shape ys = x.shape();
   ys.back() = N;
-  if (any_needs_grad({x, w1.leaf, b1.leaf, w2.leaf, b2.leaf})) {
+  if (any_needs_grad({x, w1.leaf, b1.leaf, w2.leaf, b2.leaf, resid})) {
     Param *p1 = &w1, *q1 = &b1, *p2 = &w2, *q2 = &b2;
     auto n = lambda_node("MLPGeluBackward", [x2, h, pre, p1, q1, p2, q2, M, K, I, N](std::vector<Tensor>& g) {
       if (!g[0].defined()) return std::vector<Tensor>(5);
@@ -511,9 +515,10 @@ Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2) {
       }
       bias_grad(q2, dy2);
       bias_grad(q1, dpre);
-      return std::vector<Tensor>{dx, Tensor(), Tensor(), Tensor(), Tensor()};
+      // the fused residual's gradient is the output's (an identity branch)
+      return std::vector<Tensor>{dx, Tensor(), Tensor(), Tensor(), Tensor(), g[0]};
     });
-    connect(n, {x, w1.leaf, b1.leaf, w2.leaf, b2.leaf}, {y});
+    connect(n, {x, w1.leaf, b1.leaf, w2.leaf, b2.leaf, resid}, {y});
   }
   return y.view(ys);
 }
@@ -547,7 +552,7 @@ Tensor lora_fused_a(const std::vector<LoraAdapter>& ads, bool training) {
 }
 
 Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<LoraAdapter>& ads, float s,
-                       Tensor& waug, bool training, const Tensor& drop_ctr, bool u_ready) {
+                       Tensor& waug, bool training, const Tensor& drop_ctr, bool u_ready, const Tensor& resid) {
   MFT_CHECK(!w.trainable(), "lora_linear_aug: the base weight must be frozen");
   const int64_t Ka = xa.size(-1), N = w.c.size(0);
   Tensor xa2 = xa.detach().reshape({-1, Ka});
@@ -591,7 +596,9 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
     off += R;
   }
   Tensor y = empty({M, N}, DType::BF16, xa.device());
-  gemm_nt(xa2, waug, b ? b->c : Tensor(), y);
+  // resid: y = resid + LoRA-linear(x) straight from the GEMM's epilogue (the block's residual add)
+  const Tensor r2 = resid.defined() ? resid.detach().reshape({M, N}).contiguous() : Tensor();
+  gemm_nt(xa2, waug, b ? b->c : Tensor(), y, r2);
   Shape ys = xa.shape();
   ys.back() = N;
   std::vector<Tensor> ins{xa};
@@ -599,15 +606,18 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
     ins.push_back(a.A.leaf);
     ins.push_back(a.B.leaf);
   }
+  const bool has_resid = resid.defined();
+  if (has_resid) ins.push_back(resid);  // last input: gradient = the output's (identity branch)
   if (any_needs_grad(ins)) {
     Param* pw = &w;
     std::vector<LoraAdapter>* pads = &ads;
     Tensor wa = waug;
     Shape xshape = xa.shape();
     auto n = lambda_node("LoRALinearBackward", [xa2, xshape, K, Ka, M, N, pw, pads, s, wa, training, drop_ctr, acat_f = acat,
-                                                 nin = ins.size()](std::vector<Tensor>& g) {
+                                                 nin = ins.size(), has_resid](std::vector<Tensor>& g) {
       std::vector<Tensor> out(nin);
       if (!g[0].defined()) return out;
+      if (has_resid) out[nin - 1] = g[0];
       auto& ads = *pads;
       Tensor dy2 = g[0].reshape({M, N});
       if (dy2.stride(1) != 1 || dy2.stride(0) % 8) dy2 = dy2.contiguous();

@@ -37,12 +37,17 @@ struct Param {
 // Returns {s, y} (s == x when no delta).
 // lora_a [R, N] (bf16, defined only with out_cols >= N + R): the appended columns receive u = y A^T
 // instead of zeros -- the LoRA consumer's input projection fused into the norm (lora_fused_a).
+// resid_out (no delta): s is returned as an OUTPUT of the norm node (sharing x's storage), so the gradient
+// the residual stream sends back through s is added by the norm backward kernel (its fused dresid input)
+// instead of by a separate accumulation pass -- for an x that a GEMM epilogue already summed with the
+// residual (gemm_nt resid).
 std::pair<Tensor, Tensor> add_norm(const Tensor& x, const Tensor& delta, Param& w, Param* b, float eps, bool rms,
-                                   float offset, int out_cols, const Tensor& lora_a = Tensor());
+                                   float offset, int out_cols, const Tensor& lora_a = Tensor(), bool resid_out = false);
 Tensor embed(const Tensor& ids, Param& wte, Param* wpe, float scale);
 // qkv [B, S, 3, H, D] -> o [B, S, H*D] (or [B, S, out_cols] with zeroed tail when out_cols > H*D)
 Tensor attention_packed(const Tensor& qkv, float scale, bool causal, int window, int out_cols);
-Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2);
+// resid (optional, [..., N]): the returned tensor is resid + MLP(x), added in the projection GEMM's epilogue
+Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2, const Tensor& resid = Tensor());
 // Gemma-3 attention core on the packed q|k|v projection qkv [B, S, nq + 2 nkv, D]: per-head
 // RMSNorm(offset + w) of q and k + RoPE (cos / sin [>= S, D/2] fp32 tables), then causal GQA flash
 // attention (sliding window when window > 0).  O [B, S, nq*D] (or [B, S, out_cols], zeroed tail).
@@ -69,8 +74,11 @@ int lora_aug_cols(int in_features, const std::vector<LoraAdapter>& ads);
 // the caller, W copied once); W frozen.
 // u_ready: the producer already wrote u_1..u_n into xa's appended columns (add_norm with lora_a =
 // lora_fused_a(ads)); the adapters' A must not change between that producer and this call.
+// resid (optional, [..., N]): the returned tensor is resid + the LoRA linear, added in the GEMM's epilogue
+// (needs a bias); its gradient is the output's
 Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<LoraAdapter>& ads, float scale,
-                       Tensor& waug, bool training, const Tensor& drop_ctr, bool u_ready = false);
+                       Tensor& waug, bool training, const Tensor& drop_ctr, bool u_ready = false,
+                       const Tensor& resid = Tensor());
 // the [sum r_i, in] stack of the adapters' A (bf16 compute copies) when a producer can compute u for
 // lora_linear_aug itself (no dropout in effect, sum r <= 32); undefined otherwise
 Tensor lora_fused_a(const std::vector<LoraAdapter>& ads, bool training);

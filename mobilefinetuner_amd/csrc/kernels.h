@@ -67,7 +67,10 @@ enum GemmEpi { GEMM_EPI_NONE = 0, GEMM_EPI_BIAS = 1, GEMM_EPI_BIAS_GELU = 2, GEM
                GEMM_EPI_CE_FWD = 7, GEMM_EPI_CE_DGRAD = 8,
                // GELU MLP (gemm8 only): the forward stores GELU'(pre) -- not pre -- as aux (one
                // sigmoid serves GELU and its derivative), the backward multiplies by it
-               GEMM_EPI_BIAS_GELU_D = 9, GEMM_EPI_MUL_AUX = 10 };
+               GEMM_EPI_BIAS_GELU_D = 9, GEMM_EPI_MUL_AUX = 10,
+               // residual-producing projection (gemm8 only): C = alpha A.B + bias + aux (aux = the
+               // residual stream [M, N]), i.e. the transformer's residual add in the GEMM's epilogue
+               GEMM_EPI_BIAS_ADD = 11 };
 struct GemmArgs {
   const bf16_t* A;
   long lda;  // A [M, K] row-major

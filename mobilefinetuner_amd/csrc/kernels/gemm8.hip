@@ -178,7 +178,7 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4
   const int cofs = (g4 & 1) * 16 + (g4 >> 1) * 8;
   // epilogues that read an [M, N] operand: every load of the lane's 16 pieces is issued before the
   // first store (the stores may alias it, so the compiler would otherwise wait on each load in turn)
-  constexpr bool kAux = EPI == GEMM_EPI_DGELU || EPI == GEMM_EPI_MUL_AUX;
+  constexpr bool kAux = EPI == GEMM_EPI_DGELU || EPI == GEMM_EPI_MUL_AUX || EPI == GEMM_EPI_BIAS_ADD;
   u16x8_t auxv[4][4];
   if constexpr (kAux) {
 #pragma unroll
@@ -199,7 +199,8 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4
     const bool col_ok = col < g.N;
     const int colc = min(col, g.N - 8);
     float bias_v[8];
-    if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU || EPI == GEMM_EPI_BIAS_GELU_D)
+    if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU || EPI == GEMM_EPI_BIAS_GELU_D ||
+                  EPI == GEMM_EPI_BIAS_ADD)
       load8(g.bias + colc, bias_v);
     float o[4][8];
 #pragma unroll
@@ -219,18 +220,21 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[i][e] *= g.alpha;
+      // (ranks in groups of 4: the lane's 4 x 8 slice of lora_w is 16 VGPRs, which keeps the kernel
+      // inside 256 VGPRs with the B0 fragments held across phases (KEEPB))
 #pragma unroll 1
-      for (int t8 = 0; t8 < g.lora_r; t8 += 8) {
-        u16x8_t wv[8];
+      for (int t4 = 0; t4 < g.lora_r; t4 += 4) {
+        u16x8_t wv[4];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) wv[t] = *reinterpret_cast<const u16x8_t*>(g.lora_w + (long)(t8 + t) * g.ld_lw + colc);
+        for (int t = 0; t < 4; ++t) wv[t] = *reinterpret_cast<const u16x8_t*>(g.lora_w + (long)(t4 + t) * g.ld_lw + colc);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = min(rbase + i * 16 + (lane & 15), g.M - 1);
-          float u[8];
-          load8(g.lora_u + (long)row * g.ld_lu + t8, u);
+          const uint2 ur = *reinterpret_cast<const uint2*>(g.lora_u + (long)row * g.ld_lu + t4);
+          const float u[4] = {__uint_as_float(ur.x << 16), __uint_as_float(ur.x & 0xffff0000u),
+                              __uint_as_float(ur.y << 16), __uint_as_float(ur.y & 0xffff0000u)};
 #pragma unroll
-          for (int t = 0; t < 8; ++t)
+          for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[i][e] += u[t] * bf2f(wv[t][e]);
         }
@@ -267,8 +271,10 @@ __device__ __forceinline__ void epilogue8(const GemmArgs& g, f32x4_t (&acc)[4][4
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           v[e] *= g.alpha;
-          if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU || EPI == GEMM_EPI_BIAS_GELU_D)
+          if constexpr (EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU || EPI == GEMM_EPI_BIAS_GELU_D ||
+                        EPI == GEMM_EPI_BIAS_ADD)
             v[e] += bias_v[e];
+          if constexpr (EPI == GEMM_EPI_BIAS_ADD) v[e] += bf2f(auxv[q][i][e]);
         }
       }
       if constexpr (EPI == GEMM_EPI_DGELU) {
@@ -635,10 +641,10 @@ __device__ unsigned long long* g8_stamps;
 // of adding to it: +1-4 % on every NT shape measured (profiles/r3_g8late.txt).  (Reads complete
 // before the phase's MFMAs; the half-tile they read is restaged only after the phase's second
 // barrier, so the order is safe.)  LATE = false keeps the earlier order for A/B runs.
-// KEEPB defaults on where the 16 extra VGPRs fit without spilling (not the TT wgrad form, the LoRA
-// epilogue or the CE dgrad, which spill 2-7 VGPRs with it)
+// KEEPB defaults on where the 16 extra VGPRs fit without spilling (not the TT wgrad form or the CE
+// dgrad, which spill 2-7 VGPRs with it; the LoRA epilogue fits since it walks the ranks 4 at a time)
 template <int EPI, bool AT, bool BT, bool LATE = true,
-          bool KEEPB = !(AT && BT) && EPI != GEMM_EPI_LORA && EPI != GEMM_EPI_CE_DGRAD, bool LDSEPI = false>
+          bool KEEPB = !(AT && BT) && EPI != GEMM_EPI_CE_DGRAD, bool LDSEPI = false>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   if (g.stagger > 0 && blockIdx.x < 256) {  // first round: spread each XCD's CUs over a tile round
@@ -1546,6 +1552,13 @@ void gemm8x(const GemmArgs& g0, int epi, bool a_t, bool b_t, hipStream_t st) {
     case GEMM_EPI_DGELU: launch8_layout<GEMM_EPI_DGELU>(g, a_t, b_t, st); break;
     case GEMM_EPI_BIAS_GELU_D: launch8_layout<GEMM_EPI_BIAS_GELU_D>(g, a_t, b_t, st); break;
     case GEMM_EPI_MUL_AUX: launch8_layout<GEMM_EPI_MUL_AUX>(g, a_t, b_t, st); break;
+    case GEMM_EPI_BIAS_ADD:
+      if (!g.bias || !g.aux) {
+        fprintf(stderr, "mft::gemm8: BIAS_ADD needs the bias and the residual (aux)\n");
+        abort();
+      }
+      launch8_layout<GEMM_EPI_BIAS_ADD>(g, a_t, b_t, st);
+      break;
     case GEMM_EPI_F32ACC:
       // fp32 weight-gradient accumulate: split over K into slabs (g.ws, ksplit * M * N floats) when
       // the output has few tiles, then one deterministic reduce into C; else accumulate in place
