@@ -308,8 +308,12 @@ void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y, c
   // (one fixed reduction order whatever the operands' addresses and the library's heuristic pick).
   static const char* env = std::getenv("MFT_NT");
   static const int forced = !env ? -1 : std::string(env) == "gemm8" ? 1 : std::string(env) == "lt" ? 0 : -1;
-  const bool g8 = forced >= 0 ? forced == 1 : (deterministic() || gemm8_all());
-  map_line("nt", M, N, K, g8 ? "gemm8" : "hipBLASLt");
+  // A residual-producing projection is a standard GEMM with a C input (D = A.B + bias + C, beta = 1), which
+  // hipBLASLt runs natively: 1.611-1.614 M tok/s vs 1.597-1.598 M with gemm8's BIAS_ADD epilogue on the
+  // headline (3 interleaved rounds, profiles/r4b_resid_routing_ab.txt).  MFT_RESID_G8=1 forces gemm8.
+  static const bool resid_g8 = std::getenv("MFT_RESID_G8") && std::getenv("MFT_RESID_G8")[0] == '1';
+  const bool g8 = forced >= 0 ? forced == 1 : (deterministic() || gemm8_all() || (resid.defined() && resid_g8));
+  map_line(resid.defined() ? "nt+resid" : "nt", M, N, K, g8 ? "gemm8" : "hipBLASLt");
   return g8 ? run_g8() : run_lt();
 }
 
