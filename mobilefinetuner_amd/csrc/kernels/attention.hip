@@ -666,6 +666,7 @@ constexpr int kSplitBK = 32;  // rows per staged tile
 // the Gemma-3 shape: conflict cycles -90 %, kernel time only -2..5 % -- the waves spend ~65 % of
 // their cycles in SQ_WAIT_ANY (tile staging latency), not in LDS.
 constexpr int kSplitPad = 16;
+constexpr int kOutPad = 8;  // per-wave output staging rows (store_tile16): D + 8
 
 // LDS writes / reads retired, then a raw s_barrier: unlike __syncthreads (whose fence implies
 // vmcnt(0)) it lets global prefetches issued before it stay in flight
@@ -1025,7 +1026,10 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
     int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
   constexpr int R = RPW / 16;  // 16-query halves per wave
   constexpr bool kPair = D == 256;  // row-pair images (one address base per lane), else XOR swizzle
-  constexpr int BQ = RPW * NW, BK = kSplitBK, TILE = kPair ? kPairTile : BK * D, LDO = D + kSplitPad;
+  // LDO: output staging pitch D + 8 (kOutPad): the four 16-lane groups of the 2-byte staging writes land
+  // 16 banks apart (D + 16 put groups 0 / 2 and 1 / 3 on the same banks: the forward's last 2.1 M
+  // conflict cycles, profiles/r4b_attn256_pmc.txt)
+  constexpr int BQ = RPW * NW, BK = kSplitBK, TILE = kPair ? kPairTile : BK * D, LDO = D + kOutPad;
   constexpr int OPW = 2 * (BK * D / 8 / 64) / NW;  // DMA ops per wave per ring stage (K + V)
   constexpr int RG = kPair ? 4 : kRing;  // ring depth: RG - 1 tiles in flight (4 x 34 KB at D = 256)
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // ring stage s: K at smem + 2 s TILE, V after
@@ -1326,9 +1330,9 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
   __syncthreads();  // Q/dO tiles dead: reuse LDS as per-wave output staging
   const float one[4] = {1.f, 1.f, 1.f, 1.f};
   if (wk_lo < Sk) {
-    bf16_t* T = smem + w * 16 * LD;
-    store_tile16<D>(T, LD, dKa, one, dk, dks, b, hk, wk_lo, min(16, Sk - wk_lo));
-    store_tile16<D>(T, LD, dVa, one, dv, dvs, b, hk, wk_lo, min(16, Sk - wk_lo));
+    bf16_t* T = smem + w * 16 * (D + kOutPad);
+    store_tile16<D>(T, D + kOutPad, dKa, one, dk, dks, b, hk, wk_lo, min(16, Sk - wk_lo));
+    store_tile16<D>(T, D + kOutPad, dVa, one, dv, dvs, b, hk, wk_lo, min(16, Sk - wk_lo));
   }
 }
 
@@ -1475,7 +1479,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
   vmcnt_wait<0>();  // the tail's re-read DMA must land before the LDS is reused
   __syncthreads();
   const float one[4] = {1.f, 1.f, 1.f, 1.f};
-  if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * LD, LD, dQa, one, dq, dqs, b, h, wq_lo, min(16, Sq - wq_lo));
+  if (wq_lo < Sq) store_tile16<D>(smem + w * 16 * (D + kOutPad), D + kOutPad, dQa, one, dq, dqs, b, h, wq_lo, min(16, Sq - wq_lo));
 }
 
 static AttnStrides mk(const long* st) { return AttnStrides{st[0], st[1], st[2]}; }
