@@ -51,6 +51,13 @@ __device__ __forceinline__ void glds16_8(const void* src, void* lds_wave_base) {
 }
 
 
+// v_max3_f32 as asm (see epilogue_ce_fwd)
+__device__ __forceinline__ float max3_f32(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -522,17 +529,31 @@ __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc
   for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float m = -INFINITY;
+      float m;
+      if (full) {
+        // 16 values in 8 v_max3_f32 (asm: fmaxf on MFMA results makes hipcc insert a canonicalising
+        // v_max_f32 per operand -- the epilogue measured 3.8 VALU per MFMA of the whole kernel)
+        const float* a = o[2 * qa][i];
+        const float* b = o[2 * qa + 1][i];
+        m = max3_f32(a[0], a[1], a[2]);
+        m = max3_f32(m, a[3], a[4]);
+        m = max3_f32(m, a[5], a[6]);
+        m = max3_f32(m, a[7], b[0]);
+        m = max3_f32(m, b[1], b[2]);
+        m = max3_f32(m, b[3], b[4]);
+        m = max3_f32(m, b[5], b[6]);
+        m = fmaxf(m, b[7]);
+      } else {
+        // padding columns become -inf here, so the exp pass below needs no mask (exp2(-inf) = 0)
+        m = -INFINITY;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int q = 2 * qa + h, c = qcol(q);
-        if (full) {
+        for (int h = 0; h < 2; ++h) {
+          const int q = 2 * qa + h, c = qcol(q);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) m = fmaxf(m, o[q][i][e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (c + e < g.ce_V) m = fmaxf(m, o[q][i][e]);
+          for (int e = 0; e < 8; ++e) {
+            if (c + e >= g.ce_V) o[q][i][e] = -INFINITY;
+            m = fmaxf(m, o[q][i][e]);
+          }
         }
       }
       m = fmaxf(m, xor16_pl(m));
@@ -561,23 +582,25 @@ __device__ __forceinline__ void epilogue_ce_fwd(const GemmArgs& g, f32x4_t (&acc
     for (int i = 0; i < 4; ++i) {
       const int R = m0 + qa * 128 + rl0 + i * 16;
       const bool rok = R < g.M;
-      const long lab = labs[qa][i];
-      const float mb = mt[qa][i] * 1.4426950408889634f;
+      const int lab = (int)labs[qa][i];  // vocab < 2^31; -100 (ignored) never matches a column
+      // an all-padding tile (max -inf) must not turn exp(-inf - -inf) into NaN
+      const float mb = (mt[qa][i] == -INFINITY ? 0.f : mt[qa][i]) * 1.4426950408889634f;
       float s = 0.f;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int q = 2 * qa + h, c = qcol(q);
-        const long d = lab - c;
-        if (rok && d >= 0 && d < 8) {  // the label column: one select chain, one store
+        const unsigned d = (unsigned)(lab - c);
+        // the label column: a branch the wave almost never takes (one row's label in this lane's 8
+        // columns of a 256-column tile), instead of a branch-free 64-bit select chain over every value
+        if (__builtin_expect(rok && d < 8u, 0)) {
           float xl = o[q][i][0];
 #pragma unroll
-          for (int e = 1; e < 8; ++e) xl = d == e ? o[q][i][e] : xl;
+          for (int e = 1; e < 8; ++e) xl = d == (unsigned)e ? o[q][i][e] : xl;
           g.ce_lbl[R] = xl;
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float x = fast_exp2(fmaf(o[q][i][e], 1.4426950408889634f, -mb));
-          if (!full && c + e >= g.ce_V) x = 0.f;
+          const float x = fast_exp2(fmaf(o[q][i][e], 1.4426950408889634f, -mb));
           o[q][i][e] = x;
           s += x;
         }
