@@ -170,20 +170,22 @@ __device__ __forceinline__ int ce_row_pos(int R) {
   return (R & ~255) + (rl >> 6) * 64 + (rl & 15) * 4 + ((rl >> 4) & 3);
 }
 
-// 64 rows per block.  Pass 1 (a wave per row, lanes over vocab tiles): row max of the tile maxima,
+// RB rows per block (64, or 32 / 16 when M / 64 blocks would not fill the CUs twice: Gemma-3 at
+// 8,192 rows and 1,024 vocab tiles ran 128 blocks at 293 us, latency-bound).  Pass 1 (a wave per row, lanes over vocab tiles): row max of the tile maxima,
 // lse = max + log sum_t s_t exp(m_t - max), loss, the dgrad's final factor and label weight.
 // Pass 2: ratio[t][pos(R)] = exp(m'_{t-1} - m'_t), m'_t = max(m_t, rowmax - 60) (a tile 60 below
 // the row max contributes < e^-60: clamping keeps every ratio and partial sum finite in fp32).
+template <int RB>
 __global__ __launch_bounds__(256) void ce_finalize_kernel(const float2* __restrict__ stats, const float* __restrict__ lbl,
                                                           const int64_t* __restrict__ labels, int M, int T, int V,
                                                           long mpad, const float* __restrict__ scale, float extra,
                                                           float* __restrict__ loss, float* __restrict__ lse_out,
                                                           float* __restrict__ ratio, float* __restrict__ fin,
                                                           float* __restrict__ wlab, int nsplit, int tps) {
-  __shared__ float s_mx[64];
+  __shared__ float s_mx[RB];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r0 = blockIdx.x * 64;
-  for (int rr = w; rr < 64; rr += 4) {
+  const int r0 = blockIdx.x * RB;
+  for (int rr = w; rr < RB; rr += 4) {
     const int R = r0 + rr;
     if (R >= M) break;
     const float2* st = stats + (long)R * T;
@@ -220,10 +222,10 @@ __global__ __launch_bounds__(256) void ce_finalize_kernel(const float2* __restri
   // with lanes over tiles (coalesced reads), then every thread writes one row's ratios with lanes over
   // rows (one 256-B segment per tile).  Reading the stats row-per-lane instead (64 rows T * 8 B apart
   // per instruction) made this kernel 5-7x its bandwidth time at Gemma-3's 1,024 vocab tiles.
-  __shared__ float s_m[64][65];  // [row][tile in chunk], +1 pad: the lanes-over-rows reads are conflict-free
+  __shared__ float s_m[RB][65];  // [row][tile in chunk], +1 pad: the lanes-over-rows reads are conflict-free
   __syncthreads();
-  const int nrow = min(64, M - r0);
-  const int rr2 = threadIdx.x & 63;
+  const int nrow = min(RB, M - r0);
+  const int rr2 = threadIdx.x % RB, jg = threadIdx.x / RB;  // 256 / RB tile groups
   const long dst = ce_row_pos(r0 + rr2);
   for (int c0 = 0; c0 < T - 1; c0 += 63) {  // chunk = tiles c0 .. c0 + 63: ratios of tiles c0 + 1 ..
     const int cn = min(64, T - c0);
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(256) void ce_finalize_kernel(const float2* __restri
       if (lane < cn) s_m[rr][lane] = fmaxf(stats[(long)(r0 + rr) * T + c0 + lane].x, s_mx[rr] - 60.f);
     __syncthreads();
     if (rr2 < nrow)
-      for (int j = 1 + w; j < cn; j += 4) ratio[(long)(c0 + j) * mpad + dst] = __expf(s_m[rr2][j - 1] - s_m[rr2][j]);
+      for (int j = 1 + jg; j < cn; j += 256 / RB) ratio[(long)(c0 + j) * mpad + dst] = __expf(s_m[rr2][j - 1] - s_m[rr2][j]);
     __syncthreads();
   }
 }
@@ -375,10 +377,16 @@ void lm_head_ce(const CeArgs& a, hipStream_t st) {
   gemm8x(f, GEMM_EPI_CE_FWD, false, false, st);
   const bool fused = grad && !a.materialize;
   const int nk = (a.Vpad + 63) / 64, tps = ((nk + S - 1) / S) / 4;
-  ce_finalize_kernel<<<(a.M + 63) / 64, 256, 0, st>>>(reinterpret_cast<const float2*>(L.stats), L.lbl, a.labels, a.M,
-                                                       T, a.V, mpad, a.scale, a.extra, a.loss, lse,
-                                                       fused ? L.ratio : nullptr, fused ? L.fin : nullptr, L.wlab, S,
-                                                       S > 1 ? tps : T);
+  {
+    auto fk = ce_finalize_kernel<64>;
+    int rb = 64;
+    for (; rb > 16 && (a.M + rb - 1) / rb < 2 * ce_num_cus(); rb /= 2) {}
+    if (rb == 32) fk = ce_finalize_kernel<32>;
+    if (rb == 16) fk = ce_finalize_kernel<16>;
+    fk<<<(a.M + rb - 1) / rb, 256, 0, st>>>(reinterpret_cast<const float2*>(L.stats), L.lbl, a.labels, a.M, T, a.V,
+                                            mpad, a.scale, a.extra, a.loss, lse, fused ? L.ratio : nullptr,
+                                            fused ? L.fin : nullptr, L.wlab, S, S > 1 ? tps : T);
+  }
   if (!grad) return;
   GemmArgs d{};
   d.A = a.E; d.lda = a.lde;
