@@ -309,14 +309,16 @@ __global__ void lora_wgrad_reduce_kernel(const float* __restrict__ ws, int ny, i
 //     the B operand of dB^T-tile += u^T dy, with u^T staged through a tiny [32][16] LDS image.
 // dB accumulates over the wave's tiles in 16 f32x4 registers; the 4 waves of the block fold through
 // LDS and issue one fp32 atomic per (rank, column) per block (256-B contiguous per wave instruction).
-// v partial sums per 256-column strip go to an fp32 scratch [strip][M][8] summed by lora_dy_finish.
+// v partial sums per 256-column strip go to an fp32 scratch [strip][M][8] summed by lora_dy_finish (one
+// strip, N <= 256: v is written directly).
 constexpr int kDyLd = 256 + 8;  // padded LDS row (elements): transposed reads conflict-free
 
 __global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restrict__ dy, long ldy,
                                                          const bf16_t* __restrict__ B, long ldb,
                                                          const bf16_t* __restrict__ u, long ldu, float* __restrict__ dB,
                                                          long ldd, float* __restrict__ vpart, long M, int N, long chunk,
-                                                         float s, float* __restrict__ det_ws, long det_np) {
+                                                         float s, float* __restrict__ det_ws, long det_np,
+                                                         bf16_t* __restrict__ vout, long ldv) {
   // per wave: dy image [32][kDyLd] + u^T image [32][16]; block reduction buffer aliases the images
   __shared__ __attribute__((aligned(16))) bf16_t lds[4][32 * kDyLd + 32 * 16];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -389,7 +391,11 @@ __global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restric
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const long m = t0 + 16 * rb + 4 * g + i;
-          if (m < mend) vpart[((long)blockIdx.x * M + m) * 8 + c16] = vacc[rb][i];
+          if (m >= mend) continue;
+          if (vout)  // a single 256-column strip (N <= 256): v directly, no partials to sum
+            vout[m * ldv + c16] = f2bf(vacc[rb][i] * s);
+          else
+            vpart[((long)blockIdx.x * M + m) * 8 + c16] = vacc[rb][i];
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // tr-reads done before the next tile's writes
@@ -469,8 +475,9 @@ void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t
   const long ny = dy_chunks(M, N, &chunk);
   const long np = (long)gx * 256;
   dim3 grid(gx, (unsigned)ny);
-  lora_dy_kernel<<<grid, 256, 0, st>>>(dy, ldy, B, ldb, u, ldu, dB, ldd, vpart, M, N, chunk, s, det_ws, np);
-  lora_dy_finish_kernel<<<cdiv(M * 8, 256), 256, 0, st>>>(vpart, gx, M, s, v, ldv);
+  lora_dy_kernel<<<grid, 256, 0, st>>>(dy, ldy, B, ldb, u, ldu, dB, ldd, vpart, M, N, chunk, s, det_ws, np,
+                                       gx == 1 ? v : nullptr, ldv);
+  if (gx > 1) lora_dy_finish_kernel<<<cdiv(M * 8, 256), 256, 0, st>>>(vpart, gx, M, s, v, ldv);
   if (det_ws) lora_dy_reduce_kernel<<<cdiv(8L * N, 256), 256, 0, st>>>(det_ws, (int)ny, N, np, dB, ldd);
 }
 

@@ -14,7 +14,7 @@ def _close(a, b, atol, rtol=0.0, msg=""):
     assert err <= tol, f"{msg} max abs err {err:.3e} > {tol:.3e}"
 
 
-@pytest.mark.parametrize("M,N", [(300, 768), (1000, 2304), (77, 264), (130, 520), (4096, 768)])
+@pytest.mark.parametrize("M,N", [(300, 768), (1000, 2304), (77, 264), (130, 520), (4096, 768), (1000, 256), (77, 200)])
 def test_lora_dy_matches_fp32(M, N):
     from mobilefinetuner_amd._ext import native
     C = native()
