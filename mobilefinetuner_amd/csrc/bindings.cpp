@@ -609,9 +609,13 @@ std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, 
     a.lora_w = bp(*lora_w); a.ld_lw = lora_w->stride(0);
     a.lora_r = lora_u->size(1);
   }
-  TORCH_CHECK(impl == 0, "gemm_t: impl 0 (gemm8) only -- the round-3 gemmw / gemm4 experiments are removed "
-              "(records: profiles/r3_gemm_stream_ab.txt, profiles/r3_gemm4_experiment.txt)");
-  mft::gemm8x(a, (int)epi, a_t, b_t, stream());
+  TORCH_CHECK(impl == 0 || impl == 4, "gemm_t: impl 0 (gemm8) or 4 (gemm4, hand-scheduled 4-wave kernel)");
+  if (impl == 4) {
+    TORCH_CHECK(mft::gemm4_supported(M, N, K, a_t, b_t), "gemm_t: shape / layout not supported by gemm4");
+    mft::gemm4x(a, (int)epi, a_t, b_t, stream());
+  } else {
+    mft::gemm8x(a, (int)epi, a_t, b_t, stream());
+  }
   return {C, X};
 }
 

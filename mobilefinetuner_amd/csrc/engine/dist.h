@@ -76,8 +76,9 @@ struct DistConfig {
   bool overlap = true;               // launch buckets from the grad-ready hooks during backward
   bool host_moments = false;         // stage >= 1: AdamW moments in pinned host DRAM
   bool host_fp32 = false;            // ... as fp32 (default bf16, stochastically rounded)
-  bool host_stream = true;           // ZeRO-3: stream each unit's moments through device slots during
-                                     // the next forward (false: the kernel reads them over PCIe)
+  bool host_stream = true;           // ZeRO-3: each unit's update applied in place (moments read and
+                                     // written over PCIe) during the next forward on a side stream;
+                                     // false: one update of everything after the backward
 };
 
 struct FlatPlan {

@@ -48,7 +48,7 @@ struct AdamWConfig {
   float max_grad_norm = 1.f;  // <= 0: no clipping
   bool l2_coupled = false;    // reference Adam (L2 added to the gradient)
   bool skip_nonfinite = true;
-  bool amsgrad = false;       // AMSGrad (reference optim/adam.cpp:52,78; torch semantics: max of raw v)
+  bool amsgrad = false;       // AMSGrad, reference rule (optim/adam.cpp:52,75-80): v_hat = max(v_hat, v / bc2)
 };
 
 class AdamW {

@@ -29,6 +29,12 @@ Trainer::Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDatase
   MFT_CHECK(!comm_ || dp_, "Trainer: a communicator needs its DataParallel reducer");
   const char* gc = std::getenv("MFT_GRAPH_COMM");
   graph_comm_ = !(gc && gc[0] == '0');
+  if (!graph_comm_ && dp_ && dp_->owns_optimizer()) {
+    // the streamed ZeRO-3 optimizer forks its stream inside fwd_bwd() and joins it in finish(): a
+    // capture of fwd_bwd() alone would end with an unjoined stream
+    std::fprintf(stderr, "[trainer] MFT_GRAPH_COMM=0 ignored: the host-streamed ZeRO-3 optimizer runs inside the graph\n");
+    graph_comm_ = true;
+  }
   if (comm_ && !(dp_ && dp_->params_sharded())) {  // every rank starts from rank 0's trainable weights
     comm_->broadcast(flat_.master.data_ptr(), (size_t)flat_.numel * sizeof(float), 0, stream_);
     flat_.refresh_shadow();
@@ -471,7 +477,22 @@ bool Trainer::load_state(const std::string& dir0) {
   };
   flat_.master.copy_(host_view(tw, "master", flat_.numel));
   opt_.load_state(host_view(to, "m", opt_.m.numel()), host_view(to, "v", opt_.v.numel()), st["opt_step"].as_int());
-  if (opt_.vmax.defined() && to.has("vmax")) opt_.load_vmax(host_view(to, "vmax", opt_.vmax.numel()));
+  if (opt_.vmax.defined()) {
+    if (to.has("vmax")) {
+      opt_.load_vmax(host_view(to, "vmax", opt_.vmax.numel()));
+    } else {  // a checkpoint written without AMSGrad: start the running max at the loaded v / bc2 (its
+      // first step then matches plain Adam), never at zero beside restored moments
+      const int64_t steps = st["opt_step"].as_int(), n = opt_.vmax.numel();
+      const double bc2 = 1.0 - std::pow((double)opt_.config().beta2, (double)std::max<int64_t>(steps, 1));
+      Tensor vh = host_view(to, "v", n);
+      std::vector<float> vm((size_t)n);
+      const float* src = static_cast<const float*>(vh.data_ptr());
+      for (int64_t i = 0; i < n; ++i) vm[(size_t)i] = (float)(src[i] / bc2);
+      std::fprintf(stderr, "[warn] load_state: --amsgrad but the checkpoint has no 'vmax'; initialised from v / bc2\n");
+      opt_.load_vmax(from_blob(vm.data(), {n}, DType::F32, Device::cpu()));
+      synchronize();
+    }
+  }
   synchronize();  // the mmaps go away with the files
   flat_.refresh_shadow();
   global_step = st["global_step"].as_int();

@@ -244,17 +244,19 @@ void Zero3::prepare_optimizer() {
   // the lr wait in place; the next forward applies them unit by unit
   Z3_TRACE("prepare\n");
   sopt_->prepare_delayed();
-  pending_host_ = true;
+  primed_ = true;
   std::fill(supd_.begin(), supd_.end(), 0);
   forked_ = false;
 }
 
 void Zero3::flush_optimizer() {
-  if (!sopt_ || !pending_host_) return;
+  // issued whether or not the host believes an update is pending: in graph mode the replays (never
+  // host code) leave the device flag ahead of any host-side bookkeeping, and the kernels and the
+  // commit are gated on that device flag (a no-op when nothing is pending) -- ADVICE r4
+  if (!sopt_ || !primed_) return;
   for (int i = 0; i < (int)supd_.size(); ++i) opt_update(i);
   join_opt_stream();
   synchronize();
-  pending_host_ = false;
   forked_ = false;
   std::fill(supd_.begin(), supd_.end(), 0);
   holder_.assign(holder_.size(), -1);  // every partition changed
@@ -264,7 +266,7 @@ void Zero3::gather(int u) {
   Unit& un = units_[u];
   HIP_OK(hipEventRecord(order_, current_stream()));  // the slot's previous user has been enqueued
   HIP_OK(hipStreamWaitEvent(stream_, order_, 0));
-  if (sopt_ && pending_host_ && grad_enabled()) {  // the previous step's update of this partition first
+  if (sopt_ && primed_ && grad_enabled()) {  // the previous step's update of this partition first (gated on device)
     opt_update(1 + u);
     HIP_OK(hipStreamWaitEvent(stream_, upd_ev_[1 + u], 0));
   }
@@ -312,7 +314,7 @@ float Zero3::grad_prescale() const { return 1.f / (float)comm_.world(); }
 void Zero3::zero_grad(FlatParams& flat) {
   // streamed optimizer: the replicated parameters' pending update reads their gradients -- it runs
   // before they are cleared, with the first units' moment prefetches behind it
-  if (sopt_ && pending_host_) {
+  if (sopt_ && primed_) {  // (device-gated: a no-op when a flush already applied it)
     opt_update(0);
     HIP_OK(hipStreamWaitEvent(current_stream(), upd_ev_[0], 0));
   }
@@ -368,13 +370,12 @@ std::pair<Tensor, Tensor> Zero3::gate(const Tensor& x, const Tensor& h, int bloc
 }
 
 void Zero3::finish() {
-  Z3_TRACE("finish (pending %d)\n", (int)pending_host_);
-  if (sopt_ && pending_host_) {
+  Z3_TRACE("finish (primed %d)\n", (int)primed_);
+  if (sopt_ && primed_) {
     // every pending update issued (a unit the forward did not gather) and the optimizer stream
     // joined back: a captured step ends with every stream it forked
     for (int i = 0; i < (int)supd_.size(); ++i) opt_update(i);
     join_opt_stream();
-    pending_host_ = false;
   }
   for (size_t u = 0; u < units_.size(); ++u) reduce_scatter((int)u);  // units no hook completed
   if (rep_n_ > 0) {

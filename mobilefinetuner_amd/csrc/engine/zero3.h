@@ -133,7 +133,10 @@ class Zero3 : public GradReducer, public BlockProvider {
   void opt_update(int i);      // AdamW on update i, moments in place in host DRAM
   void join_opt_stream();      // the current stream waits for the optimizer stream
   AdamW* sopt_ = nullptr;
-  bool sfp32_ = false, pending_host_ = false, forked_ = false;
+  // primed_: an update has been prepared at least once (the device flag exists); the updates are then
+  // issued at every gather / zero_grad / finish / flush and gated on the device flag -- never on host
+  // state, which a hipGraph replay does not advance
+  bool sfp32_ = false, primed_ = false, forked_ = false;
   std::vector<int> supd_;             // per update: issued this step
   std::vector<hipEvent_t> upd_ev_;    // per update: applied
   hipEvent_t fork_ev_ = nullptr, ojoin_ev_ = nullptr;

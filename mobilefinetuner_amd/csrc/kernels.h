@@ -119,6 +119,9 @@ struct GemmArgs {
 // [K, N] (NN data-grad); both: TN weight-grad (use GEMM_EPI_F32ACC with gemm8_pick_ksplit / ws)
 void gemm8(const GemmArgs& g, int epi, hipStream_t st);  // NT
 void gemm8x(const GemmArgs& g, int epi, bool a_t, bool b_t, hipStream_t st);
+// 256x256x64 4-wave GEMM with a hand-scheduled K-tile body (gemm4.hip); NT layout
+void gemm4x(const GemmArgs& g, int epi, bool a_t, bool b_t, hipStream_t st);
+bool gemm4_supported(int M, int N, int K, bool a_t, bool b_t);
 bool gemm8_supported(int M, int N, int K, bool a_t, bool b_t);
 int gemm8_pick_ksplit(int M, int N, int K);
 // NT NONE / BIAS / BIAS_GELU_D: the persistent streaming form with the deferred epilogue (opt-in,

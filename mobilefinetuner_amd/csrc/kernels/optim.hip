@@ -156,12 +156,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
         if (a.l2_coupled) gj += a.weight_decay * pp[j];
         mm[j] = a.beta1 * mm[j] + (1.f - a.beta1) * gj;
         vv[j] = a.beta2 * vv[j] + (1.f - a.beta2) * gj * gj;
-        float vd = vv[j];
-        if (!MB && a.vmax) {  // AMSGrad (torch semantics: the max of the raw second moment, then bias-corrected)
-          vd = fmaxf(a.vmax[4 * i + j], vd);
+        float denom = sqrtf(vv[j]) * rbc2 + a.eps;
+        if (!MB && a.vmax) {  // AMSGrad, the reference's rule (optim/adam.cpp:75-80): the running max of
+          // the BIAS-CORRECTED second moment, v_hat = max(v_hat, v / bc2), used as is in the denominator
+          const float vd = fmaxf(a.vmax[4 * i + j], vv[j] * (rbc2 * rbc2));
           a.vmax[4 * i + j] = vd;
+          denom = sqrtf(vd) + a.eps;
         }
-        const float denom = sqrtf(vd) * rbc2 + a.eps;
         pp[j] = pp[j] * decay - step_size * mm[j] / denom;
       }
       reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
@@ -194,12 +195,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
       if (a.l2_coupled) gj += a.weight_decay * pj;
       const float mj = a.beta1 * ld_mom<MB>(a.m, i) + (1.f - a.beta1) * gj;
       const float vj = a.beta2 * ld_mom<MB>(a.v, i) + (1.f - a.beta2) * gj * gj;
-      float vd = vj;
-      if (!MB && a.vmax) {
-        vd = fmaxf(a.vmax[i], vd);
+      float denom = sqrtf(vj) * rbc2 + a.eps;
+      if (!MB && a.vmax) {  // AMSGrad (reference rule, as above)
+        const float vd = fmaxf(a.vmax[i], vj * (rbc2 * rbc2));
         a.vmax[i] = vd;
+        denom = sqrtf(vd) + a.eps;
       }
-      pj = pj * decay - step_size * mj / (sqrtf(vd) * rbc2 + a.eps);
+      pj = pj * decay - step_size * mj / denom;
       a.p[i] = pj;
       const uint32_t r = sr_hash(seed ^ 0x5bd1e995U ^ (uint32_t)(a.sr_offset + i));
       st_mom<MB>(a.m, i, mj, r);

@@ -94,3 +94,25 @@ def lm_cross_entropy(logits, labels, ignore_index=-100, reduction="mean"):
 
 def perplexity(loss):
     return math.exp(loss)
+
+
+def adam_step(p, g, m, v, vhat, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0,
+              decoupled=True, amsgrad=False):
+    """One Adam(W) step in fp32, in place, the reference's formulas (operators/finetune_ops/optim/adam.cpp:
+    56-87): bias-corrected moments and, with AMSGrad, v_hat = max(v_hat, v / bc2) used directly in the
+    denominator (torch instead keeps the max of the RAW v and divides by the current bc2).  decoupled=False
+    is the reference's coupled L2 (grad += wd * p); True is AdamW's decay p *= 1 - lr * wd.  step: the
+    1-based index of this step."""
+    if not decoupled and weight_decay:
+        g = g + weight_decay * p
+    m.mul_(beta1).add_(g, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    bc1, bc2 = 1 - beta1 ** step, 1 - beta2 ** step
+    vc = v / bc2
+    if amsgrad:
+        torch.maximum(vhat, vc, out=vhat)
+        vc = vhat
+    if decoupled and weight_decay:
+        p.mul_(1 - lr * weight_decay)
+    p.sub_(lr * (m / bc1) / (vc.sqrt() + eps))
+    return p

@@ -663,28 +663,28 @@ def test_gated_row_pair_grid_stride():
         del gu, y, g, r, yr
 
 
-def test_adamw_amsgrad_matches_torch():
-    """AMSGrad (reference optim/adam.cpp:52,78): the fused kernel with a vmax buffer == torch.optim.AdamW(amsgrad=True)
-    over 6 steps (decoupled weight decay, fp32 moments)."""
+def test_adamw_amsgrad_matches_reference():
+    """AMSGrad, the reference's rule (optim/adam.cpp:52,75-80: v_hat = max(v_hat, v / bc2)): the fused kernel
+    with a vmax buffer == the fp64 oracle tests/oracle/reference.py::adam_step over 6 steps (decoupled
+    weight decay, fp32 moments, a large early gradient so the running max matters), tail path included."""
     from mobilefinetuner_amd._ext import native
+    from oracle.reference import adam_step
     C = native()
     torch.manual_seed(0)
     n = 4099  # tail path too
     p0 = torch.randn(n, device="cuda")
-    ref = p0.clone().requires_grad_(True)
-    opt = torch.optim.AdamW([ref], lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.05, amsgrad=True)
+    rp, rm, rv, rvh = (t.double().cpu() for t in (p0, torch.zeros(n), torch.zeros(n), torch.zeros(n)))
     p, m, v, vmax = p0.clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
     lr = torch.full((1,), 1e-2, device="cuda")
     step = torch.zeros(1, device="cuda")
     for it in range(6):
         g = torch.randn(n, device="cuda") * (3.0 if it == 1 else 0.3)  # a large early step makes the max matter
-        ref.grad = g.clone()
-        opt.step()
+        adam_step(rp, g.double().cpu(), rm, rv, rvh, it + 1, 1e-2, 0.9, 0.99, 1e-8, 0.05, True, True)
         C.adamw_step(p, g, m, v, lr, step, None, 0.9, 0.99, 1e-8, 0.05, 0.0, False, None, None, 0, vmax)
         C.adamw_commit(step, None, None)
     torch.cuda.synchronize()
-    assert torch.allclose(p, ref.detach(), rtol=1e-5, atol=1e-6), (p - ref.detach()).abs().max()
-    assert torch.allclose(vmax, opt.state[ref]["max_exp_avg_sq"], rtol=1e-5, atol=1e-9)
+    assert torch.allclose(p.cpu().double(), rp, rtol=1e-5, atol=1e-6), (p.cpu().double() - rp).abs().max()
+    assert torch.allclose(vmax.cpu().double(), rvh, rtol=1e-5, atol=1e-9)
 
 
 @pytest.mark.parametrize("M,K,R,ldx", [(1000, 640, 8, 704), (77, 768, 32, 768), (4099, 2048, 16, 2112)])
