@@ -34,8 +34,9 @@ READ_GAP = 2      # MFMAs between consecutive fragment reads
 BAR_A = 40        # MFMA index the "buffer cur free" barrier precedes
 
 
-def mfma(s, i, j):
-    return f"v_mfma_f32_16x16x32_bf16 %[c{i}{j}], %[b{s}_{j}], %[a{s}_{i}], %[c{i}{j}]"
+def mfma(s, i, j, zero_c=False):
+    c = "0" if zero_c else f"%[c{i}{j}]"
+    return f"v_mfma_f32_16x16x32_bf16 %[c{i}{j}], %[b{s}_{j}], %[a{s}_{i}], {c}"
 
 
 def read_order():
@@ -55,9 +56,12 @@ def dma(kind, j):
             f"buffer_load_dwordx4 %[o{kind}{j}], %[{srd}], %[koff] offen lds"]
 
 
-def ktile_nt(read_gap=READ_GAP, bar_a=BAR_A, dma_at=None, with_dma=True):
+def ktile_nt(read_gap=READ_GAP, bar_a=BAR_A, dma_at=None, with_dma=True, first=False, vm_extra=0):
     """One K-tile: MFMA n = 0..127 (k-step n // 64).  dma_at[q] = the MFMA index (> bar_a) the q-th of
-    the 16 LDS-DMA pieces precedes; the ones before MFMA 64 are left in flight by barrier B's vmcnt."""
+    the 16 LDS-DMA pieces precedes; the ones before MFMA 64 are left in flight by barrier B's vmcnt.
+    first: the first K-tile of an output tile (k-step 0 accumulates onto 0, not onto the registers);
+    vm_extra: VMEM operations issued between the previous K-tile's DMAs and this one's (the epilogue
+    stores of the previous tile in the persistent kernel) that barrier B may leave in flight."""
     if dma_at is None:
         dma_at = list(range(bar_a + 1, bar_a + 17))
     assert len(dma_at) == 16 and min(dma_at) > bar_a and max(dma_at) < 128
@@ -71,7 +75,7 @@ def ktile_nt(read_gap=READ_GAP, bar_a=BAR_A, dma_at=None, with_dma=True):
         ks, (i, j) = n // 64, order[n % 64]
         m = n % 64
         if n == 64:
-            lines += [f"s_waitcnt vmcnt({before_b})", "s_barrier",
+            lines += [f"s_waitcnt vmcnt({min(63, before_b + vm_extra)})", "s_barrier",
                       "v_xor_b32 %[ra0], 0x10000, %[ra0]", "v_xor_b32 %[rb0], 0x10000, %[rb0]"]
         if m % read_gap == 0 and m // read_gap < len(reads):
             kind, idx = reads[m // read_gap]
@@ -83,8 +87,96 @@ def ktile_nt(read_gap=READ_GAP, bar_a=BAR_A, dma_at=None, with_dma=True):
             lines += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
         if n in at and with_dma:
             lines += dmas[at[n]]
-        lines.append(mfma(ks, i, j))
+        lines.append(mfma(ks, i, j, zero_c=first and ks == 0))
     lines += ["v_xor_b32 %[ra1], 0x10000, %[ra1]", "v_xor_b32 %[rb1], 0x10000, %[rb1]", "s_waitcnt lgkmcnt(0)"]
+    return lines
+
+
+def ds_read_b_perm(s, j):
+    c, h = j // 2, j % 2
+    return f"ds_read_b128 %[b{s}_{j}], %[rb{s}{h}] offset:{c * 4096}"
+
+
+def ktile_v2(first=False, bar_a=20, wait_at=104, dma_at=None, rd_early=None, rd_late=None, vm_extra_mode=None):
+    """Schedule v2 (the hipBLASLt MT256x256x64 loop's placement, read from its gfx950 code object):
+    the k-step-1 fragments of THIS K-tile are read first (MFMA 0..15), one barrier frees the buffer, the
+    16 LDS-DMA pieces of K-tile t + 2 spread over the rest of the K-tile, and the wait for K-tile t + 1
+    sits as LATE as possible (MFMA wait_at), right before the next K-tile's k-step-0 reads at the end.
+    Returns (lines, n_dma_before_wait).  vm_extra_mode: None, or (mode operand, extra stores) -> the
+    wait allows that many more operations when the mode SGPR is 2 (first K-tile after an epilogue)."""
+    if dma_at is None:
+        dma_at = [bar_a + 1 + 6 * q for q in range(16)]
+    if rd_early is None:
+        rd_early = list(range(16))
+    if rd_late is None:
+        rd_late = [wait_at + 2 + q for q in range(16)]
+    assert max(rd_late) < 128 and max(dma_at) < 128 and min(dma_at) > bar_a > max(rd_early)
+    order = [(i, j) for i in range(8) for j in range(8)]
+    reads = read_order()
+    dmas = [dma("a", j) for j in range(8)] + [dma("b", j) for j in range(8)]
+    at = {n: q for q, n in enumerate(dma_at)}
+    re_ = {n: q for q, n in enumerate(rd_early)}
+    rl = {n: q for q, n in enumerate(rd_late)}
+    n_before = sum(1 for n in dma_at if n < wait_at)
+    lines = []
+    for n in range(128):
+        ks, (i, j) = n // 64, order[n % 64]
+        if n == bar_a:
+            lines += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+        if n == wait_at:
+            if vm_extra_mode:
+                lines += ["s_cmp_eq_u32 %[mode], 2", "s_cbranch_scc1 LW%=_", f"s_waitcnt vmcnt({n_before})",
+                          "s_branch LV%=_", "LW%=_:", f"s_waitcnt vmcnt({min(63, n_before + vm_extra_mode)})", "LV%=_:"]
+            else:
+                lines.append(f"s_waitcnt vmcnt({n_before})")
+            lines += ["s_barrier", "v_xor_b32 %[ra0], 0x10000, %[ra0]", "v_xor_b32 %[rb00], 0x10000, %[rb00]",
+                      "v_xor_b32 %[rb01], 0x10000, %[rb01]"]
+        if n in re_:
+            kind, idx = reads[re_[n]]
+            lines.append(ds_read(1, kind, idx, "ra1") if kind == "a" else ds_read_b_perm(1, idx))
+        if n in rl:
+            kind, idx = reads[rl[n]]
+            lines.append(ds_read(0, kind, idx, "ra0") if kind == "a" else ds_read_b_perm(0, idx))
+        if n in at:
+            lines += dmas[at[n]]
+        lines.append(mfma(ks, i, j, zero_c=first and ks == 0))
+    lines += ["v_xor_b32 %[ra1], 0x10000, %[ra1]", "v_xor_b32 %[rb10], 0x10000, %[rb10]",
+              "v_xor_b32 %[rb11], 0x10000, %[rb11]", "s_waitcnt lgkmcnt(0)"]
+    return lines
+
+
+def ktile_v2_modes(vm_extra=32, **kw):
+    """v2 with the persistent kernel's mode branch (see ktile_nt_modes): k-step 0 zero-accumulates in
+    modes 1 / 2; the late wait allows vm_extra more operations in mode 2."""
+    normal = ktile_v2(vm_extra_mode=vm_extra, **kw)
+    first = ktile_v2(first=True, vm_extra_mode=vm_extra, **kw)
+    # the bodies differ only in the k-step-0 MFMAs (index < the first k-step-1 MFMA line)
+    k1n = next(k for k, l in enumerate(normal) if l.startswith("v_mfma") and "b1_" in l)
+    k1f = next(k for k, l in enumerate(first) if l.startswith("v_mfma") and "b1_" in l)
+    assert normal[k1n:] == first[k1f:]
+    lines = ["s_nop 4", "s_cmp_eq_u32 %[mode], 0", "s_cbranch_scc0 LF%=_"]
+    lines += normal[:k1n] + ["s_branch LJ%=_", "LF%=_:"] + first[:k1f] + ["LJ%=_:"] + normal[k1n:]
+    return lines
+
+
+def ktile_nt_modes(vm_extra=32, **kw):
+    """The persistent kernel's K-tile: ONE asm statement for every position in the stream (one call
+    site keeps the compiler from shuffling the accumulators between sites), branching on the SGPR
+    operand mode: 0 = a continuing K-tile; 1 = the first K-tile of the workgroup's first tile; 2 = the
+    first K-tile of a later tile (k-step 0 accumulates onto 0, and barrier B leaves the previous tile's
+    vm_extra epilogue stores in flight).  Both k-step-0 bodies issue the same DMAs, so the counts match."""
+    normal = ktile_nt(**kw)
+    first = ktile_nt(first=True, **kw)
+    i64n = next(k for k, l in enumerate(normal) if l.startswith("s_waitcnt vmcnt("))
+    i64f = next(k for k, l in enumerate(first) if l.startswith("s_waitcnt vmcnt("))
+    assert normal[i64n + 1:] == first[i64f + 1:]
+    before_b = int(normal[i64n].split("(")[1].rstrip(")"))
+    assert normal[0] == first[0] == "s_nop 4"
+    lines = ["s_nop 4", "s_cmp_eq_u32 %[mode], 0", "s_cbranch_scc0 LF%=_"]
+    lines += normal[1:i64n] + ["s_branch LJ%=_", "LF%=_:"] + first[1:i64f] + ["LJ%=_:"]
+    lines += ["s_cmp_eq_u32 %[mode], 2", "s_cbranch_scc1 LW%=_", f"s_waitcnt vmcnt({before_b})", "s_branch LV%=_",
+              "LW%=_:", f"s_waitcnt vmcnt({min(63, before_b + vm_extra)})", "LV%=_:"]
+    lines += normal[i64n + 1:]
     return lines
 
 
@@ -95,27 +187,92 @@ VARIANTS = {
     "NT_FAST_SPREAD4": dict(read_gap=1, bar_a=20, dma_at=[21 + 4 * q for q in range(16)]),  # 2
     "NT_FAST_SPREAD2": dict(read_gap=1, bar_a=20, dma_at=[21 + 2 * q for q in range(16)]),  # 3
     "NT_SPREAD6": dict(read_gap=1, bar_a=20, dma_at=[22 + 6 * q for q in range(16)]),       # 4
+    # persistent kernel: the first K-tile of a tile (after the previous tile's 32 / 64 epilogue stores)
+    "NT_FIRST": dict(first=True),
+    "NT_FIRST_S32": dict(first=True, vm_extra=32),
+    "NT_FIRST_S64": dict(first=True, vm_extra=64),
 }
 
 
-def operands():
+def operands(modes=False):
     outs = [f'[c{i}{j}] "+a"(ACC[{i * 8 + j}])' for i in range(8) for j in range(8)]
     outs += [f'[a0_{i}] "+v"(FA0[{i}])' for i in range(8)] + [f'[b0_{j}] "+v"(FB0[{j}])' for j in range(8)]
     outs += [f'[a1_{i}] "=&v"(FA1[{i}])' for i in range(8)] + [f'[b1_{j}] "=&v"(FB1[{j}])' for j in range(8)]
     outs += ['[ra0] "+v"(RA0)', '[ra1] "+v"(RA1)', '[rb0] "+v"(RB0)', '[rb1] "+v"(RB1)']
     ins = [f'[oa{j}] "v"(OA[{j}])' for j in range(8)] + [f'[ob{j}] "v"(OB[{j}])' for j in range(8)]
     ins += ['[srda] "s"(SRDA)', '[srdb] "s"(SRDB)', '[koff] "s"(KOFF)', '[ldsm] "s"(LDSM)']
+    if modes:
+        ins.append('[mode] "s"(MODE)')
     return outs, ins
 
 
-def emit(name, lines):
-    outs, ins = operands()
+def emit(name, lines, modes=False):
+    outs, ins = operands(modes)
     body = "".join(f'    "{l}\\n"  \\\n' for l in lines)
-    return (f"#define {name}(ACC, FA0, FB0, FA1, FB1, RA0, RA1, RB0, RB1, OA, OB, SRDA, SRDB, KOFF, LDSM) \\\n"
+    extra = ", MODE" if modes else ""
+    return (f"#define {name}(ACC, FA0, FB0, FA1, FB1, RA0, RA1, RB0, RB1, OA, OB, SRDA, SRDB, KOFF, LDSM{extra}) \\\n"
             f"  asm volatile(  \\\n{body}"
             f"    : {', '.join(outs)}  \\\n"
             f"    : {', '.join(ins)}  \\\n"
-            f"    : \"memory\")\n")
+            f"    : \"memory\", \"scc\")\n")
+
+
+FRAG_BASE = 128  # explicit-register form: fragment sets in v[128:255], accumulators in a[0:255]
+
+
+def explicit(lines):
+    """Rewrite the %[...] accumulator / fragment operands to literal registers (persistent kernel: no
+    compiler-managed tuple operands, so no allocator shuffles them between statements)."""
+    import re
+
+    def acc(m):
+        i, j = int(m.group(1)), int(m.group(2))
+        b = 4 * (8 * i + j)
+        return f"a[{b}:{b + 3}]"
+
+    def frag(m):
+        kind, st, idx = m.group(1), int(m.group(2)), int(m.group(3))
+        b = FRAG_BASE + 64 * st + (0 if kind == "a" else 32) + 4 * idx
+        return f"v[{b}:{b + 3}]"
+
+    out = []
+    for l in lines:
+        l = re.sub(r"%\[c(\d)(\d)\]", acc, l)
+        l = re.sub(r"%\[([ab])([01])_(\d)\]", frag, l)
+        out.append(l)
+    return out
+
+
+def clobbers():
+    regs = [f"v{r}" for r in range(FRAG_BASE, 256)] + [f"a{r}" for r in range(256)]
+    return ", ".join(f'"{r}"' for r in regs)
+
+
+def emit_explicit(name, lines, modes=True):
+    ins = ['[ra0] "+v"(RA0)', '[ra1] "+v"(RA1)', '[rb00] "+v"(RB[0])', '[rb01] "+v"(RB[1])', '[rb10] "+v"(RB[2])',
+           '[rb11] "+v"(RB[3])']
+    ins_only = [f'[oa{j}] "v"(OA[{j}])' for j in range(8)] + [f'[ob{j}] "v"(OB[{j}])' for j in range(8)]
+    ins_only += ['[srda] "s"(SRDA)', '[srdb] "s"(SRDB)', '[koff] "s"(KOFF)', '[ldsm] "s"(LDSM)']
+    if modes:
+        ins_only.append('[mode] "s"(MODE)')
+    body = "".join(f'    "{l}\\n"  \\\n' for l in explicit(lines))
+    return (f"#define {name}(RA0, RA1, RB, OA, OB, SRDA, SRDB, KOFF, LDSM, MODE) \\\n"
+            f"  asm volatile(  \\\n{body}"
+            f"    : {', '.join(ins)}  \\\n"
+            f"    : {', '.join(ins_only)}  \\\n"
+            '    : "memory", "scc", ' + clobbers() + ")\n")
+
+
+def set0_read_explicit():
+    """The first k-step's fragments of a tile (buffer of RA0 / RB0) into set 0, waited for."""
+    lines = [f"ds_read_b128 v[{FRAG_BASE + 4 * i}:{FRAG_BASE + 4 * i + 3}], %[ra0] offset:{i * 2048}" for i in range(8)]
+    lines += [f"ds_read_b128 v[{FRAG_BASE + 32 + 4 * j}:{FRAG_BASE + 32 + 4 * j + 3}], %[rb0{j % 2}] offset:{(j // 2) * 4096}"
+              for j in range(8)]
+    lines.append("s_waitcnt lgkmcnt(0)")
+    body = "".join(f'    "{l}\\n"  \\\n' for l in lines)
+    regs = ", ".join(f'"v{r}"' for r in range(FRAG_BASE, FRAG_BASE + 64))
+    return (f"#define GEMM4_SET0_READ_X(RA0, RB) \\\n  asm volatile(  \\\n{body}"
+            '    :  \\\n    : [ra0] "v"(RA0), [rb00] "v"(RB[0]), [rb01] "v"(RB[1])  \\\n    : "memory", ' + regs + ")\n")
 
 
 def main():
@@ -133,6 +290,22 @@ def main():
             f.write(f"// {name}: {kw}\n")
             f.write(emit("GEMM4_KTILE_" + name, lines))
             f.write("\n")
+        for S in (32, 64):
+            lines = ktile_v2_modes(vm_extra=S)
+            assert sum(1 for l in lines if l.startswith("v_mfma")) == 192
+            n_dma = sum(1 for l in lines if l.startswith("buffer_load"))
+            lf, lj = lines.index("LF%=_:"), lines.index("LJ%=_:")
+            in_first = sum(1 for l in lines[lf:lj] if l.startswith("buffer_load"))
+            assert n_dma - in_first == 16, (n_dma, in_first)  # one path issues exactly 16
+            f.write(f"// V2_X{S}: schedule v2, literal registers, mode branch (persistent kernel)\n")
+            f.write(emit_explicit(f"GEMM4_KTILE_V2_X{S}", lines))
+            f.write("\n")
+
+            assert sum(1 for l in lines if l.startswith("v_mfma")) == 192
+            f.write(f"// NT_P{S}: persistent K-tile, mode-branching (previous tile's epilogue: {S} stores per wave)\n")
+            f.write(emit(f"GEMM4_KTILE_NT_P{S}", lines, modes=True))
+            f.write("\n")
+        f.write(set0_read_explicit())
     print(out)
 
 
