@@ -215,6 +215,20 @@ bool rowmajor2(const Tensor& t) { return t.dim() == 2 && t.stride(1) == 1; }
 
 }  // namespace
 
+// MFT_GEMM4=0 keeps every GEMM off gemm4 (A/B); MFT_GEMM4=all also routes the epilogues that only tie
+bool gemm4_route(int epi, bool b_kn, long M, long N, long K, long lda, long ldb) {
+  static const int mode = [] {
+    const char* e = std::getenv("MFT_GEMM4");
+    return !e ? 1 : e[0] == '0' ? 0 : std::string(e) == "all" ? 2 : 1;
+  }();
+  if (mode == 0 || b_kn || deterministic() || !::mft::gemm4_supported((int)M, (int)N, (int)K, false, false)) return false;
+  if (lda % 8 || ldb % 8) return false;
+  if (epi == ::mft::GEMM_EPI_MUL_AUX || epi == ::mft::GEMM_EPI_DGELU) return true;
+  if (mode == 2 && (epi == ::mft::GEMM_EPI_BIAS_GELU_D || epi == ::mft::GEMM_EPI_NONE || epi == ::mft::GEMM_EPI_BIAS))
+    return true;
+  return false;
+}
+
 bool gemm8_all() {
   static int v = -1;
   if (v < 0) v = (std::getenv("MFT_GEMM8_ALL") && std::getenv("MFT_GEMM8_ALL")[0] == '1') ? 1 : 0;
@@ -255,6 +269,13 @@ void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c,
     g.lora_w = (const ::mft::bf16_t*)ex.lora_w->data_ptr();
     g.ld_lw = ex.lora_w->stride(0);
     g.lora_r = (int)ex.lora_u->size(1);
+  }
+  // gemm4 (the 4-wave hand-scheduled persistent kernel, kernels/gemm4.hip) where it beats gemm8:
+  // the MUL_AUX / dGELU data gradient (+11 % at the GPT-2 MLP shape, profiles/r5_gemm4_epilogues.txt)
+  if (gemm4_route(epi, b_kn, M, N, K, g.lda, g.ldb)) {
+    map_line("gemm4", M, N, K, ::mft::GEMM_EPI_MUL_AUX == epi ? "mul_aux" : "epi");
+    ::mft::gemm4x(g, epi, false, false, current_stream());
+    return;
   }
   ::mft::gemm8x(g, epi, false, b_kn, current_stream());
 }

@@ -243,12 +243,16 @@ def explicit(lines):
     return out
 
 
-def clobbers():
-    regs = [f"v{r}" for r in range(FRAG_BASE, 256)] + [f"a{r}" for r in range(256)]
+def clobbers(fragments=True):
+    regs = ([f"v{r}" for r in range(FRAG_BASE, 256)] if fragments else []) + [f"a{r}" for r in range(256)]
     return ", ".join(f'"{r}"' for r in regs)
 
 
 def emit_explicit(name, lines, modes=True):
+    """Literal registers: the accumulators a[0:255] and both fragment sets v[128:255] are clobbers of
+    every statement, so the compiler keeps none of its own values there across a statement.  What
+    crosses statements in them (set 0 between K-tiles, the accumulators into the epilogue) is read
+    back by statements too (gemm4.hip: accr, and the kernel keeps no compiler value live there)."""
     ins = ['[ra0] "+v"(RA0)', '[ra1] "+v"(RA1)', '[rb00] "+v"(RB[0])', '[rb01] "+v"(RB[1])', '[rb10] "+v"(RB[2])',
            '[rb11] "+v"(RB[3])']
     ins_only = [f'[oa{j}] "v"(OA[{j}])' for j in range(8)] + [f'[ob{j}] "v"(OB[{j}])' for j in range(8)]
@@ -264,7 +268,7 @@ def emit_explicit(name, lines, modes=True):
 
 
 def set0_read_explicit():
-    """The first k-step's fragments of a tile (buffer of RA0 / RB0) into set 0, waited for."""
+    """The first k-step's fragments of a tile (buffer of RA0 / RB) into set 0, waited for."""
     lines = [f"ds_read_b128 v[{FRAG_BASE + 4 * i}:{FRAG_BASE + 4 * i + 3}], %[ra0] offset:{i * 2048}" for i in range(8)]
     lines += [f"ds_read_b128 v[{FRAG_BASE + 32 + 4 * j}:{FRAG_BASE + 32 + 4 * j + 3}], %[rb0{j % 2}] offset:{(j // 2) * 4096}"
               for j in range(8)]

@@ -15,7 +15,59 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mobilefinetuner_amd._ext import native
 
-EPI_NONE, EPI_BIAS = 0, 1
+EPI_NONE, EPI_BIAS, EPI_DGELU, EPI_GELU_D, EPI_MUL_AUX = 0, 1, 3, 9, 10
+
+
+def gelu_and_grad(x):
+    t = torch.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3))
+    return 0.5 * x * (1 + t), 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * x * x)
+
+
+def check_epilogues(C, dev, shapes):
+    """Fused epilogues of gemm4 (impl 4) against fp32 references: BIAS_GELU_D (two outputs), MUL_AUX, DGELU."""
+    for name in shapes:
+        M, N, K = SHAPES[name]
+        g = torch.Generator(device=dev).manual_seed(1)
+        x = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).bfloat16()
+        w = ((torch.rand(N, K, device=dev, generator=g) * 2 - 1) * 0.1).bfloat16()
+        b = (torch.rand(N, device=dev, generator=g) - 0.5).bfloat16()
+        aux = (torch.randn(M, N, device=dev, generator=g)).bfloat16()
+        pre = torch.addmm(b.float(), x.float(), w.float().t())
+        gl, gd = gelu_and_grad(pre)
+        y, d = torch.empty(M, N, device=dev, dtype=torch.bfloat16), torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        C.gemm_t(x, w, False, False, EPI_GELU_D, b, d, 1.0, y, None, None, 4)
+        mm = x.float() @ w.float().t()
+        y2 = torch.empty_like(y)
+        C.gemm_t(x, w, False, False, EPI_MUL_AUX, None, aux, 1.0, y2, None, None, 4)
+        y3 = torch.empty_like(y)
+        C.gemm_t(x, w, False, False, EPI_DGELU, None, aux, 1.0, y3, None, None, 4)
+        torch.cuda.synchronize()
+        r = lambda a, ref: ((a.float() - ref).abs().max() / ref.abs().max()).item()
+        errs = (r(y, gl), r(d, gd), r(y2, mm * aux.float()), r(y3, mm * gelu_and_grad(aux.float())[1]))
+        print(f"{name:22s} epilogues gelu {errs[0]:.1e} gelu' {errs[1]:.1e} mul_aux {errs[2]:.1e} dgelu {errs[3]:.1e}",
+              flush=True)
+        assert max(errs) < 2e-2, (name, errs)
+        del pre, gl, gd, mm
+        fl = 2.0 * M * N * K
+        line = f"{name:22s}"
+        for tag, epi, bias, ax in (("gelu_d", EPI_GELU_D, b, d), ("mul_aux", EPI_MUL_AUX, None, aux)):
+            for impl in (4, 0):
+                f = lambda: C.gemm_t(x, w, False, False, epi, bias, ax, 1.0, y, None, None, impl)
+                for _ in range(3):
+                    f()
+                ts = []
+                for _ in range(3):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(10):
+                        f()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1) * 100)
+                t = statistics.median(ts)
+                line += f" | {tag} g{impl} {t:7.1f} us {fl / t / 1e6:5.0f} TF"
+        print(line, flush=True)
+        del x, w, aux, y, d, y2, y3
 
 SHAPES = {
     "8192^3": (8192, 8192, 8192),
@@ -38,10 +90,14 @@ def main():
     ap.add_argument("--check_only", action="store_true")
     ap.add_argument("--no_check", action="store_true", help="diagnostic builds (MFT_G4_DIAG): wrong outputs")
     ap.add_argument("--only", default="", help="comma list of kernels to time (gemm4,gemm8,hipBLASLt)")
+    ap.add_argument("--epi", action="store_true", help="check the fused epilogues (then exit)")
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda")
     names = list(SHAPES) if a.shapes == "all" else a.shapes.split(",")
+    if a.epi:
+        check_epilogues(C, dev, [n for n in names if SHAPES[n][0] * SHAPES[n][1] <= 2 ** 29])
+        return
     for name in names:
         M, N, K = SHAPES[name]
         g = torch.Generator(device=dev).manual_seed(0)
