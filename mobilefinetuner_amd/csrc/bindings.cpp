@@ -578,12 +578,13 @@ std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, 
   Tensor X;
   if (epi == mft::GEMM_EPI_BIAS_GELU || epi == mft::GEMM_EPI_BIAS_GELU_D) {
     X = aux.has_value() ? *aux : torch::empty({M, N}, A.options());
-  } else if (epi == mft::GEMM_EPI_DGELU || epi == mft::GEMM_EPI_MUL_AUX) {
-    TORCH_CHECK(aux.has_value(), "gemm_t: dGELU / MUL_AUX need aux");
+  } else if (epi == mft::GEMM_EPI_DGELU || epi == mft::GEMM_EPI_MUL_AUX || epi == mft::GEMM_EPI_BIAS_ADD) {
+    TORCH_CHECK(aux.has_value(), "gemm_t: dGELU / MUL_AUX / BIAS_ADD need aux");
     X = *aux;
   }
   if (X.defined()) TORCH_CHECK(X.size(0) == M && X.size(1) == N && X.stride(1) == 1 && X.stride(0) % 8 == 0, "gemm_t: aux shape");
-  if (epi == mft::GEMM_EPI_BIAS || epi == mft::GEMM_EPI_BIAS_GELU || epi == mft::GEMM_EPI_BIAS_GELU_D)
+  if (epi == mft::GEMM_EPI_BIAS || epi == mft::GEMM_EPI_BIAS_GELU || epi == mft::GEMM_EPI_BIAS_GELU_D ||
+      epi == mft::GEMM_EPI_BIAS_ADD)
     TORCH_CHECK(bias.has_value() && bias->numel() == N && bias->scalar_type() == torch::kBFloat16, "gemm_t: bf16 bias [N]");
   mft::GemmArgs a{};
   a.A = bp(A); a.lda = A.stride(0);

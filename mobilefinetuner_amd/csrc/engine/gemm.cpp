@@ -53,6 +53,19 @@ void map_line(const char* op, long M, long N, long K, const char* backend) {
   if (seen.emplace(b, true).second) std::fprintf(stderr, "%s\n", b);
 }
 
+const char* epi_name(int epi) {
+  switch (epi) {
+    case ::mft::GEMM_EPI_NONE: return "epi none";
+    case ::mft::GEMM_EPI_BIAS: return "epi bias";
+    case ::mft::GEMM_EPI_BIAS_GELU_D: return "epi bias+gelu (+gelu')";
+    case ::mft::GEMM_EPI_MUL_AUX: return "epi x aux";
+    case ::mft::GEMM_EPI_DGELU: return "epi x gelu'(aux)";
+    case ::mft::GEMM_EPI_LORA: return "epi lora";
+    case ::mft::GEMM_EPI_BIAS_ADD: return "epi bias+resid";
+    default: return "epi other";
+  }
+}
+
 hipblasLtHandle_t lt_handle() {
   static std::mutex mu;
   static std::unordered_map<int, hipblasLtHandle_t> hs;
@@ -215,18 +228,28 @@ bool rowmajor2(const Tensor& t) { return t.dim() == 2 && t.stride(1) == 1; }
 
 }  // namespace
 
-// MFT_GEMM4=0 keeps every GEMM off gemm4 (A/B); MFT_GEMM4=all also routes the epilogues that only tie
+// MFT_GEMM4=0 keeps every GEMM off gemm4 (A/B)
 bool gemm4_route(int epi, bool b_kn, long M, long N, long K, long lda, long ldb) {
   static const int mode = [] {
     const char* e = std::getenv("MFT_GEMM4");
-    return !e ? 1 : e[0] == '0' ? 0 : std::string(e) == "all" ? 2 : 1;
+    return !e ? 1 : e[0] == '0' ? 0 : 1;
   }();
   if (mode == 0 || b_kn || deterministic() || !::mft::gemm4_supported((int)M, (int)N, (int)K, false, false)) return false;
   if (lda % 8 || ldb % 8) return false;
-  if (epi == ::mft::GEMM_EPI_MUL_AUX || epi == ::mft::GEMM_EPI_DGELU) return true;
-  if (mode == 2 && (epi == ::mft::GEMM_EPI_BIAS_GELU_D || epi == ::mft::GEMM_EPI_NONE || epi == ::mft::GEMM_EPI_BIAS))
-    return true;
-  return false;
+  // every epilogue gemm4 carries is faster there than on gemm8 (profiles/r5_gemm4_nt_stores.txt)
+  return epi == ::mft::GEMM_EPI_MUL_AUX || epi == ::mft::GEMM_EPI_DGELU || epi == ::mft::GEMM_EPI_BIAS_GELU_D ||
+         epi == ::mft::GEMM_EPI_NONE || epi == ::mft::GEMM_EPI_BIAS || epi == ::mft::GEMM_EPI_BIAS_ADD;
+}
+
+// plain NT forwards (bias / fused residual) and the W^T data gradients on gemm4: MFT_NT=gemm4 (default)
+bool nt_gemm4() {
+  static const bool v = [] {
+    const char* e = std::getenv("MFT_NT");
+    const char* g = std::getenv("MFT_GEMM4");
+    if (g && g[0] == '0') return false;
+    return !e || std::string(e) == "gemm4";
+  }();
+  return v;
 }
 
 bool gemm8_all() {
@@ -273,10 +296,11 @@ void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c,
   // gemm4 (the 4-wave hand-scheduled persistent kernel, kernels/gemm4.hip) where it beats gemm8:
   // the MUL_AUX / dGELU data gradient (+11 % at the GPT-2 MLP shape, profiles/r5_gemm4_epilogues.txt)
   if (gemm4_route(epi, b_kn, M, N, K, g.lda, g.ldb)) {
-    map_line("gemm4", M, N, K, ::mft::GEMM_EPI_MUL_AUX == epi ? "mul_aux" : "epi");
+    map_line(epi_name(epi), M, N, K, "gemm4");
     ::mft::gemm4x(g, epi, false, false, current_stream());
     return;
   }
+  map_line(epi_name(epi), M, N, K, b_kn ? "gemm8 NN" : "gemm8");
   ::mft::gemm8x(g, epi, false, b_kn, current_stream());
 }
 
@@ -322,6 +346,21 @@ void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y, c
   const bool g8_ok = K % 64 == 0 && N % 8 == 0 && x2.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 &&
                      y.stride(0) % 8 == 0 && ::mft::gemm8_supported((int)M, (int)N, (int)K, false, false);
   if (!g8_ok) return run_lt();
+  if (nt_gemm4() && !deterministic() && ::mft::gemm4_supported((int)M, (int)N, (int)K, false, false)) {
+    ::mft::GemmArgs g = args_for(x2, w, y);
+    g.M = (int)M;
+    g.N = (int)N;
+    g.K = (int)K;
+    if (bias.defined()) g.bias = (const ::mft::bf16_t*)bias.data_ptr();
+    if (resid.defined()) {
+      g.aux = (::mft::bf16_t*)resid.data_ptr();
+      g.ldaux = resid.stride(0);
+    }
+    map_line(resid.defined() ? "nt+resid" : "nt", M, N, K, "gemm4");
+    ::mft::gemm4x(g, resid.defined() ? ::mft::GEMM_EPI_BIAS_ADD : bias.defined() ? ::mft::GEMM_EPI_BIAS : ::mft::GEMM_EPI_NONE,
+                  false, false, current_stream());
+    return;
+  }
   // Static routing (no timing, identical on every rank and rerun): a PLAIN GEMM (no fused epilogue
   // beyond the bias) is a library GEMM -> hipBLASLt; every fused-epilogue GEMM (GELU, dGELU, LoRA,
   // LM-head cross entropy, split-K weight gradients) is the hand-written gemm8.  MFT_NT=gemm8|lt or
@@ -338,8 +377,21 @@ void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y, c
   return g8 ? run_g8() : run_lt();
 }
 
-void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out) {
+void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out, const Tensor& wt) {
   const long N = w.size(0), M = dy2.size(0), K = w.size(1);
+  // a resident transposed copy of a frozen weight (Param::transposed) turns the data gradient into an
+  // NT GEMM for gemm4 (the hand-scheduled kernel reads K-contiguous operands only)
+  if (wt.defined() && nt_gemm4() && !deterministic() && rowmajor2(wt) && wt.size(0) == K && wt.size(1) == N &&
+      dy2.stride(0) % 8 == 0 && wt.stride(0) % 8 == 0 && out.stride(0) % 8 == 0 &&
+      ::mft::gemm4_supported((int)M, (int)K, (int)N, false, false)) {
+    ::mft::GemmArgs g = args_for(dy2, wt, out);
+    g.M = (int)M;
+    g.N = (int)K;
+    g.K = (int)N;
+    map_line("nn (W^T)", M, K, N, "gemm4");
+    ::mft::gemm4x(g, ::mft::GEMM_EPI_NONE, false, false, current_stream());
+    return;
+  }
   auto run_g8 = [&]() { gemm8_call(dy2, w, true, ::mft::GEMM_EPI_NONE, out); };
   auto run_lt = [&]() {
     Problem p;  // out^T [K, M] = W^T [K, N] . dy^T [N, M]
@@ -427,6 +479,7 @@ void blas_gemm(const Tensor& a, bool ta, const Tensor& b, bool tb, Tensor& c, fl
   const long M = ta ? a.size(1) : a.size(0), K = ta ? a.size(0) : a.size(1);
   const long N = tb ? b.size(0) : b.size(1);
   MFT_CHECK((tb ? b.size(1) : b.size(0)) == K && c.size(0) == M && c.size(1) == N, "blas_gemm: shapes");
+  map_line(ta ? (tb ? "blas TT" : "blas TN") : (tb ? "blas NT" : "blas NN"), M, N, K, "hipBLASLt");
   Problem p;
   p.dev = cur_dev();
   p.ta = tb;  // col-major A' = B^T stored as b (row-major [K,N] == col-major [N,K])

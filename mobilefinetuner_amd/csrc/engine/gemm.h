@@ -15,7 +15,7 @@ namespace eng {
 // y[M, N] = x[M, K] . W[N, K]^T (+ bias[N]); bf16; y row-major (may be a row-strided view)
 void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y, const Tensor& resid = Tensor());
 // out[M, K] = dy[M, N] . W[N, K]   (data gradient; out may be a row-strided view)
-void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out);
+void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out, const Tensor& wt = Tensor());
 // buf[N, K] (fp32) += alpha * dy[M, N]^T . x[M, K]
 void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha = 1.f);
 // gemm8 with one of the fused epilogues of csrc/kernels.h (GEMM_EPI_*): C = epi(alpha op(A) op(B));
@@ -31,6 +31,7 @@ void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c,
 // generic (fp32 or bf16, any transposes) C = alpha op(A) op(B) + beta C through hipBLASLt
 void blas_gemm(const Tensor& a, bool ta, const Tensor& b, bool tb, Tensor& c, float alpha = 1.f, float beta = 0.f);
 bool gemm8_all();
+bool nt_gemm4();
 bool deterministic();
 void set_deterministic(bool on);
 // hipBLASLt per-shape algorithm autotuning (timing the heuristic's candidates) on / off; multi-rank

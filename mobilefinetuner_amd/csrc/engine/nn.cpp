@@ -464,7 +464,7 @@ Tensor linear_p(const Tensor& x, Param& w, Param* b) {
       Tensor dy2 = g[0].reshape({-1, N});
       if (dy2.stride(1) != 1 || dy2.stride(0) % 8) dy2 = dy2.contiguous();
       Tensor dx = empty({dy2.size(0), K}, DType::BF16, dy2.device());
-      gemm_nn(dy2, pw->c, dx);
+      gemm_nn(dy2, pw->c, dx, !pw->trainable() && !pw->streamed ? pw->transposed() : Tensor());
       if (pw->trainable()) {
         Tensor buf = grad_buffer(pw->leaf).view({N, K});
         gemm_wgrad(buf, dy2, x2);
@@ -504,7 +504,7 @@ Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2, con
       if (!p2->trainable() && !p2->streamed) gemm8_call(dy2, p2->transposed(), false, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
       else gemm8_call(dy2, p2->c, true, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
       Tensor dx = empty({M, K}, DType::BF16, dy2.device());
-      gemm_nn(dpre, p1->c, dx);
+      gemm_nn(dpre, p1->c, dx, !p1->trainable() && !p1->streamed ? p1->transposed() : Tensor());
       if (p2->trainable()) {
         Tensor b2v = grad_buffer(p2->leaf).view({N, I});
         gemm_wgrad(b2v, dy2, h);
@@ -757,7 +757,7 @@ Tensor lora_linear(const Tensor& x, Param& w, Param* b, std::vector<LoraAdapter>
       Tensor dy2 = g[0].reshape({M, N});
       if (dy2.stride(1) != 1 || dy2.stride(0) % 8) dy2 = dy2.contiguous();
       Tensor dx = empty({M, K}, DType::BF16, dy2.device());
-      gemm_nn(dy2, pw->c, dx);
+      gemm_nn(dy2, pw->c, dx, !pw->streamed ? pw->transposed() : Tensor());
       for (size_t i = 0; i < pads->size(); ++i) {
         auto& a = (*pads)[i];
         ::mft::LoraDrop d{drop_ctr.defined() ? drop_ctr.data<int64_t>() : nullptr, a.salt, training ? a.dropout : 0.f};

@@ -6,6 +6,8 @@
 // Infinity Cache is written by the LM-head GEMM, read twice here and consumed by the dgrad GEMM
 // without a round trip to HBM (see ops/lm_head.py for the chunking).
 #include "common.h"
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace mft {
@@ -374,7 +376,12 @@ void lm_head_ce(const CeArgs& a, hipStream_t st) {
   f.C = a.E; f.ldc = a.lde;
   f.M = a.M; f.N = a.Vpad; f.K = a.K; f.alpha = 1.f;
   f.ce_labels = a.labels; f.ce_stats = L.stats; f.ce_lbl = L.lbl; f.ce_V = a.V;
-  gemm8x(f, GEMM_EPI_CE_FWD, false, false, st);
+  // the logits GEMM + CE epilogue on gemm4 (4-wave hand-scheduled kernel) where it runs; MFT_CE_G4=0 -> gemm8
+  const bool ce_g4 = !(getenv("MFT_CE_G4") && getenv("MFT_CE_G4")[0] == '0');
+  if (ce_g4 && gemm4_supported(a.M, a.Vpad, a.K, false, false) && a.ldh % 8 == 0 && a.ldw % 8 == 0)
+    gemm4x(f, GEMM_EPI_CE_FWD, false, false, st);
+  else
+    gemm8x(f, GEMM_EPI_CE_FWD, false, false, st);
   const bool fused = grad && !a.materialize;
   const int nk = (a.Vpad + 63) / 64, tps = ((nk + S - 1) / S) / 4;
   {

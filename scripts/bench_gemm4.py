@@ -15,7 +15,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mobilefinetuner_amd._ext import native
 
-EPI_NONE, EPI_BIAS, EPI_DGELU, EPI_GELU_D, EPI_MUL_AUX = 0, 1, 3, 9, 10
+EPI_NONE, EPI_BIAS, EPI_DGELU, EPI_GELU_D, EPI_MUL_AUX, EPI_BIAS_ADD = 0, 1, 3, 9, 10, 11
 
 
 def gelu_and_grad(x):
@@ -41,11 +41,14 @@ def check_epilogues(C, dev, shapes):
         C.gemm_t(x, w, False, False, EPI_MUL_AUX, None, aux, 1.0, y2, None, None, 4)
         y3 = torch.empty_like(y)
         C.gemm_t(x, w, False, False, EPI_DGELU, None, aux, 1.0, y3, None, None, 4)
+        y4 = aux.clone()  # residual added in place (aux aliases the output, as the engine's fused residual may)
+        C.gemm_t(x, w, False, False, EPI_BIAS_ADD, b, y4, 1.0, y4, None, None, 4)
         torch.cuda.synchronize()
         r = lambda a, ref: ((a.float() - ref).abs().max() / ref.abs().max()).item()
-        errs = (r(y, gl), r(d, gd), r(y2, mm * aux.float()), r(y3, mm * gelu_and_grad(aux.float())[1]))
-        print(f"{name:22s} epilogues gelu {errs[0]:.1e} gelu' {errs[1]:.1e} mul_aux {errs[2]:.1e} dgelu {errs[3]:.1e}",
-              flush=True)
+        errs = (r(y, gl), r(d, gd), r(y2, mm * aux.float()), r(y3, mm * gelu_and_grad(aux.float())[1]),
+                r(y4, mm + b.float() + aux.float()))
+        print(f"{name:22s} epilogues gelu {errs[0]:.1e} gelu' {errs[1]:.1e} mul_aux {errs[2]:.1e} dgelu {errs[3]:.1e}"
+              f" bias_add {errs[4]:.1e}", flush=True)
         assert max(errs) < 2e-2, (name, errs)
         del pre, gl, gd, mm
         fl = 2.0 * M * N * K
@@ -67,7 +70,7 @@ def check_epilogues(C, dev, shapes):
                 t = statistics.median(ts)
                 line += f" | {tag} g{impl} {t:7.1f} us {fl / t / 1e6:5.0f} TF"
         print(line, flush=True)
-        del x, w, aux, y, d, y2, y3
+        del x, w, aux, y, d, y2, y3, y4
 
 SHAPES = {
     "8192^3": (8192, 8192, 8192),

@@ -1,0 +1,82 @@
+"""gemm4 (kernels/gemm4.hip: 4-wave hand-scheduled persistent MFMA GEMM, the product path for NT GEMMs)
+against plain PyTorch fp32 on the same bf16 operands, for every epilogue it carries, on ragged shapes
+(M, N not multiples of the 256 x 256 tile, the minimum K = 128, the augmented-K 832) -- the tails go
+through the range-checked loads and stores."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+NONE, BIAS, DGELU, GELU_D, MUL_AUX, BIAS_ADD = 0, 1, 3, 9, 10, 11
+SHAPES = [(300, 264, 128), (1000, 776, 832), (4096, 3072, 768), (257, 8, 192), (2048, 640, 2048)]
+
+
+def _gelu(x):
+    t = torch.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3))
+    return 0.5 * x * (1 + t), 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * x * x)
+
+
+def _ops(M, N, K, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) * 0.1).bfloat16()
+    b = (torch.rand(N, device="cuda", generator=g) - 0.5).bfloat16()
+    aux = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    return x, w, b, aux
+
+
+def _rel(a, ref):
+    return ((a.float() - ref).abs().max() / ref.abs().max().clamp(min=1e-6)).item()
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm4_epilogues_match_fp32(M, N, K):
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    x, w, b, aux = _ops(M, N, K)
+    mm = x.float() @ w.float().t()
+    pre = mm + b.float()
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    C.gemm_t(x, w, False, False, NONE, None, None, 1.0, y, None, None, 4)
+    assert _rel(y, mm) < 1e-2
+    C.gemm_t(x, w, False, False, BIAS, b, None, 1.0, y, None, None, 4)
+    assert _rel(y, pre) < 1e-2
+    d = torch.empty_like(y)
+    C.gemm_t(x, w, False, False, GELU_D, b, d, 1.0, y, None, None, 4)
+    gl, gd = _gelu(pre)
+    assert _rel(y, gl) < 2e-2 and _rel(d, gd) < 2e-2
+    C.gemm_t(x, w, False, False, MUL_AUX, None, aux, 1.0, y, None, None, 4)
+    assert _rel(y, mm * aux.float()) < 2e-2
+    C.gemm_t(x, w, False, False, DGELU, None, aux, 1.0, y, None, None, 4)
+    assert _rel(y, mm * _gelu(aux.float())[1]) < 2e-2
+    r = aux.clone()  # fused residual, in place (aux aliases the output)
+    C.gemm_t(x, w, False, False, BIAS_ADD, b, r, 1.0, r, None, None, 4)
+    assert _rel(r, pre + aux.float()) < 2e-2
+    torch.cuda.synchronize()
+
+
+def test_gemm4_row_strided_output_and_alpha():
+    """Output written into a column slice of a wider buffer (row stride > N), alpha != 1: columns outside
+    the slice stay untouched."""
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    M, N, K = 700, 512, 256
+    x, w, b, _ = _ops(M, N, K, seed=3)
+    buf = torch.full((M, N + 64), 7.0, device="cuda", dtype=torch.bfloat16)
+    y = buf[:, :N]
+    C.gemm_t(x, w, False, False, BIAS, b, None, 0.5, y, None, None, 4)
+    torch.cuda.synchronize()
+    assert _rel(y, 0.5 * (x.float() @ w.float().t()) + b.float()) < 1e-2
+    assert (buf[:, N:] == 7.0).all()
+
+
+def test_gemm4_is_deterministic():
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    x, w, b, _ = _ops(3000, 2304, 768, seed=5)
+    y1 = torch.empty(3000, 2304, device="cuda", dtype=torch.bfloat16)
+    y2 = torch.empty_like(y1)
+    C.gemm_t(x, w, False, False, BIAS, b, None, 1.0, y1, None, None, 4)
+    C.gemm_t(x, w, False, False, BIAS, b, None, 1.0, y2, None, None, 4)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)

@@ -114,3 +114,22 @@ def test_lm_head_ce_vocab_split_dgrad_matches_unsplit(M, K, V, Vpad, forced, mon
         assert ((dh.float() - ref_dh).norm() / ref_dh.norm()).item() < 1e-2
     assert ((dh2.float() - dh1.float()).norm() / dh1.float().norm()).item() < 1e-2
     assert dh2[labels < 0].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("M,K,V,Vpad", [(8192, 768, 50257, 50304), (1000, 768, 50257, 50304), (4096, 640, 262144, 262144),
+                                        (777, 128, 70001, 70016)])
+def test_lm_head_ce_gemm4_forward_matches_gemm8(M, K, V, Vpad, monkeypatch):
+    """The CE forward on gemm4 (default where supported) against gemm8's CE epilogue (MFT_CE_G4=0): the same
+    per-row losses (fp32 statistics of the same bf16 products), the same E operand up to bf16 rounding,
+    and dh against fp32."""
+    h, W, labels = _case(M, K, V, Vpad, 2.0, seed=11)
+    l4, dh4, E4 = _fused(h, W, labels, V, materialize=False)
+    monkeypatch.setenv("MFT_CE_G4", "0")
+    l8, dh8, E8 = _fused(h, W, labels, V, materialize=False)
+    monkeypatch.delenv("MFT_CE_G4")
+    _, ref_dh, _ = _ref(h, W, labels, V)
+    torch.cuda.synchronize()
+    assert abs(l4.item() - l8.item()) < 1e-4 * max(1.0, abs(l8.item())), (l4.item(), l8.item())
+    assert ((E4.float() - E8.float()).abs().max()).item() < 1e-2
+    assert ((dh4.float() - ref_dh).norm() / ref_dh.norm()).item() < 1e-2
+    assert dh4[labels < 0].abs().max().item() == 0.0
