@@ -54,6 +54,10 @@ CONFIGS = {
     # Gemma-3 270M LoRA r=8 seq 256 (RMSNorm / QK-norm+RoPE / GQA / sliding-window kernels)
     "gemma3-270m-lora": dict(model="gemma3-270m", mode="lora", batch=256, seq=256, targets="full", engine="native",
                              metric="tokens/sec Gemma-3-270M LoRA r=8 seq256 (training, whole job)"),
+    # Gemma-3 1B LoRA r=8 seq 256 (the reference's larger Gemma preset, README.md:411: 26 layers,
+    # d 1152, 4 q-heads / 1 KV head of 256, vocab 262144)
+    "gemma3-1b-lora": dict(model="gemma3-1b", mode="lora", batch=128, seq=256, targets="full", engine="native",
+                           metric="tokens/sec Gemma-3-1B LoRA r=8 seq256 (training, whole job)"),
     # GPT-2 small full fine-tuning, DP over RCCL (bucketed, backward-overlapped all-reduce).  Micro-
     # batches (profiles/r3_fullbatch_ab.txt, one MI355X): gpt2-full 512 x 128 1.046M tok/s, 1024 x 128
     # 1.075M (97 GB peak); GPT-2 XL ZeRO-3 64 x 128 70.6K, 128 x 128 84.8K, 256 x 128 87.1K (210 GB

@@ -9,6 +9,11 @@ host offload.
 """
 __version__ = "0.1.0"
 
-import torch  # noqa: F401  (the extension links libtorch / libamdhip64: load them first)
 
-from ._ext import native  # noqa: F401
+def __getattr__(name):
+    # lazy: `python -m mobilefinetuner_amd._build --native` (the torch-free engine + CLIs) must not import
+    # torch; native() loads torch before the extension that links it
+    if name == "native":
+        from ._ext import native
+        return native
+    raise AttributeError(f"module 'mobilefinetuner_amd' has no attribute {name!r}")

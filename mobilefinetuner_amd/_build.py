@@ -10,6 +10,7 @@ a source or header changed (content hash), so the ``.so`` travels with the repo 
 GPU box.  Usage::
 
     python -m mobilefinetuner_amd._build            # build (parallel)
+    python -m mobilefinetuner_amd._build --native   # kernels + engine + native CLIs only (no torch import)
     python -m mobilefinetuner_amd._build --clean
 """
 from __future__ import annotations
@@ -120,9 +121,38 @@ def _compile_one(src: str, kind: str, flags, hdr_digest: str, verbose: bool, tag
     return obj, True
 
 
+def build_native(verbose: bool = False, jobs: int | None = None, abi: int | None = None) -> list:
+    """The torch-free part alone: every HIP kernel, the runtime and the libmft engine, linked into the
+    native CLIs (mobilefinetuner_amd/bin/).  Imports nothing from torch; the C++ ABI of the objects is
+    the one torch was built with (recorded by the last full build, else MFT_CXX11_ABI, default 1) so the
+    same objects serve _C.so."""
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    if abi is None:
+        abi = int(os.environ.get("MFT_CXX11_ABI", _recorded_abi()))
+    hdr = _headers_digest()
+    hip, cpp, _ = _sources()
+    jobs = jobs or min(8, max(1, (os.cpu_count() or 4)))
+    work = [(s, "hip") for s in hip] + [(s, "cpp") for s in cpp]
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = [f.result()[0] for f in [ex.submit(_compile_one, s, k, _flags(k, [], abi), hdr, verbose) for s, k in work]]
+    return build_engine(objs_kernels=[o for (s, k), o in zip(work, objs) if k == "hip"],
+                        objs_runtime=[o for (s, k), o in zip(work, objs) if k == "cpp"], abi=abi, hdr=hdr,
+                        verbose=verbose, jobs=jobs)
+
+
+def _recorded_abi() -> str:
+    try:
+        with open(os.path.join(BUILD_DIR, "torch_abi.txt")) as f:
+            return f.read().strip() or "1"
+    except OSError:
+        return "1"
+
+
 def build(verbose: bool = False, jobs: int | None = None) -> str:
     os.makedirs(BUILD_DIR, exist_ok=True)
     incs, libdir, abi = _torch_paths()
+    with open(os.path.join(BUILD_DIR, "torch_abi.txt"), "w") as f:
+        f.write(str(abi))
     hdr = _headers_digest()
     hip, cpp, binding = _sources()
     work = [(s, "hip") for s in hip] + [(s, "cpp") for s in cpp] + [(s, "binding") for s in binding]
@@ -154,7 +184,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
 
 def build_engine(objs_kernels, objs_runtime, abi, hdr, verbose=False, jobs=None) -> list:
     """Compile the torch-free libmft engine and link the native CLIs into mobilefinetuner_amd/bin/
-    against the same kernel / runtime objects as _C.so (hipBLASLt + HIP runtime from ROCm)."""
+    against the same kernel / runtime objects as _C.so (HIP runtime + RCCL from ROCm; no GEMM library)."""
     os.makedirs(BIN_DIR, exist_ok=True)
     ehip, ecpp, apps = _engine_sources()
     work = [(s, "hip", []) for s in ehip] + [(s, "cpp", []) for s in ecpp]
@@ -176,7 +206,7 @@ def build_engine(objs_kernels, objs_runtime, abi, hdr, verbose=False, jobs=None)
     for exe, (obj, _) in aobjs.items():
         path = os.path.join(BIN_DIR, exe)
         if changed or not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(o) for o in libs):
-            cmd = [HIPCC, "-fPIC", obj, *libs, "-o", path + ".tmp", f"-L{ROCM}/lib", "-lhipblaslt", "-lrccl", "-lamdhip64",
+            cmd = [HIPCC, "-fPIC", obj, *libs, "-o", path + ".tmp", f"-L{ROCM}/lib", "-lrccl", "-lamdhip64",
                    "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM}/lib", "-ldl", "-lpthread"]
             if verbose:
                 print(" ".join(cmd), flush=True)
@@ -193,11 +223,15 @@ def main(argv=None):
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--native", action="store_true", help="the torch-free kernels + engine + CLIs only (no _C.so)")
     a = ap.parse_args(argv)
     if a.clean:
         shutil.rmtree(os.path.join(REPO_DIR, "build"), ignore_errors=True)
         if os.path.exists(OUT_SO):
             os.remove(OUT_SO)
+    if a.native:
+        print("\n".join(build_native(verbose=a.verbose, jobs=a.jobs)))
+        return
     print(build(verbose=a.verbose, jobs=a.jobs))
 
 

@@ -1,11 +1,13 @@
-// libmft engine: GEMM front-end -- routes every matrix product to the hand-written gfx950 MFMA
-// kernels (csrc/kernels/gemm8.hip: 256x256x64 8-phase pipeline, NT / NN / TN, fused epilogues) or,
-// for plain library-shaped products where it measured faster, to hipBLASLt called directly
-// (autotuned plans, no torch).  Replaces the reference's naive/cblas matmul (core/ops.cpp:486-802)
-// and MatmulBackward (core/backward_functions.cpp:94-138).  Routing (bench_gemm_t.py on MI355X):
-//   * fused epilogues (bias+GELU, x GELU'(pre), rank-r LoRA update) and NN data-grads: gemm8;
-//   * plain NT forwards y = x W^T + b: hipBLASLt (gemm8 0.74-0.93x there); MFT_GEMM8_ALL=1 -> gemm8;
-//   * fp32 weight-grad accumulation: gemm8 split-K TN for <= 2304x768 outputs, hipBLASLt beyond.
+// libmft engine: GEMM front-end -- every matrix product on a hand-written gfx950 kernel, no vendor GEMM
+// library.  Replaces the reference's naive/cblas matmul (core/ops.cpp:486-802) and MatmulBackward
+// (core/backward_functions.cpp:94-138).  Routing (static: identical on every rank and rerun;
+// MFT_GEMM_MAP=1 prints it, profiles/r5_gemm_routing_map.txt):
+//   * K-contiguous products -- NT forwards (+ bias, + fused residual), every fused NT epilogue (bias +
+//     GELU / GELU', x aux, x GELU'(aux)), the LM-head CE forward, and data gradients through a
+//     transposed weight: gemm4 (csrc/kernels/gemm4.hip, 4-wave hand-scheduled persistent kernel);
+//   * token-major layouts -- split-K TN weight gradients, NN data gradients, the CE dgrad, the LoRA
+//     epilogue: gemm8 (csrc/kernels/gemm8.hip, 8-phase pipeline, ds_read_b64_tr_b16);
+//   * anything else (fp32, K % 64 != 0, unaligned strides): the SIMT fallback (kernels/gemm_simt.hip).
 #pragma once
 #include "engine/tensor.h"
 
@@ -28,15 +30,14 @@ struct Gemm8Extra {
   float alpha = 1.f;
 };
 void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c, const Gemm8Extra& ex = {});
-// generic (fp32 or bf16, any transposes) C = alpha op(A) op(B) + beta C through hipBLASLt
+// generic (fp32 or bf16, any transposes) C = alpha op(A) op(B) + beta C (gemm4 / gemm8 / SIMT fallback)
 void blas_gemm(const Tensor& a, bool ta, const Tensor& b, bool tb, Tensor& c, float alpha = 1.f, float beta = 0.f);
 bool gemm8_all();
 bool nt_gemm4();
 bool deterministic();
 void set_deterministic(bool on);
-// hipBLASLt per-shape algorithm autotuning (timing the heuristic's candidates) on / off; multi-rank
-// apps turn it off so every rank runs the same algorithms (an explicit MFT_LT_TUNE overrides)
-void set_lt_autotune(bool on);
+void set_lt_autotune(bool on);  // no-op (no library GEMM to tune); kept for the apps' comm setup
+bool gemm4_on();                // MFT_GEMM4=0 -> gemm8 for every product (A/B)
 
 }  // namespace eng
 }  // namespace mft

@@ -128,6 +128,26 @@ int gemm8_pick_ksplit(int M, int N, int K);
 // MFT_GEMM8_STREAM=1); A/B switch for benchmarks
 void gemm8_set_stream(int on);
 void gemm8_set_stagger(int cycles);  // first-round stagger (cycles per XCD slot), A/B
+// generic SIMT fallback (gemm_simt.hip): D = alpha op(A) op(B) (+ bias[N]) + beta Cin; fp32 or bf16
+// operands (x_f32 flags), fp32 accumulation; ta: A stored [K, M]; tb: B stored [N, K]
+struct SimtGemmArgs {
+  const void* A;
+  long lda;
+  int a_f32, ta;
+  const void* B;
+  long ldb;
+  int b_f32, tb;
+  void* D;
+  long ldd;
+  int d_f32;
+  const void* Cin;
+  long ldcin;
+  int cin_f32;
+  const bf16_t* bias;
+  int M, N, K;
+  float alpha, beta;
+};
+void gemm_simt(const SimtGemmArgs& a, hipStream_t st);
 void gemm_splitk_reduce(const float* ws, int ksplit, int M, int N, float* C, long ldc, float alpha, int accumulate,
                         hipStream_t st);
 

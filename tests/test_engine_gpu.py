@@ -95,11 +95,65 @@ def _python_losses(model, tmp, steps, B, S, lr):
     return out
 
 
+def _oracle_trajectory(model, tmp, steps, B, S, lr):
+    """The fp32 oracle (tests/oracle host ops): the fixture's weights (bf16 values, exact in fp32) and
+    adapter in an fp32 CPU model, trained with torch.optim.AdamW + global-norm clipping on the same
+    batches and schedule; returns (per-step losses, adapter state)."""
+    from mobilefinetuner_amd.data.wikitext2 import LMDataset, WT2Config
+    from mobilefinetuner_amd.io.lora_checkpoint import lora_state
+    from mobilefinetuner_amd.models.gpt2 import GPT2Config, GPT2Model
+    from mobilefinetuner_amd.optim.schedules import gpt2_cli_lr
+    from mobilefinetuner_amd.peft.lora import LoraSpec, inject_gpt2, lora_parameters
+    cpu = GPT2Model(GPT2Config.preset("gpt2"), dtype=torch.float32, device="cpu", init=False)
+    inject_gpt2(cpu, LoraSpec(rank=8, alpha=16))
+    with torch.no_grad():
+        src = dict(model.named_parameters())
+        for n, p in cpu.named_parameters():
+            p.copy_(src[n].detach().float().cpu())
+    params = [p for _, p in lora_parameters(cpu)]
+    opt = torch.optim.AdamW(params, lr=lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0)
+    ds = LMDataset.from_pretokenized(WT2Config(pretokenized_path=os.path.join(tmp, "tokens.bin"), seq_len=S,
+                                               seed=42), "train")
+    out = []
+    for i in range(steps):
+        for gr in opt.param_groups:
+            gr["lr"] = gpt2_cli_lr(i, lr, 0, steps)
+        b = ds.next_batch(B)
+        opt.zero_grad(set_to_none=True)
+        loss = cpu(b["input_ids"], b["targets"])
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+        out.append(float(loss.item()))
+    return out, lora_state(cpu)[0]
+
+
+def _update_dev(init, ref, got):
+    """rel L2 between two adapters' updates (trained - initial), over every tensor together"""
+    num = den = 0.0
+    for k in ref:
+        d_ref = ref[k].float().cpu() - init[k].float()
+        d_got = got[k].float().cpu() - init[k].float()
+        num += float((d_ref - d_got).pow(2).sum())
+        den += float(d_ref.pow(2).sum())
+    assert den > 0, "no update applied"
+    return (num / den) ** 0.5
+
+
 def test_native_cli_matches_python_path(tmp_path):
+    """10 LoRA steps of the native CLI against the fp32 oracle's trajectory (losses and the adapter update),
+    at a bound set by bf16 rounding itself: the PyTorch-driven bf16 GPU stack trains the same steps, and
+    the native engine may deviate from fp32 by at most 1.5x what that other bf16 implementation does
+    (+ a 1e-3 loss / 1e-2 update floor) -- a drift in the native path shows, rounding alone does not."""
     S, B, steps, lr = 128, 16, 10, 1e-3
     tmp = str(tmp_path)
     model, lora = _make_fixture(tmp, S)
+    from mobilefinetuner_amd.io import safetensors as st
+    from mobilefinetuner_amd.io.lora_checkpoint import lora_state
+    init = st.load_file(lora)
+    ora, ora_state = _oracle_trajectory(model, tmp, steps, B, S, lr)
     py = _python_losses(model, tmp, steps, B, S, lr)
+    py_state = lora_state(model)[0]
     metrics = os.path.join(tmp, "native.jsonl")
     out_lora = os.path.join(tmp, "native_lora.safetensors")
     cmd = [_bin("gpt2_lora_finetune"), "--pretrained_dir", tmp, "--resume_from", lora, "--pretokenized_path",
@@ -109,28 +163,21 @@ def test_native_cli_matches_python_path(tmp_path):
     print(r.stdout[-3000:], r.stderr[-2000:])
     assert r.returncode == 0
     nat = [json.loads(line)["loss"] for line in open(metrics)]
+    print("fp32  :", ora)
     print("python:", py)
     print("native:", nat)
     assert len(nat) == steps
+    nat_state = st.load_file(out_lora)
+    assert sorted(ora_state) == sorted(nat_state) == sorted(py_state)
+    d_py, d_nat = _update_dev(init, ora_state, py_state), _update_dev(init, ora_state, nat_state)
+    l_py = max(abs(a - b) for a, b in zip(py, ora))
+    l_nat = max(abs(a - b) for a, b in zip(nat, ora))
+    print(f"vs fp32: loss max|d| python {l_py:.2e} native {l_nat:.2e}; update rel L2 python {d_py:.3e} native {d_nat:.3e}")
+    assert l_nat <= 1.5 * l_py + 1e-3, (l_nat, l_py)
+    assert d_nat <= 1.5 * d_py + 1e-2, (d_nat, d_py)
+    # and the two bf16 paths still see the same per-step losses
     for a, b in zip(py, nat):
         assert abs(a - b) < 2e-3, (py, nat)
-    # the trained adapters agree too: the update each path applied (trained - initial) matches
-    from mobilefinetuner_amd.io import safetensors as st
-    from mobilefinetuner_amd.io.lora_checkpoint import lora_state
-    init, mine, theirs = st.load_file(lora), lora_state(model)[0], st.load_file(out_lora)
-    assert sorted(mine) == sorted(theirs)
-    num = den = 0.0
-    for k in mine:
-        d_py = mine[k].float() - init[k].float()
-        d_nat = theirs[k].float() - init[k].float()
-        num += float((d_py - d_nat).pow(2).sum())
-        den += float(d_py.pow(2).sum())
-    assert den > 0, "no update applied"
-    # Two bf16 implementations with different rounding points: the native engine adds the residual stream
-    # inside the projection GEMMs' epilogue (fp32 sum, one bf16 rounding), the Python path rounds the branch
-    # output to bf16 before the add.  Adam's normalisation amplifies that on small-gradient elements over
-    # 10 steps (measured 0.062; both paths match the fp32 oracle in tests/test_parity_full_gpu.py).
-    assert (num / den) ** 0.5 < 0.08, (num / den) ** 0.5
 
 
 def test_native_lora_checkpoint_bytes_match_python(tmp_path):

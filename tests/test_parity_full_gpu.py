@@ -188,7 +188,10 @@ def test_gpt2_124m_step_matches_fp32(tmp_path, lora):
     _compare("native", ref, {k: v for k, v in nat.items()})
 
 
-def test_gemma3_270m_lora_step_matches_fp32(tmp_path):
+@pytest.mark.parametrize("preset", ["gemma3-270m", "gemma3-1b"])
+def test_gemma3_lora_step_matches_fp32(tmp_path, preset):
+    """Both published Gemma-3 sizes at full size (the 1B preset: 26 layers, d 1152, I 6912; reference
+    README.md:411 and graph/test_gemma_forward.cpp:96-134 check the forward of the real model)."""
     from mobilefinetuner_amd.io import safetensors as st
     from mobilefinetuner_amd.io.lora_checkpoint import save_lora
     from mobilefinetuner_amd.models.gemma3 import Gemma3Config, Gemma3Model
@@ -196,7 +199,7 @@ def test_gemma3_270m_lora_step_matches_fp32(tmp_path):
     from mobilefinetuner_amd.peft.lora import LoraSpec, inject_gemma, lora_parameters, parse_gemma_targets
     from mobilefinetuner_amd.utils.params import FlatParams
     tmp = str(tmp_path)
-    cfg = Gemma3Config.preset("gemma3-270m")
+    cfg = Gemma3Config.preset(preset)
     cpu = Gemma3Model(cfg, dtype=torch.float32, device="cpu", seed=5)
     with torch.no_grad():
         for n, p in cpu.named_parameters():
