@@ -554,6 +554,27 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
 //   A: a_t ? [K, M] : [M, K];  B: b_t ? [K, N] : [N, K];  C [M, N] (bf16, or fp32 += for F32ACC)
 // F32ACC with a_t && b_t is the TN weight gradient: split over K into fp32 slabs + deterministic
 // reduce when the output has few 256x256 tiles.
+// out[M, N] = A[M, K] B[N, K]^T + A2[M, K2] B2[N, K2]^T on gemm4 (second K segment; the LoRA data-gradient
+// form of engine/nn.cpp)
+void gemm4_seg2(Tensor A, Tensor B, Tensor A2, Tensor B2, Tensor out) {
+  CHECK_CUDA(A); CHECK_BF16(A); CHECK_BF16(B); CHECK_BF16(A2); CHECK_BF16(B2); CHECK_BF16(out);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A2.dim() == 2 && B2.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
+              A2.stride(1) == 1 && B2.stride(1) == 1 && out.stride(1) == 1, "gemm4_seg2: row-contiguous 2-D operands");
+  const int M = A.size(0), K = A.size(1), N = B.size(0), K2 = A2.size(1);
+  TORCH_CHECK(B.size(1) == K && A2.size(0) == M && B2.size(0) == N && B2.size(1) == K2 && out.size(0) == M &&
+              out.size(1) == N, "gemm4_seg2: shapes");
+  TORCH_CHECK(mft::gemm4_supported(M, N, K, false, false) && K2 % 64 == 0 && K2 > 0, "gemm4_seg2: K, K2 % 64, N % 8");
+  c10::DeviceGuard g(A.device());
+  mft::GemmArgs a{};
+  a.A = bp(A); a.lda = A.stride(0);
+  a.B = bp(B); a.ldb = B.stride(0);
+  a.C = out.data_ptr(); a.ldc = out.stride(0);
+  a.A2 = bp(A2); a.lda2 = A2.stride(0);
+  a.B2 = bp(B2); a.ldb2 = B2.stride(0);
+  a.M = M; a.N = N; a.K = K; a.K2 = K2; a.alpha = 1.f;
+  mft::gemm4x(a, mft::GEMM_EPI_NONE, false, false, stream());
+}
+
 std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, c10::optional<Tensor> bias,
                            c10::optional<Tensor> aux, double alpha, c10::optional<Tensor> out,
                            c10::optional<Tensor> lora_u, c10::optional<Tensor> lora_w, int64_t impl) {
@@ -682,6 +703,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_wgrad_multi", &lora_wgrad_multi);
   m.def("lora_merge", &lora_merge);
   m.def("lora_dy", &lora_dy);
+  m.def("gemm4_seg2", &gemm4_seg2, "out = A B^T + A2 B2^T on gemm4 (second K segment)");
   m.def("gemm_t", &gemm_t, py::arg("A"), py::arg("B"), py::arg("a_t"), py::arg("b_t"), py::arg("epi"),
         py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("alpha") = 1.0, py::arg("out") = py::none(),
         py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none(), py::arg("impl") = 0);

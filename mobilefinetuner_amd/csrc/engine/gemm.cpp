@@ -159,6 +159,33 @@ void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c,
 }
 
 
+bool lora_seg2_ok(long M, long N, long K) {
+  static const bool off = std::getenv("MFT_LORA_SEG2") && std::getenv("MFT_LORA_SEG2")[0] == '0';  // A/B: gemm8 LORA
+  return !off && gemm4_on() && ::mft::gemm4_supported((int)M, (int)N, (int)K, false, false);
+}
+
+void gemm_nt_seg2(const Tensor& a, const Tensor& b, const Tensor& a2, const Tensor& b2, Tensor& c) {
+  MFT_CHECK(rowmajor2(a) && rowmajor2(b) && rowmajor2(a2) && rowmajor2(b2) && rowmajor2(c) && a.dtype() == DType::BF16 &&
+                b.dtype() == DType::BF16 && a2.dtype() == DType::BF16 && b2.dtype() == DType::BF16,
+            "gemm_nt_seg2: bf16 row-major operands");
+  const long M = a.size(0), K = a.size(1), N = b.size(0), K2 = a2.size(1);
+  MFT_CHECK(b.size(1) == K && a2.size(0) == M && b2.size(0) == N && b2.size(1) == K2 && c.size(0) == M && c.size(1) == N &&
+                K2 % 64 == 0 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && a2.stride(0) % 8 == 0 &&
+                b2.stride(0) % 8 == 0 && c.stride(0) % 8 == 0 && lora_seg2_ok(M, N, K),
+            "gemm_nt_seg2: shapes / strides ", a.str(), " ", b.str(), " ", a2.str(), " ", b2.str(), " -> ", c.str());
+  ::mft::GemmArgs g = args_for(a, b, c);
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.A2 = (const ::mft::bf16_t*)a2.data_ptr();
+  g.lda2 = a2.stride(0);
+  g.B2 = (const ::mft::bf16_t*)b2.data_ptr();
+  g.ldb2 = b2.stride(0);
+  g.K2 = (int)K2;
+  map_line("nt + second K segment (LoRA dgrad)", M, N, K, "gemm4");
+  ::mft::gemm4x(g, ::mft::GEMM_EPI_NONE, false, false, current_stream());
+}
+
 void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y, const Tensor& resid) {
   MFT_CHECK(rowmajor2(x2) && rowmajor2(w) && rowmajor2(y) && x2.dtype() == DType::BF16 && w.dtype() == DType::BF16,
             "gemm_nt: bf16 row-major");

@@ -30,6 +30,10 @@ struct Gemm8Extra {
   float alpha = 1.f;
 };
 void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c, const Gemm8Extra& ex = {});
+// c[M, N] = a[M, K] b[N, K]^T + a2[M, K2] b2[N, K2]^T on gemm4 (second K segment, K2 % 64 == 0): the
+// LoRA data gradient dx = dy W + v A with v zero-padded to 64 columns; lora_seg2_ok: the shape runs there
+void gemm_nt_seg2(const Tensor& a, const Tensor& b, const Tensor& a2, const Tensor& b2, Tensor& c);
+bool lora_seg2_ok(long M, long N, long K);
 // generic (fp32 or bf16, any transposes) C = alpha op(A) op(B) + beta C (gemm4 / gemm8 / SIMT fallback)
 void blas_gemm(const Tensor& a, bool ta, const Tensor& b, bool tb, Tensor& c, float alpha = 1.f, float beta = 0.f);
 bool gemm8_all();

@@ -631,7 +631,11 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
       const bool fused = nodrop && rt > 0 && rt <= 32 && rt % 8 == 0 && N % 64 == 0 && K % 8 == 0;
       Tensor dxa = empty({M, Ka}, DType::BF16, dy2.device());
       Tensor dx = dxa.slice(1, 0, K);
-      Tensor vall = empty({M, (int64_t)std::max(rt, 8)}, DType::BF16, dy2.device());
+      // gemm4 form of the fused data gradient: v (= s dy B) in the first rt of 64 columns, the rest zero, read
+      // as a second K segment against A^T (dx = dy W + v A in one pass, gemm_nt_seg2)
+      const bool seg2 = fused && gemm4_on() && Ka % 8 == 0 && lora_seg2_ok(M, K, N);
+      Tensor vall = empty({M, seg2 ? (int64_t)64 : (int64_t)std::max(rt, 8)}, DType::BF16, dy2.device());
+      if (seg2) ::mft::zero_cols(bp(vall), 64, M, rt, 64 - rt, S());
       int o = 0;
       std::vector<bool> db_done(ads.size(), false);
       for (size_t i = 0; i < ads.size(); ++i) {
@@ -657,7 +661,13 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         for (auto& a : ads) as.push_back(a.A.c);
         acat = as.size() == 1 ? as[0] : cat(as, 0);
       }
-      if (fused) {
+      if (seg2) {
+        Tensor at = empty({K, 64}, DType::BF16, dy2.device());  // A^T, zero-padded to 64 columns
+        ::mft::zero_cols(bp(at), 64, K, rt, 64 - rt, S());
+        Tensor atv = at.slice(1, 0, rt);
+        k::unary(desc(atv), desc(acat.t()), k::U_AFFINE, 1.f, 0.f, S());
+        gemm_nt_seg2(dy2, pw->transposed(), vall, at, dx);
+      } else if (fused) {
         Gemm8Extra ex;
         Tensor vu = vall.slice(1, 0, rt);
         ex.lora_u = &vu;

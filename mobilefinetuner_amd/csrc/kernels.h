@@ -114,6 +114,13 @@ struct GemmArgs {
   // cycles, spreading every XCD's CUs over a tile round so their prologue fills and epilogue
   // stores do not all hit HBM at once (MFT_G8_STAGGER, A/B)
   int stagger;
+  // gemm4 second K segment (NONE epilogue): C = A B^T + A2 B2^T, A2 [M, K2], B2 [N, K2] (row strides
+  // lda2 / ldb2, K2 % 64 == 0; 0 = none)
+  const bf16_t* A2;
+  long lda2;
+  const bf16_t* B2;
+  long ldb2;
+  int K2;
 };
 // 256x256 8-phase pipelined GEMM (gemm8.hip); same epilogues.  a_t: A stored [K, M]; b_t: B stored
 // [K, N] (NN data-grad); both: TN weight-grad (use GEMM_EPI_F32ACC with gemm8_pick_ksplit / ws)

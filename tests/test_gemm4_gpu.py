@@ -80,3 +80,22 @@ def test_gemm4_is_deterministic():
     C.gemm_t(x, w, False, False, BIAS, b, None, 1.0, y2, None, None, 4)
     torch.cuda.synchronize()
     assert torch.equal(y1, y2)
+
+
+@pytest.mark.parametrize("M,N,K,K2", [(1000, 768, 2304, 64), (4096, 768, 768, 64), (300, 264, 128, 128)])
+def test_gemm4_second_k_segment(M, N, K, K2):
+    """out = A B^T + A2 B2^T in one persistent pass (the LoRA data gradient dx = dy W + v A with v = s dy B
+    zero-padded to 64 columns)."""
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    x, w, _, _ = _ops(M, N, K, seed=9)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    a2 = torch.zeros(M, K2, device="cuda", dtype=torch.bfloat16)
+    b2 = torch.zeros(N, K2, device="cuda", dtype=torch.bfloat16)
+    a2[:, :8] = torch.randn(M, 8, device="cuda", generator=g).bfloat16()
+    b2[:, :8] = (torch.randn(N, 8, device="cuda", generator=g) * 0.1).bfloat16()
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    C.gemm4_seg2(x, w, a2, b2, y)
+    ref = x.float() @ w.float().t() + a2.float() @ b2.float().t()
+    torch.cuda.synchronize()
+    assert _rel(y, ref) < 1e-2
