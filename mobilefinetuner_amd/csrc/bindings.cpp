@@ -556,14 +556,15 @@ std::vector<Tensor> gemm_op(Tensor A, Tensor B, bool b_nn, int64_t epi, c10::opt
 // reduce when the output has few 256x256 tiles.
 // out[M, N] = A[M, K] B[N, K]^T + A2[M, K2] B2[N, K2]^T on gemm4 (second K segment; the LoRA data-gradient
 // form of engine/nn.cpp)
-void gemm4_seg2(Tensor A, Tensor B, Tensor A2, Tensor B2, Tensor out) {
+void gemm4_seg2(Tensor A, Tensor B, Tensor A2, Tensor B2, Tensor out, int64_t impl) {
   CHECK_CUDA(A); CHECK_BF16(A); CHECK_BF16(B); CHECK_BF16(A2); CHECK_BF16(B2); CHECK_BF16(out);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A2.dim() == 2 && B2.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
               A2.stride(1) == 1 && B2.stride(1) == 1 && out.stride(1) == 1, "gemm4_seg2: row-contiguous 2-D operands");
   const int M = A.size(0), K = A.size(1), N = B.size(0), K2 = A2.size(1);
   TORCH_CHECK(B.size(1) == K && A2.size(0) == M && B2.size(0) == N && B2.size(1) == K2 && out.size(0) == M &&
               out.size(1) == N, "gemm4_seg2: shapes");
-  TORCH_CHECK(mft::gemm4_supported(M, N, K, false, false) && K2 % 64 == 0 && K2 > 0, "gemm4_seg2: K, K2 % 64, N % 8");
+  TORCH_CHECK((impl == 5 ? mft::gemm_s_supported(M, N, K, 0) : mft::gemm4_supported(M, N, K, false, false)) &&
+              K2 % 64 == 0 && K2 > 0, "gemm4_seg2: K, K2 % 64, N % 8");
   c10::DeviceGuard g(A.device());
   mft::GemmArgs a{};
   a.A = bp(A); a.lda = A.stride(0);
@@ -572,7 +573,8 @@ void gemm4_seg2(Tensor A, Tensor B, Tensor A2, Tensor B2, Tensor out) {
   a.A2 = bp(A2); a.lda2 = A2.stride(0);
   a.B2 = bp(B2); a.ldb2 = B2.stride(0);
   a.M = M; a.N = N; a.K = K; a.K2 = K2; a.alpha = 1.f;
-  mft::gemm4x(a, mft::GEMM_EPI_NONE, false, false, stream());
+  if (impl == 5) mft::gemm_s(a, mft::GEMM_EPI_NONE, stream());
+  else mft::gemm4x(a, mft::GEMM_EPI_NONE, false, false, stream());
 }
 
 std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, c10::optional<Tensor> bias,
@@ -631,8 +633,12 @@ std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, 
     a.lora_w = bp(*lora_w); a.ld_lw = lora_w->stride(0);
     a.lora_r = lora_u->size(1);
   }
-  TORCH_CHECK(impl == 0 || impl == 4, "gemm_t: impl 0 (gemm8) or 4 (gemm4, hand-scheduled 4-wave kernel)");
-  if (impl == 4) {
+  TORCH_CHECK(impl == 0 || impl == 4 || impl == 5,
+              "gemm_t: impl 0 (gemm8), 4 (gemm4, hand-scheduled 4-wave kernel) or 5 (gemm_s, short-token kernel)");
+  if (impl == 5) {
+    TORCH_CHECK(!a_t && !b_t && mft::gemm_s_supported(M, N, K, (int)epi), "gemm_t: shape / epilogue not supported by gemm_s");
+    mft::gemm_s(a, (int)epi, stream());
+  } else if (impl == 4) {
     TORCH_CHECK(mft::gemm4_supported(M, N, K, a_t, b_t), "gemm_t: shape / layout not supported by gemm4");
     mft::gemm4x(a, (int)epi, a_t, b_t, stream());
   } else {
@@ -703,7 +709,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_wgrad_multi", &lora_wgrad_multi);
   m.def("lora_merge", &lora_merge);
   m.def("lora_dy", &lora_dy);
-  m.def("gemm4_seg2", &gemm4_seg2, "out = A B^T + A2 B2^T on gemm4 (second K segment)");
+  m.def("gemm4_seg2", &gemm4_seg2, "out = A B^T + A2 B2^T on gemm4 (impl 4) or gemm_s (impl 5): second K segment",
+        py::arg("A"), py::arg("B"), py::arg("A2"), py::arg("B2"), py::arg("out"), py::arg("impl") = 4);
   m.def("gemm_t", &gemm_t, py::arg("A"), py::arg("B"), py::arg("a_t"), py::arg("b_t"), py::arg("epi"),
         py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("alpha") = 1.0, py::arg("out") = py::none(),
         py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none(), py::arg("impl") = 0);

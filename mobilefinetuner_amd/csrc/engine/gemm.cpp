@@ -112,6 +112,13 @@ bool gemm4_route(int epi, bool b_kn, long M, long N, long K, long lda, long ldb)
 
 bool nt_gemm4() { return gemm4_on(); }
 
+// MFT_GEMM_S=0 keeps short-token products on gemm4 / gemm8 (A/B)
+bool short_tokens(long M, long N, long K, int epi) {
+  static const bool off = std::getenv("MFT_GEMM_S") && std::getenv("MFT_GEMM_S")[0] == '0';
+  return !off && gemm4_on() && ::mft::gemm_s_preferred((int)M, (int)N, (int)K) &&
+         ::mft::gemm_s_supported((int)M, (int)N, (int)K, epi);
+}
+
 bool gemm8_all() { return !gemm4_on(); }
 bool deterministic() { return g_det; }
 void set_lt_autotune(bool) {}  // (no library GEMM left to tune; kept for the apps' comm setup)
@@ -147,6 +154,12 @@ void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c,
     g.ld_lw = ex.lora_w->stride(0);
     g.lora_r = (int)ex.lora_u->size(1);
   }
+  // short token counts: the 64 x 64 split-K-over-waves kernel (kernels/gemm_s.hip)
+  if (!b_kn && short_tokens(M, N, K, epi) && g.ldc % 8 == 0) {
+    map_line(epi_name(epi), M, N, K, "gemm_s");
+    ::mft::gemm_s(g, epi, current_stream());
+    return;
+  }
   // gemm4 (the 4-wave hand-scheduled persistent kernel, kernels/gemm4.hip) where it beats gemm8:
   // the MUL_AUX / dGELU data gradient (+11 % at the GPT-2 MLP shape, profiles/r5_gemm4_epilogues.txt)
   if (gemm4_route(epi, b_kn, M, N, K, g.lda, g.ldb)) {
@@ -161,7 +174,8 @@ void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c,
 
 bool lora_seg2_ok(long M, long N, long K) {
   static const bool off = std::getenv("MFT_LORA_SEG2") && std::getenv("MFT_LORA_SEG2")[0] == '0';  // A/B: gemm8 LORA
-  return !off && gemm4_on() && ::mft::gemm4_supported((int)M, (int)N, (int)K, false, false);
+  return !off && gemm4_on() &&
+         (::mft::gemm4_supported((int)M, (int)N, (int)K, false, false) || short_tokens(M, N, K, ::mft::GEMM_EPI_NONE));
 }
 
 void gemm_nt_seg2(const Tensor& a, const Tensor& b, const Tensor& a2, const Tensor& b2, Tensor& c) {
@@ -182,6 +196,11 @@ void gemm_nt_seg2(const Tensor& a, const Tensor& b, const Tensor& a2, const Tens
   g.B2 = (const ::mft::bf16_t*)b2.data_ptr();
   g.ldb2 = b2.stride(0);
   g.K2 = (int)K2;
+  if (short_tokens(M, N, K, ::mft::GEMM_EPI_NONE)) {
+    map_line("nt + second K segment (LoRA dgrad)", M, N, K, "gemm_s");
+    ::mft::gemm_s(g, ::mft::GEMM_EPI_NONE, current_stream());
+    return;
+  }
   map_line("nt + second K segment (LoRA dgrad)", M, N, K, "gemm4");
   ::mft::gemm4x(g, ::mft::GEMM_EPI_NONE, false, false, current_stream());
 }
@@ -220,8 +239,9 @@ void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out, const Tensor& wt_i
   // gemm4 reads K-contiguous operands only: the data gradient dx = dy W is the NT product dy (W^T)^T with
   // the frozen weight's resident transposed copy (Param::transposed), or -- a trainable weight -- a
   // transposed copy made here (|W| bytes, ~1 % of the GEMM's own traffic at the benchmark shapes)
-  if (gemm4_on() && aligned && ::mft::gemm4_supported((int)M, (int)K, (int)N, false, false) && K % 8 == 0 &&
-      dy2.dtype() == DType::BF16 && w.dtype() == DType::BF16) {
+  const bool g4 = ::mft::gemm4_supported((int)M, (int)K, (int)N, false, false);
+  const bool gs = short_tokens(M, K, N, ::mft::GEMM_EPI_NONE);
+  if (gemm4_on() && aligned && (g4 || gs) && K % 8 == 0 && dy2.dtype() == DType::BF16 && w.dtype() == DType::BF16) {
     Tensor wt = wt_in;
     if (!wt.defined() || !rowmajor2(wt) || wt.stride(0) % 8) {
       NoGradGuard ng;
@@ -231,8 +251,9 @@ void gemm_nn(const Tensor& dy2, const Tensor& w, Tensor& out, const Tensor& wt_i
     g.M = (int)M;
     g.N = (int)K;
     g.K = (int)N;
-    map_line(wt_in.defined() ? "nn (resident W^T)" : "nn (W^T copy)", M, K, N, "gemm4");
-    ::mft::gemm4x(g, ::mft::GEMM_EPI_NONE, false, false, current_stream());
+    map_line(wt_in.defined() ? "nn (resident W^T)" : "nn (W^T copy)", M, K, N, gs ? "gemm_s" : "gemm4");
+    if (gs) ::mft::gemm_s(g, ::mft::GEMM_EPI_NONE, current_stream());
+    else ::mft::gemm4x(g, ::mft::GEMM_EPI_NONE, false, false, current_stream());
     return;
   }
   if (aligned && w.stride(0) % 8 == 0 && N % 64 == 0 && K % 8 == 0 && dy2.dtype() == DType::BF16 &&

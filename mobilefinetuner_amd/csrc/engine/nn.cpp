@@ -635,7 +635,7 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
       // as a second K segment against A^T (dx = dy W + v A in one pass, gemm_nt_seg2)
       const bool seg2 = fused && gemm4_on() && Ka % 8 == 0 && lora_seg2_ok(M, K, N);
       Tensor vall = empty({M, seg2 ? (int64_t)64 : (int64_t)std::max(rt, 8)}, DType::BF16, dy2.device());
-      if (seg2) ::mft::zero_cols(bp(vall), 64, M, rt, 64 - rt, S());
+      bool v_padded = false;  // lora_dy zeroes the padding itself (one adapter of rank 8)
       int o = 0;
       std::vector<bool> db_done(ads.size(), false);
       for (size_t i = 0; i < ads.size(); ++i) {
@@ -646,9 +646,11 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         if (dB.defined() && a.rank == 8 && a.ncols % 8 == 0 && a.col0 % 8 == 0 && (K + o) % 8 == 0) {
           Tensor vpart = empty({(int64_t)((a.ncols + 255) / 256) * M * 8}, DType::F32, dy2.device());
           Tensor dw = det_ws(::mft::lora_dy_ws_floats(M, a.ncols));
+          const int vz = seg2 && ads.size() == 1 ? 64 - rt : 0;
           ::mft::lora_dy(bp(dys), dys.stride(0), bp(a.B.c), a.B.c.stride(0), bp(xa2) + K + o, xa2.stride(0), fp(dB),
-                         a.ncols, fp(vpart), bp(v), v.stride(0), M, a.ncols, s, S(), dptr(dw));
+                         a.ncols, fp(vpart), bp(v), v.stride(0), M, a.ncols, s, S(), dptr(dw), vz);
           db_done[i] = true;
+          v_padded = vz > 0;
         } else {
           ::mft::lora_rowdot(bp(dys), dys.stride(0), bp(a.B.c), a.B.c.stride(0), bp(v), v.stride(0), M, a.ncols,
                              a.rank, s, ::mft::LoraDrop{nullptr, 0, 0.f}, S());
@@ -662,8 +664,9 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         acat = as.size() == 1 ? as[0] : cat(as, 0);
       }
       if (seg2) {
-        Tensor at = empty({K, 64}, DType::BF16, dy2.device());  // A^T, zero-padded to 64 columns
-        ::mft::zero_cols(bp(at), 64, K, rt, 64 - rt, S());
+        if (!v_padded) ::mft::zero_cols(bp(vall), 64, M, rt, 64 - rt, S());
+        Tensor& at = pw->lora_at;  // A^T, zero-padded to 64 columns (persistent: the padding stays zero)
+        if (!at.defined() || at.size(0) != K) at = zeros({K, 64}, DType::BF16, dy2.device());
         Tensor atv = at.slice(1, 0, rt);
         k::unary(desc(atv), desc(acat.t()), k::U_AFFINE, 1.f, 0.f, S());
         gemm_nt_seg2(dy2, pw->transposed(), vall, at, dx);

@@ -129,6 +129,12 @@ void gemm8x(const GemmArgs& g, int epi, bool a_t, bool b_t, hipStream_t st);
 // 256x256x64 4-wave GEMM with a hand-scheduled K-tile body (gemm4.hip); NT layout
 void gemm4x(const GemmArgs& g, int epi, bool a_t, bool b_t, hipStream_t st);
 bool gemm4_supported(int M, int N, int K, bool a_t, bool b_t);
+// short-token NT GEMM (gemm_s.hip): 64 x 64 tiles, K split over the 4 waves; NONE / BIAS / BIAS_GELU_D /
+// MUL_AUX / DGELU / BIAS_ADD and the second K segment (K2, NONE only).  gemm_s_preferred: the shape's
+// gemm4 tiles would fill less than half the CUs
+bool gemm_s_supported(int M, int N, int K, int epi);
+bool gemm_s_preferred(int M, int N, int K);
+void gemm_s(const GemmArgs& g, int epi, hipStream_t st);
 bool gemm8_supported(int M, int N, int K, bool a_t, bool b_t);
 int gemm8_pick_ksplit(int M, int N, int K);
 // NT NONE / BIAS / BIAS_GELU_D: the persistent streaming form with the deferred epilogue (opt-in,
@@ -277,7 +283,7 @@ long lora_wgrad_ws_floats(long M, int K, int R);
 // rank 8, one pass over dy [M, N]:  dB[r*ldd + n] += s * sum_m u[m, r] dy[m, n]  (fp32 atomics) and
 // v[m*ldv + r] = s * sum_n dy[m, n] B[r, n]  (bf16); vpart = fp32 scratch of cdiv(N, 256) * M * 8
 void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,
-             float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st, float* det_ws = nullptr);
+             float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st, float* det_ws = nullptr, int vzero = 0);
 long lora_dy_ws_floats(long M, int N);  // deterministic-mode workspace of lora_dy (det_ws)
 // workgroups of the lora_dy / lora_xty (MFMA) grids for an [M, N] operand: <= 512, one resident round
 long lora_dy_grid_blocks(long M, int N);

@@ -425,13 +425,17 @@ __global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restric
 }
 
 // v[m, r] = s * sum over strips of vpart[strip, m, r]   (bf16 out, row stride ldv)
+// vz > 0: also zero v's columns 8 .. 8 + vz - 1 (vz % 8 == 0; 16-B stores, ldv % 8 == 0) -- the zero padding
+// of the gemm4 second K segment (engine/nn.cpp), without a launch of its own
 __global__ void lora_dy_finish_kernel(const float* __restrict__ vpart, int nstrip, long M, float s, bf16_t* __restrict__ v,
-                                      long ldv) {
+                                      long ldv, int vz) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= M * 8) return;
   float a = 0.f;
   for (int k = 0; k < nstrip; ++k) a += vpart[(long)k * M * 8 + t];
   v[(t >> 3) * ldv + (t & 7)] = f2bf(a * s);
+  const int c = (int)(t & 7);
+  if (c >= 1 && 8 * c < 8 + vz) *reinterpret_cast<uint4*>(v + (t >> 3) * ldv + 8 * c) = uint4{0u, 0u, 0u, 0u};
 }
 
 __global__ void lora_dy_reduce_kernel(const float* __restrict__ ws, int ny, int N, long np, float* __restrict__ dB,
@@ -463,7 +467,7 @@ long lora_dy_ws_floats(long M, int N) { return dy_chunks(M, N, nullptr) * 8L * c
 long lora_dy_grid_blocks(long M, int N) { return dy_chunks(M, N, nullptr) * cdiv(N, 256); }
 
 void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,
-             float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st, float* det_ws) {
+             float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st, float* det_ws, int vzero) {
   if ((N % 8) || (ldy % 8) || (ldb % 8) || (ldu % 8) || (reinterpret_cast<uintptr_t>(dy) % 16) ||
       (reinterpret_cast<uintptr_t>(B) % 16) || (reinterpret_cast<uintptr_t>(u) % 16)) {
     fprintf(stderr, "lora_dy: N and the row strides must be multiples of 8, dy/B/u 16-B aligned\n");
@@ -477,7 +481,11 @@ void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t
   dim3 grid(gx, (unsigned)ny);
   lora_dy_kernel<<<grid, 256, 0, st>>>(dy, ldy, B, ldb, u, ldu, dB, ldd, vpart, M, N, chunk, s, det_ws, np,
                                        gx == 1 ? v : nullptr, ldv);
-  if (gx > 1) lora_dy_finish_kernel<<<cdiv(M * 8, 256), 256, 0, st>>>(vpart, gx, M, s, v, ldv);
+  if (gx > 1) {
+    lora_dy_finish_kernel<<<cdiv(M * 8, 256), 256, 0, st>>>(vpart, gx, M, s, v, ldv, vzero);
+  } else if (vzero > 0) {
+    zero_cols(v, ldv, M, 8, vzero, st);
+  }
   if (det_ws) lora_dy_reduce_kernel<<<cdiv(8L * N, 256), 256, 0, st>>>(det_ws, (int)ny, N, np, dB, ldd);
 }
 

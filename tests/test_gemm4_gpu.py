@@ -29,33 +29,35 @@ def _rel(a, ref):
     return ((a.float() - ref).abs().max() / ref.abs().max().clamp(min=1e-6)).item()
 
 
+@pytest.mark.parametrize("impl", [4, 5], ids=["gemm4", "gemm_s"])
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_gemm4_epilogues_match_fp32(M, N, K):
+def test_gemm4_epilogues_match_fp32(M, N, K, impl):
     from mobilefinetuner_amd._ext import native
     C = native()
     x, w, b, aux = _ops(M, N, K)
     mm = x.float() @ w.float().t()
     pre = mm + b.float()
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    C.gemm_t(x, w, False, False, NONE, None, None, 1.0, y, None, None, 4)
+    C.gemm_t(x, w, False, False, NONE, None, None, 1.0, y, None, None, impl)
     assert _rel(y, mm) < 1e-2
-    C.gemm_t(x, w, False, False, BIAS, b, None, 1.0, y, None, None, 4)
+    C.gemm_t(x, w, False, False, BIAS, b, None, 1.0, y, None, None, impl)
     assert _rel(y, pre) < 1e-2
     d = torch.empty_like(y)
-    C.gemm_t(x, w, False, False, GELU_D, b, d, 1.0, y, None, None, 4)
+    C.gemm_t(x, w, False, False, GELU_D, b, d, 1.0, y, None, None, impl)
     gl, gd = _gelu(pre)
     assert _rel(y, gl) < 2e-2 and _rel(d, gd) < 2e-2
-    C.gemm_t(x, w, False, False, MUL_AUX, None, aux, 1.0, y, None, None, 4)
+    C.gemm_t(x, w, False, False, MUL_AUX, None, aux, 1.0, y, None, None, impl)
     assert _rel(y, mm * aux.float()) < 2e-2
-    C.gemm_t(x, w, False, False, DGELU, None, aux, 1.0, y, None, None, 4)
+    C.gemm_t(x, w, False, False, DGELU, None, aux, 1.0, y, None, None, impl)
     assert _rel(y, mm * _gelu(aux.float())[1]) < 2e-2
     r = aux.clone()  # fused residual, in place (aux aliases the output)
-    C.gemm_t(x, w, False, False, BIAS_ADD, b, r, 1.0, r, None, None, 4)
+    C.gemm_t(x, w, False, False, BIAS_ADD, b, r, 1.0, r, None, None, impl)
     assert _rel(r, pre + aux.float()) < 2e-2
     torch.cuda.synchronize()
 
 
-def test_gemm4_row_strided_output_and_alpha():
+@pytest.mark.parametrize("impl", [4, 5], ids=["gemm4", "gemm_s"])
+def test_gemm4_row_strided_output_and_alpha(impl):
     """Output written into a column slice of a wider buffer (row stride > N), alpha != 1: columns outside
     the slice stay untouched."""
     from mobilefinetuner_amd._ext import native
@@ -64,26 +66,30 @@ def test_gemm4_row_strided_output_and_alpha():
     x, w, b, _ = _ops(M, N, K, seed=3)
     buf = torch.full((M, N + 64), 7.0, device="cuda", dtype=torch.bfloat16)
     y = buf[:, :N]
-    C.gemm_t(x, w, False, False, BIAS, b, None, 0.5, y, None, None, 4)
+    C.gemm_t(x, w, False, False, BIAS, b, None, 0.5, y, None, None, impl)
     torch.cuda.synchronize()
     assert _rel(y, 0.5 * (x.float() @ w.float().t()) + b.float()) < 1e-2
     assert (buf[:, N:] == 7.0).all()
 
 
-def test_gemm4_is_deterministic():
+@pytest.mark.parametrize("impl", [4, 5], ids=["gemm4", "gemm_s"])
+def test_gemm4_is_deterministic(impl):
     from mobilefinetuner_amd._ext import native
     C = native()
     x, w, b, _ = _ops(3000, 2304, 768, seed=5)
     y1 = torch.empty(3000, 2304, device="cuda", dtype=torch.bfloat16)
     y2 = torch.empty_like(y1)
-    C.gemm_t(x, w, False, False, BIAS, b, None, 1.0, y1, None, None, 4)
-    C.gemm_t(x, w, False, False, BIAS, b, None, 1.0, y2, None, None, 4)
+    C.gemm_t(x, w, False, False, BIAS, b, None, 1.0, y1, None, None, impl)
+    C.gemm_t(x, w, False, False, BIAS, b, None, 1.0, y2, None, None, impl)
     torch.cuda.synchronize()
     assert torch.equal(y1, y2)
 
 
-@pytest.mark.parametrize("M,N,K,K2", [(1000, 768, 2304, 64), (4096, 768, 768, 64), (300, 264, 128, 128)])
-def test_gemm4_second_k_segment(M, N, K, K2):
+@pytest.mark.parametrize("impl", [4, 5], ids=["gemm4", "gemm_s"])
+@pytest.mark.parametrize("M,N,K,K2", [(1000, 768, 2304, 64), (4096, 768, 768, 64), (300, 264, 128, 128), (512, 776, 64, 64)])
+def test_gemm4_second_k_segment(M, N, K, K2, impl):
+    if impl == 4 and K < 128:
+        pytest.skip("gemm4 needs K >= 128")
     """out = A B^T + A2 B2^T in one persistent pass (the LoRA data gradient dx = dy W + v A with v = s dy B
     zero-padded to 64 columns)."""
     from mobilefinetuner_amd._ext import native
@@ -95,7 +101,7 @@ def test_gemm4_second_k_segment(M, N, K, K2):
     a2[:, :8] = torch.randn(M, 8, device="cuda", generator=g).bfloat16()
     b2[:, :8] = (torch.randn(N, 8, device="cuda", generator=g) * 0.1).bfloat16()
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    C.gemm4_seg2(x, w, a2, b2, y)
+    C.gemm4_seg2(x, w, a2, b2, y, impl)
     ref = x.float() @ w.float().t() + a2.float() @ b2.float().t()
     torch.cuda.synchronize()
     assert _rel(y, ref) < 1e-2
