@@ -123,6 +123,24 @@ __device__ __forceinline__ void gelu_tanh_and_grad(float x, float& y, float& dy)
   dy = s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x2);
 }
 
+// Two elements at once in packed fp32 (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32 on gfx950: two lanes'
+// worth per instruction), the constants folded: 10 packed ops + 2 v_exp_f32 + 2 v_rcp_f32 per pair
+// instead of ~14 scalar ops + 2 transcendentals per element -- the GELU epilogue of the fused MLP GEMM
+// was VALU-bound at one wave per SIMD (as many cycles as the tile's MFMAs).
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void gelu_tanh_and_grad2(f32x2_t x, f32x2_t& y, f32x2_t& dy) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f, l2e = 1.4426950408889634f;
+  const f32x2_t x2 = x * x;
+  const f32x2_t in = __builtin_elementwise_fma(x2 * k1, x, x);       // x + k1 x^3
+  const f32x2_t z = in * (-2.f * k0 * l2e);                            // -2u log2(e)
+  const f32x2_t d = f32x2_t{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + 1.f;
+  const f32x2_t s = f32x2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};  // sigmoid(2u)
+  y = x * s;
+  const f32x2_t t = __builtin_elementwise_fma(-s, s, s);              // s (1 - s)
+  const f32x2_t q = __builtin_elementwise_fma(x2, f32x2_t{6.f * k0 * k1, 6.f * k0 * k1}, f32x2_t{2.f * k0, 2.f * k0});
+  dy = __builtin_elementwise_fma(x * t, q, s);                         // s + 2 k0 x s (1-s) (1 + 3 k1 x^2)
+}
+
 // d/dx: s + 2 x s (1 - s) k0 (1 + 3 k1 x^2), s = sigmoid(2u)   (0.5 (1 - tanh^2) = 2 s (1 - s))
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;

@@ -506,6 +506,7 @@ Tensor Gemma3::embed_tokens(const Tensor& ids) {
 }
 
 Tensor Gemma3::hidden(const Tensor& ids) {
+  lora_prep_step_begin();  // every LoRA layer's weight prep for this forward, one launch
   const int64_t B = ids.size(0), S = ids.size(1);
   const int H = cfg_.hidden;
   const bool st = streamer_ != nullptr;

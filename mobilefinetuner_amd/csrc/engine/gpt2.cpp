@@ -500,6 +500,7 @@ std::pair<Tensor, Tensor> GPT2::block(int i, const Tensor& x0, const Tensor& h, 
 }
 
 Tensor GPT2::hidden(const Tensor& ids) {
+  lora_prep_step_begin();  // every LoRA layer's weight prep for this forward, one launch
   const int64_t B = ids.size(0), S = ids.size(1);
   MFT_CHECK(S <= cfg_.n_positions, "sequence ", S, " exceeds n_positions ", cfg_.n_positions);
   const int C = cfg_.n_embd;

@@ -2,6 +2,7 @@
 #include "engine/nn.h"
 
 #include <cstring>
+#include <unordered_map>
 
 #include <algorithm>
 #include <cmath>
@@ -523,6 +524,74 @@ Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2, con
   return y.view(ys);
 }
 
+// ------------------------------------------------------------------ LoRA weight prep (batched)
+namespace {
+struct LoraPrep {
+  struct Item {
+    Tensor dst, src;  // (held: the batch may still write a dst its layer has dropped -- harmless)
+    ::mft::LoraPrepEntry e;
+  };
+  std::vector<Item> items;
+  std::unordered_map<const void*, size_t> by_dst;
+  ::mft::LoraPrepEntry* dev = nullptr;
+  int ndev = 0;
+  bool dirty = false;   // items changed since the upload
+  bool active = false;  // the batch ran at the start of this forward
+};
+LoraPrep& lprep() {
+  static LoraPrep p;
+  return p;
+}
+bool prep_off() {
+  static const bool off = std::getenv("MFT_LORA_PREP_BATCH") && std::getenv("MFT_LORA_PREP_BATCH")[0] == '0';
+  return off;
+}
+
+// dst = scale * src (2-D bf16 views, dst row-major): skipped when this forward's batch already wrote it
+void prep_copy(const Tensor& dst, const Tensor& src, float scale) {
+  auto& P = lprep();
+  ::mft::LoraPrepEntry e{(::mft::bf16_t*)dst.data_ptr(), (long)dst.stride(0), (const ::mft::bf16_t*)src.data_ptr(),
+                         (long)src.stride(0), (long)src.stride(1), (int)dst.size(0), (int)dst.size(1), scale};
+  auto it = P.by_dst.find(e.dst);
+  const bool same = it != P.by_dst.end() && [&] {
+    const auto& o = P.items[it->second].e;
+    return o.src == e.src && o.srs == e.srs && o.scs == e.scs && o.rows == e.rows && o.cols == e.cols &&
+           o.dld == e.dld && o.scale == e.scale;
+  }();
+  if (P.active && same && (int)it->second < P.ndev) return;  // done by the batch
+  k::unary(desc(dst), desc(src), k::U_AFFINE, scale, 0.f, S());
+  if (prep_off() || dst.dtype() != DType::BF16 || src.dtype() != DType::BF16 || dst.stride(1) != 1) return;
+  if (it == P.by_dst.end()) {
+    P.by_dst.emplace(e.dst, P.items.size());
+    P.items.push_back({dst, src, e});
+    P.dirty = true;
+  } else if (!same) {
+    P.items[it->second] = {dst, src, e};
+    P.dirty = true;
+  }
+}
+}  // namespace
+
+void lora_prep_step_begin() {
+  auto& P = lprep();
+  P.active = false;
+  if (prep_off() || P.items.empty()) return;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_OK(hipStreamIsCapturing(S(), &cap));
+  if (P.dirty) {  // (re)upload -- only outside a capture; inside one the layers make their own copies
+    if (cap != hipStreamCaptureStatusNone) return;
+    std::vector<::mft::LoraPrepEntry> es;
+    for (auto& it : P.items) es.push_back(it.e);
+    if (P.dev) HIP_OK(hipFree(P.dev));
+    HIP_OK(hipMalloc(&P.dev, es.size() * sizeof(::mft::LoraPrepEntry)));
+    HIP_OK(hipMemcpy(P.dev, es.data(), es.size() * sizeof(::mft::LoraPrepEntry), hipMemcpyHostToDevice));
+    P.ndev = (int)es.size();
+    P.dirty = false;
+  }
+  ::mft::lora_prep_batched(P.dev, P.ndev, S());
+  P.active = true;
+}
+
 // ------------------------------------------------------------------ LoRA (augmented K)
 int lora_aug_cols(int in_features, const std::vector<LoraAdapter>& ads) {
   int r = 0;
@@ -592,7 +661,7 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
     }
     // s B_i^T into the slice's rows of the augmented weight
     Tensor dst = waug.slice(0, a.col0, a.col0 + a.ncols).slice(1, off, off + R);
-    k::unary(desc(dst), desc(a.B.c.t()), k::U_AFFINE, s, 0.f, S());
+    prep_copy(dst, a.B.c.t(), s);
     off += R;
   }
   Tensor y = empty({M, N}, DType::BF16, xa.device());
@@ -668,7 +737,7 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         Tensor& at = pw->lora_at;  // A^T, zero-padded to 64 columns (persistent: the padding stays zero)
         if (!at.defined() || at.size(0) != K) at = zeros({K, 64}, DType::BF16, dy2.device());
         Tensor atv = at.slice(1, 0, rt);
-        k::unary(desc(atv), desc(acat.t()), k::U_AFFINE, 1.f, 0.f, S());
+        prep_copy(atv, acat.t(), 1.f);
         gemm_nt_seg2(dy2, pw->transposed(), vall, at, dx);
       } else if (fused) {
         Gemm8Extra ex;

@@ -70,6 +70,12 @@ struct LoraAdapter {
   float dropout = 0.f;
   uint32_t salt = 0;
 };
+// The LoRA layers' per-step weight prep (s B^T into each augmented-K weight, A^T into each padded
+// second-segment operand) as ONE batched launch at the start of a model's forward: the first forwards
+// run the copies one by one and register them; lora_prep_step_begin (at the start of a forward, outside
+// graph capture for the first time) uploads the list and from then on launches it, and each layer skips
+// the copy the batch already made (an entry whose tensors changed is simply redone by its layer).
+void lora_prep_step_begin();
 // width of the augmented input [x | u_1..u_n | 0]: in + sum(r), rounded to 64
 int lora_aug_cols(int in_features, const std::vector<LoraAdapter>& ads);
 // xa [M, Ka] holds x in its first K columns (zero tail); waug [N, Ka] = [W | s B^T.. | 0] (owned by

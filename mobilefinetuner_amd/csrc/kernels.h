@@ -263,6 +263,18 @@ struct LoraDrop {
   float p;             // 0 disables
 };
 // U[m, r] = s * sum_k X[m, k] * Wt[r, k]          (u = x A^T with Wt = A; v = s dy B^T with Wt = B)
+// every LoRA layer's per-step weight prep in ONE launch (engine/nn.cpp LoraPrep): dst[r][c] = scale * src at
+// (r * srs + c * scs) for each entry (s B^T into the augmented-K weight, A^T into the padded second-segment
+// operand); entries live in device memory, one workgroup per entry
+struct LoraPrepEntry {
+  bf16_t* dst;
+  long dld;
+  const bf16_t* src;
+  long srs, scs;
+  int rows, cols;
+  float scale;
+};
+void lora_prep_batched(const LoraPrepEntry* dev_entries, int n, hipStream_t st);
 void lora_rowdot(const bf16_t* X, long ldx, const bf16_t* Wt, long ldw, bf16_t* U, long ldu, long M, int K, int R, float s,
                  LoraDrop drop, hipStream_t st);
 // Y[m, n] = base[m, n] + s * sum_r U[m, r] * W[r, n]   (Y may alias base; y += s u B, dx += v A)

@@ -4,14 +4,15 @@
 // product is one long serial K-loop (47 us for 0.6 GFLOP, profiles/r5_kernel_tables.txt).
 //
 // Design for latency, not throughput:
-//   * 64 x 64 output tile per 256-thread workgroup, and the K-loop SPLIT ACROSS THE 4 WAVES: wave w
-//     takes K-tiles w, w + 4, ... (each a full 64 x 64 x 64 product, 4 x 4 blocks of
-//     v_mfma_f32_16x16x32_bf16), so a K = 768 product is 3 dependent K-tiles per wave, not 12;
+//   * 64 x 64 output tile per 512-thread workgroup, and the K-loop SPLIT ACROSS THE 8 WAVES: wave w
+//     takes K-tiles w, w + 8, ... (each a full 64 x 64 x 64 product, 4 x 4 blocks of
+//     v_mfma_f32_16x16x32_bf16), so a K = 768 product is 2 dependent K-tiles per wave, not 12, and each
+//     SIMD holds two waves' loads in flight;
 //   * operands straight from global memory into MFMA fragments (one 16-B load per lane per fragment:
 //     both NT operands are K-contiguous), the next K-tile's 16 fragments in flight while the current
 //     one multiplies -- no LDS staging, no barriers in the loop;
-//   * the 4 partial tiles meet once in LDS (fp32, padded rows), each wave reduces 16 rows and runs the
-//     fused epilogue on 16 contiguous columns per lane (16-B loads / stores).
+//   * the 8 partial tiles meet once in LDS (fp32, padded rows, 139 KB), each wave reduces 8 rows and
+//     runs the fused epilogue on 8 contiguous columns per lane (16-B loads / stores).
 // The MFMAs run with the operands swapped (C^T = B A^T) so each lane's accumulators are 4 contiguous
 // columns of one row.
 #include "common.h"
@@ -23,63 +24,103 @@ namespace mft {
 namespace {
 
 constexpr int kLdr = 68;  // fp32 row pitch of the reduction image (64 + 4: float4 writes spread over banks)
+constexpr int kNW = 8;    // waves per workgroup, each a 1/kNW share of the K-tiles (2 per SIMD: latency hiding)
+
 
 struct Frags {
   bf16x8_t a[2][4], b[2][4];  // [k-step][block]
 };
 
-// fragments of K-tile kt (64 columns) for the tile (m0, n0): A rows m0 + 16 i + (l & 15), B rows
-// n0 + 16 j + (l & 15), columns 32 ks + 8 (l >> 4) .. + 7; rows past M / N read the last row
-__device__ __forceinline__ void load_frags(Frags& f, const bf16_t* A, long lda, const bf16_t* B, long ldb, int m0,
-                                           int n0, int M, int N, int k0) {
-  const int l = threadIdx.x & 63, r = l & 15, c = k0 + 8 * (l >> 4);
+// fragments of one K-tile (64 columns) through range-checked buffer descriptors: A rows m0 + 16 i + (l & 15),
+// B rows n0 + 16 j + (l & 15), columns k0 + 32 ks + 8 (l >> 4) .. + 7.  Rows past M / N, and a whole K-tile
+// moved out of range by its scalar offset (a wave's tiles past its last), read as zeros -- no branch and
+// no clamp around any load, so the compiler keeps the next K-tile's loads in flight under the MFMAs.
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void load_frags(Frags& f, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb,
+                                           const uint32_t (&oa)[4], const uint32_t (&ob)[4], uint32_t soff) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int ra = min(m0 + 16 * i + r, M - 1), rb = min(n0 + 16 * i + r, N - 1);
-      f.a[ks][i] = *reinterpret_cast<const bf16x8_t*>(A + (long)ra * lda + c + 32 * ks);
-      f.b[ks][i] = *reinterpret_cast<const bf16x8_t*>(B + (long)rb * ldb + c + 32 * ks);
+      f.a[ks][i] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(ra, oa[i] + 64 * ks, soff, 0));
+      f.b[ks][i] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(rb, ob[i] + 64 * ks, soff, 0));
     }
 }
 
+// in-place MFMA ("+a": the builtin lets the register allocator rename every accumulator block each K-tile
+// and then copy them back at the loop head -- 112 v_accvgpr moves per trip).  Each block is accumulated
+// once per k-step with 15 other MFMAs between, and the epilogue's first AGPR read waits behind s_nops.
 __device__ __forceinline__ void mma(f32x4_t (&acc)[4][4], const Frags& f) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(f.b[ks][j], f.a[ks][i], acc[i][j]);
+      for (int j = 0; j < 4; ++j)
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(f.b[ks][j]), "v"(f.a[ks][i]));
 }
 
 template <int EPI, bool SEG2>
-__global__ __launch_bounds__(256) void gemm_s_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][64 rows][kLdr]
+__global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [kNW waves][64 rows][kLdr]
   const int tiles_n = (g.N + 63) / 64;
   const int m0 = (blockIdx.x / tiles_n) * 64, n0 = (blockIdx.x % tiles_n) * 64;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // (uniform: scalar loop)
   const int nk = g.K / 64, nkt = nk + (SEG2 ? g.K2 / 64 : 0);
   f32x4_t acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
-  auto load = [&](Frags& f, int kt) {
-    if (SEG2 && kt >= nk) load_frags(f, g.A2, g.lda2, g.B2, g.ldb2, m0, n0, g.M, g.N, (kt - nk) * 64);
-    else load_frags(f, g.A, g.lda, g.B, g.ldb, m0, n0, g.M, g.N, kt * 64);
+  // the wave's it-th K-tile is w + 4 it; past its last one the loads are out of range (zeros: a multiply
+  // that adds nothing), so the MFMA chain is unconditional and the accumulators stay in place
+  const int n_my = w < nkt ? (nkt - w + kNW - 1) / kNW : 0;
+  auto rsrc = [](const bf16_t* p, long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p), (short)0,
+                                             (int)__builtin_amdgcn_readfirstlane((uint32_t)min(bytes, 0x7fff0000L)),
+                                             0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t ra1 = rsrc(g.A + (long)m0 * g.lda, (long)(g.M - m0) * g.lda * 2);
+  const __amdgpu_buffer_rsrc_t rb1 = rsrc(g.B + (long)n0 * g.ldb, (long)(g.N - n0) * g.ldb * 2);
+  __amdgpu_buffer_rsrc_t ra2 = ra1, rb2 = rb1;
+  if constexpr (SEG2) {
+    ra2 = rsrc(g.A2 + (long)m0 * g.lda2, (long)(g.M - m0) * g.lda2 * 2);
+    rb2 = rsrc(g.B2 + (long)n0 * g.ldb2, (long)(g.N - n0) * g.ldb2 * 2);
+  }
+  uint32_t oa1[4], ob1[4], oa2[4], ob2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 16 * i + (l & 15), c = 8 * (l >> 4);
+    oa1[i] = (uint32_t)((r * g.lda + c) * 2), ob1[i] = (uint32_t)((r * g.ldb + c) * 2);
+    if constexpr (SEG2) oa2[i] = (uint32_t)((r * g.lda2 + c) * 2), ob2[i] = (uint32_t)((r * g.ldb2 + c) * 2);
+  }
+  auto load = [&](Frags& f, int it) {  // (selects only: a branch here would make the compiler wait early)
+    const int kt = w + kNW * it;
+    const bool s2 = SEG2 && kt >= nk;
+    const uint32_t off = (it < n_my && !g.stagger ? 0u : 0x7fff0000u) + (uint32_t)(s2 ? kt - nk : min(kt, nk - 1)) * 128u;
+    if constexpr (SEG2) {
+      uint32_t oa[4], ob[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) oa[i] = s2 ? oa2[i] : oa1[i], ob[i] = s2 ? ob2[i] : ob1[i];
+      load_frags(f, s2 ? ra2 : ra1, s2 ? rb2 : rb1, oa, ob, off);
+    } else {
+      load_frags(f, ra1, rb1, oa1, ob1, off);
+    }
   };
   Frags f0, f1;
-  int kt = w;
-  if (kt < nkt) load(f0, kt);
-  while (kt < nkt) {  // two K-tiles per trip: one in flight while the other multiplies
-    if (kt + 4 < nkt) load(f1, kt + 4);
+  load(f0, 0);
+  // (sched_barrier: the scheduler would otherwise sink each load next to its first use -- load, wait, MFMA)
+  for (int it = 0; it < n_my; it += 2) {  // two K-tiles per trip: one in flight while the other multiplies
+    load(f1, it + 1);
+    __builtin_amdgcn_sched_barrier(0);
     mma(acc, f0);
-    kt += 4;
-    if (kt >= nkt) break;
-    if (kt + 4 < nkt) load(f0, kt + 4);
+    __builtin_amdgcn_sched_barrier(0);
+    load(f0, it + 2);
+    __builtin_amdgcn_sched_barrier(0);
     mma(acc, f1);
-    kt += 4;
+    __builtin_amdgcn_sched_barrier(0);
   }
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // last MFMA -> AGPR reads
   // partial tile of this wave -> LDS: lane holds row 16 i + (l & 15), columns 16 j + 4 (l >> 4) .. + 3
   float* mine = red + w * 64 * kLdr;
 #pragma unroll
@@ -88,59 +129,52 @@ __global__ __launch_bounds__(256) void gemm_s_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j)
       *reinterpret_cast<f32x4_t*>(mine + (16 * i + (l & 15)) * kLdr + 16 * j + 4 * (l >> 4)) = acc[i][j];
   __syncthreads();
-  // wave w reduces rows 16 w .. + 15: lane -> row 16 w + (l >> 2), columns 16 (l & 3) .. + 15
-  const int rt = 16 * w + (l >> 2), ct = 16 * (l & 3);
+  // wave w reduces rows 8 w .. + 7: lane -> row 8 w + (l >> 3), columns 8 (l & 7) .. + 7
+  const int rt = 8 * w + (l >> 3), ct = 8 * (l & 7);
   const int row = m0 + rt, col = n0 + ct;
-  float v[16];
+  float x[8];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < 2; ++q) {
     f32x4_t s = *reinterpret_cast<const f32x4_t*>(red + rt * kLdr + ct + 4 * q);
 #pragma unroll
-    for (int p = 1; p < 4; ++p) {
+    for (int p = 1; p < kNW; ++p) {
       const f32x4_t t = *reinterpret_cast<const f32x4_t*>(red + (p * 64 + rt) * kLdr + ct + 4 * q);
       s[0] += t[0], s[1] += t[1], s[2] += t[2], s[3] += t[3];
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[4 * q + e] = s[e] * g.alpha;
+    for (int e = 0; e < 4; ++e) x[4 * q + e] = s[e] * g.alpha;
   }
-  if (row >= g.M || col >= g.N) return;  // (N % 8 == 0: a lane's two 8-column halves are in or out together)
-  const bool hi_ok = col + 8 < g.N;
+  if (row >= g.M || col >= g.N) return;  // (N % 8 == 0: a lane's 8 columns are in or out together)
   constexpr bool kBias = EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU_D || EPI == GEMM_EPI_BIAS_ADD;
   constexpr bool kAux = EPI == GEMM_EPI_MUL_AUX || EPI == GEMM_EPI_DGELU || EPI == GEMM_EPI_BIAS_ADD;
+  if constexpr (kBias) {
+    float b[8];
+    load8(g.bias + col, b);
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (h == 1 && !hi_ok) break;
-    float* x = v + 8 * h;
-    const int c = col + 8 * h;
-    if constexpr (kBias) {
-      float b[8];
-      load8(g.bias + c, b);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] += b[e];
-    }
-    if constexpr (kAux) {
-      float a[8];
-      load8(g.aux + (long)row * g.ldaux + c, a);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        if constexpr (EPI == GEMM_EPI_MUL_AUX) x[e] *= a[e];
-        else if constexpr (EPI == GEMM_EPI_DGELU) x[e] *= gelu_tanh_grad(a[e]);
-        else x[e] += a[e];
-      }
-    }
-    if constexpr (EPI == GEMM_EPI_BIAS_GELU_D) {
-      float d[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) gelu_tanh_and_grad(x[e], x[e], d[e]);
-      store8(g.aux + (long)row * g.ldaux + c, d);
-    }
-    store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + c, x);
+    for (int e = 0; e < 8; ++e) x[e] += b[e];
   }
+  if constexpr (kAux) {
+    float a[8];
+    load8(g.aux + (long)row * g.ldaux + col, a);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if constexpr (EPI == GEMM_EPI_MUL_AUX) x[e] *= a[e];
+      else if constexpr (EPI == GEMM_EPI_DGELU) x[e] *= gelu_tanh_grad(a[e]);
+      else x[e] += a[e];
+    }
+  }
+  if constexpr (EPI == GEMM_EPI_BIAS_GELU_D) {
+    float d[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gelu_tanh_and_grad(x[e], x[e], d[e]);
+    store8(g.aux + (long)row * g.ldaux + col, d);
+  }
+  store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, x);
 }
 
 template <int EPI, bool SEG2>
 void launch_s(const GemmArgs& g, hipStream_t st) {
-  constexpr size_t shm = 4 * 64 * kLdr * sizeof(float);
+  constexpr size_t shm = kNW * 64 * kLdr * sizeof(float);
   static bool attr = false;
   if (!attr) {
     MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_s_kernel<EPI, SEG2>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -148,7 +182,7 @@ void launch_s(const GemmArgs& g, hipStream_t st) {
     attr = true;
   }
   const int tiles = ((g.M + 63) / 64) * ((g.N + 63) / 64);
-  gemm_s_kernel<EPI, SEG2><<<tiles, 256, shm, st>>>(g);
+  gemm_s_kernel<EPI, SEG2><<<tiles, 64 * kNW, shm, st>>>(g);
 }
 
 }  // namespace
@@ -172,6 +206,12 @@ void gemm_s(const GemmArgs& g, int epi, hipStream_t st) {
     abort();
   }
   if (g.K2 > 0) return launch_s<GEMM_EPI_NONE, true>(g, st);
+  static const int diag = getenv("MFT_GS_DIAG") ? atoi(getenv("MFT_GS_DIAG")) : 0;  // 1: every operand load out of range
+  if (diag) {
+    GemmArgs d = g;
+    d.stagger = 1;
+    return launch_s<GEMM_EPI_BIAS, false>(d, st);
+  }
   switch (epi) {
     case GEMM_EPI_NONE: return launch_s<GEMM_EPI_NONE, false>(g, st);
     case GEMM_EPI_BIAS: return launch_s<GEMM_EPI_BIAS, false>(g, st);

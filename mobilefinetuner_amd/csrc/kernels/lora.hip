@@ -734,4 +734,17 @@ void lora_merge(void* W, int w_is_bf16, long wsk, long wsn, const float* A, cons
     lora_merge_kernel<float><<<cdiv(n, 256), 256, 0, st>>>((float*)W, wsk, wsn, A, B, K, N, R, s);
 }
 
+__global__ __launch_bounds__(256) void lora_prep_kernel(const LoraPrepEntry* __restrict__ es) {
+  const LoraPrepEntry e = es[blockIdx.x];
+  const long n = (long)e.rows * e.cols;
+  for (long t = threadIdx.x; t < n; t += blockDim.x) {
+    const long r = t / e.cols, c = t % e.cols;
+    e.dst[r * e.dld + c] = f2bf(e.scale * bf2f(e.src[r * e.srs + c * e.scs]));
+  }
+}
+
+void lora_prep_batched(const LoraPrepEntry* dev_entries, int n, hipStream_t st) {
+  if (n > 0) lora_prep_kernel<<<n, 256, 0, st>>>(dev_entries);
+}
+
 }  // namespace mft

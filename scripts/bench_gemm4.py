@@ -82,6 +82,11 @@ SHAPES = {
     "gpt2 lm head": (32768, 50304, 768),
     "gemma gate|up fwd": (65536, 4096, 704),
     "gemma down fwd": (65536, 640, 2048),
+    # the reference recipe: 4 x 128 tokens
+    "b4 qkv fwd (aug K)": (512, 2304, 832),
+    "b4 proj fwd": (512, 768, 768),
+    "b4 fc fwd": (512, 3072, 768),
+    "b4 mproj fwd": (512, 768, 3072),
 }
 
 
@@ -92,7 +97,7 @@ def main():
     ap.add_argument("--shapes", default="all")
     ap.add_argument("--check_only", action="store_true")
     ap.add_argument("--no_check", action="store_true", help="diagnostic builds (MFT_G4_DIAG): wrong outputs")
-    ap.add_argument("--only", default="", help="comma list of kernels to time (gemm4,gemm8,hipBLASLt)")
+    ap.add_argument("--only", default="", help="comma list of kernels to time (gemm4,gemm8,gemm_s,hipBLASLt)")
     ap.add_argument("--epi", action="store_true", help="check the fused epilogues (then exit)")
     a = ap.parse_args()
     C = native()
@@ -127,6 +132,7 @@ def main():
         fns = {
             "gemm4": lambda: C.gemm_t(x, w, False, False, EPI_BIAS, b, None, 1.0, y4, None, None, 4),
             "gemm8": lambda: C.gemm_t(x, w, False, False, EPI_BIAS, b, None, 1.0, y8, None, None, 0),
+            "gemm_s": lambda: C.gemm_t(x, w, False, False, EPI_BIAS, b, None, 1.0, y8, None, None, 5),
             "hipBLASLt": lambda: torch.addmm(b, x, w.t(), out=y8),
         }
         if a.only:
