@@ -4,15 +4,14 @@
 // product is one long serial K-loop (47 us for 0.6 GFLOP, profiles/r5_kernel_tables.txt).
 //
 // Design for latency, not throughput:
-//   * 64 x 64 output tile per 512-thread workgroup, and the K-loop SPLIT ACROSS THE 8 WAVES: wave w
-//     takes K-tiles w, w + 8, ... (each a full 64 x 64 x 64 product, 4 x 4 blocks of
-//     v_mfma_f32_16x16x32_bf16), so a K = 768 product is 2 dependent K-tiles per wave, not 12, and each
-//     SIMD holds two waves' loads in flight;
+//   * 64 x 64 output tile per 256-thread workgroup, and the K-loop SPLIT ACROSS THE 4 WAVES: wave w
+//     takes K-tiles w, w + 4, ... (each a full 64 x 64 x 64 product, 4 x 4 blocks of
+//     v_mfma_f32_16x16x32_bf16), so a K = 768 product is 3 dependent K-tiles per wave, not 12;
 //   * operands straight from global memory into MFMA fragments (one 16-B load per lane per fragment:
 //     both NT operands are K-contiguous), the next K-tile's 16 fragments in flight while the current
 //     one multiplies -- no LDS staging, no barriers in the loop;
-//   * the 8 partial tiles meet once in LDS (fp32, padded rows, 139 KB), each wave reduces 8 rows and
-//     runs the fused epilogue on 8 contiguous columns per lane (16-B loads / stores).
+//   * the 4 partial tiles meet once in LDS (fp32, padded rows), each wave reduces 16 rows and runs the
+//     fused epilogue on 16 contiguous columns per lane (16-B loads / stores).
 // The MFMAs run with the operands swapped (C^T = B A^T) so each lane's accumulators are 4 contiguous
 // columns of one row.
 #include "common.h"
@@ -24,7 +23,7 @@ namespace mft {
 namespace {
 
 constexpr int kLdr = 68;  // fp32 row pitch of the reduction image (64 + 4: float4 writes spread over banks)
-constexpr int kNW = 8;    // waves per workgroup, each a 1/kNW share of the K-tiles (2 per SIMD: latency hiding)
+constexpr int kNW = 4;    // waves per workgroup, each a 1/kNW share of the K-tiles (8 measured slower: 139 KB LDS, one WG per CU)
 
 
 struct Frags {
@@ -47,17 +46,16 @@ __device__ __forceinline__ void load_frags(Frags& f, __amdgpu_buffer_rsrc_t ra, 
     }
 }
 
-// in-place MFMA ("+a": the builtin lets the register allocator rename every accumulator block each K-tile
-// and then copy them back at the loop head -- 112 v_accvgpr moves per trip).  Each block is accumulated
-// once per k-step with 15 other MFMAs between, and the epilogue's first AGPR read waits behind s_nops.
+// Builtin MFMAs (not asm): the compiler must see them to place the wait states between an MFMA still reading
+// its source VGPRs and the next write of those registers (with two waves per SIMD part of the fragments live
+// in AGPRs and are copied to VGPRs right before their MFMA -- an asm MFMA there read clobbered operands).
 __device__ __forceinline__ void mma(f32x4_t (&acc)[4][4], const Frags& f) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(f.b[ks][j]), "v"(f.a[ks][i]));
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(f.b[ks][j], f.a[ks][i], acc[i][j]);
 }
 
 template <int EPI, bool SEG2>
@@ -75,17 +73,17 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g) {
   // the wave's it-th K-tile is w + 4 it; past its last one the loads are out of range (zeros: a multiply
   // that adds nothing), so the MFMA chain is unconditional and the accumulators stay in place
   const int n_my = w < nkt ? (nkt - w + kNW - 1) / kNW : 0;
-  auto rsrc = [](const bf16_t* p, long bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p), (short)0,
-                                             (int)__builtin_amdgcn_readfirstlane((uint32_t)min(bytes, 0x7fff0000L)),
-                                             0x00020000);
-  };
-  const __amdgpu_buffer_rsrc_t ra1 = rsrc(g.A + (long)m0 * g.lda, (long)(g.M - m0) * g.lda * 2);
-  const __amdgpu_buffer_rsrc_t rb1 = rsrc(g.B + (long)n0 * g.ldb, (long)(g.N - n0) * g.ldb * 2);
-  __amdgpu_buffer_rsrc_t ra2 = ra1, rb2 = rb1;
+  // operand panels of this tile: base + byte count (rows past M / N: VGPR offsets beyond the records -> 0)
+  auto recs = [](long bytes) { return (int)__builtin_amdgcn_readfirstlane((uint32_t)min(bytes, 0x7fff0000L)); };
+  const bf16_t* pa1 = g.A + (long)m0 * g.lda;
+  const bf16_t* pb1 = g.B + (long)n0 * g.ldb;
+  const int na1 = recs((long)(g.M - m0) * g.lda * 2), nb1 = recs((long)(g.N - n0) * g.ldb * 2);
+  const bf16_t* pa2 = pa1;
+  const bf16_t* pb2 = pb1;
+  int na2 = 0, nb2 = 0;
   if constexpr (SEG2) {
-    ra2 = rsrc(g.A2 + (long)m0 * g.lda2, (long)(g.M - m0) * g.lda2 * 2);
-    rb2 = rsrc(g.B2 + (long)n0 * g.ldb2, (long)(g.N - n0) * g.ldb2 * 2);
+    pa2 = g.A2 + (long)m0 * g.lda2, pb2 = g.B2 + (long)n0 * g.ldb2;
+    na2 = recs((long)(g.M - m0) * g.lda2 * 2), nb2 = recs((long)(g.N - n0) * g.ldb2 * 2);
   }
   uint32_t oa1[4], ob1[4], oa2[4], ob2[4];
 #pragma unroll
@@ -94,23 +92,33 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g) {
     oa1[i] = (uint32_t)((r * g.lda + c) * 2), ob1[i] = (uint32_t)((r * g.ldb + c) * 2);
     if constexpr (SEG2) oa2[i] = (uint32_t)((r * g.lda2 + c) * 2), ob2[i] = (uint32_t)((r * g.ldb2 + c) * 2);
   }
+  // (the SGPR offset is not range-checked -- only the VGPR offset is -- so a K-tile past the wave's last
+  // reads through a 0-record descriptor, not through a large soffset; scalar selects of base and count,
+  // the descriptor built per load: a select between descriptor values went through scratch)
   auto load = [&](Frags& f, int it) {  // (selects only: a branch here would make the compiler wait early)
     const int kt = w + kNW * it;
-    const bool s2 = SEG2 && kt >= nk;
-    const uint32_t off = (it < n_my && !g.stagger ? 0u : 0x7fff0000u) + (uint32_t)(s2 ? kt - nk : min(kt, nk - 1)) * 128u;
+    const bool ok = it < n_my && !g.stagger, s2 = SEG2 && kt >= nk;
+    const uint32_t off = (uint32_t)(s2 ? kt - nk : min(kt, nk - 1)) * 128u;
+    const bf16_t* pa = s2 ? pa2 : pa1;
+    const bf16_t* pb = s2 ? pb2 : pb1;
+    const int na = !ok ? 0 : s2 ? na2 : na1, nb = !ok ? 0 : s2 ? nb2 : nb1;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(pa), (short)0, na, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(pb), (short)0, nb, 0x00020000);
     if constexpr (SEG2) {
       uint32_t oa[4], ob[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) oa[i] = s2 ? oa2[i] : oa1[i], ob[i] = s2 ? ob2[i] : ob1[i];
-      load_frags(f, s2 ? ra2 : ra1, s2 ? rb2 : rb1, oa, ob, off);
+      load_frags(f, ra, rb, oa, ob, off);
     } else {
-      load_frags(f, ra1, rb1, oa1, ob1, off);
+      load_frags(f, ra, rb, oa1, ob1, off);
     }
   };
+  // (sched_barrier: the scheduler would otherwise sink each load next to its first use -- load, wait, MFMA;
+  // a third K-tile in flight measured no faster and spilled: the product is bound by the MFMA time of
+  // the ~100 busy CUs and the launch / reduction floor, not by the load chain)
   Frags f0, f1;
   load(f0, 0);
-  // (sched_barrier: the scheduler would otherwise sink each load next to its first use -- load, wait, MFMA)
-  for (int it = 0; it < n_my; it += 2) {  // two K-tiles per trip: one in flight while the other multiplies
+  for (int it = 0; it < max(n_my, 1); it += 2) {  // (a wave without K-tiles multiplies zeros once: acc = 0)
     load(f1, it + 1);
     __builtin_amdgcn_sched_barrier(0);
     mma(acc, f0);
@@ -120,7 +128,6 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g) {
     mma(acc, f1);
     __builtin_amdgcn_sched_barrier(0);
   }
-  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // last MFMA -> AGPR reads
   // partial tile of this wave -> LDS: lane holds row 16 i + (l & 15), columns 16 j + 4 (l >> 4) .. + 3
   float* mine = red + w * 64 * kLdr;
 #pragma unroll
@@ -129,12 +136,13 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j)
       *reinterpret_cast<f32x4_t*>(mine + (16 * i + (l & 15)) * kLdr + 16 * j + 4 * (l >> 4)) = acc[i][j];
   __syncthreads();
-  // wave w reduces rows 8 w .. + 7: lane -> row 8 w + (l >> 3), columns 8 (l & 7) .. + 7
-  const int rt = 8 * w + (l >> 3), ct = 8 * (l & 7);
-  const int row = m0 + rt, col = n0 + ct;
-  float x[8];
+  // wave w reduces rows kRows w .. + kRows - 1: lane -> one row, kCols contiguous columns
+  constexpr int kRows = 64 / kNW, kLpr = 64 / kRows, kCols = 64 / kLpr;
+  const int rt = kRows * w + l / kLpr, ct = kCols * (l % kLpr);
+  const int row = m0 + rt;
+  float v[kCols];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < kCols / 4; ++q) {
     f32x4_t s = *reinterpret_cast<const f32x4_t*>(red + rt * kLdr + ct + 4 * q);
 #pragma unroll
     for (int p = 1; p < kNW; ++p) {
@@ -142,34 +150,44 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g) {
       s[0] += t[0], s[1] += t[1], s[2] += t[2], s[3] += t[3];
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) x[4 * q + e] = s[e] * g.alpha;
+    for (int e = 0; e < 4; ++e) v[4 * q + e] = s[e] * g.alpha;
   }
-  if (row >= g.M || col >= g.N) return;  // (N % 8 == 0: a lane's 8 columns are in or out together)
+  if (row >= g.M) return;
   constexpr bool kBias = EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU_D || EPI == GEMM_EPI_BIAS_ADD;
   constexpr bool kAux = EPI == GEMM_EPI_MUL_AUX || EPI == GEMM_EPI_DGELU || EPI == GEMM_EPI_BIAS_ADD;
-  if constexpr (kBias) {
-    float b[8];
-    load8(g.bias + col, b);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) x[e] += b[e];
-  }
-  if constexpr (kAux) {
-    float a[8];
-    load8(g.aux + (long)row * g.ldaux + col, a);
+  for (int h = 0; h < kCols / 8; ++h) {
+    const int col = n0 + ct + 8 * h;
+    if (col >= g.N) break;  // (N % 8 == 0: an 8-column group is in or out as a whole)
+    float* x = v + 8 * h;
+    if constexpr (kBias) {
+      float b[8];
+      load8(g.bias + col, b);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if constexpr (EPI == GEMM_EPI_MUL_AUX) x[e] *= a[e];
-      else if constexpr (EPI == GEMM_EPI_DGELU) x[e] *= gelu_tanh_grad(a[e]);
-      else x[e] += a[e];
+      for (int e = 0; e < 8; ++e) x[e] += b[e];
     }
-  }
-  if constexpr (EPI == GEMM_EPI_BIAS_GELU_D) {
-    float d[8];
+    if constexpr (kAux) {
+      float a[8];
+      load8(g.aux + (long)row * g.ldaux + col, a);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) gelu_tanh_and_grad(x[e], x[e], d[e]);
-    store8(g.aux + (long)row * g.ldaux + col, d);
+      for (int e = 0; e < 8; ++e) {
+        if constexpr (EPI == GEMM_EPI_MUL_AUX) x[e] *= a[e];
+        else if constexpr (EPI == GEMM_EPI_DGELU) x[e] *= gelu_tanh_grad(a[e]);
+        else x[e] += a[e];
+      }
+    }
+    if constexpr (EPI == GEMM_EPI_BIAS_GELU_D) {
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        f32x2_t y2, d2;
+        gelu_tanh_and_grad2(f32x2_t{x[e], x[e + 1]}, y2, d2);
+        x[e] = y2.x, x[e + 1] = y2.y, d[e] = d2.x, d[e + 1] = d2.y;
+      }
+      store8(g.aux + (long)row * g.ldaux + col, d);
+    }
+    store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, x);
   }
-  store8(reinterpret_cast<bf16_t*>(g.C) + (long)row * g.ldc + col, x);
 }
 
 template <int EPI, bool SEG2>
