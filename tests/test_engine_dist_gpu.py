@@ -117,7 +117,10 @@ def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
     # value in the DP export (weight decay moves every updated element): a chunk a rank never updated
     # or exported stale, or LayerNorm values a non-owning rank kept stale (fp32-compute
     # parameters under ZeRO-1/2), fail here.  (Elementwise update deltas cannot be compared tightly:
-    # parameters with a ~0 true gradient, e.g. the key bias, get noise-driven Adam steps.)
+    # parameters with a ~0 true gradient, e.g. the key bias, get noise-driven Adam steps -- and such an
+    # element may legitimately end exactly where it started in one run and not the other: bf16 moments
+    # measured one wte element the reference moved by 2.4e-6 in total (vs ~3.7e-3 for the tensor) left at
+    # its initial value, scripts/diag/z3_stale.py.  "Moved" therefore means moved by more than 1e-5.)
     init_out = str(tmp_path / "init.safetensors")
     _single("gpt2_full_finetune", [x for x in FULL if x not in ("--steps", "6")] + ["--steps", "0", "--output_path",
                                                                                        init_out], "--batch_size", 8)
@@ -125,7 +128,7 @@ def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
     wtol = 50 * tol
     for k in a:
         assert torch.allclose(a[k], b[k], atol=wtol, rtol=wtol), (extra, k, (a[k] - b[k]).abs().max())
-        moved = a[k] != w0[k]
+        moved = (a[k] - w0[k]).abs() > 1e-5
         stale = moved & (b[k] == w0[k])
         assert moved.any() and int(stale.sum()) == 0, (extra, k, int(stale.sum()), int(moved.sum()))
 
