@@ -530,6 +530,7 @@ struct LoraPrep {
   struct Item {
     Tensor dst, src;  // (held: the batch may still write a dst its layer has dropped -- harmless)
     ::mft::LoraPrepEntry e;
+    bool uploaded = false;  // the device list holds exactly this entry
   };
   std::vector<Item> items;
   std::unordered_map<const void*, size_t> by_dst;
@@ -558,15 +559,15 @@ void prep_copy(const Tensor& dst, const Tensor& src, float scale) {
     return o.src == e.src && o.srs == e.srs && o.scs == e.scs && o.rows == e.rows && o.cols == e.cols &&
            o.dld == e.dld && o.scale == e.scale;
   }();
-  if (P.active && same && (int)it->second < P.ndev) return;  // done by the batch
+  if (P.active && same && P.items[it->second].uploaded) return;  // done by the batch
   k::unary(desc(dst), desc(src), k::U_AFFINE, scale, 0.f, S());
   if (prep_off() || dst.dtype() != DType::BF16 || src.dtype() != DType::BF16 || dst.stride(1) != 1) return;
   if (it == P.by_dst.end()) {
     P.by_dst.emplace(e.dst, P.items.size());
-    P.items.push_back({dst, src, e});
+    P.items.push_back({dst, src, e, false});
     P.dirty = true;
-  } else if (!same) {
-    P.items[it->second] = {dst, src, e};
+  } else if (!same) {  // (the batch may still write the old entry first: this copy, later in the stream, wins)
+    P.items[it->second] = {dst, src, e, false};
     P.dirty = true;
   }
 }
@@ -578,8 +579,9 @@ void lora_prep_step_begin() {
   if (prep_off() || P.items.empty()) return;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIP_OK(hipStreamIsCapturing(S(), &cap));
-  if (P.dirty) {  // (re)upload -- only outside a capture; inside one the layers make their own copies
-    if (cap != hipStreamCaptureStatusNone) return;
+  // (re)upload -- only outside a capture; inside one the uploaded list still runs and the layers whose
+  // entries changed since make their own copies
+  if (P.dirty && cap == hipStreamCaptureStatusNone) {
     std::vector<::mft::LoraPrepEntry> es;
     for (auto& it : P.items) es.push_back(it.e);
     if (P.dev) HIP_OK(hipFree(P.dev));
@@ -587,7 +589,9 @@ void lora_prep_step_begin() {
     HIP_OK(hipMemcpy(P.dev, es.data(), es.size() * sizeof(::mft::LoraPrepEntry), hipMemcpyHostToDevice));
     P.ndev = (int)es.size();
     P.dirty = false;
+    for (auto& it : P.items) it.uploaded = true;
   }
+  if (P.ndev == 0) return;
   ::mft::lora_prep_batched(P.dev, P.ndev, S());
   P.active = true;
 }
@@ -715,7 +719,8 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         if (dB.defined() && a.rank == 8 && a.ncols % 8 == 0 && a.col0 % 8 == 0 && (K + o) % 8 == 0) {
           Tensor vpart = empty({(int64_t)((a.ncols + 255) / 256) * M * 8}, DType::F32, dy2.device());
           Tensor dw = det_ws(::mft::lora_dy_ws_floats(M, a.ncols));
-          const int vz = seg2 && ads.size() == 1 ? 64 - rt : 0;
+          // the last adapter's finish also zeroes the padding right after its 8 columns (o + 8 == rt)
+          const int vz = seg2 && i + 1 == ads.size() && o + 8 == rt ? 64 - rt : 0;
           ::mft::lora_dy(bp(dys), dys.stride(0), bp(a.B.c), a.B.c.stride(0), bp(xa2) + K + o, xa2.stride(0), fp(dB),
                          a.ncols, fp(vpart), bp(v), v.stride(0), M, a.ncols, s, S(), dptr(dw), vz);
           db_done[i] = true;
@@ -736,8 +741,11 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         if (!v_padded) ::mft::zero_cols(bp(vall), 64, M, rt, 64 - rt, S());
         Tensor& at = pw->lora_at;  // A^T, zero-padded to 64 columns (persistent: the padding stays zero)
         if (!at.defined() || at.size(0) != K) at = zeros({K, 64}, DType::BF16, dy2.device());
-        Tensor atv = at.slice(1, 0, rt);
-        prep_copy(atv, acat.t(), 1.f);
+        int oc = 0;  // per adapter (stable sources: a concatenated A is a new tensor every step)
+        for (auto& a : ads) {
+          prep_copy(at.slice(1, oc, oc + a.rank), a.A.c.t(), 1.f);
+          oc += a.rank;
+        }
         gemm_nt_seg2(dy2, pw->transposed(), vall, at, dx);
       } else if (fused) {
         Gemm8Extra ex;
