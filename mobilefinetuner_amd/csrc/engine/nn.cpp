@@ -646,12 +646,16 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
   if (u_ready) {
     // u_1..u_n already in the appended columns (the norm that produced xa computed them)
   } else if (nodrop && ads.size() > 1) {  // one pass over x for every u_i (adjacent appended columns)
-    std::vector<Tensor> as;
-    for (auto& a : ads) as.push_back(a.A.c);
-    {
-      NoGradGuard ng;
-      acat = cat(as, 0);
+    int rsum = 0;
+    for (auto& a : ads) rsum += a.rank;
+    Tensor& ac = w.lora_acat;  // persistent stack of the A's, refreshed by the batched weight prep
+    if (!ac.defined() || ac.size(0) != rsum || ac.size(1) != K) ac = empty({(int64_t)rsum, K}, DType::BF16, xa.device());
+    int o = 0;
+    for (auto& a : ads) {
+      prep_copy(ac.slice(0, o, o + a.rank), a.A.c, 1.f);
+      o += a.rank;
     }
+    acat = ac;
     const int R = (int)acat.size(0);
     ::mft::lora_rowdot(bp(x2), x2.stride(0), bp(acat), acat.stride(0), bp(xa2) + K, xa2.stride(0), M, K, R, 1.f,
                        ::mft::LoraDrop{nullptr, 0, 0.f}, S());

@@ -27,6 +27,8 @@ struct Param {
   Tensor leaf;  // autograd leaf: fp32 master (trainable) or the frozen compute weight itself
   Tensor c;     // compute view: bf16 shadow (trainable) or == leaf (frozen)
   Tensor wt;    // cached [in, out] transposed copy of a FROZEN 2-D weight (NT data-grad GEMMs)
+  Tensor lora_acat;  // [sum r, in] the adapters' A stacked (one rowdot pass for several adapters), refreshed
+                     // by the batched LoRA weight prep instead of a concatenation per step
   Tensor lora_at;  // [in, 64] A^T of the LoRA adapters on this frozen weight, zero-padded (gemm4 second K
                    // segment); allocated and zeroed once, the first r columns rewritten every backward
   bool streamed = false;  // a slot view of the weight-streaming tier: no cached copies of it
