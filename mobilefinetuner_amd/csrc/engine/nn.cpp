@@ -503,7 +503,15 @@ Tensor mlp_gelu(const Tensor& x, Param& w1, Param& b1, Param& w2, Param& b2, con
       Tensor aux = pre;
       e2.aux = &aux;
       if (!p2->trainable() && !p2->streamed) gemm8_call(dy2, p2->transposed(), false, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
-      else gemm8_call(dy2, p2->c, true, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
+      else if (gemm4_on()) {
+        // trainable / streamed W2: a transposed copy (|W2| bytes) puts the product on gemm4's NT path
+        Tensor w2t;
+        {
+          NoGradGuard ng;
+          w2t = p2->c.t().contiguous();
+        }
+        gemm8_call(dy2, w2t, false, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
+      } else gemm8_call(dy2, p2->c, true, ::mft::GEMM_EPI_MUL_AUX, dpre, e2);
       Tensor dx = empty({M, K}, DType::BF16, dy2.device());
       gemm_nn(dpre, p1->c, dx, !p1->trainable() && !p1->streamed ? p1->transposed() : Tensor());
       if (p2->trainable()) {

@@ -1019,7 +1019,13 @@ __device__ __forceinline__ bf16x8_t frag_tr_pr(const bf16_t* t, int c0) {
 // fragment (ds_read_b64_tr_b16) read from LDS feeds TWO MFMAs -- one per 16-query half -- so the
 // workgroup's LDS read bytes per FLOP halve (at D = 256 the 16-row form reads the whole 32 KB
 // K+V stage per wave per 32-key tile: LDS-bandwidth bound), at ~2x the accumulator registers.
-template <int D, int NW, int RPW = 16, bool SWZ = true>
+// RGF: ring depth of the D = 256 pair images (RGF - 1 tiles in flight; 4 x 34 KB holds the CU to one
+// workgroup, 2 x 34 KB lets two co-reside)
+// GQA: one workgroup per (query block, KV head, batch) -- the G = H / Hkv q-heads sharing the KV head
+// split the waves (NW / G per head, RPW x NW / G query rows each), so every K / V tile lands in LDS
+// once for all G heads (not once per q-head), and the workgroup's waves span G x fewer query rows,
+// i.e. near-equal causal key ranges (a 128-row block idles its early-row waves on the late key tiles)
+template <int D, int NW, int RPW = 16, bool SWZ = true, int RGF = 4, bool GQA = false>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
     float* __restrict__ lse, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides os, int H, int Hkv, int Sq,
@@ -1029,20 +1035,23 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
   // LDO: output staging pitch D + 8 (kOutPad): the four 16-lane groups of the 2-byte staging writes land
   // 16 banks apart (D + 16 put groups 0 / 2 and 1 / 3 on the same banks: the forward's last 2.1 M
   // conflict cycles, profiles/r4b_attn256_pmc.txt)
-  constexpr int BQ = RPW * NW, BK = kSplitBK, TILE = kPair ? kPairTile : BK * D, LDO = D + kOutPad;
+  constexpr int BK = kSplitBK, TILE = kPair ? kPairTile : BK * D, LDO = D + kOutPad;
   constexpr int OPW = 2 * (BK * D / 8 / 64) / NW;  // DMA ops per wave per ring stage (K + V)
-  constexpr int RG = kPair ? 4 : kRing;  // ring depth: RG - 1 tiles in flight (4 x 34 KB at D = 256)
+  constexpr int RG = kPair ? RGF : kRing;  // ring depth: RG - 1 tiles in flight (RGF x 34 KB at D = 256)
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // ring stage s: K at smem + 2 s TILE, V after
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, c16 = lane & 15;
-  int tx, h, b;
-  split_task(tx, h, b);
-  const int q0 = tx * BQ, hk = h / (H / Hkv);
+  int tx, hx, b;
+  split_task(tx, hx, b);
+  const int wph = GQA ? NW / (H / Hkv) : NW;  // waves per q-head
+  const int bq = RPW * wph;                    // query rows per workgroup
+  const int h = GQA ? hx * (H / Hkv) + w / wph : hx, hk = GQA ? hx : h / (H / Hkv);
+  const int q0 = tx * bq;
   const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
   const int coff = Sk - Sq;
   const float c2 = scale * kLog2e;
-  const int wq_lo = q0 + RPW * w, wq_hi = wq_lo + RPW - 1;
+  const int wq_lo = q0 + RPW * (GQA ? w % wph : w), wq_hi = wq_lo + RPW - 1;
   int kend = kv_len;
-  if (causal) kend = min(kend, q0 + BQ + coff);
+  if (causal) kend = min(kend, q0 + bq + coff);
   int kstart = 0;
   if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
   const int nt = kend > kstart ? (kend - kstart + BK - 1) / BK : 0;  // WG-uniform
@@ -1183,7 +1192,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
 // address base per lane); smaller D: register staging (Tile2) into rows padded to D + kSplitPad.
 // The causal / window / padding mask is a select in front of the exp (exp2(-inf) = 0), not a
 // branch around it: the branch split every step into divergent blocks the MFMAs could not cross.
-template <int D, int NW>
+// RGK: DMA ring slots at D = 256 (3: two tiles in flight, 102 KB -- one workgroup per CU; 2: one tile,
+// 68 KB -- two co-resident workgroups)
+template <int D, int NW, int RGK = 3>
 __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
@@ -1195,7 +1206,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
   constexpr int TILE = kDma ? kPairTile : BQ * LD;  // elements of one staged [BQ] x D tile
   // DMA: a 3-slot ring, two tiles in flight; register staging: 2 buffers
   // slots; DMA ops per wave per tile (two half-wave ops per offset-pair piece, + the row stats)
-  constexpr int RG = kDma ? 3 : 2, OPT = 2 * 2 * (16 / NW) + 1;
+  constexpr int RG = kDma ? RGK : 2, OPT = 2 * 2 * (16 / NW) + 1;
+  constexpr int PF = RG - 1;  // DMA: tiles of prefetch
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   // slot j: Q at smem + 2 j TILE, dO after it; row floats [j][lse | delta][BQ] after every slot
   float* const rowf = reinterpret_cast<float*>(smem + 2 * RG * TILE);
@@ -1252,7 +1264,9 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
   };
   if (total > 0) {
     load(0, 0);
-    if constexpr (kDma) load(min(1, total - 1), 1);  // past the end: the last tile again (uniform counts)
+    if constexpr (kDma) {
+      if constexpr (PF > 1) load(min(1, total - 1), 1);  // past the end: the last tile again (uniform counts)
+    }
   }
   bf16x8_t kf[D / 32], vf[D / 32];  // B operands: K[key][32 s + 8 g + j], V[key][...]
 #pragma unroll
@@ -1273,9 +1287,9 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
   for (int it = 0; it < total; ++it) {
     const bool more = it + 1 < total;
     if constexpr (kDma) {
-      vmcnt_wait<OPT>();  // this wave's pieces of step it's tile landed (step it + 1's may still fly)
-      lds_barrier();      // ... and every wave's; slot (it + 2) % 3, read in step it - 1, is free
-      load(min(it + 2, total - 1), (it + 2) % RG);
+      vmcnt_wait<OPT * (PF - 1)>();  // this wave's pieces of step it's tile landed (later steps' may still fly)
+      lds_barrier();                 // ... and every wave's; slot (it + PF) % RG, read in step it - 1, is free
+      load(min(it + PF, total - 1), (it + PF) % RG);
     } else {
       // step it's buffer stored by every wave; the other buffer, read in step it - 1, is free.  Raw
       // barrier: the register prefetch below stays in flight across the next one.
@@ -1343,7 +1357,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(
 // holds anyway (+ one pass over the O row) and written out for the dK/dV kernel, which runs after
 // this one -- no separate delta pass over O and dO.
 // RGD: DMA ring slots (2: one tile of prefetch, 3: two); FOLD: compute delta here (else read it)
-template <int D, int NW, int RGD = 2, bool FOLD = true>
+// GQA: workgroups per (query block, KV head, batch), the q-heads splitting the waves (as the forward)
+template <int D, int NW, int RGD = 2, bool FOLD = true, bool GQA = false>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ o, const float* __restrict__ lse,
@@ -1351,7 +1366,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
     AttnStrides dos, AttnStrides oss, AttnStrides dqs, int H, int Hkv, int Sq, int Sk, float scale, int causal,
     int window, const int* __restrict__ kv_lens) {
   constexpr bool kDma = D == 256;
-  constexpr int NT = 64 * NW, BQ = 16 * NW, BK = kSplitBK, LD = D + kSplitPad;
+  constexpr int NT = 64 * NW, BK = kSplitBK, LD = D + kSplitPad;
   constexpr int TILE = kDma ? kPairTile : BK * LD;
   // DMA: a 3-slot ring, two tiles in flight (a step is only 48 MFMAs per wave: one tile of prefetch
   // leaves the load latency exposed); register staging: 2 buffers
@@ -1359,16 +1374,19 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(
   constexpr int PF = RG - 1;                                // tiles of prefetch
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // slot j: K at smem + 2 j TILE, V after it
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, c16 = lane & 15;
-  int tx, h, b;
-  split_task(tx, h, b);
-  const int q0 = tx * BQ, hk = h / (H / Hkv);
+  int tx, hx, b;
+  split_task(tx, hx, b);
+  const int wph = GQA ? NW / (H / Hkv) : NW;  // waves per q-head
+  const int bq = 16 * wph;                     // query rows per workgroup
+  const int h = GQA ? hx * (H / Hkv) + w / wph : hx, hk = GQA ? hx : h / (H / Hkv);
+  const int q0 = tx * bq;
   const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
   const int coff = Sk - Sq;
   const float c2 = scale * kLog2e;
-  const int wq_lo = q0 + 16 * w, wq_hi = wq_lo + 15;
+  const int wq_lo = q0 + 16 * (GQA ? w % wph : w), wq_hi = wq_lo + 15;
   const int qi = wq_lo + c16;
   int kend = kv_len;
-  if (causal) kend = min(kend, q0 + BQ + coff);
+  if (causal) kend = min(kend, q0 + bq + coff);
   int kstart = 0;
   if (window > 0) kstart = max(0, q0 + coff - window + 1) / BK * BK;
   const int nt = kend > kstart ? (kend - kstart + BK - 1) / BK : 0;  // key tiles, WG-uniform
@@ -1521,17 +1539,23 @@ static void fwd_split_launch(const AttnArgs& a, hipStream_t stream) {
       a.causal, a.window, a.kv_lens);
 }
 
-template <int D, int NW, int RPW, bool SWZ>
+template <int D, int NW, int RPW, bool SWZ, int RGF = 4, bool GQA = false>
 static void fwd_dma_launch_rpw(const AttnArgs& a, hipStream_t stream) {
-  const size_t shm = std::max(D == 256 ? sizeof(bf16_t) * 4 * 2 * kPairTile : sizeof(bf16_t) * kRing * 2 * kSplitBK * D,
+  const size_t shm = std::max(D == 256 ? sizeof(bf16_t) * RGF * 2 * kPairTile : sizeof(bf16_t) * kRing * 2 * kSplitBK * D,
                               sizeof(bf16_t) * NW * 16 * (D + kSplitPad));
   static bool attr = false;
   if (!attr) {
-    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_dma_kernel<D, NW, RPW, SWZ>,
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_dma_kernel<D, NW, RPW, SWZ, RGF, GQA>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  attn_fwd_dma_kernel<D, NW, RPW, SWZ><<<dim3(cdiv(a.Sq, RPW * NW), a.H, a.B), 64 * NW, shm, stream>>>(
+  const int G = a.H / a.Hkv;
+  if (GQA && (a.H % a.Hkv || G < 2 || NW % G)) {
+    fprintf(stderr, "mft::attn_fwd: GQA workgroups need H / Hkv to divide %d waves (H=%d Hkv=%d)\n", NW, a.H, a.Hkv);
+    abort();
+  }
+  const dim3 grid = GQA ? dim3(cdiv(a.Sq, RPW * (NW / G)), a.Hkv, a.B) : dim3(cdiv(a.Sq, RPW * NW), a.H, a.B);
+  attn_fwd_dma_kernel<D, NW, RPW, SWZ, RGF, GQA><<<grid, 64 * NW, shm, stream>>>(
       a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale,
       a.causal, a.window, a.kv_lens);
 }
@@ -1543,41 +1567,74 @@ static void fwd_dma_launch(const AttnArgs& a, hipStream_t stream) {
   static const int rpw = env_int("MFT_ATTN_RPW", 16);
   // MFT_ATTN_SWZ=0: the plain (2-way bank-conflicted) K / V pair images, for A/B
   static const int swz = env_int("MFT_ATTN_SWZ", 1);
+  // GQA-packed workgroups (all q-heads of a KV head) with a 2-slot ring (two workgroups per CU) where
+  // H / Hkv divides the waves: 138 us vs 167 us per-q-head at the Gemma-3 bench shape (B 256, S 256, H 4,
+  // Hkv 1; profiles/r5_attn_gqa_fwd.txt).  A/B knobs: MFT_ATTN_GQA=0|1, MFT_ATTN_FWD_RING=2|3|4 (D = 256
+  // ring depth; 0 = 2 packed, 4 per-q-head), MFT_ATTN_NW_FWD=4|8
+  static const int gqa = env_int("MFT_ATTN_GQA", 1);
+  static const int ring_env = env_int("MFT_ATTN_FWD_RING", 0);
+  static const int nw = split_nw("MFT_ATTN_NW_FWD", 8);
+  const int G = a.H / a.Hkv;
+  if (D == 256 && rpw == 16 && swz && gqa && a.H % a.Hkv == 0 && G >= 2 && nw % G == 0) {
+    const int ring = ring_env ? ring_env : 2;
+    if (nw == 4) {
+      if (ring == 2) return fwd_dma_launch_rpw<D, 4, 16, true, 2, true>(a, stream);
+      return fwd_dma_launch_rpw<D, 4, 16, true, 4, true>(a, stream);
+    }
+    if (ring == 2) return fwd_dma_launch_rpw<D, 8, 16, true, 2, true>(a, stream);
+    return fwd_dma_launch_rpw<D, 8, 16, true, 4, true>(a, stream);
+  }
+  const int ring = ring_env ? ring_env : 4;
+  if (D == 256 && rpw == 16 && swz && (ring != 4 || nw != 8)) {
+    if (nw == 4) {
+      if (ring == 2) return fwd_dma_launch_rpw<D, 4, 16, true, 2>(a, stream);
+      if (ring == 3) return fwd_dma_launch_rpw<D, 4, 16, true, 3>(a, stream);
+      return fwd_dma_launch_rpw<D, 4, 16, true, 4>(a, stream);
+    }
+    if (ring == 2) return fwd_dma_launch_rpw<D, 8, 16, true, 2>(a, stream);
+    if (ring == 3) return fwd_dma_launch_rpw<D, 8, 16, true, 3>(a, stream);
+  }
   if (rpw == 32) fwd_dma_launch_rpw<D, 4, 32, true>(a, stream);
   else if (swz) fwd_dma_launch_rpw<D, 8, 16, true>(a, stream);
   else fwd_dma_launch_rpw<D, 8, 16, false>(a, stream);
 }
 
-template <int D, int NW>
+template <int D, int NW, int RGK = 3>
 static void dkdv_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
   constexpr int LD = D + kSplitPad;
   // two {Q, dO} tile buffers (row-pair images for the D = 256 LDS-DMA form) + their row statistics, or the
   // epilogue's per-wave output staging
-  const size_t shm = std::max(D == 256 ? sizeof(bf16_t) * 6 * kPairTile + sizeof(float) * 6 * kSplitBK
+  const size_t shm = std::max(D == 256 ? sizeof(bf16_t) * 2 * RGK * kPairTile + sizeof(float) * 2 * RGK * kSplitBK
                                         : sizeof(bf16_t) * 4 * kSplitBK * LD + sizeof(float) * 4 * kSplitBK,
                               sizeof(bf16_t) * NW * 16 * LD);
   static bool attr = false;
   if (!attr) {
-    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<D, NW>,
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<D, NW, RGK>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  attn_bwd_dkdv_kernel<D, NW><<<dim3(cdiv(a.Sk, 16 * NW), a.Hkv, a.B), 64 * NW, shm, stream>>>(
+  attn_bwd_dkdv_kernel<D, NW, RGK><<<dim3(cdiv(a.Sk, 16 * NW), a.Hkv, a.B), 64 * NW, shm, stream>>>(
       a.q, a.k, a.v, a.dout, a.lse, a.delta, a.dk, a.dv, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.do_st),
       mk(a.dk_st), mk(a.dv_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale, a.causal, a.window, a.kv_lens);
 }
 
-template <int D, int NW, int RGD, bool FOLD>
+template <int D, int NW, int RGD, bool FOLD, bool GQA = false>
 static void dq_split_launch_v(const AttnBwdArgs& a, hipStream_t stream) {
   const size_t shm = D == 256 ? std::max(sizeof(bf16_t) * RGD * 2 * kPairTile, sizeof(bf16_t) * NW * 16 * (D + kSplitPad))
                               : split_shm<D, NW>(0);
   static bool attr = false;
   if (!attr) {
-    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, NW, RGD, FOLD>,
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, NW, RGD, FOLD, GQA>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  attn_bwd_dq_kernel<D, NW, RGD, FOLD><<<dim3(cdiv(a.Sq, 16 * NW), a.H, a.B), 64 * NW, shm, stream>>>(
+  const int G = a.H / a.Hkv;
+  if (GQA && (a.H % a.Hkv || G < 2 || NW % G)) {
+    fprintf(stderr, "mft::attn_bwd: GQA dQ workgroups need H / Hkv to divide %d waves (H=%d Hkv=%d)\n", NW, a.H, a.Hkv);
+    abort();
+  }
+  const dim3 grid = GQA ? dim3(cdiv(a.Sq, 16 * (NW / G)), a.Hkv, a.B) : dim3(cdiv(a.Sq, 16 * NW), a.H, a.B);
+  attn_bwd_dq_kernel<D, NW, RGD, FOLD, GQA><<<grid, 64 * NW, shm, stream>>>(
       a.q, a.k, a.v, a.dout, a.o, a.lse, a.delta, a.dq, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.do_st), mk(a.o_st),
       mk(a.dq_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale, a.causal, a.window, a.kv_lens);
 }
@@ -1588,11 +1645,20 @@ static bool delta_fold(int D) {
   static const int f = env_int("MFT_ATTN_DELTA_FOLD", 1);
   return D != 256 || f != 0;
 }
+// GQA-packed dQ workgroups (all q-heads of a KV head; MFT_ATTN_GQA_DQ=0 per-q-head, A/B): dQ + dK/dV
+// 408 us vs 455 us at the Gemma-3 bench shape (profiles/r5_attn_gqa_fwd.txt)
+static bool dq_gqa() {
+  static const int v = env_int("MFT_ATTN_GQA_DQ", 1);
+  return v != 0;
+}
 template <int D, int NW>
 static void dq_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
   if constexpr (D == 256) {
     static const int ring = env_int("MFT_ATTN_DQ_RING", 2);
     const bool fold = delta_fold(D);
+    const int G = a.H / a.Hkv;
+    if (dq_gqa() && ring == 2 && fold && a.H % a.Hkv == 0 && G >= 2 && NW % G == 0)
+      return dq_split_launch_v<D, NW, 2, true, true>(a, stream);
     if (ring == 2) {
       if (fold) dq_split_launch_v<D, NW, 2, true>(a, stream);
       else dq_split_launch_v<D, NW, 2, false>(a, stream);
@@ -1676,10 +1742,19 @@ static void bwd_launch(const AttnBwdArgs& a, hipStream_t stream) {
                                                                               mk(a.do_st), a.B, a.H, a.Sq);
     }
     // dQ first: it writes delta (rowsum dO * O), which the dK/dV kernel reads
-    if (split_nw("MFT_ATTN_NW_DQ", 8) == 8) dq_split_launch<D, 8>(a, stream);
+    // GQA-packed dQ (D = 256, H / Hkv | 4): 4 waves, i.e. 16 query rows of every q-head per workgroup
+    const int G = a.H / a.Hkv;
+    const bool packed = D == 256 && a.H % a.Hkv == 0 && G >= 2 && 4 % G == 0 && dq_gqa();
+    if (split_nw("MFT_ATTN_NW_DQ", packed ? 4 : 8) == 8) dq_split_launch<D, 8>(a, stream);
     else dq_split_launch<D, 4>(a, stream);
     // D = 256: 8 waves (its 3-slot DMA ring holds one workgroup per CU; 4 waves would leave one per SIMD)
-    if (split_nw("MFT_ATTN_NW_DKDV", D == 256 ? 8 : 4) == 8) dkdv_split_launch<D, 8>(a, stream);
+    // D = 256: a 2-slot ring, two workgroups per CU (399 us dQ + dK/dV vs 411 us with 3 slots at the Gemma-3
+    // bench shape, profiles/r5_attn_gqa_fwd.txt; MFT_ATTN_DKDV_RING=3 for A/B)
+    static const int dkdv_ring = env_int("MFT_ATTN_DKDV_RING", 2);
+    if (D == 256 && dkdv_ring == 2) {
+      if (split_nw("MFT_ATTN_NW_DKDV", 8) == 8) dkdv_split_launch<D, 8, 2>(a, stream);
+      else dkdv_split_launch<D, 4, 2>(a, stream);
+    } else if (split_nw("MFT_ATTN_NW_DKDV", D == 256 ? 8 : 4) == 8) dkdv_split_launch<D, 8>(a, stream);
     else dkdv_split_launch<D, 4>(a, stream);
     return;
   }

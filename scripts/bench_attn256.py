@@ -1,5 +1,6 @@
 """Gemma-3 D=256 attention timing at the bench shape (B=256, S=256, H=4, Hkv=1, causal): forward,
-and forward+backward.  Variant selection by env (read once per process): MFT_ATTN_RPW=16|32.
+and forward+backward.  Variant selection by env (read once per process): MFT_ATTN_RPW=16|32, MFT_ATTN_FWD_RING=2|3|4,
+MFT_ATTN_NW_FWD=4|8.
 
 usage: MFT_ATTN_RPW=32 PYTHONPATH=. python scripts/bench_attn256.py [--window 0]
 """
@@ -42,7 +43,20 @@ def main():
     tf = min(timeit(fwd) for _ in range(3))
     tb = min(timeit(bwd) for _ in range(3))
     fl = 4.0 * B * H * S * S * D / 2  # causal
-    print(f"RPW={os.environ.get('MFT_ATTN_RPW', '16')} window={a.window}: fwd {tf:7.1f} us ({fl / tf / 1e6:5.0f} TF) "
+    # fp32 reference of the forward (GQA heads expanded)
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k.expand(B, S, H, D), v.expand(B, S, H, D)))
+    ref = torch.nn.functional.scaled_dot_product_attention(qf, kf, vf, is_causal=True, scale=sc).transpose(1, 2)
+    err = (o.float() - ref).abs().max().item()
+    # backward vs fp32 autograd (relative to each gradient's max)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    orf = torch.nn.functional.scaled_dot_product_attention(
+        qr.transpose(1, 2), kr.expand(B, S, H, D).transpose(1, 2), vr.expand(B, S, H, D).transpose(1, 2),
+        is_causal=True, scale=sc).transpose(1, 2)
+    orf.backward(go.float())
+    bwd()
+    gerr = max(((x.float() - y.grad).abs().max() / y.grad.abs().max()).item() for x, y in ((dq, qr), (dk, kr), (dv, vr)))
+    tag = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("MFT_ATTN"))
+    print(f"[{tag}] err {err:.1e} grad rel err {gerr:.1e} window={a.window}: fwd {tf:7.1f} us ({fl / tf / 1e6:5.0f} TF) "
           f"bwd {tb:7.1f} us ({2.5 * fl / tb / 1e6:5.0f} TF)  o[0,0,0,:4]={o[0, 0, 0, :4].float().tolist()}", flush=True)
 
 
