@@ -14,15 +14,26 @@
 //     fused epilogue on 16 contiguous columns per lane (16-B loads / stores).
 // The MFMAs run with the operands swapped (C^T = B A^T) so each lane's accumulators are 4 contiguous
 // columns of one row.
+// Split-K across workgroups (S > 1, long K with few tiles, e.g. 512 x 768 x 3072): the S workgroups of a
+// tile take interleaved K-tile shares, write their reduced fp32 partial tile to a workspace and count in on
+// a per-tile counter; the last to arrive sums the S partials in split order (deterministic) and runs the
+// epilogue, then re-arms the counter.  Partials and counter are agent-scope relaxed atomics (sc1 stores /
+// loads through to the coherence point; the writers wait for their stores before counting in), and the S
+// workgroups of a tile sit on one XCD (block ids congruent mod 8).
 #include "common.h"
 #include "kernels.h"
 #include "mfma.h"
+
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
 
 namespace mft {
 
 namespace {
 
 constexpr int kLdr = 68;  // fp32 row pitch of the reduction image (64 + 4: float4 writes spread over banks)
+constexpr int kMaxSplit = 4;  // K-splits across workgroups (gemm_s split-K)
 constexpr int kNW = 4;    // waves per workgroup, each a 1/kNW share of the K-tiles (8 measured slower: 139 KB LDS, one WG per CU)
 
 
@@ -35,6 +46,7 @@ struct Frags {
 // moved out of range by its scalar offset (a wave's tiles past its last), read as zeros -- no branch and
 // no clamp around any load, so the compiler keeps the next K-tile's loads in flight under the MFMAs.
 typedef int i32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void load_frags(Frags& f, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb,
                                            const uint32_t (&oa)[4], const uint32_t (&ob)[4], uint32_t soff) {
 #pragma unroll
@@ -59,20 +71,25 @@ __device__ __forceinline__ void mma(f32x4_t (&acc)[4][4], const Frags& f) {
 }
 
 template <int EPI, bool SEG2>
-__global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g) {
+__global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g, int S, float* __restrict__ ws, int* __restrict__ cnt) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [kNW waves][64 rows][kLdr]
-  const int tiles_n = (g.N + 63) / 64;
-  const int m0 = (blockIdx.x / tiles_n) * 64, n0 = (blockIdx.x % tiles_n) * 64;
+  __shared__ int last;
+  const int tiles_n = (g.N + 63) / 64, tiles = ((g.M + 63) / 64) * tiles_n;
+  // block -> (tile t, split s): the S splits of a tile on one XCD (block ids congruent mod 8)
+  const int bx = blockIdx.x & 7, bq = blockIdx.x >> 3, sp = bq % S, t = (bq / S) * 8 + bx;
+  if (t >= tiles) return;
+  const int m0 = (t / tiles_n) * 64, n0 = (t % tiles_n) * 64;
   const int w = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // (uniform: scalar loop)
   const int nk = g.K / 64, nkt = nk + (SEG2 ? g.K2 / 64 : 0);
+  const int slot = sp * kNW + w, P = S * kNW;  // this wave's K-tiles: slot, slot + P, ...
   f32x4_t acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
-  // the wave's it-th K-tile is w + 4 it; past its last one the loads are out of range (zeros: a multiply
+  // the wave's it-th K-tile is slot + P it; past its last one the loads are out of range (zeros: a multiply
   // that adds nothing), so the MFMA chain is unconditional and the accumulators stay in place
-  const int n_my = w < nkt ? (nkt - w + kNW - 1) / kNW : 0;
+  const int n_my = slot < nkt ? (nkt - slot + P - 1) / P : 0;
   // operand panels of this tile: base + byte count (rows past M / N: VGPR offsets beyond the records -> 0)
   auto recs = [](long bytes) { return (int)__builtin_amdgcn_readfirstlane((uint32_t)min(bytes, 0x7fff0000L)); };
   const bf16_t* pa1 = g.A + (long)m0 * g.lda;
@@ -96,7 +113,7 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g) {
   // reads through a 0-record descriptor, not through a large soffset; scalar selects of base and count,
   // the descriptor built per load: a select between descriptor values went through scratch)
   auto load = [&](Frags& f, int it) {  // (selects only: a branch here would make the compiler wait early)
-    const int kt = w + kNW * it;
+    const int kt = slot + P * it;
     const bool ok = it < n_my && !g.stagger, s2 = SEG2 && kt >= nk;
     const uint32_t off = (uint32_t)(s2 ? kt - nk : min(kt, nk - 1)) * 128u;
     const bf16_t* pa = s2 ? pa2 : pa1;
@@ -150,8 +167,42 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g) {
       s[0] += t[0], s[1] += t[1], s[2] += t[2], s[3] += t[3];
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[4 * q + e] = s[e] * g.alpha;
+    for (int e = 0; e < 4; ++e) v[4 * q + e] = s[e];
   }
+  if (S > 1) {  // split-K: partial out, count in; the last workgroup of the tile sums the S partials
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, 0x7fffffff, 0x00020000);
+    const uint32_t o0 = (uint32_t)(((long)t * S * 4096 + rt * 64 + ct) * 4);
+#pragma unroll
+    for (int q = 0; q < kCols / 4; ++q)  // (aux 16 = sc1: through to the agent coherence point)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, f32x4_t{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]}),
+                                             rw, o0 + (uint32_t)sp * 16384u + 16u * q, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's partial is at the coherence point
+    __syncthreads();
+    if (threadIdx.x == 0) last = __hip_atomic_fetch_add(cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+    __syncthreads();
+    if (!last) return;
+    // every split's loads issued before the first add (S <= kMaxSplit; splits past S re-read the last one,
+    // weighted 0), in split order
+    f32x4_t pv[kMaxSplit][kCols / 4];
+#pragma unroll
+    for (int p = 0; p < kMaxSplit; ++p)
+#pragma unroll
+      for (int q = 0; q < kCols / 4; ++q)
+        pv[p][q] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rw, o0 + (uint32_t)min(p, S - 1) * 16384u + 16u * q, 0, 16));
+#pragma unroll
+    for (int q = 0; q < kCols / 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = pv[0][q][e];
+#pragma unroll
+        for (int p = 1; p < kMaxSplit; ++p) a += p < S ? pv[p][q][e] : 0.f;
+        v[4 * q + e] = a;
+      }
+    if (threadIdx.x == 0) __hip_atomic_store(cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+#pragma unroll
+  for (int e = 0; e < kCols; ++e) v[e] *= g.alpha;
   if (row >= g.M) return;
   constexpr bool kBias = EPI == GEMM_EPI_BIAS || EPI == GEMM_EPI_BIAS_GELU_D || EPI == GEMM_EPI_BIAS_ADD;
   constexpr bool kAux = EPI == GEMM_EPI_MUL_AUX || EPI == GEMM_EPI_DGELU || EPI == GEMM_EPI_BIAS_ADD;
@@ -190,6 +241,39 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g) {
   }
 }
 
+// split-K workspace of a stream: kWsTiles fp32 64 x 64 partials + kCnt tile counters (zeroed once; the
+// kernels re-arm them), allocated on first use outside graph capture
+constexpr int kWsTiles = 2048, kCnt = 16384;
+struct SplitWs {
+  float* ws = nullptr;
+  int* cnt = nullptr;
+};
+static SplitWs split_ws(hipStream_t st) {
+  static std::mutex mu;
+  static std::unordered_map<hipStream_t, SplitWs> m;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = m.find(st);
+  if (it != m.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  MFT_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+  if (cs != hipStreamCaptureStatusNone) return SplitWs{};  // (no allocation inside a capture: S = 1)
+  SplitWs w;
+  MFT_HIP_CHECK(hipMalloc(&w.ws, sizeof(float) * 4096 * kWsTiles));
+  MFT_HIP_CHECK(hipMalloc(&w.cnt, sizeof(int) * kCnt));
+  MFT_HIP_CHECK(hipMemsetAsync(w.cnt, 0, sizeof(int) * kCnt, st));
+  m[st] = w;
+  return w;
+}
+
+// K-splits: enough workgroups for ~1.5 per CU, every wave at least 2 K-tiles (MFT_GS_SPLIT=0: off, A/B)
+static int pick_split(int tiles, int nkt) {
+  static const int on = getenv("MFT_GS_SPLIT") ? atoi(getenv("MFT_GS_SPLIT")) : 1;
+  if (!on || tiles >= 192) return 1;
+  int S = std::min((384 + tiles - 1) / tiles, nkt / (2 * kNW));
+  S = std::max(1, std::min({S, kMaxSplit, kWsTiles / std::max(tiles, 1)}));
+  return tiles > kCnt ? 1 : S;
+}
+
 template <int EPI, bool SEG2>
 void launch_s(const GemmArgs& g, hipStream_t st) {
   constexpr size_t shm = kNW * 64 * kLdr * sizeof(float);
@@ -200,7 +284,14 @@ void launch_s(const GemmArgs& g, hipStream_t st) {
     attr = true;
   }
   const int tiles = ((g.M + 63) / 64) * ((g.N + 63) / 64);
-  gemm_s_kernel<EPI, SEG2><<<tiles, 64 * kNW, shm, st>>>(g);
+  int S = pick_split(tiles, g.K / 64 + (SEG2 ? g.K2 / 64 : 0));
+  SplitWs w;
+  if (S > 1) {
+    w = split_ws(st);
+    if (!w.ws) S = 1;
+  }
+  const int blocks = S > 1 ? (tiles + 7) / 8 * 8 * S : tiles;
+  gemm_s_kernel<EPI, SEG2><<<blocks, 64 * kNW, shm, st>>>(g, S, w.ws, w.cnt);
 }
 
 }  // namespace

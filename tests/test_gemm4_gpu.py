@@ -8,7 +8,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 NONE, BIAS, DGELU, GELU_D, MUL_AUX, BIAS_ADD = 0, 1, 3, 9, 10, 11
-SHAPES = [(300, 264, 128), (1000, 776, 832), (4096, 3072, 768), (257, 8, 192), (2048, 640, 2048)]
+# (the last two: gemm_s splits K over 4 workgroups per tile -- few tiles, long K)
+SHAPES = [(300, 264, 128), (1000, 776, 832), (4096, 3072, 768), (257, 8, 192), (2048, 640, 2048), (512, 768, 3072),
+          (200, 136, 2048)]
 
 
 def _gelu(x):
@@ -86,7 +88,8 @@ def test_gemm4_is_deterministic(impl):
 
 
 @pytest.mark.parametrize("impl", [4, 5], ids=["gemm4", "gemm_s"])
-@pytest.mark.parametrize("M,N,K,K2", [(1000, 768, 2304, 64), (4096, 768, 768, 64), (300, 264, 128, 128), (512, 776, 64, 64)])
+@pytest.mark.parametrize("M,N,K,K2", [(1000, 768, 2304, 64), (4096, 768, 768, 64), (300, 264, 128, 128), (512, 776, 64, 64),
+                                      (512, 768, 2304, 64)])
 def test_gemm4_second_k_segment(M, N, K, K2, impl):
     if impl == 4 and K < 128:
         pytest.skip("gemm4 needs K >= 128")
@@ -105,3 +108,19 @@ def test_gemm4_second_k_segment(M, N, K, K2, impl):
     ref = x.float() @ w.float().t() + a2.float() @ b2.float().t()
     torch.cuda.synchronize()
     assert _rel(y, ref) < 1e-2
+
+
+def test_gemm_s_split_k_deterministic_and_rearmed():
+    """gemm_s with K split across workgroups (last-arriving workgroup sums the partials in split order):
+    bit-identical over repeated calls (the per-tile counters re-arm), and equal to the fp32 product."""
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    x, w, b, aux = _ops(512, 768, 3072, seed=7)
+    ys = []
+    for _ in range(6):
+        y = torch.empty(512, 768, device="cuda", dtype=torch.bfloat16)
+        C.gemm_t(x, w, False, False, MUL_AUX, None, aux, 1.0, y, None, None, 5)
+        ys.append(y)
+    torch.cuda.synchronize()
+    assert all(torch.equal(ys[0], y) for y in ys[1:])
+    assert _rel(ys[0], (x.float() @ w.float().t()) * aux.float()) < 2e-2
