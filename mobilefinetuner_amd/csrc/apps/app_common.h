@@ -251,9 +251,11 @@ struct DistSetup {
       z3->shard_optimizer(opt, d.host_moments, d.host_fp32, d.host_stream);
       std::printf("  %s%s%s%s\n", z3->describe().c_str(),
                   !d.host_moments ? "" : d.host_fp32 ? "; AdamW moments in pinned host DRAM (fp32)" : "; AdamW moments in pinned host DRAM (bf16)",
-                  !d.host_moments ? "" : d.host_stream ? ", read in place over PCIe, each unit updated during the next "
-                                                          "forward on its own stream" : ", read in place over PCIe after the backward",
-                  "");
+                  !d.host_moments ? "" : !d.host_stream ? ", read in place over PCIe after the backward"
+                  : z3->staged_slots() > 0 ? ", staged through device slots by SDMA copies (each written back after its "
+                                             "unit's update in the next forward and prefetched for the slot's next unit)"
+                                           : ", read in place over PCIe, each unit updated during the next forward on its own stream",
+                  z3->staged_slots() > 0 ? (" [" + std::to_string(z3->staged_slots()) + " slots]").c_str() : "");
     } else if (comm) {
       dp = std::make_unique<eng::DataParallel>(*flat, plan, *comm, opt, d);
       std::printf("  data parallel: %s\n", dp->describe().c_str());

@@ -58,6 +58,10 @@ class GradReducer {
   virtual bool owns_optimizer() const { return false; }
   virtual void prepare_optimizer() {}
   virtual void flush_optimizer() {}
+  // the optimizer's (host) moments were overwritten (checkpoint load): drop any device copies of them
+  virtual void optimizer_state_loaded() {}
+  // false: the step must run eagerly (its stream pattern cannot be captured into a hipGraph)
+  virtual bool graph_capturable() const { return true; }
   // ZeRO-3: each rank's flat holds only its partitions (no initial broadcast, per-rank masters)
   virtual bool params_sharded() const { return false; }
   // factor folded into the loss seed (and the fused LM-head weight grad): a reducer that SUMS

@@ -35,6 +35,12 @@ Trainer::Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDatase
     std::fprintf(stderr, "[trainer] MFT_GRAPH_COMM=0 ignored: the host-streamed ZeRO-3 optimizer runs inside the graph\n");
     graph_comm_ = true;
   }
+  if (cfg_.use_graph && dp_ && !dp_->graph_capturable()) {
+    // the staged host-moment ZeRO-3 optimizer: its copy-stream / communication-stream ping-pong crashes
+    // hipStreamEndCapture on this ROCm, and eager measured faster for it anyway (profiles/r5_offload_staged.txt)
+    std::printf("[trainer] step runs eagerly (no hipGraph): staged host-moment optimizer\n");
+    cfg_.use_graph = false;
+  }
   if (comm_ && !(dp_ && dp_->params_sharded())) {  // every rank starts from rank 0's trainable weights
     comm_->broadcast(flat_.master.data_ptr(), (size_t)flat_.numel * sizeof(float), 0, stream_);
     flat_.refresh_shadow();
@@ -477,6 +483,7 @@ bool Trainer::load_state(const std::string& dir0) {
   };
   flat_.master.copy_(host_view(tw, "master", flat_.numel));
   opt_.load_state(host_view(to, "m", opt_.m.numel()), host_view(to, "v", opt_.v.numel()), st["opt_step"].as_int());
+  if (dp_) dp_->optimizer_state_loaded();
   if (opt_.vmax.defined()) {
     if (to.has("vmax")) {
       opt_.load_vmax(host_view(to, "vmax", opt_.vmax.numel()));

@@ -140,7 +140,14 @@ Zero3::Zero3(const std::vector<NamedParams>& units, const NamedParams& rep, Comm
 }
 
 Zero3::~Zero3() {
+  if (cstream_) {
+    (void)hipStreamSynchronize(cstream_);
+    (void)hipStreamDestroy(cstream_);
+    for (auto e : h2d_ev_) (void)hipEventDestroy(e);
+    (void)hipEventDestroy(cjoin_ev_);
+  }
   if (ostream_) {
+    ::mft::gemm4_reserve_cus(0);
     (void)hipStreamSynchronize(ostream_);
     (void)hipStreamDestroy(ostream_);
   }
@@ -182,7 +189,10 @@ void Zero3::shard_optimizer(AdamW& opt, bool host_moments, bool host_fp32, bool 
   // the updates run beside the forward's kernels: a low-priority stream and a bounded grid (the
   // kernel waits on PCIe, not on the CU)
   const char* pr = std::getenv("MFT_Z3_OPT_PRIO");
-  if (!(pr && pr[0] == '0')) {
+  const char* stg = std::getenv("MFT_Z3_STAGED");
+  if (!(stg && stg[0] == '0')) {
+    // (staged: no optimizer stream)
+  } else if (!(pr && pr[0] == '0')) {
     int least = 0, greatest = 0;
     HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIP_OK(hipStreamCreateWithPriority(&ostream_, hipStreamNonBlocking, least));
@@ -191,6 +201,55 @@ void Zero3::shard_optimizer(AdamW& opt, bool host_moments, bool host_fp32, bool 
   }
   const char* gr = std::getenv("MFT_Z3_OPT_GRID");
   opt_grid_ = gr ? std::atoi(gr) : 32;  // profiles/r4_offload_modes.txt: 32 best of 16-2048
+  const char* st = std::getenv("MFT_Z3_STAGED");
+  staged_ = !(st && st[0] == '0');
+  if (staged_) {
+    // device slots for the moments of S updates (default: half of them), refilled by SDMA copies on one
+    // copy stream: update i reads / writes slot i % S on the communication stream, then the copy stream
+    // writes the slot back and prefetches the slot's next user (i + S, or next step's i % S) -- the
+    // PCIe traffic runs from the forward through the backward instead of inside the forward
+    const char* se = std::getenv("MFT_Z3_SLOTS");
+    nslot_ = se && *se ? std::atoi(se) : (nupd + 1) / 2 + 1;
+    nslot_ = std::max(1, std::min(nslot_, nupd));
+    int64_t mx = 0;
+    for (int i = 0; i < nupd; ++i) mx = std::max(mx, upd_len(i));
+    slot_elems_ = (mx + 63) / 64 * 64;
+    const int64_t es = sfp32_ ? 4 : 2;
+    slot_mv_ = empty({(int64_t)nslot_ * 2 * slot_elems_ * es / 2}, DType::BF16);
+    HIP_OK(hipStreamCreateWithFlags(&cstream_, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&cjoin_ev_, hipEventDisableTiming));
+    h2d_ev_.resize(nupd);
+    for (auto& e : h2d_ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    h2d_pending_.assign(nupd, 0);
+    for (int i = 0; i < nslot_; ++i) slot_copy(i, true);  // the first S updates' moments
+    HIP_OK(hipStreamSynchronize(cstream_));
+    return;
+  }
+  // in place: the updates' workgroups hold their CUs for milliseconds (PCIe-bound): the persistent GEMMs
+  // keep that many CUs out of their grids instead of queueing a statically assigned workgroup behind one
+  // (MFT_Z3_RESERVE=0: off, A/B; profiles/r5_offload_reserve.txt)
+  const char* rv = std::getenv("MFT_Z3_RESERVE");
+  ::mft::gemm4_reserve_cus(rv && rv[0] == '0' ? 0 : opt_grid_);
+}
+
+void* Zero3::slot_ptr(int i, int which) {
+  const int64_t es = sfp32_ ? 4 : 2;
+  return static_cast<char*>(slot_mv_.data_ptr()) + ((int64_t)(i % nslot_) * 2 + which) * slot_elems_ * es;
+}
+
+void Zero3::slot_copy(int i, bool h2d) {
+  const int64_t n = upd_len(i);
+  if (n <= 0) return;
+  const size_t es = sfp32_ ? 4 : 2, off = (size_t)upd_off(i) * es;
+  char* hm = static_cast<char*>(sopt_->m.data_ptr()) + off;
+  char* hv = static_cast<char*>(sopt_->v.data_ptr()) + off;
+  if (h2d) {
+    HIP_OK(hipMemcpyAsync(slot_ptr(i, 0), hm, (size_t)n * es, hipMemcpyHostToDevice, cstream_));
+    HIP_OK(hipMemcpyAsync(slot_ptr(i, 1), hv, (size_t)n * es, hipMemcpyHostToDevice, cstream_));
+  } else {
+    HIP_OK(hipMemcpyAsync(hm, slot_ptr(i, 0), (size_t)n * es, hipMemcpyDeviceToHost, cstream_));
+    HIP_OK(hipMemcpyAsync(hv, slot_ptr(i, 1), (size_t)n * es, hipMemcpyDeviceToHost, cstream_));
+  }
 }
 
 // ---------------------------------------------------------------- host-streamed optimizer
@@ -214,11 +273,17 @@ void Zero3::opt_fork() {
   if (forked_) return;
   forked_ = true;
   HIP_OK(hipEventRecord(fork_ev_, current_stream()));
-  HIP_OK(hipStreamWaitEvent(ostream_, fork_ev_, 0));
+  HIP_OK(hipStreamWaitEvent(staged_ ? stream_ : ostream_, fork_ev_, 0));
 }
 
 void Zero3::join_opt_stream() {
-  HIP_OK(hipEventRecord(ojoin_ev_, ostream_));
+  if (staged_) {  // copy stream -> communication stream -> current stream (never a side-stream ring)
+    HIP_OK(hipEventRecord(cjoin_ev_, cstream_));
+    HIP_OK(hipStreamWaitEvent(stream_, cjoin_ev_, 0));
+    HIP_OK(hipEventRecord(ojoin_ev_, stream_));
+  } else {
+    HIP_OK(hipEventRecord(ojoin_ev_, ostream_));
+  }
   HIP_OK(hipStreamWaitEvent(current_stream(), ojoin_ev_, 0));
 }
 
@@ -227,6 +292,31 @@ void Zero3::opt_update(int i) {
   supd_[i] = 1;
   Z3_TRACE("update %d\n", i);
   opt_fork();
+  if (staged_) {
+    // on the communication stream, which all-gathers the updated partition next.  Its slot was filled
+    // either this step (an event of this step) or in the previous one (joined at that step's finish)
+    const int nupd = (int)supd_.size();
+    if (h2d_pending_[i]) HIP_OK(hipStreamWaitEvent(stream_, h2d_ev_[i], 0));
+    h2d_pending_[i] = 0;
+    const int64_t n = upd_len(i);
+    if (n > 0)
+      sopt_->apply_delayed(upd_off(i), n, slot_ptr(i, 0), slot_ptr(i, 1), !sfp32_, stream_, 0);
+    HIP_OK(hipEventRecord(upd_ev_[i], stream_));
+    HIP_OK(hipStreamWaitEvent(cstream_, upd_ev_[i], 0));
+    slot_copy(i, false);                                          // write the moments back ...
+    const int next = i + nslot_ < nupd ? i + nslot_ : i % nslot_;  // ... and prefetch the slot's next user
+    if (next != i) {
+      slot_copy(next, true);
+      if (next > i) {
+        HIP_OK(hipEventRecord(h2d_ev_[next], cstream_));
+        h2d_pending_[next] = 1;
+      }
+    }
+    bool all = true;
+    for (int c : supd_) all = all && c;
+    if (all) sopt_->commit_delayed(stream_);
+    return;
+  }
   const int64_t n = upd_len(i);
   if (n > 0) {  // the moments of the partition, in place in pinned host DRAM
     const size_t es = sfp32_ ? 4 : 2, off = (size_t)upd_off(i) * es;
@@ -260,6 +350,15 @@ void Zero3::flush_optimizer() {
   forked_ = false;
   std::fill(supd_.begin(), supd_.end(), 0);
   holder_.assign(holder_.size(), -1);  // every partition changed
+}
+
+void Zero3::optimizer_state_loaded() {
+  if (!staged_) return;
+  // the step starts with slot k holding update k's moments
+  HIP_OK(hipDeviceSynchronize());
+  for (int i = 0; i < nslot_; ++i) slot_copy(i, true);
+  HIP_OK(hipStreamSynchronize(cstream_));
+  std::fill(h2d_pending_.begin(), h2d_pending_.end(), 0);
 }
 
 void Zero3::gather(int u) {

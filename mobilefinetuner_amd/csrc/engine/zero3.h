@@ -84,6 +84,9 @@ class Zero3 : public GradReducer, public BlockProvider {
   bool owns_optimizer() const override { return sopt_ != nullptr; }
   void prepare_optimizer() override;
   void flush_optimizer() override;
+  void optimizer_state_loaded() override;
+  bool graph_capturable() const override { return !(sopt_ && staged_); }
+  int staged_slots() const { return sopt_ && staged_ ? nslot_ : 0; }  // 0: in place (or no host moments)
   bool params_sharded() const override { return true; }
   float grad_prescale() const override;
   void zero_grad(FlatParams& flat) override;
@@ -147,6 +150,19 @@ class Zero3 : public GradReducer, public BlockProvider {
   // profiles/r4_offload_modes.txt).
   hipStream_t ostream_ = nullptr;
   int opt_grid_ = 0;  // workgroups per update (MFT_Z3_OPT_GRID)
+  // staged (default; MFT_Z3_STAGED=0: in place): the moments of update i live in device slot i % S during
+  // the step; update i runs on the communication stream (device-resident, full grid), the one copy stream
+  // writes the slot back and prefetches its next user -- streams: copy <-> communication ping-pong only
+  bool staged_ = false;
+  int nslot_ = 0;
+  int64_t slot_elems_ = 0;
+  Tensor slot_mv_;                   // [S][m | v][slot_elems_] (bf16 or fp32 moments)
+  hipStream_t cstream_ = nullptr;    // SDMA copies, both directions
+  hipEvent_t cjoin_ev_ = nullptr;
+  std::vector<hipEvent_t> h2d_ev_;   // per update: its slot filled (recorded this step)
+  std::vector<char> h2d_pending_;    // h2d_ev_[i] recorded this step and not yet waited on
+  void* slot_ptr(int i, int which);  // which: 0 = m, 1 = v
+  void slot_copy(int i, bool h2d);
 };
 
 }  // namespace eng

@@ -129,6 +129,8 @@ void gemm8x(const GemmArgs& g, int epi, bool a_t, bool b_t, hipStream_t st);
 // 256x256x64 4-wave GEMM with a hand-scheduled K-tile body (gemm4.hip); NT layout
 void gemm4x(const GemmArgs& g, int epi, bool a_t, bool b_t, hipStream_t st);
 bool gemm4_supported(int M, int N, int K, bool a_t, bool b_t);
+// persistent gemm4 grids leave n CUs free (for a long-running kernel on a side stream; 0 = every CU)
+void gemm4_reserve_cus(int n);
 // short-token NT GEMM (gemm_s.hip): 64 x 64 tiles, K split over the 4 waves; NONE / BIAS / BIAS_GELU_D /
 // MUL_AUX / DGELU / BIAS_ADD and the second K segment (K2, NONE only).  gemm_s_preferred: the shape's
 // gemm4 tiles would fill less than half the CUs

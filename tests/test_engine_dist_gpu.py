@@ -184,10 +184,11 @@ def test_native_zero3_streamed_optimizer_flushes_in_graph_mode(tmp_path, every):
     eager run without evaluations."""
     base = FULL + ["--batch_size", "4", "--zero_stage", "3", "--offload", "host", "--offload_moments", "fp32"]
     ref_out, out = str(tmp_path / "eager.safetensors"), str(tmp_path / "graph.safetensors")
-    ref = _run_ranks([_bin("gpt2_full_finetune"), *base, "--no_graph", "--output_path", ref_out], 2)
+    inplace = {"MFT_Z3_STAGED": "0"}  # (the staged variant runs eagerly: test_native_zero3_staged_moments_match_in_place)
+    ref = _run_ranks([_bin("gpt2_full_finetune"), *base, "--no_graph", "--output_path", ref_out], 2, extra_env=inplace)
     assert all(rc == 0 for rc, _, _ in ref), ref[0][1][-2000:] + ref[0][2][-2000:]
     got = _run_ranks([_bin("gpt2_full_finetune"), *base, "--eval_interval", str(every), "--eval_batches", "2",
-                      "--output_path", out], 2)
+                      "--output_path", out], 2, extra_env=inplace)
     assert all(rc == 0 for rc, _, _ in got), got[0][1][-2000:] + got[0][2][-2000:]
     assert "hipGraph" in got[0][1], got[0][1][:3000]
     assert loss_list(got[0][1], True) == pytest.approx(loss_list(ref[0][1], True), rel=2e-4, abs=2e-4)
@@ -197,6 +198,30 @@ def test_native_zero3_streamed_optimizer_flushes_in_graph_mode(tmp_path, every):
     # Adam step would move elements by ~lr = 1e-3)
     for k in a:
         assert torch.allclose(a[k], b[k], atol=2e-5, rtol=0), (every, k, (a[k] - b[k]).abs().max())
+
+
+@pytest.mark.parametrize("slots,moments", [("1", "fp32"), ("2", "bf16"), ("", "bf16")])
+def test_native_zero3_staged_moments_match_in_place(tmp_path, slots, moments):
+    """The staged host-moment optimizer (device slots refilled by SDMA copies on one copy stream: the slot
+    written back after its update and prefetched for its next user, across the step boundary) ends with the
+    same weights as the in-place zero-copy update (MFT_Z3_STAGED=0), both eager (the staged step never
+    captures), two loopback ranks, evaluations (flushes) every 2 steps -- with one slot (every update
+    waits for its own prefetch), two, and the default."""
+    base = FULL + ["--batch_size", "4", "--zero_stage", "3", "--offload", "host", "--offload_moments", moments]
+    ref_out, out = str(tmp_path / "inplace.safetensors"), str(tmp_path / "staged.safetensors")
+    ref = _run_ranks([_bin("gpt2_full_finetune"), *base, "--no_graph", "--output_path", ref_out], 2,
+                     extra_env={"MFT_Z3_STAGED": "0"})
+    assert all(rc == 0 for rc, _, _ in ref), ref[0][1][-2000:] + ref[0][2][-2000:]
+    env = {"MFT_Z3_STAGED": "1", **({"MFT_Z3_SLOTS": slots} if slots else {})}
+    got = _run_ranks([_bin("gpt2_full_finetune"), *base, "--eval_interval", "2", "--eval_batches", "2",
+                      "--output_path", out], 2, extra_env=env)
+    assert all(rc == 0 for rc, _, _ in got), got[0][1][-2000:] + got[0][2][-2000:]
+    assert "step runs eagerly" in got[0][1] and "slots]" in got[0][1], got[0][1][:3000]
+    assert loss_list(got[0][1], True) == pytest.approx(loss_list(ref[0][1], True), rel=2e-4, abs=2e-4)
+    from mobilefinetuner_amd.io import safetensors as st
+    a, b = st.load_file(ref_out), st.load_file(out)
+    for k in a:
+        assert torch.allclose(a[k], b[k], atol=2e-5, rtol=0), (slots, k, (a[k] - b[k]).abs().max())
 
 
 @pytest.mark.parametrize("stage", ["2", "3", "3+offload"])
