@@ -121,6 +121,8 @@ struct GemmArgs {
   const bf16_t* B2;
   long ldb2;
   int K2;
+  // gemm4 epilogue operand (aux) loads: 0 = non-temporal (default), 1 = default cache policy (A/B)
+  int aux_pol;
 };
 // 256x256 8-phase pipelined GEMM (gemm8.hip); same epilogues.  a_t: A stored [K, M]; b_t: B stored
 // [K, N] (NN data-grad); both: TN weight-grad (use GEMM_EPI_F32ACC with gemm8_pick_ksplit / ws)
