@@ -401,6 +401,46 @@ __device__ __forceinline__ void store_tile16(bf16_t* scratch, int ld, const f32x
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---- short-path LDS images ([rows][D] bf16, D = 64: 8 16-B chunks a row): chunk c of row r sits at
+// c ^ sws(r), sws(r) = ((r >> 1) & 3) << 1 | ((r >> 3) & 1).  A ds_read_b128 row fragment (16 rows, one
+// chunk) then covers 16 distinct 16-B bank groups, and each 32-lane half of a frag_tr_perm pair (rows
+// 4g + q, 2 chunks x 2 halves) 32 distinct 8-B slots; the plain [rows][64] image put 58 % of the kernels'
+// LDS cycles into bank conflicts (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, profiles/r5_attn64_lds.txt).
+// Rows r and r + 16 share the swizzle (the second read of a pair is an immediate offset).
+template <int D>
+__device__ __forceinline__ int sws(int r) {
+  if constexpr (D == 64) return (((r >> 1) & 3) << 1) | ((r >> 3) & 1);
+  else return 0;
+}
+template <int D>
+__device__ __forceinline__ int sw_off(int r, int ch) { return r * D + ((ch ^ sws<D>(r)) << 3); }
+template <int D>
+__device__ __forceinline__ bf16x8_t frag_row_s(const bf16_t* t, int r0, int c0) {
+  const int l = threadIdx.x & 63;
+  const int r = r0 + (l & 15), ch = (c0 >> 3) + (l >> 4);
+  return *reinterpret_cast<const bf16x8_t*>(t + sw_off<D>(r, ch));
+}
+template <int D>
+__device__ __forceinline__ bf16x8_t frag_tr_perm_s(const bf16_t* t, int r0, int c0) {  // frag_tr_perm (mfma.h)
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const int ra = r0 + 4 * g + q, col = c0 + 4 * p, ch = col >> 3, off = col & 7;
+  s16x4_t lo = ds_tr16(t + sw_off<D>(ra, ch) + off);
+  s16x4_t hi = ds_tr16(t + sw_off<D>(ra + 16, ch) + off);
+  s16x8_t rr = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, rr);
+}
+template <int D>
+__device__ __forceinline__ bf16x8_t frag_tr_s(const bf16_t* t, int r0, int c0) {  // frag_tr (mfma.h)
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const int ra = r0 + 8 * g + q, col = c0 + 4 * p, ch = col >> 3, off = col & 7;
+  s16x4_t lo = ds_tr16(t + sw_off<D>(ra, ch) + off);
+  s16x4_t hi = ds_tr16(t + sw_off<D>(ra + 4, ch) + off);
+  s16x8_t rr = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, rr);
+}
+
 // ---- v2: P (fwd) / P^T, dS^T (bwd) stay in registers -------------------------------------------
 // Scores are computed transposed (S^T = K Q^T: keys in C rows, queries in C columns), so two
 // 16-key C blocks ARE the A operand of the next MFMA over keys (pack_c2a / frag_tr_perm, mfma.h):
@@ -442,8 +482,8 @@ __global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __re
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int c = threadIdx.x + j * 512, r = c / CPR, ch = c % CPR;
-    *reinterpret_cast<u16x8_t*>(Ks + r * D + ch * 8) = kr[j];
-    *reinterpret_cast<u16x8_t*>(Vs + r * D + ch * 8) = vr[j];
+    *reinterpret_cast<u16x8_t*>(Ks + sw_off<D>(r, ch)) = kr[j];
+    *reinterpret_cast<u16x8_t*>(Vs + sw_off<D>(r, ch)) = vr[j];
   }
   __syncthreads();
   if (16 * w >= S) return;
@@ -455,7 +495,7 @@ __global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __re
     st[kb] = zero4();
     if (kb < nbmax) {
 #pragma unroll
-      for (int s = 0; s < D / 32; ++s) st[kb] = mfma16(frag_row(Ks, D, kb * 16, s * 32), qf[s], st[kb]);
+      for (int s = 0; s < D / 32; ++s) st[kb] = mfma16(frag_row_s<D>(Ks, kb * 16, s * 32), qf[s], st[kb]);
     }
   }
   float mx = -INFINITY;
@@ -492,7 +532,7 @@ __global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __re
     if (2 * kk < nbmax) {
       const bf16x8_t pa = pack_c2a(st[2 * kk], st[2 * kk + 1]);
 #pragma unroll
-      for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr_perm(Vs, D, kk * 32, n * 16), acc[n]);
+      for (int n = 0; n < D / 16; ++n) acc[n] = mfma16(pa, frag_tr_perm_s<D>(Vs, kk * 32, n * 16), acc[n]);
     }
   }
   // acc rows are queries 4g+i: fetch their 1/l from the lane that owns that query column
@@ -510,9 +550,10 @@ __global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __re
 // A operand (m = key, k = query) of dV += P^T dO and dK += dS^T Q after pack_c2a, with the B rows
 // permuted to match (frag_tr_perm).  dS is kept packed in registers; after a block barrier (V and
 // dO dead) it is written to a swizzled [query][key] image that aliases them, and phase 2 (wave w
-// owns queries 16w..) forms dQ = dS K.  LDS = K, V, Q, dO (64 KB) + lse/delta: two workgroups per CU.
+// owns queries 16w..) forms dQ = dS K.  LDS = K, V, Q, dO (64 KB) + lse/delta: two workgroups per CU,
+// which needs 4 waves per SIMD, i.e. <= 128 VGPRs (the launch bound's second argument is waves per SIMD).
 template <int D>
-__global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
+__global__ __launch_bounds__(512, 4) void attn_bwd_short2_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     bf16_t* __restrict__ dq, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, AttnStrides qs, AttnStrides ks,
@@ -550,10 +591,10 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int c = threadIdx.x + j * 512, r = c / CPR, ch = c % CPR;
-      *reinterpret_cast<u16x8_t*>(Ks + r * D + ch * 8) = kr[j];
-      *reinterpret_cast<u16x8_t*>(Vs + r * D + ch * 8) = vr[j];
-      *reinterpret_cast<u16x8_t*>(Qs + r * D + ch * 8) = qr[j];
-      *reinterpret_cast<u16x8_t*>(dOs + r * D + ch * 8) = dr[j];
+      *reinterpret_cast<u16x8_t*>(Ks + sw_off<D>(r, ch)) = kr[j];
+      *reinterpret_cast<u16x8_t*>(Vs + sw_off<D>(r, ch)) = vr[j];
+      *reinterpret_cast<u16x8_t*>(Qs + sw_off<D>(r, ch)) = qr[j];
+      *reinterpret_cast<u16x8_t*>(dOs + sw_off<D>(r, ch)) = dr[j];
       float dsum = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) dsum += bf2f(dr[j][e]) * bf2f(orr[j][e]);
@@ -581,8 +622,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
       if (live) {
 #pragma unroll
         for (int s2 = 0; s2 < D / 32; ++s2) {
-          sc[t] = mfma16(frag_row(Qs, D, 32 * kk + 16 * t, s2 * 32), frag_row(Ks, D, 16 * w, s2 * 32), sc[t]);
-          dp[t] = mfma16(frag_row(dOs, D, 32 * kk + 16 * t, s2 * 32), frag_row(Vs, D, 16 * w, s2 * 32), dp[t]);
+          sc[t] = mfma16(frag_row_s<D>(Qs, 32 * kk + 16 * t, s2 * 32), frag_row_s<D>(Ks, 16 * w, s2 * 32), sc[t]);
+          dp[t] = mfma16(frag_row_s<D>(dOs, 32 * kk + 16 * t, s2 * 32), frag_row_s<D>(Vs, 16 * w, s2 * 32), dp[t]);
         }
       }
 #pragma unroll
@@ -601,8 +642,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
       const bf16x8_t da = pack_c2a(dp[0], dp[1]);
 #pragma unroll
       for (int n = 0; n < D / 16; ++n) {
-        dVa[n] = mfma16(pa, frag_tr_perm(dOs, D, 32 * kk, n * 16), dVa[n]);
-        dKa[n] = mfma16(da, frag_tr_perm(Qs, D, 32 * kk, n * 16), dKa[n]);
+        dVa[n] = mfma16(pa, frag_tr_perm_s<D>(dOs, 32 * kk, n * 16), dVa[n]);
+        dKa[n] = mfma16(da, frag_tr_perm_s<D>(Qs, 32 * kk, n * 16), dKa[n]);
       }
     }
   }
@@ -638,7 +679,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_short2_kernel(
       const int qr = 16 * w + c16, ch = 4 * kk + g;
       const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(DS + qr * SM + ((ch ^ (qr & 15)) << 3));
 #pragma unroll
-      for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(a, frag_tr(Ks, D, kk * 32, n * 16), dQa[n]);
+      for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(a, frag_tr_s<D>(Ks, kk * 32, n * 16), dQa[n]);
     }
   }
   if (16 * w < S) store_tile16<D>(T, D, dQa, one, dq, dqs, b, h, 16 * w, min(16, S - 16 * w));
