@@ -564,7 +564,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_short2_kernel(
   bf16_t* Ks = smem;           // [SM][D]
   bf16_t* Vs = Ks + SM * D;    // [SM][D]   } phase 2: dS image [SM q][SM keys], 16-B chunks
   bf16_t* dOs = Vs + SM * D;   // [SM][D]   }   swizzled chunk ^ (q & 15)
-  bf16_t* Qs = dOs + SM * D;   // [SM][D]   (after phase 1: per-wave [16][D] output staging)
+  bf16_t* Qs = dOs + SM * D;   // [SM][D]   (after phase 1: per-wave [16][D + 8] output staging)
   bf16_t* DS = Vs;
   float* lse_s = reinterpret_cast<float*>(Qs + SM * D);  // [SM]
   float* del_s = lse_s + SM;                             // [SM]
@@ -648,23 +648,34 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_short2_kernel(
     }
   }
   __syncthreads();  // V, dO (and Q) are dead from here on
-  // dS image [q][key]: element (q, key) at q*SM + ((key/8 ^ (q&15)) * 8) + key%8
+  // dS image [q][key]: element (q, key) at q*SM + ((key/8 ^ (q&15)) * 8) + key%8.  Written as dwords (two
+  // adjacent keys): a lane holds 4 queries of one key, so lane pairs (key, key + 1) swap halves by DPP --
+  // the even lane writes queries 4g, 4g + 1, the odd lane 4g + 2, 4g + 3 (half the writes, no two lanes
+  // sharing a dword)
+  {
+    const bool odd = key & 1;
+    const int kp = key & ~1;
 #pragma unroll
-  for (int qb = 0; qb < SM / 16; ++qb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int qi = 16 * qb + 4 * g + i;
-      const uint32_t pr = dsp[qb][i >> 1];
-      const bf16_t val = (i & 1) ? (bf16_t)(pr >> 16) : (bf16_t)(pr & 0xFFFF);
-      DS[qi * SM + (((key >> 3) ^ (qi & 15)) << 3) + (key & 7)] = val;
+    for (int qb = 0; qb < SM / 16; ++qb) {
+      const uint32_t p0 = dsp[qb][0], p1 = dsp[qb][1];  // queries (4g, 4g + 1), (4g + 2, 4g + 3)
+      const uint32_t n0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p0, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+      const uint32_t n1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p1, 0xB1, 0xF, 0xF, false);
+      const uint32_t wa = odd ? ((n1 & 0xFFFFu) | (p1 << 16)) : ((p0 & 0xFFFFu) | (n0 << 16));
+      const uint32_t wb = odd ? ((n1 >> 16) | (p1 & 0xFFFF0000u)) : ((p0 >> 16) | (n0 & 0xFFFF0000u));
+      const int qa = 16 * qb + 4 * g + (odd ? 2 : 0), qc = qa + 1;
+      *reinterpret_cast<uint32_t*>(DS + qa * SM + (((kp >> 3) ^ (qa & 15)) << 3) + (kp & 7)) = wa;
+      *reinterpret_cast<uint32_t*>(DS + qc * SM + (((kp >> 3) ^ (qc & 15)) << 3) + (kp & 7)) = wb;
     }
-  // dK, dV of this wave's keys (staging tile in the dead Q region)
+  }
+  // dK, dV of this wave's keys (staging tile over the dead Q and lse / delta region, pitch D + 8: the four
+  // 16-lane groups of the 2-byte staging writes on different banks -- at pitch D they all met, 4-way)
   const int hout = dkv_per_qhead ? h : hk;
   const float one[4] = {1.f, 1.f, 1.f, 1.f};
-  bf16_t* T = Qs + w * 16 * D;
+  constexpr int LDT = D + 8;
+  bf16_t* T = Qs + w * 16 * LDT;
   if (16 * w < S) {
-    store_tile16<D>(T, D, dKa, one, dk, dks, b, hout, 16 * w, min(16, S - 16 * w));
-    store_tile16<D>(T, D, dVa, one, dv, dvs, b, hout, 16 * w, min(16, S - 16 * w));
+    store_tile16<D>(T, LDT, dKa, one, dk, dks, b, hout, 16 * w, min(16, S - 16 * w));
+    store_tile16<D>(T, LDT, dVa, one, dv, dvs, b, hout, 16 * w, min(16, S - 16 * w));
   }
   __syncthreads();
 
@@ -682,7 +693,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_short2_kernel(
       for (int n = 0; n < D / 16; ++n) dQa[n] = mfma16(a, frag_tr_s<D>(Ks, kk * 32, n * 16), dQa[n]);
     }
   }
-  if (16 * w < S) store_tile16<D>(T, D, dQa, one, dq, dqs, b, h, 16 * w, min(16, S - 16 * w));
+  if (16 * w < S) store_tile16<D>(T, LDT, dQa, one, dq, dqs, b, h, 16 * w, min(16, S - 16 * w));
 }
 
 // ============================================================================================
@@ -1754,7 +1765,9 @@ template <int D>
 static void bwd_launch(const AttnBwdArgs& a, hipStream_t stream) {
   if constexpr (D == 64) {
     if (attn_short_path(D, a.Sq, a.Sk, a.window)) {
-      const size_t shm = sizeof(bf16_t) * 4 * kShortS * D + sizeof(float) * 2 * kShortS;
+      // K, V, dO + max(Q + lse / delta, the per-wave output staging at pitch D + 8 that overlays them)
+      const size_t shm = sizeof(bf16_t) * 3 * kShortS * D +
+                         std::max(sizeof(bf16_t) * kShortS * D + sizeof(float) * 2 * kShortS, sizeof(bf16_t) * 8 * 16 * (D + 8));
       static bool attr = false;
       if (!attr) {
         MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_short2_kernel<D>,
