@@ -235,8 +235,11 @@ Tensor attention_packed(const Tensor& qkv, float scale, bool causal, int window,
   a.scale = scale;
   a.causal = causal;
   a.window = window;
+  // the widened output's zero columns: written by the short-path kernel itself (no launch of their own)
+  const bool pad_in_kernel = oc > HD && (oc - HD) % 8 == 0 && ::mft::attn_short_path(D, Sq, Sq, window);
+  a.o_pad = pad_in_kernel ? oc - HD : 0;
   ::mft::attn_fwd(a, S());
-  if (oc > HD) ::mft::zero_cols(bp(o_full), oc, (long)B * Sq, HD, oc - HD, S());
+  if (oc > HD && !pad_in_kernel) ::mft::zero_cols(bp(o_full), oc, (long)B * Sq, HD, oc - HD, S());
   if (needs_grad(qkv)) {
     auto n = lambda_node("FlashAttentionBackward", [qd, o, lse, scale, causal, window, B, Sq, H, D,
                                                      HD](std::vector<Tensor>& g) {

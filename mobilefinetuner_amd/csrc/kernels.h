@@ -38,6 +38,9 @@ struct AttnArgs {
   float scale;
   int causal, window;
   const int* kv_lens;
+  // short path (attn_short_path) only: zero o_pad columns (% 8) after the H heads of each output row (a
+  // widened output for an augmented-K consumer); other paths leave them to the caller
+  int o_pad;
 };
 struct AttnBwdArgs {
   const bf16_t *q, *k, *v, *o, *dout;

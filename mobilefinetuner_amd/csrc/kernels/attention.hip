@@ -451,7 +451,8 @@ __global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __re
                                                               const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                               float* __restrict__ lse, AttnStrides qs, AttnStrides ks,
                                                               AttnStrides vs, AttnStrides os, int H, int Hkv, int S,
-                                                              float scale, int causal, const int* __restrict__ kv_lens) {
+                                                              float scale, int causal, const int* __restrict__ kv_lens,
+                                                              int o_pad) {
   constexpr int SM = kShortS, NB = SM / 16, CPR = D / 8, LDO = D + 8;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   bf16_t* Ks = smem;                                      // [SM][D]
@@ -461,6 +462,11 @@ __global__ __launch_bounds__(512) void attn_fwd_short2_kernel(const bf16_t* __re
   const int h = blockIdx.x, b = blockIdx.y, hk = h / (H / Hkv);
   const int kv_len = kv_lens ? min(kv_lens[b], S) : S;
   const float c2 = scale * kLog2e;
+  if (h == 0 && o_pad > 0) {  // the o_pad zero columns after the H heads of every output row of batch b
+    const int per = o_pad / 8;
+    for (int c = threadIdx.x; c < S * per; c += 512)
+      *reinterpret_cast<u16x8_t*>(o + b * os.sb + (long)(c / per) * os.ss + (long)H * D + (c % per) * 8) = u16x8_t{};
+  }
   constexpr int PER = SM * CPR / 512;
   u16x8_t kr[PER], vr[PER];
 #pragma unroll
@@ -1737,7 +1743,7 @@ static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
       }
       attn_fwd_short2_kernel<D><<<dim3(a.H, a.B), 512, shm, stream>>>(a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st),
                                                                        mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.scale,
-                                                                       a.causal, a.kv_lens);
+                                                                       a.causal, a.kv_lens, a.o_pad);
       return;
     }
   }
