@@ -726,7 +726,39 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
       bool v_padded = false;  // lora_dy zeroes the padding itself (one adapter of rank 8)
       int o = 0;
       std::vector<bool> db_done(ads.size(), false);
-      for (size_t i = 0; i < ads.size(); ++i) {
+      // several rank-8 adapters on 256-aligned column ranges of this dy (Gemma-3's q | k | v, gate | up): one
+      // lora_dy launch over all of them and one finish (MFT_LORA_DY_MULTI=0: per adapter, A/B)
+      static const bool multi_off = std::getenv("MFT_LORA_DY_MULTI") && std::getenv("MFT_LORA_DY_MULTI")[0] == '0';
+      if (!multi_off && ads.size() > 1 && ads.size() <= 4 && !deterministic()) {
+        std::vector<::mft::LoraDyAdapter> la;
+        int oo = 0;
+        for (size_t i = 0; i < ads.size(); ++i) {
+          auto& a = ads[i];
+          if (a.rank != 8 || !a.B.trainable() || (K + oo) % 8) break;
+          ::mft::LoraDyAdapter e{};
+          e.B = (const ::mft::bf16_t*)a.B.c.data_ptr();
+          e.ldb = a.B.c.stride(0);
+          e.u = (const ::mft::bf16_t*)bp(xa2) + K + oo;
+          e.ldu = xa2.stride(0);
+          e.dB = fp(grad_buffer(a.B.leaf));
+          e.ldd = a.ncols;
+          e.v = (::mft::bf16_t*)bp(vall) + oo;
+          e.ldv = vall.stride(0);
+          e.col0 = a.col0;
+          e.N = a.ncols;
+          e.vz = seg2 && i + 1 == ads.size() && oo + 8 == rt ? 64 - rt : 0;
+          la.push_back(e);
+          oo += a.rank;
+        }
+        if (la.size() == ads.size() && ::mft::lora_dy_multi_ok(la.data(), (int)la.size()) && dy2.stride(0) % 8 == 0) {
+          Tensor vpart = empty({::mft::lora_dy_multi_vpart_floats(la.data(), (int)la.size(), M)}, DType::F32, dy2.device());
+          ::mft::lora_dy_multi(bp(dy2), dy2.stride(0), la.data(), (int)la.size(), fp(vpart), M, s, S());
+          std::fill(db_done.begin(), db_done.end(), true);
+          v_padded = la.back().vz > 0;
+          o = rt;
+        }
+      }
+      for (size_t i = 0; i < ads.size() && o < rt; ++i) {
         auto& a = ads[i];
         Tensor v = vall.slice(1, o, o + a.rank);
         Tensor dys = dy2.slice(1, a.col0, a.col0 + a.ncols);

@@ -304,6 +304,24 @@ long lora_wgrad_ws_floats(long M, int K, int R);
 void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t* u, long ldu, float* dB, long ldd,
              float* vpart, bf16_t* v, long ldv, long M, int N, float s, hipStream_t st, float* det_ws = nullptr, int vzero = 0);
 long lora_dy_ws_floats(long M, int N);  // deterministic-mode workspace of lora_dy (det_ws)
+// lora_dy over up to 4 rank-8 adapters on column ranges of ONE dy (q | k | v of a fused projection): one
+// launch + one finish.  col0 % 256 == 0, ranges ascending and disjoint in 256-column strips; vz: zero columns
+// 8 .. 8 + vz - 1 of that adapter's v (% 8).  vpart: fp32 scratch of (strips of the whole range) * M * 8
+struct LoraDyAdapter {
+  const bf16_t* B;
+  long ldb;
+  const bf16_t* u;
+  long ldu;
+  float* dB;
+  long ldd;
+  bf16_t* v;
+  long ldv;
+  int col0, N, vz;
+};
+bool lora_dy_multi_ok(const LoraDyAdapter* ads, int n);
+long lora_dy_multi_vpart_floats(const LoraDyAdapter* ads, int n, long M);
+void lora_dy_multi(const bf16_t* dy, long ldy, const LoraDyAdapter* ads, int n, float* vpart, long M, float s,
+                   hipStream_t st);
 // workgroups of the lora_dy / lora_xty (MFMA) grids for an [M, N] operand: <= 512, one resident round
 long lora_dy_grid_blocks(long M, int N);
 // W[k*wsk + n*wsn] += s * sum_r A[r, k] * B[r, n]   (A [R,K], B [R,N] fp32)

@@ -313,17 +313,38 @@ __global__ void lora_wgrad_reduce_kernel(const float* __restrict__ ws, int ny, i
 // strip, N <= 256: v is written directly).
 constexpr int kDyLd = 256 + 8;  // padded LDS row (elements): transposed reads conflict-free
 
+// several adapters in one launch (lora_dy_multi): strip blockIdx.x belongs to adapter a with
+// strip0[a] <= x < strip0[a + 1]; its operands replace the single-adapter arguments
+struct LoraDyTable {
+  int n;
+  int strip0[5];
+  const bf16_t* B[4];
+  long ldb[4];
+  const bf16_t* u[4];
+  long ldu[4];
+  float* dB[4];
+  long ldd[4];
+  int N[4];
+};
+
 __global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restrict__ dy, long ldy,
                                                          const bf16_t* __restrict__ B, long ldb,
                                                          const bf16_t* __restrict__ u, long ldu, float* __restrict__ dB,
                                                          long ldd, float* __restrict__ vpart, long M, int N, long chunk,
                                                          float s, float* __restrict__ det_ws, long det_np,
-                                                         bf16_t* __restrict__ vout, long ldv) {
+                                                         bf16_t* __restrict__ vout, long ldv, LoraDyTable tb) {
   // per wave: dy image [32][kDyLd] + u^T image [32][16]; block reduction buffer aliases the images
   __shared__ __attribute__((aligned(16))) bf16_t lds[4][32 * kDyLd + 32 * 16];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, c16 = lane & 15;
-  const int n0 = blockIdx.x * 256;
+  int n0 = blockIdx.x * 256;
+  if (tb.n > 0) {  // (workgroup-uniform)
+    int a = 0;
+    for (int i = 1; i < tb.n; ++i) a = (int)blockIdx.x >= tb.strip0[i] ? i : a;
+    dy += (long)tb.strip0[a] * 256;
+    B = tb.B[a], ldb = tb.ldb[a], u = tb.u[a], ldu = tb.ldu[a], dB = tb.dB[a], ldd = tb.ldd[a], N = tb.N[a];
+    n0 = ((int)blockIdx.x - tb.strip0[a]) * 256;
+  }
   bf16_t* img = lds[w];
   bf16_t* uimg = lds[w] + 32 * kDyLd;
   // B^T fragments of the strip: lane holds B[r = l&15][n0 + 32 cg + 8g + j] (zero for r >= 8 / n >= N)
@@ -424,6 +445,26 @@ __global__ __launch_bounds__(256, 2) void lora_dy_kernel(const bf16_t* __restric
   }
 }
 
+// the adapters' v from their strips' partials: adapter blockIdx.y, strips [strip0, strip1)
+struct LoraDyFinTable {
+  int strip0[5];
+  bf16_t* v[4];
+  long ldv[4];
+  int vz[4];
+};
+__global__ void lora_dy_finish_multi_kernel(const float* __restrict__ vpart, long M, float s, LoraDyFinTable ft) {
+  const int a = blockIdx.y;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= M * 8) return;
+  float acc = 0.f;
+  for (int k = ft.strip0[a]; k < ft.strip0[a + 1]; ++k) acc += vpart[(long)k * M * 8 + t];
+  bf16_t* v = ft.v[a];
+  const long ldv = ft.ldv[a];
+  v[(t >> 3) * ldv + (t & 7)] = f2bf(acc * s);
+  const int c = (int)(t & 7), vz = ft.vz[a];
+  if (c >= 1 && 8 * c < 8 + vz) *reinterpret_cast<uint4*>(v + (t >> 3) * ldv + 8 * c) = uint4{0u, 0u, 0u, 0u};
+}
+
 // v[m, r] = s * sum over strips of vpart[strip, m, r]   (bf16 out, row stride ldv)
 // vz > 0: also zero v's columns 8 .. 8 + vz - 1 (vz % 8 == 0; 16-B stores, ldv % 8 == 0) -- the zero padding
 // of the gemm4 second K segment (engine/nn.cpp), without a launch of its own
@@ -463,6 +504,50 @@ static long dy_chunks(long M, int N, long* chunk_out) {
   return cdiv(M, chunk);
 }
 
+bool lora_dy_multi_ok(const LoraDyAdapter* ads, int n) {
+  if (n < 1 || n > 4) return false;
+  int next = 0;  // first free strip
+  for (int i = 0; i < n; ++i) {
+    const LoraDyAdapter& a = ads[i];
+    if (a.col0 % 256 || a.col0 / 256 < next || a.N <= 0 || a.N % 8 || a.ldb % 8 || a.ldu % 8 || a.vz % 8 || a.vz > 56 ||
+        a.ldv % 8 || !a.dB || (reinterpret_cast<uintptr_t>(a.B) | reinterpret_cast<uintptr_t>(a.u)) % 16)
+      return false;
+    next = a.col0 / 256 + cdiv(a.N, 256);
+  }
+  return true;
+}
+
+long lora_dy_multi_vpart_floats(const LoraDyAdapter* ads, int n, long M) {
+  return (long)(ads[n - 1].col0 / 256 + cdiv(ads[n - 1].N, 256)) * M * 8;
+}
+
+void lora_dy_multi(const bf16_t* dy, long ldy, const LoraDyAdapter* ads, int n, float* vpart, long M, float s,
+                   hipStream_t st) {
+  if (!lora_dy_multi_ok(ads, n) || ldy % 8 || reinterpret_cast<uintptr_t>(dy) % 16) {
+    fprintf(stderr, "lora_dy_multi: unsupported adapter set\n");
+    abort();
+  }
+  if (M <= 0) return;
+  LoraDyTable tb{};
+  LoraDyFinTable ft{};
+  tb.n = n;
+  for (int i = 0; i < n; ++i) {
+    const LoraDyAdapter& a = ads[i];
+    tb.strip0[i] = ft.strip0[i] = a.col0 / 256;
+    tb.B[i] = a.B, tb.ldb[i] = a.ldb, tb.u[i] = a.u, tb.ldu[i] = a.ldu, tb.dB[i] = a.dB, tb.ldd[i] = a.ldd, tb.N[i] = a.N;
+    ft.v[i] = a.v, ft.ldv[i] = a.ldv, ft.vz[i] = a.vz;
+  }
+  const int gx = ads[n - 1].col0 / 256 + cdiv(ads[n - 1].N, 256);
+  tb.strip0[n] = ft.strip0[n] = gx;
+  long chunk = 0;
+  const long ny = dy_chunks(M, gx * 256, &chunk);
+  // strips between adapters (none for adjacent ranges) run the first adapter past its N: masked, no output
+  lora_dy_kernel<<<dim3(gx, (unsigned)ny), 256, 0, st>>>(dy, ldy, ads[0].B, ads[0].ldb, ads[0].u, ads[0].ldu, ads[0].dB,
+                                                           ads[0].ldd, vpart, M, ads[0].N, chunk, s, nullptr, 0, nullptr, 0,
+                                                           tb);
+  lora_dy_finish_multi_kernel<<<dim3((unsigned)cdiv(M * 8, 256), n), 256, 0, st>>>(vpart, M, s, ft);
+}
+
 long lora_dy_ws_floats(long M, int N) { return dy_chunks(M, N, nullptr) * 8L * cdiv(N, 256) * 256; }
 long lora_dy_grid_blocks(long M, int N) { return dy_chunks(M, N, nullptr) * cdiv(N, 256); }
 
@@ -480,7 +565,7 @@ void lora_dy(const bf16_t* dy, long ldy, const bf16_t* B, long ldb, const bf16_t
   const long np = (long)gx * 256;
   dim3 grid(gx, (unsigned)ny);
   lora_dy_kernel<<<grid, 256, 0, st>>>(dy, ldy, B, ldb, u, ldu, dB, ldd, vpart, M, N, chunk, s, det_ws, np,
-                                       gx == 1 ? v : nullptr, ldv);
+                                       gx == 1 ? v : nullptr, ldv, LoraDyTable{});
   if (gx > 1) {
     lora_dy_finish_kernel<<<cdiv(M * 8, 256), 256, 0, st>>>(vpart, gx, M, s, v, ldv, vzero);
   } else if (vzero > 0) {
