@@ -235,11 +235,8 @@ Tensor attention_packed(const Tensor& qkv, float scale, bool causal, int window,
   a.scale = scale;
   a.causal = causal;
   a.window = window;
-  // the widened output's zero columns: written by the short-path kernel itself (no launch of their own)
-  const bool pad_in_kernel = oc > HD && (oc - HD) % 8 == 0 && ::mft::attn_short_path(D, Sq, Sq, window);
-  a.o_pad = pad_in_kernel ? oc - HD : 0;
+  a.o_pad = oc - HD;  // the widened output's zero columns (written by the attention kernel where it can)
   ::mft::attn_fwd(a, S());
-  if (oc > HD && !pad_in_kernel) ::mft::zero_cols(bp(o_full), oc, (long)B * Sq, HD, oc - HD, S());
   if (needs_grad(qkv)) {
     auto n = lambda_node("FlashAttentionBackward", [qd, o, lse, scale, causal, window, B, Sq, H, D,
                                                      HD](std::vector<Tensor>& g) {
@@ -338,8 +335,8 @@ Tensor qknorm_rope_attention(const Tensor& qkv, int nq, int nkv, Param& wq, Para
   a.scale = scale;
   a.causal = 1;
   a.window = window;
+  a.o_pad = oc - HD;  // the widened output's zero columns (written by the attention kernel where it can)
   ::mft::attn_fwd(a, S());
-  if (oc > HD) ::mft::zero_cols(bp(o_full), oc, (long)B * Sq, HD, oc - HD, S());
   if (any_needs_grad({qkv, wq.leaf, wk.leaf})) {
     Param *pq = &wq, *pk = &wk;
     auto n = lambda_node("QKNormRoPEAttentionBackward", [qd, q, k, o, lse, rq, rk, wq32, wk32, cos_t, sin_t, pq, pk,
@@ -424,8 +421,7 @@ Tensor gated_act(const Tensor& gu, int act, int out_cols) {
   const int64_t oc = out_cols > I ? out_cols : I;
   MFT_CHECK(oc % 8 == 0, "gated_act: out_cols % 8");
   Tensor y = empty({M, oc}, DType::BF16, gu.device());
-  ::mft::gated_fwd(bp(g2), bp(y), M, (int)I, oc, act, S());
-  if (oc > I) ::mft::zero_cols(bp(y), oc, M, (int)I, (int)(oc - I), S());
+  ::mft::gated_fwd(bp(g2), bp(y), M, (int)I, oc, act, S(), (int)(oc - I));  // (zeroes the widened columns too)
   if (needs_grad(gu)) {
     Shape gshape = gu.shape();
     auto n = lambda_node("GatedActBackward", [g2, gshape, M, I, act](std::vector<Tensor>& g) {

@@ -38,8 +38,8 @@ struct AttnArgs {
   float scale;
   int causal, window;
   const int* kv_lens;
-  // short path (attn_short_path) only: zero o_pad columns (% 8) after the H heads of each output row (a
-  // widened output for an augmented-K consumer); other paths leave them to the caller
+  // zero o_pad columns (% 8) after the H heads of each output row (a widened output for an augmented-K
+  // consumer; rows batch-contiguous): the short and DMA kernels write them, other paths by a zero_cols pass
   int o_pad;
 };
 struct AttnBwdArgs {
@@ -175,7 +175,7 @@ void gemm_splitk_reduce(const float* ws, int ksplit, int M, int N, float* C, lon
 void gelu_fwd(const bf16_t* x, bf16_t* y, long n, hipStream_t st);
 void gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, long n, hipStream_t st);
 // gu: [M, 2I] (gate | up); y: [M, I]; act 0 = gelu_tanh (GeGLU), 1 = silu (SwiGLU)
-void gated_fwd(const bf16_t* gu, bf16_t* y, long M, int I, long ldy, int act, hipStream_t st);
+void gated_fwd(const bf16_t* gu, bf16_t* y, long M, int I, long ldy, int act, hipStream_t st, int zpad = 0);  // zpad: zero cols after I
 void gated_bwd(const bf16_t* gu, const bf16_t* dy, long ldd, bf16_t* dgu, long M, int I, int act, hipStream_t st);
 
 // ---------------------------------------------------------------- embedding (embed.hip)

@@ -6,6 +6,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdio>
+
 namespace mft {
 
 static inline int ew_grid(long n8) {
@@ -57,9 +59,14 @@ __global__ void gelu_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __re
 // 8-column groups, so no 64-bit division per element; two rows' loads are issued before either is used
 // (3 x 16 B per lane in flight in the forward, 6 in the backward).
 template <int ACT>
-__global__ void gated_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ y, long M, int I, long ldy) {
+__global__ void gated_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ y, long M, int I, long ldy,
+                                 int zpad) {
   for (long m0 = 2L * blockIdx.x; m0 < M; m0 += 2L * gridDim.x) {
     const bool two = m0 + 1 < M;
+    for (int c = I + threadIdx.x * 8; c < I + zpad; c += blockDim.x * 8) {  // the widened output's zero columns
+      *reinterpret_cast<uint4*>(y + m0 * ldy + c) = uint4{0u, 0u, 0u, 0u};
+      if (two) *reinterpret_cast<uint4*>(y + (m0 + 1) * ldy + c) = uint4{0u, 0u, 0u, 0u};
+    }
     for (int c = threadIdx.x * 8; c < I; c += blockDim.x * 8) {
       float g[2][8], u[2][8];
       load8(gu + m0 * 2 * I + c, g[0]);
@@ -119,10 +126,14 @@ void gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, long n, hipStream_t
 }
 // ldy / ldd: row strides of y / dy (> I when y is the widened augmented-K input of a LoRA
 // consumer, see bindings.cpp alloc_wide)
-void gated_fwd(const bf16_t* gu, bf16_t* y, long M, int I, long ldy, int act, hipStream_t st) {
+void gated_fwd(const bf16_t* gu, bf16_t* y, long M, int I, long ldy, int act, hipStream_t st, int zpad) {
   const int g = gated_grid(M);
-  if (act == 0) gated_fwd_kernel<0><<<g, 256, 0, st>>>(gu, y, M, I, ldy);
-  else gated_fwd_kernel<1><<<g, 256, 0, st>>>(gu, y, M, I, ldy);
+  if (zpad % 8 || I + zpad > ldy || I % 8) {
+    fprintf(stderr, "gated_fwd: zero padding %d after %d columns does not fit the row stride %ld\n", zpad, I, ldy);
+    abort();
+  }
+  if (act == 0) gated_fwd_kernel<0><<<g, 256, 0, st>>>(gu, y, M, I, ldy, zpad);
+  else gated_fwd_kernel<1><<<g, 256, 0, st>>>(gu, y, M, I, ldy, zpad);
 }
 void gated_bwd(const bf16_t* gu, const bf16_t* dy, long ldd, bf16_t* dgu, long M, int I, int act, hipStream_t st) {
   const int g = gated_grid(M);

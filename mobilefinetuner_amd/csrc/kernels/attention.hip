@@ -1087,7 +1087,7 @@ template <int D, int NW, int RPW = 16, bool SWZ = true, int RGF = 4, bool GQA = 
 __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
     float* __restrict__ lse, AttnStrides qs, AttnStrides ks, AttnStrides vs, AttnStrides os, int H, int Hkv, int Sq,
-    int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens) {
+    int Sk, float scale, int causal, int window, const int* __restrict__ kv_lens, int o_pad) {
   constexpr int R = RPW / 16;  // 16-query halves per wave
   constexpr bool kPair = D == 256;  // row-pair images (one address base per lane), else XOR swizzle
   // LDO: output staging pitch D + 8 (kOutPad): the four 16-lane groups of the 2-byte staging writes land
@@ -1104,6 +1104,11 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_dma_kernel(
   const int bq = RPW * wph;                    // query rows per workgroup
   const int h = GQA ? hx * (H / Hkv) + w / wph : hx, hk = GQA ? hx : h / (H / Hkv);
   const int q0 = tx * bq;
+  if (hx == 0 && o_pad > 0) {  // the widened output's zero columns of this block's rows (after the H heads)
+    const int per = o_pad / 8, nr = min(bq, Sq - q0);
+    for (int c = threadIdx.x; c < nr * per; c += 64 * NW)
+      *reinterpret_cast<u16x8_t*>(o + b * os.sb + (long)(q0 + c / per) * os.ss + (long)H * D + (c % per) * 8) = u16x8_t{};
+  }
   const int kv_len = kv_lens ? min(kv_lens[b], Sk) : Sk;
   const int coff = Sk - Sq;
   const float c2 = scale * kLog2e;
@@ -1615,7 +1620,7 @@ static void fwd_dma_launch_rpw(const AttnArgs& a, hipStream_t stream) {
   const dim3 grid = GQA ? dim3(cdiv(a.Sq, RPW * (NW / G)), a.Hkv, a.B) : dim3(cdiv(a.Sq, RPW * NW), a.H, a.B);
   attn_fwd_dma_kernel<D, NW, RPW, SWZ, RGF, GQA><<<grid, 64 * NW, shm, stream>>>(
       a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st), mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale,
-      a.causal, a.window, a.kv_lens);
+      a.causal, a.window, a.kv_lens, a.o_pad);
 }
 
 // MFT_ATTN_RPW=16|32: query rows per wave of the DMA forward (A/B).  32 rows need the 512-register
@@ -1731,7 +1736,8 @@ static void dq_split_launch(const AttnBwdArgs& a, hipStream_t stream) {
 
 
 template <int D>
-static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
+// returns whether the launched kernel wrote the o_pad zero columns itself (short and DMA paths)
+static bool fwd_launch(const AttnArgs& a, hipStream_t stream) {
   if constexpr (D == 64) {
     if (attn_short_path(D, a.Sq, a.Sk, a.window)) {
       const size_t shm = sizeof(bf16_t) * (2 * kShortS * D + 8 * 16 * (D + 8));
@@ -1744,7 +1750,7 @@ static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
       attn_fwd_short2_kernel<D><<<dim3(a.H, a.B), 512, shm, stream>>>(a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st),
                                                                        mk(a.v_st), mk(a.o_st), a.H, a.Hkv, a.Sq, a.scale,
                                                                        a.causal, a.kv_lens, a.o_pad);
-      return;
+      return true;
     }
   }
   if (attn_bwd_path(D, a.Sq, a.Sk, a.window) == 2) {
@@ -1752,12 +1758,12 @@ static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
       static const int dma = env_int("MFT_ATTN_DMA", 1);
       if (dma) {
         fwd_dma_launch<D>(a, stream);
-        return;
+        return true;
       }
     }
     if (split_nw("MFT_ATTN_NW_FWD", 8) == 8) fwd_split_launch<D, 8>(a, stream);
     else fwd_split_launch<D, 4>(a, stream);
-    return;
+    return false;
   }
   constexpr int BQ = 64, BK = 64, LDP = BK + 8;
   const size_t shm = sizeof(bf16_t) * (2 * BK * D + 4 * 16 * LDP);
@@ -1765,6 +1771,7 @@ static void fwd_launch(const AttnArgs& a, hipStream_t stream) {
   attn_fwd_kernel<D><<<grid, 256, shm, stream>>>(a.q, a.k, a.v, a.o, a.lse, mk(a.q_st), mk(a.k_st), mk(a.v_st),
                                                  mk(a.o_st), a.H, a.Hkv, a.Sq, a.Sk, a.scale, a.causal, a.window,
                                                  a.kv_lens);
+  return false;
 }
 
 template <int D>
@@ -1853,12 +1860,18 @@ void attn_fwd(const AttnArgs& a, hipStream_t s) {
     MFT_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     init = true;
   }
+  if (a.o_pad % 8 || (a.o_pad > 0 && a.o_st[0] != (long)a.Sq * a.o_st[1])) {
+    fprintf(stderr, "attn_fwd: o_pad %d needs a multiple of 8 and batch-contiguous output rows\n", a.o_pad);
+    abort();
+  }
+  bool padded = false;
   switch (a.D) {
-    case 64: fwd_launch<64>(a, s); break;
-    case 128: fwd_launch<128>(a, s); break;
-    case 256: fwd_launch<256>(a, s); break;
+    case 64: padded = fwd_launch<64>(a, s); break;
+    case 128: padded = fwd_launch<128>(a, s); break;
+    case 256: padded = fwd_launch<256>(a, s); break;
     default: fprintf(stderr, "attn_fwd: unsupported head dim %d\n", a.D); abort();
   }
+  if (a.o_pad > 0 && !padded) zero_cols(a.o, a.o_st[1], (long)a.B * a.Sq, a.H * a.D, a.o_pad, s);
 }
 
 void attn_bwd(const AttnBwdArgs& a, hipStream_t s) {
