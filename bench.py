@@ -202,10 +202,11 @@ def run_native(a, cfgd) -> int:
             "micro_batch_per_gpu": rec["batch"],
             "seq_len": rec["seq"],
             "parallelism": f"dp{rec['world']}",
-            "engine": "native libmft (C++ autograd tape, hipGraph-captured step)",
+            "engine": "native libmft (C++ autograd tape, " + ("hipGraph-captured step)" if rec.get("hipgraph")
+                                                               else "eager step, no hipGraph)"),
             "ranks": rec["world"],
             "backend": cbe if (rec["world"] > 1 or zero) else "none",
-            "hipgraph": not a.no_graph,
+            "hipgraph": bool(rec.get("hipgraph", False)),  # what the engine ran, not what was asked
             "final_loss": round(rec["final_loss"], 4),
             "model_tflops_per_gpu": round(tflops, 1),
             "mfu_bf16_dense": round(tflops / MI355X_BF16_DENSE_TFLOPS, 4),

@@ -220,7 +220,6 @@ inline std::unique_ptr<eng::Communicator> comm_from(const DistConfig& d) {
   auto c = eng::Communicator::from_env((fc && fc[0] == '1') || d.zero_stage > 0);
   // ranks must not pick kernels by timing on their own: hipBLASLt takes its heuristic's first algorithm
   // (the gemm8 / hipBLASLt routing itself is a fixed table)
-  if (c && c->world() > 1) eng::set_lt_autotune(false);
   return c;
 }
 
@@ -286,9 +285,9 @@ inline void bench_report(TrainerT& trainer, const FlatT& flat, const Args& a, in
   const eng::AllocStats ms = eng::CachingAllocator::get(dev).stats();  // HBM high-water mark of this rank
   std::printf("MFT_BENCH {\"seconds\": %.9f, \"steps\": %d, \"warmup\": %d, \"world\": %d, \"batch\": %d, "
               "\"seq\": %d, \"accum\": %d, \"final_loss\": %.6f, \"model\": \"%s\", \"n_params\": %zu, "
-              "\"n_trainable\": %lld, \"peak_allocated_gb\": %.3f, \"peak_reserved_gb\": %.3f}\n",
+              "\"n_trainable\": %lld, \"peak_allocated_gb\": %.3f, \"peak_reserved_gb\": %.3f, \"hipgraph\": %s}\n",
               secs, steps, warmup, world, batch, seq, accum, loss, model.c_str(), n_params, n_train,
-              ms.peak_allocated / 1e9, ms.peak_reserved / 1e9);
+              ms.peak_allocated / 1e9, ms.peak_reserved / 1e9, trainer.graph_replayed() ? "true" : "false");
   std::fflush(stdout);
 }
 

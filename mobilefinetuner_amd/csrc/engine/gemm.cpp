@@ -121,7 +121,6 @@ bool short_tokens(long M, long N, long K, int epi) {
 
 bool gemm8_all() { return !gemm4_on(); }
 bool deterministic() { return g_det; }
-void set_lt_autotune(bool) {}  // (no library GEMM left to tune; kept for the apps' comm setup)
 void set_deterministic(bool on) { g_det = on; }
 
 void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c, const Gemm8Extra& ex) {
@@ -296,7 +295,28 @@ void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
     if (ws) al.release(ws);
     return;
   }
+  // a token count that is not a multiple of 64 (odd batch x seq): zero-padded copies of both token-major
+  // operands to the next multiple (the padding rows add 0 to every sum) -- two copies of the operands
+  // instead of the SIMT kernel, orders of magnitude slower on a full fine-tune
+  if (M % 64 && N % 8 == 0 && K % 8 == 0 && dy2.dtype() == DType::BF16 && x2.dtype() == DType::BF16 &&
+      ::mft::gemm8_supported((int)N, (int)K, (int)((M + 63) / 64 * 64), true, true)) {
+    NoGradGuard ng;
+    const long Mp = (M + 63) / 64 * 64;
+    Tensor dyp = zeros({Mp, N}, DType::BF16, dy2.device()), xp = zeros({Mp, K}, DType::BF16, x2.device());
+    dyp.slice(0, 0, M).copy_(dy2);
+    xp.slice(0, 0, M).copy_(x2);
+    map_line("wgrad (tokens padded to 64)", N, K, M, "gemm8");
+    gemm_wgrad(buf, dyp, xp, alpha);
+    return;
+  }
   // buf [N, K] += alpha dy^T x
+  if (dy2.dtype() == DType::BF16 && x2.dtype() == DType::BF16) {
+    static bool warned = false;
+    if (!warned) {
+      warned = true;
+      std::fprintf(stderr, "[gemm] weight gradient M=%ld N=%ld K=%ld on the SIMT fallback (unaligned operands)\n", M, N, K);
+    }
+  }
   Tensor b2 = buf.view({N, K});
   simt(dy2, true, x2, false, b2, alpha, Tensor(), b2, 1.f, "wgrad");
 }

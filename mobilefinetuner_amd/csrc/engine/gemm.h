@@ -40,7 +40,6 @@ bool gemm8_all();
 bool nt_gemm4();
 bool deterministic();
 void set_deterministic(bool on);
-void set_lt_autotune(bool on);  // no-op (no library GEMM to tune); kept for the apps' comm setup
 bool gemm4_on();                // MFT_GEMM4=0 -> gemm8 for every product (A/B)
 bool short_tokens(long M, long N, long K, int epi);  // gemm_s takes this product
 

@@ -544,6 +544,7 @@ std::pair<Tensor, Tensor> Gemma3::nll(const Tensor& ids, const Tensor& labels) {
   const bool t = training;
   training = false;
   Tensor h = hidden(ids);
+  lora_prep_step_end();  // no backward follows
   training = t;
   return lm_head_nll(h, embed_, labels, cfg_.vocab_size, ce_chunk);
 }

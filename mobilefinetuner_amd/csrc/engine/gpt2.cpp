@@ -542,6 +542,7 @@ std::pair<Tensor, Tensor> GPT2::nll(const Tensor& ids, const Tensor& labels) {
   const bool t = training;
   training = false;
   Tensor h = hidden(ids);
+  lora_prep_step_end();  // no backward follows
   training = t;
   return lm_head_nll(h, wte_, labels, cfg_.vocab_size, ce_chunk);
 }

@@ -17,7 +17,8 @@ namespace eng {
 
 class LanguageModel {
  public:
-  virtual ~LanguageModel() = default;
+  // (the process-wide LoRA weight-prep registry holds this model's tensors: released with it)
+  virtual ~LanguageModel() { lora_prep_reset(); }
   // mean token NLL of one micro-batch (ids / labels [B, S], labels already shifted, -100 ignored);
   // a trainable tied embedding's gradient is produced inside the CE scaled by w_grad_scale
   virtual Tensor loss(const Tensor& ids, const Tensor& labels, float w_grad_scale = 1.f) = 0;

@@ -545,6 +545,11 @@ struct LoraPrep {
   int ndev = 0;
   bool dirty = false;   // items changed since the upload
   bool active = false;  // the batch ran at the start of this forward
+  // A captured training graph keeps the device list (and every dst / src it names) it was recorded
+  // with: a list replaced later -- e.g. an eager eval forward that registers new entries -- is retired
+  // here, never freed, so a later replay of that graph still reads live memory.
+  std::vector<::mft::LoraPrepEntry*> retired_dev;
+  std::vector<Item> retired_items;
 };
 LoraPrep& lprep() {
   static LoraPrep p;
@@ -574,11 +579,28 @@ void prep_copy(const Tensor& dst, const Tensor& src, float scale) {
     P.items.push_back({dst, src, e, false});
     P.dirty = true;
   } else if (!same) {  // (the batch may still write the old entry first: this copy, later in the stream, wins)
+    if (P.items[it->second].uploaded) P.retired_items.push_back(P.items[it->second]);  // a graph may name it
     P.items[it->second] = {dst, src, e, false};
     P.dirty = true;
   }
 }
 }  // namespace
+
+void lora_prep_step_end() { lprep().active = false; }
+
+void lora_prep_reset() {
+  // the model that registered the entries is going away: forget them (its tensors are released with
+  // the items) but keep the uploaded list's memory -- a graph of that model may not be destroyed yet
+  auto& P = lprep();
+  if (P.dev) P.retired_dev.push_back(P.dev);
+  P.dev = nullptr;
+  P.ndev = 0;
+  P.items.clear();
+  P.by_dst.clear();
+  P.retired_items.clear();
+  P.dirty = false;
+  P.active = false;
+}
 
 void lora_prep_step_begin() {
   auto& P = lprep();
@@ -587,11 +609,13 @@ void lora_prep_step_begin() {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIP_OK(hipStreamIsCapturing(S(), &cap));
   // (re)upload -- only outside a capture; inside one the uploaded list still runs and the layers whose
-  // entries changed since make their own copies
+  // entries changed since make their own copies.  The previous list is retired, not freed: a captured
+  // graph's lora_prep node still reads it on every replay.
   if (P.dirty && cap == hipStreamCaptureStatusNone) {
     std::vector<::mft::LoraPrepEntry> es;
     for (auto& it : P.items) es.push_back(it.e);
-    if (P.dev) HIP_OK(hipFree(P.dev));
+    if (P.dev) P.retired_dev.push_back(P.dev);
+    P.dev = nullptr;
     HIP_OK(hipMalloc(&P.dev, es.size() * sizeof(::mft::LoraPrepEntry)));
     HIP_OK(hipMemcpy(P.dev, es.data(), es.size() * sizeof(::mft::LoraPrepEntry), hipMemcpyHostToDevice));
     P.ndev = (int)es.size();

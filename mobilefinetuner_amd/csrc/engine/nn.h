@@ -78,6 +78,10 @@ struct LoraAdapter {
 // graph capture for the first time) uploads the list and from then on launches it, and each layer skips
 // the copy the batch already made (an entry whose tensors changed is simply redone by its layer).
 void lora_prep_step_begin();
+// the forward is over: a later LoRA layer call runs its own copies (no stale batch assumed)
+void lora_prep_step_end();
+// forget every registered entry (a model is destroyed); uploaded lists stay allocated for live graphs
+void lora_prep_reset();
 // width of the augmented input [x | u_1..u_n | 0]: in + sum(r), rounded to 64
 int lora_aug_cols(int in_features, const std::vector<LoraAdapter>& ads);
 // xa [M, Ka] holds x in its first K columns (zero tail); waug [N, Ka] = [W | s B^T.. | 0] (owned by

@@ -103,6 +103,7 @@ void Trainer::fwd_bwd() {
     Tensor loss = model_.loss(ids_[i], labels_[i], gs);
     Tensor scaled = mul_scalar(loss, gs);
     backward({scaled});
+    lora_prep_step_end();  // the LoRA weight-prep batch covered this forward + backward only
     add_(loss_acc_, loss.detach(), inv);
   }
 }
@@ -438,7 +439,11 @@ void Trainer::save_state(const std::string& dir) {
       m3 = opt_.vmax.to(Device::cpu());
       outs.push_back({"vmax", "F32", {m3.numel()}, m3.data_ptr(), (size_t)m3.numel() * sizeof(float)});
     }
-    safetensors_save(tmp + fn, outs, {{"format", opt_.sharded() ? "mft-zero-partition" : "mft-flat"}}, false, true);
+    // opt_state_version 2: 'vmax' is the running max of the bias-corrected v / bc2 (reference
+    // optim/adam.cpp:75-80); version 1 files (no key) held the running max of the raw v
+    safetensors_save(tmp + fn, outs,
+                     {{"format", opt_.sharded() ? "mft-zero-partition" : "mft-flat"}, {"opt_state_version", "2"}}, false,
+                     true);
   }
   std::ofstream f(tmp + "/trainer_state.rank" + std::to_string(r) + ".json");
   f.precision(17);
@@ -485,17 +490,23 @@ bool Trainer::load_state(const std::string& dir0) {
   opt_.load_state(host_view(to, "m", opt_.m.numel()), host_view(to, "v", opt_.v.numel()), st["opt_step"].as_int());
   if (dp_) dp_->optimizer_state_loaded();
   if (opt_.vmax.defined()) {
-    if (to.has("vmax")) {
+    const auto mv = to.metadata().find("opt_state_version");
+    const bool vmax_v2 = mv != to.metadata().end() && std::atoi(mv->second.c_str()) >= 2;
+    if (to.has("vmax") && vmax_v2) {
       opt_.load_vmax(host_view(to, "vmax", opt_.vmax.numel()));
-    } else {  // a checkpoint written without AMSGrad: start the running max at the loaded v / bc2 (its
-      // first step then matches plain Adam), never at zero beside restored moments
+    } else {  // a checkpoint written without AMSGrad, or by a build whose 'vmax' was the max of the raw v
+      // (ADVICE r5): start the running max at the loaded v / bc2 (the first step then matches plain
+      // Adam), never at zero beside restored moments
+      if (to.has("vmax"))
+        std::fprintf(stderr, "[warn] load_state: 'vmax' of an older optimizer-state version (raw-v max); rebuilt from v / bc2\n");
+      else
+        std::fprintf(stderr, "[warn] load_state: --amsgrad but the checkpoint has no 'vmax'; initialised from v / bc2\n");
       const int64_t steps = st["opt_step"].as_int(), n = opt_.vmax.numel();
       const double bc2 = 1.0 - std::pow((double)opt_.config().beta2, (double)std::max<int64_t>(steps, 1));
       Tensor vh = host_view(to, "v", n);
       std::vector<float> vm((size_t)n);
       const float* src = static_cast<const float*>(vh.data_ptr());
       for (int64_t i = 0; i < n; ++i) vm[(size_t)i] = (float)(src[i] / bc2);
-      std::fprintf(stderr, "[warn] load_state: --amsgrad but the checkpoint has no 'vmax'; initialised from v / bc2\n");
       opt_.load_vmax(from_blob(vm.data(), {n}, DType::F32, Device::cpu()));
       synchronize();
     }

@@ -79,6 +79,8 @@ class Trainer {
   // synchronize and, with a communicator, a cross-rank barrier.  Returns the MAX over ranks of the
   // timed wall seconds; *final_loss = the last step's (rank-mean) loss.
   double bench(int warmup, int steps, float* final_loss);
+  // the step actually replays a captured hipGraph (false: eager -- --no_graph or an uncapturable reducer)
+  bool graph_replayed() const { return exec_ != nullptr; }
   std::pair<double, double> evaluate(int max_batches, int batch_size);  // (nll, ppl)
   // Full training state (same directory layout as the Python CLIs' --state_dir):
   // trainable.safetensors (fp32 master) + optimizer.safetensors (AdamW m, v) from rank 0 -- data

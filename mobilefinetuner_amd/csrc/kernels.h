@@ -126,6 +126,9 @@ struct GemmArgs {
   int K2;
   // gemm4 epilogue operand (aux) loads: 0 = non-temporal (default), 1 = default cache policy (A/B)
   int aux_pol;
+  // gemm_s split-K hand-off: 1 = agent-scope release / acquire fences around the arrival counter
+  // (MFT_STRICT_HANDOFF=1); 0 = the sc1-store / sc1-load form alone (see gemm_s.hip)
+  int handoff_fence;
 };
 // 256x256 8-phase pipelined GEMM (gemm8.hip); same epilogues.  a_t: A stored [K, M]; b_t: B stored
 // [K, N] (NN data-grad); both: TN weight-grad (use GEMM_EPI_F32ACC with gemm8_pick_ksplit / ws)

@@ -279,3 +279,27 @@ def test_native_gemma_embedding_dump_and_token_preview(tmp_path):
     # the sqrt(H) normaliser rounded differently); any other row is orders of magnitude further away
     d = torch.cdist(rows, table).min(dim=1).values
     assert d.max().item() < 5e-3 * table.norm(dim=1).max().item(), d.max()
+
+
+def test_native_gemma_dropout_eval_between_graph_replays():
+    """LoRA dropout on + evaluation every 2 steps: the eager eval forward (no dropout) registers
+    weight-prep entries the dropout training forward never made, so the prep list is re-uploaded between
+    replays of the captured step.  The replayed graph keeps its own (retired, not freed) list: the
+    graph-captured run reproduces the eager run's losses step for step, evals included."""
+    common = ["--random_init", "--model", "gemma3-tiny", "--synthetic_data", "--synthetic_tokens", "50000",
+              "--max_steps", "8", "--batch", "4", "--seq_len", "64", "--lr", "2e-3", "--warmup_ratio", "0",
+              "--lora_dropout", "0.1", "--log_interval", "1", "--deterministic", "--eval_steps", "2",
+              "--eval_batches", "2"]
+
+    def run(extra):
+        r = subprocess.run([_bin("train_lora_gemma"), *common, *extra], capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        return loss_list(r.stdout, True), r.stdout
+
+    eager, out_e = run(["--no_graph"])
+    graph, out_g = run([])
+    assert len(eager) == 8 and all(math.isfinite(x) for x in eager), eager
+    assert graph == pytest.approx(eager, abs=2e-3), (graph, eager)
+    ev_e = [l for l in out_e.splitlines() if "eval" in l.lower() and "ppl" in l.lower()]
+    ev_g = [l for l in out_g.splitlines() if "eval" in l.lower() and "ppl" in l.lower()]
+    assert len(ev_g) >= 3 and len(ev_g) == len(ev_e), (ev_g, ev_e)
