@@ -29,7 +29,9 @@
 #include "engine/comm.h"
 #include "engine/dist.h"
 #include "engine/gemm.h"
+#include "engine/lm.h"
 #include "engine/optim.h"
+#include "engine/trainer.h"
 #include "engine/weight_stream.h"
 #include "engine/zero3.h"
 #include "runtime/dataset.h"
@@ -74,10 +76,33 @@ struct Args {
   bool b(const std::string& k) const { return flags.count(k) || (kv.count(k) && kv.at(k) != "0" && kv.at(k) != "false"); }
 };
 
+// The common flag block every native CLI accepts on top of its reference flags:
+//   --dtype bf16|fp32        compute precision (fp32: the reference's precision, the composite path of
+//                            every op on fp32 tensors -- eager, for parity checks; bf16: the fused kernels)
+//   --attn_impl flash|naive  flash-attention kernels, or the materialized masked softmax (reference
+//                            graph/gpt2_model.cpp:679-711 standard path)
+//   --profile_steps a:b      steps a..b inside one roctx range, profiler resumed only there
+//                            (rocprofv3 --selected-regions), per-step device times printed
+//   --compat_grad_overwrite  reference .grad overwrite across micro-batches
+//   --compat_reference       every reference-quirk switch: coupled L2 Adam (Q8), .grad overwrite (Q1),
+//                            interleaved RoPE pairs (Q9, Gemma)
+inline const std::set<std::string>& common_bool_flags() {
+  static const std::set<std::string> s = {"compat_grad_overwrite", "compat_reference"};
+  return s;
+}
+inline const std::set<std::string>& common_valued_flags() {
+  static const std::set<std::string> s = {"dtype", "attn_impl", "profile_steps"};
+  return s;
+}
+
 // kBool flags may appear bare; kValued flags take a value; anything else is an error (lenient: it
-// is recorded in Args::unknown and skipped with its value, like the reference Gemma CLI parser)
-inline Args parse_args(int argc, char** argv, const std::set<std::string>& kBool, const std::set<std::string>& kValued,
+// is recorded in Args::unknown and skipped with its value, like the reference Gemma CLI parser).  The
+// common flag block above is accepted by every program.
+inline Args parse_args(int argc, char** argv, const std::set<std::string>& kBool0, const std::set<std::string>& kValued0,
                        bool lenient = false) {
+  std::set<std::string> kBool = kBool0, kValued = kValued0;
+  kBool.insert(common_bool_flags().begin(), common_bool_flags().end());
+  kValued.insert(common_valued_flags().begin(), common_valued_flags().end());
   Args a;
   for (int i = 1; i < argc; ++i) {
     std::string s = argv[i];
@@ -117,6 +142,32 @@ inline Args parse_args(int argc, char** argv, const std::set<std::string>& kBool
     a.kv[key] = val;
   }
   return a;
+}
+
+// --dtype: before any model is built (weights are allocated in the compute dtype)
+inline void apply_dtype_flag(const Args& a) {
+  const std::string d = a.get("dtype", "bf16");
+  if (d == "fp32" || d == "float32" || d == "f32") {
+    eng::set_compute_dtype(eng::DType::F32);
+    std::printf("  --dtype fp32: reference-precision composite path (fp32 weights / activations, eager)\n");
+  } else if (d != "bf16" && d != "bfloat16") {
+    throw std::runtime_error("--dtype " + d + ": bf16 or fp32");
+  }
+}
+inline void apply_model_flags(const Args& a, eng::LanguageModel& m) {
+  const std::string ai = a.get("attn_impl", "flash");
+  if (ai != "flash" && ai != "naive") throw std::runtime_error("--attn_impl " + ai + ": flash or naive");
+  m.attn_naive = ai == "naive";
+}
+inline void apply_train_flags(const Args& a, eng::TrainConfig& tc) {
+  const std::string ps = a.get("profile_steps");
+  if (!ps.empty()) {  // a:b (1-indexed, inclusive); "a" alone = that one step
+    const size_t c = ps.find(':');
+    tc.profile_from = std::stoll(ps.substr(0, c));
+    tc.profile_to = c == std::string::npos ? tc.profile_from : std::stoll(ps.substr(c + 1));
+    if (tc.profile_from < 1 || tc.profile_to < tc.profile_from) throw std::runtime_error("--profile_steps a:b with 1 <= a <= b");
+  }
+  tc.compat_grad_overwrite = a.b("compat_grad_overwrite") || a.b("compat_reference");
 }
 
 inline bool file_exists(const std::string& p) {

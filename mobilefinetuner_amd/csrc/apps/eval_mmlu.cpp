@@ -163,6 +163,7 @@ int run(int argc, char** argv) {
   hipStream_t stream;
   HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   set_current_stream(stream);
+  mft::apps::apply_dtype_flag(a);
   const std::string mtype = a.get("model_type", "gpt2"), pdir = a.get("pretrained_dir");
   const std::string tdir = a.get("tokenizer_dir", pdir);
   const bool random_init = a.b("random_init") || pdir.empty();
@@ -186,6 +187,7 @@ int run(int argc, char** argv) {
                                             ? std::shared_ptr<ByteLevelBPE>(ByteLevelBPE::from_files(tdir + "/vocab.json", tdir + "/merges.txt"))
                                             : std::shared_ptr<ByteLevelBPE>(ByteLevelBPE::from_tokenizer_json(tdir + "/tokenizer.json"));
     enc = [tok](const std::string& s, bool) { return tok->encode(s); };
+    mft::apps::apply_model_flags(a, *m);
     model = std::move(m);
   } else if (mtype == "gemma") {
     Gemma3Config cfg = cfg_file ? Gemma3Config::from_json(pdir + "/config.json")
@@ -199,6 +201,7 @@ int run(int argc, char** argv) {
     }
     std::shared_ptr<SentencePieceBPE> tok = SentencePieceBPE::from_tokenizer_json(tdir + "/tokenizer.json");
     enc = [tok](const std::string& s, bool bos) { return tok->encode(s, bos); };
+    mft::apps::apply_model_flags(a, *m);
     model = std::move(m);
   } else {
     throw std::runtime_error("--model_type must be gpt2 or gemma");

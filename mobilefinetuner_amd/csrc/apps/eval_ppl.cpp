@@ -60,6 +60,7 @@ int run(int argc, char** argv) {
   HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   set_current_stream(stream);
 
+  mft::apps::apply_dtype_flag(a);
   const std::string pdir = a.get("pretrained_dir");
   const bool random_init = a.b("random_init") || pdir.empty();
   const std::string mtype = a.get("model_type", "gpt2");
@@ -79,6 +80,7 @@ int run(int argc, char** argv) {
       if (merge) m->merge_lora(1.f);  // W += s A^T B^T: the adapter costs nothing
     }
     vocab = cfg.vocab_size, max_pos = cfg.n_positions;
+    mft::apps::apply_model_flags(a, *m);
     model = std::move(m);
   } else {
     Gemma3Config cfg = cfg_file ? Gemma3Config::from_json(pdir + "/config.json")
@@ -91,6 +93,7 @@ int run(int argc, char** argv) {
       if (merge) m->merge_lora(1.f);
     }
     vocab = cfg.vocab_size, max_pos = cfg.max_positions, eos = cfg.eos_id;
+    mft::apps::apply_model_flags(a, *m);
     model = std::move(m);
   }
   model->training = false;

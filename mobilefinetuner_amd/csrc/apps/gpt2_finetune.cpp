@@ -10,6 +10,8 @@
 //   --pretokenized_path F [--pretokenized_meta M]   int32 token stream + meta.json
 //   --lora_targets AttnQKV,AttnProj[,MlpFcIn,MlpFcOut] --split_qkv
 //   --no_graph --compat_l2_adam --amsgrad --metrics_out F --deterministic
+//   + the common block of apps/app_common.h: --dtype bf16|fp32 --attn_impl flash|naive --profile_steps a:b
+//     --compat_grad_overwrite --compat_reference
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -108,7 +110,8 @@ void usage() {
       "          --pretokenized_meta F --lora_targets T --split_qkv --no_graph --compat_l2_adam --amsgrad --metrics_out F\n"
       "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"
       "          --inject_fault STEP:RANK (failure test: that rank throws before that step)\n"
-      "          --deterministic\n",
+      "          --deterministic\n"
+      "  common: --dtype bf16|fp32 --attn_impl flash|naive --profile_steps A:B --compat_grad_overwrite --compat_reference\n",
       kProg);
 }
 
@@ -140,6 +143,7 @@ int run(int argc, char** argv) {
   set_current_stream(stream);
   mft::apps::install_crash_report();  // again: the HIP runtime's initialisation may replace handlers
 
+  mft::apps::apply_dtype_flag(a);
   const int seq_len = a.i("seq_len", 128);
   const uint64_t seed = (uint64_t)a.l("seed", 42);
   std::printf("\n========== %s (MI355X native engine) ==========\n", kProg);
@@ -155,6 +159,7 @@ int run(int argc, char** argv) {
   else cfg = GPT2Config::preset(a.get("model", "gpt2"));
   auto model = std::make_unique<GPT2>(cfg);
   model->grad_checkpoint = a.b("activation_checkpointing");  // recompute blocks in the backward
+  mft::apps::apply_model_flags(a, *model);
   if (random_init) {
     model->init_random(1234);
     std::printf("  random-init %s (%d layers, C=%d, H=%d)\n", a.get("model", "gpt2").c_str(), cfg.n_layer,
@@ -243,7 +248,7 @@ int run(int argc, char** argv) {
   oc.lr = a.f("lr", full ? 5e-5f : 1e-4f);
   oc.weight_decay = a.f("weight_decay", full ? 0.01f : 0.f);
   oc.max_grad_norm = a.f("clip_grad_norm", 1.f);
-  oc.l2_coupled = a.b("compat_l2_adam");
+  oc.l2_coupled = a.b("compat_l2_adam") || a.b("compat_reference");
   oc.amsgrad = a.b("amsgrad");
   AdamW opt(flat, oc);
   ds.make_dp(comm.get(), opt, dcfg);
@@ -265,6 +270,7 @@ int run(int argc, char** argv) {
   tc.eval_out = a.get("eval_out");
   tc.metrics_out = a.get("metrics_out");
   tc.state_dir = a.get("state_dir");
+  mft::apps::apply_train_flags(a, tc);
   if (!a.get("inject_fault").empty()) {  // step:rank
     const std::string f = a.get("inject_fault");
     const size_t c = f.find(':');
@@ -295,7 +301,7 @@ int run(int argc, char** argv) {
               tc.batch, tc.accum);
   std::printf("\n[4/6] Optimizer: fused AdamW (%s)\n", oc.l2_coupled ? "coupled L2, reference" : "decoupled");
   std::printf("\n[5/6] Starting training (%s)...\n========================================\n",
-              tc.use_graph ? "hipGraph-captured step" : "eager");
+              trainer.uses_graph() ? "hipGraph-captured step" : "eager");
   const auto t0 = std::chrono::steady_clock::now();
   trainer.train(save);
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -101,7 +101,8 @@ void usage() {
       "          --zero_stage 0|1|2 --offload host|none --bucket_mb N --bf16_grads --no_overlap\n"
       "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"
       "          --inject_fault STEP:RANK (failure test: that rank throws before that step)\n"
-      "          --bench_steps K [--bench_warmup W] (bench.py: time K steps after W, print one MFT_BENCH line)\n",
+      "          --bench_steps K [--bench_warmup W] (bench.py: time K steps after W, print one MFT_BENCH line)\n"
+      "  common: --dtype bf16|fp32 --attn_impl flash|naive --profile_steps A:B --compat_grad_overwrite --compat_reference\n",
       kProg);
 }
 
@@ -356,6 +357,7 @@ int run(int argc, char** argv) {
   if (comm)
     std::printf("  data parallel: rank %d of %d (%s, device %d)\n", comm->rank(), comm->world(), comm->backend(),
                 comm->device());
+  mft::apps::apply_dtype_flag(a);
   const std::string mdir = a.get("model_dir");
   const bool random_init = a.b("random_init") || mdir.empty();
   Gemma3Config cfg = (!mdir.empty() && file_exists(mdir + "/config.json")) ? Gemma3Config::from_json(mdir + "/config.json")
@@ -363,7 +365,8 @@ int run(int argc, char** argv) {
   std::printf("  Gemma-3 config: layers=%d hidden=%d heads=%d/%d head_dim=%d vocab=%d\n", cfg.n_layer, cfg.hidden,
               cfg.n_head, cfg.n_kv, cfg.head_dim, cfg.vocab_size);
   auto model = std::make_unique<Gemma3>(cfg);
-  model->interleaved_rope = a.b("interleaved_rope");
+  model->interleaved_rope = a.b("interleaved_rope") || a.b("compat_reference");
+  mft::apps::apply_model_flags(a, *model);
   model->grad_checkpoint = a.b("activation_checkpointing");  // recompute blocks in the backward
   model->loss_sum = red != "mean";
   if (random_init) {
@@ -428,7 +431,7 @@ int run(int argc, char** argv) {
   oc.lr = std::stof(pick(a, {"lr", "learning_rate"}, "2e-4"));
   oc.weight_decay = a.f("weight_decay", 0.f);
   oc.max_grad_norm = a.f("max_grad_norm", 1.f);
-  oc.l2_coupled = a.b("compat_l2_adam");
+  oc.l2_coupled = a.b("compat_l2_adam") || a.b("compat_reference");
   oc.amsgrad = a.b("amsgrad");
   if (!a.get("dump_grads").empty()) {  // parity tests: one fwd+bwd, gradients in the adapter layout
     MFT_CHECK(!comm, "--dump_grads runs on one process");
@@ -459,6 +462,7 @@ int run(int argc, char** argv) {
   tc.use_graph = !a.b("no_graph");
   tc.metrics_out = a.get("metrics_out");
   tc.state_dir = a.get("state_dir");
+  mft::apps::apply_train_flags(a, tc);
   if (!a.get("inject_fault").empty()) {  // step:rank
     const std::string f = a.get("inject_fault");
     const size_t c = f.find(':');
@@ -544,7 +548,7 @@ int run(int argc, char** argv) {
     std::printf("\n[Checkpoint] Saved %s\n\n", p.c_str());
   };
   std::printf("[Plan] steps/epoch=%lld total=%lld (micro=%d x accum=%d, %s)\n", (long long)trainer.steps_per_epoch(),
-              (long long)trainer.total_steps(), tc.batch, tc.accum, tc.use_graph ? "hipGraph-captured step" : "eager");
+              (long long)trainer.total_steps(), tc.batch, tc.accum, trainer.uses_graph() ? "hipGraph-captured step" : "eager");
   const auto t0 = std::chrono::steady_clock::now();
   trainer.train(save);
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -160,26 +160,28 @@ void Gemma3::alloc() {
   const int nqkv = (cfg_.n_head + 2 * cfg_.n_kv) * D;
   MFT_CHECK((int)cfg_.sliding.size() == cfg_.n_layer, "gemma3: layer types do not match num_hidden_layers");
   NoGradGuard ng;
-  embed_ = frozen(zeros({cfg_.vocab_padded(), H}, DType::BF16));
+  const DType wd = compute_dtype();  // bf16, or fp32 for --dtype fp32 (norm weights are fp32 either way)
+  embed_ = frozen(zeros({cfg_.vocab_padded(), H}, wd));
   final_norm_ = frozen(zeros({H}, DType::F32));
   layers_.resize(cfg_.n_layer);
   for (int i = 0; i < cfg_.n_layer; ++i) {
     auto& L = layers_[i];
     L.sliding = cfg_.sliding[i];
     L.in_norm = frozen(zeros({H}, DType::F32));
-    L.qkv_w = frozen(zeros({nqkv, H}, DType::BF16));
-    L.o_w = frozen(zeros({H, cfg_.n_head * D}, DType::BF16));
+    L.qkv_w = frozen(zeros({nqkv, H}, wd));
+    L.o_w = frozen(zeros({H, cfg_.n_head * D}, wd));
     L.q_norm = frozen(zeros({D}, DType::F32));
     L.k_norm = frozen(zeros({D}, DType::F32));
     L.post_attn_norm = frozen(zeros({H}, DType::F32));
     L.pre_ff_norm = frozen(zeros({H}, DType::F32));
-    L.gu_w = frozen(zeros({2 * I, H}, DType::BF16));
-    L.down_w = frozen(zeros({H, I}, DType::BF16));
+    L.gu_w = frozen(zeros({2 * I, H}, wd));
+    L.down_w = frozen(zeros({H, I}, wd));
     L.post_ff_norm = frozen(zeros({H}, DType::F32));
   }
   dropout_ctr = zeros({1}, DType::I64);
   ce_chunk = default_ce_chunk(cfg_.vocab_padded());
-  embed_scale_ = bf16_round(std::sqrt((float)H));
+  // (the bf16 model rounds sqrt(H) to bf16 like HF does in that dtype; fp32 keeps it exact)
+  embed_scale_ = wd == DType::F32 ? std::sqrt((float)H) : bf16_round(std::sqrt((float)H));
   rope_len_ = std::min(cfg_.max_positions, 4096);
 }
 
@@ -413,7 +415,7 @@ void Gemma3::merge_lora(float sign) {
     for (auto& a : ads) {
       Tensor A = a.A.leaf.detach().contiguous(), B = a.B.leaf.detach().contiguous();
       Tensor rows = w.c.slice(0, a.col0, a.col0 + a.ncols);
-      ::mft::lora_merge(rows.data_ptr(), 1, 1, w.c.size(1), A.data<float>(), B.data<float>(), (int)A.size(1), a.ncols,
+      ::mft::lora_merge(rows.data_ptr(), w.c.dtype() == DType::BF16 ? 1 : 0, 1, w.c.size(1), A.data<float>(), B.data<float>(), (int)A.size(1), a.ncols,
                         a.rank, sign * spec_.scale(), current_stream());
     }
     w.wt = Tensor();
@@ -477,9 +479,19 @@ std::pair<Tensor, Tensor> Gemma3::layer(int i, const Tensor& x0, const Tensor& h
   Tensor x = x0;
   // attention
   Tensor qkv = proj(h, H, L.qkv_w, active(L.lqkv), L.waug_qkv, fused_a(active(L.lqkv)).defined()).view({B, S, nq + 2 * nkv, D});
-  Tensor o = qknorm_rope_attention(qkv, nq, nkv, L.q_norm, L.k_norm, cs.first, cs.second, eps, 1.f,
-                                   interleaved_rope, attn_scale, L.sliding ? cfg_.sliding_window : 0,
-                                   aug(active(L.lo), nq * D));
+  Tensor o;
+  if (attn_naive) {  // --attn_impl naive: per-head RMSNorm + RoPE + materialized GQA masked softmax
+    Tensor q = rms_norm(qkv.slice(2, 0, nq), L.q_norm.c.to(qkv.dtype()), eps, 1.f);
+    Tensor k = rms_norm(qkv.slice(2, nq, nq + nkv), L.k_norm.c.to(qkv.dtype()), eps, 1.f);
+    Tensor c = cs.first.slice(0, 0, S), sn = cs.second.slice(0, 0, S);
+    q = apply_rope(q, c, sn, interleaved_rope);
+    k = apply_rope(k, c, sn, interleaved_rope);
+    o = attention_ref(q, k, qkv.slice(2, nq + nkv, nq + 2 * nkv), attn_scale, true, L.sliding ? cfg_.sliding_window : 0);
+    o = pad_cols(o.view({B * S, nq * D}), std::max(nq * D, aug(active(L.lo), nq * D)));
+  } else {
+    o = qknorm_rope_attention(qkv, nq, nkv, L.q_norm, L.k_norm, cs.first, cs.second, eps, 1.f, interleaved_rope,
+                              attn_scale, L.sliding ? cfg_.sliding_window : 0, aug(active(L.lo), nq * D));
+  }
   o = o.view({B * S, o.size(-1)});
   Tensor a = proj(o, nq * D, L.o_w, active(L.lo), L.waug_o, false);
   a = add_norm(a, Tensor(), L.post_attn_norm, nullptr, eps, true, 1.f, 0).second;
@@ -506,6 +518,7 @@ Tensor Gemma3::embed_tokens(const Tensor& ids) {
 }
 
 Tensor Gemma3::hidden(const Tensor& ids) {
+  if (compute_dtype() == DType::F32) return hidden_ref(ids);
   lora_prep_step_begin();  // every LoRA layer's weight prep for this forward, one launch
   const int64_t B = ids.size(0), S = ids.size(1);
   const int H = cfg_.hidden;
@@ -536,6 +549,10 @@ Tensor Gemma3::hidden(const Tensor& ids) {
 
 Tensor Gemma3::loss(const Tensor& ids, const Tensor& labels, float w_grad_scale) {
   Tensor h = hidden(ids);
+  if (compute_dtype() == DType::F32) {
+    Tensor l = cross_entropy(logits_ref(h), labels.reshape({-1}), -100);
+    return loss_sum ? mul(l, valid_count(labels)) : l;
+  }
   return lm_head_ce(h, embed_, labels, cfg_.vocab_size, ce_chunk, w_grad_scale, loss_sum);
 }
 
@@ -546,8 +563,53 @@ std::pair<Tensor, Tensor> Gemma3::nll(const Tensor& ids, const Tensor& labels) {
   Tensor h = hidden(ids);
   lora_prep_step_end();  // no backward follows
   training = t;
+  if (compute_dtype() == DType::F32) {
+    Tensor cnt = valid_count(labels);
+    return {mul(cross_entropy(logits_ref(h), labels.reshape({-1}), -100), cnt), cnt};
+  }
   return lm_head_nll(h, embed_, labels, cfg_.vocab_size, ce_chunk);
 }
+
+// ------------------------------------------------------------------ composite path (--dtype fp32)
+// The reference's Gemma-3 forward (graph/gemma_model.cpp:179-944) op by op on fp32 tensors: scaled
+// embedding, per layer RMSNorm(1 + w) -> q|k|v (+ LoRA) -> q / k RMSNorm over head_dim -> RoPE (rotate-half,
+// or the reference's interleaved pairs) -> GQA masked softmax (sliding window on local layers) -> o (+ LoRA)
+// -> post-attention norm -> residual -> pre-FF norm -> gate|up (+ LoRA) -> GeGLU -> down (+ LoRA) ->
+// post-FF norm -> residual; final norm; tied LM head (no transposed copy kept).
+Tensor Gemma3::hidden_ref(const Tensor& ids) {
+  MFT_CHECK(!streamer_, "--dtype fp32: weight streaming runs the bf16 kernels only");
+  const int64_t B = ids.size(0), S = ids.size(1);
+  const int H = cfg_.hidden, D = cfg_.head_dim, nq = cfg_.n_head, nkv = cfg_.n_kv, I = cfg_.intermediate;
+  const float s = spec_.scale(), eps = cfg_.eps, attn_scale = 1.f / std::sqrt(cfg_.query_pre_attn_scalar);
+  const uint64_t step = training ? (uint64_t)dropout_ctr.item() : 0;
+  rope(false, (int)S), rope(true, (int)S);
+  Tensor x = mul_scalar(embedding(ids.reshape({-1}), cw(embed_)), embed_scale_);
+  for (int i = 0; i < cfg_.n_layer; ++i) {
+    auto& L = layers_[i];
+    const auto cs = rope(L.sliding, (int)S);
+    Tensor c = cs.first.slice(0, 0, S), sn = cs.second.slice(0, 0, S);
+    Tensor h = rms_norm(x, cw(L.in_norm), eps, 1.f);
+    Tensor qkv = lora_linear_ref(h, L.qkv_w, nullptr, active(L.lqkv), s, training, step).view({B, S, nq + 2 * nkv, D});
+    Tensor q = apply_rope(rms_norm(qkv.slice(2, 0, nq), cw(L.q_norm), eps, 1.f), c, sn, interleaved_rope);
+    Tensor k = apply_rope(rms_norm(qkv.slice(2, nq, nq + nkv), cw(L.k_norm), eps, 1.f), c, sn, interleaved_rope);
+    Tensor o = attention_ref(q, k, qkv.slice(2, nq + nkv, nq + 2 * nkv), attn_scale, true,
+                             L.sliding ? cfg_.sliding_window : 0);
+    Tensor a = lora_linear_ref(o.reshape({B * S, nq * D}), L.o_w, nullptr, active(L.lo), s, training, step);
+    x = add(x, rms_norm(a, cw(L.post_attn_norm), eps, 1.f));
+    h = rms_norm(x, cw(L.pre_ff_norm), eps, 1.f);
+    Tensor gu = lora_linear_ref(h, L.gu_w, nullptr, active(L.lgu), s, training, step);
+    Tensor g = cfg_.act == 1 ? swiglu(gu.slice(1, 0, I), gu.slice(1, I, 2 * I)) : geglu(gu.slice(1, 0, I), gu.slice(1, I, 2 * I));
+    Tensor f = rms_norm(lora_linear_ref(g, L.down_w, nullptr, active(L.ldown), s, training, step), cw(L.post_ff_norm), eps, 1.f);
+    if (!capture_layers.empty() && std::find(capture_layers.begin(), capture_layers.end(), i) != capture_layers.end()) {
+      NoGradGuard ng;
+      captured[i] = f.detach().clone();
+    }
+    x = add(x, f);
+  }
+  return rms_norm(x, cw(final_norm_), eps, 1.f);
+}
+
+Tensor Gemma3::logits_ref(const Tensor& h) { return matmul(h, cw(embed_).slice(0, 0, cfg_.vocab_size).t()); }
 
 }  // namespace eng
 }  // namespace mft

@@ -89,6 +89,9 @@ class Gemma3 : public LanguageModel {
   std::pair<Tensor, Tensor> rope(bool local, int S);
   // decoder layer i: (residual x, normed h) -> (x, h normed for the next layer)
   std::pair<Tensor, Tensor> layer(int i, const Tensor& x, const Tensor& h, int64_t B, int64_t S);
+  // the composite path (--dtype fp32): final hidden states and the full logits
+  Tensor hidden_ref(const Tensor& ids);
+  Tensor logits_ref(const Tensor& h);
   Gemma3Config cfg_;
   GemmaLoraSpec spec_;
   Param embed_, final_norm_;

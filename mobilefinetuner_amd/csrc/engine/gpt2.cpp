@@ -72,8 +72,9 @@ GPT2::GPT2(const GPT2Config& cfg) : cfg_(cfg) { alloc(); }
 void GPT2::alloc() {
   const int C = cfg_.n_embd;
   NoGradGuard ng;
-  wte_ = frozen(zeros({cfg_.vocab_padded(), C}, DType::BF16));
-  wpe_ = frozen(zeros({cfg_.n_positions, C}, DType::BF16));
+  const DType wd = compute_dtype();  // bf16, or fp32 for --dtype fp32 (LayerNorm parameters are fp32 either way)
+  wte_ = frozen(zeros({cfg_.vocab_padded(), C}, wd));
+  wpe_ = frozen(zeros({cfg_.n_positions, C}, wd));
   lnf_w_ = frozen(ones({C}, DType::F32));
   lnf_b_ = frozen(zeros({C}, DType::F32));
   blocks_.resize(cfg_.n_layer);
@@ -82,14 +83,14 @@ void GPT2::alloc() {
     b.ln1_b = frozen(zeros({C}, DType::F32));
     b.ln2_w = frozen(ones({C}, DType::F32));
     b.ln2_b = frozen(zeros({C}, DType::F32));
-    b.attn_w = frozen(zeros({3 * C, C}, DType::BF16));
-    b.attn_b = frozen(zeros({3 * C}, DType::BF16));
-    b.proj_w = frozen(zeros({C, C}, DType::BF16));
-    b.proj_b = frozen(zeros({C}, DType::BF16));
-    b.fc_w = frozen(zeros({4 * C, C}, DType::BF16));
-    b.fc_b = frozen(zeros({4 * C}, DType::BF16));
-    b.mproj_w = frozen(zeros({C, 4 * C}, DType::BF16));
-    b.mproj_b = frozen(zeros({C}, DType::BF16));
+    b.attn_w = frozen(zeros({3 * C, C}, wd));
+    b.attn_b = frozen(zeros({3 * C}, wd));
+    b.proj_w = frozen(zeros({C, C}, wd));
+    b.proj_b = frozen(zeros({C}, wd));
+    b.fc_w = frozen(zeros({4 * C, C}, wd));
+    b.fc_b = frozen(zeros({4 * C}, wd));
+    b.mproj_w = frozen(zeros({C, 4 * C}, wd));
+    b.mproj_b = frozen(zeros({C}, wd));
   }
   dropout_ctr = zeros({1}, DType::I64);
   ce_chunk = default_ce_chunk(cfg_.vocab_padded());
@@ -423,7 +424,7 @@ void GPT2::merge_lora(float sign) {
     for (auto& a : ads) {
       Tensor A = a.A.leaf.detach().contiguous(), B = a.B.leaf.detach().contiguous();
       Tensor rows = w.c.slice(0, a.col0, a.col0 + a.ncols);
-      ::mft::lora_merge(rows.data_ptr(), 1, 1, w.c.size(1), A.data<float>(), B.data<float>(), (int)A.size(1), a.ncols,
+      ::mft::lora_merge(rows.data_ptr(), w.c.dtype() == DType::BF16 ? 1 : 0, 1, w.c.size(1), A.data<float>(), B.data<float>(), (int)A.size(1), a.ncols,
                         a.rank, sign * spec_.scale(), current_stream());
     }
     w.wt = Tensor();
@@ -465,7 +466,14 @@ std::pair<Tensor, Tensor> GPT2::block(int i, const Tensor& x0, const Tensor& h, 
                : st ? lora_linear(h, b.attn_w, &b.attn_b, active(b.lqkv), scale, training, dropout_ctr)
                     : lora_linear_aug(h, C, b.attn_w, &b.attn_b, active(b.lqkv), scale, b.waug_qkv, training, dropout_ctr,
                                       u_ready);
-  Tensor o = attention_packed(qkv.view({B, S, 3, H, D}), 1.f / std::sqrt((float)D), true, 0, aug(active(b.lproj)));
+  Tensor o;
+  if (attn_naive) {  // --attn_impl naive: materialized masked softmax on the q / k / v views of qkv
+    Tensor q5 = qkv.view({B, S, 3, H, D});
+    o = attention_ref(q5.select(2, 0), q5.select(2, 1), q5.select(2, 2), 1.f / std::sqrt((float)D), true, 0);
+    o = pad_cols(o.view({B * S, C}), std::max(C, aug(active(b.lproj))));
+  } else {
+    o = attention_packed(qkv.view({B, S, 3, H, D}), 1.f / std::sqrt((float)D), true, 0, aug(active(b.lproj)));
+  }
   o = o.view({B * S, o.size(-1)});
   // The residual adds ride in the producing GEMMs' epilogues where the producer supports it (augmented-K
   // LoRA projection, the fused GELU MLP): s = x + proj(o) comes out of the projection, and the norm that
@@ -500,6 +508,7 @@ std::pair<Tensor, Tensor> GPT2::block(int i, const Tensor& x0, const Tensor& h, 
 }
 
 Tensor GPT2::hidden(const Tensor& ids) {
+  if (compute_dtype() == DType::F32) return hidden_ref(ids);
   lora_prep_step_begin();  // every LoRA layer's weight prep for this forward, one launch
   const int64_t B = ids.size(0), S = ids.size(1);
   MFT_CHECK(S <= cfg_.n_positions, "sequence ", S, " exceeds n_positions ", cfg_.n_positions);
@@ -534,6 +543,10 @@ Tensor GPT2::hidden(const Tensor& ids) {
 
 Tensor GPT2::loss(const Tensor& ids, const Tensor& labels, float w_grad_scale) {
   Tensor h = hidden(ids);
+  if (compute_dtype() == DType::F32) {  // full logits + the catalog's cross entropy (mean over valid labels)
+    Tensor l = cross_entropy(logits_ref(h), labels.reshape({-1}), -100);
+    return loss_sum ? mul(l, valid_count(labels)) : l;
+  }
   return lm_head_ce(h, wte_, labels, cfg_.vocab_size, ce_chunk, w_grad_scale, loss_sum);
 }
 
@@ -544,8 +557,43 @@ std::pair<Tensor, Tensor> GPT2::nll(const Tensor& ids, const Tensor& labels) {
   Tensor h = hidden(ids);
   lora_prep_step_end();  // no backward follows
   training = t;
+  if (compute_dtype() == DType::F32) {
+    Tensor cnt = valid_count(labels);
+    return {mul(cross_entropy(logits_ref(h), labels.reshape({-1}), -100), cnt), cnt};
+  }
   return lm_head_nll(h, wte_, labels, cfg_.vocab_size, ce_chunk);
 }
+
+// ------------------------------------------------------------------ composite path (--dtype fp32)
+// The reference's forward (graph/gpt2_model.cpp:323-442, :530-817) op by op on fp32 tensors: embedding +
+// positions, per block LayerNorm -> qkv (+ LoRA) -> masked-softmax attention -> proj (+ LoRA) -> residual
+// -> LayerNorm -> fc (+ LoRA) -> GELU-tanh -> proj (+ LoRA) -> residual, final LayerNorm; the tied LM head
+// is the full [M, V] logits GEMM.  Unlike the reference, every op has its backward.
+Tensor GPT2::hidden_ref(const Tensor& ids) {
+  MFT_CHECK(!streamer_ && !provider_, "--dtype fp32: weight streaming / ZeRO-3 run the bf16 kernels only");
+  const int64_t B = ids.size(0), S = ids.size(1);
+  MFT_CHECK(S <= cfg_.n_positions, "sequence ", S, " exceeds n_positions ", cfg_.n_positions);
+  const int C = cfg_.n_embd, H = cfg_.n_head, D = cfg_.head_dim();
+  const float s = spec_.scale();
+  const uint64_t step = training ? (uint64_t)dropout_ctr.item() : 0;  // (eager: capturable() is false)
+  std::vector<int64_t> pos((size_t)S);
+  for (int64_t i = 0; i < S; ++i) pos[(size_t)i] = i;
+  Tensor x = add(embedding(ids.reshape({-1}), cw(wte_)).view({B, S, C}), embedding(from_vector(pos, {S}, DType::I64), cw(wpe_)));
+  x = x.reshape({B * S, C});
+  for (int i = 0; i < cfg_.n_layer; ++i) {
+    auto& b = blocks_[i];
+    Tensor h = layer_norm(x, cw(b.ln1_w), cw(b.ln1_b), cfg_.eps);
+    Tensor qkv = lora_linear_ref(h, b.attn_w, &b.attn_b, active(b.lqkv), s, training, step).view({B, S, 3, H, D});
+    Tensor o = attention_ref(qkv.select(2, 0), qkv.select(2, 1), qkv.select(2, 2), 1.f / std::sqrt((float)D), true, 0);
+    x = add(x, lora_linear_ref(o.reshape({B * S, C}), b.proj_w, &b.proj_b, active(b.lproj), s, training, step));
+    h = layer_norm(x, cw(b.ln2_w), cw(b.ln2_b), cfg_.eps);
+    Tensor u = gelu(lora_linear_ref(h, b.fc_w, &b.fc_b, active(b.lfc), s, training, step), true);
+    x = add(x, lora_linear_ref(u, b.mproj_w, &b.mproj_b, active(b.lfcout), s, training, step));
+  }
+  return layer_norm(x, cw(lnf_w_), cw(lnf_b_), cfg_.eps);
+}
+
+Tensor GPT2::logits_ref(const Tensor& h) { return matmul(h, cw(wte_).slice(0, 0, cfg_.vocab_size).t()); }
 
 }  // namespace eng
 }  // namespace mft

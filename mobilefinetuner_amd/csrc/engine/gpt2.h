@@ -87,6 +87,9 @@ class GPT2 : public LanguageModel {
   void alloc();
   // transformer block i: (residual x, normed h) -> (x, h normed for the next block)
   std::pair<Tensor, Tensor> block(int i, const Tensor& x, const Tensor& h, int64_t B, int64_t S);
+  // the composite path (--dtype fp32 / --attn_impl naive): final hidden states and the full logits
+  Tensor hidden_ref(const Tensor& ids);
+  Tensor logits_ref(const Tensor& h);
   GPT2Config cfg_;
   LoraSpec spec_;
   bool lora_ = false, full_ = false;

@@ -41,6 +41,12 @@ class LanguageModel {
   // --activation_checkpointing: each block's activations are recomputed in the backward
   // (autograd.h checkpoint()) instead of kept -- one more forward for O(blocks) less memory
   bool grad_checkpoint = false;
+  // --attn_impl naive: the materialized masked-softmax attention (attention_ref) in place of the flash
+  // kernels (--dtype fp32 always takes it)
+  bool attn_naive = false;
+  // the composite path (--dtype fp32 / --attn_impl naive) reads host values (dropout step, id checks,
+  // mask tables) during the step: it runs eagerly, never inside a hipGraph capture
+  bool capturable() const { return !attn_naive && compute_dtype() != DType::F32; }
   // alignment harness: hidden() copies the listed layers' MLP outputs (after the post-FF norm)
   std::vector<int> capture_layers;
   std::map<int, Tensor> captured;

@@ -76,10 +76,70 @@ LoraAdapter make_adapter(int col0, int n, int r, const Tensor& A_init, float dro
   Tensor B = zeros({r, n}, DType::F32);
   B.requires_grad_(true);
   a.A.leaf = A;
-  a.A.c = A.to(DType::BF16);
   a.B.leaf = B;
-  a.B.c = B.to(DType::BF16);
+  // (--dtype fp32: the adapters compute on their fp32 masters; FlatParams keeps them that way)
+  const bool f32 = compute_dtype() == DType::F32;
+  a.A.c = f32 ? A : A.to(DType::BF16);
+  a.B.c = f32 ? B : B.to(DType::BF16);
   return a;
+}
+
+// ------------------------------------------------------------------ reference-precision composite path
+namespace {
+DType g_compute_dtype = DType::BF16;
+}
+void set_compute_dtype(DType d) {
+  MFT_CHECK(d == DType::BF16 || d == DType::F32, "compute dtype: bf16 or fp32");
+  g_compute_dtype = d;
+}
+DType compute_dtype() { return g_compute_dtype; }
+
+Tensor pad_cols(const Tensor& x, int64_t cols) {
+  MFT_CHECK(x.dim() == 2, "pad_cols: 2-D input");
+  if (cols <= x.size(1)) return x;
+  Tensor z = zeros({x.size(0), cols - x.size(1)}, x.dtype(), x.device());
+  return cat({x, z}, 1);
+}
+
+Tensor valid_count(const Tensor& labels) {
+  NoGradGuard ng;
+  Tensor c = zeros({1}, DType::F32, labels.device());
+  Tensor lc = labels.contiguous();
+  k::count_valid(lc.data<int64_t>(), (long)lc.numel(), -100, c.data<float>(), current_stream());
+  return c;
+}
+
+Tensor attention_ref(const Tensor& q, const Tensor& k, const Tensor& v, float scale, bool causal, int window) {
+  MFT_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4 && k.size(2) == v.size(2) && q.size(2) % k.size(2) == 0,
+            "attention_ref: q [B, Sq, H, D], k / v [B, Sk, Hkv, D]");
+  const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3), Sk = k.size(1), rep = H / k.size(2);
+  Tensor kk = repeat_kv(k, (int)rep), vv = repeat_kv(v, (int)rep);
+  Tensor sc = mul_scalar(matmul(q.transpose(1, 2), kk.transpose(1, 2).transpose(2, 3)), scale);  // [B, H, Sq, Sk]
+  if (causal || window > 0) sc = apply_mask(sc, causal_mask(Sq, Sk, window).to(q.device()));
+  Tensor o = matmul(softmax(sc), vv.transpose(1, 2));  // [B, H, Sq, D]
+  return o.transpose(1, 2).reshape({B, Sq, H * D});
+}
+
+Tensor lora_linear_ref(const Tensor& x, Param& w, Param* b, std::vector<LoraAdapter>& ads, float s, bool training,
+                       uint64_t drop_step) {
+  MFT_CHECK(x.dim() == 2, "lora_linear_ref: 2-D input");
+  Tensor y = linear(x, cw(w), b ? cw(*b) : Tensor());
+  const int64_t M = x.size(0), N = y.size(1);
+  for (auto& a : ads) {
+    const uint64_t seed = (drop_step + 1) * 0x9E3779B97F4A7C15ull ^ ((uint64_t)a.salt << 17);
+    Tensor xin = training && a.dropout > 0.f ? dropout(x, a.dropout, seed, true) : x;
+    Tensor d = mul_scalar(matmul(matmul(xin, cw(a.A).t()), cw(a.B)), s);  // [M, ncols]
+    if (a.col0 == 0 && a.ncols == N) {
+      y = add(y, d);
+    } else {
+      std::vector<Tensor> parts;
+      if (a.col0 > 0) parts.push_back(zeros({M, (int64_t)a.col0}, d.dtype(), d.device()));
+      parts.push_back(d);
+      if (a.col0 + a.ncols < N) parts.push_back(zeros({M, N - a.col0 - a.ncols}, d.dtype(), d.device()));
+      y = add(y, cat(parts, 1));
+    }
+  }
+  return y;
 }
 
 // ------------------------------------------------------------------ norms

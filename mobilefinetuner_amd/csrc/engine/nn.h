@@ -108,5 +108,29 @@ Tensor lm_head_token_nll(const Tensor& h, Param& w, const Tensor& labels, int V,
 // (sum of NLL over valid rows, number of valid rows) without gradients -- evaluation
 std::pair<Tensor, Tensor> lm_head_nll(const Tensor& h, Param& w, const Tensor& labels, int V, int64_t chunk);
 
+// ------------------------------------------------------------------ reference-precision composite path
+// --dtype: the models' compute precision.  BF16 (default) runs the fused kernels above; F32 runs the
+// reference's own precision (it computes everything in fp32, core/ops.cpp:545-573) as a composite of the
+// generic op catalog (ops.h: fp32 SIMT GEMMs, row softmax, elementwise / reduction kernels), every op
+// differentiated by the tape.  Set before a model is built (its weights are allocated in that dtype).
+void set_compute_dtype(DType d);
+DType compute_dtype();
+// materialized masked-softmax attention (the reference's standard path, graph/gpt2_model.cpp:679-711 and
+// graph/gemma_model.cpp:481-508): q [B, Sq, H, D], k / v [B, Sk, Hkv, D] (GQA through repeat_kv) ->
+// [B, Sq, H * D]; causal, window > 0 = sliding window.  --dtype fp32 and --attn_impl naive.
+Tensor attention_ref(const Tensor& q, const Tensor& k, const Tensor& v, float scale, bool causal, int window);
+// composite LoRA Linear on 2-D x (reference nn/lora_linear.cpp:47-108, + PEFT dropout on the adapter input):
+// y = x W^T (+ b) + sum_i s drop(x) A_i^T B_i over output columns [col0_i, col0_i + ncols_i); drop_step
+// seeds the dropout masks (one per step and adapter)
+Tensor lora_linear_ref(const Tensor& x, Param& w, Param* b, std::vector<LoraAdapter>& ads, float s, bool training,
+                       uint64_t drop_step);
+// the tensor the composite path computes with: the autograd leaf of a trainable parameter (its fp32
+// master -- the gradient lands in the flat grad buffer through the tape), else the compute view
+inline const Tensor& cw(const Param& p) { return p.trainable() ? p.leaf : p.c; }
+// x [M, n] -> [M, cols] with zero columns appended (differentiable); x itself when cols <= n
+Tensor pad_cols(const Tensor& x, int64_t cols);
+// number of labels != -100, fp32 [1] on the device
+Tensor valid_count(const Tensor& labels);
+
 }  // namespace eng
 }  // namespace mft

@@ -574,39 +574,33 @@ Tensor apply_rope(const Tensor& x, const Tensor& cos_t, const Tensor& sin_t, boo
 }
 
 Tensor embedding(const Tensor& ids, const Tensor& table) {
-  MFT_CHECK(ids.dtype() == DType::I64 && table.dim() == 2, "embedding: int64 ids, [V, C] table");
-  const int64_t n = ids.numel(), C = table.size(1);
+  MFT_CHECK(ids.dtype() == DType::I64 && table.dim() == 2 && table.stride(1) == 1 && table.stride(0) == table.size(1),
+            "embedding: int64 ids, contiguous [V, C] table");
+  const int64_t n = ids.numel(), C = table.size(1), V = table.size(0);
   Tensor idc = ids.contiguous();
   Tensor o;
   {
     NoGradGuard ng;
     o = empty({n, C}, table.dtype(), table.device());
-    // gather: rows of the table selected by ids (strided copy per row through the generic kernel
-    // would be n launches; use a one-row view trick: table[ids] via host loop is too slow, so reuse
-    // the fused embedding kernel when bf16, else a device index-copy)
-    std::vector<int64_t> h(n);
-    Tensor hi = empty({n}, DType::I64, Device::cpu());
-    hi.copy_(idc);
-    for (int64_t i = 0; i < n; ++i) {
-      Tensor dst = o.select(0, i);
-      dst.copy_(table.detach().select(0, hi.data<int64_t>()[i]));
-    }
+    // one gather launch (rows by id); the ids are range-checked on the host first -- the kernel skips
+    // an out-of-range id, the check makes it an error instead of a silent zero-free row
+    Tensor hi = idc.to(Device::cpu());
+    for (int64_t i = 0; i < n; ++i)
+      MFT_CHECK(hi.data<int64_t>()[i] >= 0 && hi.data<int64_t>()[i] < V, "embedding: id ", hi.data<int64_t>()[i],
+                " outside [0, ", V, ")");
+    k::gather_rows(o.data_ptr(), (int)o.dtype(), table.data_ptr(), (int)table.dtype(), idc.data<int64_t>(), n, (int)C,
+                   V, S());
   }
   Shape os = ids.shape();
   os.push_back(C);
   o = o.view(os);
   if (needs_grad(table)) {
     Shape ts = table.shape();
-    Tensor hid = empty({n}, DType::I64, Device::cpu());
-    hid.copy_(idc);
-    auto nd = lambda_node("EmbeddingBackward", [ts, hid, n, C](std::vector<Tensor>& g) {
+    auto nd = lambda_node("EmbeddingBackward", [ts, idc, n, C, V](std::vector<Tensor>& g) {
       if (!g[0].defined()) return std::vector<Tensor>{Tensor()};
       Tensor gt = zeros(ts, DType::F32, g[0].device());
-      Tensor g2 = g[0].reshape({n, C});
-      for (int64_t i = 0; i < n; ++i) {
-        Tensor row = gt.select(0, hid.data<int64_t>()[i]);
-        add_(row, g2.select(0, i));
-      }
+      Tensor g2 = g[0].reshape({n, C}).contiguous();
+      k::scatter_add_rows(gt.data<float>(), g2.data_ptr(), (int)g2.dtype(), idc.data<int64_t>(), n, (int)C, V, S());
       return std::vector<Tensor>{gt};
     });
     connect(nd, {table}, {o});

@@ -63,7 +63,11 @@ void nll_rows(const void* lp, int dt, const int64_t* target, float* out, long ro
 // dlp[r, target[r]] = -scale (ignore rows 0), other entries 0
 void nll_rows_bwd(void* dlp, int dt, const int64_t* target, long rows, int n, long ld, int ignore, const float* scale,
                   hipStream_t st);
-// gather along the last dim: out[r] = x[r, idx[r]]
+// rows of a [V, C] table: dst[r, :] = src[idx[r], :] (any float dtypes; ids outside [0, V) skipped)
+void gather_rows(void* dst, int ddt, const void* src, int sdt, const int64_t* idx, long n, int C, long V, hipStream_t st);
+// dst[idx[r], :] += src[r, :] into an fp32 table (float atomics: the order of equal ids is not fixed)
+void scatter_add_rows(float* dst, const void* src, int sdt, const int64_t* idx, long n, int C, long V, hipStream_t st);
+// number of targets != ignore -> out[0] (fp32)
 void count_valid(const int64_t* target, long n, int ignore, float* out, hipStream_t st);
 // training-loss EMA on device: ema = {value, initialised}; non-finite losses are skipped
 void ema_update(float* ema, const float* loss, float beta, hipStream_t st);

@@ -367,6 +367,25 @@ __global__ void nll_rows_bwd_kernel(void* d, int dt, const int64_t* t, long rows
   }
 }
 
+// rows of a [V, C] table selected by idx (gather) / added back into an fp32 [V, C] table (scatter-add):
+// one workgroup per row, the row's C values strided over its threads (embedding of the composite path)
+__global__ void gather_rows_kernel(void* dst, int ddt, const void* src, int sdt, const int64_t* idx, long n, int C,
+                                   long V) {
+  const long r = blockIdx.x;
+  if (r >= n) return;
+  const int64_t row = idx[r];
+  if (row < 0 || row >= V) return;  // (the host checks the ids; never read out of the table)
+  for (int j = threadIdx.x; j < C; j += blockDim.x) st(dst, ddt, r * C + j, ld(src, sdt, row * (int64_t)C + j));
+}
+
+__global__ void scatter_add_rows_kernel(float* dst, const void* src, int sdt, const int64_t* idx, long n, int C, long V) {
+  const long r = blockIdx.x;
+  if (r >= n) return;
+  const int64_t row = idx[r];
+  if (row < 0 || row >= V) return;
+  for (int j = threadIdx.x; j < C; j += blockDim.x) atomicAdd(dst + row * (int64_t)C + j, ld(src, sdt, r * C + j));
+}
+
 __global__ void count_valid_kernel(const int64_t* t, long n, int ignore, float* out) {
   __shared__ float sm[16];
   float c = 0.f;
@@ -500,6 +519,15 @@ void nll_rows_bwd(void* d, int dt, const int64_t* t, long rows, int n, long ldl,
                   hipStream_t stm) {
   if (!rows) return;
   nll_rows_bwd_kernel<<<grid_for(rows * (int64_t)n), 256, 0, stm>>>(d, dt, t, rows, n, ldl, ignore, scale);
+}
+
+void gather_rows(void* dst, int ddt, const void* src, int sdt, const int64_t* idx, long n, int C, long V,
+                 hipStream_t stm) {
+  if (n) gather_rows_kernel<<<(unsigned)n, 256, 0, stm>>>(dst, ddt, src, sdt, idx, n, C, V);
+}
+
+void scatter_add_rows(float* dst, const void* src, int sdt, const int64_t* idx, long n, int C, long V, hipStream_t stm) {
+  if (n) scatter_add_rows_kernel<<<(unsigned)n, 256, 0, stm>>>(dst, src, sdt, idx, n, C, V);
 }
 
 void count_valid(const int64_t* t, long n, int ignore, float* out, hipStream_t stm) {

@@ -15,5 +15,10 @@ class TraceRange {
   TraceRange& operator=(const TraceRange&) = delete;
 };
 
+// --profile_steps a:b: collection paused outside the window (rocprofv3 --selected-regions honours
+// roctxProfilerPause / Resume; without a tool attached both are no-ops)
+inline void profiler_pause() { roctxProfilerPause(0); }
+inline void profiler_resume() { roctxProfilerResume(0); }
+
 }  // namespace eng
 }  // namespace mft

@@ -41,6 +41,14 @@ Trainer::Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDatase
     std::printf("[trainer] step runs eagerly (no hipGraph): staged host-moment optimizer\n");
     cfg_.use_graph = false;
   }
+  if (cfg_.use_graph && !model_.capturable()) {
+    // the composite path (--dtype fp32 / --attn_impl naive) reads host values inside the step
+    std::printf("[trainer] step runs eagerly (no hipGraph): %s composite path\n",
+                compute_dtype() == DType::F32 ? "--dtype fp32" : "--attn_impl naive");
+    cfg_.use_graph = false;
+  }
+  MFT_CHECK(!(cfg_.compat_grad_overwrite && cfg.accum > 1 && dp_ && dp_->params_sharded()),
+            "--compat_grad_overwrite with ZeRO-3 is not supported");
   if (comm_ && !(dp_ && dp_->params_sharded())) {  // every rank starts from rank 0's trainable weights
     comm_->broadcast(flat_.master.data_ptr(), (size_t)flat_.numel * sizeof(float), 0, stream_);
     flat_.refresh_shadow();
@@ -100,6 +108,10 @@ void Trainer::fwd_bwd() {
   }
   for (size_t i = 0; i < ids_.size(); ++i) {
     if (dp_) dp_->begin_micro((int)i, (int)ids_.size());  // the last micro-batch's hooks launch buckets
+    if (cfg_.compat_grad_overwrite && i > 0) {  // reference .grad overwrite: earlier micro-batches drop out
+      if (dp_) dp_->zero_grad(flat_);
+      else flat_.zero_grad();
+    }
     Tensor loss = model_.loss(ids_[i], labels_[i], gs);
     Tensor scaled = mul_scalar(loss, gs);
     backward({scaled});
@@ -287,6 +299,13 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
   auto t_last = std::chrono::steady_clock::now();
   pm_t0_ = t_last;
   int64_t tok_since = 0, steps_since = 0;
+  const bool prof = cfg_.profile_to > 0 && cfg_.profile_to >= cfg_.profile_from;
+  hipEvent_t pe0 = nullptr, pe1 = nullptr;
+  if (prof) {
+    profiler_pause();
+    HIP_OK(hipEventCreate(&pe0));
+    HIP_OK(hipEventCreate(&pe1));
+  }
   for (int64_t it = global_step; it < total_steps_; ++it) {  // global_step > 0 after load_state
     if (cfg_.fault_step > 0 && it + 1 == cfg_.fault_step && (comm_ ? comm_->rank() : 0) == cfg_.fault_rank)
       throw std::runtime_error("injected fault at step " + std::to_string(it + 1) + " on rank " +
@@ -302,7 +321,25 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
       ++micro_steps_;
       if (cfg_.micro_hook) cfg_.micro_hook(micro_steps_, hid[a].data(), B, S);
     }
+    const bool in_prof = prof && it + 1 >= cfg_.profile_from && it + 1 <= cfg_.profile_to;
+    if (in_prof && it + 1 == std::max<int64_t>(cfg_.profile_from, 1)) {
+      synchronize();
+      profiler_resume();
+      roctxRangePushA("mft.profile");
+    }
+    if (in_prof) HIP_OK(hipEventRecord(pe0, stream_));
     Tensor loss = step(micro);
+    if (in_prof) {
+      HIP_OK(hipEventRecord(pe1, stream_));
+      HIP_OK(hipEventSynchronize(pe1));
+      float ms = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms, pe0, pe1));
+      std::printf("[profile] step %lld: %.3f ms device\n", (long long)(it + 1), ms);
+      if (it + 1 == cfg_.profile_to || it + 1 == total_steps_) {
+        roctxRangePop();
+        profiler_pause();
+      }
+    }
     ++global_step;
     total_tokens += tokens;
     tok_since += tokens;
@@ -385,6 +422,8 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
     }
   }
   synchronize();
+  if (pe0) (void)hipEventDestroy(pe0);
+  if (pe1) (void)hipEventDestroy(pe1);
   // the final exports (LoRA / HF writers read the fp32 masters) need every rank's ZeRO-1/2 chunks
   if (!cfg_.state_dir.empty()) save_state(cfg_.state_dir);
   else gather_for_export();

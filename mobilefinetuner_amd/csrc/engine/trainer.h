@@ -50,6 +50,13 @@ struct TrainConfig {
   int64_t fault_step = 0;
   int fault_rank = 0;
   int pm_interval = 0;
+  // --profile_steps a:b: steps a..b (1-indexed, inclusive) run inside one
+  // "mft.profile" roctx range with the profiler resumed (rocprofv3 --selected-regions collects only
+  // them) and each step's device time printed ([profile] lines, hipEvents); 0 = off
+  int64_t profile_from = 0, profile_to = 0;
+  // --compat_grad_overwrite: the reference overwrites .grad at every backward, so of
+  // an accumulated step only the last micro-batch's gradient (scaled by 1/accum) survives
+  bool compat_grad_overwrite = false;
   // learning rate of 0-indexed update `it` of `total`; unset: the GPT-2 CLI schedule (gpt2_cli_lr)
   std::function<float(int64_t it, int64_t total)> lr_fn;
   // called on the host before each optimizer step for every micro-batch, with the running 1-based
@@ -81,6 +88,8 @@ class Trainer {
   double bench(int warmup, int steps, float* final_loss);
   // the step actually replays a captured hipGraph (false: eager -- --no_graph or an uncapturable reducer)
   bool graph_replayed() const { return exec_ != nullptr; }
+  // the step will be captured (after the warm-up steps): the config's use_graph less what the trainer ruled out
+  bool uses_graph() const { return cfg_.use_graph; }
   std::pair<double, double> evaluate(int max_batches, int batch_size);  // (nll, ppl)
   // Full training state (same directory layout as the Python CLIs' --state_dir):
   // trainable.safetensors (fp32 master) + optimizer.safetensors (AdamW m, v) from rank 0 -- data

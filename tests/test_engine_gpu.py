@@ -354,3 +354,38 @@ def test_native_fault_then_resume(tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     got = losses(r.stdout)
     assert sorted(got) == [5, 6, 7, 8] and all(got[i] == ref[i] for i in got), (ref, got)
+
+
+def test_native_common_flag_block(tmp_path):
+    """The native CLIs' common flag block:
+    * --attn_impl naive (materialized masked softmax) trains like the flash kernels (bf16 noise);
+    * --dtype fp32 (reference-precision composite path, eager) trains and tracks the bf16 run;
+    * --profile_steps a:b prints one device time per step of the window and nothing else;
+    * --compat_grad_overwrite keeps only the last micro-batch's gradient (reference Q1): with two
+      micro-batches the first step's update differs from the accumulating run's."""
+    common = ["--random_init", "--model", "gpt2-tiny", "--synthetic_data", "--synthetic_tokens", "100000", "--steps",
+              "6", "--batch_size", "4", "--seq_len", "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic"]
+
+    def run(extra, prog="gpt2_lora_finetune"):
+        r = subprocess.run([_bin(prog), *common, *extra], capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        return loss_list(r.stdout, True), r.stdout
+
+    ref, _ = run([])
+    naive, out = run(["--attn_impl", "naive"])
+    assert "step runs eagerly" in out
+    assert naive == pytest.approx(ref, abs=2e-2), (naive, ref)
+    f32, out = run(["--dtype", "fp32"])
+    assert "--dtype fp32" in out and all(x == x for x in f32)
+    assert f32 == pytest.approx(ref, abs=3e-2), (f32, ref)
+    _, out = run(["--profile_steps", "2:4"])
+    prof = [ln for ln in out.splitlines() if ln.startswith("[profile] step ")]
+    assert [int(ln.split()[2].rstrip(":")) for ln in prof] == [2, 3, 4], prof
+    acc, _ = run(["--grad_accum_steps", "2"])
+    ow, _ = run(["--grad_accum_steps", "2", "--compat_grad_overwrite"])
+    assert acc[0] == pytest.approx(ow[0], abs=1e-6)  # the same first forward
+    assert ow[1:] != acc[1:]  # different updates from then on
+    # full fine-tuning in fp32 (every weight an fp32 leaf, tied embedding through both uses)
+    full, _ = run(["--dtype", "fp32"], prog="gpt2_full_finetune")
+    full_bf16, _ = run([], prog="gpt2_full_finetune")
+    assert len(full) == 6 and full == pytest.approx(full_bf16, abs=3e-2), (full, full_bf16)
