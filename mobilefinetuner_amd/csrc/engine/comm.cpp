@@ -191,7 +191,7 @@ ncclDataType_t nccl_type(CommType t) {
 }
 // CommOp::Avg is issued as ncclSum + an in-place scale: RCCL 2.26's ncclAvg (PreMulSum kernels)
 // returns wrong values in the last 4-8 elements of some lengths (fp32, 1-rank group, 66304 / 66240
-// elements; ncclSum exact at every length -- scripts/diag/rs_tail.py, profiles/r3_rccl_avg_tail.txt)
+// elements; ncclSum exact at every length -- scripts/probes/rs_tail.py, profiles/r3_rccl_avg_tail.txt)
 ncclRedOp_t nccl_op(CommOp op) { return op == CommOp::Max ? ncclMax : ncclSum; }
 void scale_inplace(void* buf, size_t n, CommType t, float s, hipStream_t st) {
   if (n == 0 || t == CommType::I32) return;

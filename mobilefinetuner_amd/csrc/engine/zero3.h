@@ -28,6 +28,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <string>
 #include <utility>
 #include <vector>
@@ -85,7 +87,11 @@ class Zero3 : public GradReducer, public BlockProvider {
   void prepare_optimizer() override;
   void flush_optimizer() override;
   void optimizer_state_loaded() override;
-  bool graph_capturable() const override { return !(sopt_ && staged_); }
+  // (MFT_Z3_CAPTURE=1: capture the staged step anyway -- diagnosis of its capture crash)
+  bool graph_capturable() const override {
+    static const bool force = std::getenv("MFT_Z3_CAPTURE") && std::getenv("MFT_Z3_CAPTURE")[0] == '1';
+    return force || !(sopt_ && staged_);
+  }
   int staged_slots() const { return sopt_ && staged_ ? nslot_ : 0; }  // 0: in place (or no host moments)
   bool params_sharded() const override { return true; }
   float grad_prescale() const override;
@@ -145,7 +151,7 @@ class Zero3 : public GradReducer, public BlockProvider {
   hipEvent_t fork_ev_ = nullptr, ojoin_ev_ = nullptr;
   // ONE side stream: a staged variant (H2D copy -> update -> D2H copy on three streams, the slot's
   // next H2D behind its D2H) forms a dependency ring over three side streams, which crashes
-  // hipStreamEndCapture on this ROCm (scripts/diag/r4_capture_probe.hip, profiles/r4_capture_probe.txt),
+  // hipStreamEndCapture on this ROCm (scripts/probes/r4_capture_probe.hip, profiles/r4_capture_probe.txt),
   // and with the copies folded onto one stream its two PCIe directions serialise (slower than in place:
   // profiles/r4_offload_modes.txt).
   hipStream_t ostream_ = nullptr;

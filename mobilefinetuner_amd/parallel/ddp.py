@@ -55,7 +55,7 @@ def _supports_avg(group=None):
 
 # Averages are SUM + divide, never ReduceOp.AVG: RCCL 2.26's AVG (its PreMulSum kernels) returns
 # wrong values in the last 4-8 elements of some lengths (66304, 66240 of fp32 on a 1-rank group;
-# SUM exact at every length and offset -- scripts/diag/rs_tail.py, profiles/r3_rccl_avg_tail.txt)
+# SUM exact at every length and offset -- scripts/probes/rs_tail.py, profiles/r3_rccl_avg_tail.txt)
 def allreduce_mean_(t: torch.Tensor, group=None, async_op=False):
     if not is_dist() or dist.get_world_size(group) == 1:
         return None

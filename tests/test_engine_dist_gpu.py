@@ -120,7 +120,7 @@ def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
     # parameters with a ~0 true gradient, e.g. the key bias, get noise-driven Adam steps -- and such an
     # element may legitimately end exactly where it started in one run and not the other: bf16 moments
     # measured one wte element the reference moved by 2.4e-6 in total (vs ~3.7e-3 for the tensor) left at
-    # its initial value, scripts/diag/z3_stale.py.  "Moved" therefore means moved by more than 1e-5.)
+    # its initial value, scripts/probes/z3_stale.py.  "Moved" therefore means moved by more than 1e-5.)
     init_out = str(tmp_path / "init.safetensors")
     _single("gpt2_full_finetune", [x for x in FULL if x not in ("--steps", "6")] + ["--steps", "0", "--output_path",
                                                                                        init_out], "--batch_size", 8)

@@ -37,7 +37,7 @@ def test_gpt2_gpu_matches_cpu_reference():
     lg = gpu(ids[:, :-1].to(DEV), ids[:, 1:].to(DEV))
     lc.backward()
     lg.backward()
-    # tolerances sized from measurements (scripts/diag/tiny_parity_errors.py, 4 seeds on MI355X:
+    # tolerances sized from measurements (scripts/probes/tiny_parity_errors.py, 4 seeds on MI355X:
     # loss |d| 6-9e-5, LoRA grad rel-L2 1.02-1.21e-2) with ~2x margin
     assert abs(lc.item() - lg.item()) < 1e-3
     gc, gg = fc.grad, fg.grad.cpu()
