@@ -577,6 +577,36 @@ void gemm4_seg2(Tensor A, Tensor B, Tensor A2, Tensor B2, Tensor out, int64_t im
   else mft::gemm4x(a, mft::GEMM_EPI_NONE, false, false, stream());
 }
 
+// The Gemma-3 GeGLU epilogues of gemm4 (kernels.h GEMM_EPI_GEGLU_*).  fwd: out = gu = A B^T [M, 2I] (B = [Wg; Wu]),
+// aux [M, >= I] <- h = gelu(g) u.  bwd: the accumulator dh = A B^T (+ A2 B2^T) [M, I] (B [I, K]) is never stored:
+// out [M, 2I] <- d gu from dh and aux = gu [M, 2I].
+void gemm4_geglu(Tensor A, Tensor B, Tensor aux, Tensor out, int64_t I, bool fwd, c10::optional<Tensor> A2,
+                 c10::optional<Tensor> B2) {
+  CHECK_CUDA(A); CHECK_BF16(A); CHECK_BF16(B); CHECK_BF16(aux); CHECK_BF16(out);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 && aux.stride(1) == 1 && out.stride(1) == 1,
+              "gemm4_geglu: row-contiguous 2-D operands");
+  const int M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && out.size(0) == M && out.size(1) == 2 * I && aux.size(0) == M &&
+                  (fwd ? N == 2 * I && aux.size(1) >= I : N == I && aux.size(1) == 2 * I) &&
+                  mft::gemm4_supported(M, N, K, false, false) && I % 128 == 0,
+              "gemm4_geglu: shapes");
+  c10::DeviceGuard g(A.device());
+  mft::GemmArgs a{};
+  a.A = bp(A); a.lda = A.stride(0);
+  a.B = bp(B); a.ldb = B.stride(0);
+  a.C = out.data_ptr(); a.ldc = out.stride(0);
+  a.aux = bp(aux); a.ldaux = aux.stride(0);
+  a.M = M; a.N = N; a.K = K; a.alpha = 1.f; a.geglu_I = (int)I;
+  if (A2.has_value()) {
+    TORCH_CHECK(!fwd && B2.has_value() && A2->size(0) == M && B2->size(0) == N && A2->size(1) == B2->size(1) &&
+                    A2->size(1) % 64 == 0, "gemm4_geglu: second K segment");
+    a.A2 = bp(*A2); a.lda2 = A2->stride(0);
+    a.B2 = bp(*B2); a.ldb2 = B2->stride(0);
+    a.K2 = A2->size(1);
+  }
+  mft::gemm4x(a, fwd ? mft::GEMM_EPI_GEGLU_FWD : mft::GEMM_EPI_GEGLU_BWD, false, false, stream());
+}
+
 std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, c10::optional<Tensor> bias,
                            c10::optional<Tensor> aux, double alpha, c10::optional<Tensor> out,
                            c10::optional<Tensor> lora_u, c10::optional<Tensor> lora_w, int64_t impl) {
@@ -711,6 +741,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("lora_dy", &lora_dy);
   m.def("gemm4_seg2", &gemm4_seg2, "out = A B^T + A2 B2^T on gemm4 (impl 4) or gemm_s (impl 5): second K segment",
         py::arg("A"), py::arg("B"), py::arg("A2"), py::arg("B2"), py::arg("out"), py::arg("impl") = 4);
+  m.def("gemm4_geglu", &gemm4_geglu, "the GeGLU MLP epilogues of gemm4 (gate|up -> gu + h; down dgrad -> d gu)",
+        py::arg("A"), py::arg("B"), py::arg("aux"), py::arg("out"), py::arg("I"), py::arg("fwd"),
+        py::arg("A2") = py::none(), py::arg("B2") = py::none());
   m.def("gemm_t", &gemm_t, py::arg("A"), py::arg("B"), py::arg("a_t"), py::arg("b_t"), py::arg("epi"),
         py::arg("bias") = py::none(), py::arg("aux") = py::none(), py::arg("alpha") = 1.0, py::arg("out") = py::none(),
         py::arg("lora_u") = py::none(), py::arg("lora_w") = py::none(), py::arg("impl") = 0);

@@ -204,6 +204,57 @@ void gemm_nt_seg2(const Tensor& a, const Tensor& b, const Tensor& a2, const Tens
   ::mft::gemm4x(g, ::mft::GEMM_EPI_NONE, false, false, current_stream());
 }
 
+bool geglu_fusable(long M, long I, long K, long Kd) {
+  static const bool off = std::getenv("MFT_GEGLU_FUSE") && std::getenv("MFT_GEGLU_FUSE")[0] == '0';
+  return !off && gemm4_on() && I % 128 == 0 && K % 64 == 0 && Kd % 64 == 0 &&
+         ::mft::gemm4_supported((int)M, (int)(2 * I), (int)K, false, false) &&
+         ::mft::gemm4_supported((int)M, (int)I, (int)Kd, false, false) && !short_tokens(M, 2 * I, K, ::mft::GEMM_EPI_NONE) &&
+         !short_tokens(M, I, Kd, ::mft::GEMM_EPI_NONE);
+}
+
+void gemm_geglu_fwd(const Tensor& x2, const Tensor& w, Tensor& gu, Tensor& h) {
+  const long M = x2.size(0), K = x2.size(1), I2 = w.size(0), I = I2 / 2;
+  MFT_CHECK(rowmajor2(x2) && rowmajor2(w) && rowmajor2(gu) && rowmajor2(h) && x2.dtype() == DType::BF16 &&
+                w.dtype() == DType::BF16 && gu.dtype() == DType::BF16 && h.dtype() == DType::BF16 && w.size(1) == K &&
+                gu.size(0) == M && gu.size(1) == I2 && h.size(0) == M && h.size(1) >= I && geglu_fusable(M, I, K, K) &&
+                x2.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && gu.stride(0) % 8 == 0 && h.stride(0) % 8 == 0,
+            "gemm_geglu_fwd: shapes / strides ", x2.str(), " ", w.str(), " -> ", gu.str(), " + ", h.str());
+  ::mft::GemmArgs g = args_for(x2, w, gu);
+  g.M = (int)M, g.N = (int)I2, g.K = (int)K;
+  g.aux = (::mft::bf16_t*)h.data_ptr();
+  g.ldaux = h.stride(0);
+  g.geglu_I = (int)I;
+  map_line("gate|up + GeGLU (h) epilogue", M, I2, K, "gemm4");
+  ::mft::gemm4x(g, ::mft::GEMM_EPI_GEGLU_FWD, false, false, current_stream());
+}
+
+void gemm_geglu_bwd(const Tensor& dy2, const Tensor& wt, const Tensor& gu, Tensor& dgu, const Tensor& a2, const Tensor& b2) {
+  const long M = dy2.size(0), K = dy2.size(1), I = wt.size(0);
+  MFT_CHECK(rowmajor2(dy2) && rowmajor2(wt) && rowmajor2(gu) && rowmajor2(dgu) && dy2.dtype() == DType::BF16 &&
+                wt.dtype() == DType::BF16 && wt.size(1) == K && gu.size(0) == M && gu.size(1) == 2 * I &&
+                dgu.size(0) == M && dgu.size(1) == 2 * I && dy2.stride(0) % 8 == 0 && wt.stride(0) % 8 == 0 &&
+                gu.stride(0) % 8 == 0 && dgu.stride(0) % 8 == 0,
+            "gemm_geglu_bwd: shapes / strides ", dy2.str(), " ", wt.str(), " ", gu.str(), " -> ", dgu.str());
+  ::mft::GemmArgs g = args_for(dy2, wt, dgu);
+  g.M = (int)M, g.N = (int)I, g.K = (int)K;
+  g.aux = (::mft::bf16_t*)gu.data_ptr();
+  g.ldaux = gu.stride(0);
+  g.geglu_I = (int)I;
+  if (a2.defined()) {
+    MFT_CHECK(rowmajor2(a2) && rowmajor2(b2) && a2.size(0) == M && b2.size(0) == I && a2.size(1) == b2.size(1) &&
+                  a2.size(1) % 64 == 0 && a2.stride(0) % 8 == 0 && b2.stride(0) % 8 == 0,
+              "gemm_geglu_bwd: second K segment ", a2.str(), " ", b2.str());
+    g.A2 = (const ::mft::bf16_t*)a2.data_ptr();
+    g.lda2 = a2.stride(0);
+    g.B2 = (const ::mft::bf16_t*)b2.data_ptr();
+    g.ldb2 = b2.stride(0);
+    g.K2 = (int)a2.size(1);
+  }
+  map_line(a2.defined() ? "down dgrad + LoRA segment + GeGLU backward epilogue" : "down dgrad + GeGLU backward epilogue", M,
+           I, K, "gemm4");
+  ::mft::gemm4x(g, ::mft::GEMM_EPI_GEGLU_BWD, false, false, current_stream());
+}
+
 void gemm_nt(const Tensor& x2, const Tensor& w, const Tensor& bias, Tensor& y, const Tensor& resid) {
   MFT_CHECK(rowmajor2(x2) && rowmajor2(w) && rowmajor2(y) && x2.dtype() == DType::BF16 && w.dtype() == DType::BF16,
             "gemm_nt: bf16 row-major");

@@ -34,6 +34,16 @@ void gemm8_call(const Tensor& a, const Tensor& b, bool b_kn, int epi, Tensor& c,
 // LoRA data gradient dx = dy W + v A with v zero-padded to 64 columns; lora_seg2_ok: the shape runs there
 void gemm_nt_seg2(const Tensor& a, const Tensor& b, const Tensor& a2, const Tensor& b2, Tensor& c);
 bool lora_seg2_ok(long M, long N, long K);
+// Gemma-3 GeGLU MLP in the gemm4 epilogues (kernels.h GEMM_EPI_GEGLU_*), replacing the gated_fwd /
+// gated_bwd passes.  geglu_fusable: gemm4 (not the short-token kernel) runs both the gate|up product
+// (M x 2I x K) and the down data gradient (M x I x Kd), I % 128 == 0 (MFT_GEGLU_FUSE=0: off, A/B)
+bool geglu_fusable(long M, long I, long K, long Kd);
+// gu = x w^T [M, 2I] (w = [W_gate; W_up] rows) and h[:, :I] = gelu(g) u (h row stride >= I, its tail untouched)
+void gemm_geglu_fwd(const Tensor& x2, const Tensor& w, Tensor& gu, Tensor& h);
+// dh = dy wt^T (+ a2 b2^T: the LoRA data gradient's second K segment) feeds the epilogue only:
+// dgu [M, 2I] = (dh u gelu'(g) | dh gelu(g)) from gu
+void gemm_geglu_bwd(const Tensor& dy2, const Tensor& wt, const Tensor& gu, Tensor& dgu, const Tensor& a2 = Tensor(),
+                    const Tensor& b2 = Tensor());
 // generic (fp32 or bf16, any transposes) C = alpha op(A) op(B) + beta C (gemm4 / gemm8 / SIMT fallback)
 void blas_gemm(const Tensor& a, bool ta, const Tensor& b, bool tb, Tensor& c, float alpha = 1.f, float beta = 0.f);
 bool gemm8_all();

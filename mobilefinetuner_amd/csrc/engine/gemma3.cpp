@@ -11,6 +11,7 @@
 #include <tuple>
 
 #include "engine/autograd.h"
+#include "engine/gemm.h"
 #include "engine/ops.h"
 #include "kernels.h"
 #include "runtime/json.h"
@@ -469,10 +470,12 @@ std::pair<Tensor, Tensor> Gemma3::layer(int i, const Tensor& x0, const Tensor& h
   auto aug = [&](std::vector<LoraAdapter>& ads, int in) { return (ads.empty() || st) ? 0 : lora_aug_cols(in, ads); };
   // the fused A stack when the producing RMSNorm computes u = y A^T itself (no dropout, sum r <= 32)
   auto fused_a = [&](std::vector<LoraAdapter>& ads) { return (ads.empty() || st) ? Tensor() : lora_fused_a(ads, training); };
-  auto proj = [&](const Tensor& x, int K, Param& w, std::vector<LoraAdapter>& ads, Tensor& waug, bool u_ready) {
-    if (ads.empty()) return linear_p(x, w, nullptr);
+  // (geglu_h / geglu_gu: the GeGLU MLP fused into the gate|up and down GEMM epilogues, nn.h linear_p)
+  auto proj = [&](const Tensor& x, int K, Param& w, std::vector<LoraAdapter>& ads, Tensor& waug, bool u_ready,
+                  Tensor* geglu_h = nullptr, const Tensor& geglu_gu = Tensor()) {
+    if (ads.empty()) return linear_p(x, w, nullptr, geglu_h, geglu_gu);
     if (st) return lora_linear(x, w, nullptr, ads, s, training, dropout_ctr);
-    return lora_linear_aug(x, K, w, nullptr, ads, s, waug, training, dropout_ctr, u_ready);
+    return lora_linear_aug(x, K, w, nullptr, ads, s, waug, training, dropout_ctr, u_ready, Tensor(), geglu_h, geglu_gu);
   };
   auto& L = layers_[i];
   const auto cs = rope(L.sliding, (int)S);
@@ -498,10 +501,22 @@ std::pair<Tensor, Tensor> Gemma3::layer(int i, const Tensor& x0, const Tensor& h
   const Tensor agu = fused_a(active(L.lgu));
   auto r = add_norm(x, a, L.pre_ff_norm, nullptr, eps, true, 1.f, aug(active(L.lgu), H), agu);
   x = r.first;
-  // GeGLU MLP
-  Tensor gu = proj(r.second, H, L.gu_w, active(L.lgu), L.waug_gu, agu.defined());
-  Tensor g = gated_act(gu, cfg_.act, aug(active(L.ldown), I));
-  Tensor f = proj(g, I, L.down_w, active(L.ldown), L.waug_down, false);
+  // GeGLU MLP: h = gelu(g) u comes out of the gate|up GEMM's epilogue and d gu out of the down data
+  // gradient's (no gated_fwd / gated_bwd pass over [M, 2I]); else the gated_act kernels
+  const int64_t M = B * S;
+  const int hc = std::max(I, aug(active(L.ldown), I));  // h with the down adapter's augmented columns
+  const int64_t Kgu = active(L.lgu).empty() || st ? H : aug(active(L.lgu), H);
+  Tensor f;
+  if (!st && cfg_.act == 0 && geglu_fusable(M, I, Kgu, H)) {
+    Tensor hbuf = empty({M, (int64_t)hc}, DType::BF16, x.device());
+    if (hc > I) ::mft::zero_cols((::mft::bf16_t*)hbuf.data_ptr(), hc, M, I, hc - I, current_stream());
+    Tensor gu = proj(r.second, H, L.gu_w, active(L.lgu), L.waug_gu, agu.defined(), &hbuf);
+    f = proj(hbuf, I, L.down_w, active(L.ldown), L.waug_down, false, nullptr, gu);
+  } else {
+    Tensor gu = proj(r.second, H, L.gu_w, active(L.lgu), L.waug_gu, agu.defined());
+    Tensor g = gated_act(gu, cfg_.act, aug(active(L.ldown), I));
+    f = proj(g, I, L.down_w, active(L.ldown), L.waug_down, false);
+  }
   f = add_norm(f, Tensor(), L.post_ff_norm, nullptr, eps, true, 1.f, 0).second;
   if (!capture_layers.empty() && std::find(capture_layers.begin(), capture_layers.end(), i) != capture_layers.end()) {
     NoGradGuard ng;

@@ -509,30 +509,57 @@ static void bias_grad(Param* b, const Tensor& dy2) {
   ::mft::reduce_rows(fp(part), fp(buf), nb, N, 1, S());
 }
 
-Tensor linear_p(const Tensor& x, Param& w, Param* b) {
+// the GeGLU backward outside a fused epilogue: d gu from dh (any producer) and gu
+static Tensor geglu_bwd_unfused(const Tensor& dh, const Tensor& gu2) {
+  Tensor dy = dh;
+  if (dy.stride(1) != 1 || dy.stride(0) % 8) dy = dy.contiguous();
+  const int64_t M = gu2.size(0), I = gu2.size(1) / 2;
+  Tensor dgu = empty({M, 2 * I}, DType::BF16, dh.device());
+  ::mft::gated_bwd(bp(gu2), bp(dy), dy.stride(0), bp(dgu), M, (int)I, 0, S());
+  return dgu;
+}
+
+Tensor linear_p(const Tensor& x, Param& w, Param* b, Tensor* geglu_h, const Tensor& geglu_gu) {
   const int64_t K = x.size(-1), N = w.c.size(0);
   Tensor x2 = x.detach().reshape({-1, K});
   if (x2.stride(1) != 1 || x2.stride(0) % 8) x2 = x2.contiguous();
   Shape ys = x.shape();
   ys.back() = N;
   Tensor y = empty({x2.size(0), N}, DType::BF16, x.device());
-  gemm_nt(x2, w.c, b ? b->c : Tensor(), y);
-  if (any_needs_grad({x, w.leaf, b ? b->leaf : Tensor()})) {
+  if (geglu_h) {
+    MFT_CHECK(!b, "linear_p: the GeGLU epilogue takes no bias");
+    gemm_geglu_fwd(x2, w.c, y, *geglu_h);
+  } else {
+    gemm_nt(x2, w.c, b ? b->c : Tensor(), y);
+  }
+  const bool gg = geglu_gu.defined();
+  const Tensor xin = gg ? geglu_gu : x;  // the GeGLU-fused down projection's input edge is gu
+  if (any_needs_grad({xin, w.leaf, b ? b->leaf : Tensor()})) {
     Param* pw = &w;
-    auto n = lambda_node("LinearBackward", [x2, pw, b, K, N](std::vector<Tensor>& g) {
+    const Tensor gu2 = gg ? geglu_gu.detach().reshape({-1, geglu_gu.size(-1)}) : Tensor();
+    const Shape gshape = gg ? geglu_gu.shape() : Shape{};
+    auto n = lambda_node("LinearBackward", [x2, pw, b, K, N, gu2, gshape, gg](std::vector<Tensor>& g) {
       if (!g[0].defined()) return std::vector<Tensor>{Tensor(), Tensor(), Tensor()};
       Tensor dy2 = g[0].reshape({-1, N});
       if (dy2.stride(1) != 1 || dy2.stride(0) % 8) dy2 = dy2.contiguous();
-      Tensor dx = empty({dy2.size(0), K}, DType::BF16, dy2.device());
-      gemm_nn(dy2, pw->c, dx, !pw->trainable() && !pw->streamed ? pw->transposed() : Tensor());
+      Tensor dx;
+      const Tensor wt = !pw->trainable() && !pw->streamed ? pw->transposed() : Tensor();
+      if (gg && wt.defined() && geglu_fusable(dy2.size(0), gu2.size(1) / 2, N, N)) {
+        dx = empty({dy2.size(0), gu2.size(1)}, DType::BF16, dy2.device());
+        gemm_geglu_bwd(dy2, wt.slice(0, 0, gu2.size(1) / 2), gu2, dx);
+      } else {
+        dx = empty({dy2.size(0), K}, DType::BF16, dy2.device());
+        gemm_nn(dy2, pw->c, dx, wt);
+        if (gg) dx = geglu_bwd_unfused(dx.slice(1, 0, gu2.size(1) / 2), gu2);
+      }
       if (pw->trainable()) {
         Tensor buf = grad_buffer(pw->leaf).view({N, K});
         gemm_wgrad(buf, dy2, x2);
       }
       bias_grad(b, dy2);
-      return std::vector<Tensor>{dx, Tensor(), Tensor()};
+      return std::vector<Tensor>{gg ? dx.view(gshape) : dx, Tensor(), Tensor()};
     });
-    connect(n, {x, w.leaf, b ? b->leaf : Tensor()}, {y});
+    connect(n, {xin, w.leaf, b ? b->leaf : Tensor()}, {y});
   }
   return y.view(ys);
 }
@@ -716,7 +743,8 @@ Tensor lora_fused_a(const std::vector<LoraAdapter>& ads, bool training) {
 }
 
 Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<LoraAdapter>& ads, float s,
-                       Tensor& waug, bool training, const Tensor& drop_ctr, bool u_ready, const Tensor& resid) {
+                       Tensor& waug, bool training, const Tensor& drop_ctr, bool u_ready, const Tensor& resid,
+                       Tensor* geglu_h, const Tensor& geglu_gu) {
   MFT_CHECK(!w.trainable(), "lora_linear_aug: the base weight must be frozen");
   const int64_t Ka = xa.size(-1), N = w.c.size(0);
   Tensor xa2 = xa.detach().reshape({-1, Ka});
@@ -766,10 +794,16 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
   Tensor y = empty({M, N}, DType::BF16, xa.device());
   // resid: y = resid + LoRA-linear(x) straight from the GEMM's epilogue (the block's residual add)
   const Tensor r2 = resid.defined() ? resid.detach().reshape({M, N}).contiguous() : Tensor();
-  gemm_nt(xa2, waug, b ? b->c : Tensor(), y, r2);
+  if (geglu_h) {  // y = gu, and h = gelu(g) u from the same epilogue
+    MFT_CHECK(!b && !resid.defined(), "lora_linear_aug: the GeGLU epilogue takes no bias / residual");
+    gemm_geglu_fwd(xa2, waug, y, *geglu_h);
+  } else {
+    gemm_nt(xa2, waug, b ? b->c : Tensor(), y, r2);
+  }
   Shape ys = xa.shape();
   ys.back() = N;
-  std::vector<Tensor> ins{xa};
+  const bool gg = geglu_gu.defined();  // (the GeGLU-fused down projection: its input edge is gu)
+  std::vector<Tensor> ins{gg ? geglu_gu : xa};
   for (auto& a : ads) {
     ins.push_back(a.A.leaf);
     ins.push_back(a.B.leaf);
@@ -780,9 +814,10 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
     Param* pw = &w;
     std::vector<LoraAdapter>* pads = &ads;
     Tensor wa = waug;
-    Shape xshape = xa.shape();
+    Shape xshape = gg ? geglu_gu.shape() : xa.shape();
+    const Tensor gu2 = gg ? geglu_gu.detach().reshape({-1, geglu_gu.size(-1)}) : Tensor();
     auto n = lambda_node("LoRALinearBackward", [xa2, xshape, K, Ka, M, N, pw, pads, s, wa, training, drop_ctr, acat_f = acat,
-                                                 nin = ins.size(), has_resid](std::vector<Tensor>& g) {
+                                                 nin = ins.size(), has_resid, gu2, gg](std::vector<Tensor>& g) {
       std::vector<Tensor> out(nin);
       if (!g[0].defined()) return out;
       if (has_resid) out[nin - 1] = g[0];
@@ -797,11 +832,15 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         nodrop = nodrop && (a.dropout <= 0.f || !training);
       }
       const bool fused = nodrop && rt > 0 && rt <= 32 && rt % 8 == 0 && N % 64 == 0 && K % 8 == 0;
-      Tensor dxa = empty({M, Ka}, DType::BF16, dy2.device());
-      Tensor dx = dxa.slice(1, 0, K);
+      Tensor dxa = empty({M, gg ? gu2.size(1) : Ka}, DType::BF16, dy2.device());
+      Tensor dx = gg ? Tensor() : dxa.slice(1, 0, K);
+      // GeGLU-fused down projection: the seg2 GEMM's epilogue writes d gu into dxa; other data-gradient
+      // paths compute dh first, then the unfused GeGLU backward
+      const bool geglu_epi = gg && geglu_fusable(M, K, N, N);
       // gemm4 form of the fused data gradient: v (= s dy B) in the first rt of 64 columns, the rest zero, read
       // as a second K segment against A^T (dx = dy W + v A in one pass, gemm_nt_seg2)
-      const bool seg2 = fused && gemm4_on() && Ka % 8 == 0 && lora_seg2_ok(M, K, N);
+      const bool seg2 = (fused && gemm4_on() && Ka % 8 == 0 && lora_seg2_ok(M, K, N)) || (geglu_epi && fused);
+      if (gg && !(geglu_epi && seg2)) dx = empty({M, (int64_t)K}, DType::BF16, dy2.device());
       Tensor vall = empty({M, seg2 ? (int64_t)64 : (int64_t)std::max(rt, 8)}, DType::BF16, dy2.device());
       bool v_padded = false;  // lora_dy zeroes the padding itself (one adapter of rank 8)
       int o = 0;
@@ -873,7 +912,8 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
           prep_copy(at.slice(1, oc, oc + a.rank), a.A.c.t(), 1.f);
           oc += a.rank;
         }
-        gemm_nt_seg2(dy2, pw->transposed(), vall, at, dx);
+        if (geglu_epi) gemm_geglu_bwd(dy2, pw->transposed(), gu2, dxa, vall, at);
+        else gemm_nt_seg2(dy2, pw->transposed(), vall, at, dx);
       } else if (fused) {
         Gemm8Extra ex;
         Tensor vu = vall.slice(1, 0, rt);
@@ -928,6 +968,7 @@ Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<
         o += a.rank;
         off += a.rank;
       }
+      if (gg && !(geglu_epi && seg2)) dxa = geglu_bwd_unfused(dx, gu2);
       out[0] = dxa.view(xshape);
       return out;
     });

@@ -63,8 +63,13 @@ Tensor qknorm_rope_attention(const Tensor& qkv, int nq, int nkv, Param& wq, Para
 // gated MLP activation on gu = [gate | up] [M, 2I]: act(gate) * up (act 0 GELU-tanh = GeGLU, 1 SiLU);
 // [M, out_cols] with zeroed tail when out_cols > I (augmented-K input of a LoRA consumer)
 Tensor gated_act(const Tensor& gu, int act, int out_cols);
-// y = x W^T + b on bf16 [M, K] rows (trainable or frozen W)
-Tensor linear_p(const Tensor& x, Param& w, Param* b);
+// y = x W^T + b on bf16 [M, K] rows (trainable or frozen W).
+// GeGLU MLP fusion (Gemma-3, gemm.h geglu_fusable):
+//   geglu_h (gate|up projection): y = gu [M, 2I]; *geglu_h [M, >= I] also receives h = gelu(g) u from the
+//     GEMM's epilogue (its columns past I are the caller's) -- no autograd edge of its own;
+//   geglu_gu (down projection): x is that h buffer, the node's input is gu instead, and the backward's data
+//     gradient GEMM writes d gu straight from its epilogue (the GeGLU backward; dh is never stored)
+Tensor linear_p(const Tensor& x, Param& w, Param* b, Tensor* geglu_h = nullptr, const Tensor& geglu_gu = Tensor());
 
 struct LoraAdapter {
   int col0 = 0, ncols = 0, rank = 8;
@@ -90,9 +95,10 @@ int lora_aug_cols(int in_features, const std::vector<LoraAdapter>& ads);
 // lora_fused_a(ads)); the adapters' A must not change between that producer and this call.
 // resid (optional, [..., N]): the returned tensor is resid + the LoRA linear, added in the GEMM's epilogue
 // (needs a bias); its gradient is the output's
+// geglu_h / geglu_gu: the GeGLU fusion of linear_p, on the augmented-K LoRA projection
 Tensor lora_linear_aug(const Tensor& xa, int K, Param& w, Param* b, std::vector<LoraAdapter>& ads, float scale,
                        Tensor& waug, bool training, const Tensor& drop_ctr, bool u_ready = false,
-                       const Tensor& resid = Tensor());
+                       const Tensor& resid = Tensor(), Tensor* geglu_h = nullptr, const Tensor& geglu_gu = Tensor());
 // the [sum r_i, in] stack of the adapters' A (bf16 compute copies) when a producer can compute u for
 // lora_linear_aug itself (no dropout in effect, sum r <= 32); undefined otherwise
 Tensor lora_fused_a(const std::vector<LoraAdapter>& ads, bool training);

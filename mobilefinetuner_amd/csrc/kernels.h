@@ -73,7 +73,13 @@ enum GemmEpi { GEMM_EPI_NONE = 0, GEMM_EPI_BIAS = 1, GEMM_EPI_BIAS_GELU = 2, GEM
                GEMM_EPI_BIAS_GELU_D = 9, GEMM_EPI_MUL_AUX = 10,
                // residual-producing projection (gemm8 only): C = alpha A.B + bias + aux (aux = the
                // residual stream [M, N]), i.e. the transformer's residual add in the GEMM's epilogue
-               GEMM_EPI_BIAS_ADD = 11 };
+               GEMM_EPI_BIAS_ADD = 11,
+               // Gemma-3 GeGLU MLP in the GEMM epilogues (gemm4 only; geglu_I = I, I % 128 == 0):
+               // GEGLU_FWD -- C = gu = x [Wg; Wu]^T [M, 2I] and aux = h = gelu(g) u [M, I] (row stride
+               // ldaux), the B rows of each 256-column tile are 128 gate rows + the matching 128 up rows;
+               // GEGLU_BWD -- the accumulator is dh [M, I] (N = I); aux = gu [M, 2I] (read), C = dgu
+               // [M, 2I] (ldc): dg = dh u gelu'(g), du = dh gelu(g)
+               GEMM_EPI_GEGLU_FWD = 12, GEMM_EPI_GEGLU_BWD = 13 };
 struct GemmArgs {
   const bf16_t* A;
   long lda;  // A [M, K] row-major
@@ -126,6 +132,8 @@ struct GemmArgs {
   int K2;
   // gemm4 epilogue operand (aux) loads: 0 = non-temporal (default), 1 = default cache policy (A/B)
   int aux_pol;
+  // GEGLU_FWD / GEGLU_BWD: the MLP width I (gate | up halves of gu)
+  int geglu_I;
   // gemm_s split-K hand-off: 1 = agent-scope release / acquire fences around the arrival counter
   // (MFT_STRICT_HANDOFF=1); 0 = the sc1-store / sc1-load form alone (see gemm_s.hip)
   int handoff_fence;

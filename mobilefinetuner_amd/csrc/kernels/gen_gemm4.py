@@ -294,7 +294,7 @@ def main():
             f.write(f"// {name}: {kw}\n")
             f.write(emit("GEMM4_KTILE_" + name, lines))
             f.write("\n")
-        for S in (32, 40, 64):  # stores per wave of the previous tile's epilogue: 32 / CE_FWD 40 / 2 outputs 64
+        for S in (32, 40, 48, 64):  # stores per wave of the previous tile's epilogue: 32 / CE_FWD 40 / GEGLU_FWD 48 / 2 outputs 64
             lines = ktile_v2_modes(vm_extra=S)
             assert sum(1 for l in lines if l.startswith("v_mfma")) == 192
             n_dma = sum(1 for l in lines if l.startswith("buffer_load"))
@@ -305,7 +305,7 @@ def main():
             f.write(emit_explicit(f"GEMM4_KTILE_V2_X{S}", lines))
             f.write("\n")
 
-            if S == 40:
+            if S in (40, 48):
                 continue
             assert sum(1 for l in lines if l.startswith("v_mfma")) == 192
             f.write(f"// NT_P{S}: persistent K-tile, mode-branching (previous tile's epilogue: {S} stores per wave)\n")

@@ -124,3 +124,45 @@ def test_gemm_s_split_k_deterministic_and_rearmed():
     torch.cuda.synchronize()
     assert all(torch.equal(ys[0], y) for y in ys[1:])
     assert _rel(ys[0], (x.float() @ w.float().t()) * aux.float()) < 2e-2
+
+
+@pytest.mark.parametrize("M,I,K", [(4096, 2048, 704), (1000, 256, 640), (300, 384, 1152)])
+def test_gemm4_geglu_epilogues_match_fp32(M, I, K):
+    """The Gemma-3 GeGLU MLP in gemm4's epilogues against fp32 torch on the same bf16 operands:
+    forward -- gu = x [Wg; Wu]^T and h = gelu(g) u (h into a wider, row-strided buffer whose tail stays
+    untouched); backward -- dh = dy Wd (plus a LoRA-style second K segment) never stored, d gu = (dh u
+    gelu'(g) | dh gelu(g)).  Ragged M, the 1B width (I 6912 is not tested: same code, I % 128)."""
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).bfloat16()
+    w = ((torch.rand(2 * I, K, device="cuda", generator=g) * 2 - 1) * 0.08).bfloat16()
+    gu = torch.empty(M, 2 * I, device="cuda", dtype=torch.bfloat16)
+    hbuf = torch.full((M, I + 64), 5.0, device="cuda", dtype=torch.bfloat16)
+    C.gemm4_geglu(x, w, hbuf, gu, I, True)
+    torch.cuda.synchronize()
+    ref = x.float() @ w.float().t()
+    assert _rel(gu, ref) < 1e-2
+    gq, uq = gu[:, :I].float(), gu[:, I:].float()  # h is formed from the stored (bf16) gu, like gated_fwd
+    assert _rel(hbuf[:, :I], _gelu(gq)[0] * uq) < 2e-2
+    assert (hbuf[:, I:] == 5.0).all()
+    # backward (down projection H -> I data gradient), with and without the second K segment
+    H = 640
+    dy = (torch.rand(M, H, device="cuda", generator=g) * 2 - 1).bfloat16()
+    wt = ((torch.rand(I, H, device="cuda", generator=g) * 2 - 1) * 0.08).bfloat16()
+    a2 = torch.zeros(M, 64, device="cuda", dtype=torch.bfloat16)
+    a2[:, :8] = (torch.rand(M, 8, device="cuda", generator=g) - 0.5).bfloat16()
+    b2 = torch.zeros(I, 64, device="cuda", dtype=torch.bfloat16)
+    b2[:, :8] = (torch.rand(I, 8, device="cuda", generator=g) - 0.5).bfloat16()
+    for seg in (False, True):
+        dgu = torch.empty(M, 2 * I, device="cuda", dtype=torch.bfloat16)
+        if seg:
+            C.gemm4_geglu(dy, wt, gu, dgu, I, False, a2, b2)
+            dh = dy.float() @ wt.float().t() + a2.float() @ b2.float().t()
+        else:
+            C.gemm4_geglu(dy, wt, gu, dgu, I, False)
+            dh = dy.float() @ wt.float().t()
+        torch.cuda.synchronize()
+        a, ag = _gelu(gq)
+        assert _rel(dgu[:, :I], dh * uq * ag) < 2e-2, seg
+        assert _rel(dgu[:, I:], dh * a) < 2e-2, seg
