@@ -1,6 +1,8 @@
 // libmft engine: bucketed / overlapped data parallelism and ZeRO-1/2 (see dist.h).
 #include "engine/dist.h"
 
+#include <cstdio>
+
 #include <algorithm>
 #include <sstream>
 
@@ -136,6 +138,7 @@ void DataParallel::begin_micro(int i, int n) {
   if (i == 0) {
     pending_ = total_;
     std::fill(done_.begin(), done_.end(), 0);
+    hooked_ = 0;
   }
   last_micro_ = i == n - 1;
 }
@@ -143,7 +146,10 @@ void DataParallel::begin_micro(int i, int n) {
 void DataParallel::on_ready(int pi) {
   if (!last_micro_ || !cfg_.overlap) return;
   const int b = plan_.bucket_of[pi];
-  if (--pending_[b] == 0) launch(b);
+  if (--pending_[b] == 0) {
+    if (!done_[b]) ++hooked_;
+    launch(b);
+  }
 }
 
 void DataParallel::launch(int b) {
@@ -175,6 +181,11 @@ void DataParallel::launch(int b) {
 }
 
 void DataParallel::finish() {
+  if (!reported_) {  // overlap evidence (tests): how many reductions the backward itself started
+    reported_ = true;
+    std::printf("[dp] first step: %d of %zu bucket reduction(s) launched from the backward's grad-ready hooks\n",
+                hooked_, plan_.buckets.size());
+  }
   for (int b = 0; b < (int)plan_.buckets.size(); ++b) launch(b);
   HIP_OK(hipEventRecord(join_ev_, stream_));
   HIP_OK(hipStreamWaitEvent(current_stream(), join_ev_, 0));

@@ -133,6 +133,8 @@ class DataParallel : public GradReducer {
   std::vector<int> pending_, total_;
   std::vector<char> done_;
   bool last_micro_ = true;
+  int hooked_ = 0;          // buckets of this step launched from a grad-ready hook (inside the backward)
+  bool reported_ = false;   // the first step's overlap line printed
   Tensor comm_buf_;  // bf16 reduce staging [numel]
 };
 

@@ -339,3 +339,39 @@ def test_native_two_ranks_print_identical_gemm_choice_maps():
     assert maps[0] and maps[0] == maps[1], (maps[0][:20], maps[1][:20])
     assert not any("hipBLASLt" in l for l in maps[0]), maps[0][:20]
     assert any("gemm_s" in l or "gemm4" in l for l in maps[0]), maps[0][:20]
+
+
+@pytest.mark.parametrize("extra", [[], ["--zero_stage", "2"], ["--zero_stage", "3"]], ids=["ddp", "zero2", "zero3"])
+def test_native_dp_four_ranks_match_single_process(tmp_path, extra):
+    """4 loopback ranks x batch 2 == 1 process x batch 8 (GPT-2-tiny full fine-tune): per-step losses and final
+    weights, DDP / ZeRO-2 / ZeRO-3 -- so ZeRO-3 == DDP at 4 ranks too.  The bucketed reducers launch every
+    bucket's reduction from the backward's grad-ready hooks (overlapped), none from the post-backward sweep."""
+    from mobilefinetuner_amd.io import safetensors as st
+    ref_out = str(tmp_path / "ref.safetensors")
+    want = loss_list(_single("gpt2_full_finetune", FULL + ["--output_path", ref_out], "--batch_size", 8).stdout, True)
+    dp_out = str(tmp_path / "dp.safetensors")
+    res = _run_ranks([_bin("gpt2_full_finetune"), *FULL, "--batch_size", "2", "--output_path", dp_out, *extra], 4,
+                     timeout=300)
+    for rc, o, e in res:
+        assert rc == 0, o[-2000:] + e[-2000:]
+    out0 = res[0][1]
+    assert "data parallel: rank 0 of 4 (loopback" in out0, out0[:3000]
+    got = loss_list(out0, True)
+    assert len(got) == 6 and got == pytest.approx(want, rel=2e-4, abs=2e-4), (extra, got, want)
+    if "3" not in extra:
+        m = re.search(r"\[dp\] first step: (\d+) of (\d+) bucket", out0)
+        assert m and int(m.group(2)) > 1 and m.group(1) == m.group(2), out0[-3000:]
+    a, b = st.load_file(ref_out), st.load_file(dp_out)
+    for k in a:
+        assert torch.allclose(a[k], b[k], atol=1e-2, rtol=1e-2), (extra, k, (a[k] - b[k]).abs().max())
+
+
+def test_native_lora_bucket_launched_inside_backward():
+    """LoRA on GPT-2-tiny, 2 loopback ranks: the single fused bucket's all-reduce is issued by the grad-ready hook
+    of its last parameter -- before the backward ends -- not by the post-backward sweep."""
+    lora = ["--random_init", "--model", "gpt2-tiny", "--synthetic_data", "--synthetic_tokens", "100000", "--seq_len",
+            "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic", "--steps", "3", "--batch_size", "4"]
+    res = _run_ranks([_bin("gpt2_lora_finetune"), *lora], 2)
+    for rc, o, e in res:
+        assert rc == 0, o[-2000:] + e[-2000:]
+    assert "[dp] first step: 1 of 1 bucket" in res[0][1], res[0][1][-3000:]
