@@ -185,6 +185,15 @@ int main() {
           }
     check("matmul fp32 [3,17,40]x[40,24]", host(matmul(dev(a, {B, M, K}), dev(b, {K, N}))), r, 1e-5);
     check("matmul fp32 batched", host(matmul(dev(a, {B, M, K}), dev(b3, {B, K, N}))), r3, 1e-5);
+    {  // several 64 x 64 tiles and 19 K stages of the fp32-MFMA generic GEMM, ragged on every side
+      const int M2 = 130, K2 = 300, N2 = 77;
+      auto a2 = rnd(M2 * K2), b2 = rnd(K2 * N2);
+      std::vector<double> r2(M2 * N2, 0.0);
+      for (int m = 0; m < M2; ++m)
+        for (int n = 0; n < N2; ++n)
+          for (int k = 0; k < K2; ++k) r2[m * N2 + n] += a2[m * K2 + k] * b2[k * N2 + n];
+      check("matmul fp32 [130,300]x[300,77] (f32 MFMA)", host(matmul(dev(a2, {M2, K2}), dev(b2, {K2, N2}))), r2, 1e-5);
+    }
     // bf16 linear on the GEMM front (hipBLASLt / gemm8): x [256, 128] W [192, 128]
     const int LM = 256, LK = 128, LN = 192;
     auto x = rnd(LM * LK), w = rnd(LN * LK, -0.1, 0.1), bias = rnd(LN, -0.5, 0.5);

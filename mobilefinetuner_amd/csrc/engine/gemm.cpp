@@ -2,7 +2,7 @@
 // gemm4 (kernels/gemm4.hip, the 4-wave hand-scheduled persistent NT GEMM) for every K-contiguous
 // product and fused epilogue it carries, gemm8 (kernels/gemm8.hip) for the token-major layouts (split-K
 // weight gradients, NN data gradients of trainable weights without a transposed copy, the LM-head CE
-// dgrad, the LoRA epilogue), and the SIMT fallback (kernels/gemm_simt.hip) for operands neither takes
+// dgrad, the LoRA epilogue), and the fp32-MFMA generic fallback (kernels/gemm_simt.hip) for operands neither takes
 // (fp32, K % 64 != 0, unaligned strides).  No vendor GEMM library is linked.
 #include "engine/gemm.h"
 

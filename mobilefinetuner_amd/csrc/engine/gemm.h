@@ -7,7 +7,8 @@
 //     transposed weight: gemm4 (csrc/kernels/gemm4.hip, 4-wave hand-scheduled persistent kernel);
 //   * token-major layouts -- split-K TN weight gradients, NN data gradients, the CE dgrad, the LoRA
 //     epilogue: gemm8 (csrc/kernels/gemm8.hip, 8-phase pipeline, ds_read_b64_tr_b16);
-//   * anything else (fp32, K % 64 != 0, unaligned strides): the SIMT fallback (kernels/gemm_simt.hip).
+//   * anything else (fp32, K % 64 != 0, unaligned strides): the generic fallback (kernels/gemm_simt.hip),
+//     fp32 MFMA (v_mfma_f32_16x16x4_f32: exact fp32, the native --dtype fp32 mode runs on it).
 #pragma once
 #include "engine/tensor.h"
 

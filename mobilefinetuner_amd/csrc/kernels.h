@@ -159,7 +159,7 @@ int gemm8_pick_ksplit(int M, int N, int K);
 // MFT_GEMM8_STREAM=1); A/B switch for benchmarks
 void gemm8_set_stream(int on);
 void gemm8_set_stagger(int cycles);  // first-round stagger (cycles per XCD slot), A/B
-// generic SIMT fallback (gemm_simt.hip): D = alpha op(A) op(B) (+ bias[N]) + beta Cin; fp32 or bf16
+// generic fallback (gemm_simt.hip, fp32 MFMA v_mfma_f32_16x16x4_f32): D = alpha op(A) op(B) (+ bias[N]) + beta Cin; fp32 or bf16
 // operands (x_f32 flags), fp32 accumulation; ta: A stored [K, M]; tb: B stored [N, K]
 struct SimtGemmArgs {
   const void* A;

@@ -37,8 +37,9 @@ constexpr int kMaxSplit = 4;  // K-splits across workgroups (gemm_s split-K)
 constexpr int kNW = 4;    // waves per workgroup, each a 1/kNW share of the K-tiles (8 measured slower: 139 KB LDS, one WG per CU)
 
 
+template <int TM>  // output rows per tile: 64 (4 row blocks) or 32 (2)
 struct Frags {
-  bf16x8_t a[2][4], b[2][4];  // [k-step][block]
+  bf16x8_t a[2][TM / 16], b[2][4];  // [k-step][block]
 };
 
 // fragments of one K-tile (64 columns) through range-checked buffer descriptors: A rows m0 + 16 i + (l & 15),
@@ -47,44 +48,52 @@ struct Frags {
 // no clamp around any load, so the compiler keeps the next K-tile's loads in flight under the MFMAs.
 typedef int i32x4v __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void load_frags(Frags& f, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb,
+template <int TM>
+__device__ __forceinline__ void load_frags(Frags<TM>& f, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb,
                                            const uint32_t (&oa)[4], const uint32_t (&ob)[4], uint32_t soff) {
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
+  for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < TM / 16; ++i)
       f.a[ks][i] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(ra, oa[i] + 64 * ks, soff, 0));
-      f.b[ks][i] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(rb, ob[i] + 64 * ks, soff, 0));
-    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      f.b[ks][j] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(rb, ob[j] + 64 * ks, soff, 0));
+  }
 }
 
 // Builtin MFMAs (not asm): the compiler must see them to place the wait states between an MFMA still reading
 // its source VGPRs and the next write of those registers (with two waves per SIMD part of the fragments live
 // in AGPRs and are copied to VGPRs right before their MFMA -- an asm MFMA there read clobbered operands).
-__device__ __forceinline__ void mma(f32x4_t (&acc)[4][4], const Frags& f) {
+template <int TM>
+__device__ __forceinline__ void mma(f32x4_t (&acc)[TM / 16][4], const Frags<TM>& f) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM / 16; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(f.b[ks][j], f.a[ks][i], acc[i][j]);
 }
 
-template <int EPI, bool SEG2>
+// TM = 32 (short products with few 64-row tiles): twice the workgroups, and a 3-deep fragment ring -- the
+// 3 K-tiles of a K = 768 wave all in flight before its first MFMA (one memory latency, not two)
+template <int EPI, bool SEG2, int TM>
 __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g, int S, float* __restrict__ ws, int* __restrict__ cnt) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [kNW waves][64 rows][kLdr]
+  constexpr int RB = TM / 16;                // row blocks per tile
+  constexpr int kDepth = TM == 32 ? 3 : 2;   // K-tiles in flight per wave
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [kNW waves][TM rows][kLdr]
   __shared__ int last;
-  const int tiles_n = (g.N + 63) / 64, tiles = ((g.M + 63) / 64) * tiles_n;
+  const int tiles_n = (g.N + 63) / 64, tiles = ((g.M + TM - 1) / TM) * tiles_n;
   // block -> (tile t, split s): the S splits of a tile on one XCD (block ids congruent mod 8)
   const int bx = blockIdx.x & 7, bq = blockIdx.x >> 3, sp = bq % S, t = (bq / S) * 8 + bx;
   if (t >= tiles) return;
-  const int m0 = (t / tiles_n) * 64, n0 = (t % tiles_n) * 64;
+  const int m0 = (t / tiles_n) * TM, n0 = (t % tiles_n) * 64;
   const int w = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // (uniform: scalar loop)
   const int nk = g.K / 64, nkt = nk + (SEG2 ? g.K2 / 64 : 0);
   const int slot = sp * kNW + w, P = S * kNW;  // this wave's K-tiles: slot, slot + P, ...
-  f32x4_t acc[4][4];
+  f32x4_t acc[RB][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < RB; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
   // the wave's it-th K-tile is slot + P it; past its last one the loads are out of range (zeros: a multiply
@@ -112,7 +121,7 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g, int S, flo
   // (the SGPR offset is not range-checked -- only the VGPR offset is -- so a K-tile past the wave's last
   // reads through a 0-record descriptor, not through a large soffset; scalar selects of base and count,
   // the descriptor built per load: a select between descriptor values went through scratch)
-  auto load = [&](Frags& f, int it) {  // (selects only: a branch here would make the compiler wait early)
+  auto load = [&](Frags<TM>& f, int it) {  // (selects only: a branch here would make the compiler wait early)
     const int kt = slot + P * it;
     const bool ok = it < n_my && !g.stagger, s2 = SEG2 && kt >= nk;
     const uint32_t off = (uint32_t)(s2 ? kt - nk : min(kt, nk - 1)) * 128u;
@@ -133,28 +142,48 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g, int S, flo
   // (sched_barrier: the scheduler would otherwise sink each load next to its first use -- load, wait, MFMA;
   // a third K-tile in flight measured no faster and spilled: the product is bound by the MFMA time of
   // the ~100 busy CUs and the launch / reduction floor, not by the load chain)
-  Frags f0, f1;
-  load(f0, 0);
-  for (int it = 0; it < max(n_my, 1); it += 2) {  // (a wave without K-tiles multiplies zeros once: acc = 0)
-    load(f1, it + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(acc, f0);
-    __builtin_amdgcn_sched_barrier(0);
-    load(f0, it + 2);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(acc, f1);
-    __builtin_amdgcn_sched_barrier(0);
+  if constexpr (kDepth == 2) {
+    Frags<TM> f0, f1;
+    load(f0, 0);
+    for (int it = 0; it < max(n_my, 1); it += 2) {  // (a wave without K-tiles multiplies zeros once: acc = 0)
+      load(f1, it + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma<TM>(acc, f0);
+      __builtin_amdgcn_sched_barrier(0);
+      load(f0, it + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      mma<TM>(acc, f1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    Frags<TM> f0, f1, f2;
+    load(f0, 0);
+    load(f1, 1);
+    for (int it = 0; it < max(n_my, 1); it += 3) {
+      load(f2, it + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      mma<TM>(acc, f0);
+      __builtin_amdgcn_sched_barrier(0);
+      load(f0, it + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      mma<TM>(acc, f1);
+      __builtin_amdgcn_sched_barrier(0);
+      load(f1, it + 4);
+      __builtin_amdgcn_sched_barrier(0);
+      mma<TM>(acc, f2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   // partial tile of this wave -> LDS: lane holds row 16 i + (l & 15), columns 16 j + 4 (l >> 4) .. + 3
-  float* mine = red + w * 64 * kLdr;
+  float* mine = red + w * TM * kLdr;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < RB; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       *reinterpret_cast<f32x4_t*>(mine + (16 * i + (l & 15)) * kLdr + 16 * j + 4 * (l >> 4)) = acc[i][j];
   __syncthreads();
   // wave w reduces rows kRows w .. + kRows - 1: lane -> one row, kCols contiguous columns
-  constexpr int kRows = 64 / kNW, kLpr = 64 / kRows, kCols = 64 / kLpr;
+  constexpr int kRows = TM / kNW, kLpr = 64 / kRows, kCols = 64 / kLpr;
   const int rt = kRows * w + l / kLpr, ct = kCols * (l % kLpr);
   const int row = m0 + rt;
   float v[kCols];
@@ -163,7 +192,7 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g, int S, flo
     f32x4_t s = *reinterpret_cast<const f32x4_t*>(red + rt * kLdr + ct + 4 * q);
 #pragma unroll
     for (int p = 1; p < kNW; ++p) {
-      const f32x4_t t = *reinterpret_cast<const f32x4_t*>(red + (p * 64 + rt) * kLdr + ct + 4 * q);
+      const f32x4_t t = *reinterpret_cast<const f32x4_t*>(red + (p * TM + rt) * kLdr + ct + 4 * q);
       s[0] += t[0], s[1] += t[1], s[2] += t[2], s[3] += t[3];
     }
 #pragma unroll
@@ -171,11 +200,11 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g, int S, flo
   }
   if (S > 1) {  // split-K: partial out, count in; the last workgroup of the tile sums the S partials
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, 0x7fffffff, 0x00020000);
-    const uint32_t o0 = (uint32_t)(((long)t * S * 4096 + rt * 64 + ct) * 4);
+    const uint32_t o0 = (uint32_t)(((long)t * S * (TM * 64) + rt * 64 + ct) * 4);
 #pragma unroll
     for (int q = 0; q < kCols / 4; ++q)  // (aux 16 = sc1: through to the agent coherence point)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, f32x4_t{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]}),
-                                             rw, o0 + (uint32_t)sp * 16384u + 16u * q, 0, 16);
+                                             rw, o0 + (uint32_t)sp * (TM * 256u) + 16u * q, 0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's partial is at the coherence point
     __syncthreads();
     // The hand-off: every partial stored sc1 and drained (vmcnt(0)) by every wave before the barrier, ONE
@@ -204,7 +233,7 @@ __global__ __launch_bounds__(64 * kNW) void gemm_s_kernel(GemmArgs g, int S, flo
 #pragma unroll
       for (int q = 0; q < kCols / 4; ++q)
         pv[p][q] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   rw, o0 + (uint32_t)min(p, S - 1) * 16384u + 16u * q, 0, 16));
+                                                   rw, o0 + (uint32_t)min(p, S - 1) * (TM * 256u) + 16u * q, 0, 16));
 #pragma unroll
     for (int q = 0; q < kCols / 4; ++q)
 #pragma unroll
@@ -281,25 +310,27 @@ static SplitWs split_ws(hipStream_t st) {
 }
 
 // K-splits: enough workgroups for ~1.5 per CU, every wave at least 2 K-tiles (MFT_GS_SPLIT=0: off, A/B)
-static int pick_split(int tiles, int nkt) {
+// (MFT_GS_SPLIT_TILES: the tile count from which no product splits, A/B)
+static int pick_split(int tiles, int nkt, int tm) {
   static const int on = getenv("MFT_GS_SPLIT") ? atoi(getenv("MFT_GS_SPLIT")) : 1;
-  if (!on || tiles >= 192) return 1;
+  static const int lim = getenv("MFT_GS_SPLIT_TILES") ? atoi(getenv("MFT_GS_SPLIT_TILES")) : 192;
+  if (!on || tiles >= lim) return 1;
   int S = std::min((384 + tiles - 1) / tiles, nkt / (2 * kNW));
-  S = std::max(1, std::min({S, kMaxSplit, kWsTiles / std::max(tiles, 1)}));
+  S = std::max(1, std::min({S, kMaxSplit, kWsTiles * (64 / tm) / std::max(tiles, 1)}));
   return tiles > kCnt ? 1 : S;
 }
 
-template <int EPI, bool SEG2>
-void launch_s(const GemmArgs& g, hipStream_t st) {
-  constexpr size_t shm = kNW * 64 * kLdr * sizeof(float);
+template <int EPI, bool SEG2, int TM>
+void launch_s_tm(const GemmArgs& g, hipStream_t st) {
+  constexpr size_t shm = kNW * TM * kLdr * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_s_kernel<EPI, SEG2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    MFT_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_s_kernel<EPI, SEG2, TM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)shm));
     attr = true;
   }
-  const int tiles = ((g.M + 63) / 64) * ((g.N + 63) / 64);
-  int S = pick_split(tiles, g.K / 64 + (SEG2 ? g.K2 / 64 : 0));
+  const int tiles = ((g.M + TM - 1) / TM) * ((g.N + 63) / 64);
+  int S = pick_split(tiles, g.K / 64 + (SEG2 ? g.K2 / 64 : 0), TM);
   SplitWs w;
   if (S > 1) {
     w = split_ws(st);
@@ -309,7 +340,17 @@ void launch_s(const GemmArgs& g, hipStream_t st) {
   static const int strict = getenv("MFT_STRICT_HANDOFF") && getenv("MFT_STRICT_HANDOFF")[0] == '1';
   GemmArgs gs = g;
   gs.handoff_fence = strict;
-  gemm_s_kernel<EPI, SEG2><<<blocks, 64 * kNW, shm, st>>>(gs, S, w.ws, w.cnt);
+  gemm_s_kernel<EPI, SEG2, TM><<<blocks, 64 * kNW, shm, st>>>(gs, S, w.ws, w.cnt);
+}
+
+// 32-row tiles while the 64-row tiles would leave more than half the CUs idle (MFT_GS_TM=64 | 32 forces one)
+template <int EPI, bool SEG2>
+void launch_s(const GemmArgs& g, hipStream_t st) {
+  static const int force = getenv("MFT_GS_TM") ? atoi(getenv("MFT_GS_TM")) : 0;
+  const long tiles64 = (long)((g.M + 63) / 64) * ((g.N + 63) / 64);
+  const bool t32 = force == 32 || (force != 64 && tiles64 < 128);
+  if (t32) launch_s_tm<EPI, SEG2, 32>(g, st);
+  else launch_s_tm<EPI, SEG2, 64>(g, st);
 }
 
 }  // namespace

@@ -5,7 +5,7 @@ set -o pipefail
 TAG=$1
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd $R
-timeout -k 10 1500 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 \
+timeout -k 10 1500 python3 -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 \
   || { tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -3 gpurun_out/${TAG}_tests.log
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { tail gpurun_out/${TAG}_smoke.log; exit 1; }

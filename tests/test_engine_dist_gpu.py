@@ -51,8 +51,10 @@ def _env(rank=0, world=1, port=None, backend="loopback", **extra):
     return env
 
 
-def _run_ranks(cmd, world, timeout=240, backend="loopback", extra_env=None, per_rank=None):
-    """Start `world` native rank processes (one shared GPU); returns [(rc, stdout, stderr)]."""
+def _run_ranks(cmd, world, timeout=150, backend="loopback", extra_env=None, per_rank=None):
+    """Start `world` native rank processes (one shared GPU); returns [(rc, stdout, stderr)].  A rank still
+    running after `timeout` s (these runs take seconds) fails the test with every rank's output tail --
+    well inside the GPU runner's 180-s silence limit."""
     port = _port()
     procs = []
     for r in range(world):
@@ -66,7 +68,12 @@ def _run_ranks(cmd, world, timeout=240, backend="loopback", extra_env=None, per_
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
-            raise
+            tails = []
+            for r, q in enumerate(procs):
+                o, e = q.communicate()
+                tails.append(f"--- rank {r} (rc {q.returncode}) stdout ---\n{(o or '')[-1500:]}\n"
+                             f"--- rank {r} stderr ---\n{(e or '')[-1500:]}")
+            raise AssertionError(f"{world} ranks timed out after {timeout} s: {' '.join(cmd)}\n" + "\n".join(tails))
         out.append((p.returncode, o, e))
     return out
 
@@ -76,7 +83,7 @@ FULL = ["--random_init", "--model", "gpt2-tiny", "--synthetic_data", "--syntheti
 
 
 def _single(prog, args, batch_flag, batch):
-    r = subprocess.run([_bin(prog), *args, batch_flag, str(batch)], capture_output=True, text=True, timeout=240,
+    r = subprocess.run([_bin(prog), *args, batch_flag, str(batch)], capture_output=True, text=True, timeout=150,
                        env=_env())
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     return r
@@ -156,7 +163,7 @@ def test_native_rccl_zero2_step_in_graph():
     hipGraph: the capture succeeds and the losses match the plain single-process step."""
     want = loss_list(_single("gpt2_full_finetune", FULL, "--batch_size", 4).stdout, True)
     r = subprocess.run([_bin("gpt2_full_finetune"), *FULL, "--batch_size", "4", "--zero_stage", "2"],
-                       capture_output=True, text=True, timeout=240, env=_env(backend="rccl", MFT_DP_FORCE_COMM="1"))
+                       capture_output=True, text=True, timeout=150, env=_env(backend="rccl", MFT_DP_FORCE_COMM="1"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "data parallel: rank 0 of 1 (rccl" in r.stdout and "ZeRO-2" in r.stdout, r.stdout[:3000]
     assert loss_list(r.stdout, True) == pytest.approx(want, rel=2e-4, abs=2e-4)
@@ -169,7 +176,7 @@ def test_native_rccl_zero3_step_in_graph():
     args = FULL + ["--batch_size", "2", "--grad_accum_steps", "2"]
     want = loss_list(_single("gpt2_full_finetune", args[:-2], "--grad_accum_steps", 2).stdout, True)
     r = subprocess.run([_bin("gpt2_full_finetune"), *args, "--zero_stage", "3"],
-                       capture_output=True, text=True, timeout=240, env=_env(backend="rccl", MFT_DP_FORCE_COMM="1"))
+                       capture_output=True, text=True, timeout=150, env=_env(backend="rccl", MFT_DP_FORCE_COMM="1"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "ZeRO-3 over 1 rank(s) [rccl]" in r.stdout and "hipGraph" in r.stdout, r.stdout[:3000]
     assert loss_list(r.stdout, True) == pytest.approx(want, rel=2e-4, abs=2e-4)
@@ -278,7 +285,7 @@ def test_native_bench_json_line(tmp_path):
     CLI's MFT_BENCH line (a short GPT-2 LoRA run)."""
     import json
     r = subprocess.run(["python", os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "3", "--batch", "64"],
-                       capture_output=True, text=True, timeout=300, env=_env(), cwd=ROOT)
+                       capture_output=True, text=True, timeout=160, env=_env(), cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["value"] > 0 and "native" in rec["config"]["engine"]
@@ -296,7 +303,7 @@ def test_native_bench_under_torchrun_two_ranks():
     r = subprocess.run(["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(_port()),
                         os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2", "--batch", "64"],
-                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+                       capture_output=True, text=True, timeout=160, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     lines = [l for l in r.stdout.strip().splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
@@ -321,7 +328,7 @@ def test_native_activation_checkpointing_same_losses(prog, args, bflag):
     want = loss_list(_single(prog, args, bflag, 4).stdout, True)
     extra_env = {"MFT_DP_FORCE_COMM": "1"} if "--zero_stage" in args else {}
     r = subprocess.run([_bin(prog), *args, bflag, "4", "--activation_checkpointing"], capture_output=True, text=True,
-                       timeout=240, env=_env(backend="rccl", **extra_env) if extra_env else _env())
+                       timeout=150, env=_env(backend="rccl", **extra_env) if extra_env else _env())
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     got = loss_list(r.stdout, True)
     assert len(got) == len(want) and got == pytest.approx(want, rel=1e-5, abs=1e-5), (got, want)
@@ -351,7 +358,7 @@ def test_native_dp_four_ranks_match_single_process(tmp_path, extra):
     want = loss_list(_single("gpt2_full_finetune", FULL + ["--output_path", ref_out], "--batch_size", 8).stdout, True)
     dp_out = str(tmp_path / "dp.safetensors")
     res = _run_ranks([_bin("gpt2_full_finetune"), *FULL, "--batch_size", "2", "--output_path", dp_out, *extra], 4,
-                     timeout=300)
+                     timeout=160)
     for rc, o, e in res:
         assert rc == 0, o[-2000:] + e[-2000:]
     out0 = res[0][1]
