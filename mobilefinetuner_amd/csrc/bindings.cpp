@@ -364,7 +364,7 @@ void lora_rowdot(Tensor X, Tensor Wt, Tensor U, double s, double drop_p, int64_t
   TORCH_CHECK(X.stride(-1) == 1 && U.stride(-1) == 1 && Wt.stride(-1) == 1, "rows must be contiguous");
   const int K = X.size(-1), R = Wt.size(0);
   TORCH_CHECK(Wt.size(1) == K && U.size(-1) == R, "lora_rowdot: shape mismatch");
-  TORCH_CHECK(K % 32 == 0, "lora: in-features must be a multiple of 32");
+  TORCH_CHECK(K % 8 == 0, "lora_rowdot: in-features must be a multiple of 8");
   TORCH_CHECK(X.stride(-2) % 8 == 0 && Wt.stride(0) % 8 == 0, "lora_rowdot: row strides must be multiples of 8");
   const long M = X.numel() / K;
   mft::lora_rowdot(bp(X), X.stride(-2), bp(Wt), Wt.stride(0), bp(U), U.stride(-2), M, K, R, (float)s,

@@ -7,8 +7,8 @@
 // Internal layouts: A is [R, K] (PEFT lora_A.weight), B is [R, N] (reference lora_B layout), so
 // every rank-r operand is read along contiguous rows.  For y = x W^T + s (x A^T) B:
 //   lora_rowdot : U[m, r] = s * sum_k X[m, k] Wt[r, k]           u = x A^T (Wt = A), v = s dy B^T (Wt = B)
-//                 MFMA 16x16x32: one 16-row tile per 4-wave block, K split over the waves and
-//                 reduced through LDS; X streamed once from HBM with 16-B loads.
+//                 MFMA 16x16x32: one 16-row tile and the whole K per wave (no LDS, no barrier);
+//                 X streamed once from HBM with 16-B loads, two batches of k-steps in flight.
 //   lora_update : Y[m, n] = base[m, n] + s * sum_r U[m, r] W[r, n]  y += s u B (W = B), dx += v A (W = A)
 //                 VALU; each thread keeps its 8 columns of W in registers for a strip of rows.
 //   lora_wgrad  : out[k*osk + r*osr] += scale * sum_m X[m, k] Y[m, r]
@@ -51,65 +51,65 @@ __device__ __forceinline__ bf16x8_t apply_drop8(bf16x8_t a, const LoraDrop& d, u
 }
 
 // ------------------------------------------------------------------------------------ rowdot
-// block = 4 waves; rows [16*blockIdx.x, +16); wave w handles k in [w*Kq, (w+1)*Kq).
-// Each 16-col output tile covers ranks [16*t, 16*t+16) of R (RT tiles).
+// U[m, r] = s * sum_k X[m, k] Wt[r, k] on v_mfma_f32_16x16x32_bf16.  A wave owns 16 rows and the WHOLE K --
+// no cross-wave reduction, no LDS, no barrier.  X / Wt fragments come in batches of UNR k-steps, the next
+// batch's loads issued before the current batch's MFMAs (two batches in flight); k past K (K % 8 == 0) and
+// rows past M read as zeros.  (Round 5's form split K over the 4 waves of a 16-row workgroup and reduced
+// through LDS behind a barrier, and silently dropped a K % 32 tail; this one measured the same end to end,
+// profiles/r6_rowdot_wave_ab.txt.)
 template <int RT>
-__global__ __launch_bounds__(256) void lora_rowdot_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Wt,
-                                                          long ldw, bf16_t* __restrict__ U, long ldu, long M, int K, int R,
-                                                          float s, LoraDrop drop) {
-  __shared__ __attribute__((aligned(16))) float red[4][RT][64][4];
+__global__ __launch_bounds__(256) void lora_rowdot_kernel(const bf16_t* __restrict__ X, long ldx,
+                                                            const bf16_t* __restrict__ Wt, long ldw, bf16_t* __restrict__ U,
+                                                            long ldu, long M, int K, int R, float s, LoraDrop drop) {
+  constexpr int UNR = RT == 1 ? 8 : RT == 2 ? 4 : 2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long m0 = ((long)blockIdx.x * 4 + w) * 16;
+  if (m0 >= M) return;  // (wave-uniform; nothing below synchronises the workgroup)
   const uint32_t dseed = drop.p > 0.f ? drop_seed(drop) : 0u;
-  const long m0 = (long)blockIdx.x * 16;
   const long mr = m0 + (lane & 15);
   const bool row_ok = mr < M;
-  const int nks = K / 32;
-  const int per = (nks + 3) / 4;
-  const int ks0 = w * per, ks1 = min(nks, ks0 + per);
+  const int nks = (K + 31) / 32;
   f32x4_t acc[RT];
 #pragma unroll
   for (int t = 0; t < RT; ++t) acc[t] = zero4();
-  // UNR k-steps per batch: every X / W load of the batch is issued before the first MFMA consumes
-  // one (a one-step loop exposed the full load latency on each of its few iterations: K / 128 per
-  // wave, e.g. 5 at Gemma's K = 640)
-  constexpr int UNR = 4;
-  for (int kb = ks0; kb < ks1; kb += UNR) {
-    bf16x8_t a[UNR], b[UNR][RT];
+  bf16x8_t a[2][UNR], b[2][UNR][RT];
+  auto load = [&](int buf, int kb) {
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const bool ok = kb + u < ks1;
       const int k = (kb + u) * 32 + 8 * (lane >> 4);
-      a[u] = (ok && row_ok) ? *reinterpret_cast<const bf16x8_t*>(X + mr * ldx + k) : bf16x8_t{};
+      const bool ok = k < K;  // (K % 8 == 0: an 8-column chunk is in or out as a whole)
+      a[buf][u] = (ok && row_ok) ? *reinterpret_cast<const bf16x8_t*>(X + mr * ldx + k) : bf16x8_t{};
 #pragma unroll
       for (int t = 0; t < RT; ++t) {
         const int r = t * 16 + (lane & 15);
-        b[u][t] = (ok && r < R) ? *reinterpret_cast<const bf16x8_t*>(Wt + (long)r * ldw + k) : bf16x8_t{};
+        b[buf][u][t] = (ok && r < R) ? *reinterpret_cast<const bf16x8_t*>(Wt + (long)r * ldw + k) : bf16x8_t{};
       }
     }
+  };
+  auto mul = [&](int buf, int kb) {
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      if (drop.p > 0.f) a[u] = apply_drop8(a[u], drop, dseed, mr, (kb + u) * 32 + 8 * (lane >> 4), K);
+      bf16x8_t x = a[buf][u];
+      if (drop.p > 0.f) x = apply_drop8(x, drop, dseed, mr, (kb + u) * 32 + 8 * (lane >> 4), K);
 #pragma unroll
-      for (int t = 0; t < RT; ++t) acc[t] = mfma16(a[u], b[u][t], acc[t]);
+      for (int t = 0; t < RT; ++t) acc[t] = mfma16(x, b[buf][u][t], acc[t]);
     }
+  };
+  load(0, 0);
+  for (int kb = 0; kb < nks; kb += 2 * UNR) {
+    load(1, kb + UNR);
+    mul(0, kb);
+    if (kb + 2 * UNR < nks) load(0, kb + 2 * UNR);
+    if (kb + UNR < nks) mul(1, kb + UNR);
   }
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) red[w][t][lane][i] = acc[t][i];
-  __syncthreads();
-  if (w == 0) {
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float v = red[0][t][lane][i] + red[1][t][lane][i] + red[2][t][lane][i] + red[3][t][lane][i];
-        const long m = m0 + 4 * (lane >> 4) + i;
-        const int r = t * 16 + (lane & 15);
-        if (m < M && r < R) U[m * ldu + r] = f2bf(v * s);
-      }
+    for (int i = 0; i < 4; ++i) {
+      const long m = m0 + 4 * (lane >> 4) + i;
+      const int r = t * 16 + (lane & 15);
+      if (m < M && r < R) U[m * ldu + r] = f2bf(acc[t][i] * s);
     }
-  }
 }
 
 // ------------------------------------------------------------------------------------ update
@@ -592,7 +592,12 @@ __global__ void lora_merge_kernel(T* W, long wsk, long wsn, const float* __restr
 
 void lora_rowdot(const bf16_t* X, long ldx, const bf16_t* Wt, long ldw, bf16_t* U, long ldu, long M, int K, int R, float s,
                  LoraDrop drop, hipStream_t st) {
-  const int grid = cdiv(M, 16);
+  if (K % 8 || ldx % 8 || ldw % 8 || R > 64 || (reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Wt)) % 16) {
+    fprintf(stderr, "lora_rowdot: K and the row strides must be multiples of 8, X / Wt 16-B aligned, R <= 64\n");
+    abort();
+  }
+  if (M <= 0) return;
+  const int grid = cdiv(M, 64);
   if (R <= 16) lora_rowdot_kernel<1><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);
   else if (R <= 32) lora_rowdot_kernel<2><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);
   else lora_rowdot_kernel<4><<<grid, 256, 0, st>>>(X, ldx, Wt, ldw, U, ldu, M, K, R, s, drop);

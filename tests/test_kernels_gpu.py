@@ -687,10 +687,12 @@ def test_adamw_amsgrad_matches_reference():
     assert torch.allclose(vmax.cpu().double(), rvh, rtol=1e-5, atol=1e-9)
 
 
-@pytest.mark.parametrize("M,K,R,ldx", [(1000, 640, 8, 704), (77, 768, 32, 768), (4099, 2048, 16, 2112)])
+@pytest.mark.parametrize("M,K,R,ldx", [(1000, 640, 8, 704), (77, 768, 32, 768), (4099, 2048, 16, 2112),
+                                        (300, 200, 8, 264), (513, 2304, 8, 2304), (130, 1152, 64, 1152)])
 def test_lora_rowdot_matches_fp32(M, K, R, ldx, monkeypatch):
-    """u = s x A^T on the row-per-wave MFMA kernel (default) against fp32, with X a strided column slice
-    of a wider row (the augmented-K buffer) and ragged row counts."""
+    """u = s x A^T on the wave-per-16-rows MFMA kernel (default) against fp32, with X a strided column slice
+    of a wider row (the augmented-K buffer), ragged row counts, K not a multiple of 32 (200: the masked tail
+    chunk) and every rank-tile count (R 8 / 16 / 32 / 64)."""
     from mobilefinetuner_amd._ext import native
     C = native()
     g = torch.Generator(device=DEV).manual_seed(11)
