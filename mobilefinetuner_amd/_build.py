@@ -168,7 +168,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         tmp = OUT_SO + ".tmp"
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp,
                f"-L{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip",
-               "-ltorch_hip", "-lhipblaslt", "-lamdhip64", f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{libdir}",
+               "-ltorch_hip", "-lamdhip64", f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{libdir}",
                f"-Wl,-rpath,{ROCM}/lib", "-ldl", "-lpthread"]
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -705,7 +705,6 @@ void zero_cols(Tensor t, int64_t c0) {
 }  // namespace
 
 void register_runtime(py::module_& m);  // csrc/runtime_bindings.cpp
-void register_gemm_lt(py::module_& m);  // csrc/gemm_lt.cpp
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "mobilefinetuner_amd native kernels (gfx950 HIP) and C++ runtime";
@@ -763,5 +762,4 @@ PYBIND11_MODULE(_C, m) {
   m.def("scale_bf16", &scale_bf16);
   m.def("add_bf16", &add_bf16);
   register_runtime(m);
-  register_gemm_lt(m);
 }

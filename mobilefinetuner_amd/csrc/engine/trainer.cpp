@@ -300,6 +300,7 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
   pm_t0_ = t_last;
   int64_t tok_since = 0, steps_since = 0;
   const bool prof = cfg_.profile_to > 0 && cfg_.profile_to >= cfg_.profile_from;
+  bool prof_open = false;  // (a resumed run may start inside the window: open it at its first step)
   hipEvent_t pe0 = nullptr, pe1 = nullptr;
   if (prof) {
     profiler_pause();
@@ -322,10 +323,11 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
       if (cfg_.micro_hook) cfg_.micro_hook(micro_steps_, hid[a].data(), B, S);
     }
     const bool in_prof = prof && it + 1 >= cfg_.profile_from && it + 1 <= cfg_.profile_to;
-    if (in_prof && it + 1 == std::max<int64_t>(cfg_.profile_from, 1)) {
+    if (in_prof && !prof_open) {
       synchronize();
       profiler_resume();
       roctxRangePushA("mft.profile");
+      prof_open = true;
     }
     if (in_prof) HIP_OK(hipEventRecord(pe0, stream_));
     Tensor loss = step(micro);
@@ -338,6 +340,7 @@ void Trainer::train(const std::function<void(int64_t)>& save_fn) {
       if (it + 1 == cfg_.profile_to || it + 1 == total_steps_) {
         roctxRangePop();
         profiler_pause();
+        prof_open = false;
       }
     }
     ++global_step;

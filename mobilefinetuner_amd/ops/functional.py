@@ -538,22 +538,12 @@ def gemm_dx(dy2, wc, out=None):
 
 
 def _mm_wgrad_into(buf, dy2, x2, alpha=1.0):
-    """buf (fp32 [N, K]) += alpha * dy2^T @ x2, accumulated in place in the fp32 grad buffer."""
+    """buf (fp32 [N, K]) += alpha * dy2^T @ x2, accumulated in place in the fp32 grad buffer: the TN gemm8
+    (split-K slabs + a fixed-order reduce, bitwise reproducible) where its shape rules hold, else torch."""
     M = dy2.shape[0]
-    # gemm8's split-major split-K TN form beats hipBLASLt on small outputs IN ISOLATION (qkv dW 540 vs
-    # 556 us, proj dW 195 vs 273 us at 65536 tokens) but not inside the full-FT step (69.9 vs 72.1
-    # ms/step, A/B in one call: the fp32 slabs + reduce pass compete with the step's other traffic);
-    # hipBLASLt (beta = 1, in place) stays the default, MFT_G8_SMALL_WGRAD=1 opts in
-    small = dy2.shape[1] * x2.shape[1] <= 2304 * 768 and os.environ.get("MFT_G8_SMALL_WGRAD", "0") == "1"
-    g8 = deterministic() or _gemm8_all() or small
-    if (g8 and _g8_ok(dy2, x2) and buf.is_contiguous() and M % 64 == 0 and dy2.shape[1] % 8 == 0
+    if (_g8_ok(dy2, x2) and buf.is_contiguous() and M % 64 == 0 and dy2.shape[1] % 8 == 0
             and x2.shape[1] % 8 == 0):
-        # TN gemm8: split-K slabs + fixed-order reduce (bitwise reproducible, no atomics)
         native().gemm_t(dy2, x2, True, True, GEMM_EPI_F32ACC, alpha=float(alpha), out=buf.view(dy2.shape[1], -1))
-        return
-    if (buf.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and dy2.stride(-1) == 1
-            and x2.stride(-1) == 1 and buf.is_contiguous()):
-        native().lt_wgrad_acc(x2, dy2, buf.view(dy2.shape[1], -1), float(alpha))  # hipBLASLt, beta = 1
         return
     buf.add_(torch.mm(dy2.t(), x2, out_dtype=torch.float32), alpha=alpha)
 

@@ -627,7 +627,7 @@ def test_lora_dropout_consistent_fwd_bwd():
 
 
 def test_colsum_and_wgrad_accumulate():
-    """Bias-grad column sums and hipBLASLt beta=1 weight-grad accumulation into fp32 buffers."""
+    """Bias-grad column sums and the TN gemm8 weight-grad accumulation (beta = 1) into fp32 buffers."""
     from mobilefinetuner_amd._ext import native
     C = native()
     M, N, K = 1000, 264, 200
@@ -639,8 +639,9 @@ def test_colsum_and_wgrad_accumulate():
     C.colsum_acc(dy[:, :256], out[:256], False)
     _close(out[:256], dy[:, :256].float().sum(0), 0.02, 1e-3, msg="colsum strided")
     w = torch.ones(N, K, device=DEV)
-    C.lt_wgrad_acc(x, dy, w, 0.5)
-    _close(w, 1.0 + 0.5 * dy.float().t() @ x.float(), 0.05, 1e-3, msg="wgrad acc")
+    Mw = M // 64 * 64  # (the TN form takes token counts in whole 64-row K-tiles)
+    C.gemm_t(dy[:Mw], x[:Mw], True, True, 4, None, None, 0.5, w, None, None, 0)  # 4 = GEMM_EPI_F32ACC
+    _close(w, 1.0 + 0.5 * dy[:Mw].float().t() @ x[:Mw].float(), 0.05, 1e-3, msg="wgrad acc")
 
 
 def test_gated_row_pair_grid_stride():
