@@ -297,8 +297,10 @@ static int ce_num_cus() {
 // tiles (Gemma-3 at 8,192 rows: 96 for 256 CUs), so a row chunk alone leaves most CUs idle and
 // bounding the E buffer by small chunks used to cost 17 % (profiles/r3_ce_budget_and_attn_nw_ab.txt).
 // Split the vocab (the dgrad's K) so tiles x splits fills the CUs in as few, as full rounds as
-// possible: time ~ rounds / splits, a split only for a > 5 % gain, >= 16 vocab tiles per split, whole
+// possible: time ~ rounds / splits, a split only for a > 5 % gain, >= 4 vocab tiles per split, whole
 // vocab tiles per split (the per-tile rescale chain restarts at a split's first tile with acc = 0).
+// The reference recipe's 512-row chunk (6 output tiles) takes 40 splits: +1.5 % over the old floor of
+// 16 vocab tiles per split (11 splits, 66 workgroups; profiles/r6_ce_split_short_ab.txt).
 // MFT_CE_SPLIT forces a count (1 = off).
 int ce_dgrad_splits(int M, int K, int Vpad) {
   const int nk = (Vpad + 63) / 64, T = (Vpad + 255) / 256;
@@ -309,12 +311,12 @@ int ce_dgrad_splits(int M, int K, int Vpad) {
   };
   if (const char* e = getenv("MFT_CE_SPLIT")) {
     const int f = atoi(e);
-    if (f >= 1 && f <= 32 && ok(f)) return f;
+    if (f >= 1 && f <= 64 && ok(f)) return f;
   }
   const int cus = ce_num_cus();
   int best = 1;
   double best_t = 1.0 * ((tiles + cus - 1) / cus);
-  for (int sp = 2; sp <= 32 && T / sp >= 16; ++sp) {
+  for (int sp = 2; sp <= 64 && T / sp >= 4; ++sp) {
     if (!ok(sp)) continue;
     const double t = (double)((tiles * sp + cus - 1) / cus) / sp;
     if (t < best_t * 0.95) {

@@ -93,7 +93,8 @@ def test_lm_head_token_nll_matches_fp32():
     assert abs(nll.item() - ref.item()) < 1e-4 * abs(ref.item()), (nll.item(), ref.item())
 
 
-@pytest.mark.parametrize("M,K,V,Vpad,forced", [(8192, 640, 262144, 262144, "4"), (6000, 768, 50257, 50304, "9")])
+@pytest.mark.parametrize("M,K,V,Vpad,forced", [(8192, 640, 262144, 262144, "4"), (6000, 768, 50257, 50304, "9"),
+                                                (512, 768, 50257, 50304, "22")])  # (the 4 x 128 chunk: 40 automatically)
 def test_lm_head_ce_vocab_split_dgrad_matches_unsplit(M, K, V, Vpad, forced, monkeypatch):
     """The vocab-split CE dgrad (fp32 slabs per split, reduced in split order; chosen automatically when a
     row chunk's dh tiles cannot fill the CUs) against the single-pass dgrad (MFT_CE_SPLIT=1) and fp32."""
