@@ -239,7 +239,9 @@ inline bool load_token_splits(const Args& a, DataConfig& dc, int vocab, TokenDat
 //   --zero_stage 0|1|2|3 optimizer partition (1) + reduce-scattered gradients (2) + partitioned
 //                        parameters (3, full fine-tuning: engine/zero3.h); > 0 also on one process
 //                        (a 1-rank communicator: the partitioned code path runs)
-//   --offload host|none  AdamW moments in pinned host DRAM (--offload_moments bf16 (stochastically
+//   --offload host|disk|none  AdamW moments in pinned host DRAM, or (disk, --offload_dir D, default
+//                        ./mft_offload; ZeRO stages 0-2) in files under D streamed through device chunks
+//                        each step (--offload_moments bf16 (stochastically
 //                        rounded, default) | fp32); ZeRO-3: --offload_mode stream (default: each
 //                        unit updated during the next forward, on its own stream, under the
 //                        compute) | zerocopy (one update after the backward); both read / write the
@@ -254,8 +256,9 @@ inline DistConfig dist_config_from(const Args& a) {
   d.bf16_reduce = a.b("bf16_grads");
   d.overlap = !a.b("no_overlap");
   const std::string off = a.get("offload", "none");
-  if (off != "none" && off != "host") throw std::runtime_error("--offload host|none (got '" + off + "')");
+  if (off != "none" && off != "host" && off != "disk") throw std::runtime_error("--offload host|disk|none (got '" + off + "')");
   d.host_moments = off == "host";
+  if (off == "disk") d.disk_dir = a.get("offload_dir", "mft_offload");
   const std::string om = a.get("offload_moments", "bf16");
   if (om != "bf16" && om != "fp32") throw std::runtime_error("--offload_moments bf16|fp32 (got '" + om + "')");
   d.host_fp32 = om == "fp32";
@@ -297,6 +300,7 @@ struct DistSetup {
   }
   // after the optimizer exists (the reducer shards it)
   void make_dp(eng::Communicator* comm, eng::AdamW& opt, const DistConfig& d) {
+    if (z3 && !d.disk_dir.empty()) throw std::runtime_error("--offload disk: ZeRO stages 0-2 (ZeRO-3 takes --offload host)");
     if (z3) {
       z3->shard_optimizer(opt, d.host_moments, d.host_fp32, d.host_stream);
       std::printf("  %s%s%s%s\n", z3->describe().c_str(),
@@ -312,6 +316,11 @@ struct DistSetup {
     } else if (d.host_moments) {
       opt.shard({eng::OptSegment{0, flat->numel, 0}}, nullptr, true, d.host_fp32);
       std::printf("  AdamW moments in pinned host DRAM (%s)\n", d.host_fp32 ? "fp32" : "bf16");
+    }
+    if (!d.disk_dir.empty()) {  // after the reducer planned this rank's optimizer segments
+      opt.to_disk(d.disk_dir, comm ? comm->rank() : 0, d.host_fp32);
+      std::printf("  AdamW moments on disk (%s, %s/adamw_{m,v}.rank%d.bin), streamed through device chunks each step\n",
+                  d.host_fp32 ? "fp32" : "bf16", d.disk_dir.c_str(), comm ? comm->rank() : 0);
     }
   }
   eng::GradReducer* reducer() { return z3 ? static_cast<eng::GradReducer*>(z3.get()) : dp.get(); }

@@ -63,7 +63,7 @@ const std::set<std::string> kValued = {
     "eval_batch_size", "save_every", "ema_beta", "seed", "pm_interval", "pm_batt_thresh", "pm_temp_thresh",
     "pm_fb_high", "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "pm_power_cap",
     "shard_dir", "shard_budget_mb", "shard_fp16_disk", "model", "synthetic_tokens", "pretokenized_path",
-    "pretokenized_meta", "lora_targets", "metrics_out", "device", "bench_steps", "bench_warmup", "zero_stage", "offload", "offload_moments", "offload_mode", "bucket_mb", "dump_grads"};
+    "pretokenized_meta", "lora_targets", "metrics_out", "device", "bench_steps", "bench_warmup", "zero_stage", "offload", "offload_moments", "offload_mode", "offload_dir", "bucket_mb", "dump_grads"};
 
 Args parse(int argc, char** argv) { return parse_args(argc, argv, kBool, kValued); }
 
@@ -111,6 +111,8 @@ void usage() {
       "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"
       "          --inject_fault STEP:RANK (failure test: that rank throws before that step)\n"
       "          --deterministic\n"
+      "  multi-GPU / memory: --zero_stage 0|1|2|3 --offload host|disk|none [--offload_dir D] --offload_moments bf16|fp32\n"
+      "          --offload_mode stream|zerocopy --bucket_mb N --bf16_grads --no_overlap\n"
       "  common: --dtype bf16|fp32 --attn_impl flash|naive --profile_steps A:B --compat_grad_overwrite --compat_reference\n",
       kProg);
 }

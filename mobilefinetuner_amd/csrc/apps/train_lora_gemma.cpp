@@ -70,7 +70,7 @@ const std::set<std::string> kValued = {
     "data_fraction", "log_interval", "eval_steps", "eval_batches", "save_every", "seed", "model", "synthetic_tokens",
     "resume_from", "state_dir", "inject_fault", "metrics_out", "eval_out", "pm_interval", "pm_batt_thresh", "pm_temp_thresh", "pm_fb_high",
     "pm_fb_low", "pm_ft_high", "pm_ft_low", "pm_manual_batt", "pm_manual_temp", "pm_schedule", "pm_power_cap", "device",
-    "shard_budget_mb", "shard_dir", "shard_fp16_disk", "bench_steps", "bench_warmup", "zero_stage", "offload", "offload_moments", "offload_mode", "bucket_mb",
+    "shard_budget_mb", "shard_dir", "shard_fp16_disk", "bench_steps", "bench_warmup", "zero_stage", "offload", "offload_moments", "offload_mode", "offload_dir", "bucket_mb",
     "align_dump_dir", "align_layers", "align_pt_weights_dir", "align_numeric_eps", "align_numeric_count",
     "align_numeric_targets", "dump_grads", "dump_embedding", "dump_embedding_step", "dump_embedding_dir",
     "preview_tokens"};
@@ -98,7 +98,7 @@ void usage() {
       "  --dump_embedding 1 --dump_embedding_step N --dump_embedding_dir D --preview_tokens N\n"
       "  extras: --model P --random_init --synthetic_data --synthetic_tokens N --resume_from F --no_graph\n"
       "          --compat_l2_adam --amsgrad --metrics_out F --deterministic --interleaved_rope\n"
-      "          --zero_stage 0|1|2 --offload host|none --bucket_mb N --bf16_grads --no_overlap\n"
+      "          --zero_stage 0|1|2 --offload host|disk|none [--offload_dir D] --bucket_mb N --bf16_grads --no_overlap\n"
       "          --state_dir D (full training state: written at --save_every and at the end, resumed if present)\n"
       "          --inject_fault STEP:RANK (failure test: that rank throws before that step)\n"
       "          --bench_steps K [--bench_warmup W] (bench.py: time K steps after W, print one MFT_BENCH line)\n"

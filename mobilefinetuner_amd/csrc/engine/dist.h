@@ -80,6 +80,8 @@ struct DistConfig {
   bool overlap = true;               // launch buckets from the grad-ready hooks during backward
   bool host_moments = false;         // stage >= 1: AdamW moments in pinned host DRAM
   bool host_fp32 = false;            // ... as fp32 (default bf16, stochastically rounded)
+  std::string disk_dir;              // --offload disk: AdamW moments in files under this directory
+                                     // (AdamW::to_disk; stages 0-2, eager step)
   bool host_stream = true;           // ZeRO-3: each unit's update applied in place (moments read and
                                      // written over PCIe) during the next forward on a side stream;
                                      // false: one update of everything after the backward

@@ -1,6 +1,13 @@
 // libmft engine: flat params + fused AdamW + schedules (see optim.h).
 #include "engine/optim.h"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <cstring>
+#include <filesystem>
+
 #include <algorithm>
 #include <cmath>
 
@@ -153,6 +160,7 @@ void AdamW::step() {
   hipStream_t s = current_stream();
   prepare();
   ::mft::AdamWArgs a = args();
+  if (disk_.active) return step_disk(a, s);
   float* g0 = flat_.grad.data<float>();
   a.moments_bf16 = m.dtype() == DType::BF16;
   const size_t ms = m.dtype() == DType::BF16 ? 2 : 4;
@@ -174,6 +182,81 @@ void AdamW::step() {
     k::Desc d = desc(skipped_dev), x = desc(nonfinite_dev);
     k::binary(d, d, x, k::B_ADD, 1.f, s);
   }
+}
+
+// ---------------------------------------------------------------- moments on disk (--offload disk)
+void AdamW::to_disk(const std::string& dir, int rank, bool fp32) {
+  MFT_CHECK(!disk_.active, "AdamW::to_disk: already on disk");
+  MFT_CHECK(!host_moments_ && !vmax.defined(), "AdamW::to_disk: not with host moments or AMSGrad");
+  NoGradGuard ng;
+  std::error_code ec;
+  std::filesystem::create_directories(dir, ec);
+  const int64_t n = std::max<int64_t>(state_numel_, 4);
+  disk_.elem = fp32 ? 4 : 2;
+  disk_.bytes = (size_t)n * disk_.elem;
+  const char* names[2] = {"m", "v"};
+  for (int i = 0; i < 2; ++i) {
+    const std::string path = dir + "/adamw_" + names[i] + ".rank" + std::to_string(rank) + ".bin";
+    const int fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
+    MFT_CHECK(fd >= 0, "AdamW::to_disk: cannot create ", path);
+    MFT_CHECK(::ftruncate(fd, (off_t)disk_.bytes) == 0, "AdamW::to_disk: cannot size ", path);  // zeros
+    void* p = ::mmap(nullptr, disk_.bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    MFT_CHECK(p != MAP_FAILED, "AdamW::to_disk: cannot map ", path);
+    disk_.map[i] = p;
+  }
+  const DType md = fp32 ? DType::F32 : DType::BF16;
+  m = from_blob(disk_.map[0], {n}, md, Device::cpu());
+  v = from_blob(disk_.map[1], {n}, md, Device::cpu());
+  static const int64_t env_chunk = std::getenv("MFT_DISK_CHUNK") ? std::atoll(std::getenv("MFT_DISK_CHUNK")) : 0;
+  disk_.chunk = std::min<int64_t>(n, env_chunk > 0 ? (env_chunk + 3) / 4 * 4 : (int64_t)16 << 20);
+  for (int i = 0; i < 2; ++i) {
+    disk_.dev[i] = empty({disk_.chunk}, md);
+    disk_.pin[i] = empty({disk_.chunk}, md, Device::cpu(true));
+  }
+  disk_.active = true;
+}
+
+void AdamW::step_disk(::mft::AdamWArgs a, hipStream_t s) {
+  float* g0 = flat_.grad.data<float>();
+  a.moments_bf16 = disk_.elem == 2;
+  char* mp[2] = {static_cast<char*>(disk_.map[0]), static_cast<char*>(disk_.map[1])};
+  for (auto& sg : segs_) {
+    for (int64_t o = 0; o < sg.len; o += disk_.chunk) {
+      const int64_t len = std::min(disk_.chunk, sg.len - o);
+      const size_t off = (size_t)(sg.state_off + o) * disk_.elem, nb = (size_t)len * disk_.elem;
+      for (int i = 0; i < 2; ++i) {  // mapping -> pinned -> device (the page cache faults the file in)
+        std::memcpy(disk_.pin[i].data_ptr(), mp[i] + off, nb);
+        HIP_OK(hipMemcpyAsync(disk_.dev[i].data_ptr(), disk_.pin[i].data_ptr(), nb, hipMemcpyHostToDevice, s));
+      }
+      a.p = flat_.master.data<float>() + sg.off + o;
+      a.g = g0 + sg.off + o;
+      a.m = static_cast<float*>(disk_.dev[0].data_ptr());
+      a.v = static_cast<float*>(disk_.dev[1].data_ptr());
+      a.vmax = nullptr;
+      a.n = len;
+      a.shadow = (::mft::bf16_t*)flat_.shadow.data_ptr() + sg.off + o;
+      a.sr_offset = sg.off + o;
+      ::mft::adamw_step(a, s);
+      for (int i = 0; i < 2; ++i)
+        HIP_OK(hipMemcpyAsync(disk_.pin[i].data_ptr(), disk_.dev[i].data_ptr(), nb, hipMemcpyDeviceToHost, s));
+      HIP_OK(hipStreamSynchronize(s));
+      for (int i = 0; i < 2; ++i) std::memcpy(mp[i] + off, disk_.pin[i].data_ptr(), nb);  // dirty pages -> file
+    }
+  }
+  ::mft::adamw_commit(step_dev.data<float>(), a.nonfinite, a.sumsq, s, cfg_.skip_nonfinite ? nonfinite_dev.data<int>() : nullptr);
+  if (cfg_.skip_nonfinite) {
+    k::Desc d = desc(skipped_dev), x = desc(nonfinite_dev);
+    k::binary(d, d, x, k::B_ADD, 1.f, s);
+  }
+}
+
+AdamW::~AdamW() {
+  if (!disk_.active) return;
+  m = Tensor();
+  v = Tensor();
+  for (void* p : disk_.map)
+    if (p) ::munmap(p, disk_.bytes);
 }
 
 // ---------------------------------------------------------------- delayed (streamed) updates

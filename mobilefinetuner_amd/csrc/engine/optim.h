@@ -85,8 +85,27 @@ class AdamW {
   bool sharded() const { return comm_ != nullptr; }
   bool moments_on_host() const { return host_moments_; }
   int64_t state_numel() const { return state_numel_; }
+  // --offload disk: the moments (this rank's state_numel() of each) live in file-backed memory --
+  // MAP_SHARED mappings of <dir>/adamw_{m,v}.rank<r>.bin, so the page cache keeps what fits and the
+  // kernel writes the rest back to the file -- and step() streams them through two device chunk buffers
+  // (mapping -> pinned staging -> device -> fused AdamW -> back), chunk by chunk.  Host copies run inside
+  // the step, so it is not graph-capturable (the trainer runs it eagerly).  Call after shard().
+  void to_disk(const std::string& dir, int rank, bool fp32);
+  bool moments_on_disk() const { return disk_.active; }
+  ~AdamW();
+  AdamW(const AdamW&) = delete;
+  AdamW& operator=(const AdamW&) = delete;
 
  private:
+  struct DiskMoments {
+    bool active = false;
+    void* map[2] = {nullptr, nullptr};  // m, v mappings
+    size_t bytes = 0, elem = 4;
+    int64_t chunk = 0;
+    Tensor dev[2], pin[2];  // device chunk buffers, pinned staging
+  };
+  DiskMoments disk_;
+  void step_disk(::mft::AdamWArgs a, hipStream_t s);
   FlatParams& flat_;
   AdamWConfig cfg_;
   std::vector<OptSegment> segs_;  // default: one segment = the whole flat buffer

@@ -41,6 +41,10 @@ Trainer::Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDatase
     std::printf("[trainer] step runs eagerly (no hipGraph): staged host-moment optimizer\n");
     cfg_.use_graph = false;
   }
+  if (cfg_.use_graph && opt_.moments_on_disk()) {  // host copies from the file mappings inside the step
+    std::printf("[trainer] step runs eagerly (no hipGraph): AdamW moments on disk\n");
+    cfg_.use_graph = false;
+  }
   if (cfg_.use_graph && !model_.capturable()) {
     // the composite path (--dtype fp32 / --attn_impl naive) reads host values inside the step
     std::printf("[trainer] step runs eagerly (no hipGraph): %s composite path\n",

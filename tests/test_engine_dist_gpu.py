@@ -102,10 +102,13 @@ def _single(prog, args, batch_flag, batch):
     (["--zero_stage", "2", "--offload", "host", "--offload_moments", "fp32"], 2e-4),  # fp32 host moments: exact
     (["--zero_stage", "3", "--offload", "host", "--offload_moments", "fp32"], 2e-4),  # streamed (default)
     (["--zero_stage", "3", "--offload", "host", "--offload_mode", "zerocopy"], 3e-3),
+    (["--zero_stage", "2", "--offload", "disk", "--offload_moments", "fp32"], 2e-4),  # moments in files, streamed
 ])
 def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
     """2 loopback ranks x batch 4 == 1 process x batch 8 (GPT-2-tiny full fine-tune, ~8 buckets):
     the same per-step losses and the same final weights."""
+    if "disk" in extra:
+        extra = extra + ["--offload_dir", str(tmp_path / "offload")]
     ref_out = str(tmp_path / "ref.safetensors")
     ref = _single("gpt2_full_finetune", FULL + ["--output_path", ref_out], "--batch_size", 8)
     want = loss_list(ref.stdout, True)
@@ -138,6 +141,33 @@ def test_native_dp_two_ranks_match_single_process(tmp_path, extra, tol):
         moved = (a[k] - w0[k]).abs() > 1e-5
         stale = moved & (b[k] == w0[k])
         assert moved.any() and int(stale.sum()) == 0, (extra, k, int(stale.sum()), int(moved.sum()))
+
+
+@pytest.mark.parametrize("moments,chunk", [("fp32", ""), ("fp32", "1000"), ("bf16", "1000")])
+def test_native_offload_disk_matches_device_moments(tmp_path, moments, chunk):
+    """--offload disk (AdamW moments in file mappings, streamed through device chunks each step; eager)
+    == moments on the device (fp32) / in pinned host DRAM (bf16, the same stochastic rounding): the same
+    per-step losses and final weights, several chunks per step (MFT_DISK_CHUNK), and the moment files on disk."""
+    import os
+    env_chunk = {"MFT_DISK_CHUNK": chunk} if chunk else {}
+    ref_args = ["--offload", "host", "--offload_moments", "bf16"] if moments == "bf16" else []
+    ref_out, out = str(tmp_path / "ref.safetensors"), str(tmp_path / "disk.safetensors")
+    ref = _single("gpt2_full_finetune", FULL + ["--output_path", ref_out] + ref_args, "--batch_size", 4)
+    d = str(tmp_path / "offload")
+    r = subprocess.run([_bin("gpt2_full_finetune"), *FULL, "--batch_size", "4", "--output_path", out, "--offload", "disk",
+                        "--offload_dir", d, "--offload_moments", moments], capture_output=True, text=True, timeout=150,
+                       env=_env(**env_chunk))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "AdamW moments on disk" in r.stdout and "step runs eagerly" in r.stdout, r.stdout[:3000]
+    got, want = loss_list(r.stdout, True), loss_list(ref.stdout, True)
+    assert len(got) == 6 and got == pytest.approx(want, rel=1e-5, abs=1e-5), (got, want)
+    from mobilefinetuner_amd.io import safetensors as st
+    a, b = st.load_file(ref_out), st.load_file(out)
+    for k in a:
+        assert torch.allclose(a[k], b[k], atol=1e-5, rtol=1e-5), (k, (a[k] - b[k]).abs().max())
+    for name in ("m", "v"):
+        f = os.path.join(d, f"adamw_{name}.rank0.bin")
+        assert os.path.getsize(f) > 0 and any(open(f, "rb").read(1 << 16)), f  # written back, not all zero
 
 
 def test_native_dp_lora_and_gemma_two_ranks():
