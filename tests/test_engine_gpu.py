@@ -300,12 +300,16 @@ def test_native_weight_streaming_matches_resident(tmp_path):
     ("gpt2_lora_finetune", "gpt2-tiny", "--steps", ["--batch_size", "4", "--warmup_steps", "100", "--lora_dropout", "0.1"]),
     ("train_lora_gemma", "gemma3-tiny", "--max_steps", ["--batch", "4", "--lr_schedule", "constant",
                                                         "--lora_dropout", "0.1"]),
+    # full fine-tune with the AdamW moments on disk (--offload disk): saved from / restored into the file mappings
+    ("gpt2_full_finetune", "gpt2-tiny", "--steps", ["--batch_size", "4", "--warmup_steps", "100", "--offload", "disk",
+                                                    "--offload_moments", "fp32", "--offload_dir", "{tmp}/offload"]),
 ])
 def test_native_full_state_resume(tmp_path, prog, model, steps_flag, extra):
     """--state_dir: 4 steps, then a fresh process resumes from the saved state (fp32 master, AdamW
     moments + step, data cursor / shuffle RNG, EMA, LoRA-dropout counter) and runs steps 5-8; its
     losses equal the uninterrupted 8-step run's (deterministic mode; the schedule is chosen so the
     learning rate does not depend on the run's total step count)."""
+    extra = [x.replace("{tmp}", str(tmp_path)) for x in extra]
     common = [_bin(prog), "--random_init", "--model", model, "--synthetic_data", "--synthetic_tokens", "100000",
               "--seq_len", "64", "--lr", "1e-3", "--log_interval", "1", "--deterministic", *extra]
 
