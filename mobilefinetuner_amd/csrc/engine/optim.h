@@ -90,6 +90,8 @@ class AdamW {
   // kernel writes the rest back to the file -- and step() streams them through two device chunk buffers
   // (mapping -> pinned staging -> device -> fused AdamW -> back), chunk by chunk.  Host copies run inside
   // the step, so it is not graph-capturable (the trainer runs it eagerly).  Call after shard().
+  // (SURVEY §5.6's `--offload none|host|disk`; the reference's own disk tier holds frozen weights only,
+  // opt_ops/sharding/parameter_sharder.cpp:94-276 -- here engine/weight_stream.h's --shard_dir.)
   void to_disk(const std::string& dir, int rank, bool fp32);
   bool moments_on_disk() const { return disk_.active; }
   ~AdamW();
