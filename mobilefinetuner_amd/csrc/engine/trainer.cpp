@@ -36,9 +36,9 @@ Trainer::Trainer(LanguageModel& model, FlatParams& flat, AdamW& opt, TokenDatase
     graph_comm_ = true;
   }
   if (cfg_.use_graph && dp_ && !dp_->graph_capturable()) {
-    // the staged host-moment ZeRO-3 optimizer: its copy-stream / communication-stream ping-pong crashes
-    // hipStreamEndCapture on this ROCm, and eager measured faster for it anyway (profiles/r5_offload_staged.txt)
-    std::printf("[trainer] step runs eagerly (no hipGraph): staged host-moment optimizer\n");
+    // the staged host-moment ZeRO-3 optimizer: eager by default, faster than its captured form
+    // (engine/zero3.h graph_capturable(); MFT_Z3_CAPTURE=1 captures it)
+    std::printf("[trainer] step runs eagerly (no hipGraph): staged host-moment optimizer (faster eager; MFT_Z3_CAPTURE=1)\n");
     cfg_.use_graph = false;
   }
   if (cfg_.use_graph && opt_.moments_on_disk()) {  // host copies from the file mappings inside the step
@@ -136,9 +136,15 @@ void Trainer::capture() {
   if (graph_comm_) eager_step();
   else fwd_bwd();
   if (std::getenv("MFT_Z3_TRACE")) std::fprintf(stderr, "[trainer] ending capture\n");
+  const auto tc0 = std::chrono::steady_clock::now();
   HIP_OK(hipStreamEndCapture(stream_, &graph_));
   CachingAllocator::set_current_pool(0);
-  if (std::getenv("MFT_Z3_TRACE")) std::fprintf(stderr, "[trainer] captured; instantiating\n");
+  if (std::getenv("MFT_Z3_TRACE")) {
+    size_t nn = 0;
+    (void)hipGraphGetNodes(graph_, nullptr, &nn);
+    std::fprintf(stderr, "[trainer] captured %zu nodes in %.1f ms; instantiating\n", nn,
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count());
+  }
   HIP_OK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
   if (std::getenv("MFT_Z3_TRACE")) std::fprintf(stderr, "[trainer] instantiated\n");
 }

@@ -367,7 +367,10 @@ void Zero3::gather(int u) {
   HIP_OK(hipStreamWaitEvent(stream_, order_, 0));
   if (sopt_ && primed_ && grad_enabled()) {  // the previous step's update of this partition first (gated on device)
     opt_update(1 + u);
-    HIP_OK(hipStreamWaitEvent(stream_, upd_ev_[1 + u], 0));
+    // (staged: the update ran on this same stream, already in order.  A stream waiting on an event it
+    // recorded itself is a self-edge in a captured graph: hipStreamEndCapture then recursed without end
+    // -- a stack-overflow segfault, or a hang with an unlimited stack; profiles/r6_z3_capture_trace.txt)
+    if (!staged_) HIP_OK(hipStreamWaitEvent(stream_, upd_ev_[1 + u], 0));
   }
   const ::mft::bf16_t* src = (const ::mft::bf16_t*)flat_.shadow.data_ptr() + un.local;
   comm_.all_gather(src, slot_[un.slot].data_ptr(), (size_t)un.s, CommType::BF16, stream_);

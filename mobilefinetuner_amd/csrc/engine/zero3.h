@@ -87,10 +87,13 @@ class Zero3 : public GradReducer, public BlockProvider {
   void prepare_optimizer() override;
   void flush_optimizer() override;
   void optimizer_state_loaded() override;
-  // (MFT_Z3_CAPTURE=1: capture the staged step anyway -- diagnosis of its capture crash)
+  // The staged step captures since round 6 (it crashed hipStreamEndCapture before: gather() made the
+  // communication stream wait on an event it had recorded itself -- a self-edge in the captured graph;
+  // profiles/r6_z3_capture_trace.txt), but it runs eagerly by default: as graph memcpy nodes its SDMA
+  // moment copies measured 57 K against 80 K tok/s eager (gpt2-xl).  MFT_Z3_CAPTURE=1 captures it.
   bool graph_capturable() const override {
-    static const bool force = std::getenv("MFT_Z3_CAPTURE") && std::getenv("MFT_Z3_CAPTURE")[0] == '1';
-    return force || !(sopt_ && staged_);
+    static const bool on = std::getenv("MFT_Z3_CAPTURE") && std::getenv("MFT_Z3_CAPTURE")[0] == '1';
+    return on || !(sopt_ && staged_);
   }
   int staged_slots() const { return sopt_ && staged_ ? nslot_ : 0; }  // 0: in place (or no host moments)
   bool params_sharded() const override { return true; }

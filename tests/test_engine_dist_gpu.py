@@ -237,23 +237,26 @@ def test_native_zero3_streamed_optimizer_flushes_in_graph_mode(tmp_path, every):
         assert torch.allclose(a[k], b[k], atol=2e-5, rtol=0), (every, k, (a[k] - b[k]).abs().max())
 
 
-@pytest.mark.parametrize("slots,moments", [("1", "fp32"), ("2", "bf16"), ("", "bf16")])
-def test_native_zero3_staged_moments_match_in_place(tmp_path, slots, moments):
+@pytest.mark.parametrize("slots,moments,capture", [("1", "fp32", ""), ("2", "bf16", ""), ("", "bf16", ""), ("", "bf16", "1"),
+                                                   ("1", "fp32", "1")])
+def test_native_zero3_staged_moments_match_in_place(tmp_path, slots, moments, capture):
     """The staged host-moment optimizer (device slots refilled by SDMA copies on one copy stream: the slot
     written back after its update and prefetched for its next user, across the step boundary) ends with the
-    same weights as the in-place zero-copy update (MFT_Z3_STAGED=0), both eager (the staged step never
-    captures), two loopback ranks, evaluations (flushes) every 2 steps -- with one slot (every update
-    waits for its own prefetch), two, and the default."""
+    same weights as the in-place zero-copy update (MFT_Z3_STAGED=0, eager), two loopback ranks, evaluations
+    (flushes) every 2 steps -- with one slot (every update waits for its own prefetch), two, and the
+    default; eager (the default: faster for this step) and captured in a hipGraph (MFT_Z3_CAPTURE=1, since
+    the round-6 fix of the communication stream's self-wait)."""
     base = FULL + ["--batch_size", "4", "--zero_stage", "3", "--offload", "host", "--offload_moments", moments]
     ref_out, out = str(tmp_path / "inplace.safetensors"), str(tmp_path / "staged.safetensors")
     ref = _run_ranks([_bin("gpt2_full_finetune"), *base, "--no_graph", "--output_path", ref_out], 2,
                      extra_env={"MFT_Z3_STAGED": "0"})
     assert all(rc == 0 for rc, _, _ in ref), ref[0][1][-2000:] + ref[0][2][-2000:]
-    env = {"MFT_Z3_STAGED": "1", **({"MFT_Z3_SLOTS": slots} if slots else {})}
+    env = {"MFT_Z3_STAGED": "1", **({"MFT_Z3_SLOTS": slots} if slots else {}), **({"MFT_Z3_CAPTURE": capture} if capture else {})}
     got = _run_ranks([_bin("gpt2_full_finetune"), *base, "--eval_interval", "2", "--eval_batches", "2",
                       "--output_path", out], 2, extra_env=env)
     assert all(rc == 0 for rc, _, _ in got), got[0][1][-2000:] + got[0][2][-2000:]
-    assert "step runs eagerly" in got[0][1] and "slots]" in got[0][1], got[0][1][:3000]
+    mode = "hipGraph-captured step" if capture == "1" else "step runs eagerly"
+    assert mode in got[0][1] and "slots]" in got[0][1], got[0][1][:3000]
     assert loss_list(got[0][1], True) == pytest.approx(loss_list(ref[0][1], True), rel=2e-4, abs=2e-4)
     from mobilefinetuner_amd.io import safetensors as st
     a, b = st.load_file(ref_out), st.load_file(out)
