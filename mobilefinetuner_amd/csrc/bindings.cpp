@@ -647,8 +647,9 @@ std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, 
   a.aux = X.defined() ? bp(X) : nullptr; a.ldaux = X.defined() ? X.stride(0) : 0;
   a.M = M; a.N = N; a.K = K; a.alpha = (float)alpha;
   Tensor ws;
+  const bool tn4 = impl == 4 && a_t && b_t;  // the 4-wave TN weight-gradient kernel (gemm4_tn)
   if (f32) {
-    a.ksplit = mft::gemm8_pick_ksplit(M, N, K);
+    a.ksplit = tn4 ? mft::gemm4_tn_pick_ksplit(M, N, K) : mft::gemm8_pick_ksplit(M, N, K);
     if (a.ksplit > 1) {
       ws = torch::empty({(long)a.ksplit * M * N}, A.options().dtype(torch::kFloat32));
       a.ws = fp(ws);
@@ -668,6 +669,9 @@ std::vector<Tensor> gemm_t(Tensor A, Tensor B, bool a_t, bool b_t, int64_t epi, 
   if (impl == 5) {
     TORCH_CHECK(!a_t && !b_t && mft::gemm_s_supported(M, N, K, (int)epi), "gemm_t: shape / epilogue not supported by gemm_s");
     mft::gemm_s(a, (int)epi, stream());
+  } else if (tn4) {
+    TORCH_CHECK(f32 && mft::gemm4_tn_supported(M, N, K, a.lda, a.ldb), "gemm_t: gemm4 TN needs the F32ACC epilogue and a supported shape");
+    mft::gemm4_tn(a, stream());
   } else if (impl == 4) {
     TORCH_CHECK(mft::gemm4_supported(M, N, K, a_t, b_t), "gemm_t: shape / layout not supported by gemm4");
     mft::gemm4x(a, (int)epi, a_t, b_t, stream());

@@ -318,6 +318,34 @@ void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
   MFT_CHECK(buf.dtype() == DType::F32 && buf.is_contiguous(), "gemm_wgrad: fp32 contiguous grad buffer");
   const long M = dy2.size(0), N = dy2.size(1), K = x2.size(1);
   MFT_CHECK(x2.size(0) == M && buf.numel() == N * K, "gemm_wgrad: shapes");
+  // the 4-wave TN kernel (gemm4_tn: AGPR accumulators, transposed LDS reads, token split into fp32 slabs);
+  // MFT_WGRAD=gemm8 keeps the 8-wave kernel below (A/B)
+  static const bool wg8 = getenv("MFT_WGRAD") && std::string(getenv("MFT_WGRAD")) == "gemm8";
+  if (!wg8 && M % 64 == 0 && dy2.dtype() == DType::BF16 && x2.dtype() == DType::BF16 &&
+      ::mft::gemm4_tn_supported((int)N, (int)K, (int)M, dy2.stride(0), x2.stride(0))) {
+    ::mft::GemmArgs g{};
+    g.A = (const ::mft::bf16_t*)dy2.data_ptr();
+    g.lda = dy2.stride(0);
+    g.B = (const ::mft::bf16_t*)x2.data_ptr();
+    g.ldb = x2.stride(0);
+    g.C = buf.data_ptr();
+    g.ldc = K;
+    g.M = (int)N;
+    g.N = (int)K;
+    g.K = (int)M;
+    g.alpha = alpha;
+    g.ksplit = ::mft::gemm4_tn_pick_ksplit((int)N, (int)K, (int)M);
+    map_line("wgrad", N, K, M, g.ksplit > 1 ? "gemm4_tn split-K" : "gemm4_tn");
+    void* ws = nullptr;
+    auto& al = CachingAllocator::get(cur_dev());
+    if (g.ksplit > 1) {
+      ws = al.allocate((size_t)g.ksplit * N * K * 4, current_stream());
+      g.ws = (float*)ws;
+    }
+    ::mft::gemm4_tn(g, current_stream());
+    if (ws) al.release(ws);
+    return;
+  }
   // gemm8 TN (both operands token-major, read with ds_read_b64_tr_b16) with the F32ACC epilogue straight
   // into the flat grad, split-K over the tokens when the output alone does not fill the CUs
   if (M % 64 == 0 && N % 8 == 0 && K % 8 == 0 && dy2.stride(0) % 8 == 0 && x2.stride(0) % 8 == 0 &&

@@ -145,6 +145,11 @@ void gemm8x(const GemmArgs& g, int epi, bool a_t, bool b_t, hipStream_t st);
 // 256x256x64 4-wave GEMM with a hand-scheduled K-tile body (gemm4.hip); NT layout
 void gemm4x(const GemmArgs& g, int epi, bool a_t, bool b_t, hipStream_t st);
 bool gemm4_supported(int M, int N, int K, bool a_t, bool b_t);
+// TN weight gradient on the 4-wave kernel: C fp32 [M, N] (ldc) += alpha A^T B, A [K, M] (lda), B [K, N]
+// (ldb), K = tokens; ksplit > 1 (gemm4_tn_pick_ksplit) needs ws = ksplit x M x N floats
+bool gemm4_tn_supported(int M, int N, int K, long lda, long ldb);
+int gemm4_tn_pick_ksplit(int M, int N, int K);
+void gemm4_tn(const GemmArgs& g, hipStream_t st);
 // persistent gemm4 grids leave n CUs free (for a long-running kernel on a side stream; 0 = every CU)
 void gemm4_reserve_cus(int n);
 // short-token NT GEMM (gemm_s.hip): 64 x 64 tiles, K split over the 4 waves; NONE / BIAS / BIAS_GELU_D /

@@ -279,6 +279,105 @@ def set0_read_explicit():
             '    :  \\\n    : [ra0] "v"(RA0), [rb00] "v"(RB[0]), [rb01] "v"(RB[1])  \\\n    : "memory", ' + regs + ")\n")
 
 
+def ktile_tn(bar_a=32, wait_at=96, late_at=97, late_per=2, early_per=1, dma_at0=None, dma_step=4):
+    """TN K-tile (weight gradient dW = dy^T x, both operands token-major): the LDS images are [64 k][256
+    columns] (512-B rows, 16-B chunks XOR-swizzled on bits 1..3 by the row), and a fragment is TWO
+    ds_read_b64_tr_b16 (rows k .. k + 3 and k + 4 .. k + 7 of a 16-lane group -> the lane's column, CDNA
+    HIP guide T10) into the halves of its 4-VGPR register.  The swizzle makes fragment i's address
+    base + 32 (i ^ t) with a per-lane t, so every fragment has its own address VGPR (%[ra{i}] / %[rb{j}],
+    16 in all); the k-step (16384 B) and the half (2048 B) are immediate offsets, and one v_xor of all 16
+    moves them to the other buffer.  Schedule (per K-tile t, buffer cur = t & 1; the product placement
+    TN_VARIANTS["GEMM4_KTILE_TN_X"]):
+        MFMA 0..15    32 reads of (t, ks 1) -> set 1 (two per MFMA)
+        MFMA 16       lgkmcnt(0) + barrier: buffer cur is free
+        MFMA 17..107  16 LDS-DMA pieces of K-tile t + 2 -> buffer cur (one per 6 MFMAs)
+        MFMA 112      vmcnt(16) + barrier: K-tile t + 1 landed; the 16 addresses -> buffer cur ^ 1
+        MFMA 112..127 32 reads of (t + 1, ks 0) -> set 0 (two per MFMA); lgkmcnt(0) at the end"""
+    order = [(i, j) for i in range(8) for j in range(8)]
+    reads = []
+    for kind, idx in read_order():
+        reads += [(kind, idx, 0), (kind, idx, 1)]
+
+    def rd(s, ks, r):
+        kind, idx, h = r
+        b = FRAG_BASE + 64 * s + (0 if kind == "a" else 32) + 4 * idx + 2 * h
+        return f"ds_read_b64_tr_b16 v[{b}:{b + 1}], %[r{kind}{idx}] offset:{ks * 16384 + h * 2048}"
+
+    def dma_tn(kind, j):
+        off = (0 if kind == "a" else 32768) + j * 4096
+        return [f"s_add_u32 m0, %[ldsm], {off}", "s_nop 0",
+                f"buffer_load_dwordx4 %[o{kind}{j}], %[srd{kind}], %[koff{kind}] offen lds"]
+
+    dmas = [dma_tn("a", j) for j in range(8)] + [dma_tn("b", j) for j in range(8)]
+    d0 = bar_a + 1 if dma_at0 is None else dma_at0
+    dma_at = {d0 + dma_step * q: q for q in range(16)}
+    assert max(dma_at) < wait_at and min(dma_at) > bar_a and 32 // early_per <= bar_a
+    late = {}
+    for q in range(32):
+        late.setdefault(late_at + q // late_per, []).append(q)
+    assert max(late) < 128
+    lines = ["s_nop 4"]
+    for n in range(128):
+        ks, (i, j) = n // 64, order[n % 64]
+        if n == bar_a:
+            lines += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+        if n == wait_at:
+            lines += ["s_waitcnt vmcnt(16)", "s_barrier"]
+            lines += [f"v_xor_b32 %[r{k}{x}], 0x10000, %[r{k}{x}]" for k in "ab" for x in range(8)]
+        for q in range(n * early_per, (n + 1) * early_per):
+            if q < 32:
+                lines.append(rd(1, 1, reads[q]))
+        for q in late.get(n, []):
+            lines.append(rd(0, 0, reads[q]))
+        if n in dma_at:
+            lines += dmas[dma_at[n]]
+        lines.append(mfma(ks, i, j))
+    lines.append("s_waitcnt lgkmcnt(0)")
+    return lines
+
+
+# TN schedule variants (gemm4.hip gemm4_tn_kernel template SCHED, MFT_WGRAD_SCHED=0..2 for A/B)
+TN_VARIANTS = {
+    # 0 (product): k-step-1 reads two per MFMA (0..15), DMAs one per 6 MFMAs (17..107), the wait late (112),
+    # the next k-step-0 reads two per MFMA -- the best of 7 placements measured (profiles/r6_wgrad_tn.txt)
+    "GEMM4_KTILE_TN_X": dict(early_per=2, bar_a=16, dma_at0=17, dma_step=6, wait_at=112, late_at=112),
+    "GEMM4_KTILE_TN_X1": dict(dma_step=5, wait_at=110, late_at=110),               # 1: reads one per MFMA
+    "GEMM4_KTILE_TN_X2": dict(dma_step=4, wait_at=96, late_at=97),                 # 2: the first placement
+}
+
+
+def emit_tn(name, lines):
+    ins = [f'[ra{i}] "+v"(RA[{i}])' for i in range(8)] + [f'[rb{j}] "+v"(RB[{j}])' for j in range(8)]
+    ins_only = [f'[oa{j}] "v"(OA[{j}])' for j in range(8)] + [f'[ob{j}] "v"(OB[{j}])' for j in range(8)]
+    ins_only += ['[srda] "s"(SRDA)', '[srdb] "s"(SRDB)', '[koffa] "s"(KOFFA)', '[koffb] "s"(KOFFB)', '[ldsm] "s"(LDSM)']
+    body = "".join(f'    "{l}\\n"  \\\n' for l in explicit(lines))
+    return (f"#define {name}(RA, RB, OA, OB, SRDA, SRDB, KOFFA, KOFFB, LDSM) \\\n"
+            f"  asm volatile(  \\\n{body}"
+            f"    : {', '.join(ins)}  \\\n"
+            f"    : {', '.join(ins_only)}  \\\n"
+            '    : "memory", "scc", ' + clobbers() + ")\n")
+
+
+def tn_set0_read():
+    """The first k-step's fragments (buffer of RA / RB, ks 0) into set 0, waited for."""
+    lines = []
+    for kind, idx in read_order():
+        for h in range(2):
+            b = FRAG_BASE + (0 if kind == "a" else 32) + 4 * idx + 2 * h
+            lines.append(f"ds_read_b64_tr_b16 v[{b}:{b + 1}], %[r{kind}{idx}] offset:{h * 2048}")
+    lines.append("s_waitcnt lgkmcnt(0)")
+    body = "".join(f'    "{l}\\n"  \\\n' for l in lines)
+    ins = [f'[ra{i}] "v"(RA[{i}])' for i in range(8)] + [f'[rb{j}] "v"(RB[{j}])' for j in range(8)]
+    regs = ", ".join(f'"v{r}"' for r in range(FRAG_BASE, FRAG_BASE + 64))
+    return (f"#define GEMM4_TN_SET0_READ_X(RA, RB) \\\n  asm volatile(  \\\n{body}"
+            f"    :  \\\n    : {', '.join(ins)}  \\\n    : \"memory\", " + regs + ")\n")
+
+
+def zero_acc():
+    body = "".join(f'    "v_accvgpr_write_b32 a{r}, 0\\n"  \\\n' for r in range(256))
+    return "#define GEMM4_ZERO_ACC_X() \\\n  asm volatile(  \\\n" + body + "    ::: " + clobbers(fragments=False) + ")\n"
+
+
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
     out = os.path.join(here, "gemm4_sched.h")
@@ -312,6 +411,17 @@ def main():
             f.write(emit(f"GEMM4_KTILE_NT_P{S}", lines, modes=True))
             f.write("\n")
         f.write(set0_read_explicit())
+        for name, kw in TN_VARIANTS.items():
+            lines = ktile_tn(**kw)
+            assert sum(1 for l in lines if l.startswith("v_mfma")) == 128
+            assert sum(1 for l in lines if l.startswith("ds_read_b64_tr_b16")) == 64
+            assert sum(1 for l in lines if l.startswith("buffer_load")) == 16
+            f.write(f"\n// {name}: weight-gradient K-tile (token-major operands, transposed LDS reads), literal registers {kw}\n")
+            f.write(emit_tn(name, lines))
+            f.write("\n")
+        f.write(tn_set0_read())
+        f.write("\n")
+        f.write(zero_acc())
     print(out)
 
 

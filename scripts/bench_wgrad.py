@@ -1,7 +1,8 @@
 """Weight-gradient GEMMs (dW[N, K] += dy^T x, fp32 accumulate into the flat grad buffer) and the
-plain NT forwards on the GPT-2 small / XL training shapes: gemm8 (split-K from gemm8_pick_ksplit)
-vs hipBLASLt (torch.mm, bf16 out -- a lower bound on its fp32-accumulate cost).  Each gemm8 result
-is checked against an fp32 reference first.  Interleaved rounds, min over rounds.
+plain NT forwards on the GPT-2 small / XL training shapes: the 4-wave TN kernel (gemm4_tn, split from
+gemm4_tn_pick_ksplit) vs the 8-wave gemm8 (split from gemm8_pick_ksplit) vs torch.mm (bf16 out -- a
+lower bound on an fp32-accumulate cost).  Each result is checked against an fp32 reference first.
+Interleaved rounds, min over rounds.
 
 usage: PYTHONPATH=. python scripts/bench_wgrad.py [--iters 10] [--rounds 3]
 """
@@ -32,26 +33,29 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     C = native()
-    wg = [("gpt2 qkv", 65536, 2304, 768), ("gpt2 proj", 65536, 768, 768), ("gpt2 fc", 65536, 3072, 768),
-          ("gpt2 mproj", 65536, 768, 3072), ("xl qkv", 8192, 4800, 1600), ("xl proj", 8192, 1600, 1600),
-          ("xl fc", 8192, 6400, 1600), ("xl mproj", 8192, 1600, 6400)]
+    T, TX = 131072, 32768  # bench.py gpt2-full (1024 x 128) and gpt2-xl (256 x 128) tokens per step
+    wg = [("gpt2 qkv", T, 2304, 768), ("gpt2 proj", T, 768, 768), ("gpt2 fc", T, 3072, 768),
+          ("gpt2 mproj", T, 768, 3072), ("xl qkv", TX, 4800, 1600), ("xl proj", TX, 1600, 1600),
+          ("xl fc", TX, 6400, 1600), ("xl mproj", TX, 1600, 6400)]
     for name, M, N, K in wg:
         dy = (torch.randn(M, N, device="cuda") * 0.1).bfloat16()
         x = torch.randn(M, K, device="cuda").bfloat16()
         ref = dy.float().t() @ x.float()
-        buf = torch.zeros(N, K, device="cuda")
-        C.gemm_t(dy, x, True, True, F32ACC, alpha=1.0, out=buf)
-        err = ((buf - ref).abs().max() / ref.abs().max()).item()
-        assert err < 1e-2, (name, err)
+        err = {}
+        for impl in (4, 0):
+            buf = torch.zeros(N, K, device="cuda")
+            C.gemm_t(dy, x, True, True, F32ACC, None, None, 1.0, buf, None, None, impl)
+            err[impl] = ((buf - ref).abs().max() / ref.abs().max()).item()
+            assert err[impl] < 1e-4, (name, impl, err[impl])
         fl = 2.0 * M * N * K
-        g8, lt = [], []
+        g4, g8, lt = [], [], []
         for _ in range(a.rounds):
-            g8.append(timeit(lambda: C.gemm_t(dy, x, True, True, F32ACC, alpha=1.0, out=buf), a.iters))
+            g4.append(timeit(lambda: C.gemm_t(dy, x, True, True, F32ACC, None, None, 1.0, buf, None, None, 4), a.iters))
+            g8.append(timeit(lambda: C.gemm_t(dy, x, True, True, F32ACC, None, None, 1.0, buf, None, None, 0), a.iters))
             lt.append(timeit(lambda: torch.mm(dy.t(), x), a.iters))
-        ks = C.gemm8_pick_ksplit(N, K, M) if hasattr(C, "gemm8_pick_ksplit") else -1
-        print(f"wgrad {name:10s} tokens={M:6d} N={N:5d} K={K:5d} ks={ks:2d} | gemm8 {min(g8):8.1f} us "
-              f"{fl / min(g8) / 1e6:6.0f} TF | hipBLASLt(bf16 out) {min(lt):8.1f} us {fl / min(lt) / 1e6:6.0f} TF "
-              f"| err {err:.1e}", flush=True)
+        print(f"wgrad {name:10s} tokens={M:6d} N={N:5d} K={K:5d} | gemm4_tn {min(g4):7.1f} us {fl / min(g4) / 1e6:5.0f} TF"
+              f" | gemm8 {min(g8):7.1f} us {fl / min(g8) / 1e6:5.0f} TF | torch.mm(bf16 out) {min(lt):7.1f} us "
+              f"{fl / min(lt) / 1e6:5.0f} TF | err {err[4]:.1e} / {err[0]:.1e}", flush=True)
         del dy, x, ref, buf
     nt = [("xl qkv fwd", 8192, 1600, 4800), ("xl proj fwd", 8192, 1600, 1600), ("xl fc fwd", 8192, 1600, 6400),
           ("xl mproj fwd", 8192, 6400, 1600)]

@@ -167,3 +167,34 @@ def test_gemm4_geglu_epilogues_match_fp32(M, I, K):
         a, ag = _gelu(gq)
         assert _rel(dgu[:, :I], dh * uq * ag) < 2e-2, seg
         assert _rel(dgu[:, I:], dh * a) < 2e-2, seg
+
+
+# gemm4 TN (gemm4_tn_kernel): the full fine-tune weight gradient C (fp32) += alpha A^T B over K tokens, both
+# operands token-major.  Shapes: GPT-2 qkv / proj at a token split (fp32 slabs + ordered reduce), the
+# minimum K = 128 (no split), ragged M / N (tiles past the edges read out of range), XL's 1600 columns,
+# and row strides wider than the operands (column views).
+TN_SHAPES = [(2304, 768, 8192, 0), (768, 768, 16384, 0), (256, 256, 128, 0), (1600, 1600, 4096, 0), (200, 72, 640, 0),
+             (776, 264, 2048, 64), (50304, 768, 45056, 0)]  # (the last: the tied LM-head weight, a 4.5 GB operand)
+
+
+@pytest.mark.parametrize("M,N,K,pad", TN_SHAPES)
+def test_gemm4_tn_wgrad_matches_fp32(M, N, K, pad):
+    from mobilefinetuner_amd._ext import native
+    C = native()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    a_full = (torch.rand(K, M + pad, device="cuda", generator=g) * 2 - 1).bfloat16()
+    b_full = (torch.rand(K, N + pad, device="cuda", generator=g) * 2 - 1).bfloat16()
+    a, b = a_full[:, :M], b_full[:, :N]
+    c0 = torch.randn(M, N, device="cuda", generator=g)
+    ref = c0.clone()
+    for k in range(0, K, 8192):
+        ref += 0.5 * (a[k:k + 8192].float().t() @ b[k:k + 8192].float())
+    out = c0.clone()
+    F32ACC = 4
+    C.gemm_t(a, b, True, True, F32ACC, None, None, 0.5, out, None, None, 4)
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 1e-4, _rel(out, ref)
+    # and the 8-wave kernel it replaces agrees
+    out8 = c0.clone()
+    C.gemm_t(a, b, True, True, F32ACC, None, None, 0.5, out8, None, None, 0)
+    assert _rel(out8, out) < 1e-4
