@@ -1,8 +1,9 @@
 // libmft engine: GEMM routing (see gemm.h).  Every product of the engine runs on a hand-written kernel:
 // gemm4 (kernels/gemm4.hip, the 4-wave hand-scheduled persistent NT GEMM) for every K-contiguous
-// product and fused epilogue it carries, gemm8 (kernels/gemm8.hip) for the token-major layouts (split-K
-// weight gradients, NN data gradients of trainable weights without a transposed copy, the LM-head CE
-// dgrad, the LoRA epilogue), and the fp32-MFMA generic fallback (kernels/gemm_simt.hip) for operands neither takes
+// product and fused epilogue it carries, gemm4_tn (the same 4-wave design with token-major K-tiles) for
+// the split-K weight gradients, gemm8 (kernels/gemm8.hip) for the other token-major layouts (NN data
+// gradients of trainable weights without a transposed copy, the LM-head CE dgrad, the LoRA epilogue),
+// and the fp32-MFMA generic fallback (kernels/gemm_simt.hip) for operands neither takes
 // (fp32, K % 64 != 0, unaligned strides).  No vendor GEMM library is linked.
 #include "engine/gemm.h"
 
@@ -384,7 +385,7 @@ void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
     Tensor dyp = zeros({Mp, N}, DType::BF16, dy2.device()), xp = zeros({Mp, K}, DType::BF16, x2.device());
     dyp.slice(0, 0, M).copy_(dy2);
     xp.slice(0, 0, M).copy_(x2);
-    map_line("wgrad (tokens padded to 64)", N, K, M, "gemm8");
+    map_line("wgrad (tokens padded to 64)", N, K, M, "gemm4_tn / gemm8");
     gemm_wgrad(buf, dyp, xp, alpha);
     return;
   }
