@@ -158,50 +158,79 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int j = 0; j < 8; ++j) dwa[c][j] = dba[c][j] = 0.f;
   }
-  for (int row = blockIdx.x * 4 + wid; row < M; row += gridDim.x * 4) {
-    const float mean = RMS ? 0.f : mean_in[row];
-    const float rstd = rstd_in[row];
-    float xh[CH][8], g[CH][8];
-    float s1 = 0.f, s2 = 0.f;
+  // the lane's weights, once
+  float wv[CH][8];
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int ch = lane + c * 64;
-      if (ch < nch) {
-        float xv[8], dv[8];
-        load8(x + (long)row * N + ch * 8, xv);
-        load8(dy + (long)row * lddy + ch * 8, dv);
-        const float4* w4 = reinterpret_cast<const float4*>(w + ch * 8);
-        float4 wa = w4[0], wb = w4[1];
-        float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+  for (int c = 0; c < CH; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      const float4* w4 = reinterpret_cast<const float4*>(w + ch * 8);
+      const float4 wa = w4[0], wb = w4[1];
+      wv[c][0] = wa.x + w_offset, wv[c][1] = wa.y + w_offset, wv[c][2] = wa.z + w_offset, wv[c][3] = wa.w + w_offset;
+      wv[c][4] = wb.x + w_offset, wv[c][5] = wb.y + w_offset, wv[c][6] = wb.z + w_offset, wv[c][7] = wb.w + w_offset;
+    }
+  }
+  // U rows per wave per iteration, every load of the U rows issued before the first is used: the
+  // weight-gradient form runs a bounded grid (512 blocks, one row at a time left it latency-bound at
+  // ~2 TB/s: a few MB in flight across the chip)
+  constexpr int U = WGRAD ? 4 : 1;
+  const int stride = gridDim.x * 4;
+  for (int row0 = blockIdx.x * 4 + wid; row0 < M; row0 += stride * U) {
+    u16x8_t xr[U][CH], dr[U][CH], rr[U][CH];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xh[c][j] = (xv[j] - mean) * rstd;
-          g[c][j] = dv[j] * (wv[j] + w_offset);
-          s1 += g[c][j];
-          s2 += g[c][j] * xh[c][j];
-          if (WGRAD) {
-            dwa[c][j] += dv[j] * xh[c][j];
-            dba[c][j] += dv[j];
-          }
+    for (int u = 0; u < U; ++u) {
+      const int row = row0 + u * stride;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int ch = lane + c * 64;
+        if (row < M && ch < nch) {
+          xr[u][c] = *reinterpret_cast<const u16x8_t*>(x + (long)row * N + ch * 8);
+          dr[u][c] = *reinterpret_cast<const u16x8_t*>(dy + (long)row * lddy + ch * 8);
+          if (dresid) rr[u][c] = *reinterpret_cast<const u16x8_t*>(dresid + (long)row * N + ch * 8);
         }
       }
     }
-    s1 = RMS ? 0.f : wave_sum(s1) / N;
-    s2 = wave_sum(s2) / N;
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int ch = lane + c * 64;
-      if (ch < nch) {
-        float o[8];
+    for (int u = 0; u < U; ++u) {
+      const int row = row0 + u * stride;
+      if (row >= M) break;  // (wave-uniform)
+      const float mean = RMS ? 0.f : mean_in[row];
+      const float rstd = rstd_in[row];
+      float xh[CH][8], g[CH][8];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[c][j] - s1 - xh[c][j] * s2);
-        if (dresid) {
-          float r[8];
-          load8(dresid + (long)row * N + ch * 8, r);
+      for (int c = 0; c < CH; ++c) {
+        const int ch = lane + c * 64;
+        if (ch < nch) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
+          for (int j = 0; j < 8; ++j) {
+            const float dv = bf2f(dr[u][c][j]);
+            xh[c][j] = (bf2f(xr[u][c][j]) - mean) * rstd;
+            g[c][j] = dv * wv[c][j];
+            s1 += g[c][j];
+            s2 += g[c][j] * xh[c][j];
+            if (WGRAD) {
+              dwa[c][j] += dv * xh[c][j];
+              dba[c][j] += dv;
+            }
+          }
         }
-        store8(dx + (long)row * N + ch * 8, o);
+      }
+      s1 = RMS ? 0.f : wave_sum(s1) / N;
+      s2 = wave_sum(s2) / N;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int ch = lane + c * 64;
+        if (ch < nch) {
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = rstd * (g[c][j] - s1 - xh[c][j] * s2);
+          if (dresid) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] += bf2f(rr[u][c][j]);
+          }
+          store8(dx + (long)row * N + ch * 8, o);
+        }
       }
     }
   }
