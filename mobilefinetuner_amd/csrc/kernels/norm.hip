@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
 // plus optional dresid added in (residual branch of a fused add+norm).  dw/db partials are
 // accumulated per block over its rows (grid-stride) into part[blockIdx][N] (fp32); a second tiny
 // kernel sums the partials, so no float atomics are needed and the result is deterministic.
-template <int CH, bool RMS, bool WGRAD>
+template <int CH, bool RMS, bool WGRAD, int U = WGRAD ? 4 : 1>
 __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                        const float* __restrict__ w, const float* __restrict__ mean_in,
                                                        const float* __restrict__ rstd_in, const bf16_t* __restrict__ dresid,
@@ -173,7 +173,6 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
   // U rows per wave per iteration, every load of the U rows issued before the first is used: the
   // weight-gradient form runs a bounded grid (512 blocks, one row at a time left it latency-bound at
   // ~2 TB/s: a few MB in flight across the chip)
-  constexpr int U = WGRAD ? 4 : 1;
   const int stride = gridDim.x * 4;
   for (int row0 = blockIdx.x * 4 + wid; row0 < M; row0 += stride * U) {
     u16x8_t xr[U][CH], dr[U][CH], rr[U][CH];
@@ -325,7 +324,9 @@ static void norm_bwd_dispatch(const bf16_t* x, const bf16_t* dy, const float* w,
   const int nch = N / 8, ch = (nch + 63) / 64;
   const bool wgrad = dw != nullptr;
   // with weight grads: a bounded grid so the partial buffer stays small (work: 2*nb*N floats)
-  const int nb = wgrad ? norm_bwd_partial_blocks(M) : cdiv(M, 4);
+  // without weight grads: U rows per wave (MFT_NORM_BWD_U=1|2, A/B), the grid covering M once
+  static const int unw = getenv("MFT_NORM_BWD_U") && getenv("MFT_NORM_BWD_U")[0] == '2' ? 2 : 1;
+  const int nb = wgrad ? norm_bwd_partial_blocks(M) : cdiv(M, 4 * unw);
   float* dw_part = work;
   float* db_part = work ? work + (long)nb * N : nullptr;
   const size_t shm = wgrad ? sizeof(float) * 8 * N : 0;
@@ -333,6 +334,8 @@ static void norm_bwd_dispatch(const bf16_t* x, const bf16_t* dy, const float* w,
 #define MFT_NB(CHV)                                                                                           \
   if (wgrad)                                                                                                  \
     norm_bwd_kernel<CHV, RMS, true><<<grid, block, shm, st>>>(x, dy, w, mean, rstd, dresid, dx, dw_part, db_part, M, N, w_offset, lddy); \
+  else if (unw == 2)                                                                                          \
+    norm_bwd_kernel<CHV, RMS, false, 2><<<grid, block, 0, st>>>(x, dy, w, mean, rstd, dresid, dx, dw_part, db_part, M, N, w_offset, lddy); \
   else                                                                                                        \
     norm_bwd_kernel<CHV, RMS, false><<<grid, block, 0, st>>>(x, dy, w, mean, rstd, dresid, dx, dw_part, db_part, M, N, w_offset, lddy);
   if (ch <= 1) { MFT_NB(1) }
