@@ -301,6 +301,11 @@ void lm_head_ce(Tensor h, Tensor W, Tensor labels, int64_t V, c10::optional<Tens
   a.dh = dh.has_value() ? bp(*dh) : nullptr; a.lddh = dh.has_value() ? dh->stride(0) : 0;
   a.materialize = materialize;
   a.ws = fp(ws);
+  Tensor wt;  // the engine's form: with E := dlogits, dh = dlogits W on gemm4 through W^T
+  if (materialize && dh.has_value()) {
+    wt = W.t().contiguous();
+    a.Wt = bp(wt); a.ldwt = wt.stride(0);
+  }
   mft::lm_head_ce(a, stream());
 }
 Tensor logsoftmax_gather(Tensor logits, Tensor idx, int64_t V) {

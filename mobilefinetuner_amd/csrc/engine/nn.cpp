@@ -1068,6 +1068,13 @@ Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_
   const bool need = need_h || need_w;
   Tensor dh = need ? empty({M, C}, DType::BF16, h.device()) : Tensor();
   Tensor wbuf = need_w ? grad_buffer(w.leaf).view({Vp, C}) : Tensor();
+  // the trainable (tied) head: dh = dlogits W on gemm4 through W^T, one transposed copy per call (|W|
+  // bytes, against the 4 x 32768 x Vp dlogits the chunks' products read)
+  Tensor wt;
+  if (need_h && need_w) {
+    NoGradGuard ng;
+    wt = w.c.t().contiguous();
+  }
   if (chunk <= 0) chunk = M;
   for (int64_t i = 0; i < M; i += chunk) {
     const int64_t r = std::min(chunk, M - i);
@@ -1087,6 +1094,7 @@ Tensor lm_head_ce(const Tensor& h, Param& w, const Tensor& labels, int V, int64_
     a.dh = need ? bp(dh) + i * C : nullptr; a.lddh = C;
     a.materialize = need_w ? 1 : 0;
     a.ws = fp(ws);
+    if (wt.defined()) a.Wt = bp(wt), a.ldwt = wt.stride(0);
     ::mft::lm_head_ce(a, S());
     if (need_w) gemm_wgrad(wbuf, E, hi, w_grad_scale);
   }

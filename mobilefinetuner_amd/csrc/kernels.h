@@ -231,6 +231,7 @@ struct CeArgs {
   bf16_t* dh; long lddh;       // [M, K] out (null: no gradient)
   int materialize;             // E := dlogits (for a W gradient by the caller)
   float* ws;                   // lm_head_ce_ws_floats(M, Vpad, K) floats
+  const bf16_t* Wt; long ldwt; // optional W^T [K, Vpad] (materialize): dh = dlogits W as gemm4's NT product
 };
 long lm_head_ce_ws_floats(int M, int Vpad, int K);
 // vocab splits of the CE dgrad for an M-row chunk (1 = one pass straight into dh)

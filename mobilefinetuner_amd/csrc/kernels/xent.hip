@@ -405,7 +405,16 @@ void lm_head_ce(const CeArgs& a, hipStream_t st) {
   if (a.materialize) {
     ce_materialize_kernel<<<a.M, 256, 0, st>>>(a.E, a.lde, a.Vpad, reinterpret_cast<const float2*>(L.stats), T, lse,
                                                a.labels, a.V, a.scale, a.extra);
-    gemm8x(d, GEMM_EPI_NONE, false, true, st);
+    // with the caller's W^T: the 4-wave NT kernel (K = Vpad contiguous in both operands) instead of the
+    // 8-wave NN form (MFT_CE_NN8=1 keeps it, A/B)
+    static const bool nn8 = getenv("MFT_CE_NN8") && getenv("MFT_CE_NN8")[0] == '1';
+    if (!nn8 && a.Wt && a.ldwt % 8 == 0 && a.lde % 8 == 0 && gemm4_supported(a.M, a.K, a.Vpad, false, false)) {
+      d.B = a.Wt;
+      d.ldb = a.ldwt;
+      gemm4x(d, GEMM_EPI_NONE, false, false, st);
+    } else {
+      gemm8x(d, GEMM_EPI_NONE, false, true, st);
+    }
   } else {
     d.ce_labels = a.labels; d.ce_ratio = L.ratio; d.ce_fin = L.fin; d.ce_wlab = L.wlab;
     if (S > 1) {
