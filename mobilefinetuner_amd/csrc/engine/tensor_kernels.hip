@@ -197,6 +197,27 @@ __global__ void copy_kernel(Desc d, Desc s, int64_t n) {
   }
 }
 
+// 2-D transpose (same dtype): d [R, C] row-major (row stride ld) = the transpose of the row-major source
+// S [C, R] (row stride ls), through a 64 x 64 LDS tile so both sides are read / written along rows --
+// the per-step W^T copies of trainable weights (the element-wise strided copy_kernel ran them at
+// ~0.7 TB/s: 12.5 ms of a gpt2-xl step)
+template <typename T>
+__global__ __launch_bounds__(256) void transpose2d_kernel(const T* __restrict__ s, int64_t ls, T* __restrict__ d,
+                                                          int64_t ld, int64_t R, int64_t C) {
+  __shared__ T tile[64][65];
+  const int64_t i0 = (int64_t)blockIdx.x * 64, j0 = (int64_t)blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int64_t j = j0 + r, i = i0 + tx;
+    if (j < C && i < R) tile[r][tx] = s[j * ls + i];
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int64_t i = i0 + r, j = j0 + tx;
+    if (i < R && j < C) d[i * ld + j] = tile[tx][r];
+  }
+}
+
 // contiguous same-dtype fast path: 16-B vector copy
 __global__ void copy16_kernel(const uint4* __restrict__ s, uint4* __restrict__ d, int64_t n16) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
@@ -430,6 +451,20 @@ void copy(const Desc& d, const Desc& s, hipStream_t stm) {
       return;
     }
     MFT_HIP_CHECK(hipMemcpyAsync(d.ptr, s.ptr, bytes, hipMemcpyDeviceToDevice, stm));
+    return;
+  }
+  // a transposed 2-D view into a row-major destination: the LDS-tiled transpose (MFT_COPY_T=0: off, A/B)
+  static const bool tr_off = getenv("MFT_COPY_T") && getenv("MFT_COPY_T")[0] == '0';
+  if (!tr_off && d.dtype == s.dtype && d.ndim == 2 && s.ndim == 2 && s.shape[0] == d.shape[0] && s.shape[1] == d.shape[1] &&
+      d.stride[1] == 1 && d.stride[0] >= d.shape[1] && s.stride[0] == 1 && s.stride[1] >= s.shape[0] &&
+      (dsize(d.dtype) == 2 || dsize(d.dtype) == 4) && (d.shape[0] + 63) / 64 < (1L << 31) && (d.shape[1] + 63) / 64 < 65536) {
+    const dim3 grid((unsigned)((d.shape[0] + 63) / 64), (unsigned)((d.shape[1] + 63) / 64));
+    if (dsize(d.dtype) == 2)
+      transpose2d_kernel<uint16_t><<<grid, 256, 0, stm>>>((const uint16_t*)s.ptr, s.stride[1], (uint16_t*)d.ptr, d.stride[0],
+                                                         d.shape[0], d.shape[1]);
+    else
+      transpose2d_kernel<uint32_t><<<grid, 256, 0, stm>>>((const uint32_t*)s.ptr, s.stride[1], (uint32_t*)d.ptr, d.stride[0],
+                                                         d.shape[0], d.shape[1]);
     return;
   }
   copy_kernel<<<grid_for(n), 256, 0, stm>>>(d, s, n);
