@@ -260,6 +260,19 @@ int main() {
     for (int i = 0; i < 4; ++i)
       for (int j = 1; j < 4; ++j) gv[i * 6 + j] = 2 * xv[i * 6 + j];
     check("view/slice/transpose backward", host(tv.grad()), gv, 1e-5);
+    // transposed 2-D views copied into row-major tensors (the LDS-tiled transpose path of k::copy): a
+    // column slice of a wider matrix, ragged 64-tiles, fp32 and bf16
+    for (DType dt : {DType::F32, DType::BF16}) {
+      const int Rr = 131, Cc = 70, ld = 77;
+      auto xs = rnd((size_t)Rr * ld);
+      Tensor src = dev(xs, {Rr, ld}, dt);
+      Tensor tr = src.slice(1, 0, Cc).t().contiguous();  // [Cc, Rr]
+      std::vector<double> want((size_t)Cc * Rr);
+      const std::vector<double> hs = host(src);
+      for (int i = 0; i < Cc; ++i)
+        for (int j = 0; j < Rr; ++j) want[(size_t)i * Rr + j] = hs[(size_t)j * ld + i];
+      check(dt == DType::F32 ? "transposed copy fp32" : "transposed copy bf16", host(tr), want, 0.0);
+    }
     // cross entropy with ignore_index vs host
     const int Nr = 9, C = 13;
     auto lg = rnd(Nr * C, -2, 2);
