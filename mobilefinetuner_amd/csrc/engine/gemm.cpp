@@ -323,6 +323,7 @@ void gemm_wgrad(Tensor& buf, const Tensor& dy2, const Tensor& x2, float alpha) {
   // MFT_WGRAD=gemm8 keeps the 8-wave kernel below (A/B)
   static const bool wg8 = getenv("MFT_WGRAD") && std::string(getenv("MFT_WGRAD")) == "gemm8";
   if (!wg8 && M % 64 == 0 && dy2.dtype() == DType::BF16 && x2.dtype() == DType::BF16 &&
+      reinterpret_cast<uintptr_t>(dy2.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x2.data_ptr()) % 16 == 0 &&
       ::mft::gemm4_tn_supported((int)N, (int)K, (int)M, dy2.stride(0), x2.stride(0))) {
     ::mft::GemmArgs g{};
     g.A = (const ::mft::bf16_t*)dy2.data_ptr();
